@@ -1,0 +1,76 @@
+# Native build for bitcoincashplus_amd.
+#   make            -> core static lib, HIP kernels (gfx950), Python extension, node binaries
+#   make pyext      -> only the Python extension
+#   make clean
+# CPU code is built with g++ (C++17); HIP kernels with hipcc --offload-arch=gfx950.
+# Everything lands in-tree: build/ for objects, bitcoincashplus_amd/_bcpnative*.so, bin/.
+
+ROCM       ?= /opt/rocm
+HIPCC      ?= $(ROCM)/bin/hipcc
+CXX        ?= g++
+PYTHON     ?= python3
+GPU_ARCH   ?= gfx950
+OPT        ?= -O2
+
+PY_INC     := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC := $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+PY_EXT     := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+CXXFLAGS   := -std=c++17 $(OPT) -g1 -fPIC -Wall -Wno-unused-function -Wno-sign-compare -Icsrc -pthread
+HIPFLAGS   := -std=c++17 $(OPT) -fPIC --offload-arch=$(GPU_ARCH) -Icsrc -munsafe-fp-atomics \
+              -Wno-unused-result -Wno-unused-variable -Wno-pass-failed
+LDLIBS     := -L$(ROCM)/lib -lamdhip64 -pthread -ldl -Wl,-rpath,$(ROCM)/lib
+
+CORE_SRCS  := $(wildcard csrc/crypto/*.cpp csrc/primitives/*.cpp csrc/consensus/*.cpp \
+                csrc/script/*.cpp csrc/secp256k1/*.cpp csrc/util/*.cpp csrc/node/*.cpp \
+                csrc/rpc/*.cpp csrc/net/*.cpp csrc/wallet/*.cpp)
+GPU_HOST   := $(wildcard csrc/gpu/*.cpp)
+HIP_SRCS   := $(wildcard csrc/kernels/*.hip)
+PY_SRCS    := $(wildcard csrc/python/*.cpp)
+TOOL_SRCS  := $(wildcard csrc/tools/*.cpp)
+
+CORE_OBJS  := $(patsubst csrc/%.cpp,build/obj/%.o,$(CORE_SRCS) $(GPU_HOST))
+HIP_OBJS   := $(patsubst csrc/%.hip,build/obj/%.o,$(HIP_SRCS))
+PY_OBJS    := $(patsubst csrc/%.cpp,build/obj/%.o,$(PY_SRCS))
+TOOLS      := $(patsubst csrc/tools/%.cpp,bin/%,$(TOOL_SRCS))
+
+PYEXT      := bitcoincashplus_amd/_bcpnative$(PY_EXT)
+CORELIB    := build/libbcpcore.a
+
+.PHONY: all pyext tools clean kernels
+all: pyext tools
+pyext: $(PYEXT)
+kernels: $(HIP_OBJS)
+tools: $(TOOLS)
+
+build/obj/%.o: csrc/%.cpp
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -MMD -MP -c $< -o $@
+
+build/obj/python/%.o: csrc/python/%.cpp
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -I$(PY_INC) -I$(PYBIND_INC) -fvisibility=hidden -MMD -MP -c $< -o $@
+
+build/obj/kernels/%.o: csrc/kernels/%.hip
+	@mkdir -p $(dir $@)
+	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+
+$(CORELIB): $(CORE_OBJS) $(HIP_OBJS)
+	@mkdir -p $(dir $@)
+	rm -f $@ && ar rcs $@ $^
+
+$(PYEXT): $(PY_OBJS) $(CORELIB)
+	$(CXX) -shared -o $@ $(PY_OBJS) -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS)
+
+bin/%: build/obj/tools/%.o $(CORELIB)
+	@mkdir -p bin
+	$(CXX) -o $@ $< $(CORELIB) $(LDLIBS)
+
+build/obj/tools/%.o: csrc/tools/%.cpp
+	@mkdir -p $(dir $@)
+	$(CXX) $(CXXFLAGS) -MMD -MP -c $< -o $@
+
+clean:
+	rm -rf build bin bitcoincashplus_amd/_bcpnative*.so
+
+-include $(shell find build -name '*.d' 2>/dev/null)

@@ -1,0 +1,101 @@
+// Device BLAKE2b for Equihash on CDNA4.
+//
+// One work-item runs one full 12-round compression on 64-bit lanes. The 64-bit
+// rotations by 32/24/16/63 lower to v_alignbit_b32 pairs / register swaps, the
+// adds to v_add_co/v_addc pairs; the base state (chaining value after the
+// 128-byte header block plus the g-independent message words) is
+// wave-uniform, so it sits in SGPRs and only the message word that carries
+// le32(g) is per-lane.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace bcpk {
+
+// Host-prepared, g-independent part of H(I||V||le32(g)): chaining value after all
+// full blocks, the final (partial) block with the g slot zeroed, byte counter.
+struct EhBaseState {
+    uint64_t h[8];
+    uint64_t m[16];
+    uint64_t t0;        // total bytes hashed including the 4-byte g
+    uint32_t g_byte;    // byte offset of le32(g) within the final block
+    uint32_t outlen;    // digest bytes (HashOutput)
+};
+
+__device__ __constant__ static const uint8_t kB2Sigma[12][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4},
+    {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13},
+    {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11},
+    {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5},
+    {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0},
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
+    {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
+
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+#define BCPK_B2G(a, b, c, d, x, y)       \
+    a = a + b + (x);                     \
+    d = rotr64(d ^ a, 32);               \
+    c = c + d;                           \
+    b = rotr64(b ^ c, 24);               \
+    a = a + b + (y);                     \
+    d = rotr64(d ^ a, 16);               \
+    c = c + d;                           \
+    b = rotr64(b ^ c, 63);
+
+// Final-block compression with message m; writes the new chaining value to out.
+__device__ __forceinline__ void blake2b_compress_final(const uint64_t hin[8], const uint64_t m[16], uint64_t t0,
+                                                       uint64_t out[8]) {
+    const uint64_t IV0 = 0x6a09e667f3bcc908ULL, IV1 = 0xbb67ae8584caa73bULL, IV2 = 0x3c6ef372fe94f82bULL,
+                   IV3 = 0xa54ff53a5f1d36f1ULL, IV4 = 0x510e527fade682d1ULL, IV5 = 0x9b05688c2b3e6c1fULL,
+                   IV6 = 0x1f83d9abfb41bd6bULL, IV7 = 0x5be0cd19137e2179ULL;
+    uint64_t v0 = hin[0], v1 = hin[1], v2 = hin[2], v3 = hin[3], v4 = hin[4], v5 = hin[5], v6 = hin[6],
+             v7 = hin[7];
+    uint64_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3, v12 = IV4 ^ t0, v13 = IV5, v14 = ~IV6, v15 = IV7;
+#pragma unroll
+    for (int r = 0; r < 12; ++r) {
+        BCPK_B2G(v0, v4, v8, v12, m[kB2Sigma[r][0]], m[kB2Sigma[r][1]]);
+        BCPK_B2G(v1, v5, v9, v13, m[kB2Sigma[r][2]], m[kB2Sigma[r][3]]);
+        BCPK_B2G(v2, v6, v10, v14, m[kB2Sigma[r][4]], m[kB2Sigma[r][5]]);
+        BCPK_B2G(v3, v7, v11, v15, m[kB2Sigma[r][6]], m[kB2Sigma[r][7]]);
+        BCPK_B2G(v0, v5, v10, v15, m[kB2Sigma[r][8]], m[kB2Sigma[r][9]]);
+        BCPK_B2G(v1, v6, v11, v12, m[kB2Sigma[r][10]], m[kB2Sigma[r][11]]);
+        BCPK_B2G(v2, v7, v8, v13, m[kB2Sigma[r][12]], m[kB2Sigma[r][13]]);
+        BCPK_B2G(v3, v4, v9, v14, m[kB2Sigma[r][14]], m[kB2Sigma[r][15]]);
+    }
+    out[0] = hin[0] ^ v0 ^ v8;
+    out[1] = hin[1] ^ v1 ^ v9;
+    out[2] = hin[2] ^ v2 ^ v10;
+    out[3] = hin[3] ^ v3 ^ v11;
+    out[4] = hin[4] ^ v4 ^ v12;
+    out[5] = hin[5] ^ v5 ^ v13;
+    out[6] = hin[6] ^ v6 ^ v14;
+    out[7] = hin[7] ^ v7 ^ v15;
+}
+
+// H(base || le32(g)) -> 8 chaining words (digest = first outlen bytes, little-endian).
+__device__ __forceinline__ void eh_hash_g(const EhBaseState& bs, uint32_t g, uint64_t out[8]) {
+    uint64_t m[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) m[i] = bs.m[i];
+    // Insert le32(g) at byte g_byte (may straddle two 64-bit words).
+    const uint32_t w = bs.g_byte >> 3, sh = (bs.g_byte & 7) * 8;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        if (i == (int)w) m[i] |= (uint64_t)g << sh;
+        if (sh > 32 && i == (int)w + 1) m[i] |= (uint64_t)g >> (64 - sh);
+    }
+    blake2b_compress_final(bs.h, m, bs.t0, out);
+}
+
+// Byte k (0-based) of the digest held in 8 little-endian words.
+__device__ __forceinline__ uint32_t digest_byte(const uint64_t h[8], int k) {
+    return (uint32_t)(h[k >> 3] >> ((k & 7) * 8)) & 0xff;
+}
+
+} // namespace bcpk

@@ -1,0 +1,96 @@
+// Host-side API of the CDNA4 (gfx950) kernels. Every function here is
+// implemented in a csrc/kernels/*.hip translation unit and launches hand-written
+// HIP kernels; nothing here falls back to the CPU. Callers that must run
+// without a GPU (the node on a CPU-only host) check GpuAvailable() first and
+// use the CPU consensus code instead.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <string>
+#include <vector>
+
+namespace bcp {
+class CBlake2b;
+namespace gpu {
+
+bool GpuAvailable();
+int DeviceCount();
+std::string DeviceName(int device);
+// Throws std::runtime_error with the HIP error string.
+void Check(int hip_status, const char* what);
+
+// --------------------------------------------------------------- Equihash
+// Host mirror of bcpk::EhBaseState (csrc/kernels/blake2b_device.h).
+struct EhBaseState {
+    uint64_t h[8];
+    uint64_t m[16];
+    uint64_t t0;
+    uint32_t g_byte;
+    uint32_t outlen;
+};
+// Build the g-independent state from a BLAKE2b state that already absorbed
+// CEquihashInput || nNonce (the solver/verifier then appends le32(g)).
+EhBaseState MakeEhBaseState(const CBlake2b& st);
+
+struct EhGpuStats {
+    uint64_t nonces = 0;
+    uint64_t candidates = 0;
+    uint64_t duplicates = 0;
+    uint64_t solutions = 0;
+    uint64_t dropped_rows = 0;   // rows lost to bucket overflow (sampled)
+    double gpu_ms = 0;
+};
+
+// Batched Equihash solver: one launch sequence solves `batch` nonces at once
+// (8 + 3 kernels per batch, bucket-per-workgroup collision rounds in LDS).
+class EquihashGpuSolver {
+public:
+    EquihashGpuSolver(unsigned n, unsigned k, int batch, int device = -1);
+    ~EquihashGpuSolver();
+    unsigned N() const;
+    unsigned K() const;
+    int Batch() const;
+    // states.size() <= batch. Returns, per nonce, canonical index lists of all
+    // valid (distinct-index) solutions found.
+    std::vector<std::vector<std::vector<uint32_t>>> Solve(const std::vector<EhBaseState>& states);
+    // Asynchronous split used by the pipelined miner/bench: Launch enqueues the
+    // whole sequence on the solver's stream; Collect waits and decodes.
+    void Launch(const std::vector<EhBaseState>& states);
+    std::vector<std::vector<std::vector<uint32_t>>> Collect();
+    const EhGpuStats& Stats() const;
+    void ResetStats();
+    size_t DeviceBytes() const;
+    struct Impl;
+private:
+    std::unique_ptr<Impl> impl;
+};
+
+// Batched consensus verifier (reference CheckEquihashSolution / IsValidSolution).
+// One workgroup per solution: 2^K lanes hash their index, LDS tree reduction.
+std::vector<uint8_t> EquihashVerifyBatch(unsigned n, unsigned k, const std::vector<EhBaseState>& states,
+                                         const std::vector<std::vector<unsigned char>>& solutions,
+                                         int device = -1);
+
+// --------------------------------------------------------------- SHA-256d
+// out[i] = SHA256d(in[offs[i] .. offs[i]+lens[i]))
+std::vector<unsigned char> Sha256dBatch(const std::vector<unsigned char>& data, const std::vector<uint64_t>& offs,
+                                        const std::vector<uint32_t>& lens, int device = -1);
+// out[i] = SHA256d(in[64*i .. 64*i+64))
+std::vector<unsigned char> Sha256d64Batch(const std::vector<unsigned char>& data, int device = -1);
+// Merkle root of 32-byte leaves with the reference's mutation flag
+// (reference src/consensus/merkle.cpp:47-175, CVE-2012-2459).
+std::vector<unsigned char> MerkleRoot(const std::vector<unsigned char>& leaves, bool* mutated, int device = -1);
+// Legacy 80-byte header nonce sweep: returns the first nonce in
+// [start, start+count) with SHA256d(header) <= target, or -1.
+int64_t Sha256dScanNonces(const unsigned char header80[80], const unsigned char target_le[32], uint32_t start,
+                          uint64_t count, int device = -1);
+
+// --------------------------------------------------------------- secp256k1
+// ECDSA verification batch. msg/r/s are 32-byte big-endian, pubkeys 64-byte
+// (x||y big-endian, already parsed/decompressed on the host). s must be
+// low-S-normalised by the caller (reference CPubKey::Verify semantics).
+std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
+                                      const std::vector<unsigned char>& pub64, int device = -1);
+
+} // namespace gpu
+} // namespace bcp

@@ -1,0 +1,69 @@
+// Small host helpers shared by the .hip translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+
+#define BCP_HIP_CHECK(expr)                                                                            \
+    do {                                                                                               \
+        hipError_t _e = (expr);                                                                        \
+        if (_e != hipSuccess)                                                                          \
+            throw std::runtime_error(std::string("HIP error in ") + #expr + ": " + hipGetErrorString(_e) + \
+                                     " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")");          \
+    } while (0)
+
+namespace bcp {
+namespace gpu {
+
+// Resolves -1 to the caller's current device and makes `device` current.
+inline int UseDevice(int device) {
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        throw std::runtime_error("bitcoincashplus_amd: no HIP device available (gfx950 kernels need an MI355X)");
+    if (device < 0) BCP_HIP_CHECK(hipGetDevice(&device));
+    if (device >= count) throw std::runtime_error("bitcoincashplus_amd: device index out of range");
+    BCP_HIP_CHECK(hipSetDevice(device));
+    return device;
+}
+
+// RAII device buffer.
+template <typename T> struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    DevBuf() {}
+    explicit DevBuf(size_t count) { alloc(count); }
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) BCP_HIP_CHECK(hipMalloc((void**)&p, count * sizeof(T)));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~DevBuf() { release(); }
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+};
+
+// RAII pinned host buffer.
+template <typename T> struct HostBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    void alloc(size_t count) {
+        release();
+        n = count;
+        if (count) BCP_HIP_CHECK(hipHostMalloc((void**)&p, count * sizeof(T), hipHostMallocDefault));
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    ~HostBuf() { release(); }
+};
+
+} // namespace gpu
+} // namespace bcp

@@ -1,0 +1,165 @@
+// Python bindings for the CDNA4 kernels (csrc/kernels/*.hip).
+#include "consensus/equihash.h"
+#include "kernels/gpu_api.h"
+#include "python/bind.h"
+
+namespace bcp {
+namespace py {
+
+static std::vector<gpu::EhBaseState> states_from(const std::vector<CBlake2b>& sts) {
+    std::vector<gpu::EhBaseState> v;
+    v.reserve(sts.size());
+    for (auto& s : sts) v.push_back(gpu::MakeEhBaseState(s));
+    return v;
+}
+
+void bind_gpu(pyb::module_& m) {
+    m.def("gpu_available", &gpu::GpuAvailable);
+    m.def("gpu_device_count", &gpu::DeviceCount);
+    m.def("gpu_device_name", &gpu::DeviceName);
+
+    pyb::class_<gpu::EquihashGpuSolver>(m, "EquihashGpuSolver")
+        .def(pyb::init<unsigned, unsigned, int, int>(), pyb::arg("n"), pyb::arg("k"), pyb::arg("batch") = 1,
+             pyb::arg("device") = -1)
+        .def_property_readonly("n", &gpu::EquihashGpuSolver::N)
+        .def_property_readonly("k", &gpu::EquihashGpuSolver::K)
+        .def_property_readonly("batch", &gpu::EquihashGpuSolver::Batch)
+        .def_property_readonly("device_bytes", &gpu::EquihashGpuSolver::DeviceBytes)
+        // states: list of EquihashState (header+nonce absorbed) -> per nonce list of minimal solutions
+        .def("solve",
+             [](gpu::EquihashGpuSolver& s, const std::vector<CBlake2b>& sts) {
+                 auto bs = states_from(sts);
+                 std::vector<std::vector<std::vector<uint32_t>>> r;
+                 {
+                     pyb::gil_scoped_release rel;
+                     r = s.Solve(bs);
+                 }
+                 const size_t cbl = s.N() / (s.K() + 1);
+                 pyb::list out;
+                 for (auto& per : r) {
+                     pyb::list l;
+                     for (auto& idx : per) l.append(to_bytes(GetMinimalFromIndices(idx, cbl)));
+                     out.append(l);
+                 }
+                 return out;
+             })
+        .def("launch", [](gpu::EquihashGpuSolver& s, const std::vector<CBlake2b>& sts) { s.Launch(states_from(sts)); })
+        .def("collect",
+             [](gpu::EquihashGpuSolver& s) {
+                 std::vector<std::vector<std::vector<uint32_t>>> r;
+                 {
+                     pyb::gil_scoped_release rel;
+                     r = s.Collect();
+                 }
+                 const size_t cbl = s.N() / (s.K() + 1);
+                 pyb::list out;
+                 for (auto& per : r) {
+                     pyb::list l;
+                     for (auto& idx : per) l.append(to_bytes(GetMinimalFromIndices(idx, cbl)));
+                     out.append(l);
+                 }
+                 return out;
+             })
+        // Launch+collect many batches back to back; returns total solutions (for benchmarking).
+        .def("run_nonces",
+             [](gpu::EquihashGpuSolver& s, const std::vector<CBlake2b>& sts) {
+                 auto bs = states_from(sts);
+                 uint64_t total = 0;
+                 pyb::gil_scoped_release rel;
+                 const size_t B = s.Batch();
+                 for (size_t off = 0; off < bs.size(); off += B) {
+                     std::vector<gpu::EhBaseState> chunk(bs.begin() + off, bs.begin() + std::min(bs.size(), off + B));
+                     auto r = s.Solve(chunk);
+                     for (auto& per : r) total += per.size();
+                 }
+                 return total;
+             })
+        .def("stats",
+             [](const gpu::EquihashGpuSolver& s) {
+                 auto& st = s.Stats();
+                 pyb::dict d;
+                 d["nonces"] = st.nonces;
+                 d["candidates"] = st.candidates;
+                 d["duplicates"] = st.duplicates;
+                 d["solutions"] = st.solutions;
+                 d["dropped_rows_sampled"] = st.dropped_rows;
+                 d["gpu_ms"] = st.gpu_ms;
+                 return d;
+             })
+        .def("reset_stats", &gpu::EquihashGpuSolver::ResetStats);
+
+    m.def(
+        "eh_verify_batch_gpu",
+        [](unsigned n, unsigned k, const std::vector<CBlake2b>& sts, const std::vector<pyb::bytes>& sols, int device) {
+            auto bs = states_from(sts);
+            std::vector<std::vector<unsigned char>> v;
+            for (auto& b : sols) v.push_back(to_vec(b));
+            std::vector<uint8_t> r;
+            {
+                pyb::gil_scoped_release rel;
+                r = gpu::EquihashVerifyBatch(n, k, bs, v, device);
+            }
+            return std::vector<bool>(r.begin(), r.end());
+        },
+        pyb::arg("n"), pyb::arg("k"), pyb::arg("states"), pyb::arg("solutions"), pyb::arg("device") = -1);
+
+    m.def(
+        "sha256d_batch_gpu",
+        [](const std::vector<pyb::bytes>& msgs, int device) {
+            std::vector<unsigned char> data;
+            std::vector<uint64_t> offs;
+            std::vector<uint32_t> lens;
+            for (auto& b : msgs) {
+                std::string s = b;
+                offs.push_back(data.size());
+                lens.push_back((uint32_t)s.size());
+                data.insert(data.end(), s.begin(), s.end());
+            }
+            std::vector<unsigned char> out;
+            {
+                pyb::gil_scoped_release rel;
+                out = gpu::Sha256dBatch(data, offs, lens, device);
+            }
+            pyb::list l;
+            for (size_t i = 0; i < msgs.size(); ++i) l.append(to_bytes(out.data() + 32 * i, 32));
+            return l;
+        },
+        pyb::arg("msgs"), pyb::arg("device") = -1);
+    m.def(
+        "sha256d64_batch_gpu",
+        [](const pyb::bytes& data, int device) {
+            auto v = to_vec(data);
+            std::vector<unsigned char> out;
+            {
+                pyb::gil_scoped_release rel;
+                out = gpu::Sha256d64Batch(v, device);
+            }
+            return to_bytes(out);
+        },
+        pyb::arg("data"), pyb::arg("device") = -1);
+    m.def(
+        "merkle_root_gpu",
+        [](const pyb::bytes& leaves, int device) {
+            auto v = to_vec(leaves);
+            bool mutated = false;
+            std::vector<unsigned char> root;
+            {
+                pyb::gil_scoped_release rel;
+                root = gpu::MerkleRoot(v, &mutated, device);
+            }
+            return pyb::make_tuple(to_bytes(root), mutated);
+        },
+        pyb::arg("leaves"), pyb::arg("device") = -1);
+    m.def(
+        "sha256d_scan_nonces_gpu",
+        [](const pyb::bytes& header80, const pyb::bytes& target_le, uint32_t start, uint64_t count, int device) {
+            auto h = to_vec(header80), t = to_vec(target_le);
+            if (h.size() != 80 || t.size() != 32) throw std::invalid_argument("header80/target sizes");
+            pyb::gil_scoped_release rel;
+            return gpu::Sha256dScanNonces(h.data(), t.data(), start, count, device);
+        },
+        pyb::arg("header80"), pyb::arg("target_le"), pyb::arg("start"), pyb::arg("count"), pyb::arg("device") = -1);
+}
+
+} // namespace py
+} // namespace bcp
