@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "4")))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "8")))
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
     args = ap.parse_args()
 

@@ -238,6 +238,14 @@ bool EhBasicSolve(const EquihashParams& p, const CBlake2b& base,
             while (j < nrows && order[j].first == order[i].first) ++j;
             for (size_t a = i; a < j; ++a) {
                 for (size_t b = a + 1; b < j; ++b) {
+                    if (r >= 2) {
+                        // Depth-1 duplicate pruning: rows sharing a parent row merge to a tree
+                        // with repeated leaves (cheap early reject, as on the GPU).
+                        const uint64_t pa = refs[r - 1][order[a].second], pb = refs[r - 1][order[b].second];
+                        const uint32_t a0 = (uint32_t)(pa >> 32), a1 = (uint32_t)pa, b0 = (uint32_t)(pb >> 32),
+                                       b1 = (uint32_t)pb;
+                        if (a0 == b0 || a0 == b1 || a1 == b0 || a1 == b1) continue;
+                    }
                     const uint32_t* ra = &cur[(size_t)order[a].second * width];
                     const uint32_t* rb = &cur[(size_t)order[b].second * width];
                     bool allzero = true;
@@ -272,6 +280,15 @@ bool EhBasicSolve(const EquihashParams& p, const CBlake2b& base,
         while (j < nrows && order[j].first == order[i].first) ++j;
         for (size_t a = i; a < j; ++a) {
             for (size_t b = a + 1; b < j; ++b) {
+                {
+                    const uint64_t pa = refs[p.K - 1][order[a].second], pb = refs[p.K - 1][order[b].second];
+                    const uint32_t a0 = (uint32_t)(pa >> 32), a1 = (uint32_t)pa, b0 = (uint32_t)(pb >> 32),
+                                   b1 = (uint32_t)pb;
+                    if (a0 == b0 || a0 == b1 || a1 == b0 || a1 == b1) {
+                        if (stats) stats->duplicates++;
+                        continue;
+                    }
+                }
                 if (stats) stats->candidates++;
                 // Expand the tree top-down.
                 std::vector<uint32_t> nodes = {order[a].second, order[b].second};

@@ -93,6 +93,18 @@ __device__ __forceinline__ void eh_hash_g(const EhBaseState& bs, uint32_t g, uin
     blake2b_compress_final(bs.h, m, bs.t0, out);
 }
 
+// Specialisation for the block-header input (CEquihashInput 108 B || nonce 32 B): the final
+// block holds 12 bytes of nonce then le32(g), so m[0] is wave-uniform, m[1] = uniform |
+// g << 32 and m[2..15] are zero — the 168 zero-word additions fold away at compile time.
+__device__ __forceinline__ void eh_hash_g_hdr(const EhBaseState& bs, uint32_t g, uint64_t out[8]) {
+    uint64_t m[16];
+    m[0] = bs.m[0];
+    m[1] = bs.m[1] | ((uint64_t)g << 32);
+#pragma unroll
+    for (int i = 2; i < 16; ++i) m[i] = 0;
+    blake2b_compress_final(bs.h, m, bs.t0, out);
+}
+
 // Byte k (0-based) of the digest held in 8 little-endian words.
 __device__ __forceinline__ uint32_t digest_byte(const uint64_t h[8], int k) {
     return (uint32_t)(h[k >> 3] >> ((k & 7) * 8)) & 0xff;

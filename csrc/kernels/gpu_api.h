@@ -37,8 +37,9 @@ struct EhGpuStats {
     uint64_t candidates = 0;
     uint64_t duplicates = 0;
     uint64_t solutions = 0;
-    uint64_t dropped_rows = 0;   // rows lost to bucket overflow (sampled)
+    uint64_t dropped_rows = 0;   // rows lost to bucket overflow (debug mode, nonce 0 of each batch)
     double gpu_ms = 0;
+    std::vector<uint64_t> stage_rows, stage_dropped, stage_maxfill; // debug mode, last batch
 };
 
 // Batched Equihash solver: one launch sequence solves `batch` nonces at once
@@ -58,6 +59,9 @@ public:
     void Launch(const std::vector<EhBaseState>& states);
     std::vector<std::vector<std::vector<uint32_t>>> Collect();
     const EhGpuStats& Stats() const;
+    void SetDebug(bool on);   // collect per-stage bucket statistics (extra D2H copies)
+    void SetStampMode(bool on); // diagnostic: launch phase-timestamped round kernels
+    std::vector<std::vector<double>> PhaseCycles(int nonces);
     void ResetStats();
     size_t DeviceBytes() const;
     struct Impl;

@@ -84,9 +84,15 @@ void bind_gpu(pyb::module_& m) {
                  d["solutions"] = st.solutions;
                  d["dropped_rows_sampled"] = st.dropped_rows;
                  d["gpu_ms"] = st.gpu_ms;
+                 d["stage_rows"] = st.stage_rows;
+                 d["stage_dropped"] = st.stage_dropped;
+                 d["stage_maxfill"] = st.stage_maxfill;
                  return d;
              })
-        .def("reset_stats", &gpu::EquihashGpuSolver::ResetStats);
+        .def("reset_stats", &gpu::EquihashGpuSolver::ResetStats)
+        .def("set_debug", &gpu::EquihashGpuSolver::SetDebug)
+        .def("set_stamp_mode", &gpu::EquihashGpuSolver::SetStampMode)
+        .def("phase_cycles", &gpu::EquihashGpuSolver::PhaseCycles);
 
     m.def(
         "eh_verify_batch_gpu",
