@@ -47,6 +47,10 @@ public:
 };
 
 // ---------------------------------------------------------------- primitives
+// Tag selecting stream-deserialising constructors, e.g. CTransaction(deserialize, stream).
+struct deserialize_type {};
+constexpr deserialize_type deserialize{};
+
 template <typename S> inline void ser_u8(S& s, uint8_t v) { s.write((const char*)&v, 1); }
 template <typename S> inline void ser_u16(S& s, uint16_t v) { s.write((const char*)&v, 2); }
 template <typename S> inline void ser_u32(S& s, uint32_t v) { s.write((const char*)&v, 4); }
@@ -237,7 +241,7 @@ template <typename S, typename K, typename C> void Unserialize(S& s, std::set<K,
 }
 template <typename S, typename T> void Serialize(S& s, const std::shared_ptr<const T>& p) { Serialize(s, *p); }
 template <typename S, typename T> void Unserialize(S& s, std::shared_ptr<const T>& p) {
-    p = std::make_shared<const T>(s);  // T must have a stream-deserialising constructor
+    p = std::make_shared<const T>(deserialize, s);  // T(deserialize_type, S&) constructor
 }
 
 // Fixed-size array of POD bytes

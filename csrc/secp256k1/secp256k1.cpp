@@ -1,0 +1,933 @@
+// secp256k1 CPU implementation. See secp256k1.h.
+#include "secp256k1/secp256k1.h"
+#include "crypto/hashes.h"
+#include "crypto/common.h"
+
+#include <cstring>
+#include <mutex>
+
+namespace bcp {
+namespace secp {
+
+typedef unsigned __int128 u128;
+
+// ---------------------------------------------------------------- field
+static const uint64_t P[4] = {0xFFFFFFFEFFFFFC2FULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL};
+static const uint64_t PC = 0x1000003D1ULL; // 2^256 - p
+
+static inline bool geq4(const uint64_t* a, const uint64_t* b) {
+    for (int i = 3; i >= 0; --i) {
+        if (a[i] != b[i]) return a[i] > b[i];
+    }
+    return true;
+}
+static inline uint64_t sub4(uint64_t* r, const uint64_t* a, const uint64_t* b) {
+    uint64_t borrow = 0;
+    for (int i = 0; i < 4; ++i) {
+        u128 d = (u128)a[i] - b[i] - borrow;
+        r[i] = (uint64_t)d;
+        borrow = (uint64_t)(d >> 127) & 1;
+    }
+    return borrow;
+}
+static inline uint64_t add4(uint64_t* r, const uint64_t* a, const uint64_t* b) {
+    u128 c = 0;
+    for (int i = 0; i < 4; ++i) {
+        c += (u128)a[i] + b[i];
+        r[i] = (uint64_t)c;
+        c >>= 64;
+    }
+    return (uint64_t)c;
+}
+
+static inline void fe_reduce_once(uint64_t* r) {
+    if (geq4(r, P)) sub4(r, r, P);
+}
+
+void fe_set_b32(Fe& r, const unsigned char* b, bool* overflow) {
+    for (int i = 0; i < 4; ++i) {
+        uint64_t v = 0;
+        for (int j = 0; j < 8; ++j) v = (v << 8) | b[(3 - i) * 8 + j];
+        r.n[i] = v;
+    }
+    bool of = geq4(r.n, P);
+    if (overflow) *overflow = of;
+    if (of) sub4(r.n, r.n, P);
+}
+void fe_get_b32(unsigned char* b, const Fe& a) {
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 8; ++j) b[(3 - i) * 8 + j] = (unsigned char)(a.n[i] >> (56 - 8 * j));
+}
+void fe_set_int(Fe& r, uint64_t v) { r.n[0] = v; r.n[1] = r.n[2] = r.n[3] = 0; }
+bool fe_is_zero(const Fe& a) { return (a.n[0] | a.n[1] | a.n[2] | a.n[3]) == 0; }
+bool fe_equal(const Fe& a, const Fe& b) { return memcmp(a.n, b.n, 32) == 0; }
+bool fe_is_odd(const Fe& a) { return a.n[0] & 1; }
+
+void fe_add(Fe& r, const Fe& a, const Fe& b) {
+    uint64_t c = add4(r.n, a.n, b.n);
+    if (c) { // value = 2^256 + r  ==  r + PC (mod p); cannot overflow again
+        u128 t = (u128)r.n[0] + PC;
+        r.n[0] = (uint64_t)t;
+        for (int i = 1; i < 4 && (t >> 64); ++i) {
+            t = (u128)r.n[i] + 1;
+            r.n[i] = (uint64_t)t;
+        }
+    }
+    fe_reduce_once(r.n);
+}
+void fe_sub(Fe& r, const Fe& a, const Fe& b) {
+    uint64_t borrow = sub4(r.n, a.n, b.n);
+    if (borrow) { // wrapped value = a - b + 2^256; subtract PC to get a - b + p
+        u128 t = (u128)r.n[0] - PC;
+        r.n[0] = (uint64_t)t;
+        uint64_t br = (uint64_t)(t >> 127) & 1;
+        for (int i = 1; i < 4 && br; ++i) {
+            u128 u = (u128)r.n[i] - 1;
+            r.n[i] = (uint64_t)u;
+            br = (uint64_t)(u >> 127) & 1;
+        }
+    }
+}
+void fe_neg(Fe& r, const Fe& a) {
+    Fe z;
+    fe_set_int(z, 0);
+    fe_sub(r, z, a);
+}
+
+// Reduce an 8-limb product mod p.
+static void fe_reduce8(uint64_t* r, const uint64_t* t) {
+    // u = lo + hi * PC   (hi * PC < 2^290)
+    uint64_t u[5];
+    u128 c = 0;
+    for (int i = 0; i < 4; ++i) {
+        c += (u128)t[i] + (u128)t[4 + i] * PC;
+        u[i] = (uint64_t)c;
+        c >>= 64;
+    }
+    u[4] = (uint64_t)c;
+    // fold u[4] (<= 2^34) once more
+    c = (u128)u[0] + (u128)u[4] * PC;
+    r[0] = (uint64_t)c;
+    c >>= 64;
+    for (int i = 1; i < 4; ++i) {
+        c += u[i];
+        r[i] = (uint64_t)c;
+        c >>= 64;
+    }
+    if (c) { // one more 2^256 -> PC
+        u128 d = (u128)r[0] + PC;
+        r[0] = (uint64_t)d;
+        for (int i = 1; i < 4 && (d >> 64); ++i) {
+            d = (u128)r[i] + 1;
+            r[i] = (uint64_t)d;
+        }
+    }
+    fe_reduce_once(r);
+}
+
+void fe_mul(Fe& r, const Fe& a, const Fe& b) {
+    uint64_t t[8] = {0};
+    for (int i = 0; i < 4; ++i) {
+        u128 c = 0;
+        for (int j = 0; j < 4; ++j) {
+            c += (u128)a.n[i] * b.n[j] + t[i + j];
+            t[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+        t[i + 4] = (uint64_t)c;
+    }
+    fe_reduce8(r.n, t);
+}
+void fe_sqr(Fe& r, const Fe& a) { fe_mul(r, a, a); }
+
+static void fe_pow(Fe& r, const Fe& a, const uint64_t* e) {
+    Fe acc;
+    fe_set_int(acc, 1);
+    for (int i = 255; i >= 0; --i) {
+        fe_sqr(acc, acc);
+        if ((e[i / 64] >> (i % 64)) & 1) fe_mul(acc, acc, a);
+    }
+    r = acc;
+}
+void fe_inv(Fe& r, const Fe& a) {
+    static const uint64_t PM2[4] = {0xFFFFFFFEFFFFFC2DULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL,
+                                    0xFFFFFFFFFFFFFFFFULL};
+    fe_pow(r, a, PM2);
+}
+bool fe_sqrt(Fe& r, const Fe& a) {
+    static const uint64_t E[4] = {0xFFFFFFFFBFFFFF0CULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL,
+                                  0x3FFFFFFFFFFFFFFFULL}; // (p+1)/4
+    Fe s, chk;
+    fe_pow(s, a, E);
+    fe_sqr(chk, s);
+    r = s;
+    return fe_equal(chk, a);
+}
+
+// ---------------------------------------------------------------- scalar
+static const uint64_t N[4] = {0xBFD25E8CD0364141ULL, 0xBAAEDCE6AF48A03BULL, 0xFFFFFFFFFFFFFFFEULL, 0xFFFFFFFFFFFFFFFFULL};
+static const uint64_t NC[3] = {0x402DA1732FC9BEBFULL, 0x4551231950B75FC4ULL, 0x1ULL}; // 2^256 - n
+static const uint64_t NH[4] = {0xDFE92F46681B20A0ULL, 0x5D576E7357A4501DULL, 0xFFFFFFFFFFFFFFFFULL,
+                               0x7FFFFFFFFFFFFFFFULL}; // n/2
+
+void sc_set_b32(Scalar& r, const unsigned char* b, bool* overflow) {
+    for (int i = 0; i < 4; ++i) {
+        uint64_t v = 0;
+        for (int j = 0; j < 8; ++j) v = (v << 8) | b[(3 - i) * 8 + j];
+        r.n[i] = v;
+    }
+    bool of = geq4(r.n, N);
+    if (overflow) *overflow = of;
+    if (of) sub4(r.n, r.n, N);
+}
+void sc_get_b32(unsigned char* b, const Scalar& a) {
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 8; ++j) b[(3 - i) * 8 + j] = (unsigned char)(a.n[i] >> (56 - 8 * j));
+}
+bool sc_is_zero(const Scalar& a) { return (a.n[0] | a.n[1] | a.n[2] | a.n[3]) == 0; }
+bool sc_is_high(const Scalar& a) {
+    for (int i = 3; i >= 0; --i) {
+        if (a.n[i] != NH[i]) return a.n[i] > NH[i];
+    }
+    return false;
+}
+void sc_add(Scalar& r, const Scalar& a, const Scalar& b) {
+    uint64_t c = add4(r.n, a.n, b.n);
+    if (c || geq4(r.n, N)) sub4(r.n, r.n, N);
+}
+void sc_neg(Scalar& r, const Scalar& a) {
+    if (sc_is_zero(a)) {
+        r = a;
+        return;
+    }
+    sub4(r.n, N, a.n);
+}
+// reduce a little-endian multi-limb number (up to 8 limbs) mod n
+static void sc_reduce(uint64_t* out, const uint64_t* tin) {
+    uint64_t t[9] = {0};
+    memcpy(t, tin, 8 * sizeof(uint64_t));
+    for (int iter = 0; iter < 4; ++iter) {
+        if ((t[4] | t[5] | t[6] | t[7] | t[8]) == 0) break;
+        // t = lo + hi * NC
+        uint64_t hi[5] = {t[4], t[5], t[6], t[7], t[8]};
+        uint64_t acc[9] = {t[0], t[1], t[2], t[3], 0, 0, 0, 0, 0};
+        for (int i = 0; i < 5; ++i) {
+            if (!hi[i]) continue;
+            u128 c = 0;
+            for (int j = 0; j < 3; ++j) {
+                c += (u128)hi[i] * NC[j] + acc[i + j];
+                acc[i + j] = (uint64_t)c;
+                c >>= 64;
+            }
+            for (int k = i + 3; c && k < 9; ++k) {
+                c += acc[k];
+                acc[k] = (uint64_t)c;
+                c >>= 64;
+            }
+        }
+        memcpy(t, acc, sizeof(acc));
+    }
+    while (geq4(t, N)) sub4(t, t, N);
+    memcpy(out, t, 32);
+}
+void sc_mul(Scalar& r, const Scalar& a, const Scalar& b) {
+    uint64_t t[8] = {0};
+    for (int i = 0; i < 4; ++i) {
+        u128 c = 0;
+        for (int j = 0; j < 4; ++j) {
+            c += (u128)a.n[i] * b.n[j] + t[i + j];
+            t[i + j] = (uint64_t)c;
+            c >>= 64;
+        }
+        t[i + 4] = (uint64_t)c;
+    }
+    sc_reduce(r.n, t);
+}
+void sc_inv(Scalar& r, const Scalar& a) {
+    static const uint64_t NM2[4] = {0xBFD25E8CD036413FULL, 0xBAAEDCE6AF48A03BULL, 0xFFFFFFFFFFFFFFFEULL,
+                                    0xFFFFFFFFFFFFFFFFULL};
+    Scalar acc = {{1, 0, 0, 0}};
+    for (int i = 255; i >= 0; --i) {
+        sc_mul(acc, acc, acc);
+        if ((NM2[i / 64] >> (i % 64)) & 1) sc_mul(acc, acc, a);
+    }
+    r = acc;
+}
+
+// ---------------------------------------------------------------- group
+static Ge make_generator() {
+    static const unsigned char gx[32] = {0x79, 0xBE, 0x66, 0x7E, 0xF9, 0xDC, 0xBB, 0xAC, 0x55, 0xA0, 0x62,
+                                         0x95, 0xCE, 0x87, 0x0B, 0x07, 0x02, 0x9B, 0xFC, 0xDB, 0x2D, 0xCE,
+                                         0x28, 0xD9, 0x59, 0xF2, 0x81, 0x5B, 0x16, 0xF8, 0x17, 0x98};
+    static const unsigned char gy[32] = {0x48, 0x3A, 0xDA, 0x77, 0x26, 0xA3, 0xC4, 0x65, 0x5D, 0xA4, 0xFB,
+                                         0xFC, 0x0E, 0x11, 0x08, 0xA8, 0xFD, 0x17, 0xB4, 0x48, 0xA6, 0x85,
+                                         0x54, 0x19, 0x9C, 0x47, 0xD0, 0x8F, 0xFB, 0x10, 0xD4, 0xB8};
+    Ge g;
+    fe_set_b32(g.x, gx);
+    fe_set_b32(g.y, gy);
+    g.inf = false;
+    return g;
+}
+const Ge& generator() {
+    static const Ge g = make_generator();
+    return g;
+}
+
+void gej_set_ge(Gej& r, const Ge& a) {
+    r.inf = a.inf;
+    r.x = a.x;
+    r.y = a.y;
+    fe_set_int(r.z, 1);
+}
+
+void gej_double(Gej& r, const Gej& a) {
+    if (a.inf || fe_is_zero(a.y)) {
+        r.inf = true;
+        return;
+    }
+    Fe A, B, C, D, E, F, t, X3, Y3, Z3;
+    fe_sqr(A, a.x);
+    fe_sqr(B, a.y);
+    fe_sqr(C, B);
+    fe_add(t, a.x, B);
+    fe_sqr(t, t);
+    fe_sub(t, t, A);
+    fe_sub(t, t, C);
+    fe_add(D, t, t);
+    fe_add(E, A, A);
+    fe_add(E, E, A);
+    fe_sqr(F, E);
+    fe_add(t, D, D);
+    fe_sub(X3, F, t);
+    fe_sub(t, D, X3);
+    fe_mul(Y3, E, t);
+    fe_add(t, C, C);
+    fe_add(t, t, t);
+    fe_add(t, t, t);
+    fe_sub(Y3, Y3, t);
+    fe_mul(Z3, a.y, a.z);
+    fe_add(Z3, Z3, Z3);
+    r.x = X3;
+    r.y = Y3;
+    r.z = Z3;
+    r.inf = false;
+}
+
+void gej_add_ge(Gej& r, const Gej& a, const Ge& b) {
+    if (b.inf) {
+        r = a;
+        return;
+    }
+    if (a.inf) {
+        gej_set_ge(r, b);
+        return;
+    }
+    Fe Z1Z1, U2, S2, H, rr, HH, I, J, V, t, X3, Y3, Z3;
+    fe_sqr(Z1Z1, a.z);
+    fe_mul(U2, b.x, Z1Z1);
+    fe_mul(S2, b.y, a.z);
+    fe_mul(S2, S2, Z1Z1);
+    fe_sub(H, U2, a.x);
+    fe_sub(rr, S2, a.y);
+    fe_add(rr, rr, rr);
+    if (fe_is_zero(H)) {
+        if (fe_is_zero(rr)) {
+            gej_double(r, a);
+        } else {
+            r.inf = true;
+        }
+        return;
+    }
+    fe_sqr(HH, H);
+    fe_add(I, HH, HH);
+    fe_add(I, I, I);
+    fe_mul(J, H, I);
+    fe_mul(V, a.x, I);
+    fe_sqr(X3, rr);
+    fe_sub(X3, X3, J);
+    fe_sub(X3, X3, V);
+    fe_sub(X3, X3, V);
+    fe_sub(t, V, X3);
+    fe_mul(Y3, rr, t);
+    fe_mul(t, a.y, J);
+    fe_add(t, t, t);
+    fe_sub(Y3, Y3, t);
+    fe_add(Z3, a.z, H);
+    fe_sqr(Z3, Z3);
+    fe_sub(Z3, Z3, Z1Z1);
+    fe_sub(Z3, Z3, HH);
+    r.x = X3;
+    r.y = Y3;
+    r.z = Z3;
+    r.inf = false;
+}
+
+void gej_add(Gej& r, const Gej& a, const Gej& b) {
+    if (a.inf) {
+        r = b;
+        return;
+    }
+    if (b.inf) {
+        r = a;
+        return;
+    }
+    Fe Z1Z1, Z2Z2, U1, U2, S1, S2, H, rr, I, J, V, t, X3, Y3, Z3;
+    fe_sqr(Z1Z1, a.z);
+    fe_sqr(Z2Z2, b.z);
+    fe_mul(U1, a.x, Z2Z2);
+    fe_mul(U2, b.x, Z1Z1);
+    fe_mul(S1, a.y, b.z);
+    fe_mul(S1, S1, Z2Z2);
+    fe_mul(S2, b.y, a.z);
+    fe_mul(S2, S2, Z1Z1);
+    fe_sub(H, U2, U1);
+    fe_sub(rr, S2, S1);
+    fe_add(rr, rr, rr);
+    if (fe_is_zero(H)) {
+        if (fe_is_zero(rr)) {
+            gej_double(r, a);
+        } else {
+            r.inf = true;
+        }
+        return;
+    }
+    fe_add(I, H, H);
+    fe_sqr(I, I);
+    fe_mul(J, H, I);
+    fe_mul(V, U1, I);
+    fe_sqr(X3, rr);
+    fe_sub(X3, X3, J);
+    fe_sub(X3, X3, V);
+    fe_sub(X3, X3, V);
+    fe_sub(t, V, X3);
+    fe_mul(Y3, rr, t);
+    fe_mul(t, S1, J);
+    fe_add(t, t, t);
+    fe_sub(Y3, Y3, t);
+    fe_add(Z3, a.z, b.z);
+    fe_sqr(Z3, Z3);
+    fe_sub(Z3, Z3, Z1Z1);
+    fe_sub(Z3, Z3, Z2Z2);
+    fe_mul(Z3, Z3, H);
+    r.x = X3;
+    r.y = Y3;
+    r.z = Z3;
+    r.inf = false;
+}
+
+void ge_set_gej(Ge& r, const Gej& a) {
+    if (a.inf) {
+        r.inf = true;
+        return;
+    }
+    Fe zi, zi2, zi3;
+    fe_inv(zi, a.z);
+    fe_sqr(zi2, zi);
+    fe_mul(zi3, zi2, zi);
+    fe_mul(r.x, a.x, zi2);
+    fe_mul(r.y, a.y, zi3);
+    r.inf = false;
+}
+
+// Batch Jacobian -> affine with one inversion (Montgomery's trick).
+static void batch_to_affine(Ge* out, const Gej* in, size_t n) {
+    std::vector<Fe> acc(n);
+    Fe run;
+    fe_set_int(run, 1);
+    for (size_t i = 0; i < n; ++i) {
+        acc[i] = run;
+        if (!in[i].inf) fe_mul(run, run, in[i].z);
+    }
+    Fe inv;
+    fe_inv(inv, run);
+    for (size_t i = n; i-- > 0;) {
+        if (in[i].inf) {
+            out[i].inf = true;
+            continue;
+        }
+        Fe zi, zi2, zi3;
+        fe_mul(zi, inv, acc[i]);
+        fe_mul(inv, inv, in[i].z);
+        fe_sqr(zi2, zi);
+        fe_mul(zi3, zi2, zi);
+        fe_mul(out[i].x, in[i].x, zi2);
+        fe_mul(out[i].y, in[i].y, zi3);
+        out[i].inf = false;
+    }
+}
+
+bool ge_is_valid(const Ge& a) {
+    if (a.inf) return false;
+    Fe y2, x3, seven;
+    fe_sqr(y2, a.y);
+    fe_sqr(x3, a.x);
+    fe_mul(x3, x3, a.x);
+    fe_set_int(seven, 7);
+    fe_add(x3, x3, seven);
+    return fe_equal(y2, x3);
+}
+
+// table[i][j] = j * 256^i * G  (i < 32, 1 <= j < 256)
+static std::vector<Ge>* g_gen_table = nullptr;
+static std::once_flag g_gen_once;
+static void build_gen_table() {
+    std::vector<Gej> jac(32 * 256);
+    Gej base;
+    gej_set_ge(base, generator());
+    for (int i = 0; i < 32; ++i) {
+        Gej acc;
+        acc.inf = true;
+        jac[i * 256].inf = true;
+        for (int j = 1; j < 256; ++j) {
+            gej_add(acc, acc, base);
+            jac[i * 256 + j] = acc;
+        }
+        // base *= 256
+        for (int k = 0; k < 8; ++k) gej_double(base, base);
+    }
+    auto* t = new std::vector<Ge>(32 * 256);
+    batch_to_affine(t->data(), jac.data(), jac.size());
+    g_gen_table = t;
+}
+
+void ecmult_gen(Gej& r, const Scalar& k) {
+    std::call_once(g_gen_once, build_gen_table);
+    r.inf = true;
+    for (int i = 0; i < 32; ++i) {
+        const unsigned byte = (unsigned)(k.n[i / 8] >> ((i % 8) * 8)) & 0xff;
+        if (byte) gej_add_ge(r, r, (*g_gen_table)[i * 256 + byte]);
+    }
+}
+
+// width-w NAF of a scalar; returns number of digits
+static int wnaf(int* digits, const Scalar& s, int w) {
+    uint64_t k[5] = {s.n[0], s.n[1], s.n[2], s.n[3], 0};
+    int len = 0;
+    auto is_zero = [&] { return (k[0] | k[1] | k[2] | k[3] | k[4]) == 0; };
+    while (!is_zero()) {
+        int d = 0;
+        if (k[0] & 1) {
+            d = (int)(k[0] & ((1u << w) - 1));
+            if (d >= (1 << (w - 1))) d -= (1 << w);
+            // k -= d
+            if (d > 0) {
+                u128 t = (u128)k[0] - (uint64_t)d;
+                k[0] = (uint64_t)t;
+                uint64_t br = (uint64_t)(t >> 127) & 1;
+                for (int i = 1; i < 5 && br; ++i) {
+                    u128 u = (u128)k[i] - 1;
+                    k[i] = (uint64_t)u;
+                    br = (uint64_t)(u >> 127) & 1;
+                }
+            } else {
+                u128 t = (u128)k[0] + (uint64_t)(-d);
+                k[0] = (uint64_t)t;
+                uint64_t c = (uint64_t)(t >> 64);
+                for (int i = 1; i < 5 && c; ++i) {
+                    u128 u = (u128)k[i] + 1;
+                    k[i] = (uint64_t)u;
+                    c = (uint64_t)(u >> 64);
+                }
+            }
+        }
+        digits[len++] = d;
+        // k >>= 1
+        for (int i = 0; i < 4; ++i) k[i] = (k[i] >> 1) | (k[i + 1] << 63);
+        k[4] >>= 1;
+    }
+    return len;
+}
+
+void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng) {
+    Gej acc;
+    acc.inf = true;
+    if (!a.inf && !sc_is_zero(na)) {
+        // odd multiples A, 3A, ..., 15A
+        Gej pre_j[8], a2;
+        pre_j[0] = a;
+        gej_double(a2, a);
+        for (int i = 1; i < 8; ++i) gej_add(pre_j[i], pre_j[i - 1], a2);
+        Ge pre[8];
+        batch_to_affine(pre, pre_j, 8);
+        int digits[260];
+        int len = wnaf(digits, na, 5);
+        for (int i = len - 1; i >= 0; --i) {
+            gej_double(acc, acc);
+            int d = digits[i];
+            if (d > 0) {
+                gej_add_ge(acc, acc, pre[(d - 1) / 2]);
+            } else if (d < 0) {
+                Ge neg = pre[(-d - 1) / 2];
+                fe_neg(neg.y, neg.y);
+                gej_add_ge(acc, acc, neg);
+            }
+        }
+    }
+    if (!sc_is_zero(ng)) {
+        Gej g;
+        ecmult_gen(g, ng);
+        gej_add(acc, acc, g);
+    }
+    r = acc;
+}
+
+// ---------------------------------------------------------------- keys
+bool pubkey_parse(Ge& r, const unsigned char* in, size_t len) {
+    r.inf = true;
+    if (len == 33 && (in[0] == 0x02 || in[0] == 0x03)) {
+        bool of;
+        fe_set_b32(r.x, in + 1, &of);
+        if (of) return false;
+        Fe x3, seven, y;
+        fe_sqr(x3, r.x);
+        fe_mul(x3, x3, r.x);
+        fe_set_int(seven, 7);
+        fe_add(x3, x3, seven);
+        if (!fe_sqrt(y, x3)) return false;
+        if (fe_is_odd(y) != (in[0] == 0x03)) fe_neg(y, y);
+        r.y = y;
+        r.inf = false;
+        return true;
+    }
+    if (len == 65 && (in[0] == 0x04 || in[0] == 0x06 || in[0] == 0x07)) {
+        bool ofx, ofy;
+        fe_set_b32(r.x, in + 1, &ofx);
+        fe_set_b32(r.y, in + 33, &ofy);
+        if (ofx || ofy) return false;
+        r.inf = false;
+        if ((in[0] == 0x06 || in[0] == 0x07) && fe_is_odd(r.y) != (in[0] == 0x07)) {
+            r.inf = true;
+            return false;
+        }
+        if (!ge_is_valid(r)) {
+            r.inf = true;
+            return false;
+        }
+        return true;
+    }
+    return false;
+}
+
+std::vector<unsigned char> pubkey_serialize(const Ge& p, bool compressed) {
+    std::vector<unsigned char> out(compressed ? 33 : 65);
+    fe_get_b32(&out[1], p.x);
+    if (compressed) {
+        out[0] = fe_is_odd(p.y) ? 0x03 : 0x02;
+    } else {
+        out[0] = 0x04;
+        fe_get_b32(&out[33], p.y);
+    }
+    return out;
+}
+
+bool seckey_verify(const unsigned char* seckey32) {
+    Scalar s;
+    bool of;
+    sc_set_b32(s, seckey32, &of);
+    return !of && !sc_is_zero(s);
+}
+
+bool pubkey_create(Ge& r, const unsigned char* seckey32) {
+    Scalar s;
+    bool of;
+    sc_set_b32(s, seckey32, &of);
+    if (of || sc_is_zero(s)) return false;
+    Gej pj;
+    ecmult_gen(pj, s);
+    ge_set_gej(r, pj);
+    return true;
+}
+
+bool seckey_tweak_add(unsigned char* seckey32, const unsigned char* tweak32) {
+    Scalar s, t;
+    bool of1, of2;
+    sc_set_b32(s, seckey32, &of1);
+    sc_set_b32(t, tweak32, &of2);
+    if (of1 || of2) return false;
+    sc_add(s, s, t);
+    if (sc_is_zero(s)) return false;
+    sc_get_b32(seckey32, s);
+    return true;
+}
+
+bool pubkey_tweak_add(Ge& p, const unsigned char* tweak32) {
+    Scalar t;
+    bool of;
+    sc_set_b32(t, tweak32, &of);
+    if (of) return false;
+    Gej pj, tg;
+    gej_set_ge(pj, p);
+    ecmult_gen(tg, t);
+    gej_add(pj, pj, tg);
+    if (pj.inf) return false;
+    ge_set_gej(p, pj);
+    return true;
+}
+
+// ---------------------------------------------------------------- ECDSA
+bool sig_parse_compact(Signature& sig, const unsigned char* in64) {
+    bool of1, of2;
+    sc_set_b32(sig.r, in64, &of1);
+    sc_set_b32(sig.s, in64 + 32, &of2);
+    if (of1 || of2) {
+        memset(&sig, 0, sizeof(sig));
+        return false;
+    }
+    return true;
+}
+void sig_serialize_compact(unsigned char* out64, const Signature& sig) {
+    sc_get_b32(out64, sig.r);
+    sc_get_b32(out64 + 32, sig.s);
+}
+
+bool sig_parse_der_lax(Signature& sig, const unsigned char* input, size_t inputlen) {
+    size_t rpos, rlen, spos, slen, pos = 0, lenbyte;
+    unsigned char tmp[64] = {0};
+    memset(&sig, 0, sizeof(sig));
+    if (pos == inputlen || input[pos] != 0x30) return false;
+    pos++;
+    if (pos == inputlen) return false;
+    lenbyte = input[pos++];
+    if (lenbyte & 0x80) {
+        lenbyte -= 0x80;
+        if (pos + lenbyte > inputlen) return false;
+        pos += lenbyte;
+    }
+    auto read_int = [&](size_t& ipos, size_t& ilen) -> bool {
+        if (pos == inputlen || input[pos] != 0x02) return false;
+        pos++;
+        if (pos == inputlen) return false;
+        lenbyte = input[pos++];
+        if (lenbyte & 0x80) {
+            lenbyte -= 0x80;
+            if (pos + lenbyte > inputlen) return false;
+            while (lenbyte > 0 && input[pos] == 0) {
+                pos++;
+                lenbyte--;
+            }
+            if (lenbyte >= sizeof(size_t)) return false;
+            ilen = 0;
+            while (lenbyte > 0) {
+                ilen = (ilen << 8) + input[pos];
+                pos++;
+                lenbyte--;
+            }
+        } else {
+            ilen = lenbyte;
+        }
+        if (ilen > inputlen - pos) return false;
+        ipos = pos;
+        pos += ilen;
+        return true;
+    };
+    if (!read_int(rpos, rlen)) return false;
+    if (!read_int(spos, slen)) return false;
+    bool overflow = false;
+    while (rlen > 0 && input[rpos] == 0) {
+        rlen--;
+        rpos++;
+    }
+    if (rlen > 32) overflow = true;
+    else memcpy(tmp + 32 - rlen, input + rpos, rlen);
+    while (slen > 0 && input[spos] == 0) {
+        slen--;
+        spos++;
+    }
+    if (slen > 32) overflow = true;
+    else memcpy(tmp + 64 - slen, input + spos, slen);
+    if (!overflow) overflow = !sig_parse_compact(sig, tmp);
+    if (overflow) memset(&sig, 0, sizeof(sig)); // parsed but invalid
+    return true;
+}
+
+bool sig_parse_der_strict(Signature& sig, const unsigned char* in, size_t len) {
+    // 0x30 [len] 0x02 [rlen] [r] 0x02 [slen] [s], minimal encodings
+    if (len < 8 || len > 72 || in[0] != 0x30 || in[1] != len - 2) return false;
+    size_t rlen = in[3];
+    if (in[2] != 0x02 || rlen == 0 || 5 + rlen >= len) return false;
+    size_t slen = in[5 + rlen];
+    if (in[4 + rlen] != 0x02 || slen == 0 || rlen + slen + 6 != len) return false;
+    if ((in[4] & 0x80) || (rlen > 1 && in[4] == 0 && !(in[5] & 0x80))) return false;
+    if ((in[6 + rlen] & 0x80) || (slen > 1 && in[6 + rlen] == 0 && !(in[7 + rlen] & 0x80))) return false;
+    return sig_parse_der_lax(sig, in, len) && !(sc_is_zero(sig.r) && sc_is_zero(sig.s));
+}
+
+std::vector<unsigned char> sig_serialize_der(const Signature& sig) {
+    unsigned char r[33] = {0}, s[33] = {0};
+    sc_get_b32(r + 1, sig.r);
+    sc_get_b32(s + 1, sig.s);
+    const unsigned char* rp = r;
+    const unsigned char* sp = s;
+    size_t lenR = 33, lenS = 33;
+    while (lenR > 1 && rp[0] == 0 && rp[1] < 0x80) {
+        lenR--;
+        rp++;
+    }
+    while (lenS > 1 && sp[0] == 0 && sp[1] < 0x80) {
+        lenS--;
+        sp++;
+    }
+    std::vector<unsigned char> out;
+    out.push_back(0x30);
+    out.push_back((unsigned char)(4 + lenR + lenS));
+    out.push_back(0x02);
+    out.push_back((unsigned char)lenR);
+    out.insert(out.end(), rp, rp + lenR);
+    out.push_back(0x02);
+    out.push_back((unsigned char)lenS);
+    out.insert(out.end(), sp, sp + lenS);
+    return out;
+}
+
+bool sig_normalize(Signature& sig) {
+    if (sc_is_high(sig.s)) {
+        sc_neg(sig.s, sig.s);
+        return true;
+    }
+    return false;
+}
+
+bool ecdsa_verify(const Signature& sig, const unsigned char* msg32, const Ge& pub) {
+    if (pub.inf || sc_is_zero(sig.r) || sc_is_zero(sig.s) || sc_is_high(sig.s)) return false;
+    Scalar e, w, u1, u2;
+    sc_set_b32(e, msg32);
+    sc_inv(w, sig.s);
+    sc_mul(u1, e, w);
+    sc_mul(u2, sig.r, w);
+    Gej pj, R;
+    gej_set_ge(pj, pub);
+    ecmult(R, pj, u2, u1);
+    if (R.inf) return false;
+    Ge Ra;
+    ge_set_gej(Ra, R);
+    unsigned char xb[32];
+    fe_get_b32(xb, Ra.x);
+    Scalar xr;
+    sc_set_b32(xr, xb);
+    return memcmp(xr.n, sig.r.n, 32) == 0;
+}
+
+void rfc6979_nonce(unsigned char* out32, const unsigned char* msg32, const unsigned char* key32,
+                   const unsigned char* extra32, unsigned int counter) {
+    unsigned char keydata[96];
+    size_t kl = 64;
+    memcpy(keydata, key32, 32);
+    memcpy(keydata + 32, msg32, 32);
+    if (extra32) {
+        memcpy(keydata + 64, extra32, 32);
+        kl = 96;
+    }
+    unsigned char v[32], k[32];
+    memset(v, 0x01, 32);
+    memset(k, 0x00, 32);
+    const unsigned char zero = 0x00, one = 0x01;
+    CHMAC_SHA256(k, 32).Write(v, 32).Write(&zero, 1).Write(keydata, kl).Finalize(k);
+    CHMAC_SHA256(k, 32).Write(v, 32).Finalize(v);
+    CHMAC_SHA256(k, 32).Write(v, 32).Write(&one, 1).Write(keydata, kl).Finalize(k);
+    CHMAC_SHA256(k, 32).Write(v, 32).Finalize(v);
+    bool retry = false;
+    for (unsigned int i = 0; i <= counter; ++i) {
+        if (retry) {
+            CHMAC_SHA256(k, 32).Write(v, 32).Write(&zero, 1).Finalize(k);
+            CHMAC_SHA256(k, 32).Write(v, 32).Finalize(v);
+        }
+        CHMAC_SHA256(k, 32).Write(v, 32).Finalize(v);
+        memcpy(out32, v, 32);
+        retry = true;
+    }
+    memory_cleanse(k, 32);
+    memory_cleanse(v, 32);
+    memory_cleanse(keydata, sizeof(keydata));
+}
+
+bool ecdsa_sign(Signature& sig, int* recid, const unsigned char* msg32, const unsigned char* seckey32,
+                const unsigned char* extra32) {
+    Scalar d, e;
+    bool of;
+    sc_set_b32(d, seckey32, &of);
+    if (of || sc_is_zero(d)) return false;
+    sc_set_b32(e, msg32);
+    for (unsigned int counter = 0; counter < 1000; ++counter) {
+        unsigned char nonce[32];
+        rfc6979_nonce(nonce, msg32, seckey32, extra32, counter);
+        Scalar k;
+        sc_set_b32(k, nonce, &of);
+        if (of || sc_is_zero(k)) continue;
+        Gej Rj;
+        ecmult_gen(Rj, k);
+        Ge R;
+        ge_set_gej(R, Rj);
+        unsigned char xb[32];
+        fe_get_b32(xb, R.x);
+        bool xof;
+        sc_set_b32(sig.r, xb, &xof);
+        int rid = (xof ? 2 : 0) | (fe_is_odd(R.y) ? 1 : 0);
+        Scalar n, kinv;
+        sc_mul(n, sig.r, d);
+        sc_add(n, n, e);
+        sc_inv(kinv, k);
+        sc_mul(sig.s, kinv, n);
+        if (sc_is_zero(sig.r) || sc_is_zero(sig.s)) continue;
+        if (sc_is_high(sig.s)) {
+            sc_neg(sig.s, sig.s);
+            rid ^= 1;
+        }
+        if (recid) *recid = rid;
+        return true;
+    }
+    return false;
+}
+
+bool ecdsa_recover(Ge& pub, const Signature& sig, int recid, const unsigned char* msg32) {
+    if (sc_is_zero(sig.r) || sc_is_zero(sig.s) || recid < 0 || recid > 3) return false;
+    unsigned char rb[32];
+    sc_get_b32(rb, sig.r);
+    Fe x;
+    fe_set_b32(x, rb);
+    if (recid & 2) {
+        // x = r + n, must be < p
+        static const uint64_t NN[4] = {0xBFD25E8CD0364141ULL, 0xBAAEDCE6AF48A03BULL, 0xFFFFFFFFFFFFFFFEULL,
+                                       0xFFFFFFFFFFFFFFFFULL};
+        uint64_t t[4];
+        if (add4(t, x.n, NN)) return false;
+        if (geq4(t, P)) return false;
+        memcpy(x.n, t, 32);
+    }
+    Fe x3, seven, y;
+    fe_sqr(x3, x);
+    fe_mul(x3, x3, x);
+    fe_set_int(seven, 7);
+    fe_add(x3, x3, seven);
+    if (!fe_sqrt(y, x3)) return false;
+    if (fe_is_odd(y) != (bool)(recid & 1)) fe_neg(y, y);
+    Ge R;
+    R.x = x;
+    R.y = y;
+    R.inf = false;
+    Scalar e, rn, u1, u2;
+    sc_set_b32(e, msg32);
+    sc_inv(rn, sig.r);
+    sc_mul(u1, rn, e);
+    sc_neg(u1, u1);
+    sc_mul(u2, rn, sig.s);
+    Gej Rj, Q;
+    gej_set_ge(Rj, R);
+    ecmult(Q, Rj, u2, u1);
+    if (Q.inf) return false;
+    ge_set_gej(pub, Q);
+    return true;
+}
+
+bool VerifySignature(const unsigned char* pub, size_t publen, const unsigned char* sig, size_t siglen,
+                     const unsigned char* msg32) {
+    Ge p;
+    if (!pubkey_parse(p, pub, publen)) return false;
+    if (siglen == 0) return false;
+    Signature s;
+    if (!sig_parse_der_lax(s, sig, siglen)) return false;
+    sig_normalize(s);
+    return ecdsa_verify(s, msg32, p);
+}
+
+} // namespace secp
+} // namespace bcp
