@@ -1,0 +1,310 @@
+#include "node/coins.h"
+#include "keys/key.h"
+#include "secp256k1/secp256k1.h"
+
+#include <cassert>
+#include <cstring>
+
+namespace bcp {
+
+// ------------------------------------------------------------------ amount compression
+uint64_t CompressAmount(uint64_t n) {
+    if (n == 0) return 0;
+    int e = 0;
+    while ((n % 10) == 0 && e < 9) {
+        n /= 10;
+        e++;
+    }
+    if (e < 9) {
+        const int d = (int)(n % 10);
+        n /= 10;
+        return 1 + (n * 9 + d - 1) * 10 + e;
+    }
+    return 1 + (n - 1) * 10 + 9;
+}
+
+uint64_t DecompressAmount(uint64_t x) {
+    if (x == 0) return 0;
+    x--;
+    int e = (int)(x % 10);
+    x /= 10;
+    uint64_t n = 0;
+    if (e < 9) {
+        const int d = (int)(x % 9) + 1;
+        x /= 9;
+        n = x * 10 + d;
+    } else {
+        n = x + 1;
+    }
+    while (e) {
+        n *= 10;
+        e--;
+    }
+    return n;
+}
+
+// ------------------------------------------------------------------ script compression
+bool CompressScript(const CScript& s, std::vector<unsigned char>& out) {
+    if (s.size() == 25 && s[0] == OP_DUP && s[1] == OP_HASH160 && s[2] == 20 && s[23] == OP_EQUALVERIFY &&
+        s[24] == OP_CHECKSIG) {
+        out.assign(21, 0);
+        memcpy(&out[1], &s[3], 20);
+        return true;
+    }
+    if (s.size() == 23 && s[0] == OP_HASH160 && s[1] == 20 && s[22] == OP_EQUAL) {
+        out.assign(21, 1);
+        memcpy(&out[1], &s[2], 20);
+        return true;
+    }
+    if (s.size() == 35 && s[0] == 33 && s[34] == OP_CHECKSIG && (s[1] == 0x02 || s[1] == 0x03)) {
+        out.assign(33, s[1]);
+        memcpy(&out[1], &s[2], 32);
+        return true;
+    }
+    if (s.size() == 67 && s[0] == 65 && s[66] == OP_CHECKSIG && s[1] == 0x04) {
+        CPubKey pk(s.begin() + 1, s.begin() + 66);
+        if (!pk.IsFullyValid()) return false; // only valid keys can be re-derived from x
+        out.assign(33, 0x04 | (s[65] & 0x01));
+        memcpy(&out[1], &s[2], 32);
+        return true;
+    }
+    return false;
+}
+
+unsigned GetSpecialScriptSize(unsigned nSize) {
+    if (nSize == 0 || nSize == 1) return 20;
+    if (nSize >= 2 && nSize <= 5) return 32;
+    return 0;
+}
+
+bool DecompressScript(CScript& s, unsigned nSize, const std::vector<unsigned char>& in) {
+    switch (nSize) {
+    case 0:
+        s.resize(25);
+        s[0] = OP_DUP;
+        s[1] = OP_HASH160;
+        s[2] = 20;
+        memcpy(&s[3], in.data(), 20);
+        s[23] = OP_EQUALVERIFY;
+        s[24] = OP_CHECKSIG;
+        return true;
+    case 1:
+        s.resize(23);
+        s[0] = OP_HASH160;
+        s[1] = 20;
+        memcpy(&s[2], in.data(), 20);
+        s[22] = OP_EQUAL;
+        return true;
+    case 2:
+    case 3:
+        s.resize(35);
+        s[0] = 33;
+        s[1] = (unsigned char)nSize;
+        memcpy(&s[2], in.data(), 32);
+        s[34] = OP_CHECKSIG;
+        return true;
+    case 4:
+    case 5: {
+        unsigned char vch[33];
+        vch[0] = (unsigned char)(nSize - 2);
+        memcpy(&vch[1], in.data(), 32);
+        CPubKey pk(vch, vch + 33);
+        if (!pk.Decompress()) return false;
+        s.resize(67);
+        s[0] = 65;
+        memcpy(&s[1], pk.begin(), 65);
+        s[66] = OP_CHECKSIG;
+        return true;
+    }
+    }
+    return false;
+}
+
+// ------------------------------------------------------------------ cache
+SaltedOutpointHasher::SaltedOutpointHasher() {
+    static const std::pair<uint64_t, uint64_t> salt = [] {
+        uint64_t a, b;
+        GetRandBytes((unsigned char*)&a, 8);
+        GetRandBytes((unsigned char*)&b, 8);
+        return std::make_pair(a, b);
+    }();
+    k0 = salt.first;
+    k1 = salt.second;
+}
+
+CCoinsViewCache::CCoinsViewCache(CCoinsView* b) : CCoinsViewBacked(b) {}
+
+size_t CCoinsViewCache::DynamicMemoryUsage() const {
+    // node overhead (~ key + entry + bucket pointer) plus script heap usage
+    return cacheCoins.size() * (sizeof(COutPoint) + sizeof(CCoinsCacheEntry) + 2 * sizeof(void*)) +
+           cacheCoins.bucket_count() * sizeof(void*) + cachedCoinsUsage;
+}
+
+CCoinsMap::iterator CCoinsViewCache::FetchCoin(const COutPoint& outpoint) const {
+    auto it = cacheCoins.find(outpoint);
+    if (it != cacheCoins.end()) return it;
+    Coin tmp;
+    if (!base->GetCoin(outpoint, tmp)) return cacheCoins.end();
+    auto ret = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint),
+                                  std::forward_as_tuple(std::move(tmp)))
+                   .first;
+    if (ret->second.coin.IsSpent()) {
+        // a spent coin in the parent is FRESH from our point of view
+        ret->second.flags = CCoinsCacheEntry::FRESH;
+    }
+    cachedCoinsUsage += ret->second.coin.DynamicMemoryUsage();
+    return ret;
+}
+
+bool CCoinsViewCache::GetCoin(const COutPoint& outpoint, Coin& coin) const {
+    auto it = FetchCoin(outpoint);
+    if (it == cacheCoins.end()) return false;
+    coin = it->second.coin;
+    return !coin.IsSpent();
+}
+
+void CCoinsViewCache::AddCoin(const COutPoint& outpoint, Coin&& coin, bool possible_overwrite) {
+    assert(!coin.IsSpent());
+    if (coin.out.scriptPubKey.IsUnspendable()) return;
+    auto ins = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
+    auto it = ins.first;
+    bool fresh = false;
+    if (!ins.second) cachedCoinsUsage -= it->second.coin.DynamicMemoryUsage();
+    if (!possible_overwrite) {
+        if (!it->second.coin.IsSpent()) throw std::logic_error("Adding new coin that replaces non-pruned entry");
+        fresh = !(it->second.flags & CCoinsCacheEntry::DIRTY);
+    }
+    it->second.coin = std::move(coin);
+    it->second.flags |= CCoinsCacheEntry::DIRTY | (fresh ? CCoinsCacheEntry::FRESH : 0);
+    cachedCoinsUsage += it->second.coin.DynamicMemoryUsage();
+}
+
+void AddCoins(CCoinsViewCache& cache, const CTransaction& tx, int nHeight, bool check) {
+    const bool fCoinbase = tx.IsCoinBase();
+    const uint256& txid = tx.GetHash();
+    for (size_t i = 0; i < tx.vout.size(); ++i) {
+        const COutPoint op(txid, (uint32_t)i);
+        const bool overwrite = check ? cache.HaveCoin(op) : fCoinbase;
+        cache.AddCoin(op, Coin(tx.vout[i], nHeight, fCoinbase), overwrite);
+    }
+}
+
+bool CCoinsViewCache::SpendCoin(const COutPoint& outpoint, Coin* moveout) {
+    auto it = FetchCoin(outpoint);
+    if (it == cacheCoins.end()) return false;
+    cachedCoinsUsage -= it->second.coin.DynamicMemoryUsage();
+    if (moveout) *moveout = std::move(it->second.coin);
+    if (it->second.flags & CCoinsCacheEntry::FRESH) {
+        cacheCoins.erase(it);
+    } else {
+        it->second.flags |= CCoinsCacheEntry::DIRTY;
+        it->second.coin.Clear();
+    }
+    return true;
+}
+
+static const Coin coinEmpty;
+
+const Coin& CCoinsViewCache::AccessCoin(const COutPoint& outpoint) const {
+    auto it = FetchCoin(outpoint);
+    if (it == cacheCoins.end()) return coinEmpty;
+    return it->second.coin;
+}
+
+bool CCoinsViewCache::HaveCoin(const COutPoint& outpoint) const {
+    auto it = FetchCoin(outpoint);
+    return it != cacheCoins.end() && !it->second.coin.IsSpent();
+}
+
+bool CCoinsViewCache::HaveCoinInCache(const COutPoint& outpoint) const {
+    auto it = cacheCoins.find(outpoint);
+    return it != cacheCoins.end() && !it->second.coin.IsSpent();
+}
+
+uint256 CCoinsViewCache::GetBestBlock() const {
+    if (hashBlock.IsNull()) hashBlock = base->GetBestBlock();
+    return hashBlock;
+}
+
+void CCoinsViewCache::SetBestBlock(const uint256& h) { hashBlock = h; }
+
+bool CCoinsViewCache::BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlockIn) {
+    for (auto it = mapCoins.begin(); it != mapCoins.end(); it = mapCoins.erase(it)) {
+        if (!(it->second.flags & CCoinsCacheEntry::DIRTY)) continue; // non-dirty: nothing to merge
+        auto itUs = cacheCoins.find(it->first);
+        if (itUs == cacheCoins.end()) {
+            // child has a modified entry the parent lacks; a FRESH spent one can be dropped
+            if (!(it->second.flags & CCoinsCacheEntry::FRESH && it->second.coin.IsSpent())) {
+                CCoinsCacheEntry& entry = cacheCoins[it->first];
+                entry.coin = std::move(it->second.coin);
+                cachedCoinsUsage += entry.coin.DynamicMemoryUsage();
+                entry.flags = CCoinsCacheEntry::DIRTY;
+                if (it->second.flags & CCoinsCacheEntry::FRESH) entry.flags |= CCoinsCacheEntry::FRESH;
+            }
+        } else {
+            if ((it->second.flags & CCoinsCacheEntry::FRESH) && !itUs->second.coin.IsSpent())
+                throw std::logic_error("FRESH flag misapplied to cache entry for base transaction with spendable outputs");
+            if ((itUs->second.flags & CCoinsCacheEntry::FRESH) && it->second.coin.IsSpent()) {
+                // parent entry is FRESH and now spent: forget it entirely
+                cachedCoinsUsage -= itUs->second.coin.DynamicMemoryUsage();
+                cacheCoins.erase(itUs);
+            } else {
+                cachedCoinsUsage -= itUs->second.coin.DynamicMemoryUsage();
+                itUs->second.coin = std::move(it->second.coin);
+                cachedCoinsUsage += itUs->second.coin.DynamicMemoryUsage();
+                itUs->second.flags |= CCoinsCacheEntry::DIRTY;
+            }
+        }
+    }
+    hashBlock = hashBlockIn;
+    return true;
+}
+
+bool CCoinsViewCache::Flush() {
+    const bool ok = base->BatchWrite(cacheCoins, hashBlock);
+    cacheCoins.clear();
+    cachedCoinsUsage = 0;
+    return ok;
+}
+
+void CCoinsViewCache::Uncache(const COutPoint& outpoint) {
+    auto it = cacheCoins.find(outpoint);
+    if (it != cacheCoins.end() && it->second.flags == 0) {
+        cachedCoinsUsage -= it->second.coin.DynamicMemoryUsage();
+        cacheCoins.erase(it);
+    }
+}
+
+const CTxOut& CCoinsViewCache::GetOutputFor(const CTxIn& input) const {
+    const Coin& c = AccessCoin(input.prevout);
+    if (c.IsSpent()) throw std::logic_error("GetOutputFor on spent coin");
+    return c.out;
+}
+
+Amount CCoinsViewCache::GetValueIn(const CTransaction& tx) const {
+    if (tx.IsCoinBase()) return 0;
+    Amount n = 0;
+    for (const auto& in : tx.vin) n += GetOutputFor(in).nValue;
+    return n;
+}
+
+bool CCoinsViewCache::HaveInputs(const CTransaction& tx) const {
+    if (tx.IsCoinBase()) return true;
+    for (const auto& in : tx.vin)
+        if (!HaveCoin(in.prevout)) return false;
+    return true;
+}
+
+static const size_t MAX_OUTPUTS_PER_TX = 1000000 / 9; // min txout size
+
+const Coin& AccessByTxid(const CCoinsViewCache& view, const uint256& txid) {
+    COutPoint iter(txid, 0);
+    while (iter.n < MAX_OUTPUTS_PER_TX) {
+        const Coin& alt = view.AccessCoin(iter);
+        if (!alt.IsSpent()) return alt;
+        ++iter.n;
+    }
+    return coinEmpty;
+}
+
+} // namespace bcp

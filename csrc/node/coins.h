@@ -1,0 +1,230 @@
+// UTXO set: Coin, compressed on-disk encoding, layered coin views and the cache.
+// Parity: reference src/coins.{h,cpp} (Coin :27-70 height<<1|coinbase, CCoinsView,
+// CCoinsViewBacked, CCoinsViewCache with DIRTY/FRESH flags, BatchWrite, AddCoins,
+// SpendCoin with undo capture, AccessByTxid) and src/compressor.{h,cpp}
+// (CompressAmount/DecompressAmount, 6 special script encodings), src/undo.h
+// (CTxUndo/CBlockUndo, TxInUndoSerializer).
+#pragma once
+#include "crypto/hashes.h"
+#include "primitives/transaction.h"
+
+#include <functional>
+#include <memory>
+#include <unordered_map>
+
+namespace bcp {
+
+uint64_t CompressAmount(uint64_t n);
+uint64_t DecompressAmount(uint64_t x);
+
+// Script compression: P2PKH/P2SH/P2PK stored in 21 or 33 bytes.
+bool CompressScript(const CScript& script, std::vector<unsigned char>& out);
+unsigned GetSpecialScriptSize(unsigned nSize);
+bool DecompressScript(CScript& script, unsigned nSize, const std::vector<unsigned char>& in);
+static const unsigned int nSpecialScripts = 6;
+
+template <typename S> void SerializeCompressedScript(S& s, const CScript& script) {
+    std::vector<unsigned char> compr;
+    if (CompressScript(script, compr)) {
+        s.write((const char*)compr.data(), compr.size());
+        return;
+    }
+    WriteVarInt(s, script.size() + nSpecialScripts);
+    s.write((const char*)script.data(), script.size());
+}
+template <typename S> void UnserializeCompressedScript(S& s, CScript& script) {
+    unsigned nSize = (unsigned)ReadVarInt(s);
+    if (nSize < nSpecialScripts) {
+        std::vector<unsigned char> v(GetSpecialScriptSize(nSize));
+        s.read((char*)v.data(), v.size());
+        DecompressScript(script, nSize, v);
+        return;
+    }
+    nSize -= nSpecialScripts;
+    if (nSize > (unsigned)MAX_SCRIPT_SIZE) {
+        // overly long script: replace with a short unspendable one, skip the payload
+        script.clear();
+        script << OP_RETURN;
+        std::vector<char> skip(nSize);
+        s.read(skip.data(), nSize);
+    } else {
+        script.resize(nSize);
+        s.read((char*)script.data(), nSize);
+    }
+}
+template <typename S> void SerializeCompressedTxOut(S& s, const CTxOut& out) {
+    WriteVarInt(s, CompressAmount((uint64_t)out.nValue));
+    SerializeCompressedScript(s, out.scriptPubKey);
+}
+template <typename S> void UnserializeCompressedTxOut(S& s, CTxOut& out) {
+    out.nValue = (Amount)DecompressAmount(ReadVarInt(s));
+    UnserializeCompressedScript(s, out.scriptPubKey);
+}
+
+class Coin {
+public:
+    CTxOut out;
+    bool fCoinBase = false;
+    uint32_t nHeight = 0;
+
+    Coin() {}
+    Coin(CTxOut o, int h, bool cb) : out(std::move(o)), fCoinBase(cb), nHeight((uint32_t)h) {}
+    void Clear() {
+        out.SetNull();
+        fCoinBase = false;
+        nHeight = 0;
+    }
+    bool IsSpent() const { return out.IsNull(); }
+    bool IsCoinBase() const { return fCoinBase; }
+    uint32_t GetHeight() const { return nHeight; }
+    const CTxOut& GetTxOut() const { return out; }
+    size_t DynamicMemoryUsage() const { return out.scriptPubKey.capacity(); }
+
+    template <typename S> void Serialize(S& s) const {
+        WriteVarInt(s, (uint64_t)nHeight * 2 + (fCoinBase ? 1 : 0));
+        SerializeCompressedTxOut(s, out);
+    }
+    template <typename S> void Unserialize(S& s) {
+        const uint64_t code = ReadVarInt(s);
+        nHeight = (uint32_t)(code >> 1);
+        fCoinBase = code & 1;
+        UnserializeCompressedTxOut(s, out);
+    }
+};
+
+// Undo record of one spent input: the coin, with height/coinbase always present
+// (format is the reference's post-0.15 TxInUndoSerializer: VARINT(h*2+cb), [VARINT(0)
+// if h>0], compressed txout).
+struct TxInUndoFormatter {
+    template <typename S> static void Ser(S& s, const Coin& c) {
+        WriteVarInt(s, (uint64_t)c.nHeight * 2 + (c.fCoinBase ? 1 : 0));
+        if (c.nHeight > 0) WriteVarInt(s, 0); // legacy tx-version placeholder
+        SerializeCompressedTxOut(s, c.out);
+    }
+    template <typename S> static void Unser(S& s, Coin& c) {
+        const uint64_t code = ReadVarInt(s);
+        c.nHeight = (uint32_t)(code >> 1);
+        c.fCoinBase = code & 1;
+        if (c.nHeight > 0) ReadVarInt(s);
+        UnserializeCompressedTxOut(s, c.out);
+    }
+};
+
+class CTxUndo {
+public:
+    std::vector<Coin> vprevout;
+    template <typename S> void Serialize(S& s) const {
+        WriteCompactSize(s, vprevout.size());
+        for (const Coin& c : vprevout) TxInUndoFormatter::Ser(s, c);
+    }
+    template <typename S> void Unserialize(S& s) {
+        const uint64_t n = ReadCompactSize(s);
+        if (n > MAX_TX_SIZE_FOR_UNDO) throw ser_error("too many input undo records");
+        vprevout.resize(n);
+        for (Coin& c : vprevout) TxInUndoFormatter::Unser(s, c);
+    }
+    static const uint64_t MAX_TX_SIZE_FOR_UNDO = 1000000 / 41; // min txin size
+};
+
+class CBlockUndo {
+public:
+    std::vector<CTxUndo> vtxundo; // one per tx except the coinbase
+    template <typename S> void Serialize(S& s) const { ::bcp::Serialize(s, vtxundo); }
+    template <typename S> void Unserialize(S& s) { ::bcp::Unserialize(s, vtxundo); }
+};
+
+struct SaltedOutpointHasher {
+    uint64_t k0, k1;
+    SaltedOutpointHasher();
+    size_t operator()(const COutPoint& o) const { return SipHashUint256Extra(k0, k1, o.hash.begin(), o.n); }
+};
+
+struct CCoinsCacheEntry {
+    Coin coin;
+    unsigned char flags = 0;
+    enum Flags { DIRTY = 1, FRESH = 2 };
+    CCoinsCacheEntry() {}
+    explicit CCoinsCacheEntry(Coin&& c) : coin(std::move(c)) {}
+};
+typedef std::unordered_map<COutPoint, CCoinsCacheEntry, SaltedOutpointHasher> CCoinsMap;
+
+class CCoinsViewCursor {
+public:
+    virtual ~CCoinsViewCursor() {}
+    virtual bool GetKey(COutPoint& key) const = 0;
+    virtual bool GetValue(Coin& coin) const = 0;
+    virtual bool Valid() const = 0;
+    virtual void Next() = 0;
+    const uint256& GetBestBlock() const { return hashBlock; }
+
+protected:
+    uint256 hashBlock;
+};
+
+class CCoinsView {
+public:
+    virtual ~CCoinsView() {}
+    virtual bool GetCoin(const COutPoint& outpoint, Coin& coin) const { return false; }
+    virtual bool HaveCoin(const COutPoint& outpoint) const {
+        Coin c;
+        return GetCoin(outpoint, c);
+    }
+    virtual uint256 GetBestBlock() const { return uint256(); }
+    virtual bool BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlock) { return false; }
+    virtual std::unique_ptr<CCoinsViewCursor> Cursor() const { return nullptr; }
+    virtual size_t EstimateSize() const { return 0; }
+};
+
+class CCoinsViewBacked : public CCoinsView {
+public:
+    explicit CCoinsViewBacked(CCoinsView* v) : base(v) {}
+    bool GetCoin(const COutPoint& o, Coin& c) const override { return base->GetCoin(o, c); }
+    bool HaveCoin(const COutPoint& o) const override { return base->HaveCoin(o); }
+    uint256 GetBestBlock() const override { return base->GetBestBlock(); }
+    bool BatchWrite(CCoinsMap& m, const uint256& h) override { return base->BatchWrite(m, h); }
+    std::unique_ptr<CCoinsViewCursor> Cursor() const override { return base->Cursor(); }
+    size_t EstimateSize() const override { return base->EstimateSize(); }
+    void SetBackend(CCoinsView& v) { base = &v; }
+
+protected:
+    CCoinsView* base;
+};
+
+class CCoinsViewCache : public CCoinsViewBacked {
+public:
+    explicit CCoinsViewCache(CCoinsView* base);
+    CCoinsViewCache(const CCoinsViewCache&) = delete;
+
+    bool GetCoin(const COutPoint& outpoint, Coin& coin) const override;
+    bool HaveCoin(const COutPoint& outpoint) const override;
+    uint256 GetBestBlock() const override;
+    void SetBestBlock(const uint256& hashBlock);
+    bool BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlock) override;
+    std::unique_ptr<CCoinsViewCursor> Cursor() const override {
+        throw std::logic_error("CCoinsViewCache cursor iteration not supported");
+    }
+
+    bool HaveCoinInCache(const COutPoint& outpoint) const;
+    const Coin& AccessCoin(const COutPoint& output) const;
+    void AddCoin(const COutPoint& outpoint, Coin&& coin, bool possible_overwrite);
+    bool SpendCoin(const COutPoint& outpoint, Coin* moveto = nullptr);
+    bool Flush();
+    void Uncache(const COutPoint& outpoint);
+    unsigned int GetCacheSize() const { return (unsigned)cacheCoins.size(); }
+    size_t DynamicMemoryUsage() const;
+    Amount GetValueIn(const CTransaction& tx) const;
+    bool HaveInputs(const CTransaction& tx) const;
+    const CTxOut& GetOutputFor(const CTxIn& input) const;
+
+protected:
+    CCoinsMap::iterator FetchCoin(const COutPoint& outpoint) const;
+    mutable uint256 hashBlock;
+    mutable CCoinsMap cacheCoins;
+    mutable size_t cachedCoinsUsage = 0;
+};
+
+// Add all outputs of a tx. check=true handles the BIP30 overwrite case.
+void AddCoins(CCoinsViewCache& cache, const CTransaction& tx, int nHeight, bool check = false);
+const Coin& AccessByTxid(const CCoinsViewCache& cache, const uint256& txid);
+
+} // namespace bcp

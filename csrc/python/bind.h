@@ -20,6 +20,7 @@ void bind_crypto(pyb::module_& m);
 void bind_equihash(pyb::module_& m);
 void bind_gpu(pyb::module_& m);
 void bind_consensus(pyb::module_& m);
+void bind_script(pyb::module_& m);
 void bind_node(pyb::module_& m);
 
 } // namespace py

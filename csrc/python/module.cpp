@@ -8,5 +8,6 @@ PYBIND11_MODULE(_bcpnative, m) {
     bcp::py::bind_equihash(m);
     bcp::py::bind_gpu(m);
     bcp::py::bind_consensus(m);
+    bcp::py::bind_script(m);
     bcp::py::bind_node(m);
 }
