@@ -90,11 +90,14 @@ int64_t Sha256dScanNonces(const unsigned char header80[80], const unsigned char 
                           uint64_t count, int device = -1);
 
 // --------------------------------------------------------------- secp256k1
-// ECDSA verification batch. msg/r/s are 32-byte big-endian, pubkeys 64-byte
-// (x||y big-endian, already parsed/decompressed on the host). s must be
-// low-S-normalised by the caller (reference CPubKey::Verify semantics).
+// ECDSA verification batch: N jobs, msg32 = N*32 (big-endian digest bytes as signed),
+// sig64 = N*64 (r||s big-endian, s low-S-normalised, r,s in [1,n-1] checked on host),
+// pub33 = N*33 compressed keys (0x02/0x03 || x; the host converts uncompressed/hybrid
+// keys after its on-curve check). The GPU decompresses, computes u1*G + u2*Q and
+// compares x(R) mod n with r. result[i] = 1 iff valid. Batches below the GPU
+// threshold should stay on the CPU (launch latency ~10 us).
 std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
-                                      const std::vector<unsigned char>& pub64, int device = -1);
+                                      const std::vector<unsigned char>& pub33, int device = -1);
 
 } // namespace gpu
 } // namespace bcp

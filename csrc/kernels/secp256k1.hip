@@ -1,0 +1,699 @@
+// Batched secp256k1 ECDSA verification on CDNA4 (gfx950).
+//
+// Replaces the CCheckQueue fan-out of CPubKey::Verify (reference src/pubkey.cpp:170-193,
+// src/validation.cpp:1740 scriptcheckqueue) for block validation.
+//
+// Work split (see csrc/node/sigverify.cpp):
+//   host  : lax-DER parse, low-S normalisation, r,s range, batch inversion of s
+//           (Montgomery trick: 1 inversion + 3 muls per signature), u1 = z/s, u2 = r/s
+//   device: pubkey decompression (sqrt chain), R = u1*G + u2*Q, check x(R) == r (mod n)
+//           without any field inversion: X == r*Z^2  or  X == (r+n)*Z^2 when r+n < p.
+//
+// Field arithmetic: 8 x 32-bit limbs (one VGPR each), schoolbook products through
+// 32x32+64 -> 64 multiply-adds, reduction by 2^256 = 2^32 + 977 (mod p).
+// u1*G: fixed-base comb over 32 byte-windows, table[i][j] = j*256^i*G (affine,
+// 512 KiB in global memory, L2/MALL resident) -> 32 mixed additions, no doublings.
+// u2*Q: width-4 wNAF with 4 odd multiples of Q held in LDS (96 B each per lane).
+// One lane per signature, 128-lane workgroups (2 waves) -> 48 KiB LDS per WG.
+#include <hip/hip_runtime.h>
+
+#include "kernels/gpu_api.h"
+#include "kernels/hip_util.h"
+#include "secp256k1/secp256k1.h"
+
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+namespace bcp {
+namespace gpu {
+
+namespace {
+
+struct fe {
+    uint32_t v[8];
+};
+
+__device__ __constant__ uint32_t P_LIMBS[8] = {0xFFFFFC2F, 0xFFFFFFFE, 0xFFFFFFFF, 0xFFFFFFFF,
+                                               0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF};
+
+__device__ __forceinline__ void fe_set(fe& r, const fe& a) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = a.v[i];
+}
+
+// r = a - p if a >= p (a < 2p)
+__device__ __forceinline__ void fe_cond_sub_p(fe& a, uint32_t carry_in) {
+    uint32_t t[8];
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t d = (uint64_t)a.v[i] - P_LIMBS[i] - borrow;
+        t[i] = (uint32_t)d;
+        borrow = (d >> 63) & 1;
+    }
+    // take t if carry_in (value >= 2^256) or no borrow (a >= p)
+    const bool take = carry_in || !borrow;
+#pragma unroll
+    for (int i = 0; i < 8; i++) a.v[i] = take ? t[i] : a.v[i];
+}
+
+__device__ __forceinline__ void fe_add(fe& r, const fe& a, const fe& b) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        c += (uint64_t)a.v[i] + b.v[i];
+        r.v[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    fe_cond_sub_p(r, (uint32_t)c);
+}
+
+__device__ __forceinline__ void fe_sub(fe& r, const fe& a, const fe& b) {
+    uint64_t borrow = 0;
+    uint32_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t d = (uint64_t)a.v[i] - b.v[i] - borrow;
+        t[i] = (uint32_t)d;
+        borrow = (d >> 63) & 1;
+    }
+    // if negative, add p back
+    uint64_t c = 0;
+    const uint32_t mask = borrow ? 0xFFFFFFFFu : 0u;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        c += (uint64_t)t[i] + (P_LIMBS[i] & mask);
+        r.v[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+
+__device__ __forceinline__ void fe_mul_small(fe& r, const fe& a, uint32_t m) {
+    // r = a*m mod p for small m (2, 3, 4, 8)
+    uint64_t c = 0;
+    uint32_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        c += (uint64_t)a.v[i] * m;
+        t[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    // fold c * 2^256 = c * (2^32 + 977)
+    uint64_t f = (uint64_t)t[0] + c * 977u;
+    r.v[0] = (uint32_t)f;
+    f = (f >> 32) + (uint64_t)t[1] + c;
+    r.v[1] = (uint32_t)f;
+    f >>= 32;
+#pragma unroll
+    for (int i = 2; i < 8; i++) {
+        f += t[i];
+        r.v[i] = (uint32_t)f;
+        f >>= 32;
+    }
+    fe_cond_sub_p(r, (uint32_t)f);
+}
+
+// 512-bit product reduced mod p.
+__device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) {
+    uint32_t t[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            const uint64_t p = (uint64_t)a.v[i] * b.v[j] + t[i + j] + carry;
+            t[i + j] = (uint32_t)p;
+            carry = p >> 32;
+        }
+        t[i + 8] = (uint32_t)carry;
+    }
+    // lo + hi * (2^32 + 977)
+    uint32_t u[9];
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        c += (uint64_t)t[i] + (uint64_t)t[8 + i] * 977u;
+        u[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    u[8] = (uint32_t)c;
+    // add hi << 32
+    c = 0;
+#pragma unroll
+    for (int i = 1; i < 9; i++) {
+        c += (uint64_t)u[i] + t[8 + i - 1];
+        u[i] = (uint32_t)c;
+        c >>= 32;
+    }
+    // u[8] + c*2^32 is the overflow limb(s): value = u[0..7] + (u[8] + c<<32) * 2^256
+    const uint64_t top = (uint64_t)u[8] + (c << 32);
+    // fold top * (2^32 + 977)
+    uint64_t f = (uint64_t)u[0] + (top & 0xFFFFFFFFu) * 977u;
+    const uint64_t topHi977 = (top >> 32) * 977u; // top>>32 is tiny (0 or 1)
+    r.v[0] = (uint32_t)f;
+    f = (f >> 32) + (uint64_t)u[1] + (top & 0xFFFFFFFFu) + topHi977;
+    r.v[1] = (uint32_t)f;
+    f = (f >> 32) + (uint64_t)u[2] + (top >> 32);
+    r.v[2] = (uint32_t)f;
+    f >>= 32;
+#pragma unroll
+    for (int i = 3; i < 8; i++) {
+        f += u[i];
+        r.v[i] = (uint32_t)f;
+        f >>= 32;
+    }
+    // f is 0 or 1 here; a final fold keeps r < 2^256 then reduce below p
+    if (f) {
+        uint64_t g = (uint64_t)r.v[0] + 977u;
+        r.v[0] = (uint32_t)g;
+        g = (g >> 32) + (uint64_t)r.v[1] + 1u;
+        r.v[1] = (uint32_t)g;
+        g >>= 32;
+#pragma unroll
+        for (int i = 2; i < 8; i++) {
+            g += r.v[i];
+            r.v[i] = (uint32_t)g;
+            g >>= 32;
+        }
+    }
+    fe_cond_sub_p(r, 0);
+}
+
+__device__ __forceinline__ void fe_sqr(fe& r, const fe& a) { fe_mul(r, a, a); }
+
+__device__ __forceinline__ void fe_sqr_n(fe& r, const fe& a, int n) {
+    fe_sqr(r, a);
+    for (int i = 1; i < n; i++) fe_sqr(r, r);
+}
+
+__device__ __forceinline__ bool fe_is_zero(const fe& a) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) o |= a.v[i];
+    return o == 0;
+}
+
+__device__ __forceinline__ bool fe_eq(const fe& a, const fe& b) {
+    uint32_t o = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) o |= a.v[i] ^ b.v[i];
+    return o == 0;
+}
+
+// r = a^((p+1)/4); returns whether r^2 == a (libsecp256k1 addition chain).
+__device__ bool fe_sqrt(fe& r, const fe& a) {
+    fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t1;
+    fe_sqr(x2, a);
+    fe_mul(x2, x2, a);
+    fe_sqr(x3, x2);
+    fe_mul(x3, x3, a);
+    fe_sqr_n(x6, x3, 3);
+    fe_mul(x6, x6, x3);
+    fe_sqr_n(x9, x6, 3);
+    fe_mul(x9, x9, x3);
+    fe_sqr_n(x11, x9, 2);
+    fe_mul(x11, x11, x2);
+    fe_sqr_n(x22, x11, 11);
+    fe_mul(x22, x22, x11);
+    fe_sqr_n(x44, x22, 22);
+    fe_mul(x44, x44, x22);
+    fe_sqr_n(x88, x44, 44);
+    fe_mul(x88, x88, x44);
+    fe_sqr_n(x176, x88, 88);
+    fe_mul(x176, x176, x88);
+    fe_sqr_n(x220, x176, 44);
+    fe_mul(x220, x220, x44);
+    fe_sqr_n(x223, x220, 3);
+    fe_mul(x223, x223, x3);
+    fe_sqr_n(t1, x223, 23);
+    fe_mul(t1, t1, x22);
+    fe_sqr_n(t1, t1, 6);
+    fe_mul(t1, t1, x2);
+    fe_sqr_n(r, t1, 2);
+    fe chk;
+    fe_sqr(chk, r);
+    return fe_eq(chk, a);
+}
+
+struct gej {
+    fe x, y, z;
+    bool inf;
+};
+
+// dbl-2009-l (a = 0): 2M + 5S
+__device__ __forceinline__ void gej_double(gej& r, const gej& p) {
+    if (p.inf) {
+        r.inf = true;
+        return;
+    }
+    fe A, B, C, D, E, F, t;
+    fe_sqr(A, p.x);
+    fe_sqr(B, p.y);
+    fe_sqr(C, B);
+    fe_add(t, p.x, B);
+    fe_sqr(t, t);
+    fe_sub(t, t, A);
+    fe_sub(t, t, C);
+    fe_mul_small(D, t, 2);
+    fe_mul_small(E, A, 3);
+    fe_sqr(F, E);
+    fe z3;
+    fe_mul(z3, p.y, p.z);
+    fe_mul_small(r.z, z3, 2);
+    fe_mul_small(t, D, 2);
+    fe_sub(r.x, F, t);
+    fe_sub(t, D, r.x);
+    fe_mul(t, E, t);
+    fe C8;
+    fe_mul_small(C8, C, 8);
+    fe_sub(r.y, t, C8);
+    r.inf = false;
+}
+
+// add-2007-bl, general Jacobian + Jacobian
+__device__ void gej_add(gej& r, const gej& a, const gej& b) {
+    if (a.inf) {
+        r = b;
+        return;
+    }
+    if (b.inf) {
+        r = a;
+        return;
+    }
+    fe z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t;
+    fe_sqr(z1z1, a.z);
+    fe_sqr(z2z2, b.z);
+    fe_mul(u1, a.x, z2z2);
+    fe_mul(u2, b.x, z1z1);
+    fe_mul(s1, a.y, b.z);
+    fe_mul(s1, s1, z2z2);
+    fe_mul(s2, b.y, a.z);
+    fe_mul(s2, s2, z1z1);
+    fe_sub(h, u2, u1);
+    fe_sub(rr, s2, s1);
+    if (fe_is_zero(h)) {
+        if (fe_is_zero(rr)) {
+            gej_double(r, a);
+        } else {
+            r.inf = true;
+        }
+        return;
+    }
+    fe_mul_small(i, h, 2);
+    fe_sqr(i, i);
+    fe_mul(j, h, i);
+    fe_mul_small(rr, rr, 2);
+    fe_mul(v, u1, i);
+    fe x3, y3, z3;
+    fe_sqr(x3, rr);
+    fe_sub(x3, x3, j);
+    fe_mul_small(t, v, 2);
+    fe_sub(x3, x3, t);
+    fe_sub(t, v, x3);
+    fe_mul(y3, rr, t);
+    fe_mul(t, s1, j);
+    fe_mul_small(t, t, 2);
+    fe_sub(y3, y3, t);
+    fe_add(t, a.z, b.z);
+    fe_sqr(t, t);
+    fe_sub(t, t, z1z1);
+    fe_sub(t, t, z2z2);
+    fe_mul(z3, t, h);
+    r.x = x3;
+    r.y = y3;
+    r.z = z3;
+    r.inf = false;
+}
+
+// madd-2007-bl, Jacobian + affine
+__device__ void gej_add_ge(gej& r, const gej& a, const fe& bx, const fe& by) {
+    if (a.inf) {
+        r.x = bx;
+        r.y = by;
+#pragma unroll
+        for (int k = 0; k < 8; k++) r.z.v[k] = k == 0 ? 1u : 0u;
+        r.inf = false;
+        return;
+    }
+    fe z1z1, u2, s2, h, hh, i, j, rr, v, t;
+    fe_sqr(z1z1, a.z);
+    fe_mul(u2, bx, z1z1);
+    fe_mul(s2, by, a.z);
+    fe_mul(s2, s2, z1z1);
+    fe_sub(h, u2, a.x);
+    fe_sub(rr, s2, a.y);
+    if (fe_is_zero(h)) {
+        if (fe_is_zero(rr)) {
+            gej_double(r, a);
+        } else {
+            r.inf = true;
+        }
+        return;
+    }
+    fe_sqr(hh, h);
+    fe_mul_small(i, hh, 4);
+    fe_mul(j, h, i);
+    fe_mul_small(rr, rr, 2);
+    fe_mul(v, a.x, i);
+    fe x3, y3, z3;
+    fe_sqr(x3, rr);
+    fe_sub(x3, x3, j);
+    fe_mul_small(t, v, 2);
+    fe_sub(x3, x3, t);
+    fe_sub(t, v, x3);
+    fe_mul(y3, rr, t);
+    fe_mul(t, a.y, j);
+    fe_mul_small(t, t, 2);
+    fe_sub(y3, y3, t);
+    fe_add(t, a.z, h);
+    fe_sqr(t, t);
+    fe_sub(t, t, z1z1);
+    fe_sub(z3, t, hh);
+    r.x = x3;
+    r.y = y3;
+    r.z = z3;
+    r.inf = false;
+}
+
+__device__ __forceinline__ void load_be32(fe& r, const unsigned char* b) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const unsigned char* q = b + 28 - 4 * i;
+        r.v[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+}
+
+__device__ __forceinline__ bool fe_lt_p(const fe& a) {
+    // a < p  <=>  a - p borrows
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t d = (uint64_t)a.v[i] - P_LIMBS[i] - borrow;
+        borrow = (d >> 63) & 1;
+    }
+    return borrow != 0;
+}
+
+constexpr int WG = 128;
+constexpr int WNAF_W = 4;              // odd multiples 1,3,5,7
+constexpr int NPRE = 1 << (WNAF_W - 2); // 4
+
+struct Job {
+    unsigned char u1[32];   // big-endian scalar for the G comb
+    unsigned char r[32];    // big-endian r
+    unsigned char rn[32];   // big-endian r + n (valid when rplusn_ok)
+    unsigned char pub[33];  // compressed key
+    unsigned char rplusn_ok;
+    unsigned char wnaf[130]; // u2 as width-4 wNAF, 2 signed nibbles per byte, digit b at wnaf[b>>1]
+    unsigned char nwnaf_lo, nwnaf_hi; // number of digits
+    unsigned char pad[10];
+};
+static_assert(sizeof(Job) == 272, "job layout");
+
+__device__ __forceinline__ int wnaf_digit(const Job& J, int b) {
+    const int byte = J.wnaf[b >> 1];
+    const int nib = (b & 1) ? (byte >> 4) : (byte & 15);
+    return nib >= 8 ? nib - 16 : nib;
+}
+
+__global__ __launch_bounds__(WG) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
+                                                          uint8_t* __restrict__ out, int n) {
+    // word-major layout: lane-consecutive words -> conflict-free LDS access
+    __shared__ uint32_t preX[NPRE][8][WG], preY[NPRE][8][WG], preZ[NPRE][8][WG];
+    const int tid = threadIdx.x;
+    const int idx = blockIdx.x * WG + tid;
+    if (idx >= n) return;
+    const Job& J = jobs[idx];
+
+    // ---- decompress Q
+    fe qx, qy;
+    load_be32(qx, J.pub + 1);
+    bool ok = (J.pub[0] == 2 || J.pub[0] == 3) && fe_lt_p(qx);
+    fe y2, seven;
+#pragma unroll
+    for (int i = 0; i < 8; i++) seven.v[i] = i == 0 ? 7u : 0u;
+    fe_sqr(y2, qx);
+    fe_mul(y2, y2, qx);
+    fe_add(y2, y2, seven);
+    ok = ok && fe_sqrt(qy, y2);
+    if ((qy.v[0] & 1) != (uint32_t)(J.pub[0] & 1)) {
+        fe zero;
+#pragma unroll
+        for (int i = 0; i < 8; i++) zero.v[i] = 0;
+        fe_sub(qy, zero, qy);
+    }
+
+    // ---- odd multiples Q, 3Q, 5Q, 7Q (Jacobian) into LDS
+    gej q1;
+    q1.x = qx;
+    q1.y = qy;
+#pragma unroll
+    for (int i = 0; i < 8; i++) q1.z.v[i] = i == 0 ? 1u : 0u;
+    q1.inf = false;
+    gej q2;
+    gej_double(q2, q1);
+    gej cur = q1;
+    for (int m = 0; m < NPRE; m++) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            preX[m][k][tid] = cur.x.v[k];
+            preY[m][k][tid] = cur.y.v[k];
+            preZ[m][k][tid] = cur.z.v[k];
+        }
+        gej nx;
+        gej_add(nx, cur, q2);
+        cur = nx;
+    }
+
+    // ---- u2*Q by wNAF
+    const int len = J.nwnaf_lo | (J.nwnaf_hi << 8);
+    gej acc;
+    acc.inf = true;
+    for (int b = len - 1; b >= 0; b--) {
+        gej d;
+        gej_double(d, acc);
+        acc = d;
+        const int dg = wnaf_digit(J, b);
+        if (dg) {
+            const int m = (dg > 0 ? dg : -dg) >> 1;
+            gej p;
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                p.x.v[k] = preX[m][k][tid];
+                p.y.v[k] = preY[m][k][tid];
+                p.z.v[k] = preZ[m][k][tid];
+            }
+            p.inf = false;
+            if (dg < 0) {
+                fe zero;
+#pragma unroll
+                for (int i = 0; i < 8; i++) zero.v[i] = 0;
+                fe_sub(p.y, zero, p.y);
+            }
+            gej s;
+            gej_add(s, acc, p);
+            acc = s;
+        }
+    }
+
+    // ---- + u1*G via byte-window comb table (affine, 16 words per entry)
+    for (int i = 0; i < 32; i++) {
+        const unsigned byte = J.u1[31 - i];
+        if (!byte) continue;
+        const uint32_t* e = gtab + ((size_t)i * 256 + byte) * 16;
+        fe gx, gy;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            gx.v[k] = e[k];
+            gy.v[k] = e[8 + k];
+        }
+        gej s;
+        gej_add_ge(s, acc, gx, gy);
+        acc = s;
+    }
+
+    // ---- x(R) == r (mod n) without inversion
+    bool match = false;
+    if (!acc.inf) {
+        fe z2, rz, r;
+        fe_sqr(z2, acc.z);
+        load_be32(r, J.r);
+        fe_mul(rz, r, z2);
+        match = fe_eq(rz, acc.x);
+        if (!match && J.rplusn_ok) {
+            load_be32(r, J.rn);
+            fe_mul(rz, r, z2);
+            match = fe_eq(rz, acc.x);
+        }
+    }
+    out[idx] = (ok && match) ? 1 : 0;
+}
+
+struct State {
+    std::once_flag once;
+    uint32_t* d_gtab = nullptr;
+    std::mutex m;
+    Job* d_jobs = nullptr;
+    uint8_t* d_out = nullptr;
+    size_t cap = 0;
+    hipStream_t stream = nullptr;
+};
+State& S() {
+    static State s;
+    return s;
+}
+
+// Width-4 wNAF of a big-endian 256-bit scalar into signed nibbles; returns digit count.
+int WnafEncode(unsigned char* out, const unsigned char* be) {
+    uint32_t k[9];
+    for (int i = 0; i < 8; i++) {
+        const unsigned char* q = be + 28 - 4 * i;
+        k[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+    }
+    k[8] = 0;
+    memset(out, 0, 130);
+    int len = 0;
+    for (int b = 0; b < 258; b++) {
+        bool nz = false;
+        for (int i = 0; i < 9; i++) nz |= k[i] != 0;
+        if (!nz) break;
+        int d = 0;
+        if (k[0] & 1) {
+            d = (int)(k[0] & 15);
+            if (d >= 8) d -= 16;
+            // k -= d
+            if (d > 0) {
+                uint64_t borrow = (uint64_t)d;
+                for (int i = 0; i < 9 && borrow; i++) {
+                    const uint64_t x = (uint64_t)k[i] - borrow;
+                    k[i] = (uint32_t)x;
+                    borrow = (x >> 63) & 1;
+                }
+            } else {
+                uint64_t carry = (uint64_t)(-d);
+                for (int i = 0; i < 9 && carry; i++) {
+                    carry += k[i];
+                    k[i] = (uint32_t)carry;
+                    carry >>= 32;
+                }
+            }
+        }
+        out[b >> 1] |= (unsigned char)((d & 15) << ((b & 1) * 4));
+        if (d) len = b + 1;
+        for (int i = 0; i < 8; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
+        k[8] >>= 1;
+    }
+    return len;
+}
+
+void InitTable() {
+    // 32 x 256 affine points, 8 LE limbs for x then y
+    const std::vector<secp::Ge>& t = secp::generator_table();
+    std::vector<uint32_t> h(32 * 256 * 16, 0);
+    for (size_t e = 0; e < t.size(); e++) {
+        unsigned char bx[32], by[32];
+        if (t[e].inf) continue;
+        secp::fe_get_b32(bx, t[e].x);
+        secp::fe_get_b32(by, t[e].y);
+        for (int k = 0; k < 8; k++) {
+            const unsigned char* q = bx + 28 - 4 * k;
+            h[e * 16 + k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+            q = by + 28 - 4 * k;
+            h[e * 16 + 8 + k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
+        }
+    }
+    BCP_HIP_CHECK(hipMalloc(&S().d_gtab, h.size() * 4));
+    BCP_HIP_CHECK(hipMemcpy(S().d_gtab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    BCP_HIP_CHECK(hipStreamCreateWithFlags(&S().stream, hipStreamNonBlocking));
+}
+
+} // namespace
+
+std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
+                                      const std::vector<unsigned char>& pub33, int device) {
+    const size_t n = msg32.size() / 32;
+    if (sig64.size() != n * 64 || pub33.size() != n * 33) throw std::invalid_argument("EcdsaVerifyBatch: sizes");
+    std::vector<uint8_t> result(n, 0);
+    if (n == 0) return result;
+    UseDevice(device);
+    State& st = S();
+    std::call_once(st.once, InitTable);
+
+    // host: batch inversion of s, u1 = z/s, u2 = r/s
+    std::vector<secp::Scalar> s(n), r(n), z(n), pref(n);
+    std::vector<uint8_t> hostOk(n, 1);
+    secp::Scalar accum;
+    secp::sc_set_b32(accum, (const unsigned char*)"\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\1");
+    for (size_t i = 0; i < n; i++) {
+        bool of1 = false, of2 = false;
+        secp::sc_set_b32(r[i], &sig64[i * 64], &of1);
+        secp::sc_set_b32(s[i], &sig64[i * 64 + 32], &of2);
+        secp::sc_set_b32(z[i], &msg32[i * 32]);
+        if (of1 || of2 || secp::sc_is_zero(r[i]) || secp::sc_is_zero(s[i])) {
+            hostOk[i] = 0;
+            secp::sc_set_b32(s[i], (const unsigned char*)"\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\1");
+        }
+        pref[i] = accum;
+        secp::sc_mul(accum, accum, s[i]);
+    }
+    secp::Scalar inv;
+    secp::sc_inv(inv, accum);
+    std::vector<Job> jobs(n);
+    for (size_t i = n; i-- > 0;) {
+        secp::Scalar sinv;
+        secp::sc_mul(sinv, inv, pref[i]); // 1/s_i
+        secp::sc_mul(inv, inv, s[i]);     // drop s_i from the running inverse
+        secp::Scalar u1, u2;
+        secp::sc_mul(u1, z[i], sinv);
+        secp::sc_mul(u2, r[i], sinv);
+        Job& J = jobs[i];
+        memset(&J, 0, sizeof(J));
+        secp::sc_get_b32(J.u1, u1);
+        unsigned char u2b[32];
+        secp::sc_get_b32(u2b, u2);
+        const int len = WnafEncode(J.wnaf, u2b);
+        J.nwnaf_lo = (unsigned char)(len & 0xff);
+        J.nwnaf_hi = (unsigned char)(len >> 8);
+        memcpy(J.r, &sig64[i * 64], 32);
+        memcpy(J.pub, &pub33[i * 33], 33);
+        // r + n < p  <=>  r < p - n  (p - n = 0x14551231950b75fc4402da1722fc9baee)
+        static const unsigned char PMN[32] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,
+                                              0x45, 0x51, 0x23, 0x19, 0x50, 0xb7, 0x5f, 0xc4,
+                                              0x40, 0x2d, 0xa1, 0x72, 0x2f, 0xc9, 0xba, 0xee};
+        if (memcmp(J.r, PMN, 32) < 0) {
+            J.rplusn_ok = 1;
+            static const unsigned char N[32] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
+                                                0xFF, 0xFF, 0xFF, 0xFF, 0xFE, 0xBA, 0xAE, 0xDC, 0xE6, 0xAF, 0x48,
+                                                0xA0, 0x3B, 0xBF, 0xD2, 0x5E, 0x8C, 0xD0, 0x36, 0x41, 0x41};
+            unsigned c = 0;
+            for (int b = 31; b >= 0; b--) {
+                c += (unsigned)J.r[b] + N[b];
+                J.rn[b] = (unsigned char)c;
+                c >>= 8;
+            }
+        }
+    }
+
+    std::lock_guard<std::mutex> l(st.m);
+    if (st.cap < n) {
+        if (st.d_jobs) BCP_HIP_CHECK(hipFree(st.d_jobs));
+        if (st.d_out) BCP_HIP_CHECK(hipFree(st.d_out));
+        st.cap = std::max<size_t>(n, 4096);
+        BCP_HIP_CHECK(hipMalloc(&st.d_jobs, st.cap * sizeof(Job)));
+        BCP_HIP_CHECK(hipMalloc(&st.d_out, st.cap));
+    }
+    BCP_HIP_CHECK(hipMemcpyAsync(st.d_jobs, jobs.data(), n * sizeof(Job), hipMemcpyHostToDevice, st.stream));
+    const int grid = (int)((n + WG - 1) / WG);
+    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, st.stream, st.d_jobs, st.d_gtab, st.d_out, (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+    BCP_HIP_CHECK(hipMemcpyAsync(result.data(), st.d_out, n, hipMemcpyDeviceToHost, st.stream));
+    BCP_HIP_CHECK(hipStreamSynchronize(st.stream));
+    for (size_t i = 0; i < n; i++) result[i] &= hostOk[i];
+    return result;
+}
+
+} // namespace gpu
+} // namespace bcp

@@ -1,0 +1,442 @@
+#include "node/miner.h"
+#include "consensus/equihash.h"
+#include "crypto/common.h"
+#include "consensus/merkle.h"
+#include "consensus/pow.h"
+#include "kernels/gpu_api.h"
+#include "keys/key.h"
+#include "node/policy.h"
+#include "node/txmempool.h"
+#include "util/strencodings.h"
+
+#include <algorithm>
+#include <cassert>
+#include <mutex>
+
+namespace bcp {
+
+uint64_t BlockAssembler::nLastBlockTx = 0;
+uint64_t BlockAssembler::nLastBlockSize = 0;
+
+static const unsigned MAX_COINBASE_SCRIPTSIG_SIZE = 100;
+
+BlockAssembler::Options::Options()
+    : nMaxGeneratedBlockSize((uint64_t)gArgs.GetArg("-blockmaxsize", (int64_t)DEFAULT_MAX_GENERATED_BLOCK_SIZE)),
+      blockMinFeeRate(gArgs.IsArgSet("-blockmintxfee")
+                          ? [] {
+                                int64_t n = 0;
+                                ParseMoney(gArgs.GetArg("-blockmintxfee", ""), n);
+                                return CFeeRate(n);
+                            }()
+                          : CFeeRate(DEFAULT_BLOCK_MIN_TX_FEE)),
+      nBlockPriorityPercentage(gArgs.GetArg("-blockprioritypercentage", (int64_t)DEFAULT_BLOCK_PRIORITY_PERCENTAGE)) {}
+
+uint64_t ComputeMaxGeneratedBlockSize(uint64_t excessiveBlockSize) {
+    // leave room for the coinbase; never exceed the excessive block size
+    uint64_t n = (uint64_t)gArgs.GetArg("-blockmaxsize", (int64_t)DEFAULT_MAX_GENERATED_BLOCK_SIZE);
+    n = std::max<uint64_t>(1000, std::min<uint64_t>(excessiveBlockSize - 1000, n));
+    return n;
+}
+
+std::string GetSubVersionEB(uint64_t maxBlockSize) {
+    // one decimal place of MB, e.g. 8000000 -> "8.0"
+    const uint64_t tenths = maxBlockSize / 100000;
+    return strprintf("%llu.%llu", (unsigned long long)(tenths / 10), (unsigned long long)(tenths % 10));
+}
+
+int64_t UpdateTime(CBlockHeader* pblock, const Consensus::Params& params, const CBlockIndex* pindexPrev) {
+    const int64_t nOldTime = pblock->nTime;
+    const int64_t nNewTime = std::max(pindexPrev->GetMedianTimePast() + 1, GetAdjustedTime());
+    if (nOldTime < nNewTime) pblock->nTime = (uint32_t)nNewTime;
+    // testnet: a late block may use minimum difficulty, which depends on the time
+    if (params.fPowAllowMinDifficultyBlocks) pblock->nBits = GetNextWorkRequired(pindexPrev, pblock, params);
+    return nNewTime - nOldTime;
+}
+
+BlockAssembler::BlockAssembler(Chainstate& cs, CTxMemPool* mp, const Options& o) : chainstate(cs), mempool(mp), options(o) {
+    nMaxGeneratedBlockSize = std::max<uint64_t>(1000, std::min<uint64_t>(chainstate.MaxBlockSize() - 1000,
+                                                                          options.nMaxGeneratedBlockSize));
+}
+
+void BlockAssembler::resetBlock() {
+    inBlock.clear();
+    nBlockSize = 1000; // reserve space for the coinbase
+    nBlockSigOps = 100;
+    nBlockTx = 0;
+    nFees = 0;
+}
+
+bool BlockAssembler::TestTxForBlock(const CTransaction& tx, uint64_t size, int64_t sigops) const {
+    if (nBlockSize + size >= nMaxGeneratedBlockSize) return false;
+    if (nBlockSigOps + sigops >= GetMaxBlockSigOpsCount(nBlockSize + size)) return false;
+    CValidationState state;
+    if (!chainstate.ContextualCheckTransaction(tx, state, nHeight, nLockTimeCutoff)) return false;
+    return true;
+}
+
+void BlockAssembler::AddToBlock(const CTransactionRef& tx, Amount fee, int64_t sigops) {
+    pblock->vtx.push_back(tx);
+    pblocktemplate->vTxFees.push_back(fee);
+    pblocktemplate->vTxSigOpsCount.push_back(sigops);
+    nBlockSize += tx->GetTotalSize();
+    ++nBlockTx;
+    nBlockSigOps += sigops;
+    nFees += fee;
+    inBlock.insert(tx->GetHash());
+}
+
+void BlockAssembler::addPriorityTxs() {
+    // a fraction of the block is reserved for high-priority (coin age) transactions
+    if (options.nBlockPriorityPercentage == 0) return;
+    const uint64_t nBlockPrioritySize = nMaxGeneratedBlockSize * options.nBlockPriorityPercentage / 100;
+    std::vector<std::pair<double, const CTxMemPoolEntry*>> vecPriority;
+    for (const CTxMemPoolEntry* e : mempool->SortedByDepthAndScore()) {
+        double dPriority = e->GetPriority(nHeight);
+        Amount dummy = 0;
+        mempool->ApplyDeltas(e->GetTx().GetHash(), dPriority, dummy);
+        vecPriority.push_back(std::make_pair(dPriority, e));
+    }
+    std::stable_sort(vecPriority.begin(), vecPriority.end(),
+                     [](const std::pair<double, const CTxMemPoolEntry*>& a, const std::pair<double, const CTxMemPoolEntry*>& b) {
+                         return a.first > b.first;
+                     });
+    bool progress = true;
+    while (progress && nBlockSize < nBlockPrioritySize) {
+        progress = false;
+        for (const auto& p : vecPriority) {
+            const CTxMemPoolEntry* e = p.second;
+            const uint256& h = e->GetTx().GetHash();
+            if (inBlock.count(h)) continue;
+            if (!AllowFree(p.first)) return; // priority area closed below the free threshold
+            bool dependent = false;
+            for (const CTxIn& in : e->GetTx().vin)
+                if (mempool->exists(in.prevout.hash) && !inBlock.count(in.prevout.hash)) dependent = true;
+            if (dependent) continue;
+            if (!TestTxForBlock(e->GetTx(), e->GetTxSize(), e->GetSigOpCount())) continue;
+            AddToBlock(e->GetSharedTx(), e->GetFee(), e->GetSigOpCount());
+            progress = true;
+            if (nBlockSize >= nBlockPrioritySize) return;
+        }
+    }
+}
+
+// Ancestor-feerate package selection: highest ancestor score first; each package is
+// the candidate plus its not-yet-included ancestors, added in topological order.
+void BlockAssembler::addPackageTxs() {
+    std::vector<CTxMemPool::txiter> order = mempool->SortedByAncestorScore();
+    int nConsecutiveFailed = 0;
+    for (CTxMemPool::txiter it : order) {
+        const CTxMemPoolEntry& e = *it->second;
+        if (inBlock.count(it->first)) continue;
+        std::vector<const CTxMemPoolEntry*> pkg = mempool->GetAncestors(it->first);
+        pkg.erase(std::remove_if(pkg.begin(), pkg.end(),
+                                 [&](const CTxMemPoolEntry* a) { return inBlock.count(a->GetTx().GetHash()) > 0; }),
+                  pkg.end());
+        pkg.push_back(&e);
+        uint64_t pkgSize = 0;
+        int64_t pkgSigOps = 0;
+        Amount pkgFees = 0;
+        for (const CTxMemPoolEntry* p : pkg) {
+            pkgSize += p->GetTxSize();
+            pkgSigOps += p->GetSigOpCount();
+            pkgFees += p->GetModifiedFee();
+        }
+        if (pkgFees < options.blockMinFeeRate.GetFee(pkgSize)) break; // sorted: nothing better follows
+        bool fits = nBlockSize + pkgSize < nMaxGeneratedBlockSize &&
+                    nBlockSigOps + pkgSigOps < GetMaxBlockSigOpsCount(nBlockSize + pkgSize);
+        if (fits) {
+            for (const CTxMemPoolEntry* p : pkg)
+                if (!TestTxForBlock(p->GetTx(), 0, 0)) fits = false;
+        }
+        if (!fits) {
+            ++nConsecutiveFailed;
+            if (nConsecutiveFailed > 1000 && nBlockSize > nMaxGeneratedBlockSize - 1000) break;
+            continue;
+        }
+        std::sort(pkg.begin(), pkg.end(), [](const CTxMemPoolEntry* a, const CTxMemPoolEntry* b) {
+            if (a->GetCountWithAncestors() != b->GetCountWithAncestors())
+                return a->GetCountWithAncestors() < b->GetCountWithAncestors();
+            return a->GetTx().GetHash() < b->GetTx().GetHash();
+        });
+        for (const CTxMemPoolEntry* p : pkg) AddToBlock(p->GetSharedTx(), p->GetFee(), p->GetSigOpCount());
+        nConsecutiveFailed = 0;
+    }
+}
+
+std::unique_ptr<CBlockTemplate> BlockAssembler::CreateNewBlock(const CScript& scriptPubKeyIn) {
+    const int64_t nTimeStart = GetTimeMicros();
+    resetBlock();
+    pblocktemplate.reset(new CBlockTemplate());
+    pblock = &pblocktemplate->block;
+    pblock->vtx.emplace_back();
+    pblocktemplate->vTxFees.push_back(-1);
+    pblocktemplate->vTxSigOpsCount.push_back(-1);
+    std::lock_guard<std::recursive_mutex> l(chainstate.cs());
+    std::unique_ptr<std::lock_guard<std::recursive_mutex>> lmp;
+    if (mempool) lmp.reset(new std::lock_guard<std::recursive_mutex>(mempool->cs));
+    const CChainParams& chainparams = chainstate.Params();
+    const Consensus::Params& cp = chainparams.GetConsensus();
+    CBlockIndex* pindexPrev = chainstate.Tip();
+    nHeight = pindexPrev->nHeight + 1;
+    pblock->nVersion = chainstate.ComputeBlockVersion(pindexPrev);
+    if (chainparams.MineBlocksOnDemand()) pblock->nVersion = (int32_t)gArgs.GetArg("-blockversion", (int64_t)pblock->nVersion);
+    pblock->nTime = (uint32_t)GetAdjustedTime();
+    nLockTimeCutoff = (STANDARD_LOCKTIME_VERIFY_FLAGS & LOCKTIME_MEDIAN_TIME_PAST) ? pindexPrev->GetMedianTimePast()
+                                                                                   : pblock->GetBlockTime();
+    if (mempool) {
+        addPriorityTxs();
+        addPackageTxs();
+    }
+    nLastBlockTx = nBlockTx;
+    nLastBlockSize = nBlockSize;
+
+    CMutableTransaction coinbaseTx;
+    coinbaseTx.vin.resize(1);
+    coinbaseTx.vin[0].prevout.SetNull();
+    coinbaseTx.vout.resize(1);
+    coinbaseTx.vout[0].scriptPubKey = scriptPubKeyIn;
+    coinbaseTx.vout[0].nValue = nFees + GetBlockSubsidy(nHeight, cp);
+    coinbaseTx.vin[0].scriptSig = CScript() << nHeight << OP_0;
+    pblock->vtx[0] = MakeTransactionRef(std::move(coinbaseTx));
+    pblocktemplate->vTxFees[0] = -1 * nFees;
+
+    arith_uint256 nonce;
+    if (nHeight >= cp.BCPHeight) {
+        // random 256-bit nonce; top and bottom 16 bits cleared for local counters/flags
+        nonce = UintToArith256(GetRandHash());
+        nonce <<= 32;
+        nonce >>= 16;
+    }
+    pblock->hashPrevBlock = pindexPrev->GetBlockHash();
+    pblock->nHeight = (uint32_t)nHeight;
+    memset(pblock->nReserved, 0, sizeof(pblock->nReserved));
+    UpdateTime(pblock, cp, pindexPrev);
+    pblock->nBits = GetNextWorkRequired(pindexPrev, pblock, cp);
+    pblock->nNonce = ArithToUint256(nonce);
+    pblock->nSolution.clear();
+    pblocktemplate->vTxSigOpsCount[0] = (int64_t)GetSigOpCountWithoutP2SH(*pblock->vtx[0]);
+    pblock->hashMerkleRoot = BlockMerkleRoot(*pblock);
+
+    CValidationState state;
+    if (!chainstate.TestBlockValidity(state, *pblock, pindexPrev, false, false))
+        throw std::runtime_error(strprintf("CreateNewBlock: TestBlockValidity failed: %s", FormatStateMessage(state).c_str()));
+    LogPrint(BCLog::BENCH, "CreateNewBlock(): %u txs, fees %lld, %.2fms\n", (unsigned)nBlockTx, (long long)nFees,
+             0.001 * (GetTimeMicros() - nTimeStart));
+    return std::move(pblocktemplate);
+}
+
+void IncrementExtraNonce(CBlock* pblock, const CBlockIndex* pindexPrev, unsigned& nExtraNonce, uint64_t maxBlockSize) {
+    static uint256 hashPrevBlock;
+    static std::mutex m;
+    {
+        std::lock_guard<std::mutex> l(m);
+        if (hashPrevBlock != pblock->hashPrevBlock) {
+            nExtraNonce = 0;
+            hashPrevBlock = pblock->hashPrevBlock;
+        }
+    }
+    ++nExtraNonce;
+    const int nHeight = pindexPrev->nHeight + 1;
+    CMutableTransaction txCoinbase(*pblock->vtx[0]);
+    const std::string eb = "/EB" + GetSubVersionEB(maxBlockSize) + "/";
+    txCoinbase.vin[0].scriptSig = CScript() << nHeight << CScriptNum((int64_t)nExtraNonce)
+                                            << std::vector<unsigned char>(eb.begin(), eb.end());
+    if (txCoinbase.vin[0].scriptSig.size() > MAX_COINBASE_SCRIPTSIG_SIZE) throw std::logic_error("coinbase scriptSig too large");
+    pblock->vtx[0] = MakeTransactionRef(std::move(txCoinbase));
+    pblock->hashMerkleRoot = BlockMerkleRoot(*pblock);
+}
+
+// ------------------------------------------------------------------ PoW search
+static std::mutex g_minerMutex;
+static MinerStats g_minerStats;
+MinerStats GetMinerStats() {
+    std::lock_guard<std::mutex> l(g_minerMutex);
+    return g_minerStats;
+}
+
+namespace {
+struct GpuSolverCache {
+    std::mutex m;
+    std::unique_ptr<gpu::EquihashGpuSolver> solver;
+    unsigned n = 0, k = 0;
+};
+GpuSolverCache& SolverCache() {
+    static GpuSolverCache c;
+    return c;
+}
+} // namespace
+
+static bool SolveLegacy(CBlock& block, const Consensus::Params& cp, uint64_t& nMaxTries, bool useGpu,
+                        const std::atomic<bool>* cancel) {
+    // nonce lives in the low 32 bits of nNonce in the 80-byte legacy header
+    uint32_t n32 = ReadLE32(block.nNonce.begin());
+    // cheap CPU attempts first: regtest/min-difficulty targets pass almost immediately
+    for (int i = 0; i < 4096 && nMaxTries > 0; i++) {
+        if (CheckProofOfWork(block.GetHash(cp), block.nBits, false, cp)) return true;
+        if (cancel && cancel->load()) return false;
+        ++n32;
+        WriteLE32(block.nNonce.begin(), n32);
+        --nMaxTries;
+        std::lock_guard<std::mutex> l(g_minerMutex);
+        g_minerStats.sha_nonces++;
+    }
+    if (!useGpu || !gpu::GpuAvailable()) {
+        while (nMaxTries > 0) {
+            if (CheckProofOfWork(block.GetHash(cp), block.nBits, false, cp)) return true;
+            if (cancel && cancel->load()) return false;
+            ++n32;
+            WriteLE32(block.nNonce.begin(), n32);
+            --nMaxTries;
+        }
+        return false;
+    }
+    arith_uint256 target;
+    target.SetCompact(block.nBits);
+    const uint256 t = ArithToUint256(target);
+    while (nMaxTries > 0) {
+        std::vector<unsigned char> hdr = SerializeToBytes(static_cast<const CBlockHeader&>(block), SER_NETWORK,
+                                                          PROTOCOL_VERSION | SERIALIZE_BLOCK_LEGACY);
+        const uint64_t count = std::min<uint64_t>(nMaxTries, 1ull << 30);
+        const int64_t t0 = GetTimeMicros();
+        const int64_t found = gpu::Sha256dScanNonces(hdr.data(), t.begin(), n32, count);
+        {
+            std::lock_guard<std::mutex> l(g_minerMutex);
+            g_minerStats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
+            g_minerStats.sha_nonces += count;
+        }
+        if (found >= 0) {
+            WriteLE32(block.nNonce.begin(), (uint32_t)found);
+            nMaxTries -= std::min<uint64_t>(nMaxTries, (uint32_t)found - n32 + 1);
+            return CheckProofOfWork(block.GetHash(cp), block.nBits, false, cp);
+        }
+        nMaxTries -= count;
+        n32 += (uint32_t)count;
+        if (cancel && cancel->load()) return false;
+        if (n32 == 0) {
+            // nonce space exhausted: bump the time and restart
+            block.nTime++;
+        }
+    }
+    return false;
+}
+
+static bool SolveEquihash(CBlock& block, const CChainParams& params, uint64_t& nMaxTries, bool useGpu,
+                          const std::atomic<bool>* cancel) {
+    const Consensus::Params& cp = params.GetConsensus();
+    const EquihashParams ep(params.EquihashN(), params.EquihashK());
+    CBlake2b base = EhInitialiseState(ep);
+    const std::vector<unsigned char> input = block.EquihashInput();
+    base.Write(input.data(), input.size());
+    auto tryState = [&](const std::vector<unsigned char>& soln) {
+        block.nSolution = soln;
+        return CheckProofOfWork(block.GetHash(cp), block.nBits, true, cp);
+    };
+    const bool gpuOk = useGpu && ep.N >= 96 && gpu::GpuAvailable();
+    if (gpuOk) {
+        GpuSolverCache& sc = SolverCache();
+        std::lock_guard<std::mutex> l(sc.m);
+        if (!sc.solver || sc.n != ep.N || sc.k != ep.K) {
+            sc.solver.reset(new gpu::EquihashGpuSolver(ep.N, ep.K, ep.N == 200 ? 8 : 16));
+            sc.n = ep.N;
+            sc.k = ep.K;
+        }
+        const int batch = sc.solver->Batch();
+        while (nMaxTries > 0) {
+            const int nb = (int)std::min<uint64_t>(nMaxTries, (uint64_t)batch);
+            std::vector<gpu::EhBaseState> states;
+            std::vector<uint256> nonces;
+            arith_uint256 nn = UintToArith256(block.nNonce);
+            for (int b = 0; b < nb; b++) {
+                nn += 1;
+                const uint256 nonce = ArithToUint256(nn);
+                CBlake2b st = base;
+                st.Write(nonce.begin(), 32);
+                states.push_back(gpu::MakeEhBaseState(st));
+                nonces.push_back(nonce);
+            }
+            const int64_t t0 = GetTimeMicros();
+            auto sols = sc.solver->Solve(states);
+            {
+                std::lock_guard<std::mutex> ls(g_minerMutex);
+                g_minerStats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
+                g_minerStats.eh_nonces += nb;
+            }
+            nMaxTries -= nb;
+            for (int b = 0; b < nb; b++) {
+                for (const auto& idx : sols[b]) {
+                    block.nNonce = nonces[b];
+                    std::vector<unsigned char> minimal = GetMinimalFromIndices(idx, ep.N / (ep.K + 1));
+                    {
+                        std::lock_guard<std::mutex> ls(g_minerMutex);
+                        g_minerStats.eh_solutions++;
+                    }
+                    if (tryState(minimal)) return true;
+                }
+            }
+            block.nNonce = nonces.back();
+            if (cancel && cancel->load()) return false;
+        }
+        return false;
+    }
+    while (nMaxTries > 0) {
+        block.nNonce = ArithToUint256(UintToArith256(block.nNonce) + 1);
+        CBlake2b st = base;
+        st.Write(block.nNonce.begin(), 32);
+        --nMaxTries;
+        {
+            std::lock_guard<std::mutex> ls(g_minerMutex);
+            g_minerStats.eh_nonces++;
+        }
+        if (EhBasicSolve(ep, st, tryState, [&] { return cancel && cancel->load(); })) return true;
+        if (cancel && cancel->load()) return false;
+    }
+    return false;
+}
+
+bool SolveBlock(CBlock& block, const CChainParams& params, uint64_t& nMaxTries, bool useGpu,
+                const std::atomic<bool>* cancel) {
+    const bool ok = (int)block.nHeight < params.GetConsensus().BCPHeight
+                        ? SolveLegacy(block, params.GetConsensus(), nMaxTries, useGpu, cancel)
+                        : SolveEquihash(block, params, nMaxTries, useGpu, cancel);
+    if (ok) {
+        std::lock_guard<std::mutex> l(g_minerMutex);
+        g_minerStats.blocks++;
+    }
+    return ok;
+}
+
+std::vector<uint256> GenerateBlocks(Chainstate& chainstate, CTxMemPool* mempool, const CScript& coinbaseScript,
+                                    int nGenerate, uint64_t nMaxTries, bool useGpu, std::string* err) {
+    std::vector<uint256> hashes;
+    int nHeight, nHeightEnd;
+    {
+        std::lock_guard<std::recursive_mutex> l(chainstate.cs());
+        nHeight = chainstate.Height();
+        nHeightEnd = nHeight + nGenerate;
+    }
+    unsigned nExtraNonce = 0;
+    const CChainParams& params = chainstate.Params();
+    while (nHeight < nHeightEnd) {
+        std::unique_ptr<CBlockTemplate> tmpl = BlockAssembler(chainstate, mempool).CreateNewBlock(coinbaseScript);
+        CBlock* pblock = &tmpl->block;
+        {
+            std::lock_guard<std::recursive_mutex> l(chainstate.cs());
+            IncrementExtraNonce(pblock, chainstate.Tip(), nExtraNonce, chainstate.MaxBlockSize());
+        }
+        if (!SolveBlock(*pblock, params, nMaxTries, useGpu)) {
+            if (nMaxTries == 0) break;
+            continue;
+        }
+        auto shared = std::make_shared<const CBlock>(*pblock);
+        CValidationState state;
+        if (!chainstate.ProcessNewBlock(shared, true, nullptr, &state)) {
+            if (err) *err = "ProcessNewBlock, block not accepted: " + FormatStateMessage(state);
+            return hashes;
+        }
+        ++nHeight;
+        hashes.push_back(pblock->GetHash(params.GetConsensus()));
+    }
+    return hashes;
+}
+
+} // namespace bcp

@@ -1,0 +1,158 @@
+#include "node/sigverify.h"
+#include "kernels/gpu_api.h"
+#include "keys/key.h"
+#include "secp256k1/secp256k1.h"
+
+#include <atomic>
+#include <cstring>
+
+namespace bcp {
+
+SignatureCache::SignatureCache(size_t n) : maxEntries(n) { GetRandBytes(nonce.begin(), 32); }
+
+uint256 SignatureCache::Entry(const uint256& sighash, const std::vector<unsigned char>& sig,
+                              const std::vector<unsigned char>& pubkey) const {
+    CSHA256 h;
+    h.Write(nonce.begin(), 32).Write(sighash.begin(), 32).Write(pubkey.data(), pubkey.size()).Write(sig.data(), sig.size());
+    uint256 r;
+    h.Finalize(r.begin());
+    return r;
+}
+bool SignatureCache::Get(const uint256& e, bool erase) {
+    std::lock_guard<std::mutex> l(cs);
+    auto it = set.find(e);
+    if (it == set.end()) return false;
+    if (erase) set.erase(it);
+    return true;
+}
+void SignatureCache::Set(const uint256& e) {
+    std::lock_guard<std::mutex> l(cs);
+    if (set.size() >= maxEntries) set.erase(set.begin()); // random-ish eviction (hash order)
+    set.insert(e);
+}
+size_t SignatureCache::Size() const {
+    std::lock_guard<std::mutex> l(cs);
+    return set.size();
+}
+SignatureCache& GetSignatureCache() {
+    static SignatureCache c;
+    return c;
+}
+
+static std::atomic<size_t> g_gpuThreshold{256};
+void SetGpuSigThreshold(size_t n) { g_gpuThreshold = n; }
+size_t GetGpuSigThreshold() { return g_gpuThreshold.load(); }
+
+static std::mutex g_statsMutex;
+static SigVerifyStats g_stats;
+SigVerifyStats GetSigVerifyStats() {
+    std::lock_guard<std::mutex> l(g_statsMutex);
+    return g_stats;
+}
+
+bool CachingTransactionSignatureChecker::VerifySignature(const std::vector<unsigned char>& sig,
+                                                         const std::vector<unsigned char>& pubkey,
+                                                         const uint256& sighash) const {
+    SignatureCache& cache = GetSignatureCache();
+    const uint256 e = cache.Entry(sighash, sig, pubkey);
+    if (cache.Get(e, !store)) return true;
+    if (!TransactionSignatureChecker::VerifySignature(sig, pubkey, sighash)) return false;
+    if (store) cache.Set(e);
+    return true;
+}
+
+std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool) {
+    // host: DER parse + low-S normalisation + key form; device: decompression + ecmult
+    const size_t n = checks.size();
+    std::vector<unsigned char> msg(n * 32), sig(n * 64), pub(n * 33);
+    std::vector<uint8_t> hostOk(n, 1);
+    auto prep = [&](size_t j) {
+        const DeferredSigCheck& c = *checks[j];
+        secp::Signature s;
+        if (!secp::sig_parse_der_lax(s, c.sig.data(), c.sig.size())) {
+            hostOk[j] = 0;
+            return;
+        }
+        secp::sig_normalize(s);
+        secp::sig_serialize_compact(&sig[j * 64], s);
+        if (secp::sc_is_zero(s.r) || secp::sc_is_zero(s.s)) hostOk[j] = 0;
+        memcpy(&msg[j * 32], c.sighash.begin(), 32);
+        const std::vector<unsigned char>& pk = c.pubkey;
+        if (pk.size() == 33 && (pk[0] == 2 || pk[0] == 3)) {
+            memcpy(&pub[j * 33], pk.data(), 33);
+        } else {
+            secp::Ge q;
+            if (!secp::pubkey_parse(q, pk.data(), pk.size())) {
+                hostOk[j] = 0;
+                pub[j * 33] = 2;
+                return;
+            }
+            std::vector<unsigned char> comp = secp::pubkey_serialize(q, true);
+            memcpy(&pub[j * 33], comp.data(), 33);
+        }
+    };
+    if (pool) pool->ParallelFor(n, prep, 64);
+    else
+        for (size_t j = 0; j < n; j++) prep(j);
+    for (size_t j = 0; j < n; j++)
+        if (!hostOk[j]) pub[j * 33] = 2; // keep device input well-formed; result masked below
+    std::vector<uint8_t> res = gpu::EcdsaVerifyBatch(msg, sig, pub);
+    for (size_t j = 0; j < n; j++) res[j] &= hostOk[j];
+    return res;
+}
+
+bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* pool, bool useGpu, bool cacheStore,
+                           bool cacheErase) {
+    if (checks.empty()) return true;
+    SignatureCache& cache = GetSignatureCache();
+    std::vector<uint256> entries(checks.size());
+    std::vector<size_t> todo;
+    todo.reserve(checks.size());
+    uint64_t hits = 0;
+    for (size_t i = 0; i < checks.size(); i++) {
+        entries[i] = cache.Entry(checks[i].sighash, checks[i].sig, checks[i].pubkey);
+        if (cache.Get(entries[i], cacheErase)) hits++;
+        else todo.push_back(i);
+    }
+    bool ok = true;
+    const size_t n = todo.size();
+    if (n > 0) {
+        const bool gpu = useGpu && n >= g_gpuThreshold.load() && gpu::GpuAvailable();
+        const int64_t t0 = GetTimeMicros();
+        if (gpu) {
+            std::vector<const DeferredSigCheck*> ptrs(n);
+            for (size_t j = 0; j < n; j++) ptrs[j] = &checks[todo[j]];
+            std::vector<uint8_t> res = GpuVerifyDeferred(ptrs, pool);
+            for (size_t j = 0; j < n; j++) {
+                if (!res[j]) ok = false;
+                else if (cacheStore) cache.Set(entries[todo[j]]);
+            }
+            std::lock_guard<std::mutex> l(g_statsMutex);
+            g_stats.gpu_batches++;
+            g_stats.gpu_sigs += n;
+            g_stats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
+        } else {
+            std::atomic<bool> allOk{true};
+            auto work = [&](size_t j) {
+                if (!allOk.load(std::memory_order_relaxed)) return;
+                const DeferredSigCheck& c = checks[todo[j]];
+                if (!secp::VerifySignature(c.pubkey.data(), c.pubkey.size(), c.sig.data(), c.sig.size(),
+                                           c.sighash.begin()))
+                    allOk = false;
+                else if (cacheStore)
+                    cache.Set(entries[todo[j]]);
+            };
+            if (pool) pool->ParallelFor(n, work, 8);
+            else for (size_t j = 0; j < n; j++) work(j);
+            ok = allOk.load();
+            std::lock_guard<std::mutex> l(g_statsMutex);
+            g_stats.cpu_sigs += n;
+            g_stats.cpu_ms += (GetTimeMicros() - t0) / 1000.0;
+        }
+    }
+    std::lock_guard<std::mutex> l(g_statsMutex);
+    g_stats.cache_hits += hits;
+    return ok;
+}
+
+} // namespace bcp

@@ -1,0 +1,66 @@
+// Signature cache and batched ECDSA verification (CPU pool or MI355X).
+// Parity: reference src/script/sigcache.{h,cpp} (salted cache of valid (sighash,
+// pubkey, sig) triples, -maxsigcachesize, erase-on-block-use) and src/checkqueue.h
+// (CCheckQueue fan-out of CScriptCheck across -par threads). Here script evaluation
+// runs on the CPU pool and the deferred ECDSA checks (interpreter.h) are verified in
+// one batch: on the GPU when available and the batch is large enough, else on the pool.
+#pragma once
+#include "script/interpreter.h"
+#include "util/util.h"
+
+#include <unordered_set>
+
+namespace bcp {
+
+class SignatureCache {
+public:
+    explicit SignatureCache(size_t maxEntries = 1 << 20);
+    bool Get(const uint256& entry, bool erase);
+    void Set(const uint256& entry);
+    uint256 Entry(const uint256& sighash, const std::vector<unsigned char>& sig,
+                  const std::vector<unsigned char>& pubkey) const;
+    void SetMaxEntries(size_t n) { maxEntries = n; }
+    size_t Size() const;
+
+private:
+    struct H {
+        size_t operator()(const uint256& u) const { return (size_t)u.GetUint64(0); }
+    };
+    uint256 nonce;
+    size_t maxEntries;
+    mutable std::mutex cs;
+    std::unordered_set<uint256, H> set;
+};
+SignatureCache& GetSignatureCache();
+
+struct SigVerifyStats {
+    uint64_t gpu_batches = 0, gpu_sigs = 0, cpu_sigs = 0, cache_hits = 0;
+    double gpu_ms = 0, cpu_ms = 0;
+};
+
+// Verify all checks; returns true iff every one is valid. cacheStore: remember
+// successes (mempool acceptance); block validation erases consumed entries.
+bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* pool, bool useGpu, bool cacheStore,
+                           bool cacheErase);
+// Device verification of the given checks (no cache); result[i] = 1 iff valid.
+std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool);
+void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path (default 256)
+size_t GetGpuSigThreshold();
+SigVerifyStats GetSigVerifyStats();
+
+// TransactionSignatureChecker that consults/updates the signature cache.
+class CachingTransactionSignatureChecker : public TransactionSignatureChecker {
+public:
+    CachingTransactionSignatureChecker(const CTransaction* tx, unsigned nIn, Amount amount, bool store,
+                                       const PrecomputedTransactionData* txdata)
+        : TransactionSignatureChecker(tx, nIn, amount, txdata), store(store) {}
+
+protected:
+    bool VerifySignature(const std::vector<unsigned char>& sig, const std::vector<unsigned char>& pubkey,
+                         const uint256& sighash) const override;
+
+private:
+    bool store;
+};
+
+} // namespace bcp

@@ -1,0 +1,1386 @@
+// Chainstate engine: block/header acceptance, connect/disconnect, activation.
+// See validation.h for the parity map.
+#include "node/validation.h"
+#include "consensus/merkle.h"
+#include "consensus/pow.h"
+#include "node/policy.h"
+#include "node/signals.h"
+#include "node/sigverify.h"
+#include "node/txmempool.h"
+#include "script/interpreter.h"
+#include "util/strencodings.h"
+
+#include <algorithm>
+#include <deque>
+#include <unistd.h>
+#include <cassert>
+#include <cmath>
+
+namespace bcp {
+
+static Chainstate* g_chainstate = nullptr;
+Chainstate* GetChainstate() { return g_chainstate; }
+void SetChainstate(Chainstate* cs) { g_chainstate = cs; }
+
+std::string FormatStateMessage(const CValidationState& state) {
+    return strprintf("%s%s (code %i)", state.GetRejectReason().c_str(),
+                     state.GetDebugMessage().empty() ? "" : (", " + state.GetDebugMessage()).c_str(),
+                     state.GetRejectCode());
+}
+
+// ------------------------------------------------------------------ block-level caches
+// Script execution cache: (txid, flags) validated with all inputs (reference
+// src/script/scriptcache.cpp). Filled by mempool acceptance, consumed by ConnectBlock.
+namespace {
+struct ScriptCache {
+    std::mutex m;
+    std::unordered_set<uint256, Uint256Hasher> set;
+    uint256 nonce;
+    ScriptCache() { GetRandBytes(nonce.begin(), 32); }
+    uint256 Key(const CTransaction& tx, uint32_t flags) {
+        uint256 r;
+        CSHA256().Write(nonce.begin(), 32).Write(tx.GetHash().begin(), 32).Write((const unsigned char*)&flags, 4).Finalize(r.begin());
+        return r;
+    }
+    bool Has(const uint256& k, bool erase) {
+        std::lock_guard<std::mutex> l(m);
+        auto it = set.find(k);
+        if (it == set.end()) return false;
+        if (erase) set.erase(it);
+        return true;
+    }
+    void Add(const uint256& k) {
+        std::lock_guard<std::mutex> l(m);
+        if (set.size() > 500000) set.erase(set.begin());
+        set.insert(k);
+    }
+};
+ScriptCache& GetScriptCache() {
+    static ScriptCache c;
+    return c;
+}
+
+// Block validation checker: script logic on the CPU pool, ECDSA deferred to a batch,
+// eager checks served from the signature cache when possible.
+class BlockSigChecker : public DeferringSignatureChecker {
+public:
+    BlockSigChecker(const CTransaction* tx, unsigned nIn, Amount amount, const PrecomputedTransactionData* txdata,
+                    std::vector<DeferredSigCheck>* sink)
+        : DeferringSignatureChecker(tx, nIn, amount, txdata, sink) {}
+
+protected:
+    bool VerifySignature(const std::vector<unsigned char>& sig, const std::vector<unsigned char>& pubkey,
+                         const uint256& sighash) const override {
+        SignatureCache& cache = GetSignatureCache();
+        const uint256 e = cache.Entry(sighash, sig, pubkey);
+        if (cache.Get(e, true)) return true;
+        return TransactionSignatureChecker::VerifySignature(sig, pubkey, sighash);
+    }
+};
+
+struct ScriptJob {
+    const CTransaction* tx;
+    unsigned nIn;
+    CScript scriptPubKey;
+    Amount amount;
+    const PrecomputedTransactionData* txdata;
+};
+} // namespace
+
+// ------------------------------------------------------------------ construction
+bool Chainstate::WorkComparator::operator()(const CBlockIndex* pa, const CBlockIndex* pb) const {
+    if (pa->nChainWork > pb->nChainWork) return false;
+    if (pa->nChainWork < pb->nChainWork) return true;
+    if (pa->nSequenceId < pb->nSequenceId) return false;
+    if (pa->nSequenceId > pb->nSequenceId) return true;
+    if (pa < pb) return false;
+    if (pa > pb) return true;
+    return false;
+}
+
+Chainstate::Chainstate(const CChainParams& p, const ChainstateOptions& o) : params(p), opts(o) {
+    const std::string base = opts.datadir.empty() ? std::string(".") : opts.datadir;
+    if (!opts.memoryOnly) {
+        TryCreateDirectories(base + "/blocks");
+        SetBlocksDir(base + "/blocks");
+    } else {
+        TryCreateDirectories(base + "/blocks");
+        SetBlocksDir(base + "/blocks");
+    }
+    pblocktree.reset(new CBlockTreeDB(base + "/blocks/index", opts.memoryOnly, opts.wipe));
+    pcoinsdbview.reset(new CCoinsViewDB(base + "/chainstate", opts.memoryOnly, opts.wipe));
+    pcoinsTip.reset(new CCoinsViewCache(pcoinsdbview.get()));
+    int threads = opts.scriptThreads <= 0 ? GetNumCores() : opts.scriptThreads;
+    threads = std::max(1, std::min(threads, MAX_SCRIPTCHECK_THREADS));
+    pool.reset(new WorkerPool(threads));
+    fReindex = opts.wipe;
+}
+
+Chainstate::~Chainstate() {
+    if (g_chainstate == this) g_chainstate = nullptr;
+}
+
+void Chainstate::Shutdown() {
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    CValidationState state;
+    FlushStateToDisk(state, FLUSH_STATE_ALWAYS);
+}
+
+CBlockIndex* Chainstate::LookupBlockIndex(const uint256& hash) const {
+    auto it = mapBlockIndex.find(hash);
+    return it == mapBlockIndex.end() ? nullptr : it->second;
+}
+
+CBlockIndex* Chainstate::InsertBlockIndex(const uint256& hash) {
+    if (hash.IsNull()) return nullptr;
+    auto it = mapBlockIndex.find(hash);
+    if (it != mapBlockIndex.end()) return it->second;
+    blockIndexStorage.emplace_back(new CBlockIndex());
+    CBlockIndex* pindexNew = blockIndexStorage.back().get();
+    auto ins = mapBlockIndex.emplace(hash, pindexNew);
+    pindexNew->phashBlock = &ins.first->first;
+    return pindexNew;
+}
+
+CBlockIndex* Chainstate::AddToBlockIndex(const CBlockHeader& block) {
+    const uint256 hash = block.GetHash(params.GetConsensus());
+    auto it = mapBlockIndex.find(hash);
+    if (it != mapBlockIndex.end()) return it->second;
+    blockIndexStorage.emplace_back(new CBlockIndex(block));
+    CBlockIndex* pindexNew = blockIndexStorage.back().get();
+    // BlockIndexes are only accessed under cs_main; sequence ids assigned on full data
+    pindexNew->nSequenceId = 0;
+    auto mi = mapBlockIndex.emplace(hash, pindexNew).first;
+    pindexNew->phashBlock = &mi->first;
+    auto miPrev = mapBlockIndex.find(block.hashPrevBlock);
+    if (miPrev != mapBlockIndex.end()) {
+        pindexNew->pprev = miPrev->second;
+        pindexNew->nHeight = pindexNew->pprev->nHeight + 1;
+        pindexNew->BuildSkip();
+    }
+    pindexNew->nTimeMax = pindexNew->pprev ? std::max(pindexNew->pprev->nTimeMax, pindexNew->nTime) : pindexNew->nTime;
+    pindexNew->nChainWork = (pindexNew->pprev ? pindexNew->pprev->nChainWork : arith_uint256(0)) + GetBlockProof(*pindexNew);
+    pindexNew->RaiseValidity(BLOCK_VALID_TREE);
+    if (pindexBestHeader == nullptr || pindexBestHeader->nChainWork < pindexNew->nChainWork) pindexBestHeader = pindexNew;
+    setDirtyBlockIndex.insert(pindexNew);
+    return pindexNew;
+}
+
+// ------------------------------------------------------------------ checks
+uint32_t Chainstate::GetBlockScriptFlags(const CBlockIndex* pindex) const {
+    const Consensus::Params& cp = params.GetConsensus();
+    const int64_t nBIP16SwitchTime = 1333238400;
+    uint32_t flags = pindex->GetBlockTime() >= nBIP16SwitchTime ? SCRIPT_VERIFY_P2SH : SCRIPT_VERIFY_NONE;
+    if (pindex->nHeight >= cp.BIP66Height) flags |= SCRIPT_VERIFY_DERSIG;
+    if (pindex->nHeight >= cp.BIP65Height) flags |= SCRIPT_VERIFY_CHECKLOCKTIMEVERIFY;
+    if (VersionBitsState(pindex->pprev, cp, Consensus::DEPLOYMENT_CSV, const_cast<VersionBitsCache&>(versionbitscache)) ==
+        THRESHOLD_ACTIVE)
+        flags |= SCRIPT_VERIFY_CHECKSEQUENCEVERIFY;
+    flags |= SCRIPT_ENABLE_SIGHASH_FORKID;
+    if (IsBCPEnabled(pindex->pprev)) flags |= SCRIPT_VERIFY_STRICTENC | SCRIPT_VERIFY_LOW_S | SCRIPT_VERIFY_NULLFAIL;
+    else flags |= SCRIPT_ALLOW_NON_FORKID;
+    return flags;
+}
+
+bool Chainstate::CheckBlockHeader(const CBlockHeader& block, CValidationState& state, bool fCheckPOW) const {
+    const bool postfork = IsBCPEnabled((int)block.nHeight);
+    if (fCheckPOW && postfork && !CheckEquihashSolution(&block, params))
+        return state.DoS(100, error("CheckBlockHeader(): Equihash solution invalid"), REJECT_INVALID,
+                         "invalid-solution");
+    if (fCheckPOW && !CheckProofOfWork(block.GetHash(params.GetConsensus()), block.nBits, postfork, params.GetConsensus()))
+        return state.DoS(50, false, REJECT_INVALID, "high-hash", false, "proof of work failed");
+    return true;
+}
+
+bool Chainstate::CheckBlock(const CBlock& block, CValidationState& state, bool fCheckPOW, bool fCheckMerkleRoot) const {
+    if (block.fChecked) return true;
+    if (!CheckBlockHeader(block, state, fCheckPOW)) return false;
+    if (fCheckMerkleRoot) {
+        bool mutated = false;
+        const uint256 root = BlockMerkleRoot(block, &mutated);
+        if (block.hashMerkleRoot != root)
+            return state.DoS(100, false, REJECT_INVALID, "bad-txnmrklroot", true, "hashMerkleRoot mismatch");
+        // CVE-2012-2459: a duplicated tail would give the same root
+        if (mutated) return state.DoS(100, false, REJECT_INVALID, "bad-txns-duplicate", true, "duplicate transaction");
+    }
+    if (block.vtx.empty()) return state.DoS(100, false, REJECT_INVALID, "bad-cb-missing", false, "first tx is not coinbase");
+    const int serFlags = IsBCPEnabled((int)block.nHeight) ? 0 : SERIALIZE_BLOCK_LEGACY;
+    const uint64_t nMaxBlockSize = opts.maxBlockSize;
+    if (block.vtx.size() * MIN_TRANSACTION_SIZE > nMaxBlockSize)
+        return state.DoS(100, false, REJECT_INVALID, "bad-blk-length", false, "size limits failed");
+    const uint64_t currentBlockSize = GetSerializeSize(block, PROTOCOL_VERSION | serFlags);
+    if (currentBlockSize > nMaxBlockSize)
+        return state.DoS(100, false, REJECT_INVALID, "bad-blk-length", false, "size limits failed");
+    if (!CheckCoinbase(*block.vtx[0], state, false))
+        return state.Invalid(false, state.GetRejectCode(), state.GetRejectReason(),
+                             strprintf("Coinbase check failed (txid %s) %s", block.vtx[0]->GetHash().ToString().c_str(),
+                                       state.GetDebugMessage().c_str()));
+    uint64_t nSigOps = 0;
+    const uint64_t nMaxSigOpsCount = GetMaxBlockSigOpsCount(currentBlockSize);
+    for (size_t i = 0; i < block.vtx.size(); i++) {
+        const CTransaction& tx = *block.vtx[i];
+        nSigOps += GetSigOpCountWithoutP2SH(tx);
+        if (nSigOps > nMaxSigOpsCount)
+            return state.DoS(100, false, REJECT_INVALID, "bad-blk-sigops", false, "out-of-bounds SigOpCount");
+        if (i > 0 && !CheckRegularTransaction(tx, state, false))
+            return state.Invalid(false, state.GetRejectCode(), state.GetRejectReason(),
+                                 strprintf("Transaction check failed (txid %s) %s", tx.GetHash().ToString().c_str(),
+                                           state.GetDebugMessage().c_str()));
+    }
+    if (fCheckPOW && fCheckMerkleRoot) block.fChecked = true;
+    return true;
+}
+
+bool Chainstate::CheckIndexAgainstCheckpoint(const CBlockIndex* pindexPrev, CValidationState& state) const {
+    if (*pindexPrev->phashBlock == params.GetConsensus().hashGenesisBlock) return true;
+    const int nHeight = pindexPrev->nHeight + 1;
+    // last checkpoint present in our index
+    const auto& cps = params.Checkpoints().mapCheckpoints;
+    for (auto it = cps.rbegin(); it != cps.rend(); ++it) {
+        CBlockIndex* p = LookupBlockIndex(it->second);
+        if (p) {
+            if (nHeight < p->nHeight)
+                return state.DoS(100, error("forked chain older than last checkpoint (height %d)", nHeight));
+            break;
+        }
+    }
+    return true;
+}
+
+bool Chainstate::ContextualCheckBlockHeader(const CBlockHeader& block, CValidationState& state,
+                                            const CBlockIndex* pindexPrev, int64_t nAdjustedTime) const {
+    const Consensus::Params& cp = params.GetConsensus();
+    const int nHeight = pindexPrev == nullptr ? 0 : pindexPrev->nHeight + 1;
+    if (block.nBits != GetNextWorkRequired(pindexPrev, &block, cp))
+        return state.DoS(100, false, REJECT_INVALID, "bad-diffbits", false, "incorrect proof of work");
+    if (IsBCPEnabled(nHeight) && block.nHeight != (uint32_t)nHeight)
+        return state.Invalid(false, REJECT_INVALID, "bad-height", "incorrect block height");
+    if (block.GetBlockTime() <= pindexPrev->GetMedianTimePast())
+        return state.Invalid(false, REJECT_INVALID, "time-too-old", "block's timestamp is too early");
+    if (block.GetBlockTime() > nAdjustedTime + 2 * 60 * 60)
+        return state.Invalid(false, REJECT_INVALID, "time-too-new", "block timestamp too far in the future");
+    if ((block.nVersion < 2 && nHeight >= cp.BIP34Height) || (block.nVersion < 3 && nHeight >= cp.BIP66Height) ||
+        (block.nVersion < 4 && nHeight >= cp.BIP65Height))
+        return state.Invalid(false, REJECT_OBSOLETE, strprintf("bad-version(0x%08x)", block.nVersion),
+                             strprintf("rejected nVersion=0x%08x block", block.nVersion));
+    return true;
+}
+
+bool Chainstate::ContextualCheckTransaction(const CTransaction& tx, CValidationState& state, int nHeight,
+                                            int64_t nLockTimeCutoff) const {
+    if (!IsFinalTx(tx, nHeight, nLockTimeCutoff))
+        return state.DoS(10, false, REJECT_INVALID, "bad-txns-nonfinal", false, "non-final transaction");
+    const Consensus::Params& cp = params.GetConsensus();
+    if (IsBCPEnabled(nHeight) && nHeight <= cp.antiReplayOpReturnSunsetHeight) {
+        for (const CTxOut& o : tx.vout)
+            if (o.scriptPubKey.IsCommitment(cp.antiReplayOpReturnCommitment))
+                return state.DoS(10, false, REJECT_INVALID, "bad-txn-replay", false, "non playable transaction");
+    }
+    return true;
+}
+
+bool Chainstate::ContextualCheckTransactionForCurrentBlock(const CTransaction& tx, CValidationState& state,
+                                                           int flags) const {
+    flags = std::max(flags, 0);
+    const int nBlockHeight = chainActive.Height() + 1;
+    const int64_t cutoff = (flags & LOCKTIME_MEDIAN_TIME_PAST) ? chainActive.Tip()->GetMedianTimePast() : GetAdjustedTime();
+    return ContextualCheckTransaction(tx, state, nBlockHeight, cutoff);
+}
+
+bool Chainstate::ContextualCheckBlock(const CBlock& block, CValidationState& state, const CBlockIndex* pindexPrev) const {
+    const Consensus::Params& cp = params.GetConsensus();
+    const int nHeight = pindexPrev == nullptr ? 0 : pindexPrev->nHeight + 1;
+    int nLockTimeFlags = 0;
+    if (VersionBitsState(pindexPrev, cp, Consensus::DEPLOYMENT_CSV, const_cast<VersionBitsCache&>(versionbitscache)) ==
+        THRESHOLD_ACTIVE)
+        nLockTimeFlags |= LOCKTIME_MEDIAN_TIME_PAST;
+    const int64_t nMedianTimePast = pindexPrev == nullptr ? 0 : pindexPrev->GetMedianTimePast();
+    const int64_t cutoff = (nLockTimeFlags & LOCKTIME_MEDIAN_TIME_PAST) ? nMedianTimePast : block.GetBlockTime();
+    for (const auto& tx : block.vtx)
+        if (!ContextualCheckTransaction(*tx, state, nHeight, cutoff)) return false;
+    if (nHeight >= cp.BIP34Height) {
+        CScript expect = CScript() << nHeight;
+        const CScript& sig = block.vtx[0]->vin[0].scriptSig;
+        if (sig.size() < expect.size() || !std::equal(expect.begin(), expect.end(), sig.begin()))
+            return state.DoS(100, false, REJECT_INVALID, "bad-cb-height", false, "block height mismatch in coinbase");
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ header / block acceptance
+bool Chainstate::AcceptBlockHeader(const CBlockHeader& block, CValidationState& state, CBlockIndex** ppindex,
+                                   bool equihashChecked) {
+    const uint256 hash = block.GetHash(params.GetConsensus());
+    CBlockIndex* pindex = nullptr;
+    if (hash != params.GetConsensus().hashGenesisBlock) {
+        auto miSelf = mapBlockIndex.find(hash);
+        if (miSelf != mapBlockIndex.end()) {
+            pindex = miSelf->second;
+            if (ppindex) *ppindex = pindex;
+            if (pindex->nStatus & BLOCK_FAILED_MASK)
+                return state.Invalid(error("%s: block %s is marked invalid", __func__, hash.ToString().c_str()), 0,
+                                     "duplicate");
+            return true;
+        }
+        if (equihashChecked) {
+            const bool postfork = IsBCPEnabled((int)block.nHeight);
+            if (!CheckProofOfWork(hash, block.nBits, postfork, params.GetConsensus()))
+                return state.DoS(50, false, REJECT_INVALID, "high-hash", false, "proof of work failed");
+        } else if (!CheckBlockHeader(block, state)) {
+            return error("%s: Consensus::CheckBlockHeader: %s, %s", __func__, hash.ToString().c_str(),
+                         FormatStateMessage(state).c_str());
+        }
+        auto mi = mapBlockIndex.find(block.hashPrevBlock);
+        if (mi == mapBlockIndex.end()) return state.DoS(10, error("%s: prev block not found", __func__), 0, "bad-prevblk");
+        CBlockIndex* pindexPrev = mi->second;
+        if (pindexPrev->nStatus & BLOCK_FAILED_MASK)
+            return state.DoS(100, error("%s: prev block invalid", __func__), REJECT_INVALID, "bad-prevblk");
+        if (opts.checkpoints && !CheckIndexAgainstCheckpoint(pindexPrev, state))
+            return error("%s: CheckIndexAgainstCheckpoint(): %s", __func__, state.GetRejectReason().c_str());
+        if (!ContextualCheckBlockHeader(block, state, pindexPrev, GetAdjustedTime()))
+            return error("%s: Consensus::ContextualCheckBlockHeader: %s, %s", __func__, hash.ToString().c_str(),
+                         FormatStateMessage(state).c_str());
+    }
+    if (pindex == nullptr) pindex = AddToBlockIndex(block);
+    if (ppindex) *ppindex = pindex;
+    CheckBlockIndex();
+    return true;
+}
+
+void Chainstate::NotifyHeaderTip() {
+    static CBlockIndex* pindexHeaderOld = nullptr;
+    CBlockIndex* pindexHeader = nullptr;
+    bool fNotify = false, ibd = false;
+    {
+        std::lock_guard<std::recursive_mutex> l(cs_main);
+        pindexHeader = pindexBestHeader;
+        if (pindexHeader != pindexHeaderOld) {
+            fNotify = true;
+            ibd = IsInitialBlockDownload();
+            pindexHeaderOld = pindexHeader;
+        }
+    }
+    if (fNotify) GetMainSignals().NotifyHeaderTip(pindexHeader, ibd);
+}
+
+bool Chainstate::ProcessNewBlockHeaders(const std::vector<CBlockHeader>& headers, CValidationState& state,
+                                        const CBlockIndex** ppindex) {
+    // Batch the Equihash checks of unknown post-fork headers (GPU when >= 4 headers).
+    std::vector<const CBlockHeader*> toCheck;
+    std::vector<size_t> pos;
+    {
+        std::lock_guard<std::recursive_mutex> l(cs_main);
+        for (size_t i = 0; i < headers.size(); i++) {
+            if (!IsBCPEnabled((int)headers[i].nHeight)) continue;
+            if (mapBlockIndex.count(headers[i].GetHash(params.GetConsensus()))) continue;
+            toCheck.push_back(&headers[i]);
+            pos.push_back(i);
+        }
+    }
+    std::vector<bool> eqOk(headers.size(), true);
+    if (!toCheck.empty()) {
+        std::vector<bool> r = CheckEquihashSolutions(toCheck, params, opts.useGpu);
+        for (size_t j = 0; j < r.size(); j++) eqOk[pos[j]] = r[j];
+    }
+    {
+        std::lock_guard<std::recursive_mutex> l(cs_main);
+        for (size_t i = 0; i < headers.size(); i++) {
+            if (!eqOk[i])
+                return state.DoS(100, error("ProcessNewBlockHeaders(): Equihash solution invalid"), REJECT_INVALID,
+                                 "invalid-solution");
+            CBlockIndex* pindex = nullptr;
+            if (!AcceptBlockHeader(headers[i], state, &pindex, IsBCPEnabled((int)headers[i].nHeight))) return false;
+            if (ppindex) *ppindex = pindex;
+        }
+    }
+    NotifyHeaderTip();
+    return true;
+}
+
+bool Chainstate::FindBlockPos(CValidationState& state, CDiskBlockPos& pos, unsigned nAddSize, unsigned nHeight,
+                              uint64_t nTime, bool fKnown) {
+    unsigned nFile = fKnown ? pos.nFile : nLastBlockFile;
+    if (vinfoBlockFile.size() <= nFile) vinfoBlockFile.resize(nFile + 1);
+    if (!fKnown) {
+        while (vinfoBlockFile[nFile].nSize + nAddSize >= MAX_BLOCKFILE_SIZE) {
+            nFile++;
+            if (vinfoBlockFile.size() <= nFile) vinfoBlockFile.resize(nFile + 1);
+        }
+        pos.nFile = nFile;
+        pos.nPos = vinfoBlockFile[nFile].nSize;
+    }
+    if ((int)nFile != nLastBlockFile) {
+        if (!fKnown) LogPrintf("Leaving block file %i: %s\n", nLastBlockFile, vinfoBlockFile[nLastBlockFile].ToString().c_str());
+        FlushBlockFile(!fKnown);
+        nLastBlockFile = nFile;
+    }
+    vinfoBlockFile[nFile].AddBlock(nHeight, nTime);
+    if (fKnown) vinfoBlockFile[nFile].nSize = std::max(pos.nPos + nAddSize, vinfoBlockFile[nFile].nSize);
+    else vinfoBlockFile[nFile].nSize += nAddSize;
+    if (!fKnown) {
+        const unsigned nOldChunks = (pos.nPos + BLOCKFILE_CHUNK_SIZE - 1) / BLOCKFILE_CHUNK_SIZE;
+        const unsigned nNewChunks = (vinfoBlockFile[nFile].nSize + BLOCKFILE_CHUNK_SIZE - 1) / BLOCKFILE_CHUNK_SIZE;
+        if (nNewChunks > nOldChunks) {
+            if (PruneMode()) fCheckForPruning = true;
+            FILE* file = OpenBlockFile(pos);
+            if (file) {
+                AllocateFileRange(file, pos.nPos, nNewChunks * BLOCKFILE_CHUNK_SIZE - pos.nPos);
+                fclose(file);
+            } else {
+                return state.Error("out of disk space");
+            }
+        }
+    }
+    setDirtyFileInfo.insert(nFile);
+    return true;
+}
+
+bool Chainstate::FindUndoPos(CValidationState& state, int nFile, CDiskBlockPos& pos, unsigned nAddSize) {
+    pos.nFile = nFile;
+    const unsigned nNewSize = vinfoBlockFile[nFile].nUndoSize += nAddSize;
+    pos.nPos = nNewSize - nAddSize;
+    setDirtyFileInfo.insert(nFile);
+    const unsigned nOldChunks = (pos.nPos + UNDOFILE_CHUNK_SIZE - 1) / UNDOFILE_CHUNK_SIZE;
+    const unsigned nNewChunks = (nNewSize + UNDOFILE_CHUNK_SIZE - 1) / UNDOFILE_CHUNK_SIZE;
+    if (nNewChunks > nOldChunks) {
+        if (PruneMode()) fCheckForPruning = true;
+        FILE* file = OpenUndoFile(pos);
+        if (!file) return state.Error("out of disk space");
+        AllocateFileRange(file, pos.nPos, nNewChunks * UNDOFILE_CHUNK_SIZE - pos.nPos);
+        fclose(file);
+    }
+    return true;
+}
+
+void Chainstate::FlushBlockFile(bool fFinalize) {
+    CDiskBlockPos posOld(nLastBlockFile, 0);
+    if (FILE* f = OpenBlockFile(posOld)) {
+        if (fFinalize && nLastBlockFile < (int)vinfoBlockFile.size() &&
+            ftruncate(fileno(f), vinfoBlockFile[nLastBlockFile].nSize) != 0) {
+        }
+        FileCommit(f);
+        fclose(f);
+    }
+    if (FILE* f = OpenUndoFile(posOld)) {
+        if (fFinalize && nLastBlockFile < (int)vinfoBlockFile.size() &&
+            ftruncate(fileno(f), vinfoBlockFile[nLastBlockFile].nUndoSize) != 0) {
+        }
+        FileCommit(f);
+        fclose(f);
+    }
+}
+
+bool Chainstate::ReceivedBlockTransactions(const CBlock& block, CValidationState& state, CBlockIndex* pindexNew,
+                                           const CDiskBlockPos& pos) {
+    pindexNew->nTx = (unsigned)block.vtx.size();
+    pindexNew->nChainTx = 0;
+    pindexNew->nFile = pos.nFile;
+    pindexNew->nDataPos = pos.nPos;
+    pindexNew->nUndoPos = 0;
+    pindexNew->nStatus |= BLOCK_HAVE_DATA;
+    pindexNew->RaiseValidity(BLOCK_VALID_TRANSACTIONS);
+    setDirtyBlockIndex.insert(pindexNew);
+    if (pindexNew->pprev == nullptr || pindexNew->pprev->nChainTx) {
+        // the block and all its descendants waiting for data can now be linked
+        std::deque<CBlockIndex*> queue;
+        queue.push_back(pindexNew);
+        while (!queue.empty()) {
+            CBlockIndex* pindex = queue.front();
+            queue.pop_front();
+            pindex->nChainTx = (pindex->pprev ? pindex->pprev->nChainTx : 0) + pindex->nTx;
+            pindex->nSequenceId = nBlockSequenceId++;
+            if (chainActive.Tip() == nullptr || !setBlockIndexCandidates.value_comp()(pindex, chainActive.Tip()))
+                setBlockIndexCandidates.insert(pindex);
+            auto range = mapBlocksUnlinked.equal_range(pindex);
+            while (range.first != range.second) {
+                queue.push_back(range.first->second);
+                range.first = mapBlocksUnlinked.erase(range.first);
+            }
+        }
+    } else if (pindexNew->pprev && pindexNew->pprev->IsValid(BLOCK_VALID_TREE)) {
+        mapBlocksUnlinked.insert(std::make_pair(pindexNew->pprev, pindexNew));
+    }
+    return true;
+}
+
+bool Chainstate::AcceptBlock(const std::shared_ptr<const CBlock>& pblock, CValidationState& state, CBlockIndex** ppindex,
+                             bool fRequested, const CDiskBlockPos* dbp, bool* fNewBlock) {
+    const CBlock& block = *pblock;
+    if (fNewBlock) *fNewBlock = false;
+    CBlockIndex* pindexDummy = nullptr;
+    CBlockIndex*& pindex = ppindex ? *ppindex : pindexDummy;
+    if (!AcceptBlockHeader(block, state, &pindex)) return false;
+    const bool fAlreadyHave = pindex->nStatus & BLOCK_HAVE_DATA;
+    const bool fHasMoreWork = chainActive.Tip() ? pindex->nChainWork > chainActive.Tip()->nChainWork : true;
+    const bool fTooFarAhead = pindex->nHeight > int(chainActive.Height() + MIN_BLOCKS_TO_KEEP);
+    if (fAlreadyHave) return true;
+    if (!fRequested) {
+        if (pindex->nTx != 0) return true;
+        if (!fHasMoreWork) return true;
+        if (fTooFarAhead) return true;
+    }
+    if (fNewBlock) *fNewBlock = true;
+    if (!CheckBlock(block, state) || !ContextualCheckBlock(block, state, pindex->pprev)) {
+        if (state.IsInvalid() && !state.CorruptionPossible()) {
+            pindex->nStatus |= BLOCK_FAILED_VALID;
+            setDirtyBlockIndex.insert(pindex);
+        }
+        return error("%s: %s (block %s)", __func__, FormatStateMessage(state).c_str(),
+                     block.GetHash(params.GetConsensus()).ToString().c_str());
+    }
+    if (!IsInitialBlockDownload() && chainActive.Tip() == pindex->pprev) GetMainSignals().NewPoWValidBlock(pindex, pblock);
+    const int nHeight = pindex->nHeight;
+    try {
+        const unsigned nBlockSize = (unsigned)GetSerializeSize(block, PROTOCOL_VERSION);
+        CDiskBlockPos blockPos;
+        if (dbp != nullptr) blockPos = *dbp;
+        if (!FindBlockPos(state, blockPos, nBlockSize + 8, nHeight, block.GetBlockTime(), dbp != nullptr))
+            return error("AcceptBlock(): FindBlockPos failed");
+        if (dbp == nullptr && !WriteBlockToDisk(block, blockPos, params.DiskMagic()))
+            return state.Error("Failed to write block");
+        if (!ReceivedBlockTransactions(block, state, pindex, blockPos))
+            return error("AcceptBlock(): ReceivedBlockTransactions failed");
+    } catch (const std::runtime_error& e) {
+        return state.Error(std::string("System error: ") + e.what());
+    }
+    if (fCheckForPruning) FlushStateToDisk(state, FLUSH_STATE_NONE);
+    return true;
+}
+
+bool Chainstate::ProcessNewBlock(const std::shared_ptr<const CBlock>& pblock, bool fForceProcessing, bool* fNewBlock,
+                                 CValidationState* stateOut) {
+    {
+        CBlockIndex* pindex = nullptr;
+        if (fNewBlock) *fNewBlock = false;
+        CValidationState state;
+        // the expensive context-free checks (Equihash, merkle) run before taking cs_main
+        bool ret = CheckBlock(*pblock, state);
+        std::lock_guard<std::recursive_mutex> l(cs_main);
+        if (ret) ret = AcceptBlock(pblock, state, &pindex, fForceProcessing, nullptr, fNewBlock);
+        CheckBlockIndex();
+        if (!ret) {
+            GetMainSignals().BlockChecked(*pblock, state);
+            if (stateOut) *stateOut = state;
+            return error("%s: AcceptBlock FAILED (%s)", __func__, FormatStateMessage(state).c_str());
+        }
+    }
+    NotifyHeaderTip();
+    CValidationState state;
+    if (!ActivateBestChain(state, pblock)) {
+        if (stateOut) *stateOut = state;
+        return error("%s: ActivateBestChain failed (%s)", __func__, FormatStateMessage(state).c_str());
+    }
+    if (stateOut) *stateOut = state;
+    return true;
+}
+
+bool Chainstate::TestBlockValidity(CValidationState& state, const CBlock& block, CBlockIndex* pindexPrev, bool fCheckPOW,
+                                   bool fCheckMerkleRoot) {
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    if (!(pindexPrev && pindexPrev == chainActive.Tip())) return state.Error("TestBlockValidity: not on tip");
+    CCoinsViewCache viewNew(pcoinsTip.get());
+    CBlockIndex indexDummy(block);
+    indexDummy.pprev = pindexPrev;
+    indexDummy.nHeight = pindexPrev->nHeight + 1;
+    if (!ContextualCheckBlockHeader(block, state, pindexPrev, GetAdjustedTime()))
+        return error("%s: Consensus::ContextualCheckBlockHeader: %s", __func__, FormatStateMessage(state).c_str());
+    if (!CheckBlock(block, state, fCheckPOW, fCheckMerkleRoot))
+        return error("%s: Consensus::CheckBlock: %s", __func__, FormatStateMessage(state).c_str());
+    if (!ContextualCheckBlock(block, state, pindexPrev))
+        return error("%s: Consensus::ContextualCheckBlock: %s", __func__, FormatStateMessage(state).c_str());
+    if (!ConnectBlock(block, state, &indexDummy, viewNew, true)) return false;
+    return true;
+}
+
+// ------------------------------------------------------------------ connect / disconnect
+bool Chainstate::CheckInputs(const CTransaction& tx, CValidationState& state, const CCoinsViewCache& inputs,
+                             bool fScriptChecks, uint32_t flags, bool cacheStore,
+                             const PrecomputedTransactionData& txdata) {
+    // mempool path: eager evaluation with the caching checker (block path is batched in ConnectBlock)
+    if (!Consensus::CheckTxInputs(tx, state, inputs, chainActive.Height() + 1)) return false;
+    if (!fScriptChecks) return true;
+    ScriptCache& sc = GetScriptCache();
+    const uint256 key = sc.Key(tx, flags);
+    if (sc.Has(key, false)) return true;
+    for (size_t i = 0; i < tx.vin.size(); i++) {
+        const Coin& coin = inputs.AccessCoin(tx.vin[i].prevout);
+        const CScript& spk = coin.GetTxOut().scriptPubKey;
+        const Amount amount = coin.GetTxOut().nValue;
+        ScriptError err;
+        CachingTransactionSignatureChecker checker(&tx, (unsigned)i, amount, cacheStore, &txdata);
+        if (!VerifyScript(tx.vin[i].scriptSig, spk, flags, checker, &err)) {
+            if (flags & STANDARD_NOT_MANDATORY_VERIFY_FLAGS) {
+                ScriptError err2;
+                CachingTransactionSignatureChecker checker2(&tx, (unsigned)i, amount, cacheStore, &txdata);
+                if (VerifyScript(tx.vin[i].scriptSig, spk, flags & ~STANDARD_NOT_MANDATORY_VERIFY_FLAGS, checker2, &err2))
+                    return state.Invalid(false, REJECT_NONSTANDARD,
+                                         strprintf("non-mandatory-script-verify-flag (%s)", ScriptErrorString(err)));
+            }
+            return state.DoS(100, false, REJECT_INVALID,
+                             strprintf("mandatory-script-verify-flag-failed (%s)", ScriptErrorString(err)));
+        }
+    }
+    if (cacheStore) sc.Add(key);
+    return true;
+}
+
+bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
+                              bool fJustCheck) {
+    const int64_t nTimeStart = GetTimeMicros();
+    const Consensus::Params& cp = params.GetConsensus();
+    if (!CheckBlock(block, state, !fJustCheck, !fJustCheck))
+        return error("%s: Consensus::CheckBlock: %s", __func__, FormatStateMessage(state).c_str());
+    const uint256 hashPrevBlock = pindex->pprev == nullptr ? uint256() : pindex->pprev->GetBlockHash();
+    if (hashPrevBlock != view.GetBestBlock()) return state.Error("ConnectBlock: view best block mismatch");
+    if (block.GetHash(cp) == cp.hashGenesisBlock) {
+        if (!fJustCheck) view.SetBestBlock(pindex->GetBlockHash());
+        return true;
+    }
+    bool fScriptChecks = true;
+    if (!opts.assumeValid.IsNull()) {
+        auto it = mapBlockIndex.find(opts.assumeValid);
+        if (it != mapBlockIndex.end() && it->second->GetAncestor(pindex->nHeight) == pindex && pindexBestHeader &&
+            pindexBestHeader->GetAncestor(pindex->nHeight) == pindex &&
+            pindexBestHeader->nChainWork >= UintToArith256(cp.nMinimumChainWork)) {
+            fScriptChecks = GetBlockProofEquivalentTime(*pindexBestHeader, *pindex, *pindexBestHeader, cp) <=
+                            60 * 60 * 24 * 7 * 2;
+        }
+    }
+    // BIP30 (exceptions for the two historic duplicate coinbases; moot after BIP34 block)
+    bool fEnforceBIP30 =
+        (!pindex->phashBlock) ||
+        !((pindex->nHeight == 91842 &&
+           pindex->GetBlockHash() == uint256S("0x00000000000a4d0a398161ffc163c503763b1f4360639393e0e4c8e300e0caec")) ||
+          (pindex->nHeight == 91880 &&
+           pindex->GetBlockHash() == uint256S("0x00000000000743f190a18c5577a3c2d2a1f610ae9601ac046a38084ccb7cd721")));
+    const CBlockIndex* pindexBIP34height = pindex->pprev->GetAncestor(cp.BIP34Height);
+    fEnforceBIP30 = fEnforceBIP30 && (!pindexBIP34height || !(pindexBIP34height->GetBlockHash() == cp.BIP34Hash));
+    if (fEnforceBIP30) {
+        for (const auto& tx : block.vtx)
+            for (size_t o = 0; o < tx->vout.size(); o++)
+                if (view.HaveCoin(COutPoint(tx->GetHash(), (uint32_t)o)))
+                    return state.DoS(100, error("ConnectBlock(): tried to overwrite transaction"), REJECT_INVALID,
+                                     "bad-txns-BIP30");
+    }
+    int nLockTimeFlags = 0;
+    if (VersionBitsState(pindex->pprev, cp, Consensus::DEPLOYMENT_CSV, versionbitscache) == THRESHOLD_ACTIVE)
+        nLockTimeFlags |= LOCKTIME_VERIFY_SEQUENCE;
+    const uint32_t flags = GetBlockScriptFlags(pindex);
+    const bool postfork = IsBCPEnabled(pindex->nHeight);
+
+    CBlockUndo blockundo;
+    std::vector<int> prevheights;
+    Amount nFees = 0;
+    int nInputs = 0;
+    uint64_t nSigOpsCount = 0;
+    const uint64_t currentBlockSize = GetSerializeSize(block, PROTOCOL_VERSION);
+    const uint64_t nMaxSigOpsCount = GetMaxBlockSigOpsCount(currentBlockSize);
+    CDiskTxPos pos(pindex->GetBlockPos(), GetSizeOfCompactSize(block.vtx.size()));
+    std::vector<std::pair<uint256, CDiskTxPos>> vPos;
+    vPos.reserve(block.vtx.size());
+    blockundo.vtxundo.reserve(block.vtx.size() - 1);
+    std::vector<std::unique_ptr<PrecomputedTransactionData>> txdatas(block.vtx.size());
+    std::vector<ScriptJob> jobs;
+    std::vector<uint256> scriptCacheKeys;
+    ScriptCache& sc = GetScriptCache();
+
+    for (size_t i = 0; i < block.vtx.size(); i++) {
+        const CTransaction& tx = *block.vtx[i];
+        nInputs += (int)tx.vin.size();
+        if (!tx.IsCoinBase()) {
+            if (!view.HaveInputs(tx))
+                return state.DoS(100, error("ConnectBlock(): inputs missing/spent"), REJECT_INVALID,
+                                 "bad-txns-inputs-missingorspent");
+            prevheights.resize(tx.vin.size());
+            for (size_t j = 0; j < tx.vin.size(); j++) prevheights[j] = view.AccessCoin(tx.vin[j].prevout).GetHeight();
+            if (!SequenceLocks(tx, nLockTimeFlags, &prevheights, *pindex))
+                return state.DoS(100, error("%s: contains a non-BIP68-final transaction", __func__), REJECT_INVALID,
+                                 "bad-txns-nonfinal");
+        }
+        const uint64_t txSigOps = GetTransactionSigOpCount(tx, view, flags);
+        if (txSigOps > MAX_TX_SIGOPS_COUNT) return state.DoS(100, false, REJECT_INVALID, "bad-txn-sigops");
+        nSigOpsCount += txSigOps;
+        if (nSigOpsCount > nMaxSigOpsCount)
+            return state.DoS(100, error("ConnectBlock(): too many sigops"), REJECT_INVALID, "bad-blk-sigops");
+        if (!tx.IsCoinBase()) {
+            nFees += view.GetValueIn(tx) - tx.GetValueOut();
+            if (!Consensus::CheckTxInputs(tx, state, view, pindex->nHeight))
+                return error("ConnectBlock(): CheckTxInputs on %s failed with %s", tx.GetHash().ToString().c_str(),
+                             FormatStateMessage(state).c_str());
+            if (fScriptChecks) {
+                const uint256 key = sc.Key(tx, flags);
+                // transactions fully validated under these flags in the mempool skip re-execution
+                if (!sc.Has(key, !fJustCheck)) {
+                    txdatas[i].reset(new PrecomputedTransactionData(tx));
+                    for (size_t j = 0; j < tx.vin.size(); j++) {
+                        const Coin& coin = view.AccessCoin(tx.vin[j].prevout);
+                        jobs.push_back(ScriptJob{&tx, (unsigned)j, coin.GetTxOut().scriptPubKey, coin.GetTxOut().nValue,
+                                                 txdatas[i].get()});
+                    }
+                }
+            }
+        }
+        CTxUndo undoDummy;
+        if (i > 0) blockundo.vtxundo.push_back(CTxUndo());
+        CTxUndo& undo = i == 0 ? undoDummy : blockundo.vtxundo.back();
+        if (!tx.IsCoinBase()) {
+            undo.vprevout.reserve(tx.vin.size());
+            for (const CTxIn& in : tx.vin) {
+                undo.vprevout.emplace_back();
+                if (!view.SpendCoin(in.prevout, &undo.vprevout.back())) return state.Error("ConnectBlock: spend failed");
+            }
+        }
+        AddCoins(view, tx, pindex->nHeight);
+        vPos.push_back(std::make_pair(tx.GetHash(), pos));
+        pos.nTxOffset += (unsigned)GetSerializeSize(tx, PROTOCOL_VERSION);
+    }
+    const int64_t nTime2 = GetTimeMicros();
+
+    const Amount blockReward = nFees + GetBlockSubsidy(pindex->nHeight, cp);
+    if (block.vtx[0]->GetValueOut() > blockReward)
+        return state.DoS(100,
+                         error("ConnectBlock(): coinbase pays too much (actual=%lld vs limit=%lld)",
+                               (long long)block.vtx[0]->GetValueOut(), (long long)blockReward),
+                         REJECT_INVALID, "bad-cb-amount");
+
+    // ---- scripts on the CPU pool, ECDSA batched (GPU when large enough)
+    if (!jobs.empty()) {
+        std::vector<std::vector<DeferredSigCheck>> sinks(jobs.size());
+        std::vector<uint8_t> scriptOk(jobs.size(), 1);
+        std::atomic<bool> anyFail{false};
+        pool->ParallelFor(
+            jobs.size(),
+            [&](size_t k) {
+                if (anyFail.load(std::memory_order_relaxed)) return;
+                const ScriptJob& J = jobs[k];
+                BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k]);
+                ScriptError err;
+                if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, J.scriptPubKey, flags, checker, &err)) {
+                    scriptOk[k] = 0;
+                    anyFail = true;
+                }
+            },
+            4);
+        bool ok = !anyFail.load();
+        if (ok) {
+            size_t total = 0;
+            for (auto& s : sinks) total += s.size();
+            std::vector<DeferredSigCheck> all;
+            all.reserve(total);
+            for (auto& s : sinks)
+                for (auto& c : s) all.push_back(std::move(c));
+            ok = BatchVerifySignatures(all, pool.get(), opts.useGpu, false, !fJustCheck);
+        }
+        // Before the fork script failures do not invalidate blocks (reference validation.cpp:2121-2126).
+        if (!ok && postfork)
+            return state.DoS(100, false, REJECT_INVALID, "blk-bad-inputs", false, "parallel script check failed");
+    }
+    const int64_t nTime4 = GetTimeMicros();
+    LogPrint(BCLog::BENCH, "    - Connect %u txs (%d inputs, %zu script jobs): %.2fms, verify %.2fms\n",
+             (unsigned)block.vtx.size(), nInputs, jobs.size(), 0.001 * (nTime2 - nTimeStart), 0.001 * (nTime4 - nTime2));
+    if (fJustCheck) return true;
+
+    if (pindex->GetUndoPos().IsNull() || !pindex->IsValid(BLOCK_VALID_SCRIPTS)) {
+        if (pindex->GetUndoPos().IsNull()) {
+            CDiskBlockPos upos;
+            if (!FindUndoPos(state, pindex->nFile, upos, (unsigned)GetSerializeSize(blockundo, PROTOCOL_VERSION) + 40))
+                return error("ConnectBlock(): FindUndoPos failed");
+            if (!UndoWriteToDisk(blockundo, upos, pindex->pprev->GetBlockHash(), params.DiskMagic()))
+                return state.Error("Failed to write undo data");
+            pindex->nUndoPos = upos.nPos;
+            pindex->nStatus |= BLOCK_HAVE_UNDO;
+        }
+        pindex->RaiseValidity(BLOCK_VALID_SCRIPTS);
+        setDirtyBlockIndex.insert(pindex);
+    }
+    if (opts.txindex && !pblocktree->WriteTxIndex(vPos)) return state.Error("Failed to write transaction index");
+    view.SetBestBlock(pindex->GetBlockHash());
+    nLastConnectMicros = GetTimeMicros() - nTimeStart;
+    return true;
+}
+
+static DisconnectResult UndoCoinSpend(const Coin& undo, CCoinsViewCache& view, const COutPoint& out) {
+    bool fClean = true;
+    if (view.HaveCoin(out)) fClean = false; // overwriting transaction output
+    if (undo.GetHeight() == 0) {
+        // pre-0.15 undo records lacked height/coinbase: recover them from another output of the tx
+        const Coin& alternate = AccessByTxid(view, out.hash);
+        if (alternate.IsSpent()) return DISCONNECT_FAILED;
+        Coin c = undo;
+        c.nHeight = alternate.nHeight;
+        c.fCoinBase = alternate.fCoinBase;
+        view.AddCoin(out, std::move(c), !fClean);
+        return fClean ? DISCONNECT_OK : DISCONNECT_UNCLEAN;
+    }
+    Coin c = undo;
+    view.AddCoin(out, std::move(c), !fClean);
+    return fClean ? DISCONNECT_OK : DISCONNECT_UNCLEAN;
+}
+
+DisconnectResult Chainstate::DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view) {
+    CBlockUndo blockUndo;
+    CDiskBlockPos pos = pindex->GetUndoPos();
+    if (pos.IsNull()) {
+        error("DisconnectBlock(): no undo data available");
+        return DISCONNECT_FAILED;
+    }
+    if (!UndoReadFromDisk(blockUndo, pos, pindex->pprev->GetBlockHash())) {
+        error("DisconnectBlock(): failure reading undo data");
+        return DISCONNECT_FAILED;
+    }
+    if (blockUndo.vtxundo.size() + 1 != block.vtx.size()) {
+        error("DisconnectBlock(): block and undo data inconsistent");
+        return DISCONNECT_FAILED;
+    }
+    bool fClean = true;
+    for (int i = (int)block.vtx.size() - 1; i >= 0; i--) {
+        const CTransaction& tx = *block.vtx[i];
+        const uint256& txid = tx.GetHash();
+        // outputs must be unspent; remove them
+        for (size_t o = 0; o < tx.vout.size(); o++) {
+            if (tx.vout[o].scriptPubKey.IsUnspendable()) continue;
+            COutPoint out(txid, (uint32_t)o);
+            Coin coin;
+            const bool is_spent = view.SpendCoin(out, &coin);
+            if (!is_spent || tx.vout[o] != coin.GetTxOut() || (uint32_t)pindex->nHeight != coin.GetHeight() ||
+                tx.IsCoinBase() != coin.IsCoinBase())
+                fClean = false;
+        }
+        if (i > 0) {
+            const CTxUndo& txundo = blockUndo.vtxundo[i - 1];
+            if (txundo.vprevout.size() != tx.vin.size()) {
+                error("DisconnectBlock(): transaction and undo data inconsistent");
+                return DISCONNECT_FAILED;
+            }
+            for (size_t j = tx.vin.size(); j-- > 0;) {
+                const DisconnectResult res = UndoCoinSpend(txundo.vprevout[j], view, tx.vin[j].prevout);
+                if (res == DISCONNECT_FAILED) return DISCONNECT_FAILED;
+                fClean = fClean && res != DISCONNECT_UNCLEAN;
+            }
+        }
+    }
+    view.SetBestBlock(pindex->pprev->GetBlockHash());
+    return fClean ? DISCONNECT_OK : DISCONNECT_UNCLEAN;
+}
+
+// ------------------------------------------------------------------ flushing
+uint64_t Chainstate::CalculateCurrentUsage() const {
+    uint64_t r = 0;
+    for (const CBlockFileInfo& f : vinfoBlockFile) r += f.nSize + f.nUndoSize;
+    return r;
+}
+
+bool Chainstate::FlushStateToDisk(CValidationState& state, FlushStateMode mode, int nManualPruneHeight) {
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    const int64_t nMempoolUsage = mempool ? (int64_t)mempool->DynamicMemoryUsage() : 0;
+    std::set<int> setFilesToPrune;
+    bool fFlushForPrune = false;
+    try {
+        if (PruneMode() && (fCheckForPruning || nManualPruneHeight > 0) && !fReindex) {
+            if (nManualPruneHeight > 0) FindFilesToPruneManual(setFilesToPrune, nManualPruneHeight);
+            else FindFilesToPrune(setFilesToPrune, params.PruneAfterHeight());
+            fCheckForPruning = false;
+            if (!setFilesToPrune.empty()) {
+                fFlushForPrune = true;
+                if (!fHavePruned) {
+                    pblocktree->WriteFlag("prunedblockfiles", true);
+                    fHavePruned = true;
+                }
+            }
+        }
+        const int64_t nNow = GetTimeMicros();
+        if (nLastWrite == 0) nLastWrite = nNow;
+        if (nLastFlush == 0) nLastFlush = nNow;
+        if (nLastSetChain == 0) nLastSetChain = nNow;
+        const int64_t nMempoolSizeMax = gArgs.GetArg("-maxmempool", (int64_t)DEFAULT_MAX_MEMPOOL_SIZE) * 1000000;
+        const int64_t cacheSize = (int64_t)pcoinsTip->DynamicMemoryUsage();
+        const int64_t nTotalSpace = (int64_t)opts.coinsCacheBytes + std::max<int64_t>(nMempoolSizeMax - nMempoolUsage, 0);
+        const bool fCacheLarge = mode == FLUSH_STATE_PERIODIC &&
+                                 cacheSize > std::max((9 * nTotalSpace) / 10, nTotalSpace - (int64_t)(10u << 20));
+        const bool fCacheCritical = mode == FLUSH_STATE_IF_NEEDED && cacheSize > nTotalSpace;
+        const bool fPeriodicWrite = mode == FLUSH_STATE_PERIODIC && nNow > nLastWrite + (int64_t)DATABASE_WRITE_INTERVAL * 1000000;
+        const bool fPeriodicFlush = mode == FLUSH_STATE_PERIODIC && nNow > nLastFlush + (int64_t)DATABASE_FLUSH_INTERVAL * 1000000;
+        const bool fDoFullFlush = (mode == FLUSH_STATE_ALWAYS) || fCacheLarge || fCacheCritical || fPeriodicFlush || fFlushForPrune;
+        if (fDoFullFlush || fPeriodicWrite) {
+            FlushBlockFile();
+            std::vector<std::pair<int, const CBlockFileInfo*>> vFiles;
+            for (int f : setDirtyFileInfo) vFiles.push_back(std::make_pair(f, &vinfoBlockFile[f]));
+            setDirtyFileInfo.clear();
+            std::vector<const CBlockIndex*> vBlocks(setDirtyBlockIndex.begin(), setDirtyBlockIndex.end());
+            setDirtyBlockIndex.clear();
+            if (!pblocktree->WriteBatchSync(vFiles, nLastBlockFile, vBlocks))
+                return state.Error("Failed to write to block index database");
+            if (fFlushForPrune) UnlinkPrunedFiles(setFilesToPrune);
+            nLastWrite = nNow;
+        }
+        if (fDoFullFlush) {
+            if (!pcoinsTip->Flush()) return state.Error("Failed to write to coin database");
+            nLastFlush = nNow;
+        }
+        if (fDoFullFlush || ((mode == FLUSH_STATE_ALWAYS || mode == FLUSH_STATE_PERIODIC) &&
+                             nNow > nLastSetChain + (int64_t)DATABASE_WRITE_INTERVAL * 1000000)) {
+            if (chainActive.Tip()) GetMainSignals().SetBestChain(chainActive.GetLocator());
+            nLastSetChain = nNow;
+        }
+    } catch (const std::runtime_error& e) {
+        return state.Error(std::string("System error while flushing: ") + e.what());
+    }
+    return true;
+}
+
+void Chainstate::FlushStateToDisk() {
+    CValidationState state;
+    FlushStateToDisk(state, FLUSH_STATE_ALWAYS);
+}
+
+// ------------------------------------------------------------------ tip management
+void Chainstate::UpdateTip(CBlockIndex* pindexNew) {
+    chainActive.SetTip(pindexNew);
+    if (mempool) mempool->AddTransactionsUpdated(1);
+    cvBlockChange.notify_all();
+    strMiscWarning.clear();
+    if (!IsInitialBlockDownload()) {
+        int nUpgraded = 0;
+        const CBlockIndex* pindex = chainActive.Tip();
+        for (int i = 0; i < 100 && pindex != nullptr; i++) {
+            const int32_t nExpectedVersion = bcp::ComputeBlockVersion(pindex->pprev, params.GetConsensus(), versionbitscache);
+            if (pindex->nVersion > VERSIONBITS_LAST_OLD_BLOCK_VERSION && (pindex->nVersion & ~nExpectedVersion) != 0)
+                ++nUpgraded;
+            pindex = pindex->pprev;
+        }
+        if (nUpgraded > 100 / 2)
+            strMiscWarning = "Warning: Unknown block versions being mined! It's possible unknown rules are in effect";
+    }
+    LogPrintf("UpdateTip: new best=%s height=%d version=0x%08x log2_work=%.8g tx=%lu date='%lld' cache=%.1fMiB(%utxo)\n",
+              chainActive.Tip()->GetBlockHash().ToString().c_str(), chainActive.Height(), chainActive.Tip()->nVersion,
+              std::log(chainActive.Tip()->nChainWork.getdouble()) / std::log(2.0),
+              (unsigned long)chainActive.Tip()->nChainTx, (long long)chainActive.Tip()->GetBlockTime(),
+              pcoinsTip->DynamicMemoryUsage() * (1.0 / (1 << 20)), pcoinsTip->GetCacheSize());
+}
+
+bool Chainstate::ReadBlock(CBlock& block, const CBlockIndex* pindex, bool checkPow) const {
+    return ReadBlockFromDisk(block, pindex, params, checkPow);
+}
+
+bool Chainstate::DisconnectTip(CValidationState& state, bool fBare) {
+    CBlockIndex* pindexDelete = chainActive.Tip();
+    auto pblock = std::make_shared<CBlock>();
+    if (!ReadBlockFromDisk(*pblock, pindexDelete, params)) return state.Error("Failed to read block");
+    {
+        CCoinsViewCache view(pcoinsTip.get());
+        if (DisconnectBlock(*pblock, pindexDelete, view) != DISCONNECT_OK)
+            return error("DisconnectTip(): DisconnectBlock %s failed", pindexDelete->GetBlockHash().ToString().c_str());
+        view.Flush();
+    }
+    if (!FlushStateToDisk(state, FLUSH_STATE_IF_NEEDED)) return false;
+    UpdateTip(pindexDelete->pprev);
+    if (!fBare && mempool) UpdateMempoolForReorg(pblock->vtx, true);
+    GetMainSignals().BlockDisconnected(pblock);
+    return true;
+}
+
+bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, const std::shared_ptr<const CBlock>& pblock,
+                            ConnectTrace& trace) {
+    std::shared_ptr<const CBlock> pthisBlock;
+    if (!pblock) {
+        auto pblockNew = std::make_shared<CBlock>();
+        if (!ReadBlockFromDisk(*pblockNew, pindexNew, params)) return state.Error("Failed to read block");
+        pthisBlock = pblockNew;
+    } else {
+        pthisBlock = pblock;
+    }
+    trace.blocksConnected.emplace_back(pindexNew, pthisBlock);
+    const CBlock& blockConnecting = *pthisBlock;
+    {
+        CCoinsViewCache view(pcoinsTip.get());
+        const bool rv = ConnectBlock(blockConnecting, state, pindexNew, view);
+        GetMainSignals().BlockChecked(blockConnecting, state);
+        if (!rv) {
+            if (state.IsInvalid()) InvalidBlockFound(pindexNew, state);
+            return error("ConnectTip(): ConnectBlock %s failed (%s)", pindexNew->GetBlockHash().ToString().c_str(),
+                         FormatStateMessage(state).c_str());
+        }
+        view.Flush();
+    }
+    if (!FlushStateToDisk(state, FLUSH_STATE_IF_NEEDED)) return false;
+    if (mempool) mempool->removeForBlock(blockConnecting.vtx, pindexNew->nHeight);
+    UpdateTip(pindexNew);
+    return true;
+}
+
+CBlockIndex* Chainstate::FindMostWorkChain() {
+    while (true) {
+        if (setBlockIndexCandidates.empty()) return nullptr;
+        CBlockIndex* pindexNew = *setBlockIndexCandidates.rbegin();
+        CBlockIndex* pindexTest = pindexNew;
+        bool fInvalidAncestor = false;
+        while (pindexTest && !chainActive.Contains(pindexTest)) {
+            const bool fFailedChain = pindexTest->nStatus & BLOCK_FAILED_MASK;
+            const bool fMissingData = !(pindexTest->nStatus & BLOCK_HAVE_DATA);
+            if (fFailedChain || fMissingData) {
+                if (fFailedChain && (pindexBestInvalid == nullptr || pindexNew->nChainWork > pindexBestInvalid->nChainWork))
+                    pindexBestInvalid = pindexNew;
+                CBlockIndex* pindexFailed = pindexNew;
+                while (pindexTest != pindexFailed) {
+                    if (fFailedChain) pindexFailed->nStatus |= BLOCK_FAILED_CHILD;
+                    else if (fMissingData) mapBlocksUnlinked.insert(std::make_pair(pindexFailed->pprev, pindexFailed));
+                    setBlockIndexCandidates.erase(pindexFailed);
+                    pindexFailed = pindexFailed->pprev;
+                }
+                setBlockIndexCandidates.erase(pindexTest);
+                fInvalidAncestor = true;
+                break;
+            }
+            pindexTest = pindexTest->pprev;
+        }
+        if (!fInvalidAncestor) return pindexNew;
+    }
+}
+
+void Chainstate::PruneBlockIndexCandidates() {
+    auto it = setBlockIndexCandidates.begin();
+    while (it != setBlockIndexCandidates.end() && setBlockIndexCandidates.value_comp()(*it, chainActive.Tip()))
+        setBlockIndexCandidates.erase(it++);
+}
+
+void Chainstate::InvalidChainFound(CBlockIndex* pindexNew) {
+    if (!pindexBestInvalid || pindexNew->nChainWork > pindexBestInvalid->nChainWork) pindexBestInvalid = pindexNew;
+    LogPrintf("InvalidChainFound: invalid block=%s height=%d\n", pindexNew->GetBlockHash().ToString().c_str(),
+              pindexNew->nHeight);
+}
+
+void Chainstate::InvalidBlockFound(CBlockIndex* pindex, const CValidationState& state) {
+    if (!state.CorruptionPossible()) {
+        pindex->nStatus |= BLOCK_FAILED_VALID;
+        setDirtyBlockIndex.insert(pindex);
+        setBlockIndexCandidates.erase(pindex);
+        InvalidChainFound(pindex);
+    }
+}
+
+bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pindexMostWork,
+                                       const std::shared_ptr<const CBlock>& pblock, bool& fInvalidFound,
+                                       ConnectTrace& trace) {
+    const CBlockIndex* pindexOldTip = chainActive.Tip();
+    const CBlockIndex* pindexFork = chainActive.FindFork(pindexMostWork);
+    bool fBlocksDisconnected = false;
+    while (chainActive.Tip() && chainActive.Tip() != pindexFork) {
+        if (!DisconnectTip(state)) return false;
+        fBlocksDisconnected = true;
+    }
+    std::vector<CBlockIndex*> vpindexToConnect;
+    bool fContinue = true;
+    int nHeight = pindexFork ? pindexFork->nHeight : -1;
+    while (fContinue && nHeight != pindexMostWork->nHeight) {
+        // connect in batches of 32 so the tip (and RPC) progresses during long reorgs / IBD
+        const int nTargetHeight = std::min(nHeight + 32, pindexMostWork->nHeight);
+        vpindexToConnect.clear();
+        CBlockIndex* pindexIter = pindexMostWork->GetAncestor(nTargetHeight);
+        while (pindexIter && pindexIter->nHeight != nHeight) {
+            vpindexToConnect.push_back(pindexIter);
+            pindexIter = pindexIter->pprev;
+        }
+        nHeight = nTargetHeight;
+        for (auto it = vpindexToConnect.rbegin(); it != vpindexToConnect.rend(); ++it) {
+            CBlockIndex* pindexConnect = *it;
+            if (!ConnectTip(state, pindexConnect, pindexConnect == pindexMostWork ? pblock : std::shared_ptr<const CBlock>(),
+                            trace)) {
+                if (state.IsInvalid()) {
+                    if (!state.CorruptionPossible()) InvalidChainFound(vpindexToConnect.front());
+                    state = CValidationState();
+                    fInvalidFound = true;
+                    fContinue = false;
+                    trace.blocksConnected.pop_back();
+                    break;
+                }
+                return false;
+            }
+            PruneBlockIndexCandidates();
+            if (!pindexOldTip || chainActive.Tip()->nChainWork > pindexOldTip->nChainWork) {
+                fContinue = false;
+                break;
+            }
+        }
+    }
+    if (fBlocksDisconnected && mempool) {
+        const int nMemHeight = chainActive.Tip()->nHeight + 1;
+        mempool->removeForReorg(
+            pcoinsTip.get(), (unsigned)nMemHeight, STANDARD_LOCKTIME_VERIFY_FLAGS,
+            [&](const CTransaction& tx, LockPoints& lp, bool validLP) {
+                CValidationState st;
+                if (!ContextualCheckTransactionForCurrentBlock(tx, st, STANDARD_LOCKTIME_VERIFY_FLAGS)) return false;
+                return CheckSequenceLocks(tx, STANDARD_LOCKTIME_VERIFY_FLAGS, &lp, validLP);
+            },
+            [&](const LockPoints* lp) { return TestLockPointValidity(lp); });
+        LimitMempoolSize(gArgs.GetArg("-maxmempool", (int64_t)DEFAULT_MAX_MEMPOOL_SIZE) * 1000000,
+                         gArgs.GetArg("-mempoolexpiry", (int64_t)DEFAULT_MEMPOOL_EXPIRY) * 60 * 60);
+    }
+    if (mempool) mempool->check(pcoinsTip.get(), chainActive.Height() + 1);
+    return true;
+}
+
+bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<const CBlock> pblock) {
+    CBlockIndex* pindexMostWork = nullptr;
+    CBlockIndex* pindexNewTip = nullptr;
+    do {
+        const CBlockIndex* pindexFork;
+        bool fInitialDownload;
+        ConnectTrace trace;
+        {
+            std::lock_guard<std::recursive_mutex> l(cs_main);
+            CBlockIndex* pindexOldTip = chainActive.Tip();
+            if (pindexMostWork == nullptr) pindexMostWork = FindMostWorkChain();
+            if (pindexMostWork == nullptr || pindexMostWork == chainActive.Tip()) return true;
+            bool fInvalidFound = false;
+            std::shared_ptr<const CBlock> nullBlockPtr;
+            if (!ActivateBestChainStep(state, pindexMostWork,
+                                       pblock && pblock->GetHash(params.GetConsensus()) == pindexMostWork->GetBlockHash()
+                                           ? pblock
+                                           : nullBlockPtr,
+                                       fInvalidFound, trace))
+                return false;
+            if (fInvalidFound) pindexMostWork = nullptr;
+            pindexNewTip = chainActive.Tip();
+            pindexFork = chainActive.FindFork(pindexOldTip);
+            fInitialDownload = IsInitialBlockDownload();
+            for (const auto& pb : trace.blocksConnected) {
+                std::vector<CTransactionRef> conflicted;
+                GetMainSignals().BlockConnected(pb.second, pb.first, conflicted);
+            }
+        }
+        if (pindexFork != pindexNewTip) GetMainSignals().UpdatedBlockTip(pindexNewTip, pindexFork, fInitialDownload);
+    } while (pindexNewTip != pindexMostWork);
+    CheckBlockIndex();
+    if (!FlushStateToDisk(state, FLUSH_STATE_PERIODIC)) return false;
+    return true;
+}
+
+bool Chainstate::PreciousBlock(CValidationState& state, CBlockIndex* pindex) {
+    {
+        std::lock_guard<std::recursive_mutex> l(cs_main);
+        if (pindex->nChainWork < chainActive.Tip()->nChainWork) return true;
+        if (chainActive.Tip()->nChainWork > nLastPreciousChainwork) nBlockReverseSequenceId = -1;
+        nLastPreciousChainwork = chainActive.Tip()->nChainWork;
+        setBlockIndexCandidates.erase(pindex);
+        pindex->nSequenceId = nBlockReverseSequenceId;
+        if (nBlockReverseSequenceId > std::numeric_limits<int32_t>::min()) nBlockReverseSequenceId--;
+        if (pindex->IsValid(BLOCK_VALID_TRANSACTIONS) && pindex->nChainTx) {
+            setBlockIndexCandidates.insert(pindex);
+            PruneBlockIndexCandidates();
+        }
+    }
+    return ActivateBestChain(state);
+}
+
+bool Chainstate::InvalidateBlock(CValidationState& state, CBlockIndex* pindex) {
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    pindex->nStatus |= BLOCK_FAILED_VALID;
+    setDirtyBlockIndex.insert(pindex);
+    setBlockIndexCandidates.erase(pindex);
+    while (chainActive.Contains(pindex)) {
+        CBlockIndex* pindexWalk = chainActive.Tip();
+        pindexWalk->nStatus |= BLOCK_FAILED_CHILD;
+        setDirtyBlockIndex.insert(pindexWalk);
+        setBlockIndexCandidates.erase(pindexWalk);
+        if (!DisconnectTip(state)) {
+            if (mempool)
+                mempool->removeForReorg(
+                    pcoinsTip.get(), (unsigned)chainActive.Tip()->nHeight + 1, STANDARD_LOCKTIME_VERIFY_FLAGS,
+                    [&](const CTransaction& tx, LockPoints& lp, bool validLP) {
+                        CValidationState st;
+                        if (!ContextualCheckTransactionForCurrentBlock(tx, st, STANDARD_LOCKTIME_VERIFY_FLAGS)) return false;
+                        return CheckSequenceLocks(tx, STANDARD_LOCKTIME_VERIFY_FLAGS, &lp, validLP);
+                    },
+                    [&](const LockPoints* lp) { return TestLockPointValidity(lp); });
+            return false;
+        }
+    }
+    LimitMempoolSize(gArgs.GetArg("-maxmempool", (int64_t)DEFAULT_MAX_MEMPOOL_SIZE) * 1000000,
+                     gArgs.GetArg("-mempoolexpiry", (int64_t)DEFAULT_MEMPOOL_EXPIRY) * 60 * 60);
+    // the chain tip may now be worse than other candidates: re-add everything better
+    for (const auto& kv : mapBlockIndex) {
+        CBlockIndex* p = kv.second;
+        if (p->IsValid(BLOCK_VALID_TRANSACTIONS) && p->nChainTx && !setBlockIndexCandidates.value_comp()(p, chainActive.Tip()))
+            setBlockIndexCandidates.insert(p);
+    }
+    InvalidChainFound(pindex);
+    if (mempool)
+        mempool->removeForReorg(
+            pcoinsTip.get(), (unsigned)chainActive.Tip()->nHeight + 1, STANDARD_LOCKTIME_VERIFY_FLAGS,
+            [&](const CTransaction& tx, LockPoints& lp, bool validLP) {
+                CValidationState st;
+                if (!ContextualCheckTransactionForCurrentBlock(tx, st, STANDARD_LOCKTIME_VERIFY_FLAGS)) return false;
+                return CheckSequenceLocks(tx, STANDARD_LOCKTIME_VERIFY_FLAGS, &lp, validLP);
+            },
+            [&](const LockPoints* lp) { return TestLockPointValidity(lp); });
+    return true;
+}
+
+bool Chainstate::ResetBlockFailureFlags(CBlockIndex* pindex) {
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    const int nHeight = pindex->nHeight;
+    for (const auto& kv : mapBlockIndex) {
+        CBlockIndex* it = kv.second;
+        if (!it->IsValid() && it->GetAncestor(nHeight) == pindex) {
+            it->nStatus &= ~BLOCK_FAILED_MASK;
+            setDirtyBlockIndex.insert(it);
+            if (it->IsValid(BLOCK_VALID_TRANSACTIONS) && it->nChainTx &&
+                setBlockIndexCandidates.value_comp()(chainActive.Tip(), it))
+                setBlockIndexCandidates.insert(it);
+            if (it == pindexBestInvalid) pindexBestInvalid = nullptr;
+        }
+    }
+    while (pindex != nullptr) {
+        if (pindex->nStatus & BLOCK_FAILED_MASK) {
+            pindex->nStatus &= ~BLOCK_FAILED_MASK;
+            setDirtyBlockIndex.insert(pindex);
+        }
+        pindex = pindex->pprev;
+    }
+    return true;
+}
+
+// ------------------------------------------------------------------ queries
+bool Chainstate::IsInitialBlockDownload() const {
+    if (latchToFalse.load(std::memory_order_relaxed)) return false;
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    if (latchToFalse.load(std::memory_order_relaxed)) return false;
+    if (fReindex) return true;
+    if (chainActive.Tip() == nullptr) return true;
+    if (chainActive.Tip()->nChainWork < UintToArith256(params.GetConsensus().nMinimumChainWork)) return true;
+    if (chainActive.Tip()->GetBlockTime() < (GetTime() - opts.maxTipAge)) return true;
+    latchToFalse.store(true, std::memory_order_relaxed);
+    return false;
+}
+
+CBlockIndex* Chainstate::FindForkInGlobalIndex(const CBlockLocator& locator) const {
+    for (const uint256& hash : locator.vHave) {
+        CBlockIndex* pindex = LookupBlockIndex(hash);
+        if (pindex) {
+            if (chainActive.Contains(pindex)) return pindex;
+            if (pindex->GetAncestor(chainActive.Height()) == chainActive.Tip()) return chainActive.Tip();
+        }
+    }
+    return chainActive.Genesis();
+}
+
+std::vector<const CBlockIndex*> Chainstate::GetChainTips() const {
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::set<const CBlockIndex*> setOrphans, setPrevs;
+    for (const auto& kv : mapBlockIndex) {
+        if (!chainActive.Contains(kv.second)) {
+            setOrphans.insert(kv.second);
+            setPrevs.insert(kv.second->pprev);
+        }
+    }
+    std::vector<const CBlockIndex*> tips;
+    for (const CBlockIndex* p : setOrphans)
+        if (setPrevs.erase(p) == 0) tips.push_back(p);
+    tips.push_back(chainActive.Tip());
+    std::sort(tips.begin(), tips.end(), [](const CBlockIndex* a, const CBlockIndex* b) { return a->nHeight > b->nHeight; });
+    return tips;
+}
+
+double Chainstate::GuessVerificationProgress(const CBlockIndex* pindex) const {
+    if (pindex == nullptr) return 0.0;
+    const ChainTxData& data = params.TxData();
+    const int64_t nNow = time(nullptr);
+    double fTxTotal;
+    if (pindex->nChainTx <= (unsigned)data.nTxCount) fTxTotal = (double)data.nTxCount + (nNow - data.nTime) * data.dTxRate;
+    else fTxTotal = pindex->nChainTx + (nNow - pindex->GetBlockTime()) * data.dTxRate;
+    return fTxTotal > 0 ? std::min(1.0, pindex->nChainTx / fTxTotal) : 1.0;
+}
+
+ThresholdState Chainstate::DeploymentState(const CBlockIndex* pindexPrev, Consensus::DeploymentPos pos) {
+    return VersionBitsState(pindexPrev, params.GetConsensus(), pos, versionbitscache);
+}
+int32_t Chainstate::ComputeBlockVersion(const CBlockIndex* pindexPrev) {
+    return bcp::ComputeBlockVersion(pindexPrev, params.GetConsensus(), versionbitscache);
+}
+
+void Chainstate::WaitForBlockChange(int64_t timeoutMillis, const uint256& from) {
+    std::unique_lock<std::recursive_mutex> l(cs_main);
+    auto pred = [&] { return chainActive.Tip() && chainActive.Tip()->GetBlockHash() != from; };
+    if (timeoutMillis <= 0) cvBlockChange.wait(l, pred);
+    else cvBlockChange.wait_for(l, std::chrono::milliseconds(timeoutMillis), pred);
+}
+
+bool Chainstate::GetTransaction(const uint256& txid, CTransactionRef& txOut, uint256& hashBlock, bool fAllowSlow) {
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    if (mempool) {
+        CTransactionRef ptx = mempool->get(txid);
+        if (ptx) {
+            txOut = ptx;
+            return true;
+        }
+    }
+    if (opts.txindex) {
+        CDiskTxPos postx;
+        if (pblocktree->ReadTxIndex(txid, postx)) {
+            CBlock block;
+            CBlockIndex* found = nullptr;
+            // locate the block by position
+            for (const auto& kv : mapBlockIndex)
+                if ((kv.second->nStatus & BLOCK_HAVE_DATA) && kv.second->nFile == postx.nFile &&
+                    kv.second->nDataPos == postx.nPos) {
+                    found = kv.second;
+                    break;
+                }
+            if (found && ReadBlockFromDisk(block, found, params, false)) {
+                for (const auto& tx : block.vtx)
+                    if (tx->GetHash() == txid) {
+                        txOut = tx;
+                        hashBlock = found->GetBlockHash();
+                        return true;
+                    }
+            }
+        }
+    }
+    if (fAllowSlow) {
+        const Coin& coin = AccessByTxid(*pcoinsTip, txid);
+        CBlockIndex* pindexSlow = coin.IsSpent() ? nullptr : chainActive[coin.GetHeight()];
+        if (pindexSlow) {
+            CBlock block;
+            if (ReadBlockFromDisk(block, pindexSlow, params, false)) {
+                for (const auto& tx : block.vtx)
+                    if (tx->GetHash() == txid) {
+                        txOut = tx;
+                        hashBlock = pindexSlow->GetBlockHash();
+                        return true;
+                    }
+            }
+        }
+    }
+    return false;
+}
+
+// ------------------------------------------------------------------ consistency checks
+void Chainstate::CheckBlockIndex() {
+    if (!opts.checkBlockIndex) return;
+    std::lock_guard<std::recursive_mutex> l(cs_main);
+    if (chainActive.Height() < 0) return;
+    size_t nNodes = 0;
+    for (const auto& kv : mapBlockIndex) {
+        const CBlockIndex* p = kv.second;
+        nNodes++;
+        if (p->pprev == nullptr) {
+            if (p->GetBlockHash() != params.GetConsensus().hashGenesisBlock)
+                throw std::logic_error("CheckBlockIndex: orphan index entry " + p->GetBlockHash().ToString());
+            continue;
+        }
+        if (p->nHeight != p->pprev->nHeight + 1) throw std::logic_error("CheckBlockIndex: height mismatch");
+        if (p->nChainWork < p->pprev->nChainWork) throw std::logic_error("CheckBlockIndex: chainwork decreases");
+        if (p->nTx > 0 && p->pprev->nChainTx > 0 && p->nChainTx != 0 && p->nChainTx != p->pprev->nChainTx + p->nTx)
+            throw std::logic_error("CheckBlockIndex: nChainTx inconsistent");
+        if ((p->nStatus & BLOCK_FAILED_MASK) == 0 && (p->pprev->nStatus & BLOCK_FAILED_MASK) != 0 &&
+            chainActive.Contains(p))
+            throw std::logic_error("CheckBlockIndex: valid child of invalid parent in active chain");
+        if (p->pskip && p->pskip->nHeight >= p->nHeight) throw std::logic_error("CheckBlockIndex: bad skip");
+    }
+    for (const CBlockIndex* c : setBlockIndexCandidates)
+        if (!c->IsValid(BLOCK_VALID_TRANSACTIONS) || !c->nChainTx)
+            throw std::logic_error("CheckBlockIndex: candidate without data");
+    (void)nNodes;
+}
+
+} // namespace bcp

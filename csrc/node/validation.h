@@ -1,0 +1,280 @@
+// Chainstate engine: block index, header/block acceptance, connect/disconnect with
+// undo, best-chain activation and reorgs, flushing, mempool acceptance.
+//
+// Parity map (reference src/validation.cpp):
+//   CheckBlockHeader :3202 (Equihash at header nHeight >= BCPHeight, PoW vs PowLimit(postfork))
+//   CheckBlock :3222, ContextualCheckBlockHeader :3362 (bad-diffbits, bad-height, time rules,
+//   bad-version), ContextualCheckTransaction :3413 (anti-replay commitment until sunset),
+//   ContextualCheckBlock :3474 (BIP34 coinbase height), AcceptBlockHeader :3519,
+//   AcceptBlock :3615, ProcessNewBlock :3736, ProcessNewBlockHeaders :3590,
+//   TestBlockValidity :3774, GetBlockScriptFlags :1803 (FORKID always, STRICTENC|LOW_S|NULLFAIL
+//   post-fork, ALLOW_NON_FORKID pre-fork), ConnectBlock :1868 (script failures ignored before
+//   the fork, :2124), DisconnectBlock/ApplyBlockUndo :1634-1714, FlushStateToDisk :2196,
+//   UpdateTip :2348, DisconnectTip :2435, ConnectTip :2525, FindMostWorkChain :2598,
+//   ActivateBestChainStep :2678, ActivateBestChain :2793, PreciousBlock :2889,
+//   InvalidateBlock :2919, ResetBlockFailureFlags :2967, AddToBlockIndex :3005,
+//   ReceivedBlockTransactions :3049, FindBlockPos :3104, LoadBlockIndexDB :4033,
+//   VerifyDB :4167, RewindBlockIndex :4324, InitBlockIndex :4412, LoadExternalBlockFile :4461,
+//   CheckBlockIndex :4618, AcceptToMemoryPoolWorker :666, LoadMempool/DumpMempool :4948-5070,
+//   GuessVerificationProgress :5073, IsInitialBlockDownload :1180.
+//
+// MI355X design: ConnectBlock evaluates all input scripts on the CPU worker pool with a
+// DeferringSignatureChecker, then verifies the collected ECDSA checks in one batch on the
+// GPU (csrc/kernels/secp256k1.hip) when the batch is large enough. Headers arriving in
+// bulk (ProcessNewBlockHeaders) have their Equihash solutions verified as one GPU batch.
+#pragma once
+#include "consensus/chain.h"
+#include "consensus/params.h"
+#include "consensus/tx_verify.h"
+#include "consensus/validation_state.h"
+#include "consensus/versionbits.h"
+#include "node/coins.h"
+#include "node/txdb.h"
+#include "util/util.h"
+
+#include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <set>
+#include <string>
+
+namespace bcp {
+
+class CTxMemPool;
+struct LockPoints;
+
+static const int64_t DEFAULT_MAX_TIP_AGE = 24 * 60 * 60;
+static const unsigned int MIN_BLOCKS_TO_KEEP = 288;
+static const int DEFAULT_CHECKBLOCKS = 6;
+static const unsigned int DEFAULT_CHECKLEVEL = 3;
+static const uint64_t MIN_DISK_SPACE_FOR_BLOCK_FILES = 550 * 1024 * 1024;
+static const int MAX_SCRIPTCHECK_THREADS = 64;
+static const unsigned int DATABASE_WRITE_INTERVAL = 60 * 60;
+static const unsigned int DATABASE_FLUSH_INTERVAL = 24 * 60 * 60;
+static const uint64_t MIN_TRANSACTION_SIZE = 10; // smallest serialisable tx with one in/out: guards vtx count
+static const unsigned int DEFAULT_ANCESTOR_LIMIT = 25;
+static const unsigned int DEFAULT_ANCESTOR_SIZE_LIMIT = 101;
+static const unsigned int DEFAULT_DESCENDANT_LIMIT = 25;
+static const unsigned int DEFAULT_DESCENDANT_SIZE_LIMIT = 101;
+static const unsigned int DEFAULT_MEMPOOL_EXPIRY = 336;
+static const Amount DEFAULT_MIN_RELAY_TX_FEE = 1000; // per kB
+static const Amount DEFAULT_TRANSACTION_MAXFEE = COIN / 10;
+
+enum FlushStateMode { FLUSH_STATE_NONE, FLUSH_STATE_IF_NEEDED, FLUSH_STATE_PERIODIC, FLUSH_STATE_ALWAYS };
+enum DisconnectResult { DISCONNECT_OK, DISCONNECT_UNCLEAN, DISCONNECT_FAILED };
+
+struct ChainstateOptions {
+    std::string datadir;            // <datadir> (net specific); blocks/ chainstate/ blocks/index/
+    bool memoryOnly = false;        // in-memory databases (tests)
+    bool wipe = false;              // -reindex / fresh start
+    size_t coinsCacheBytes = 450u << 20;
+    bool txindex = false;
+    int scriptThreads = 0;          // <= 0: auto (cores)
+    bool useGpu = true;             // batch ECDSA + header Equihash verification on the GPU
+    bool checkBlockIndex = false;   // -checkblockindex (expensive consistency checks)
+    bool checkpoints = true;
+    uint64_t maxBlockSize = DEFAULT_MAX_BLOCK_SIZE;
+    uint64_t pruneTarget = 0;       // bytes; 0 = no pruning
+    uint256 assumeValid;
+    int64_t maxTipAge = DEFAULT_MAX_TIP_AGE;
+};
+
+// Mempool acceptance outcome.
+struct MempoolAcceptResult {
+    bool accepted = false;
+    bool missingInputs = false;
+    Amount fee = 0;
+};
+
+class Chainstate {
+public:
+    Chainstate(const CChainParams& params, const ChainstateOptions& opts);
+    ~Chainstate();
+    Chainstate(const Chainstate&) = delete;
+
+    // ---- lifecycle
+    bool LoadBlockIndex(std::string& err);  // block tree + chain tip from disk
+    bool InitBlockIndex(std::string& err);  // genesis when empty
+    bool ReplayBlocks(std::string& err);    // recover from an interrupted UTXO flush
+    bool RewindBlockIndex();                // drop blocks validated without the current rules
+    bool VerifyDB(int nCheckLevel, int nCheckDepth);
+    bool LoadExternalBlockFile(FILE* fileIn, CDiskBlockPos* dbp = nullptr);
+    bool Reindex();                         // re-import all blk*.dat files
+    void Shutdown();                        // final flush
+
+    // ---- block processing
+    bool ProcessNewBlock(const std::shared_ptr<const CBlock>& block, bool fForceProcessing, bool* fNewBlock,
+                         CValidationState* stateOut = nullptr);
+    bool ProcessNewBlockHeaders(const std::vector<CBlockHeader>& headers, CValidationState& state,
+                                const CBlockIndex** ppindex = nullptr);
+    bool ActivateBestChain(CValidationState& state, std::shared_ptr<const CBlock> pblock = nullptr);
+    bool TestBlockValidity(CValidationState& state, const CBlock& block, CBlockIndex* pindexPrev, bool fCheckPOW,
+                           bool fCheckMerkleRoot);
+    bool InvalidateBlock(CValidationState& state, CBlockIndex* pindex);
+    bool ResetBlockFailureFlags(CBlockIndex* pindex);
+    bool PreciousBlock(CValidationState& state, CBlockIndex* pindex);
+    bool FlushStateToDisk(CValidationState& state, FlushStateMode mode, int nManualPruneHeight = 0);
+    void FlushStateToDisk();
+    void PruneBlockFilesManual(int nManualPruneHeight);
+
+    // context-free / contextual checks (also used by the miner and RPC)
+    bool CheckBlockHeader(const CBlockHeader& block, CValidationState& state, bool fCheckPOW = true) const;
+    bool CheckBlock(const CBlock& block, CValidationState& state, bool fCheckPOW = true,
+                    bool fCheckMerkleRoot = true) const;
+    bool ContextualCheckBlockHeader(const CBlockHeader& block, CValidationState& state, const CBlockIndex* pindexPrev,
+                                    int64_t nAdjustedTime) const;
+    bool ContextualCheckTransaction(const CTransaction& tx, CValidationState& state, int nHeight,
+                                    int64_t nLockTimeCutoff) const;
+    bool ContextualCheckTransactionForCurrentBlock(const CTransaction& tx, CValidationState& state,
+                                                   int flags = -1) const;
+    bool ContextualCheckBlock(const CBlock& block, CValidationState& state, const CBlockIndex* pindexPrev) const;
+    uint32_t GetBlockScriptFlags(const CBlockIndex* pindex) const;
+    bool IsBCPEnabled(int nHeight) const { return nHeight >= params.GetConsensus().BCPHeight; }
+    bool IsBCPEnabled(const CBlockIndex* pindexPrev) const {
+        return pindexPrev != nullptr && IsBCPEnabled(pindexPrev->nHeight);
+    }
+
+    // ---- mempool
+    void SetMempool(CTxMemPool* pool) { mempool = pool; }
+    CTxMemPool* Mempool() const { return mempool; }
+    bool AcceptToMemoryPool(CValidationState& state, const CTransactionRef& tx, bool fLimitFree,
+                            bool* pfMissingInputs, bool fOverrideMempoolLimit = false, Amount nAbsurdFee = 0,
+                            int64_t nAcceptTime = 0, Amount* feeOut = nullptr);
+    bool CheckSequenceLocks(const CTransaction& tx, int flags, LockPoints* lp = nullptr,
+                            bool useExistingLockPoints = false);
+    bool TestLockPointValidity(const LockPoints* lp) const;
+    bool LoadMempool(const std::string& path);
+    bool DumpMempool(const std::string& path);
+    void LimitMempoolSize(size_t limit, unsigned long age);
+
+    // ---- queries
+    std::recursive_mutex& cs() const { return cs_main; }
+    const CChainParams& Params() const { return params; }
+    CChain& ActiveChain() { return chainActive; }
+    const CChain& ActiveChain() const { return chainActive; }
+    CBlockIndex* Tip() const { return chainActive.Tip(); }
+    int Height() const { return chainActive.Height(); }
+    CBlockIndex* BestHeader() const { return pindexBestHeader; }
+    CBlockIndex* LookupBlockIndex(const uint256& hash) const;
+    const BlockMap& BlockIndex() const { return mapBlockIndex; }
+    CCoinsViewCache& CoinsTip() { return *pcoinsTip; }
+    CCoinsViewDB& CoinsDB() { return *pcoinsdbview; }
+    CBlockTreeDB& BlockTree() { return *pblocktree; }
+    bool IsInitialBlockDownload() const;
+    bool ReadBlock(CBlock& block, const CBlockIndex* pindex, bool checkPow = true) const;
+    bool GetTransaction(const uint256& txid, CTransactionRef& txOut, uint256& hashBlock, bool fAllowSlow);
+    CBlockIndex* FindForkInGlobalIndex(const CBlockLocator& locator) const;
+    std::vector<const CBlockIndex*> GetChainTips() const;
+    double GuessVerificationProgress(const CBlockIndex* pindex) const;
+    ThresholdState DeploymentState(const CBlockIndex* pindexPrev, Consensus::DeploymentPos pos);
+    int32_t ComputeBlockVersion(const CBlockIndex* pindexPrev);
+    VersionBitsCache& VersionBits() { return versionbitscache; }
+    uint64_t MaxBlockSize() const { return opts.maxBlockSize; }
+    void SetMaxBlockSize(uint64_t n) { opts.maxBlockSize = n; }
+    bool TxIndexEnabled() const { return opts.txindex; }
+    bool PruneMode() const { return opts.pruneTarget > 0; }
+    bool HavePruned() const { return fHavePruned; }
+    uint64_t CalculateCurrentUsage() const;
+    WorkerPool& Pool() { return *pool; }
+    bool UseGpu() const { return opts.useGpu; }
+    void SetUseGpu(bool v) { opts.useGpu = v; }
+    const std::string& Warnings() const { return strMiscWarning; }
+    // block-change notification for RPC long-poll / waitfornewblock
+    void WaitForBlockChange(int64_t timeoutMillis, const uint256& from);
+    std::condition_variable_any& BlockChangeCV() { return cvBlockChange; }
+    int64_t LastBlockConnectMicros() const { return nLastConnectMicros; }
+
+private:
+    struct WorkComparator {
+        bool operator()(const CBlockIndex* a, const CBlockIndex* b) const;
+    };
+    struct ConnectTrace {
+        std::vector<std::pair<CBlockIndex*, std::shared_ptr<const CBlock>>> blocksConnected;
+    };
+
+    CBlockIndex* InsertBlockIndex(const uint256& hash);
+    CBlockIndex* AddToBlockIndex(const CBlockHeader& block);
+    bool AcceptBlockHeader(const CBlockHeader& block, CValidationState& state, CBlockIndex** ppindex,
+                           bool skipPow = false);
+    bool AcceptBlock(const std::shared_ptr<const CBlock>& pblock, CValidationState& state, CBlockIndex** ppindex,
+                     bool fRequested, const CDiskBlockPos* dbp, bool* fNewBlock);
+    bool ReceivedBlockTransactions(const CBlock& block, CValidationState& state, CBlockIndex* pindexNew,
+                                   const CDiskBlockPos& pos);
+    bool FindBlockPos(CValidationState& state, CDiskBlockPos& pos, unsigned nAddSize, unsigned nHeight,
+                      uint64_t nTime, bool fKnown = false);
+    bool FindUndoPos(CValidationState& state, int nFile, CDiskBlockPos& pos, unsigned nAddSize);
+    void FlushBlockFile(bool fFinalize = false);
+    bool ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
+                      bool fJustCheck = false);
+    DisconnectResult DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view);
+    bool DisconnectTip(CValidationState& state, bool fBare = false);
+    bool ConnectTip(CValidationState& state, CBlockIndex* pindexNew, const std::shared_ptr<const CBlock>& pblock,
+                    ConnectTrace& trace);
+    CBlockIndex* FindMostWorkChain();
+    void PruneBlockIndexCandidates();
+    bool ActivateBestChainStep(CValidationState& state, CBlockIndex* pindexMostWork,
+                               const std::shared_ptr<const CBlock>& pblock, bool& fInvalidFound, ConnectTrace& trace);
+    void UpdateTip(CBlockIndex* pindexNew);
+    void InvalidChainFound(CBlockIndex* pindexNew);
+    void InvalidBlockFound(CBlockIndex* pindex, const CValidationState& state);
+    void CheckBlockIndex();
+    bool LoadBlockIndexDB(std::string& err);
+    bool LoadChainTip();
+    void NotifyHeaderTip();
+    bool CheckIndexAgainstCheckpoint(const CBlockIndex* pindexPrev, CValidationState& state) const;
+    void FindFilesToPrune(std::set<int>& setFilesToPrune, uint64_t nPruneAfterHeight);
+    void FindFilesToPruneManual(std::set<int>& setFilesToPrune, int nManualPruneHeight);
+    void PruneOneBlockFile(int fileNumber);
+    void UnlinkPrunedFiles(const std::set<int>& setFilesToPrune);
+    bool CheckInputs(const CTransaction& tx, CValidationState& state, const CCoinsViewCache& inputs,
+                     bool fScriptChecks, uint32_t flags, bool cacheStore, const PrecomputedTransactionData& txdata);
+    bool AcceptToMemoryPoolWorker(CValidationState& state, const CTransactionRef& ptx, bool fLimitFree,
+                                  bool* pfMissingInputs, int64_t nAcceptTime, bool fOverrideMempoolLimit,
+                                  Amount nAbsurdFee, std::vector<COutPoint>& coins_to_uncache, Amount* feeOut);
+    void UpdateMempoolForReorg(const std::vector<CTransactionRef>& disconnected, bool fAddToMempool);
+
+    const CChainParams& params;
+    ChainstateOptions opts;
+    mutable std::recursive_mutex cs_main;
+    std::condition_variable_any cvBlockChange;
+
+    BlockMap mapBlockIndex;
+    std::vector<std::unique_ptr<CBlockIndex>> blockIndexStorage;
+    std::vector<std::unique_ptr<uint256>> hashStorage;
+    CChain chainActive;
+    CBlockIndex* pindexBestHeader = nullptr;
+    CBlockIndex* pindexBestInvalid = nullptr;
+    CBlockIndex* pindexBestForkTip = nullptr;
+    CBlockIndex* pindexBestForkBase = nullptr;
+    std::set<CBlockIndex*, WorkComparator> setBlockIndexCandidates;
+    std::multimap<CBlockIndex*, CBlockIndex*> mapBlocksUnlinked;
+    std::set<CBlockIndex*> setDirtyBlockIndex;
+    std::set<int> setDirtyFileInfo;
+    std::vector<CBlockFileInfo> vinfoBlockFile;
+    int nLastBlockFile = 0;
+    int32_t nBlockSequenceId = 1;
+    int32_t nBlockReverseSequenceId = -1;
+    arith_uint256 nLastPreciousChainwork = 0;
+    bool fHavePruned = false;
+    bool fCheckForPruning = false;
+    bool fReindex = false;
+    mutable std::atomic<bool> latchToFalse{false};
+    int64_t nLastWrite = 0, nLastFlush = 0, nLastSetChain = 0;
+    std::atomic<int64_t> nLastConnectMicros{0};
+    std::string strMiscWarning;
+
+    std::unique_ptr<CBlockTreeDB> pblocktree;
+    std::unique_ptr<CCoinsViewDB> pcoinsdbview;
+    std::unique_ptr<CCoinsViewCache> pcoinsTip;
+    std::unique_ptr<WorkerPool> pool;
+    VersionBitsCache versionbitscache;
+    CTxMemPool* mempool = nullptr;
+};
+
+// Process-wide node chainstate (RPC, P2P and the wallet reach it through here).
+Chainstate* GetChainstate();
+void SetChainstate(Chainstate* cs);
+
+std::string FormatStateMessage(const CValidationState& state);
+
+} // namespace bcp

@@ -2,6 +2,8 @@
 #include "consensus/equihash.h"
 #include "kernels/gpu_api.h"
 #include "python/bind.h"
+#include "node/sigverify.h"
+#include "secp256k1/secp256k1.h"
 
 namespace bcp {
 namespace py {
@@ -165,6 +167,42 @@ void bind_gpu(pyb::module_& m) {
             return gpu::Sha256dScanNonces(h.data(), t.data(), start, count, device);
         },
         pyb::arg("header80"), pyb::arg("target_le"), pyb::arg("start"), pyb::arg("count"), pyb::arg("device") = -1);
+
+    // ECDSA batch verification: items = [(pubkey, der_sig, msg32)], CPUsemantics = CPubKey::Verify.
+    m.def(
+        "ecdsa_verify_batch",
+        [](const std::vector<std::tuple<pyb::bytes, pyb::bytes, pyb::bytes>>& items, bool use_gpu, int threads) {
+            std::vector<DeferredSigCheck> checks(items.size());
+            for (size_t i = 0; i < items.size(); i++) {
+                checks[i].pubkey = to_vec(std::get<0>(items[i]));
+                checks[i].sig = to_vec(std::get<1>(items[i]));
+                auto m32 = to_vec(std::get<2>(items[i]));
+                if (m32.size() != 32) throw std::invalid_argument("msg32");
+                memcpy(checks[i].sighash.begin(), m32.data(), 32);
+            }
+            std::vector<uint8_t> res(checks.size());
+            double ms = 0;
+            {
+                pyb::gil_scoped_release nogil;
+                WorkerPool pool(std::max(1, threads));
+                const int64_t t0 = GetTimeMicros();
+                if (use_gpu) {
+                    std::vector<const DeferredSigCheck*> ptrs;
+                    for (auto& c : checks) ptrs.push_back(&c);
+                    res = GpuVerifyDeferred(ptrs, &pool);
+                } else {
+                    pool.ParallelFor(checks.size(), [&](size_t i) {
+                        const DeferredSigCheck& c = checks[i];
+                        res[i] = secp::VerifySignature(c.pubkey.data(), c.pubkey.size(), c.sig.data(), c.sig.size(),
+                                                       c.sighash.begin());
+                    }, 16);
+                }
+                ms = (GetTimeMicros() - t0) / 1000.0;
+            }
+            std::vector<bool> out(res.begin(), res.end());
+            return pyb::make_tuple(out, ms);
+        },
+        pyb::arg("items"), pyb::arg("use_gpu") = true, pyb::arg("threads") = 8);
 }
 
 } // namespace py

@@ -490,6 +490,11 @@ static void build_gen_table() {
     g_gen_table = t;
 }
 
+const std::vector<Ge>& generator_table() {
+    std::call_once(g_gen_once, build_gen_table);
+    return *g_gen_table;
+}
+
 void ecmult_gen(Gej& r, const Scalar& k) {
     std::call_once(g_gen_once, build_gen_table);
     r.inf = true;

@@ -70,7 +70,9 @@ void gej_add_ge(Gej& r, const Gej& a, const Ge& b);
 void gej_add(Gej& r, const Gej& a, const Gej& b);
 void ge_set_gej(Ge& r, const Gej& a);
 bool ge_is_valid(const Ge& a);
-void ecmult_gen(Gej& r, const Scalar& k);                                  // k*G
+void ecmult_gen(Gej& r, const Scalar& k);
+// Affine comb table, entry [i*256 + j] = j * 256^i * G (j = 0 is the point at infinity).
+const std::vector<Ge>& generator_table();                                  // k*G
 void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng);     // na*A + ng*G
 
 // ---- keys / serialization
