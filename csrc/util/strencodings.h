@@ -3,6 +3,7 @@
 #pragma once
 #include <cstdint>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace bcp {
@@ -11,6 +12,11 @@ bool IsHex(const std::string& str);
 bool IsHexNumber(const std::string& str);
 std::vector<unsigned char> ParseHex(const std::string& str);
 std::string HexStr(const unsigned char* b, const unsigned char* e);
+template <typename It, typename = decltype(*std::declval<It>())>
+std::string HexStr(It b, It e) {
+    if (b == e) return std::string();
+    return HexStr(&*b, &*b + (e - b));
+}
 template <typename T> std::string HexStr(const T& v) {
     return HexStr((const unsigned char*)v.data(), (const unsigned char*)v.data() + v.size());
 }
