@@ -1,0 +1,317 @@
+#include "node/init.h"
+#include "consensus/params.h"
+#include "kernels/gpu_api.h"
+#include "node/node.h"
+#include "node/policy.h"
+#include "node/sigverify.h"
+#include "rpc/httpserver.h"
+#include "rpc/server.h"
+#include "script/standard.h"
+#include "util/strencodings.h"
+#include "util/util.h"
+
+#include <csignal>
+#include <cstdio>
+#include <fcntl.h>
+#include <sys/file.h>
+#include <unistd.h>
+
+namespace bcp {
+
+// Subsystem hooks: strong definitions live in the net / wallet / zmq modules.
+__attribute__((weak)) bool StartNetwork(NodeContext&, std::string&) { return true; }
+__attribute__((weak)) void StopNetwork(NodeContext&) {}
+__attribute__((weak)) bool StartWallet(NodeContext&, std::string&) { return true; }
+__attribute__((weak)) void StopWallet(NodeContext&) {}
+__attribute__((weak)) bool StartZMQ(NodeContext&, std::string&) { return true; }
+__attribute__((weak)) void StopZMQ(NodeContext&) {}
+__attribute__((weak)) std::string NetHelp() { return ""; }
+__attribute__((weak)) std::string WalletHelp() { return ""; }
+
+std::string HelpMessage() {
+    std::string s = "Usage:\n  bcpd [options]                     Start Bitcoin Cash Plus Daemon (MI355X build)\n\nOptions:\n";
+    const std::pair<const char*, const char*> opts[] = {
+        {"-?", "Print this help message and exit"},
+        {"-version", "Print version and exit"},
+        {"-conf=<file>", "Specify configuration file (default: bitcoincashplus.conf)"},
+        {"-datadir=<dir>", "Specify data directory"},
+        {"-daemon", "Run in the background as a daemon and accept commands"},
+        {"-pid=<file>", "Specify pid file (default: bitcoincashplusd.pid)"},
+        {"-testnet", "Use the test chain"},
+        {"-regtest", "Enter regression test mode (Equihash 48,5; fork at height 3000)"},
+        {"-dbcache=<n>", "Set database cache size in megabytes (default: 450)"},
+        {"-par=<n>", "Number of script verification threads (0 = auto)"},
+        {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
+        {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 256)"},
+        {"-txindex", "Maintain a full transaction index (default: 0)"},
+        {"-prune=<n>", "Reduce storage by pruning old blocks (MiB target, >= 550)"},
+        {"-reindex", "Rebuild chain state and block index from the blk*.dat files on disk"},
+        {"-reindex-chainstate", "Rebuild chain state from the currently indexed blocks"},
+        {"-checkblocks=<n>", "How many blocks to check at startup (default: 6, 0 = all)"},
+        {"-checklevel=<n>", "How thorough the block verification of -checkblocks is (0-4, default: 3)"},
+        {"-maxmempool=<n>", "Keep the transaction memory pool below <n> megabytes (default: 300)"},
+        {"-mempoolexpiry=<n>", "Do not keep transactions in the mempool longer than <n> hours (default: 336)"},
+        {"-persistmempool", "Whether to save the mempool on shutdown and load on restart (default: 1)"},
+        {"-excessiveblocksize=<n>", "Do not accept blocks larger than this limit, in bytes (default: 8000000)"},
+        {"-blockmaxsize=<n>", "Set maximum block size in bytes for mining (default: 2000000)"},
+        {"-blockprioritypercentage=<n>", "Set maximum percentage of a block reserved to high-priority transactions (default: 5)"},
+        {"-blockmintxfee=<amt>", "Set lowest fee rate (BCP/kB) for transactions to be included in block creation"},
+        {"-minrelaytxfee=<amt>", "Fees (BCP/kB) smaller than this are considered zero fee for relaying (default: 0.00001)"},
+        {"-limitfreerelay=<n>", "Continuously rate-limit free transactions to <n>*1000 bytes per minute"},
+        {"-relaypriority", "Require high priority for relaying free or low-fee transactions (default: 1)"},
+        {"-datacarrier", "Relay and mine data carrier transactions (default: 1)"},
+        {"-datacarriersize=<n>", "Maximum size of data in data carrier transactions (default: 83)"},
+        {"-permitbaremultisig", "Relay non-P2SH multisig (default: 1)"},
+        {"-usecashaddr", "Use Cash Address for destination encoding (default: 1)"},
+        {"-server", "Accept command line and JSON-RPC commands (default: 1 for bcpd)"},
+        {"-rest", "Accept public REST requests (default: 0)"},
+        {"-rpcbind=<addr>[:port]", "Bind to given address to listen for JSON-RPC connections"},
+        {"-rpcport=<port>", "Listen for JSON-RPC connections on <port> (default: 8332 / testnet and regtest 18332)"},
+        {"-rpcallowip=<ip>", "Allow JSON-RPC connections from specified source (IP or subnet)"},
+        {"-rpcuser=<user>", "Username for JSON-RPC connections"},
+        {"-rpcpassword=<pw>", "Password for JSON-RPC connections"},
+        {"-rpcauth=<userpw>", "Username and hashed password for JSON-RPC connections (user:salt$hmac)"},
+        {"-rpcthreads=<n>", "Set the number of threads to service RPC calls (default: 4)"},
+        {"-rpcservertimeout=<n>", "Timeout during HTTP requests (default: 30)"},
+        {"-debug=<category>", "Output debugging information (net, mempool, http, bench, rpc, gpu, ...)"},
+        {"-printtoconsole", "Send trace/debug info to console instead of debug.log file"},
+        {"-shrinkdebugfile", "Shrink debug.log file on client startup (default: 1)"},
+        {"-checkblockindex", "Do a full consistency check of the block index (regtest default)"},
+        {"-checkmempool=<n>", "Run checks every <n> transactions"},
+        {"-blockversion=<n>", "Override block version to test forking scenarios (regtest)"},
+    };
+    for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);
+    s += NetHelp();
+    s += WalletHelp();
+    return s;
+}
+
+static int g_lockFd = -1;
+static bool LockDataDirectory(const std::string& datadir) {
+    const std::string path = datadir + "/.lock";
+    g_lockFd = open(path.c_str(), O_RDWR | O_CREAT, 0600);
+    if (g_lockFd < 0) return false;
+    return flock(g_lockFd, LOCK_EX | LOCK_NB) == 0;
+}
+
+static std::atomic<bool> g_signalled{false};
+static void HandleSIGTERM(int) {
+    g_signalled = true;
+}
+
+static bool ParseFeeArg(const char* name, CFeeRate& out) {
+    if (!gArgs.IsArgSet(name)) return true;
+    int64_t n = 0;
+    if (!ParseMoney(gArgs.GetArg(name, ""), n)) return false;
+    out = CFeeRate(n);
+    return true;
+}
+
+int AppMain(int argc, char* argv[]) {
+    gArgs.ParseParameters(argc, argv);
+    if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help")) {
+        printf("%s", HelpMessage().c_str());
+        return 0;
+    }
+    if (gArgs.IsArgSet("-version")) {
+        printf("%s version %s\n", CLIENT_NAME, FormatFullVersion().c_str());
+        return 0;
+    }
+    const std::string datadirBase = gArgs.GetArg("-datadir", GetDefaultDataDir());
+    if (!TryCreateDirectories(datadirBase)) {
+        fprintf(stderr, "Error: Specified data directory \"%s\" does not exist.\n", datadirBase.c_str());
+        return 1;
+    }
+    SetDataDir(datadirBase);
+    gArgs.ReadConfigFile(datadirBase + "/" + gArgs.GetArg("-conf", "bitcoincashplus.conf"));
+    std::string chain;
+    try {
+        chain = gArgs.GetChainName();
+    } catch (const std::exception& e) {
+        fprintf(stderr, "Error: %s\n", e.what());
+        return 1;
+    }
+    SelectParams(chain);
+    const std::string datadir = GetDataDir(true);
+    TryCreateDirectories(datadir);
+
+    // daemonize before any GPU/thread initialisation (fork without exec)
+    if (gArgs.GetBoolArg("-daemon", false)) {
+        fprintf(stdout, "Bitcoin Cash Plus server starting\n");
+        fflush(stdout);
+        const pid_t pid = fork();
+        if (pid < 0) {
+            fprintf(stderr, "Error: fork() returned %d errno %d\n", pid, errno);
+            return 1;
+        }
+        if (pid > 0) return 0;
+        setsid();
+    }
+    if (!LockDataDirectory(datadir)) {
+        fprintf(stderr, "Error: Cannot obtain a lock on data directory %s. Bitcoin Cash Plus is probably already running.\n",
+                datadir.c_str());
+        return 1;
+    }
+    const bool console = gArgs.GetBoolArg("-printtoconsole", false);
+    if (gArgs.GetBoolArg("-shrinkdebugfile", true) && !console) {
+        LogInit(datadir + "/debug.log", false);
+        ShrinkDebugFile();
+    }
+    LogInit(console ? "" : datadir + "/debug.log", console);
+    for (const std::string& c : gArgs.GetArgs("-debug"))
+        if (!LogEnableCategory(c)) LogPrintf("Unsupported logging category -debug=%s.\n", c.c_str());
+    for (const std::string& c : gArgs.GetArgs("-debugexclude")) LogDisableCategory(c);
+    LogPrintf("\n\n\n\n\n");
+    LogPrintf("%s version %s (MI355X)\n", CLIENT_NAME, FormatFullVersion().c_str());
+    LogPrintf("Using data directory %s\n", datadir.c_str());
+
+    {
+        const std::string pidfile = datadir + "/" + gArgs.GetArg("-pid", "bitcoincashplusd.pid");
+        if (FILE* f = fopen(pidfile.c_str(), "w")) {
+            fprintf(f, "%d\n", (int)getpid());
+            fclose(f);
+        }
+    }
+    signal(SIGTERM, HandleSIGTERM);
+    signal(SIGINT, HandleSIGTERM);
+    signal(SIGPIPE, SIG_IGN);
+
+    // ---- parameter interaction (policy globals)
+    const CChainParams& params = Params();
+        fIsBareMultisigStd = gArgs.GetBoolArg("-permitbaremultisig", DEFAULT_PERMIT_BAREMULTISIG);
+    fAcceptDatacarrier = gArgs.GetBoolArg("-datacarrier", DEFAULT_ACCEPT_DATACARRIER);
+    nMaxDatacarrierBytes = (unsigned)gArgs.GetArg("-datacarriersize", (int64_t)nMaxDatacarrierBytes);
+    nBytesPerSigOp = (unsigned)gArgs.GetArg("-bytespersigop", (int64_t)nBytesPerSigOp);
+    SetUseCashAddr(gArgs.GetBoolArg("-usecashaddr", true));
+    if (!ParseFeeArg("-minrelaytxfee", minRelayTxFee) || !ParseFeeArg("-dustrelayfee", dustRelayFee) ||
+        !ParseFeeArg("-incrementalrelayfee", incrementalRelayFee)) {
+        LogPrintf("Error: invalid fee amount argument\n");
+        return 1;
+    }
+    SetGpuSigThreshold((size_t)gArgs.GetArg("-gpusigthreshold", (int64_t)GetGpuSigThreshold()));
+    const bool useGpu = gArgs.GetBoolArg("-gpu", true) && gpu::GpuAvailable();
+    LogPrintf("GPU acceleration: %s\n", useGpu ? gpu::DeviceName(0).c_str() : "disabled");
+
+    // ---- RPC server starts in warmup so clients get RPC_IN_WARMUP while loading
+    RegisterAllRPCCommands(tableRPC);
+    std::unique_ptr<HTTPServer> http;
+    if (gArgs.GetBoolArg("-server", true)) {
+        HTTPServer::Options ho;
+        const int defaultPort = (int)gArgs.GetArg("-rpcport", (int64_t)params.GetRPCPort());
+        std::vector<std::string> binds = gArgs.GetArgs("-rpcbind");
+        if (binds.empty() || !gArgs.IsArgSet("-rpcallowip")) {
+            ho.bind.push_back({"127.0.0.1", defaultPort});
+            ho.bind.push_back({"::1", defaultPort});
+        } else {
+            for (const std::string& b : binds) {
+                const size_t colon = b.rfind(':');
+                if (colon != std::string::npos && b.find(':') == colon)
+                    ho.bind.push_back({b.substr(0, colon), atoi(b.substr(colon + 1).c_str())});
+                else
+                    ho.bind.push_back({b, defaultPort});
+            }
+        }
+        ho.allowSubnets = gArgs.GetArgs("-rpcallowip");
+        if (!ho.allowSubnets.empty()) {
+            ho.allowSubnets.push_back("127.0.0.1");
+            ho.allowSubnets.push_back("::1");
+        }
+        ho.threads = (int)gArgs.GetArg("-rpcthreads", (int64_t)4);
+        ho.timeoutSeconds = (int)gArgs.GetArg("-rpcservertimeout", (int64_t)30);
+        http.reset(new HTTPServer(ho));
+        std::string err;
+        if (!http->Start(err)) {
+            LogPrintf("Error: %s\n", err.c_str());
+            fprintf(stderr, "Error: %s\n", err.c_str());
+            return 1;
+        }
+        if (!StartHTTPRPC(*http, datadir, err)) {
+            fprintf(stderr, "Error: %s\n", err.c_str());
+            return 1;
+        }
+        if (gArgs.GetBoolArg("-rest", false)) StartREST(*http);
+    }
+
+    // ---- chainstate
+    SetRPCWarmupStatus("Loading block index...");
+    const bool reindex = gArgs.GetBoolArg("-reindex", false) || gArgs.GetBoolArg("-reindex-chainstate", false);
+    std::string err;
+    std::unique_ptr<NodeContext> node;
+    {
+        const bool wipe = reindex;
+        node = BuildNode(chain, datadir, false, wipe, useGpu);
+        SetNode(node.get());
+        node->scheduler.reset(new Scheduler());
+        if (reindex) {
+            SetRPCWarmupStatus("Reindexing blocks...");
+            if (!node->chainstate->Reindex()) {
+                LogPrintf("Error: reindex failed\n");
+                return 1;
+            }
+        } else {
+            if (!node->chainstate->LoadBlockIndex(err) || !node->chainstate->InitBlockIndex(err)) {
+                LogPrintf("Error: %s\n", err.c_str());
+                fprintf(stderr, "Error: %s\n", err.c_str());
+                return 1;
+            }
+        }
+        SetRPCWarmupStatus("Verifying blocks...");
+        if (!node->chainstate->RewindBlockIndex()) LogPrintf("Warning: RewindBlockIndex failed\n");
+        if (!node->chainstate->VerifyDB((int)gArgs.GetArg("-checklevel", (int64_t)DEFAULT_CHECKLEVEL),
+                                        (int)gArgs.GetArg("-checkblocks", (int64_t)DEFAULT_CHECKBLOCKS))) {
+            LogPrintf("Error: corrupted block database detected; restart with -reindex\n");
+            fprintf(stderr, "Error: Corrupted block database detected. Please restart with -reindex.\n");
+            return 1;
+        }
+    }
+    if (gArgs.GetBoolArg("-persistmempool", true)) {
+        SetRPCWarmupStatus("Loading mempool...");
+        node->chainstate->LoadMempool(datadir + "/mempool.dat");
+    }
+    SetRPCWarmupStatus("Loading wallet...");
+    if (!StartWallet(*node, err)) {
+        fprintf(stderr, "Error: %s\n", err.c_str());
+        return 1;
+    }
+    SetRPCWarmupStatus("Starting network threads...");
+    if (!StartNetwork(*node, err)) {
+        fprintf(stderr, "Error: %s\n", err.c_str());
+        return 1;
+    }
+    if (!StartZMQ(*node, err)) {
+        fprintf(stderr, "Error: %s\n", err.c_str());
+        return 1;
+    }
+    // periodic flush + mempool expiry
+    node->scheduler->ScheduleEvery(
+        [] {
+            if (Chainstate* cs = GetChainstate()) {
+                CValidationState st;
+                cs->FlushStateToDisk(st, FLUSH_STATE_PERIODIC);
+            }
+        },
+        60 * 1000);
+    SetRPCWarmupFinished();
+    LogPrintf("init message: Done loading\n");
+
+    while (!g_signalled.load() && !ShutdownRequested()) MilliSleep(200);
+
+    // ---- shutdown (reference init.cpp Shutdown(): RPC, network, wallet, mempool dump, flush)
+    LogPrintf("Shutdown: In progress...\n");
+    if (http) http->Stop();
+    StopHTTPRPC(datadir);
+    StopZMQ(*node);
+    StopNetwork(*node);
+    if (gArgs.GetBoolArg("-persistmempool", true)) node->chainstate->DumpMempool(datadir + "/mempool.dat");
+    StopWallet(*node);
+    if (node->scheduler) node->scheduler->Stop();
+    node->chainstate->Shutdown();
+    SetChainstate(nullptr);
+    SetNode(nullptr);
+    RemoveFile(datadir + "/" + gArgs.GetArg("-pid", "bitcoincashplusd.pid"));
+    LogPrintf("Shutdown: done\n");
+    LogShutdown();
+    return 0;
+}
+
+} // namespace bcp

@@ -7,19 +7,20 @@ static NodeContext* g_node = nullptr;
 NodeContext* GetNode() { return g_node; }
 void SetNode(NodeContext* n) { g_node = n; }
 
-std::unique_ptr<NodeContext> CreateNode(const std::string& chain, const std::string& datadir, bool memoryOnly,
-                                        bool useGpu, std::string& err) {
+std::unique_ptr<NodeContext> BuildNode(const std::string& chain, const std::string& datadir, bool memoryOnly,
+                                       bool wipe, bool useGpu) {
     SelectParams(chain);
     std::unique_ptr<NodeContext> node(new NodeContext());
     node->params = &Params();
     node->datadir = datadir;
     node->useGpu = useGpu;
-    fRequireStandard = node->params->RequireStandard();
+    fRequireStandard = !gArgs.GetBoolArg("-acceptnonstdtxn", !node->params->RequireStandard());
     node->estimator.reset(new CBlockPolicyEstimator());
     node->mempool.reset(new CTxMemPool(node->estimator.get()));
     ChainstateOptions o;
     o.datadir = datadir;
     o.memoryOnly = memoryOnly;
+    o.wipe = wipe;
     o.useGpu = useGpu;
     o.txindex = gArgs.GetBoolArg("-txindex", false);
     o.checkBlockIndex = gArgs.GetBoolArg("-checkblockindex", node->params->DefaultConsistencyChecks());
@@ -35,9 +36,17 @@ std::unique_ptr<NodeContext> CreateNode(const std::string& chain, const std::str
     node->chainstate.reset(new Chainstate(*node->params, o));
     node->chainstate->SetMempool(node->mempool.get());
     node->mempool->setSanityCheck(gArgs.GetArg("-checkmempool", node->params->DefaultConsistencyChecks() ? 1 : 0));
-    if (!node->chainstate->LoadBlockIndex(err)) return nullptr;
-    if (!node->chainstate->InitBlockIndex(err)) return nullptr;
     SetChainstate(node->chainstate.get());
+    return node;
+}
+
+std::unique_ptr<NodeContext> CreateNode(const std::string& chain, const std::string& datadir, bool memoryOnly,
+                                        bool useGpu, std::string& err) {
+    std::unique_ptr<NodeContext> node = BuildNode(chain, datadir, memoryOnly, false, useGpu);
+    if (!node->chainstate->LoadBlockIndex(err) || !node->chainstate->InitBlockIndex(err)) {
+        SetChainstate(nullptr);
+        return nullptr;
+    }
     return node;
 }
 

@@ -39,6 +39,10 @@ void SetNode(NodeContext* n);
 // the embedded-node path used by tests and tools.
 std::unique_ptr<NodeContext> CreateNode(const std::string& chain, const std::string& datadir, bool memoryOnly,
                                         bool useGpu, std::string& err);
+// Construct the subsystems without loading the block index (bcpd drives loading so it
+// can -reindex and report warmup progress).
+std::unique_ptr<NodeContext> BuildNode(const std::string& chain, const std::string& datadir, bool memoryOnly,
+                                       bool wipe, bool useGpu);
 void ShutdownNode(NodeContext& node);
 
 } // namespace bcp
