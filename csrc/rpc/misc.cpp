@@ -8,6 +8,7 @@
 #include "node/sigverify.h"
 #include "node/txmempool.h"
 #include "rpc/core_io.h"
+#include "net/net.h"
 #include "rpc/server.h"
 #include "script/sign.h"
 #include "script/standard.h"
@@ -62,7 +63,7 @@ static UniValue getinfo(const JSONRPCRequest& req) {
     if (g_walletGetInfo) g_walletGetInfo(obj);
     obj.pushKV("blocks", cs.Height());
     obj.pushKV("timeoffset", GetTimeOffset());
-    obj.pushKV("connections", 0);
+    obj.pushKV("connections", GetConnman() ? (int64_t)GetConnman()->GetNodeCount(CONNECTIONS_ALL) : (int64_t)0);
     obj.pushKV("proxy", "");
     obj.pushKV("difficulty", GetDifficulty(cs.Tip()));
     obj.pushKV("testnet", cs.Params().NetworkIDString() == "test");
