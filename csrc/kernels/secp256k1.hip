@@ -4,10 +4,13 @@
 // src/validation.cpp:1740 scriptcheckqueue) for block validation.
 //
 // Work split (see csrc/node/sigverify.cpp):
-//   host  : lax-DER parse, low-S normalisation, r,s range, batch inversion of s
-//           (Montgomery trick: 1 inversion + 3 muls per signature), u1 = z/s, u2 = r/s
-//   device: pubkey decompression (sqrt chain), R = u1*G + u2*Q, check x(R) == r (mod n)
-//           without any field inversion: X == r*Z^2  or  X == (r+n)*Z^2 when r+n < p.
+//   host  : lax-DER parse and low-S normalisation only (copies r, s, z, pubkey)
+//   device: ecdsa_prep_kernel  - r,s range checks, s^-1 mod n (Montgomery CIOS,
+//                                Fermat exponent n-2), u1 = z/s, u2 = r/s, width-4 wNAF
+//                                recoding of u2, r+n precompute
+//           ecdsa_verify_kernel - pubkey decompression (sqrt chain), R = u1*G + u2*Q,
+//                                check x(R) == r (mod n) without any field inversion:
+//                                X == r*Z^2  or  X == (r+n)*Z^2 when r+n < p.
 //
 // Field arithmetic: 8 x 32-bit limbs (one VGPR each), schoolbook products through
 // 32x32+64 -> 64 multiply-adds, reduction by 2^256 = 2^32 + 977 (mod p).
@@ -204,7 +207,7 @@ __device__ __forceinline__ bool fe_eq(const fe& a, const fe& b) {
 }
 
 // r = a^((p+1)/4); returns whether r^2 == a (libsecp256k1 addition chain).
-__device__ bool fe_sqrt(fe& r, const fe& a) {
+__device__ __forceinline__ bool fe_sqrt(fe& r, const fe& a) {
     fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t1;
     fe_sqr(x2, a);
     fe_mul(x2, x2, a);
@@ -274,7 +277,7 @@ __device__ __forceinline__ void gej_double(gej& r, const gej& p) {
 }
 
 // add-2007-bl, general Jacobian + Jacobian
-__device__ void gej_add(gej& r, const gej& a, const gej& b) {
+__device__ __forceinline__ void gej_add(gej& r, const gej& a, const gej& b) {
     if (a.inf) {
         r = b;
         return;
@@ -329,7 +332,7 @@ __device__ void gej_add(gej& r, const gej& a, const gej& b) {
 }
 
 // madd-2007-bl, Jacobian + affine
-__device__ void gej_add_ge(gej& r, const gej& a, const fe& bx, const fe& by) {
+__device__ __forceinline__ void gej_add_ge(gej& r, const gej& a, const fe& bx, const fe& by) {
     if (a.inf) {
         r.x = bx;
         r.y = by;
@@ -409,8 +412,10 @@ struct Job {
     unsigned char rplusn_ok;
     unsigned char wnaf[130]; // u2 as width-4 wNAF, 2 signed nibbles per byte, digit b at wnaf[b>>1]
     unsigned char nwnaf_lo, nwnaf_hi; // number of digits
-    unsigned char pad[10];
+    unsigned char scalar_ok;          // set by the prep kernel: r, s in [1, n-1]
+    unsigned char pad[9];
 };
+// Host-filled input to the prep kernel (u1 <- z, rn <- s before prep).
 static_assert(sizeof(Job) == 272, "job layout");
 
 __device__ __forceinline__ int wnaf_digit(const Job& J, int b) {
@@ -419,7 +424,189 @@ __device__ __forceinline__ int wnaf_digit(const Job& J, int b) {
     return nib >= 8 ? nib - 16 : nib;
 }
 
-__global__ __launch_bounds__(WG) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
+
+// ---------------------------------------------------------------- scalars mod n
+__device__ __constant__ uint32_t N_LIMBS[8] = {0xD0364141, 0xBFD25E8C, 0xAF48A03B, 0xBAAEDCE6,
+                                               0xFFFFFFFE, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF};
+__device__ __constant__ uint32_t N_R2[8] = {0x67D7D140, 0x896CF214, 0x0E7CF878, 0x741496C2,
+                                            0x5BCD07C6, 0xE697F5E4, 0x81C69BC5, 0x9D671CD5};
+__device__ __constant__ uint32_t N_ONE_M[8] = {0x2FC9BEBF, 0x402DA173, 0x50B75FC4, 0x45512319, 1, 0, 0, 0};
+__device__ __constant__ uint32_t N_MINUS_2[8] = {0xD036413F, 0xBFD25E8C, 0xAF48A03B, 0xBAAEDCE6,
+                                                 0xFFFFFFFE, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF};
+constexpr uint32_t N_INV32 = 0x5588B13F; // -n^-1 mod 2^32
+
+// a < n ?
+__device__ __forceinline__ bool sc_lt_n(const fe& a) {
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t d = (uint64_t)a.v[i] - N_LIMBS[i] - borrow;
+        borrow = (d >> 63) & 1;
+    }
+    return borrow != 0;
+}
+
+__device__ __forceinline__ void sc_sub_n(fe& a) {
+    uint64_t borrow = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t d = (uint64_t)a.v[i] - N_LIMBS[i] - borrow;
+        a.v[i] = (uint32_t)d;
+        borrow = (d >> 63) & 1;
+    }
+}
+
+// Montgomery product a*b/2^256 mod n (CIOS, 8 x 32-bit limbs).
+__device__ __forceinline__ void sc_mont_mul(fe& r, const fe& a, const fe& b) {
+    uint32_t t[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            c += (uint64_t)t[j] + (uint64_t)a.v[j] * b.v[i];
+            t[j] = (uint32_t)c;
+            c >>= 32;
+        }
+        uint64_t s2 = (uint64_t)t[8] + c;
+        t[8] = (uint32_t)s2;
+        t[9] = (uint32_t)(s2 >> 32);
+        const uint32_t m = t[0] * N_INV32;
+        c = ((uint64_t)t[0] + (uint64_t)m * N_LIMBS[0]) >> 32;
+#pragma unroll
+        for (int j = 1; j < 8; j++) {
+            c += (uint64_t)t[j] + (uint64_t)m * N_LIMBS[j];
+            t[j - 1] = (uint32_t)c;
+            c >>= 32;
+        }
+        s2 = (uint64_t)t[8] + c;
+        t[7] = (uint32_t)s2;
+        t[8] = t[9] + (uint32_t)(s2 >> 32);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.v[i] = t[i];
+    if (t[8] || !sc_lt_n(r)) sc_sub_n(r);
+}
+
+__device__ __forceinline__ void store_be32(unsigned char* b, const fe& a) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        unsigned char* q = b + 28 - 4 * i;
+        q[0] = (unsigned char)(a.v[i] >> 24);
+        q[1] = (unsigned char)(a.v[i] >> 16);
+        q[2] = (unsigned char)(a.v[i] >> 8);
+        q[3] = (unsigned char)a.v[i];
+    }
+}
+
+// One lane per signature: scalar checks, s^-1, u1, u2, wNAF(u2), r+n.
+__global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs, int n) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n) return;
+    Job& J = jobs[idx];
+    fe r, s, z;
+    load_be32(r, J.r);
+    load_be32(s, J.rn);
+    load_be32(z, J.u1);
+    const bool ok = sc_lt_n(r) && sc_lt_n(s) && !fe_is_zero(r) && !fe_is_zero(s);
+    if (!sc_lt_n(z)) sc_sub_n(z); // z < 2^256 < 2n
+    fe one;
+#pragma unroll
+    for (int i = 0; i < 8; i++) one.v[i] = i == 0 ? 1u : 0u;
+    if (!ok) s = one;
+    // s^(n-2) in the Montgomery domain, left-to-right binary over the constant exponent
+    fe r2, sm, acc;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        r2.v[i] = N_R2[i];
+        acc.v[i] = N_ONE_M[i];
+    }
+    sc_mont_mul(sm, s, r2);
+    for (int w = 7; w >= 0; w--) {
+        const uint32_t e = N_MINUS_2[w];
+        for (int b = 31; b >= 0; b--) {
+            sc_mont_mul(acc, acc, acc);
+            if ((e >> b) & 1) sc_mont_mul(acc, acc, sm);
+        }
+    }
+    // acc = s^-1 * R ; montmul with a plain value gives a plain product
+    fe u1, u2;
+    sc_mont_mul(u1, acc, z);
+    sc_mont_mul(u2, acc, r);
+    store_be32(J.u1, u1);
+    J.scalar_ok = ok ? 1 : 0;
+    // r + n (only meaningful when r + n < p)
+    // p - n = 0x14551231950b75fc4402da1722fc9baee
+    {
+        // r < p - n  <=>  r + n < p
+        const uint32_t pmn[8] = {0x2FC9BAEE, 0x402DA172, 0x50B75FC4, 0x45512319, 1, 0, 0, 0};
+        uint64_t borrow = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint64_t d = (uint64_t)r.v[i] - pmn[i] - borrow;
+            borrow = (d >> 63) & 1;
+        }
+        J.rplusn_ok = borrow ? 1 : 0;
+        fe rn;
+        uint64_t c = 0;
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            c += (uint64_t)r.v[i] + N_LIMBS[i];
+            rn.v[i] = (uint32_t)c;
+            c >>= 32;
+        }
+        store_be32(J.rn, rn);
+    }
+    // width-4 wNAF of u2, LSB first, two signed nibbles per byte
+    uint32_t k[9];
+#pragma unroll
+    for (int i = 0; i < 8; i++) k[i] = u2.v[i];
+    k[8] = 0;
+    int len = 0;
+    unsigned char cur = 0;
+    for (int b = 0; b < 258; b++) {
+        uint32_t nz = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) nz |= k[i];
+        if (!nz) {
+            if (b & 1) J.wnaf[b >> 1] = cur;
+            for (int q = (b + 1) >> 1; q < 130; q++) J.wnaf[q] = 0;
+            break;
+        }
+        int d = 0;
+        if (k[0] & 1) {
+            d = (int)(k[0] & 15);
+            if (d >= 8) d -= 16;
+            // k -= d (two's complement add of -d with sign extension)
+            const uint32_t addend = (uint32_t)(-d);
+            const uint32_t ext = d > 0 ? 0xFFFFFFFFu : 0u;
+            uint64_t c = 0;
+#pragma unroll
+            for (int i = 0; i < 9; i++) {
+                c += (uint64_t)k[i] + (i == 0 ? addend : ext);
+                k[i] = (uint32_t)c;
+                c >>= 32;
+            }
+            len = b + 1;
+        }
+        const unsigned char nib = (unsigned char)(d & 15);
+        if (b & 1) {
+            J.wnaf[b >> 1] = cur | (unsigned char)(nib << 4);
+            cur = 0;
+        } else {
+            cur = nib;
+        }
+#pragma unroll
+        for (int i = 0; i < 8; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
+        k[8] >>= 1;
+    }
+    J.nwnaf_lo = (unsigned char)(len & 0xff);
+    J.nwnaf_hi = (unsigned char)(len >> 8);
+}
+
+__global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
                                                           uint8_t* __restrict__ out, int n) {
     // word-major layout: lane-consecutive words -> conflict-free LDS access
     __shared__ uint32_t preX[NPRE][8][WG], preY[NPRE][8][WG], preZ[NPRE][8][WG];
@@ -529,7 +716,7 @@ __global__ __launch_bounds__(WG) void ecdsa_verify_kernel(const Job* __restrict_
             match = fe_eq(rz, acc.x);
         }
     }
-    out[idx] = (ok && match) ? 1 : 0;
+    out[idx] = (ok && match && J.scalar_ok) ? 1 : 0;
 }
 
 struct State {
@@ -544,49 +731,6 @@ struct State {
 State& S() {
     static State s;
     return s;
-}
-
-// Width-4 wNAF of a big-endian 256-bit scalar into signed nibbles; returns digit count.
-int WnafEncode(unsigned char* out, const unsigned char* be) {
-    uint32_t k[9];
-    for (int i = 0; i < 8; i++) {
-        const unsigned char* q = be + 28 - 4 * i;
-        k[i] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
-    }
-    k[8] = 0;
-    memset(out, 0, 130);
-    int len = 0;
-    for (int b = 0; b < 258; b++) {
-        bool nz = false;
-        for (int i = 0; i < 9; i++) nz |= k[i] != 0;
-        if (!nz) break;
-        int d = 0;
-        if (k[0] & 1) {
-            d = (int)(k[0] & 15);
-            if (d >= 8) d -= 16;
-            // k -= d
-            if (d > 0) {
-                uint64_t borrow = (uint64_t)d;
-                for (int i = 0; i < 9 && borrow; i++) {
-                    const uint64_t x = (uint64_t)k[i] - borrow;
-                    k[i] = (uint32_t)x;
-                    borrow = (x >> 63) & 1;
-                }
-            } else {
-                uint64_t carry = (uint64_t)(-d);
-                for (int i = 0; i < 9 && carry; i++) {
-                    carry += k[i];
-                    k[i] = (uint32_t)carry;
-                    carry >>= 32;
-                }
-            }
-        }
-        out[b >> 1] |= (unsigned char)((d & 15) << ((b & 1) * 4));
-        if (d) len = b + 1;
-        for (int i = 0; i < 8; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
-        k[8] >>= 1;
-    }
-    return len;
 }
 
 void InitTable() {
@@ -622,59 +766,15 @@ std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, c
     State& st = S();
     std::call_once(st.once, InitTable);
 
-    // host: batch inversion of s, u1 = z/s, u2 = r/s
-    std::vector<secp::Scalar> s(n), r(n), z(n), pref(n);
-    std::vector<uint8_t> hostOk(n, 1);
-    secp::Scalar accum;
-    secp::sc_set_b32(accum, (const unsigned char*)"\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\1");
-    for (size_t i = 0; i < n; i++) {
-        bool of1 = false, of2 = false;
-        secp::sc_set_b32(r[i], &sig64[i * 64], &of1);
-        secp::sc_set_b32(s[i], &sig64[i * 64 + 32], &of2);
-        secp::sc_set_b32(z[i], &msg32[i * 32]);
-        if (of1 || of2 || secp::sc_is_zero(r[i]) || secp::sc_is_zero(s[i])) {
-            hostOk[i] = 0;
-            secp::sc_set_b32(s[i], (const unsigned char*)"\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\0\1");
-        }
-        pref[i] = accum;
-        secp::sc_mul(accum, accum, s[i]);
-    }
-    secp::Scalar inv;
-    secp::sc_inv(inv, accum);
+    // host: copy r, s, z, pubkey; all scalar arithmetic runs in ecdsa_prep_kernel
     std::vector<Job> jobs(n);
-    for (size_t i = n; i-- > 0;) {
-        secp::Scalar sinv;
-        secp::sc_mul(sinv, inv, pref[i]); // 1/s_i
-        secp::sc_mul(inv, inv, s[i]);     // drop s_i from the running inverse
-        secp::Scalar u1, u2;
-        secp::sc_mul(u1, z[i], sinv);
-        secp::sc_mul(u2, r[i], sinv);
+    for (size_t i = 0; i < n; i++) {
         Job& J = jobs[i];
         memset(&J, 0, sizeof(J));
-        secp::sc_get_b32(J.u1, u1);
-        unsigned char u2b[32];
-        secp::sc_get_b32(u2b, u2);
-        const int len = WnafEncode(J.wnaf, u2b);
-        J.nwnaf_lo = (unsigned char)(len & 0xff);
-        J.nwnaf_hi = (unsigned char)(len >> 8);
+        memcpy(J.u1, &msg32[i * 32], 32);
         memcpy(J.r, &sig64[i * 64], 32);
+        memcpy(J.rn, &sig64[i * 64 + 32], 32);
         memcpy(J.pub, &pub33[i * 33], 33);
-        // r + n < p  <=>  r < p - n  (p - n = 0x14551231950b75fc4402da1722fc9baee)
-        static const unsigned char PMN[32] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1,
-                                              0x45, 0x51, 0x23, 0x19, 0x50, 0xb7, 0x5f, 0xc4,
-                                              0x40, 0x2d, 0xa1, 0x72, 0x2f, 0xc9, 0xba, 0xee};
-        if (memcmp(J.r, PMN, 32) < 0) {
-            J.rplusn_ok = 1;
-            static const unsigned char N[32] = {0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF, 0xFF,
-                                                0xFF, 0xFF, 0xFF, 0xFF, 0xFE, 0xBA, 0xAE, 0xDC, 0xE6, 0xAF, 0x48,
-                                                0xA0, 0x3B, 0xBF, 0xD2, 0x5E, 0x8C, 0xD0, 0x36, 0x41, 0x41};
-            unsigned c = 0;
-            for (int b = 31; b >= 0; b--) {
-                c += (unsigned)J.r[b] + N[b];
-                J.rn[b] = (unsigned char)c;
-                c >>= 8;
-            }
-        }
     }
 
     std::lock_guard<std::mutex> l(st.m);
@@ -686,12 +786,13 @@ std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, c
         BCP_HIP_CHECK(hipMalloc(&st.d_out, st.cap));
     }
     BCP_HIP_CHECK(hipMemcpyAsync(st.d_jobs, jobs.data(), n * sizeof(Job), hipMemcpyHostToDevice, st.stream));
+    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st.stream, st.d_jobs, (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
     const int grid = (int)((n + WG - 1) / WG);
     hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, st.stream, st.d_jobs, st.d_gtab, st.d_out, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
     BCP_HIP_CHECK(hipMemcpyAsync(result.data(), st.d_out, n, hipMemcpyDeviceToHost, st.stream));
     BCP_HIP_CHECK(hipStreamSynchronize(st.stream));
-    for (size_t i = 0; i < n; i++) result[i] &= hostOk[i];
     return result;
 }
 

@@ -16,7 +16,7 @@ for i in range(512):
     k = os.urandom(32)
     m = os.urandom(32)
     base.append((nat.ec_pubkey_create(k, True), nat.ec_sign(k, m), m))
-items = (base * (n // len(base) + 1))[:n]
+items = (base * (4 * n // len(base) + 1))[:4 * n]
 print(f"generated {len(base)} unique sigs in {time.time()-t:.1f}s", flush=True)
 out = {"n": n}
 r, ms = nat.ecdsa_verify_batch(items[:2000], use_gpu=False, threads=os.cpu_count() or 8)
@@ -24,7 +24,7 @@ out["cpu_sig_per_s"] = 2000 / ms * 1e3
 assert all(r)
 if b.gpu_available():
     nat.ecdsa_verify_batch(items[:256], use_gpu=True)  # warm-up (table upload, code load)
-    for size in (1024, 8192, n):
+    for size in (1024, 8192, n, 4 * n):
         r, ms = nat.ecdsa_verify_batch(items[:size], use_gpu=True)
         assert all(r), "GPU rejected a valid signature"
         out[f"gpu_sig_per_s_{size}"] = size / ms * 1e3
