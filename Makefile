@@ -64,7 +64,7 @@ $(PYEXT): $(PY_OBJS) $(CORELIB)
 
 bin/%: build/obj/tools/%.o $(CORELIB)
 	@mkdir -p bin
-	$(CXX) -o $@ $< -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS)
+	$(CXX) -rdynamic -o $@ $< -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS)
 
 build/obj/tools/%.o: csrc/tools/%.cpp
 	@mkdir -p $(dir $@)

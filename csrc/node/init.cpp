@@ -11,7 +11,9 @@
 #include "util/util.h"
 
 #include <csignal>
+#include <execinfo.h>
 #include <cstdio>
+#include <cstring>
 #include <fcntl.h>
 #include <sys/file.h>
 #include <unistd.h>
@@ -95,6 +97,20 @@ static bool LockDataDirectory(const std::string& datadir) {
 }
 
 static std::atomic<bool> g_signalled{false};
+
+// Fatal-signal reporter: symbolised backtrace to stderr (failure diagnostics; the
+// reference relies on core dumps).
+static void HandleFatalSignal(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char* name = sig == SIGSEGV ? "SIGSEGV" : sig == SIGABRT ? "SIGABRT" : sig == SIGBUS ? "SIGBUS" : "SIGFPE";
+    (void)!write(2, "\n*** fatal signal ", 18);
+    (void)!write(2, name, strlen(name));
+    (void)!write(2, " ***\n", 5);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
 static void HandleSIGTERM(int) {
     g_signalled = true;
 }
@@ -175,6 +191,18 @@ int AppMain(int argc, char* argv[]) {
     signal(SIGTERM, HandleSIGTERM);
     signal(SIGINT, HandleSIGTERM);
     signal(SIGPIPE, SIG_IGN);
+    if (!getenv("BCP_NO_CRASH_HANDLER")) {
+        // alternate stack so a stack overflow can still be reported
+        static std::vector<char> altstack(1 << 16);
+        stack_t ss = {};
+        ss.ss_sp = altstack.data();
+        ss.ss_size = altstack.size();
+        sigaltstack(&ss, nullptr);
+        struct sigaction sa = {};
+        sa.sa_handler = HandleFatalSignal;
+        sa.sa_flags = SA_ONSTACK;
+        for (int sig : {SIGSEGV, SIGABRT, SIGBUS, SIGFPE}) sigaction(sig, &sa, nullptr);
+    }
 
     // ---- parameter interaction (policy globals)
     const CChainParams& params = Params();

@@ -15,7 +15,8 @@ std::string HexStr(const unsigned char* b, const unsigned char* e);
 template <typename It, typename = decltype(*std::declval<It>())>
 std::string HexStr(It b, It e) {
     if (b == e) return std::string();
-    return HexStr(&*b, &*b + (e - b));
+    const unsigned char* p = (const unsigned char*)&*b;
+    return HexStr(p, p + (e - b));
 }
 template <typename T> std::string HexStr(const T& v) {
     return HexStr((const unsigned char*)v.data(), (const unsigned char*)v.data() + v.size());

@@ -1,0 +1,193 @@
+// Wallet start/stop for bcpd (reference src/wallet/wallet.cpp CWallet::CreateWalletFromFile
+// and InitLoadWallet: first-run HD seed + default key, keypool top-up, rescan from the
+// stored best-block locator (or genesis with -rescan), -zapwallettxes, -walletbroadcast,
+// -paytxfee/-txconfirmtarget; and the wallet hooks used by generate/getinfo/validateaddress).
+#include "node/node.h"
+#include "node/txmempool.h"
+#include "node/validation.h"
+#include "rpc/server.h"
+#include "util/strencodings.h"
+#include "wallet/wallet.h"
+
+#include <functional>
+
+namespace bcp {
+
+extern std::function<CScript()> g_walletMiningScript;
+extern std::function<void(UniValue&)> g_walletGetInfo;
+extern std::function<bool(const CTxDestination&, UniValue&)> g_walletDescribeAddress;
+
+static std::vector<std::unique_ptr<CWallet>> g_ownedWallets;
+
+std::string WalletHelp() {
+    std::string s = "\nWallet options:\n";
+    const std::pair<const char*, const char*> opts[] = {
+        {"-disablewallet", "Do not load the wallet and disable wallet RPC calls"},
+        {"-keypool=<n>", "Set key pool size to <n> (default: 100)"},
+        {"-fallbackfee=<amt>", "A fee rate (in BCP/kB) used when fee estimation has insufficient data (default: 0.0002)"},
+        {"-mintxfee=<amt>", "Fees (in BCP/kB) smaller than this are considered zero fee for transaction creation (default: 0.00001)"},
+        {"-paytxfee=<amt>", "Fee (in BCP/kB) to add to transactions you send (default: 0.00)"},
+        {"-rescan", "Rescan the block chain for missing wallet transactions on startup"},
+        {"-spendzeroconfchange", "Spend unconfirmed change when sending transactions (default: 1)"},
+        {"-txconfirmtarget=<n>", "If paytxfee is not set, include enough fee so transactions begin confirmation within n blocks (default: 6)"},
+        {"-usehd", "Use hierarchical deterministic key generation (HD) after BIP32. Only has effect during wallet creation/first start (default: 1)"},
+        {"-wallet=<file>", "Specify wallet store (within data directory) (default: wallet.dat)"},
+        {"-walletbroadcast", "Make the wallet broadcast transactions (default: 1)"},
+        {"-walletnotify=<cmd>", "Execute command when a wallet transaction changes (%s in cmd is replaced by TxID)"},
+        {"-zapwallettxes", "Delete all wallet transactions and only recover those parts of the blockchain through -rescan on startup"},
+    };
+    for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);
+    return s;
+}
+
+static bool LoadOneWallet(NodeContext& node, const std::string& name, std::string& err) {
+    Chainstate& cs = *node.chainstate;
+    const std::string path = node.datadir + "/" + name;
+    std::unique_ptr<CWallet> w(new CWallet(name, path, false));
+    bool firstRun = false;
+    if (!w->Load(err, firstRun)) return false;
+    if (gArgs.GetBoolArg("-zapwallettxes", false)) {
+        KVBatch b;
+        for (const auto& kv : w->mapWallet) b.Erase(std::make_pair(std::string("tx"), kv.first));
+        w->DB().WriteBatch(b, true);
+        w->mapWallet.clear();
+        w->wtxOrdered.clear();
+    }
+    w->Attach(&cs, node.mempool.get());
+    if (gArgs.IsArgSet("-paytxfee")) {
+        int64_t n = 0;
+        if (!ParseMoney(gArgs.GetArg("-paytxfee", ""), n)) {
+            err = "Invalid amount for -paytxfee=<amount>: '" + gArgs.GetArg("-paytxfee", "") + "'";
+            return false;
+        }
+        w->payTxFee = CFeeRate(n);
+    }
+    w->nTxConfirmTarget = (unsigned)gArgs.GetArg("-txconfirmtarget", (int64_t)DEFAULT_TX_CONFIRM_TARGET);
+    w->fBroadcastTransactions = gArgs.GetBoolArg("-walletbroadcast", DEFAULT_WALLETBROADCAST);
+    if (firstRun) {
+        if (gArgs.GetBoolArg("-usehd", true) && !w->IsHDEnabled()) {
+            if (!w->SetHDMasterKey(w->GenerateNewHDMasterKey())) {
+                err = "Storing master key failed";
+                return false;
+            }
+        }
+        w->TopUpKeyPool();
+        CPubKey def;
+        if (w->GetKeyFromPool(def)) {
+            w->vchDefaultKey = def;
+            w->SetAddressBook(def.GetID(), "", "receive");
+            w->DB().Write(std::string("defaultkey"), def, true);
+        }
+    }
+    // rescan from the wallet's best block (or genesis) to the tip
+    const CBlockIndex* start = nullptr;
+    {
+        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        CBlockLocator loc;
+        if (!gArgs.GetBoolArg("-rescan", false) && !gArgs.GetBoolArg("-zapwallettxes", false) &&
+            w->DB().Read(std::string("bestblock"), loc)) {
+            start = cs.FindForkInGlobalIndex(loc);
+        } else {
+            start = cs.ActiveChain().Genesis();
+        }
+        if (start && start != cs.Tip()) start = cs.ActiveChain().Next(start) ? start : nullptr;
+    }
+    GetMainSignals().Register(w.get());
+    if (start && start != cs.Tip()) {
+        LogPrintf("Rescanning last %i blocks (from block %i)...\n", cs.Height() - start->nHeight, start->nHeight);
+        w->ScanForWalletTransactions(start, true);
+        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        w->SetBestChain(cs.ActiveChain().GetLocator());
+    }
+    w->ReacceptWalletTransactions();
+    g_ownedWallets.push_back(std::move(w));
+    return true;
+}
+
+bool StartWallet(NodeContext& node, std::string& err) {
+    if (gArgs.GetBoolArg("-disablewallet", false)) {
+        LogPrintf("Wallet disabled!\n");
+        return true;
+    }
+    std::vector<std::string> names = gArgs.GetArgs("-wallet");
+    if (names.empty()) names.push_back("wallet.dat");
+    for (const std::string& n : names) {
+        if (n.find('/') != std::string::npos) {
+            err = "Wallet parameter must only specify a filename (not a path): " + n;
+            return false;
+        }
+        if (!LoadOneWallet(node, n, err)) return false;
+    }
+    CWallet* w = g_ownedWallets.front().get();
+    node.wallet = w;
+    node.keystore = w;
+    g_walletMiningScript = [w]() {
+        CReserveKey rk(w);
+        CPubKey pub;
+        if (!rk.GetReservedKey(pub)) ThrowRPC(RPC_WALLET_KEYPOOL_RAN_OUT, "Error: Keypool ran out, please call keypoolrefill first");
+        rk.KeepKey();
+        return GetScriptForDestination(pub.GetID());
+    };
+    g_walletGetInfo = [w](UniValue& obj) {
+        obj.pushKV("walletversion", WALLET_FEATURE_LATEST);
+        obj.pushKV("balance", ValueFromAmount(w->GetBalance()));
+        obj.pushKV("keypoololdest", w->GetOldestKeyPoolTime());
+        obj.pushKV("keypoolsize", (int64_t)w->KeypoolCountExternalKeys());
+        if (w->IsCrypted()) obj.pushKV("unlocked_until", w->nRelockTime);
+        obj.pushKV("paytxfee", ValueFromAmount(w->payTxFee.GetFeePerK()));
+    };
+    g_walletDescribeAddress = [w](const CTxDestination& d, UniValue& ret) {
+        std::lock_guard<std::recursive_mutex> l(w->cs_wallet);
+        const isminetype mine = IsMine(*w, d);
+        ret.pushKV("ismine", (mine & ISMINE_SPENDABLE) != 0);
+        ret.pushKV("iswatchonly", (mine & ISMINE_WATCH_ONLY) != 0);
+        if (d.type == DestType::KEYID) {
+            CPubKey pub;
+            ret.pushKV("isscript", false);
+            if (w->GetPubKey(CKeyID(d.hash), pub)) {
+                ret.pushKV("pubkey", HexStr(pub.begin(), pub.end()));
+                ret.pushKV("iscompressed", pub.IsCompressed());
+            }
+        } else if (d.type == DestType::SCRIPTID) {
+            ret.pushKV("isscript", true);
+            CScript s;
+            if (w->GetCScript(CScriptID(d.hash), s)) ret.pushKV("hex", HexStr(s.begin(), s.end()));
+        }
+        auto it = w->mapAddressBook.find(d);
+        if (it != w->mapAddressBook.end()) ret.pushKV("account", it->second.name);
+        if (d.type == DestType::KEYID) {
+            auto m = w->mapKeyMetadata.find(CKeyID(d.hash));
+            if (m != w->mapKeyMetadata.end()) {
+                ret.pushKV("timestamp", m->second.nCreateTime);
+                if (!m->second.hdKeypath.empty()) {
+                    ret.pushKV("hdkeypath", m->second.hdKeypath);
+                    ret.pushKV("hdmasterkeyid", m->second.hdMasterKeyID.GetHex());
+                }
+            }
+        }
+        return true;
+    };
+    // periodic rebroadcast of unconfirmed wallet transactions
+    if (node.scheduler)
+        node.scheduler->ScheduleEvery(
+            [] {
+                for (CWallet* x : GetWallets()) x->ResendWalletTransactions(GetTime());
+            },
+            60 * 1000);
+    return true;
+}
+
+void StopWallet(NodeContext& node) {
+    g_walletMiningScript = nullptr;
+    g_walletGetInfo = nullptr;
+    g_walletDescribeAddress = nullptr;
+    for (auto& w : g_ownedWallets) {
+        GetMainSignals().Unregister(w.get());
+        w->Flush();
+    }
+    node.wallet = nullptr;
+    node.keystore = nullptr;
+    g_ownedWallets.clear();
+}
+
+} // namespace bcp
