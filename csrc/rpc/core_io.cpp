@@ -124,11 +124,12 @@ void ScriptPubKeyToUniv(const CScript& scriptPubKey, UniValue& out, bool fInclud
     out.pushKV("addresses", a);
 }
 
-void TxToUniv(const CTransaction& tx, const uint256& hashBlock, UniValue& entry, const CChainParams& params) {
+void TxToUniv(const CTransaction& tx, const uint256& hashBlock, UniValue& entry, const CChainParams& params,
+              bool fRpcSize) {
     entry.pushKV("txid", tx.GetHash().GetHex());
     entry.pushKV("hash", tx.GetHash().GetHex());
     entry.pushKV("version", tx.nVersion);
-    entry.pushKV("size", (int)tx.GetTotalSize());
+    if (fRpcSize) entry.pushKV("size", (int)tx.GetTotalSize());
     entry.pushKV("locktime", (int64_t)tx.nLockTime);
     UniValue vin(UniValue::VARR);
     for (const CTxIn& txin : tx.vin) {

@@ -20,7 +20,10 @@ uint256 ParseHashStr(const std::string& str, const std::string& name);
 int ParseSighashString(const std::string& s); // "ALL|FORKID" etc.; throws
 std::string FormatScript(const CScript& script);
 void ScriptPubKeyToUniv(const CScript& scriptPubKey, UniValue& out, bool fIncludeHex, const CChainParams& params);
-void TxToUniv(const CTransaction& tx, const uint256& hashBlock, UniValue& entry, const CChainParams& params);
+// fRpcSize: include "size" like the RPC TxToJSON (reference rpc/rawtransaction.cpp:65); the
+// core_write.cpp TxToUniv used by bitcoin-tx and REST omits it.
+void TxToUniv(const CTransaction& tx, const uint256& hashBlock, UniValue& entry, const CChainParams& params,
+              bool fRpcSize = true);
 double GetDifficultyFromBits(uint32_t nBits);
 
 } // namespace bcp

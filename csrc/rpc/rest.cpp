@@ -85,7 +85,7 @@ static bool rest_tx(const HTTPRequest& req, HTTPReply& rep, const std::string& s
     uint256 hashBlock;
     if (!n->chainstate->GetTransaction(uint256S(hashStr), tx, hashBlock, true)) return RESTERR(rep, 404, hashStr + " not found");
     UniValue obj(UniValue::VOBJ);
-    if (rf == RF_JSON) TxToUniv(*tx, hashBlock, obj, n->chainstate->Params());
+    if (rf == RF_JSON) TxToUniv(*tx, hashBlock, obj, n->chainstate->Params(), false);
     return Reply(rep, rf, SerializeToBytes(*tx), obj);
 }
 
