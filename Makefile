@@ -36,9 +36,11 @@ TOOLS      := $(patsubst csrc/tools/%.cpp,bin/%,$(TOOL_SRCS))
 
 PYEXT      := bitcoincashplus_amd/_bcpnative$(PY_EXT)
 CORELIB    := build/libbcpcore.a
+CONSLIB    := lib/libbcpconsensus.so
 
-.PHONY: all pyext tools clean kernels
-all: pyext tools
+.PHONY: all pyext tools clean kernels conslib
+conslib: $(CONSLIB)
+all: pyext tools conslib
 pyext: $(PYEXT)
 kernels: $(HIP_OBJS)
 tools: $(TOOLS)
@@ -70,7 +72,11 @@ build/obj/tools/%.o: csrc/tools/%.cpp
 	@mkdir -p $(dir $@)
 	$(CXX) $(CXXFLAGS) -MMD -MP -c $< -o $@
 
+$(CONSLIB): build/obj/consensuslib/bitcoinconsensus.o $(CORELIB)
+	@mkdir -p lib
+	$(CXX) -shared -o $@ $< $(CORELIB) $(LDLIBS)
+
 clean:
-	rm -rf build bin bitcoincashplus_amd/_bcpnative*.so
+	rm -rf build bin lib bitcoincashplus_amd/_bcpnative*.so
 
 -include $(shell find build -name '*.d' 2>/dev/null)
