@@ -23,7 +23,7 @@ LDLIBS     := -L$(ROCM)/lib -lamdhip64 -pthread -ldl -Wl,-rpath,$(ROCM)/lib
 
 CORE_SRCS  := $(wildcard csrc/crypto/*.cpp csrc/primitives/*.cpp csrc/consensus/*.cpp \
                 csrc/script/*.cpp csrc/secp256k1/*.cpp csrc/util/*.cpp csrc/node/*.cpp \
-                csrc/rpc/*.cpp csrc/net/*.cpp csrc/wallet/*.cpp csrc/keys/*.cpp)
+                csrc/rpc/*.cpp csrc/net/*.cpp csrc/wallet/*.cpp csrc/keys/*.cpp csrc/zmq/*.cpp)
 GPU_HOST   := $(wildcard csrc/gpu/*.cpp)
 HIP_SRCS   := $(wildcard csrc/kernels/*.hip)
 PY_SRCS    := $(wildcard csrc/python/*.cpp)
