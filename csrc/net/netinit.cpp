@@ -14,6 +14,9 @@ namespace bcp {
 
 extern std::function<void(const uint256&)> g_relayTransaction;
 
+void StartTorControl(NodeContext& node, int listenPort);
+void StopTorControl();
+
 static std::unique_ptr<CConnman> g_connman;
 static std::unique_ptr<PeerLogicValidation> g_peerLogic;
 
@@ -39,6 +42,9 @@ std::string NetHelp() {
         {"-whitelist=<IP/netmask>", "Whitelist peers connecting from the given IP address or CIDR netmask"},
         {"-blocksonly", "Whether to operate in a blocks only mode (default: 0)"},
         {"-maxorphantx=<n>", "Keep at most <n> unconnectable transactions in memory (default: 100)"},
+        {"-listenonion", "Automatically create Tor hidden service (default: 1)"},
+        {"-torcontrol=<ip>:<port>", "Tor control port to use if onion listening enabled (default: 127.0.0.1:9051)"},
+        {"-torpassword=<pass>", "Tor control port password (default: empty)"},
     };
     for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);
     return s;
@@ -120,6 +126,7 @@ bool StartNetwork(NodeContext& node, std::string& err) {
         g_connman.reset();
         return false;
     }
+    StartTorControl(node, port);
     LogPrintf("Network started: listen=%d port=%d services=%llx\n", (int)o.fListen, port,
               (unsigned long long)o.nLocalServices);
     return true;
@@ -127,6 +134,7 @@ bool StartNetwork(NodeContext& node, std::string& err) {
 
 void StopNetwork(NodeContext& node) {
     if (!g_connman) return;
+    StopTorControl();
     g_relayTransaction = nullptr;
     g_connman->Interrupt();
     g_connman->Stop();
