@@ -7,10 +7,7 @@
 
 namespace bcp {
 
-void memory_cleanse(void* ptr, size_t len) {
-    memset(ptr, 0, len);
-    __asm__ __volatile__("" : : "r"(ptr) : "memory");
-}
+// memory_cleanse lives in util/lockedpool.cpp
 
 // ---------------------------------------------------------------- SHA-256
 namespace {

@@ -13,6 +13,7 @@
 #include "script/sign.h"
 #include "script/standard.h"
 #include "kernels/gpu_api.h"
+#include "util/lockedpool.h"
 #include "util/strencodings.h"
 
 #include <mutex>
@@ -77,12 +78,13 @@ static UniValue getmemoryinfo(const JSONRPCRequest& req) {
     NodeContext& n = Node();
     UniValue obj(UniValue::VOBJ);
     UniValue locked(UniValue::VOBJ);
-    locked.pushKV("used", 0);
-    locked.pushKV("free", 0);
-    locked.pushKV("total", 0);
-    locked.pushKV("locked", 0);
-    locked.pushKV("chunks_used", 0);
-    locked.pushKV("chunks_free", 0);
+    const LockedPool::Stats st = LockedPoolManager::Instance().stats();
+    locked.pushKV("used", (int64_t)st.used);
+    locked.pushKV("free", (int64_t)st.free);
+    locked.pushKV("total", (int64_t)st.total);
+    locked.pushKV("locked", (int64_t)st.locked);
+    locked.pushKV("chunks_used", (int64_t)st.chunks_used);
+    locked.pushKV("chunks_free", (int64_t)st.chunks_free);
     obj.pushKV("locked", locked);
     obj.pushKV("coins_cache_bytes", (int64_t)n.chainstate->CoinsTip().DynamicMemoryUsage());
     obj.pushKV("mempool_bytes", (int64_t)n.mempool->DynamicMemoryUsage());

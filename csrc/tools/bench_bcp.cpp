@@ -1,0 +1,390 @@
+// bench_bcp: native micro-benchmark harness.
+// Parity: reference src/bench/ (bench.{h,cpp} adaptive State::KeepRunning with min/max/
+// median per-iteration timing, -filter regex, CSV-like output; benches Sleep100ms, Trig,
+// Base58Encode/CheckEncode/Decode, CCoinsCaching, DeserializeBlockTest,
+// DeserializeAndCheckBlockTest (bench/data/block413567.raw, legacy header format),
+// CCheckQueueSpeed, CoinSelection, RIPEMD160, SHA1, SHA256, SHA512, SHA256_32b,
+// SipHash_32b, FastRandom_32bit/1bit, LockedPool, MempoolEviction, RollingBloom) plus
+// MI355X batches (SHA256d64 batch, Merkle root, ECDSA batch verify) when a GPU is visible.
+#include "consensus/merkle.h"
+#include "consensus/merkleblock.h"
+#include "consensus/params.h"
+#include "crypto/hashes.h"
+#include "kernels/gpu_api.h"
+#include "keys/key.h"
+#include "node/coins.h"
+#include "node/sigverify.h"
+#include "node/txmempool.h"
+#include "node/validation.h"
+#include "primitives/block.h"
+#include "util/lockedpool.h"
+#include "util/strencodings.h"
+#include "util/util.h"
+#include "wallet/wallet.h"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <fstream>
+#include <functional>
+#include <regex>
+#include <thread>
+
+using namespace bcp;
+
+namespace bench {
+
+class State {
+public:
+    State(const std::string& name, double minTime) : name(name), minTime(minTime) {}
+    bool KeepRunning() {
+        const auto now = std::chrono::steady_clock::now();
+        if (count == 0) {
+            start = last = now;
+            count = 1;
+            return true;
+        }
+        const double dt = std::chrono::duration<double>(now - last).count();
+        samples.push_back(dt);
+        last = now;
+        count++;
+        const double elapsed = std::chrono::duration<double>(now - start).count();
+        return elapsed < minTime && count < 1000000000ULL;
+    }
+    void Report() const {
+        if (samples.empty()) return;
+        std::vector<double> s = samples;
+        std::sort(s.begin(), s.end());
+        double total = 0;
+        for (double d : s) total += d;
+        printf("%-34s %10zu %14.9f %14.9f %14.9f %14.9f\n", name.c_str(), s.size(), total, s.front(), s.back(),
+               s[s.size() / 2]);
+        fflush(stdout);
+    }
+
+private:
+    std::string name;
+    double minTime;
+    uint64_t count = 0;
+    std::chrono::steady_clock::time_point start, last;
+    std::vector<double> samples;
+};
+
+typedef std::function<void(State&)> BenchFn;
+std::vector<std::pair<std::string, BenchFn>>& Registry() {
+    static std::vector<std::pair<std::string, BenchFn>> r;
+    return r;
+}
+struct Reg {
+    Reg(const char* n, BenchFn f) { Registry().push_back({n, f}); }
+};
+#define BENCHMARK(fn) static bench::Reg reg_##fn(#fn, fn)
+
+} // namespace bench
+using bench::State;
+
+static std::string g_dataDir = "bench/data";
+
+// ------------------------------------------------------------------ benches
+static void Sleep100ms(State& st) {
+    while (st.KeepRunning()) std::this_thread::sleep_for(std::chrono::milliseconds(100));
+}
+BENCHMARK(Sleep100ms);
+
+static void Trig(State& st) {
+    double sum = 0, d = 0.01;
+    while (st.KeepRunning()) {
+        sum += sin(d);
+        d += 0.000001;
+    }
+    if (sum == 42) printf("x");
+}
+BENCHMARK(Trig);
+
+static void Base58Encode(State& st) {
+    unsigned char buf[32] = {17, 79, 8, 99, 150, 189, 208, 162, 22, 23, 203, 163, 36, 58, 147, 227,
+                             139, 2, 215, 100, 91, 38, 11, 141, 253, 40, 117, 21, 16, 90, 200, 24};
+    while (st.KeepRunning()) EncodeBase58(buf, buf + 32);
+}
+BENCHMARK(Base58Encode);
+
+static void Base58CheckEncode(State& st) {
+    std::vector<unsigned char> v(32, 7);
+    while (st.KeepRunning()) EncodeBase58Check(v);
+}
+BENCHMARK(Base58CheckEncode);
+
+static void Base58Decode(State& st) {
+    const std::string addr = "17VZNX1SN5NtKa8UQFxwQbFeFc3iqRYhem";
+    std::vector<unsigned char> v;
+    while (st.KeepRunning()) DecodeBase58(addr, v);
+}
+BENCHMARK(Base58Decode);
+
+static void HashBench(State& st, int which) {
+    std::vector<unsigned char> in(1000 * 1000, 0);
+    unsigned char out[64];
+    while (st.KeepRunning()) {
+        switch (which) {
+        case 0: CRIPEMD160().Write(in.data(), in.size()).Finalize(out); break;
+        case 1: CSHA1().Write(in.data(), in.size()).Finalize(out); break;
+        case 2: CSHA256().Write(in.data(), in.size()).Finalize(out); break;
+        case 3: CSHA512().Write(in.data(), in.size()).Finalize(out); break;
+        }
+    }
+}
+static void RIPEMD160(State& st) { HashBench(st, 0); }
+static void SHA1(State& st) { HashBench(st, 1); }
+static void SHA256(State& st) { HashBench(st, 2); }
+static void SHA512(State& st) { HashBench(st, 3); }
+BENCHMARK(RIPEMD160);
+BENCHMARK(SHA1);
+BENCHMARK(SHA256);
+BENCHMARK(SHA512);
+
+static void SHA256_32b(State& st) {
+    std::vector<unsigned char> in(32, 0);
+    while (st.KeepRunning())
+        for (int i = 0; i < 1000000; i++) CSHA256().Write(in.data(), in.size()).Finalize(in.data());
+}
+BENCHMARK(SHA256_32b);
+
+static void SipHash_32b(State& st) {
+    uint256 x;
+    uint64_t k1 = 0;
+    while (st.KeepRunning())
+        for (int i = 0; i < 1000000; i++) *((uint64_t*)x.begin()) = SipHashUint256(0, ++k1, x.begin());
+}
+BENCHMARK(SipHash_32b);
+
+static void FastRandom_32bit(State& st) {
+    FastRandomContext rng(true);
+    uint32_t x = 0;
+    while (st.KeepRunning())
+        for (int i = 0; i < 1000000; i++) x += (uint32_t)rng.randbits(32);
+    if (x == 42) printf("x");
+}
+BENCHMARK(FastRandom_32bit);
+
+static void FastRandom_1bit(State& st) {
+    FastRandomContext rng(true);
+    uint32_t x = 0;
+    while (st.KeepRunning())
+        for (int i = 0; i < 1000000; i++) x += (uint32_t)rng.randbits(1);
+    if (x == 42) printf("x");
+}
+BENCHMARK(FastRandom_1bit);
+
+static void RollingBloom(State& st) {
+    CRollingBloomFilter filter(120000, 0.000001);
+    std::vector<unsigned char> data(32);
+    uint32_t count = 0;
+    while (st.KeepRunning()) {
+        count++;
+        memcpy(data.data(), &count, 4);
+        filter.insert(data);
+        data[0] ^= 0xff;
+        filter.contains(data);
+    }
+}
+BENCHMARK(RollingBloom);
+
+static void LockedPoolBench(State& st) {
+    void* synth_base = reinterpret_cast<void*>(0x08000000);
+    const size_t synth_size = 1024 * 1024;
+    Arena b(synth_base, synth_size, 16);
+    std::vector<void*> addr(128, nullptr);
+    uint32_t s = 0x12345678;
+    while (st.KeepRunning()) {
+        for (int x = 0; x < 1000; ++x) {
+            const int idx = s & (addr.size() - 1);
+            if (s & 0x80000000) {
+                b.free(addr[idx]);
+                addr[idx] = nullptr;
+            } else if (!addr[idx]) {
+                addr[idx] = b.alloc((s >> 16) & 2047);
+            }
+            const bool lsb = s & 1;
+            s >>= 1;
+            if (lsb) s ^= 0xf00f00f0;
+        }
+    }
+    for (void* p : addr) b.free(p);
+}
+static bench::Reg reg_LockedPool("LockedPool", LockedPoolBench);
+
+static std::vector<unsigned char> LoadBlockFile() {
+    std::ifstream f(g_dataDir + "/block413567.raw", std::ios::binary);
+    return std::vector<unsigned char>((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+}
+
+static void DeserializeBlockTest(State& st) {
+    const std::vector<unsigned char> raw = LoadBlockFile();
+    if (raw.empty()) return;
+    while (st.KeepRunning()) {
+        CBlock block;
+        SpanReader r(raw.data(), raw.size(), SER_NETWORK, PROTOCOL_VERSION | SERIALIZE_BLOCK_LEGACY);
+        r >> block;
+    }
+}
+BENCHMARK(DeserializeBlockTest);
+
+static void DeserializeAndCheckBlockTest(State& st) {
+    const std::vector<unsigned char> raw = LoadBlockFile();
+    if (raw.empty()) return;
+    SelectParams("main");
+    ChainstateOptions o;
+    o.memoryOnly = true;
+    o.useGpu = false;
+    Chainstate cs(Params(), o);
+    while (st.KeepRunning()) {
+        CBlock block;
+        SpanReader r(raw.data(), raw.size(), SER_NETWORK, PROTOCOL_VERSION | SERIALIZE_BLOCK_LEGACY);
+        r >> block;
+        CValidationState state;
+        if (!cs.CheckBlock(block, state)) {
+            fprintf(stderr, "CheckBlock failed: %s\n", state.GetRejectReason().c_str());
+            exit(1);
+        }
+    }
+}
+BENCHMARK(DeserializeAndCheckBlockTest);
+
+static void CCheckQueueSpeed(State& st) {
+    // 128 batches of trivial jobs through the worker pool (reference: prevector-free jobs)
+    WorkerPool pool(std::max(2, GetNumCores()));
+    std::atomic<uint64_t> sink{0};
+    while (st.KeepRunning()) pool.ParallelFor(128 * 30, [&](size_t i) { sink += i; }, 30);
+}
+BENCHMARK(CCheckQueueSpeed);
+
+static void CCoinsCaching(State& st) {
+    CCoinsView base;
+    CCoinsViewCache coins(&base);
+    CBasicKeyStore ks;
+    CKey key;
+    key.MakeNewKey(true);
+    ks.AddKey(key);
+    CMutableTransaction prev;
+    prev.vout.resize(2);
+    prev.vout[0] = CTxOut(21 * 100000000LL, GetScriptForDestination(key.GetPubKey().GetID()));
+    prev.vout[1] = CTxOut(22 * 100000000LL, GetScriptForDestination(key.GetPubKey().GetID()));
+    const CTransaction prevTx(prev);
+    AddCoins(coins, prevTx, 0);
+    CMutableTransaction t;
+    t.vin.resize(2);
+    t.vin[0].prevout = COutPoint(prevTx.GetHash(), 0);
+    t.vin[1].prevout = COutPoint(prevTx.GetHash(), 1);
+    t.vout.resize(1);
+    t.vout[0].nValue = 90 * 100000000LL;
+    const CTransaction tx(t);
+    while (st.KeepRunning()) {
+        bool ok = true;
+        for (const CTxIn& in : tx.vin) ok &= coins.HaveCoin(in.prevout);
+        Amount v = 0;
+        for (const CTxIn& in : tx.vin) v += coins.AccessCoin(in.prevout).out.nValue;
+        if (!ok || v == 0) exit(1);
+    }
+}
+BENCHMARK(CCoinsCaching);
+
+static void CoinSelection(State& st) {
+    SelectParams("regtest");
+    CWallet wallet("bench", "", true);
+    std::vector<COutput> vCoins;
+    std::vector<std::unique_ptr<CWalletTx>> wtxs;
+    auto addCoin = [&](Amount nValue) {
+        CMutableTransaction tx;
+        tx.nLockTime = (uint32_t)wtxs.size();
+        tx.vout.resize(1);
+        tx.vout[0].nValue = nValue;
+        wtxs.emplace_back(new CWalletTx(&wallet, MakeTransactionRef(std::move(tx))));
+        wtxs.back()->fFromMe = true;
+        vCoins.push_back({wtxs.back().get(), 0, 6 * 24, true, true});
+    };
+    for (int i = 0; i < 1000; i++) addCoin(1000 * 100000000LL);
+    addCoin(3 * 100000000LL);
+    while (st.KeepRunning()) {
+        std::set<std::pair<const CWalletTx*, unsigned int>> setCoinsRet;
+        Amount nValueRet;
+        const bool ok = wallet.SelectCoinsMinConf(1003 * 100000000LL, 1, 6, vCoins, setCoinsRet, nValueRet);
+        if (!ok || nValueRet != 1003 * 100000000LL || setCoinsRet.size() != 2) exit(1);
+    }
+}
+BENCHMARK(CoinSelection);
+
+static void MempoolEviction(State& st) {
+    CTxMemPool pool(nullptr);
+    std::vector<CTransactionRef> txs;
+    for (int i = 0; i < 7; i++) {
+        CMutableTransaction tx;
+        tx.vin.resize(1);
+        tx.vin[0].prevout = COutPoint(uint256S(strprintf("%064x", i + 1)), 0);
+        tx.vin[0].scriptSig = CScript() << OP_1;
+        tx.vout.resize(1);
+        tx.vout[0].scriptPubKey = CScript() << OP_1 << OP_EQUAL;
+        tx.vout[0].nValue = 10 * 100000000LL;
+        txs.push_back(MakeTransactionRef(std::move(tx)));
+    }
+    while (st.KeepRunning()) {
+        int64_t t = 0;
+        for (size_t i = 0; i < txs.size(); i++) {
+            CTxMemPoolEntry e(txs[i], (Amount)(1000 * (i + 1)), t++, 0.0, 1, 0, false, 1, LockPoints());
+            pool.addUnchecked(txs[i]->GetHash(), e);
+        }
+        pool.TrimToSize(pool.DynamicMemoryUsage() * 3 / 4);
+        pool.TrimToSize(GetSerializeSize(*txs[0]));
+        pool.clear();
+    }
+}
+BENCHMARK(MempoolEviction);
+
+// ---- MI355X batches (skipped without a GPU)
+static void GpuSha256d64Batch(State& st) {
+    if (!gpu::GpuAvailable()) return;
+    std::vector<unsigned char> data(64 * (1 << 20), 1);
+    while (st.KeepRunning()) gpu::Sha256d64Batch(data);
+}
+static bench::Reg reg_GpuSha("GPU_SHA256d64_1M", GpuSha256d64Batch);
+
+static void GpuMerkle(State& st) {
+    if (!gpu::GpuAvailable()) return;
+    std::vector<unsigned char> leaves(32 * (1 << 20), 3);
+    bool mut = false;
+    while (st.KeepRunning()) gpu::MerkleRoot(leaves, &mut);
+}
+static bench::Reg reg_GpuMerkle("GPU_MerkleRoot_1M", GpuMerkle);
+
+static void CpuMerkle(State& st) {
+    std::vector<uint256> leaves(1 << 20);
+    for (size_t i = 0; i < leaves.size(); i++) *(uint64_t*)leaves[i].begin() = i;
+    while (st.KeepRunning()) {
+        bool mut = false;
+        ComputeMerkleRoot(leaves, &mut);
+    }
+}
+static bench::Reg reg_CpuMerkle("CPU_MerkleRoot_1M", CpuMerkle);
+
+int main(int argc, char* argv[]) {
+    gArgs.ParseParameters(argc, argv);
+    if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help")) {
+        printf("Usage: bench_bcp [-filter=<regex>] [-time=<seconds per bench>] [-list] [-datadir=bench/data]\n");
+        return 0;
+    }
+    g_dataDir = gArgs.GetArg("-datadir", g_dataDir);
+    const std::regex filter(gArgs.GetArg("-filter", ".*"));
+    const double minTime = atof(gArgs.GetArg("-time", "1.0").c_str());
+    if (gArgs.IsArgSet("-list")) {
+        for (const auto& b : bench::Registry()) printf("%s\n", b.first.c_str());
+        return 0;
+    }
+    printf("# %-32s %10s %14s %14s %14s %14s\n", "Benchmark", "iterations", "total", "min", "max", "median");
+    for (const auto& b : bench::Registry()) {
+        if (!std::regex_match(b.first, filter)) continue;
+        State st(b.first, minTime);
+        b.second(st);
+        st.Report();
+    }
+    return 0;
+}

@@ -7,6 +7,7 @@
 #pragma once
 #include "keys/key.h"
 #include "script/sign.h"
+#include "util/lockedpool.h"
 
 #include <map>
 #include <string>
@@ -18,7 +19,7 @@ static const unsigned int WALLET_CRYPTO_KEY_SIZE = 32;
 static const unsigned int WALLET_CRYPTO_SALT_SIZE = 8;
 static const unsigned int WALLET_CRYPTO_IV_SIZE = 16;
 
-typedef std::vector<unsigned char> CKeyingMaterial; // wiped on destruction by users
+typedef std::vector<unsigned char, secure_allocator<unsigned char>> CKeyingMaterial; // mlocked, cleansed on free
 
 class CMasterKey {
 public:
