@@ -88,7 +88,7 @@ class BcpdProcess:
         chainflag = {"regtest": ["-regtest"], "test": ["-testnet"], "main": []}[self.chain]
         return [self.binary, f"-datadir={self.datadir}", *chainflag, f"-rpcport={self.rpcport}",
                 f"-port={self.p2p_port}", f"-rpcuser={self.user}", f"-rpcpassword={self.password}",
-                "-listenonion=0", "-discover=0", "-dnsseed=0", *self.extra_args]
+                "-listenonion=0", "-discover=0", "-dnsseed=0", "-debuglockorder=1", *self.extra_args]
 
     def start(self, wait=True, timeout=60):
         log = open(os.path.join(self.datadir, "stdout.log"), "ab")

@@ -70,7 +70,7 @@ double CAddrInfo::GetChance(int64_t now) const {
 CAddrMan::CAddrMan() { Clear(); }
 
 void CAddrMan::Clear() {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     nKey = GetRandHash();
     mapInfo.clear();
     mapAddr.clear();
@@ -82,15 +82,15 @@ void CAddrMan::Clear() {
 }
 
 size_t CAddrMan::size() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return vRandom.size();
 }
 size_t CAddrMan::NumTried() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return nTried;
 }
 size_t CAddrMan::NumNew() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return nNew;
 }
 
@@ -100,7 +100,7 @@ int CAddrMan::Id(const CService& addr) const {
 }
 
 bool CAddrMan::Find(const CService& addr, CAddrInfo* out) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     const int id = Id(addr);
     if (id < 0) return false;
     if (out) *out = mapInfo.at(id);
@@ -179,7 +179,7 @@ void CAddrMan::MakeTried(int id) {
 }
 
 bool CAddrMan::Add(const CAddress& addr, const CNetAddr& source, int64_t nTimePenalty) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     if (!addr.IsRoutable()) return false;
     const int64_t now = GetAdjustedTime();
     if (addr == source) nTimePenalty = 0;
@@ -238,7 +238,7 @@ bool CAddrMan::Add(const std::vector<CAddress>& v, const CNetAddr& source, int64
 }
 
 void CAddrMan::Good(const CService& addr, int64_t nTime) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     if (!nTime) nTime = GetAdjustedTime();
     nLastGood = nTime;
     const int id = Id(addr);
@@ -253,7 +253,7 @@ void CAddrMan::Good(const CService& addr, int64_t nTime) {
 }
 
 void CAddrMan::Attempt(const CService& addr, bool fCountFailure, int64_t nTime) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     if (!nTime) nTime = GetAdjustedTime();
     const int id = Id(addr);
     if (id < 0) return;
@@ -264,7 +264,7 @@ void CAddrMan::Attempt(const CService& addr, bool fCountFailure, int64_t nTime) 
 }
 
 CAddrInfo CAddrMan::Select(bool newOnly) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     if (vRandom.empty()) return CAddrInfo();
     if (newOnly && nNew == 0) return CAddrInfo();
     const int64_t now = GetAdjustedTime();
@@ -287,7 +287,7 @@ CAddrInfo CAddrMan::Select(bool newOnly) {
 }
 
 std::vector<CAddress> CAddrMan::GetAddr() {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<CAddress> out;
     size_t n = GETADDR_MAX_PCT * vRandom.size() / 100;
     n = std::min<size_t>(n, GETADDR_MAX);
@@ -302,7 +302,7 @@ std::vector<CAddress> CAddrMan::GetAddr() {
 }
 
 void CAddrMan::Connected(const CService& addr, int64_t nTime) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     if (!nTime) nTime = GetAdjustedTime();
     const int id = Id(addr);
     if (id < 0) return;
@@ -311,7 +311,7 @@ void CAddrMan::Connected(const CService& addr, int64_t nTime) {
 }
 
 void CAddrMan::SetServices(const CService& addr, uint64_t services) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     const int id = Id(addr);
     if (id >= 0) mapInfo[id].nServices = services;
 }
@@ -321,7 +321,7 @@ static const uint8_t ADDRMAN_FORMAT = 1;
 bool CAddrMan::Write(const std::string& path, const unsigned char* magic) const {
     std::vector<unsigned char> payload;
     {
-        std::lock_guard<std::recursive_mutex> l(cs);
+        std::lock_guard<CCriticalSection> l(cs);
         VectorWriter w(payload, SER_DISK, CLIENT_VERSION);
         w.write((const char*)magic, 4);
         w << ADDRMAN_FORMAT << nKey;
@@ -363,7 +363,7 @@ bool CAddrMan::Read(const std::string& path, const unsigned char* magic) {
         uint32_t count;
         r >> fmt >> key >> count;
         if (fmt != ADDRMAN_FORMAT) return false;
-        std::lock_guard<std::recursive_mutex> l(cs);
+        std::lock_guard<CCriticalSection> l(cs);
         Clear();
         nKey = key;
         for (uint32_t i = 0; i < count; i++) {

@@ -7,6 +7,7 @@
 //
 // Design: one mutex-protected table of CAddrInfo indexed by id; bucket slots hold ids.
 #pragma once
+#include "util/sync.h"
 #include "net/netaddress.h"
 #include "primitives/uint256.h"
 
@@ -89,7 +90,7 @@ private:
     void MakeTried(int id);
     void SwapRandom(int a, int b);
 
-    mutable std::recursive_mutex cs;
+    mutable CCriticalSection cs{"addrman.cs"};
     uint256 nKey;
     std::map<int, CAddrInfo> mapInfo;
     std::map<std::vector<unsigned char>, int> mapAddr;

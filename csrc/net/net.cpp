@@ -408,7 +408,7 @@ void CConnman::Stop() {
     DumpData();
     std::vector<CNode*> nodes;
     {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         nodes = vNodes;
         vNodes.clear();
     }
@@ -442,7 +442,7 @@ void CConnman::SetNetworkActive(bool active) {
     if (fNetworkActive == active) return;
     fNetworkActive = active;
     if (!active) {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         for (CNode* p : vNodes) p->fDisconnect = true;
     }
 }
@@ -454,26 +454,26 @@ bool CConnman::IsWhitelistedRange(const CNetAddr& addr) {
 }
 
 CNode* CConnman::FindNode(const CNetAddr& ip) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if ((CNetAddr)p->addr == ip) return p;
     return nullptr;
 }
 CNode* CConnman::FindNode(const std::string& name) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if (p->addrName == name) return p;
     return nullptr;
 }
 CNode* CConnman::FindNode(const CService& addr) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if ((CService)p->addr == addr) return p;
     return nullptr;
 }
 
 bool CConnman::CheckIncomingNonce(uint64_t nonce) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if (!p->fSuccessfullyConnected && !p->fInbound && p->GetLocalNonce() == nonce) return false;
     return true;
@@ -495,7 +495,7 @@ CNode* CConnman::ConnectNode(CAddress addrConnect, const char* pszDest) {
         if (Lookup(pszDest, resolved, Params().GetDefaultPort(), true, 256) && !resolved.empty()) {
             addrConnect = CAddress(resolved[GetRand(resolved.size())], NODE_NONE);
             if (!addrConnect.IsValid()) return nullptr;
-            std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+            std::lock_guard<CCriticalSection> l(cs_vNodes);
             if (FindNode((CService)addrConnect)) {
                 LogPrintf("Failed to open new connection, already connected\n");
                 return nullptr;
@@ -557,7 +557,7 @@ bool CConnman::OpenNetworkConnection(const CAddress& addrConnect, bool fCountFai
     p->fAddnode = fAddnode;
     if (events) events->InitializeNode(p);
     {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         vNodes.push_back(p);
     }
     WakeMessageHandler();
@@ -574,7 +574,7 @@ bool CConnman::AttemptToEvictConnection() {
     };
     std::vector<Cand> cands;
     {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         for (CNode* p : vNodes) {
             if (p->fWhitelisted || !p->fInbound || p->fDisconnect) continue;
             cands.push_back({p->GetId(), p->nTimeConnected, p->nMinPingUsecTime, p->nKeyedNetGroup});
@@ -611,7 +611,7 @@ void CConnman::AcceptConnection(const ListenSocket& ls) {
     const bool whitelisted = ls.whitelisted || IsWhitelistedRange(addr);
     int nInbound = 0;
     {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         for (CNode* p : vNodes)
             if (p->fInbound) nInbound++;
     }
@@ -646,7 +646,7 @@ void CConnman::AcceptConnection(const ListenSocket& ls) {
     if (events) events->InitializeNode(p);
     LogPrint(BCLog::NET, "connection from %s accepted\n", addr.ToString().c_str());
     {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         vNodes.push_back(p);
     }
 }
@@ -757,7 +757,7 @@ void CConnman::ThreadSocketHandler() {
     while (!interruptNet) {
         // ---- disconnect and reap nodes
         {
-            std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+            std::lock_guard<CCriticalSection> l(cs_vNodes);
             std::vector<CNode*> copy = vNodes;
             for (CNode* p : copy) {
                 if (p->fDisconnect) {
@@ -782,7 +782,7 @@ void CConnman::ThreadSocketHandler() {
         }
         size_t n;
         {
-            std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+            std::lock_guard<CCriticalSection> l(cs_vNodes);
             n = vNodes.size();
         }
         if (n != nPrevNodeCount) nPrevNodeCount = n;
@@ -794,7 +794,7 @@ void CConnman::ThreadSocketHandler() {
         for (const ListenSocket& ls : vhListenSocket) fds.push_back({ls.fd, POLLIN, 0});
         const size_t nodeBase = fds.size();
         {
-            std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+            std::lock_guard<CCriticalSection> l(cs_vNodes);
             for (CNode* p : vNodes) {
                 short ev = 0;
                 {
@@ -911,7 +911,7 @@ void CConnman::ThreadMessageHandler() {
     while (!flagInterruptMsgProc) {
         std::vector<CNode*> copy;
         {
-            std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+            std::lock_guard<CCriticalSection> l(cs_vNodes);
             for (CNode* p : vNodes) copy.push_back(p->AddRef());
         }
         bool fMoreWork = false;
@@ -979,7 +979,7 @@ void CConnman::ThreadOpenConnections() {
         int nOutbound = 0;
         std::set<std::vector<unsigned char>> setConnected;
         {
-            std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+            std::lock_guard<CCriticalSection> l(cs_vNodes);
             for (CNode* p : vNodes)
                 if (!p->fInbound && !p->fAddnode) {
                     setConnected.insert(p->addr.GetGroup());
@@ -1029,7 +1029,7 @@ std::vector<AddedNodeInfo> CConnman::GetAddedNodeInfo() {
     std::map<CService, bool> mapConnected;
     std::map<std::string, std::pair<bool, CService>> mapConnectedByName;
     {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         for (CNode* p : vNodes) {
             if (p->addr.IsValid()) mapConnected[p->addr] = p->fInbound;
             if (!p->addrName.empty()) mapConnectedByName[p->addrName] = {p->fInbound, p->addr};
@@ -1083,7 +1083,7 @@ void CConnman::ThreadDNSAddressSeed() {
     // only query DNS seeds when the address book is thin (reference net.cpp:1582)
     if (!InterruptibleSleep(11000)) return;
     if (addrman.size() > 0) {
-        std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+        std::lock_guard<CCriticalSection> l(cs_vNodes);
         int n = 0;
         for (CNode* p : vNodes) n += (p->fSuccessfullyConnected && !p->fOneShot && !p->fFeeler && !p->fInbound);
         if (n >= 2) return;
@@ -1109,14 +1109,14 @@ void CConnman::ThreadDNSAddressSeed() {
 }
 
 bool CConnman::ForNode(NodeId id, std::function<bool(CNode*)> func) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if (p->GetId() == id) return !p->fDisconnect && func(p);
     return false;
 }
 
 void CConnman::ForEachNode(std::function<void(CNode*)> func) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if (p->fSuccessfullyConnected && !p->fDisconnect) func(p);
 }
@@ -1127,7 +1127,7 @@ void CConnman::Ban(const CNetAddr& addr, BanReason reason, int64_t bantime, bool
 
 void CConnman::Ban(const CSubNet& sub, BanReason reason, int64_t bantime, bool sinceUnixEpoch) {
     banman.Ban(sub, reason, bantime, sinceUnixEpoch);
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if (sub.Match(p->addr)) p->fDisconnect = true;
     if (reason == BanReasonManuallyAdded) DumpData();
@@ -1163,7 +1163,7 @@ bool CConnman::RemoveAddedNode(const std::string& node) {
 }
 
 size_t CConnman::GetNodeCount(NumConnections flags) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     if (flags == CONNECTIONS_ALL) return vNodes.size();
     size_t n = 0;
     for (CNode* p : vNodes)
@@ -1173,7 +1173,7 @@ size_t CConnman::GetNodeCount(NumConnections flags) {
 
 void CConnman::GetNodeStats(std::vector<CNodeStats>& v) {
     v.clear();
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes) {
         v.emplace_back();
         p->CopyStats(v.back());
@@ -1204,7 +1204,7 @@ bool CConnman::DisconnectNode(const CNetAddr& addr) {
 }
 
 bool CConnman::DisconnectNode(NodeId id) {
-    std::lock_guard<std::recursive_mutex> l(cs_vNodes);
+    std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if (p->GetId() == id) {
             p->fDisconnect = true;

@@ -378,7 +378,7 @@ private:
     bool fConnectOnly = false;
     bool fDNSSeed = true;
     std::vector<CSubNet> vWhitelistedRange;
-    mutable std::recursive_mutex cs_vNodes;
+    mutable CCriticalSection cs_vNodes{"cs_vNodes"};
     std::vector<CNode*> vNodes;
     std::list<CNode*> vNodesDisconnected;
     std::atomic<NodeId> nLastNodeId{0};

@@ -111,7 +111,7 @@ struct PeerLogicValidation::Impl {
     int64_t nTimeBestReceived = 0;
     FastRandomContext rng;
 
-    std::recursive_mutex& csMain() { return cs->cs(); }
+    CCriticalSection& csMain() { return cs->cs(); }
     CNodeState* State(NodeId id) {
         auto it = mapNodeState.find(id);
         return it == mapNodeState.end() ? nullptr : &it->second;
@@ -135,7 +135,7 @@ struct PeerLogicValidation::Impl {
     }
 
     void Misbehaving(NodeId id, int howmuch, const std::string& reason = "") {
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         MisbehavingLocked(id, howmuch, reason);
     }
 
@@ -423,7 +423,7 @@ void PeerLogicValidation::Impl::PushNodeVersion(CNode* pnode, int64_t nTime) {
 
 void PeerLogicValidation::InitializeNode(CNode* pnode) {
     {
-        std::lock_guard<std::recursive_mutex> l(impl->csMain());
+        std::lock_guard<CCriticalSection> l(impl->csMain());
         CNodeState& st = impl->mapNodeState[pnode->GetId()];
         st.address = pnode->addr;
         st.name = pnode->GetAddrName();
@@ -433,7 +433,7 @@ void PeerLogicValidation::InitializeNode(CNode* pnode) {
 
 void PeerLogicValidation::FinalizeNode(NodeId id, bool& fUpdateConnectionTime) {
     fUpdateConnectionTime = false;
-    std::lock_guard<std::recursive_mutex> l(impl->csMain());
+    std::lock_guard<CCriticalSection> l(impl->csMain());
     CNodeState* st = impl->State(id);
     if (!st) return;
     if (st->fSyncStarted) impl->nSyncStarted--;
@@ -453,7 +453,7 @@ void PeerLogicValidation::FinalizeNode(NodeId id, bool& fUpdateConnectionTime) {
 }
 
 bool PeerLogicValidation::GetNodeStateStats(NodeId id, CNodeStateStats& stats) {
-    std::lock_guard<std::recursive_mutex> l(impl->csMain());
+    std::lock_guard<CCriticalSection> l(impl->csMain());
     CNodeState* st = impl->State(id);
     if (!st) return false;
     stats.nMisbehavior = st->nMisbehavior;
@@ -465,7 +465,7 @@ bool PeerLogicValidation::GetNodeStateStats(NodeId id, CNodeStateStats& stats) {
 }
 
 void PeerLogicValidation::Misbehaving(NodeId id, int howmuch, const std::string& reason) {
-    std::lock_guard<std::recursive_mutex> l(impl->csMain());
+    std::lock_guard<CCriticalSection> l(impl->csMain());
     impl->MisbehavingLocked(id, howmuch, reason);
 }
 
@@ -475,7 +475,7 @@ size_t PeerLogicValidation::OrphanCount() {
 }
 
 void PeerLogicValidation::RelayTransaction(const CTransaction& tx) {
-    std::lock_guard<std::recursive_mutex> l(impl->csMain());
+    std::lock_guard<CCriticalSection> l(impl->csMain());
     impl->RelayTransaction(tx);
 }
 
@@ -517,7 +517,7 @@ void PeerLogicValidation::BlockConnected(const std::shared_ptr<const CBlock>& bl
 
 void PeerLogicValidation::NewPoWValidBlock(const CBlockIndex* pindex, const std::shared_ptr<const CBlock>& pblock) {
     auto pcmpct = std::make_shared<const CBlockHeaderAndShortTxIDs>(*pblock, impl->rng.rand64());
-    std::lock_guard<std::recursive_mutex> l(impl->csMain());
+    std::lock_guard<CCriticalSection> l(impl->csMain());
     static int nHighestFastAnnounce = 0;
     if (pindex->nHeight <= nHighestFastAnnounce) return;
     nHighestFastAnnounce = pindex->nHeight;
@@ -542,7 +542,7 @@ void PeerLogicValidation::NewPoWValidBlock(const CBlockIndex* pindex, const std:
 }
 
 void PeerLogicValidation::BlockChecked(const CBlock& block, const CValidationState& state) {
-    std::lock_guard<std::recursive_mutex> l(impl->csMain());
+    std::lock_guard<CCriticalSection> l(impl->csMain());
     const uint256 hash = block.GetHash();
     auto it = impl->mapBlockSource.find(hash);
     int nDoS = 0;
@@ -593,7 +593,7 @@ void PeerLogicValidation::Impl::ProcessGetData(CNode* pfrom, std::deque<CInv>& v
     std::vector<CInv> vNotFound;
     const CNetMsgMaker msgMaker(pfrom->GetSendVersion());
     const int legacyFlag = pfrom->IsLegacyBlockHeader(pfrom->GetSendVersion()) ? SERIALIZE_BLOCK_LEGACY : 0;
-    std::lock_guard<std::recursive_mutex> l(csMain());
+    std::lock_guard<CCriticalSection> l(csMain());
     auto it = vRecvGetData.begin();
     while (it != vRecvGetData.end()) {
         if (pfrom->fPauseSend) break;
@@ -705,7 +705,7 @@ bool PeerLogicValidation::Impl::ProcessHeadersMessage(CNode* pfrom, const std::v
     bool received_new_header = false;
     const CBlockIndex* pindexLast = nullptr;
     {
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         CNodeState* st = State(pfrom->GetId());
         // unconnecting headers: ask for the gap, punish repeated offenders
         if (!cs->LookupBlockIndex(headers[0].hashPrevBlock) && nCount < MAX_BLOCKS_TO_ANNOUNCE) {
@@ -734,13 +734,13 @@ bool PeerLogicValidation::Impl::ProcessHeadersMessage(CNode* pfrom, const std::v
     if (!cs->ProcessNewBlockHeaders(headers, state, &pindexLast)) {
         int nDoS;
         if (state.IsInvalid(nDoS)) {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             if (nDoS > 0) MisbehavingLocked(pfrom->GetId(), nDoS, state.GetRejectReason());
             else if (punishDuplicateInvalid) MisbehavingLocked(pfrom->GetId(), 0, state.GetRejectReason());
             return false;
         }
     }
-    std::lock_guard<std::recursive_mutex> l(csMain());
+    std::lock_guard<CCriticalSection> l(csMain());
     CNodeState* st = State(pfrom->GetId());
     if (!st) return true;
     if (st->nUnconnectingHeaders > 0)
@@ -928,7 +928,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         pfrom->SetSendVersion(std::min(nVersion, PROTOCOL_VERSION));
         pfrom->nVersion = nVersion;
         {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             CNodeState* st = State(pfrom->GetId());
             if (st) UpdatePreferredDownload(pfrom, st);
         }
@@ -973,7 +973,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
     if (strCommand == NetMsgType::VERACK) {
         pfrom->SetRecvVersion(std::min(pfrom->nVersion.load(), PROTOCOL_VERSION));
         if (!pfrom->fInbound) {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             if (CNodeState* st = State(pfrom->GetId())) st->fCurrentlyConnected = true;
         }
         if (pfrom->nVersion >= SENDHEADERS_VERSION) Push(pfrom, msgMaker.Make(NetMsgType::SENDHEADERS));
@@ -1020,7 +1020,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
     }
 
     if (strCommand == NetMsgType::SENDHEADERS) {
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         if (CNodeState* st = State(pfrom->GetId())) st->fPreferHeaders = true;
         return true;
     }
@@ -1030,7 +1030,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         uint64_t nCMPCTBLOCKVersion = 0;
         vRecv >> fAnnounceUsingCMPCTBLOCK >> nCMPCTBLOCKVersion;
         if (nCMPCTBLOCKVersion == 1) {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             if (CNodeState* st = State(pfrom->GetId())) {
                 if (!st->fProvidesHeaderAndIDs) {
                     st->fProvidesHeaderAndIDs = true;
@@ -1051,7 +1051,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         }
         bool fBlocksOnly = gArgs.GetBoolArg("-blocksonly", false);
         if (pfrom->fWhitelisted && gArgs.GetBoolArg("-whitelistrelay", true)) fBlocksOnly = false;
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         std::vector<CInv> vToFetch;
         for (const CInv& inv : vInv) {
             if (interrupt) return true;
@@ -1099,7 +1099,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         CBlockLocator locator;
         uint256 hashStop;
         vRecv >> locator >> hashStop;
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         const CBlockIndex* pi = cs->FindForkInGlobalIndex(locator);
         if (pi) pi = cs->ActiveChain().Next(pi);
         int nLimit = MAX_GETBLOCKS_RESULTS;
@@ -1125,7 +1125,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
             std::lock_guard<std::mutex> lr(cs_most_recent);
             if (most_recent_block_hash == req.blockhash) recent = most_recent_block;
         }
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         const CBlockIndex* pi = cs->LookupBlockIndex(req.blockhash);
         if (!pi || !(pi->nStatus & BLOCK_HAVE_DATA)) {
             LogPrintf("Peer %d sent us a getblocktxn for a block we don't have\n", (int)pfrom->GetId());
@@ -1160,7 +1160,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         CBlockLocator locator;
         uint256 hashStop;
         vRecv >> locator >> hashStop;
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         if (cs->IsInitialBlockDownload() && !pfrom->fWhitelisted) {
             LogPrint(BCLog::NET, "Ignoring getheaders from peer=%d because node is in initial block download\n",
                      (int)pfrom->GetId());
@@ -1197,7 +1197,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         const CTransaction& tx = *ptx;
         const CInv inv(MSG_TX, tx.GetHash());
         pfrom->AddInventoryKnown(inv);
-        std::lock_guard<std::recursive_mutex> l(csMain());
+        std::lock_guard<CCriticalSection> l(csMain());
         bool fMissingInputs = false;
         CValidationState state;
         {
@@ -1267,7 +1267,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         vRecv >> cmpctblock;
         bool received_new_header = false;
         {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             if (!cs->LookupBlockIndex(cmpctblock.header.hashPrevBlock)) {
                 // doesn't connect: ask for headers
                 if (!cs->IsInitialBlockDownload())
@@ -1293,7 +1293,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         bool fBlockReconstructed = false;
         std::shared_ptr<CBlock> pblock = std::make_shared<CBlock>();
         {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             if (!pindex) return true;
             UpdateBlockAvailability(pfrom->GetId(), pindex->GetBlockHash());
             CNodeState* st = State(pfrom->GetId());
@@ -1369,13 +1369,13 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         if (fRevertToHeaderProcessing) return ProcessHeadersMessage(pfrom, {cmpctblock.header}, true);
         if (fBlockReconstructed) {
             {
-                std::lock_guard<std::recursive_mutex> l(csMain());
+                std::lock_guard<CCriticalSection> l(csMain());
                 mapBlockSource.emplace(pblock->GetHash(), std::make_pair(pfrom->GetId(), false));
             }
             bool fNewBlock = false;
             cs->ProcessNewBlock(pblock, true, &fNewBlock);
             if (fNewBlock) pfrom->nLastBlockTime = GetTime();
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             if (pindex->IsValid(BLOCK_VALID_TRANSACTIONS)) MarkBlockAsReceived(pblock->GetHash());
         }
         return true;
@@ -1387,7 +1387,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         std::shared_ptr<CBlock> pblock = std::make_shared<CBlock>();
         bool fBlockRead = false;
         {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             auto it = mapBlocksInFlight.find(resp.blockhash);
             if (it == mapBlocksInFlight.end() || !it->second.second->partialBlock ||
                 it->second.first != pfrom->GetId()) {
@@ -1443,7 +1443,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         bool forceProcessing = false;
         const uint256 hash = pblock->GetHash();
         {
-            std::lock_guard<std::recursive_mutex> l(csMain());
+            std::lock_guard<CCriticalSection> l(csMain());
             forceProcessing |= MarkBlockAsReceived(hash);
             mapBlockSource.emplace(hash, std::make_pair(pfrom->GetId(), true));
         }
@@ -1637,7 +1637,7 @@ bool PeerLogicValidation::Impl::SendRejectsAndCheckIfBanned(CNode* pnode) {
 bool PeerLogicValidation::ProcessMessages(CNode* pfrom, std::atomic<bool>& interrupt) {
     bool fMoreWork = false;
     {
-        std::lock_guard<std::recursive_mutex> l(impl->csMain());
+        std::lock_guard<CCriticalSection> l(impl->csMain());
         auto it = impl->mapGetData.find(pfrom->GetId());
         if (it != impl->mapGetData.end() && !it->second.empty()) impl->ProcessGetData(pfrom, it->second, interrupt);
         if (it != impl->mapGetData.end() && !it->second.empty()) return true;
@@ -1661,7 +1661,7 @@ bool PeerLogicValidation::ProcessMessages(CNode* pfrom, std::atomic<bool>& inter
         fRet = impl->ProcessMessage(pfrom, strCommand, vRecv, msg.nTime, interrupt);
         if (interrupt) return false;
         {
-            std::lock_guard<std::recursive_mutex> l(impl->csMain());
+            std::lock_guard<CCriticalSection> l(impl->csMain());
             auto it = impl->mapGetData.find(pfrom->GetId());
             if (it != impl->mapGetData.end() && !it->second.empty()) fMoreWork = true;
         }
@@ -1678,7 +1678,7 @@ bool PeerLogicValidation::ProcessMessages(CNode* pfrom, std::atomic<bool>& inter
     if (!fRet)
         LogPrint(BCLog::NET, "%s(%s, %u bytes) FAILED peer=%d\n", __func__, SanitizeString(strCommand).c_str(),
                  msg.hdr.nMessageSize, (int)pfrom->GetId());
-    std::lock_guard<std::recursive_mutex> l(impl->csMain());
+    std::lock_guard<CCriticalSection> l(impl->csMain());
     impl->SendRejectsAndCheckIfBanned(pfrom);
     return fMoreWork;
 }
@@ -1708,7 +1708,7 @@ bool PeerLogicValidation::SendMessages(CNode* pto, std::atomic<bool>& interrupt)
         }
     }
 
-    std::unique_lock<std::recursive_mutex> lockMain(I.csMain(), std::try_to_lock);
+    std::unique_lock<CCriticalSection> lockMain(I.csMain(), std::try_to_lock);
     if (!lockMain) return true; // busy validating: try again next round
     if (I.SendRejectsAndCheckIfBanned(pto)) return true;
     CNodeState* st = I.State(pto->GetId());

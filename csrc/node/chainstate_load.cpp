@@ -91,7 +91,7 @@ bool Chainstate::LoadChainTip() {
 }
 
 bool Chainstate::LoadBlockIndex(std::string& err) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     if (fReindex) return true;
     if (!LoadBlockIndexDB(err)) return false;
     if (!mapBlockIndex.empty()) {
@@ -105,7 +105,7 @@ bool Chainstate::LoadBlockIndex(std::string& err) {
 }
 
 bool Chainstate::InitBlockIndex(std::string& err) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     if (chainActive.Genesis() != nullptr) return true;
     pblocktree->WriteFlag("txindex", opts.txindex);
     try {
@@ -196,7 +196,7 @@ bool Chainstate::ReplayBlocks(std::string& err) {
 bool Chainstate::RewindBlockIndex() {
     // Blocks validated under rules that changed (none in this chain's history): only
     // verify that every connected block still carries BLOCK_VALID_SCRIPTS and undo data.
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     for (int h = 1; h <= chainActive.Height(); h++) {
         CBlockIndex* p = chainActive[h];
         if (!(p->nStatus & BLOCK_HAVE_UNDO) && !PruneMode()) {
@@ -211,7 +211,7 @@ bool Chainstate::RewindBlockIndex() {
 }
 
 bool Chainstate::VerifyDB(int nCheckLevel, int nCheckDepth) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     if (chainActive.Tip() == nullptr || chainActive.Tip()->pprev == nullptr) return true;
     if (nCheckDepth <= 0 || nCheckDepth > chainActive.Height()) nCheckDepth = chainActive.Height();
     nCheckLevel = std::max(0, std::min(4, nCheckLevel));
@@ -311,7 +311,7 @@ bool Chainstate::LoadExternalBlockFile(FILE* fileIn, CDiskBlockPos* dbp) {
             pos.nPos = (unsigned)blockPos;
         }
         {
-            std::lock_guard<std::recursive_mutex> l(cs_main);
+            std::lock_guard<CCriticalSection> l(cs_main);
             if (hash != params.GetConsensus().hashGenesisBlock && !mapBlockIndex.count(pblock->hashPrevBlock)) {
                 if (dbp) mapBlocksUnknownParent.insert(std::make_pair(pblock->hashPrevBlock, pos));
                 continue;
@@ -334,7 +334,7 @@ bool Chainstate::LoadExternalBlockFile(FILE* fileIn, CDiskBlockPos* dbp) {
                 CDiskBlockPos childPos = range.first->second;
                 auto child = std::make_shared<CBlock>();
                 if (ReadBlockFromDisk(*child, childPos, params)) {
-                    std::lock_guard<std::recursive_mutex> l(cs_main);
+                    std::lock_guard<CCriticalSection> l(cs_main);
                     CValidationState dummy;
                     if (AcceptBlock(child, dummy, nullptr, true, &childPos, nullptr)) {
                         nLoaded++;
@@ -353,7 +353,7 @@ bool Chainstate::LoadExternalBlockFile(FILE* fileIn, CDiskBlockPos* dbp) {
 
 bool Chainstate::Reindex() {
     {
-        std::lock_guard<std::recursive_mutex> l(cs_main);
+        std::lock_guard<CCriticalSection> l(cs_main);
         pblocktree->WriteReindexing(true);
         fReindex = true;
     }
@@ -367,7 +367,7 @@ bool Chainstate::Reindex() {
         LoadExternalBlockFile(f, &pos);
         fclose(f);
     }
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     pblocktree->WriteReindexing(false);
     fReindex = false;
     if (!InitBlockIndex(err)) return false;

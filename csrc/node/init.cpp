@@ -188,6 +188,7 @@ int AppMain(int argc, char* argv[]) {
             fclose(f);
         }
     }
+    if (gArgs.GetBoolArg("-debuglockorder", false)) SetLockOrderChecking(true, gArgs.GetBoolArg("-debuglockorderabort", true));
     signal(SIGTERM, HandleSIGTERM);
     signal(SIGINT, HandleSIGTERM);
     signal(SIGPIPE, SIG_IGN);

@@ -78,7 +78,7 @@ bool Chainstate::AcceptToMemoryPoolWorker(CValidationState& state, const CTransa
                          ctxState.GetDebugMessage());
     if (mempool->exists(txid)) return state.Invalid(false, REJECT_ALREADY_KNOWN_CODE, "txn-already-in-mempool");
     {
-        std::lock_guard<std::recursive_mutex> lp(mempool->cs);
+        std::lock_guard<CCriticalSection> lp(mempool->cs);
         for (const CTxIn& in : tx.vin)
             if (mempool->mapNextTx.count(in.prevout))
                 return state.Invalid(false, REJECT_CONFLICT_CODE, "txn-mempool-conflict");
@@ -88,7 +88,7 @@ bool Chainstate::AcceptToMemoryPoolWorker(CValidationState& state, const CTransa
     Amount nValueIn = 0;
     LockPoints lp;
     {
-        std::lock_guard<std::recursive_mutex> lpool(mempool->cs);
+        std::lock_guard<CCriticalSection> lpool(mempool->cs);
         CCoinsViewMemPool viewMemPool(pcoinsTip.get(), *mempool);
         view.SetBackend(viewMemPool);
         for (size_t out = 0; out < tx.vout.size(); out++) {
@@ -197,7 +197,7 @@ bool Chainstate::AcceptToMemoryPool(CValidationState& state, const CTransactionR
                                     bool* pfMissingInputs, bool fOverrideMempoolLimit, Amount nAbsurdFee,
                                     int64_t nAcceptTime, Amount* feeOut) {
     if (!mempool) return state.Error("no mempool");
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     std::vector<COutPoint> coins_to_uncache;
     const bool res = AcceptToMemoryPoolWorker(state, tx, fLimitFree, pfMissingInputs, nAcceptTime ? nAcceptTime : GetTime(),
                                               fOverrideMempoolLimit, nAbsurdFee, coins_to_uncache, feeOut);
@@ -250,7 +250,7 @@ bool Chainstate::LoadMempool(const std::string& path) {
             if (nFeeDelta) mempool->PrioritiseTransaction(tx->GetHash(), 0, nFeeDelta);
             CValidationState state;
             if (nTime + nExpiryTimeout > nNow) {
-                std::lock_guard<std::recursive_mutex> l(cs_main);
+                std::lock_guard<CCriticalSection> l(cs_main);
                 std::vector<COutPoint> unc;
                 if (AcceptToMemoryPoolWorker(state, tx, true, nullptr, nTime, false, 0, unc, nullptr)) count++;
                 else failed++;
@@ -275,7 +275,7 @@ bool Chainstate::DumpMempool(const std::string& path) {
     std::map<uint256, int64_t> mapDeltas;
     std::vector<TxMempoolInfo> vinfo;
     {
-        std::lock_guard<std::recursive_mutex> l(mempool->cs);
+        std::lock_guard<CCriticalSection> l(mempool->cs);
         for (const auto& d : mempool->GetDeltas()) mapDeltas[d.first] = d.second.second;
         vinfo = mempool->infoAll();
     }

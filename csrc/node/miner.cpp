@@ -171,9 +171,9 @@ std::unique_ptr<CBlockTemplate> BlockAssembler::CreateNewBlock(const CScript& sc
     pblock->vtx.emplace_back();
     pblocktemplate->vTxFees.push_back(-1);
     pblocktemplate->vTxSigOpsCount.push_back(-1);
-    std::lock_guard<std::recursive_mutex> l(chainstate.cs());
-    std::unique_ptr<std::lock_guard<std::recursive_mutex>> lmp;
-    if (mempool) lmp.reset(new std::lock_guard<std::recursive_mutex>(mempool->cs));
+    std::lock_guard<CCriticalSection> l(chainstate.cs());
+    std::unique_ptr<std::lock_guard<CCriticalSection>> lmp;
+    if (mempool) lmp.reset(new std::lock_guard<CCriticalSection>(mempool->cs));
     const CChainParams& chainparams = chainstate.Params();
     const Consensus::Params& cp = chainparams.GetConsensus();
     CBlockIndex* pindexPrev = chainstate.Tip();
@@ -410,7 +410,7 @@ std::vector<uint256> GenerateBlocks(Chainstate& chainstate, CTxMemPool* mempool,
     std::vector<uint256> hashes;
     int nHeight, nHeightEnd;
     {
-        std::lock_guard<std::recursive_mutex> l(chainstate.cs());
+        std::lock_guard<CCriticalSection> l(chainstate.cs());
         nHeight = chainstate.Height();
         nHeightEnd = nHeight + nGenerate;
     }
@@ -420,7 +420,7 @@ std::vector<uint256> GenerateBlocks(Chainstate& chainstate, CTxMemPool* mempool,
         std::unique_ptr<CBlockTemplate> tmpl = BlockAssembler(chainstate, mempool).CreateNewBlock(coinbaseScript);
         CBlock* pblock = &tmpl->block;
         {
-            std::lock_guard<std::recursive_mutex> l(chainstate.cs());
+            std::lock_guard<CCriticalSection> l(chainstate.cs());
             IncrementExtraNonce(pblock, chainstate.Tip(), nExtraNonce, chainstate.MaxBlockSize());
         }
         if (!SolveBlock(*pblock, params, nMaxTries, useGpu)) {

@@ -139,7 +139,7 @@ void CTxMemPool::UpdateEntryForAncestors(txiter it, const setEntries& setAncesto
 }
 
 void CTxMemPool::addUnchecked(const uint256& hash, const CTxMemPoolEntry& entry, bool validFeeEstimate) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     setEntries setAncestors;
     std::string dummy;
     const uint64_t nNoLimit = std::numeric_limits<uint64_t>::max();
@@ -149,7 +149,7 @@ void CTxMemPool::addUnchecked(const uint256& hash, const CTxMemPoolEntry& entry,
 
 void CTxMemPool::addUnchecked(const uint256& hash, const CTxMemPoolEntry& entry, setEntries& setAncestors,
                               bool validFeeEstimate) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     auto ins = mapTx.emplace(hash, std::unique_ptr<CTxMemPoolEntry>(new CTxMemPoolEntry(entry)));
     txiter newit = ins.first;
     mapLinks.emplace(newit, Links());
@@ -236,13 +236,13 @@ void CTxMemPool::removeUnchecked(txiter it, MemPoolRemovalReason reason) {
 }
 
 void CTxMemPool::RemoveStaged(setEntries& stage, bool updateDescendants, MemPoolRemovalReason reason) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     UpdateForRemoveFromMempool(stage, updateDescendants);
     for (txiter it : stage) removeUnchecked(it, reason);
 }
 
 void CTxMemPool::removeRecursive(const CTransaction& origTx, MemPoolRemovalReason reason) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     setEntries txToRemove;
     auto origit = mapTx.find(origTx.GetHash());
     if (origit != mapTx.end()) {
@@ -264,7 +264,7 @@ void CTxMemPool::removeRecursive(const CTransaction& origTx, MemPoolRemovalReaso
 void CTxMemPool::removeForReorg(const CCoinsViewCache* pcoins, unsigned nMemPoolHeight, int flags,
                                 const std::function<bool(const CTransaction&, LockPoints&, bool)>& checkLocks,
                                 const std::function<bool(const LockPoints*)>& lpValid) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     (void)flags;
     setEntries txToRemove;
     for (auto it = mapTx.begin(); it != mapTx.end(); ++it) {
@@ -292,7 +292,7 @@ void CTxMemPool::removeForReorg(const CCoinsViewCache* pcoins, unsigned nMemPool
 }
 
 void CTxMemPool::removeConflicts(const CTransaction& tx) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     for (const CTxIn& in : tx.vin) {
         auto it = mapNextTx.find(in.prevout);
         if (it == mapNextTx.end()) continue;
@@ -305,7 +305,7 @@ void CTxMemPool::removeConflicts(const CTransaction& tx) {
 }
 
 void CTxMemPool::removeForBlock(const std::vector<CTransactionRef>& vtx, unsigned nBlockHeight) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<uint256> confirmed;
     for (const auto& tx : vtx)
         if (mapTx.count(tx->GetHash())) confirmed.push_back(tx->GetHash());
@@ -324,7 +324,7 @@ void CTxMemPool::removeForBlock(const std::vector<CTransactionRef>& vtx, unsigne
 }
 
 void CTxMemPool::clear() {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     mapLinks.clear();
     mapTx.clear();
     mapNextTx.clear();
@@ -337,7 +337,7 @@ void CTxMemPool::clear() {
 }
 
 int CTxMemPool::Expire(int64_t time) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     setEntries toremove;
     for (auto it = mapTx.begin(); it != mapTx.end(); ++it)
         if (it->second->GetTime() < time) toremove.insert(it);
@@ -355,7 +355,7 @@ void CTxMemPool::trackPackageRemoved(const CFeeRate& rate) {
 }
 
 CFeeRate CTxMemPool::GetMinFee(size_t sizelimit) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     if (!blockSinceLastRollingFeeBump || rollingMinimumFeeRate == 0) return CFeeRate((Amount)rollingMinimumFeeRate);
     const int64_t time = GetTime();
     if (time > lastRollingFeeUpdate + 10) {
@@ -380,7 +380,7 @@ static double DescendantScore(const CTxMemPoolEntry& e) {
 }
 
 void CTxMemPool::TrimToSize(size_t sizelimit, std::vector<COutPoint>* pvNoSpendsRemaining) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     unsigned nTxnRemoved = 0;
     CFeeRate maxFeeRateRemoved(0);
     while (!mapTx.empty() && DynamicMemoryUsage() > sizelimit) {
@@ -456,7 +456,7 @@ void CTxMemPool::UpdateForDescendants(txiter updateIt, std::map<txiter, setEntri
 }
 
 void CTxMemPool::UpdateTransactionsFromBlock(const std::vector<uint256>& vHashesToUpdate) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::map<txiter, setEntries, IterCmp> mapMemPoolDescendantsToUpdate;
     std::set<uint256> setAlreadyIncluded(vHashesToUpdate.begin(), vHashesToUpdate.end());
     for (auto hit = vHashesToUpdate.rbegin(); hit != vHashesToUpdate.rend(); ++hit) {
@@ -477,7 +477,7 @@ void CTxMemPool::UpdateTransactionsFromBlock(const std::vector<uint256>& vHashes
 }
 
 void CTxMemPool::PrioritiseTransaction(const uint256& hash, double dPriorityDelta, Amount nFeeDelta) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     auto& d = mapDeltas[hash];
     d.first += dPriorityDelta;
     d.second += nFeeDelta;
@@ -503,44 +503,44 @@ void CTxMemPool::PrioritiseTransaction(const uint256& hash, double dPriorityDelt
 }
 
 void CTxMemPool::ApplyDeltas(const uint256& hash, double& dPriorityDelta, Amount& nFeeDelta) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     auto pos = mapDeltas.find(hash);
     if (pos == mapDeltas.end()) return;
     dPriorityDelta += pos->second.first;
     nFeeDelta += pos->second.second;
 }
 void CTxMemPool::ClearPrioritisation(const uint256& hash) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     mapDeltas.erase(hash);
 }
 std::map<uint256, std::pair<double, Amount>> CTxMemPool::GetDeltas() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return mapDeltas;
 }
 
 bool CTxMemPool::exists(const uint256& hash) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return mapTx.count(hash) > 0;
 }
 CTransactionRef CTxMemPool::get(const uint256& hash) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     auto it = mapTx.find(hash);
     return it == mapTx.end() ? nullptr : it->second->GetSharedTx();
 }
 const CTxMemPoolEntry* CTxMemPool::GetEntry(const uint256& hash) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     auto it = mapTx.find(hash);
     return it == mapTx.end() ? nullptr : it->second.get();
 }
 TxMempoolInfo CTxMemPool::info(const uint256& hash) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     auto it = mapTx.find(hash);
     if (it == mapTx.end()) return TxMempoolInfo();
     const CTxMemPoolEntry& e = *it->second;
     return TxMempoolInfo{e.GetSharedTx(), e.GetTime(), CFeeRate(e.GetFee(), e.GetTxSize()), e.GetModifiedFee() - e.GetFee()};
 }
 std::vector<TxMempoolInfo> CTxMemPool::infoAll() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<TxMempoolInfo> r;
     for (const auto* e : SortedByDepthAndScore())
         r.push_back(TxMempoolInfo{e->GetSharedTx(), e->GetTime(), CFeeRate(e->GetFee(), e->GetTxSize()),
@@ -548,7 +548,7 @@ std::vector<TxMempoolInfo> CTxMemPool::infoAll() const {
     return r;
 }
 void CTxMemPool::queryHashes(std::vector<uint256>& vtxid) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     vtxid.clear();
     for (const auto* e : SortedByDepthAndScore()) vtxid.push_back(e->GetTx().GetHash());
 }
@@ -558,16 +558,16 @@ bool CTxMemPool::HasNoInputsOf(const CTransaction& tx) const {
     return true;
 }
 bool CTxMemPool::isSpent(const COutPoint& outpoint) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return mapNextTx.count(outpoint) > 0;
 }
 const CTransaction* CTxMemPool::GetConflictTx(const COutPoint& prevout) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     auto it = mapNextTx.find(prevout);
     return it == mapNextTx.end() ? nullptr : it->second;
 }
 std::vector<const CTxMemPoolEntry*> CTxMemPool::GetAncestors(const uint256& hash) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<const CTxMemPoolEntry*> r;
     auto it = mapTx.find(hash);
     if (it == mapTx.end()) return r;
@@ -579,7 +579,7 @@ std::vector<const CTxMemPoolEntry*> CTxMemPool::GetAncestors(const uint256& hash
     return r;
 }
 std::vector<const CTxMemPoolEntry*> CTxMemPool::GetDescendants(const uint256& hash) const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<const CTxMemPoolEntry*> r;
     CTxMemPool* self = const_cast<CTxMemPool*>(this);
     auto it = self->mapTx.find(hash);
@@ -598,7 +598,7 @@ static double AncestorScore(const CTxMemPoolEntry& e) {
 }
 
 std::vector<CTxMemPool::txiter> CTxMemPool::SortedByAncestorScore() {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<txiter> v;
     v.reserve(mapTx.size());
     for (auto it = mapTx.begin(); it != mapTx.end(); ++it) v.push_back(it);
@@ -611,7 +611,7 @@ std::vector<CTxMemPool::txiter> CTxMemPool::SortedByAncestorScore() {
 }
 
 std::vector<const CTxMemPoolEntry*> CTxMemPool::SortedByDepthAndScore() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<const CTxMemPoolEntry*> v;
     for (const auto& kv : mapTx) v.push_back(kv.second.get());
     std::sort(v.begin(), v.end(), [](const CTxMemPoolEntry* a, const CTxMemPoolEntry* b) {
@@ -625,38 +625,38 @@ std::vector<const CTxMemPoolEntry*> CTxMemPool::SortedByDepthAndScore() const {
 }
 
 std::vector<CTransactionRef> CTxMemPool::AllTransactions() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     std::vector<CTransactionRef> r;
     for (const auto* e : SortedByDepthAndScore()) r.push_back(e->GetSharedTx());
     return r;
 }
 
 unsigned long CTxMemPool::size() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return mapTx.size();
 }
 uint64_t CTxMemPool::GetTotalTxSize() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return totalTxSize;
 }
 size_t CTxMemPool::DynamicMemoryUsage() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return mapTx.size() * (sizeof(CTxMemPoolEntry) + 96) + mapNextTx.size() * 80 + mapLinks.size() * 128 +
            mapDeltas.size() * 64 + cachedInnerUsage;
 }
 unsigned CTxMemPool::GetTransactionsUpdated() const {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     return nTransactionsUpdated;
 }
 void CTxMemPool::AddTransactionsUpdated(unsigned n) {
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     nTransactionsUpdated += n;
 }
 
 void CTxMemPool::check(const CCoinsViewCache* pcoins, int spendHeight) const {
     if (nCheckFrequency == 0) return;
     if (GetRandInt(1 << 30) >= (int)(nCheckFrequency >> 2)) return;
-    std::lock_guard<std::recursive_mutex> l(cs);
+    std::lock_guard<CCriticalSection> l(cs);
     uint64_t checkTotal = 0;
     CCoinsViewCache mempoolDuplicate(const_cast<CCoinsViewCache*>(pcoins));
     for (const auto& kv : mapTx) {

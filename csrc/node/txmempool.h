@@ -11,6 +11,7 @@
 #include "node/coins.h"
 #include "primitives/amount.h"
 #include "primitives/transaction.h"
+#include "util/sync.h"
 
 #include <map>
 #include <memory>
@@ -121,7 +122,7 @@ public:
     typedef std::set<txiter, IterCmp> setEntries;
 
     explicit CTxMemPool(CBlockPolicyEstimator* estimator = nullptr);
-    mutable std::recursive_mutex cs;
+    mutable CCriticalSection cs{"mempool.cs"};
 
     void addUnchecked(const uint256& hash, const CTxMemPoolEntry& entry, setEntries& setAncestors,
                       bool validFeeEstimate = true);

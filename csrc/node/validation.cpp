@@ -121,7 +121,7 @@ Chainstate::~Chainstate() {
 }
 
 void Chainstate::Shutdown() {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     CValidationState state;
     FlushStateToDisk(state, FLUSH_STATE_ALWAYS);
 }
@@ -352,7 +352,7 @@ void Chainstate::NotifyHeaderTip() {
     CBlockIndex* pindexHeader = nullptr;
     bool fNotify = false, ibd = false;
     {
-        std::lock_guard<std::recursive_mutex> l(cs_main);
+        std::lock_guard<CCriticalSection> l(cs_main);
         pindexHeader = pindexBestHeader;
         if (pindexHeader != pindexHeaderOld) {
             fNotify = true;
@@ -369,7 +369,7 @@ bool Chainstate::ProcessNewBlockHeaders(const std::vector<CBlockHeader>& headers
     std::vector<const CBlockHeader*> toCheck;
     std::vector<size_t> pos;
     {
-        std::lock_guard<std::recursive_mutex> l(cs_main);
+        std::lock_guard<CCriticalSection> l(cs_main);
         for (size_t i = 0; i < headers.size(); i++) {
             if (!IsBCPEnabled((int)headers[i].nHeight)) continue;
             if (mapBlockIndex.count(headers[i].GetHash(params.GetConsensus()))) continue;
@@ -383,7 +383,7 @@ bool Chainstate::ProcessNewBlockHeaders(const std::vector<CBlockHeader>& headers
         for (size_t j = 0; j < r.size(); j++) eqOk[pos[j]] = r[j];
     }
     {
-        std::lock_guard<std::recursive_mutex> l(cs_main);
+        std::lock_guard<CCriticalSection> l(cs_main);
         for (size_t i = 0; i < headers.size(); i++) {
             if (!eqOk[i])
                 return state.DoS(100, error("ProcessNewBlockHeaders(): Equihash solution invalid"), REJECT_INVALID,
@@ -555,7 +555,7 @@ bool Chainstate::ProcessNewBlock(const std::shared_ptr<const CBlock>& pblock, bo
         CValidationState state;
         // the expensive context-free checks (Equihash, merkle) run before taking cs_main
         bool ret = CheckBlock(*pblock, state);
-        std::lock_guard<std::recursive_mutex> l(cs_main);
+        std::lock_guard<CCriticalSection> l(cs_main);
         if (ret) ret = AcceptBlock(pblock, state, &pindex, fForceProcessing, nullptr, fNewBlock);
         CheckBlockIndex();
         if (!ret) {
@@ -576,7 +576,7 @@ bool Chainstate::ProcessNewBlock(const std::shared_ptr<const CBlock>& pblock, bo
 
 bool Chainstate::TestBlockValidity(CValidationState& state, const CBlock& block, CBlockIndex* pindexPrev, bool fCheckPOW,
                                    bool fCheckMerkleRoot) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     if (!(pindexPrev && pindexPrev == chainActive.Tip())) return state.Error("TestBlockValidity: not on tip");
     CCoinsViewCache viewNew(pcoinsTip.get());
     CBlockIndex indexDummy(block);
@@ -871,7 +871,7 @@ uint64_t Chainstate::CalculateCurrentUsage() const {
 }
 
 bool Chainstate::FlushStateToDisk(CValidationState& state, FlushStateMode mode, int nManualPruneHeight) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     const int64_t nMempoolUsage = mempool ? (int64_t)mempool->DynamicMemoryUsage() : 0;
     std::set<int> setFilesToPrune;
     bool fFlushForPrune = false;
@@ -1127,7 +1127,7 @@ bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<cons
         bool fInitialDownload;
         ConnectTrace trace;
         {
-            std::lock_guard<std::recursive_mutex> l(cs_main);
+            std::lock_guard<CCriticalSection> l(cs_main);
             CBlockIndex* pindexOldTip = chainActive.Tip();
             if (pindexMostWork == nullptr) pindexMostWork = FindMostWorkChain();
             if (pindexMostWork == nullptr || pindexMostWork == chainActive.Tip()) return true;
@@ -1157,7 +1157,7 @@ bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<cons
 
 bool Chainstate::PreciousBlock(CValidationState& state, CBlockIndex* pindex) {
     {
-        std::lock_guard<std::recursive_mutex> l(cs_main);
+        std::lock_guard<CCriticalSection> l(cs_main);
         if (pindex->nChainWork < chainActive.Tip()->nChainWork) return true;
         if (chainActive.Tip()->nChainWork > nLastPreciousChainwork) nBlockReverseSequenceId = -1;
         nLastPreciousChainwork = chainActive.Tip()->nChainWork;
@@ -1173,7 +1173,7 @@ bool Chainstate::PreciousBlock(CValidationState& state, CBlockIndex* pindex) {
 }
 
 bool Chainstate::InvalidateBlock(CValidationState& state, CBlockIndex* pindex) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     pindex->nStatus |= BLOCK_FAILED_VALID;
     setDirtyBlockIndex.insert(pindex);
     setBlockIndexCandidates.erase(pindex);
@@ -1217,7 +1217,7 @@ bool Chainstate::InvalidateBlock(CValidationState& state, CBlockIndex* pindex) {
 }
 
 bool Chainstate::ResetBlockFailureFlags(CBlockIndex* pindex) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     const int nHeight = pindex->nHeight;
     for (const auto& kv : mapBlockIndex) {
         CBlockIndex* it = kv.second;
@@ -1243,7 +1243,7 @@ bool Chainstate::ResetBlockFailureFlags(CBlockIndex* pindex) {
 // ------------------------------------------------------------------ queries
 bool Chainstate::IsInitialBlockDownload() const {
     if (latchToFalse.load(std::memory_order_relaxed)) return false;
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     if (latchToFalse.load(std::memory_order_relaxed)) return false;
     if (fReindex) return true;
     if (chainActive.Tip() == nullptr) return true;
@@ -1265,7 +1265,7 @@ CBlockIndex* Chainstate::FindForkInGlobalIndex(const CBlockLocator& locator) con
 }
 
 std::vector<const CBlockIndex*> Chainstate::GetChainTips() const {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     std::set<const CBlockIndex*> setOrphans, setPrevs;
     for (const auto& kv : mapBlockIndex) {
         if (!chainActive.Contains(kv.second)) {
@@ -1299,14 +1299,14 @@ int32_t Chainstate::ComputeBlockVersion(const CBlockIndex* pindexPrev) {
 }
 
 void Chainstate::WaitForBlockChange(int64_t timeoutMillis, const uint256& from) {
-    std::unique_lock<std::recursive_mutex> l(cs_main);
+    std::unique_lock<CCriticalSection> l(cs_main);
     auto pred = [&] { return chainActive.Tip() && chainActive.Tip()->GetBlockHash() != from; };
     if (timeoutMillis <= 0) cvBlockChange.wait(l, pred);
     else cvBlockChange.wait_for(l, std::chrono::milliseconds(timeoutMillis), pred);
 }
 
 bool Chainstate::GetTransaction(const uint256& txid, CTransactionRef& txOut, uint256& hashBlock, bool fAllowSlow) {
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     if (mempool) {
         CTransactionRef ptx = mempool->get(txid);
         if (ptx) {
@@ -1357,7 +1357,7 @@ bool Chainstate::GetTransaction(const uint256& txid, CTransactionRef& txOut, uin
 // ------------------------------------------------------------------ consistency checks
 void Chainstate::CheckBlockIndex() {
     if (!opts.checkBlockIndex) return;
-    std::lock_guard<std::recursive_mutex> l(cs_main);
+    std::lock_guard<CCriticalSection> l(cs_main);
     if (chainActive.Height() < 0) return;
     size_t nNodes = 0;
     for (const auto& kv : mapBlockIndex) {

@@ -148,7 +148,7 @@ public:
     void LimitMempoolSize(size_t limit, unsigned long age);
 
     // ---- queries
-    std::recursive_mutex& cs() const { return cs_main; }
+    CCriticalSection& cs() const { return cs_main; }
     const CChainParams& Params() const { return params; }
     CChain& ActiveChain() { return chainActive; }
     const CChain& ActiveChain() const { return chainActive; }
@@ -235,7 +235,7 @@ private:
 
     const CChainParams& params;
     ChainstateOptions opts;
-    mutable std::recursive_mutex cs_main;
+    mutable CCriticalSection cs_main{"cs_main"};
     std::condition_variable_any cvBlockChange;
 
     BlockMap mapBlockIndex;

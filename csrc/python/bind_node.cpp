@@ -40,6 +40,24 @@ void bind_node(pyb::module_& m) {
         g_pynode.reset();
     });
     m.def("node_running", []() { return (bool)g_pynode; });
+    // Lock-order detector probe (reference DEBUG_LOCKORDER): a->b then b->a in one thread.
+    m.def("lockorder_probe", []() {
+        const uint64_t before = LockOrderViolations();
+        const bool was = LockOrderChecking();
+        SetLockOrderChecking(true, false);
+        CCriticalSection a("probe.a"), b("probe.b");
+        {
+            std::lock_guard<CCriticalSection> la(a);
+            std::lock_guard<CCriticalSection> lb(b);
+        }
+        const uint64_t mid = LockOrderViolations();
+        {
+            std::lock_guard<CCriticalSection> lb(b);
+            std::lock_guard<CCriticalSection> la(a);
+        }
+        SetLockOrderChecking(was, true);
+        return pyb::make_tuple(mid - before, LockOrderViolations() - before);
+    });
     // JSON in, JSON out: {"result": ..., "error": ...}
     m.def("rpc_json", [](const std::string& method, const std::string& paramsJson) {
         std::string out;

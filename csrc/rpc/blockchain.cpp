@@ -89,26 +89,26 @@ UniValue blockToJSON(const CBlock& block, const CBlockIndex* blockindex, bool tx
 static UniValue getblockcount(const JSONRPCRequest& req) {
     if (req.params.size() != 0) ThrowRPC(RPC_INVALID_PARAMS, "getblockcount takes no arguments");
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     return cs.Height();
 }
 
 static UniValue getbestblockhash(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     return cs.Tip()->GetBlockHash().GetHex();
 }
 
 static UniValue getdifficulty(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     return GetDifficulty(cs.Tip());
 }
 
 static UniValue getblockhash(const JSONRPCRequest& req) {
     if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "getblockhash height");
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     const int nHeight = req.params[0].get_int();
     if (nHeight < 0 || nHeight > cs.Height()) ThrowRPC(RPC_INVALID_PARAMETER, "Block height out of range");
     return cs.ActiveChain()[nHeight]->GetBlockHash().GetHex();
@@ -117,7 +117,7 @@ static UniValue getblockhash(const JSONRPCRequest& req) {
 static UniValue getblockheader(const JSONRPCRequest& req) {
     if (req.params.size() < 1 || req.params.size() > 2) ThrowRPC(RPC_INVALID_PARAMS, "getblockheader \"hash\" ( verbose )");
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     const uint256 hash = uint256S(req.params[0].get_str());
     const bool fVerbose = req.params.size() > 1 && !req.params[1].isNull() ? req.params[1].get_bool() : true;
     CBlockIndex* pblockindex = cs.LookupBlockIndex(hash);
@@ -133,7 +133,7 @@ static UniValue getblockheader(const JSONRPCRequest& req) {
 static UniValue getblock(const JSONRPCRequest& req) {
     if (req.params.size() < 1 || req.params.size() > 3) ThrowRPC(RPC_INVALID_PARAMS, "getblock \"blockhash\" ( verbose legacy )");
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     const uint256 hash = uint256S(req.params[0].get_str());
     int verbosity = 1;
     if (req.params.size() > 1 && !req.params[1].isNull())
@@ -151,7 +151,7 @@ static UniValue getblock(const JSONRPCRequest& req) {
 
 static UniValue getchaintips(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     UniValue res(UniValue::VARR);
     for (const CBlockIndex* block : cs.GetChainTips()) {
         UniValue obj(UniValue::VOBJ);
@@ -199,7 +199,7 @@ static UniValue SoftForkDesc(const std::string& name, int version, const CBlockI
 
 static UniValue getblockchaininfo(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     const Consensus::Params& cp = cs.Params().GetConsensus();
     UniValue obj(UniValue::VOBJ);
     obj.pushKV("chain", cs.Params().NetworkIDString());
@@ -259,7 +259,7 @@ UniValue mempoolToJSON(bool fVerbose) {
     NodeContext& n = Node();
     CTxMemPool& pool = *n.mempool;
     if (fVerbose) {
-        std::lock_guard<std::recursive_mutex> l(pool.cs);
+        std::lock_guard<CCriticalSection> l(pool.cs);
         UniValue o(UniValue::VOBJ);
         for (const CTxMemPoolEntry* e : pool.SortedByDepthAndScore())
             o.pushKV(e->GetTx().GetHash().ToString(), entryToJSON(*e, pool, n.chainstate->Height()));
@@ -281,7 +281,7 @@ static UniValue mempoolRelatives(const JSONRPCRequest& req, bool ancestors) {
     NodeContext& n = Node();
     const uint256 hash = ParseHashV(req.params[0], "parameter 1");
     const bool fVerbose = req.params.size() > 1 && !req.params[1].isNull() && req.params[1].get_bool();
-    std::lock_guard<std::recursive_mutex> l(n.mempool->cs);
+    std::lock_guard<CCriticalSection> l(n.mempool->cs);
     if (!n.mempool->exists(hash)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Transaction not in mempool");
     auto rel = ancestors ? n.mempool->GetAncestors(hash) : n.mempool->GetDescendants(hash);
     if (!fVerbose) {
@@ -299,7 +299,7 @@ static UniValue getmempooldescendants(const JSONRPCRequest& req) { return mempoo
 static UniValue getmempoolentry(const JSONRPCRequest& req) {
     NodeContext& n = Node();
     const uint256 hash = ParseHashV(req.params[0], "parameter 1");
-    std::lock_guard<std::recursive_mutex> l(n.mempool->cs);
+    std::lock_guard<CCriticalSection> l(n.mempool->cs);
     const CTxMemPoolEntry* e = n.mempool->GetEntry(hash);
     if (!e) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Transaction not in mempool");
     return entryToJSON(*e, *n.mempool, n.chainstate->Height());
@@ -323,13 +323,13 @@ static UniValue gettxout(const JSONRPCRequest& req) {
     if (req.params.size() < 2 || req.params.size() > 3) ThrowRPC(RPC_INVALID_PARAMS, "gettxout \"txid\" n ( include_mempool )");
     NodeContext& n = Node();
     Chainstate& cs = *n.chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     const uint256 hash = ParseHashV(req.params[0], "txid");
     const COutPoint out(hash, (uint32_t)req.params[1].get_int());
     const bool fMempool = req.params.size() > 2 && !req.params[2].isNull() ? req.params[2].get_bool() : true;
     Coin coin;
     if (fMempool) {
-        std::lock_guard<std::recursive_mutex> lm(n.mempool->cs);
+        std::lock_guard<CCriticalSection> lm(n.mempool->cs);
         CCoinsViewMemPool view(&cs.CoinsTip(), *n.mempool);
         if (!view.GetCoin(out, coin) || n.mempool->isSpent(out)) return UniValue::NullUniValue;
     } else {
@@ -349,7 +349,7 @@ static UniValue gettxout(const JSONRPCRequest& req) {
 
 static UniValue gettxoutsetinfo(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     cs.FlushStateToDisk();
     std::unique_ptr<CCoinsViewCursor> pcursor = cs.CoinsDB().Cursor();
     HashWriter ss;
@@ -410,7 +410,7 @@ static UniValue preciousblock(const JSONRPCRequest& req) {
     const uint256 hash = uint256S(req.params[0].get_str());
     CBlockIndex* pindex;
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        std::lock_guard<CCriticalSection> l(cs.cs());
         pindex = cs.LookupBlockIndex(hash);
         if (!pindex) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Block not found");
     }
@@ -425,7 +425,7 @@ static UniValue invalidateblock(const JSONRPCRequest& req) {
     const uint256 hash = uint256S(req.params[0].get_str());
     CValidationState state;
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        std::lock_guard<CCriticalSection> l(cs.cs());
         CBlockIndex* pindex = cs.LookupBlockIndex(hash);
         if (!pindex) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Block not found");
         cs.InvalidateBlock(state, pindex);
@@ -439,7 +439,7 @@ static UniValue reconsiderblock(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
     const uint256 hash = uint256S(req.params[0].get_str());
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        std::lock_guard<CCriticalSection> l(cs.cs());
         CBlockIndex* pindex = cs.LookupBlockIndex(hash);
         if (!pindex) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Block not found");
         cs.ResetBlockFailureFlags(pindex);
@@ -453,7 +453,7 @@ static UniValue reconsiderblock(const JSONRPCRequest& req) {
 static UniValue pruneblockchain(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
     if (!cs.PruneMode()) ThrowRPC(RPC_MISC_ERROR, "Cannot prune blocks because node is not in prune mode.");
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     int heightParam = req.params[0].get_int();
     if (heightParam < 0) ThrowRPC(RPC_INVALID_PARAMETER, "Negative block height.");
     if (heightParam > 1000000000) {
@@ -477,7 +477,7 @@ static UniValue waitforblockimpl(const JSONRPCRequest& req, const uint256* targe
     const size_t idx = (target || targetHeight >= 0) ? 1 : 0;
     if (req.params.size() > idx && !req.params[idx].isNull()) timeout = req.params[idx].get_int();
     const int64_t deadline = GetTimeMillis() + timeout;
-    std::unique_lock<std::recursive_mutex> l(cs.cs());
+    std::unique_lock<CCriticalSection> l(cs.cs());
     const uint256 start = cs.Tip()->GetBlockHash();
     auto done = [&] {
         if (ShutdownRequested()) return true;

@@ -48,7 +48,7 @@ static UniValue GetNetworkHashPS(int lookup, int height) {
 
 static UniValue getnetworkhashps(const JSONRPCRequest& req) {
     Chainstate& cs = *Node().chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     return GetNetworkHashPS(req.params.size() > 0 && !req.params[0].isNull() ? req.params[0].get_int() : 120,
                             req.params.size() > 1 && !req.params[1].isNull() ? req.params[1].get_int() : -1);
 }
@@ -93,7 +93,7 @@ static UniValue generatetoaddress(const JSONRPCRequest& req) {
 static UniValue getmininginfo(const JSONRPCRequest& req) {
     NodeContext& n = Node();
     Chainstate& cs = *n.chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     UniValue obj(UniValue::VOBJ);
     obj.pushKV("blocks", cs.Height());
     obj.pushKV("currentblocksize", (uint64_t)BlockAssembler(cs, n.mempool.get()).LastBlockSize());
@@ -151,7 +151,7 @@ static UniValue getblocktemplate(const JSONRPCRequest& req) {
             if (!dataval.isStr()) ThrowRPC(RPC_TYPE_ERROR, "Missing data String key for proposal");
             CBlock block;
             if (!DecodeHexBlk(block, dataval.get_str())) ThrowRPC(RPC_DESERIALIZATION_ERROR, "Block decode failed");
-            std::lock_guard<std::recursive_mutex> l(cs.cs());
+            std::lock_guard<CCriticalSection> l(cs.cs());
             const uint256 hash = block.GetHash(cs.Params().GetConsensus());
             CBlockIndex* pindex = cs.LookupBlockIndex(hash);
             if (pindex) {
@@ -186,7 +186,7 @@ static UniValue getblocktemplate(const JSONRPCRequest& req) {
             nTransactionsUpdatedLastLP = nTransactionsUpdatedLast;
         }
         int64_t checktxtime = GetTimeMillis() + 60000;
-        std::unique_lock<std::recursive_mutex> l(cs.cs());
+        std::unique_lock<CCriticalSection> l(cs.cs());
         while (cs.Tip()->GetBlockHash() == hashWatchedChain && !ShutdownRequested()) {
             cs.BlockChangeCV().wait_for(l, std::chrono::milliseconds(1000));
             if (GetTimeMillis() > checktxtime) {
@@ -201,7 +201,7 @@ static UniValue getblocktemplate(const JSONRPCRequest& req) {
     static std::unique_ptr<CBlockTemplate> pblocktemplate;
     static std::mutex csTemplate;
     std::lock_guard<std::mutex> lt(csTemplate);
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     if (pindexPrev != cs.Tip() ||
         (n.mempool->GetTransactionsUpdated() != nTransactionsUpdatedLast && GetTime() - nStart > 5)) {
         pindexPrev = nullptr;
@@ -320,7 +320,7 @@ static UniValue submitblock(const JSONRPCRequest& req) {
     const uint256 hash = blockptr->GetHash(cs.Params().GetConsensus());
     bool fBlockPresent = false;
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        std::lock_guard<CCriticalSection> l(cs.cs());
         CBlockIndex* pindex = cs.LookupBlockIndex(hash);
         if (pindex) {
             if (pindex->IsValid(BLOCK_VALID_SCRIPTS)) return "duplicate";

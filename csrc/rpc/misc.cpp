@@ -57,7 +57,7 @@ static UniValue uptime(const JSONRPCRequest& req) { return GetTime() - GetStartu
 static UniValue getinfo(const JSONRPCRequest& req) {
     NodeContext& n = Node();
     Chainstate& cs = *n.chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     UniValue obj(UniValue::VOBJ);
     obj.pushKV("version", CLIENT_VERSION);
     obj.pushKV("protocolversion", PROTOCOL_VERSION);

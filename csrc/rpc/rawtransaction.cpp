@@ -48,7 +48,7 @@ static UniValue getrawtransaction(const JSONRPCRequest& req) {
     result.pushKV("hex", strHex);
     TxToUniv(*tx, hashBlock, result, n.chainstate->Params());
     if (!hashBlock.IsNull()) {
-        std::lock_guard<std::recursive_mutex> l(n.chainstate->cs());
+        std::lock_guard<CCriticalSection> l(n.chainstate->cs());
         CBlockIndex* pindex = n.chainstate->LookupBlockIndex(hashBlock);
         if (pindex) {
             if (n.chainstate->ActiveChain().Contains(pindex)) {
@@ -172,8 +172,8 @@ static UniValue signrawtransaction(const JSONRPCRequest& req) {
     CCoinsView viewDummy;
     CCoinsViewCache view(&viewDummy);
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
-        std::lock_guard<std::recursive_mutex> lm(n.mempool->cs);
+        std::lock_guard<CCriticalSection> l(cs.cs());
+        std::lock_guard<CCriticalSection> lm(n.mempool->cs);
         CCoinsViewCache& viewChain = cs.CoinsTip();
         CCoinsViewMemPool viewMempool(&viewChain, *n.mempool);
         view.SetBackend(viewMempool);
@@ -275,7 +275,7 @@ static UniValue sendrawtransaction(const JSONRPCRequest& req) {
     if (req.params.size() > 1 && !req.params[1].isNull() && req.params[1].get_bool()) nMaxRawTxFee = 0;
     bool fHaveChain = false;
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        std::lock_guard<CCriticalSection> l(cs.cs());
         for (size_t o = 0; !fHaveChain && o < tx->vout.size(); o++)
             fHaveChain = !cs.CoinsTip().AccessCoin(COutPoint(txid, (uint32_t)o)).IsSpent();
     }
@@ -312,7 +312,7 @@ static UniValue gettxoutproof(const JSONRPCRequest& req) {
         setTxids.insert(hash);
         oneTxid = hash;
     }
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     CBlockIndex* pblockindex = nullptr;
     uint256 hashBlock;
     if (req.params.size() > 1) {
@@ -363,7 +363,7 @@ static UniValue verifytxoutproof(const JSONRPCRequest& req) {
     std::vector<uint256> vMatch;
     std::vector<unsigned> vIndex;
     if (merkleBlock.txn.ExtractMatches(vMatch, vIndex) != merkleBlock.header.hashMerkleRoot) return res;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     CBlockIndex* pindex = cs.LookupBlockIndex(merkleBlock.header.GetHash(cs.Params().GetConsensus()));
     if (!pindex || !cs.ActiveChain().Contains(pindex)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Block not found in chain");
     for (const uint256& h : vMatch) res.push_back(h.GetHex());

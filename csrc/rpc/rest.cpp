@@ -64,7 +64,7 @@ static bool rest_block(const HTTPRequest& req, HTTPReply& rep, const std::string
     if (hashStr.size() != 64 || !IsHex(hashStr)) return RESTERR(rep, 400, "Invalid hash: " + hashStr);
     const uint256 hash = uint256S(hashStr);
     Chainstate& cs = *n->chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     CBlockIndex* pindex = cs.LookupBlockIndex(hash);
     if (!pindex) return RESTERR(rep, 404, hashStr + " not found");
     if (cs.HavePruned() && !(pindex->nStatus & BLOCK_HAVE_DATA) && pindex->nTx > 0)
@@ -99,7 +99,7 @@ static bool rest_headers(const HTTPRequest& req, HTTPReply& rep, const std::stri
     if (count < 1 || count > 2000) return RESTERR(rep, 400, "Header count out of range: " + path[0]);
     if (path[1].size() != 64 || !IsHex(path[1])) return RESTERR(rep, 400, "Invalid hash: " + path[1]);
     Chainstate& cs = *n->chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     std::vector<const CBlockIndex*> headers;
     const CBlockIndex* pindex = cs.LookupBlockIndex(uint256S(path[1]));
     while (pindex != nullptr && cs.ActiveChain().Contains(pindex)) {
@@ -145,8 +145,8 @@ static bool rest_getutxos(const HTTPRequest& req, HTTPReply& rep, const std::str
     std::vector<Coin> outs;
     std::string bitmapStringRepresentation;
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
-        std::lock_guard<std::recursive_mutex> lm(n->mempool->cs);
+        std::lock_guard<CCriticalSection> l(cs.cs());
+        std::lock_guard<CCriticalSection> lm(n->mempool->cs);
         CCoinsViewMemPool viewMempool(&cs.CoinsTip(), *n->mempool);
         CCoinsView& view = fCheckMemPool ? static_cast<CCoinsView&>(viewMempool) : static_cast<CCoinsView&>(cs.CoinsTip());
         for (size_t i = 0; i < vOutPoints.size(); i++) {

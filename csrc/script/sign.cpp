@@ -6,29 +6,29 @@ typedef std::vector<unsigned char> valtype;
 
 // ------------------------------------------------------------------ keystore
 bool CBasicKeyStore::AddKeyPubKey(const CKey& key, const CPubKey& pubkey) {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     mapKeys[pubkey.GetID()] = key;
     return true;
 }
 bool CBasicKeyStore::HaveKey(const CKeyID& a) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     return mapKeys.count(a) > 0;
 }
 bool CBasicKeyStore::GetKey(const CKeyID& a, CKey& out) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     auto it = mapKeys.find(a);
     if (it == mapKeys.end()) return false;
     out = it->second;
     return true;
 }
 std::set<CKeyID> CBasicKeyStore::GetKeys() const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     std::set<CKeyID> r;
     for (const auto& kv : mapKeys) r.insert(kv.first);
     return r;
 }
 bool CBasicKeyStore::GetPubKey(const CKeyID& a, CPubKey& out) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     CKey k;
     if (GetKey(a, k)) {
         out = k.GetPubKey();
@@ -41,16 +41,16 @@ bool CBasicKeyStore::GetPubKey(const CKeyID& a, CPubKey& out) const {
 }
 bool CBasicKeyStore::AddCScript(const CScript& s) {
     if (s.size() > (size_t)MAX_SCRIPT_ELEMENT_SIZE) return false; // redeemScript must be pushable
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     mapScripts[CScriptID(s)] = s;
     return true;
 }
 bool CBasicKeyStore::HaveCScript(const CScriptID& h) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     return mapScripts.count(h) > 0;
 }
 bool CBasicKeyStore::GetCScript(const CScriptID& h, CScript& out) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     auto it = mapScripts.find(h);
     if (it == mapScripts.end()) return false;
     out = it->second;
@@ -65,25 +65,25 @@ static bool ExtractPubKey(const CScript& dest, CPubKey& pubKeyOut) {
     return pubKeyOut.IsFullyValid();
 }
 bool CBasicKeyStore::AddWatchOnly(const CScript& dest) {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     setWatchOnly.insert(dest);
     CPubKey pk;
     if (ExtractPubKey(dest, pk)) mapWatchKeys[pk.GetID()] = pk;
     return true;
 }
 bool CBasicKeyStore::RemoveWatchOnly(const CScript& dest) {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     setWatchOnly.erase(dest);
     CPubKey pk;
     if (ExtractPubKey(dest, pk)) mapWatchKeys.erase(pk.GetID());
     return true;
 }
 bool CBasicKeyStore::HaveWatchOnly(const CScript& dest) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     return setWatchOnly.count(dest) > 0;
 }
 bool CBasicKeyStore::HaveWatchOnly() const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     return !setWatchOnly.empty();
 }
 

@@ -4,6 +4,7 @@
 // DummySignatureCreator (72-byte placeholder sigs for fee estimation),
 // ProduceSignature/SignSignature/CombineSignatures, default SIGHASH_ALL|FORKID in callers).
 #pragma once
+#include "util/sync.h"
 #include "keys/key.h"
 #include "script/interpreter.h"
 #include "script/standard.h"
@@ -48,7 +49,7 @@ public:
     bool HaveWatchOnly() const override;
 
 protected:
-    mutable std::recursive_mutex cs_KeyStore;
+    mutable CCriticalSection cs_KeyStore{"cs_KeyStore"};
     std::map<CKeyID, CKey> mapKeys;
     std::map<CKeyID, CPubKey> mapWatchKeys;
     std::map<CScriptID, CScript> mapScripts;

@@ -215,7 +215,7 @@ void ShrinkDebugFile() {
 ArgsManager gArgs;
 
 void ArgsManager::ParseParameters(int argc, const char* const argv[]) {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     mapArgs.clear();
     mapMultiArgs.clear();
     for (int i = 1; i < argc; i++) {
@@ -240,7 +240,7 @@ void ArgsManager::ParseParameters(int argc, const char* const argv[]) {
 bool ArgsManager::ReadConfigFile(const std::string& path) {
     std::ifstream f(path);
     if (!f.good()) return false;
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     std::string line;
     while (std::getline(f, line)) {
         const size_t hash = line.find('#');
@@ -258,48 +258,48 @@ bool ArgsManager::ReadConfigFile(const std::string& path) {
 }
 
 std::vector<std::string> ArgsManager::GetArgs(const std::string& a) const {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     auto it = mapMultiArgs.find(a);
     return it == mapMultiArgs.end() ? std::vector<std::string>() : it->second;
 }
 bool ArgsManager::IsArgSet(const std::string& a) const {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     return mapArgs.count(a) > 0;
 }
 std::string ArgsManager::GetArg(const std::string& a, const std::string& d) const {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     auto it = mapArgs.find(a);
     return it == mapArgs.end() ? d : it->second;
 }
 int64_t ArgsManager::GetArg(const std::string& a, int64_t d) const {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     auto it = mapArgs.find(a);
     return it == mapArgs.end() ? d : atoi64(it->second);
 }
 static bool InterpretBool(const std::string& v) { return v.empty() ? true : atoi64(v) != 0; }
 bool ArgsManager::GetBoolArg(const std::string& a, bool d) const {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     auto it = mapArgs.find(a);
     return it == mapArgs.end() ? d : InterpretBool(it->second);
 }
 bool ArgsManager::SoftSetArg(const std::string& a, const std::string& v) {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     if (mapArgs.count(a)) return false;
     ForceSetArg(a, v);
     return true;
 }
 bool ArgsManager::SoftSetBoolArg(const std::string& a, bool v) { return SoftSetArg(a, v ? "1" : "0"); }
 void ArgsManager::ForceSetArg(const std::string& a, const std::string& v) {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     mapArgs[a] = v;
     mapMultiArgs[a] = {v};
 }
 void ArgsManager::ForceSetMultiArg(const std::string& a, const std::string& v) {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     mapMultiArgs[a].push_back(v);
 }
 void ArgsManager::ClearArg(const std::string& a) {
-    std::lock_guard<std::recursive_mutex> l(cs_args);
+    std::lock_guard<CCriticalSection> l(cs_args);
     mapArgs.erase(a);
     mapMultiArgs.erase(a);
 }

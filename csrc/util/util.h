@@ -6,6 +6,7 @@
 // median of up to 200 peer offsets, +-70 minute cap), src/checkqueue.h (worker pool,
 // replaced here by ParallelFor), src/scheduler.{h,cpp}.
 #pragma once
+#include "util/sync.h"
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -79,7 +80,7 @@ public:
     const std::map<std::string, std::string>& Args() const { return mapArgs; }
 
 private:
-    mutable std::recursive_mutex cs_args;
+    mutable CCriticalSection cs_args;
     std::map<std::string, std::string> mapArgs;
     std::map<std::string, std::vector<std::string>> mapMultiArgs;
 };

@@ -95,7 +95,7 @@ static bool DecryptKey(const CKeyingMaterial& masterKey, const std::vector<unsig
 }
 
 bool CCryptoKeyStore::SetCrypted() {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (fUseCrypto) return true;
     if (!mapKeys.empty()) return false;
     fUseCrypto = true;
@@ -103,20 +103,20 @@ bool CCryptoKeyStore::SetCrypted() {
 }
 
 bool CCryptoKeyStore::IsLocked() const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     return fUseCrypto && vMasterKey.empty();
 }
 
 bool CCryptoKeyStore::Lock() {
     if (!SetCrypted()) return false;
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     std::fill(vMasterKey.begin(), vMasterKey.end(), 0);
     vMasterKey.clear();
     return true;
 }
 
 bool CCryptoKeyStore::Unlock(const CKeyingMaterial& masterKeyIn) {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!SetCrypted()) return false;
     bool keyPass = false, keyFail = false;
     for (const auto& kv : mapCryptedKeys) {
@@ -139,7 +139,7 @@ bool CCryptoKeyStore::Unlock(const CKeyingMaterial& masterKeyIn) {
 }
 
 bool CCryptoKeyStore::AddKeyPubKey(const CKey& key, const CPubKey& pubkey) {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!IsCrypted()) return CBasicKeyStore::AddKeyPubKey(key, pubkey);
     if (IsLocked()) return false;
     std::vector<unsigned char> crypted;
@@ -149,20 +149,20 @@ bool CCryptoKeyStore::AddKeyPubKey(const CKey& key, const CPubKey& pubkey) {
 }
 
 bool CCryptoKeyStore::AddCryptedKey(const CPubKey& pubkey, const std::vector<unsigned char>& crypted) {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!SetCrypted()) return false;
     mapCryptedKeys[pubkey.GetID()] = {pubkey, crypted};
     return true;
 }
 
 bool CCryptoKeyStore::HaveKey(const CKeyID& address) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!IsCrypted()) return CBasicKeyStore::HaveKey(address);
     return mapCryptedKeys.count(address) > 0;
 }
 
 bool CCryptoKeyStore::GetKey(const CKeyID& address, CKey& keyOut) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!IsCrypted()) return CBasicKeyStore::GetKey(address, keyOut);
     auto it = mapCryptedKeys.find(address);
     if (it == mapCryptedKeys.end() || vMasterKey.empty()) return false;
@@ -170,7 +170,7 @@ bool CCryptoKeyStore::GetKey(const CKeyID& address, CKey& keyOut) const {
 }
 
 bool CCryptoKeyStore::GetPubKey(const CKeyID& address, CPubKey& out) const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!IsCrypted()) return CBasicKeyStore::GetPubKey(address, out);
     auto it = mapCryptedKeys.find(address);
     if (it != mapCryptedKeys.end()) {
@@ -182,7 +182,7 @@ bool CCryptoKeyStore::GetPubKey(const CKeyID& address, CPubKey& out) const {
 }
 
 std::set<CKeyID> CCryptoKeyStore::GetKeys() const {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!IsCrypted()) return CBasicKeyStore::GetKeys();
     std::set<CKeyID> s;
     for (const auto& kv : mapCryptedKeys) s.insert(kv.first);
@@ -190,7 +190,7 @@ std::set<CKeyID> CCryptoKeyStore::GetKeys() const {
 }
 
 bool CCryptoKeyStore::EncryptKeys(const CKeyingMaterial& masterKeyIn) {
-    std::lock_guard<std::recursive_mutex> l(cs_KeyStore);
+    std::lock_guard<CCriticalSection> l(cs_KeyStore);
     if (!mapCryptedKeys.empty() || IsCrypted()) return false;
     fUseCrypto = true;
     for (const auto& kv : mapKeys) {

@@ -90,7 +90,7 @@ static UniValue getnewaddress(const JSONRPCRequest& req) {
     if (req.params.size() > 1) ThrowRPC(RPC_INVALID_PARAMS, "getnewaddress ( \"account\" )");
     std::string account;
     if (!req.params.empty() && !req.params[0].isNull()) account = AccountFromValue(req.params[0]);
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     if (!w.IsLocked()) w.TopUpKeyPool();
     CPubKey pub;
     if (!w.GetKeyFromPool(pub)) ThrowRPC(RPC_WALLET_KEYPOOL_RAN_OUT, "Error: Keypool ran out, please call keypoolrefill first");
@@ -110,7 +110,7 @@ static UniValue getaccountaddress(const JSONRPCRequest& req) {
 static UniValue getrawchangeaddress(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() > 1) ThrowRPC(RPC_INVALID_PARAMS, "getrawchangeaddress");
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     if (!w.IsLocked()) w.TopUpKeyPool();
     CReserveKey rk(&w);
     CPubKey pub;
@@ -125,7 +125,7 @@ static UniValue setaccount(const JSONRPCRequest& req) {
     const CTxDestination d = ParseDest(req.params[0].get_str());
     std::string account;
     if (req.params.size() > 1) account = AccountFromValue(req.params[1]);
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     if (!IsMine(w, d)) ThrowRPC(RPC_MISC_ERROR, "setaccount can only be used with own address");
     w.SetAddressBook(d, account, "receive");
     return UniValue::NullUniValue;
@@ -135,7 +135,7 @@ static UniValue getaccount(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "getaccount \"address\"");
     const CTxDestination d = ParseDest(req.params[0].get_str());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     return LabelOf(w, d);
 }
 
@@ -350,8 +350,8 @@ static UniValue fundrawtransaction(const JSONRPCRequest& req) {
 static UniValue getbalance(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() > 3) ThrowRPC(RPC_INVALID_PARAMS, "getbalance ( \"account\" minconf include_watchonly )");
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     if (req.params.empty()) return ValueFromAmount(w.GetBalance());
     int nMinDepth = 1;
     if (req.params.size() > 1 && !req.params[1].isNull()) nMinDepth = req.params[1].get_int();
@@ -385,7 +385,7 @@ static UniValue getunconfirmedbalance(const JSONRPCRequest& req) {
 
 static Amount ReceivedByDests(CWallet& w, const std::set<CScript>& scripts, int nMinDepth) {
     Amount n = 0;
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     for (const auto& kv : w.mapWallet) {
         const CWalletTx& wtx = kv.second;
         if (wtx.IsCoinBase() || !IsFinalTx(*wtx.tx, GetNode()->chainstate->Height() + 1, GetAdjustedTime())) continue;
@@ -430,7 +430,7 @@ static UniValue ListReceived(CWallet& w, const UniValue& params, bool fByAccount
         std::vector<uint256> txids;
         bool fIsWatchonly = false;
     };
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     std::map<CTxDestination, Tally> mapTally;
     for (const auto& kv : w.mapWallet) {
         const CWalletTx& wtx = kv.second;
@@ -580,8 +580,8 @@ static UniValue listtransactions(const JSONRPCRequest& req) {
     if (req.params.size() > 3 && !req.params[3].isNull() && req.params[3].get_bool()) filter = filter | ISMINE_WATCH_ONLY;
     if (nCount < 0) ThrowRPC(RPC_INVALID_PARAMETER, "Negative count");
     if (nFrom < 0) ThrowRPC(RPC_INVALID_PARAMETER, "Negative from");
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     UniValue ret(UniValue::VARR);
     // newest first, then reverse the window (reference semantics)
     for (auto it = w.wtxOrdered.rbegin(); it != w.wtxOrdered.rend(); ++it) {
@@ -607,8 +607,8 @@ static UniValue listaccounts(const JSONRPCRequest& req) {
     isminefilter includeWatchonly = ISMINE_SPENDABLE;
     if (req.params.size() > 1 && !req.params[1].isNull() && req.params[1].get_bool())
         includeWatchonly = includeWatchonly | ISMINE_WATCH_ONLY;
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     std::map<std::string, Amount> mapAccountBalances;
     for (const auto& kv : w.mapAddressBook)
         if (IsMine(w, kv.first) & includeWatchonly) mapAccountBalances[kv.second.name] = 0;
@@ -636,8 +636,8 @@ static UniValue listsinceblock(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() > 3) ThrowRPC(RPC_INVALID_PARAMS, "listsinceblock ( \"blockhash\" target_confirmations include_watchonly)");
     Chainstate& cs = *GetNode()->chainstate;
-    std::lock_guard<std::recursive_mutex> lm(cs.cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(cs.cs());
+    WalletLock l(w);
     const CBlockIndex* pindex = nullptr;
     int target_confirms = 1;
     isminefilter filter = ISMINE_SPENDABLE;
@@ -670,8 +670,8 @@ static UniValue gettransaction(const JSONRPCRequest& req) {
     const uint256 hash = ParseHashV(req.params[0], "txid");
     isminefilter filter = ISMINE_SPENDABLE;
     if (req.params.size() > 1 && !req.params[1].isNull() && req.params[1].get_bool()) filter = filter | ISMINE_WATCH_ONLY;
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     auto it = w.mapWallet.find(hash);
     if (it == w.mapWallet.end()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid or non-wallet transaction id");
     const CWalletTx& wtx = it->second;
@@ -694,8 +694,8 @@ static UniValue abandontransaction(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "abandontransaction \"txid\"");
     const uint256 hash = ParseHashV(req.params[0], "txid");
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     if (!w.mapWallet.count(hash)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid or non-wallet transaction id");
     if (!w.AbandonTransaction(hash)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Transaction not eligible for abandonment");
     return UniValue::NullUniValue;
@@ -718,8 +718,8 @@ static UniValue listunspent(const JSONRPCRequest& req) {
     }
     bool include_unsafe = true;
     if (req.params.size() > 3 && !req.params[3].isNull()) include_unsafe = req.params[3].get_bool();
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     std::vector<COutput> vecOutputs;
     w.AvailableCoins(vecOutputs, !include_unsafe, nullptr, true);
     UniValue results(UniValue::VARR);
@@ -788,8 +788,8 @@ static UniValue listlockunspent(const JSONRPCRequest& req) {
 static UniValue listaddressgroupings(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (!req.params.empty()) ThrowRPC(RPC_INVALID_PARAMS, "listaddressgroupings");
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     UniValue jsonGroupings(UniValue::VARR);
     std::map<CTxDestination, Amount> balances = w.GetAddressBalances();
     for (const std::set<CTxDestination>& grouping : w.GetAddressGroupings()) {
@@ -816,7 +816,7 @@ static UniValue move(const JSONRPCRequest& req) {
     if (nAmount <= 0) ThrowRPC(RPC_TYPE_ERROR, "Invalid amount for send");
     std::string comment;
     if (req.params.size() > 4) comment = req.params[4].get_str();
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     const int64_t nNow = GetAdjustedTime();
     CAccountingEntry debit;
     debit.nOrderPos = w.IncOrderPosNext();
@@ -841,8 +841,8 @@ static UniValue move(const JSONRPCRequest& req) {
 static UniValue getwalletinfo(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (!req.params.empty()) ThrowRPC(RPC_INVALID_PARAMS, "getwalletinfo");
-    std::lock_guard<std::recursive_mutex> lm(GetNode()->chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(GetNode()->chainstate->cs());
+    WalletLock l(w);
     UniValue obj(UniValue::VOBJ);
     obj.pushKV("walletname", w.GetName());
     obj.pushKV("walletversion", WALLET_FEATURE_LATEST);
@@ -893,7 +893,7 @@ static void ScheduleRelock(CWallet& w, int64_t nSleepTime) {
     if (n && n->scheduler)
         n->scheduler->ScheduleFromNow(
             [&w, when] {
-                std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+                WalletLock l(w);
                 if (w.nRelockTime == when) {
                     w.Lock();
                     w.nRelockTime = 0;
@@ -930,7 +930,7 @@ static UniValue walletlock(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (w.IsCrypted() && !req.params.empty()) ThrowRPC(RPC_INVALID_PARAMS, "walletlock");
     if (!w.IsCrypted()) ThrowRPC(RPC_WALLET_WRONG_ENC_STATE, "Error: running with an unencrypted wallet, but walletlock was called.");
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     w.Lock();
     w.nRelockTime = 0;
     return UniValue::NullUniValue;
@@ -977,7 +977,7 @@ static void RescanFromGenesis(CWallet& w, int64_t nTimeBegin = 0) {
     Chainstate& cs = *GetNode()->chainstate;
     const CBlockIndex* start;
     {
-        std::lock_guard<std::recursive_mutex> lm(cs.cs());
+        std::lock_guard<CCriticalSection> lm(cs.cs());
         start = cs.ActiveChain().Genesis();
         if (nTimeBegin > 0) {
             const CBlockIndex* t = cs.ActiveChain().FindEarliestAtLeast(nTimeBegin - 7200);
@@ -1001,7 +1001,7 @@ static UniValue importprivkey(const JSONRPCRequest& req) {
     const CPubKey pub = key.GetPubKey();
     const CKeyID vchAddress = pub.GetID();
     {
-        std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+        WalletLock l(w);
         w.SetAddressBook(vchAddress, label, "receive");
         if (w.HaveKey(vchAddress)) return UniValue::NullUniValue;
         w.mapKeyMetadata[vchAddress].nCreateTime = 1;
@@ -1038,7 +1038,7 @@ static UniValue importaddress(const JSONRPCRequest& req) {
     const std::string s = req.params[0].get_str();
     const CTxDestination d = DecodeDestination(s, P());
     {
-        std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+        WalletLock l(w);
         if (d.IsValid()) {
             if (fP2SH) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Cannot use the p2sh flag with an address - use a script instead");
             ImportScript(w, GetScriptForDestination(d), label, false);
@@ -1065,7 +1065,7 @@ static UniValue importpubkey(const JSONRPCRequest& req) {
     const CPubKey pub(data.begin(), data.end());
     if (!pub.IsFullyValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Pubkey is not a valid public key");
     {
-        std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+        WalletLock l(w);
         ImportScript(w, GetScriptForDestination(pub.GetID()), label, false);
         ImportScript(w, GetScriptForRawPubKey(pub), label, false);
     }
@@ -1130,8 +1130,8 @@ static UniValue dumpwallet(const JSONRPCRequest& req) {
     std::ofstream file(req.params[0].get_str());
     if (!file.is_open()) ThrowRPC(RPC_INVALID_PARAMETER, "Cannot open wallet dump file");
     Chainstate& cs = *GetNode()->chainstate;
-    std::lock_guard<std::recursive_mutex> lm(cs.cs());
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    std::lock_guard<CCriticalSection> lm(cs.cs());
+    WalletLock l(w);
     std::map<CKeyID, int64_t> mapKeyBirth;
     for (const CKeyID& id : w.GetKeys()) {
         auto it = w.mapKeyMetadata.find(id);
@@ -1200,7 +1200,7 @@ static UniValue importwallet(const JSONRPCRequest& req) {
         if (!key.IsValid()) continue;
         const CPubKey pub = key.GetPubKey();
         const CKeyID keyid = pub.GetID();
-        std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+        WalletLock l(w);
         if (w.HaveKey(keyid)) continue;
         const int64_t nTime = DecodeDumpTime(v[1]);
         std::string label;
@@ -1264,7 +1264,7 @@ static UniValue importmulti(const JSONRPCRequest& req) {
             }
             if (!internal && !dest.IsValid() && !spk.isObject())
                 ThrowRPC(RPC_INVALID_PARAMETER, "Internal must be set for hex scriptPubKey");
-            std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+            WalletLock l(w);
             if (d.exists("redeemscript")) {
                 const std::vector<unsigned char> rs = ParseHex(d["redeemscript"].get_str());
                 w.AddCScript(CScript(rs.begin(), rs.end()));
@@ -1329,7 +1329,7 @@ static UniValue importprunedfunds(const JSONRPCRequest& req) {
     std::vector<uint256> vMatch;
     std::vector<unsigned int> vIndex;
     Chainstate& cs = *GetNode()->chainstate;
-    std::lock_guard<std::recursive_mutex> lm(cs.cs());
+    std::lock_guard<CCriticalSection> lm(cs.cs());
     if (mb.txn.ExtractMatches(vMatch, vIndex) != mb.header.hashMerkleRoot)
         ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Something wrong with merkleblock");
     const CBlockIndex* pi = cs.LookupBlockIndex(mb.header.GetHash());
@@ -1338,7 +1338,7 @@ static UniValue importprunedfunds(const JSONRPCRequest& req) {
     for (size_t i = 0; i < vMatch.size(); i++)
         if (vMatch[i] == tx->GetHash()) txnIndex = (int)vIndex[i];
     if (txnIndex < 0) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Transaction given doesn't exist in proof");
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     if (!w.IsMine(*tx)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "No addresses in wallet correspond to included transaction");
     CWalletTx wtx(&w, tx);
     wtx.hashBlock = pi->GetBlockHash();
@@ -1351,7 +1351,7 @@ static UniValue removeprunedfunds(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "removeprunedfunds \"txid\"");
     const uint256 h = ParseHashV(req.params[0], "txid");
-    std::lock_guard<std::recursive_mutex> l(w.cs_wallet);
+    WalletLock l(w);
     auto it = w.mapWallet.find(h);
     if (it == w.mapWallet.end()) ThrowRPC(RPC_INVALID_PARAMETER, "Transaction does not exist in wallet.");
     for (auto o = w.wtxOrdered.begin(); o != w.wtxOrdered.end();) {

@@ -96,11 +96,16 @@ isminetype IsMine(const CKeyStore& ks, const CScript& script) {
 
 isminetype IsMine(const CKeyStore& ks, const CTxDestination& dest) { return IsMine(ks, GetScriptForDestination(dest)); }
 
+WalletLock::WalletLock(const CWallet& w) {
+    if (w.chainstate) m = std::unique_lock<CCriticalSection>(w.chainstate->cs());
+    l = std::unique_lock<CCriticalSection>(w.cs_wallet);
+}
+
 // ------------------------------------------------------------------ CWalletTx
 int CWalletTx::GetDepthInMainChain(const CBlockIndex** ppindex) const {
     if (hashBlock.IsNull() || IsAbandoned() || !pwallet || !pwallet->chainstate) return 0;
     Chainstate& cs = *pwallet->chainstate;
-    std::lock_guard<std::recursive_mutex> l(cs.cs());
+    std::lock_guard<CCriticalSection> l(cs.cs());
     const CBlockIndex* pi = cs.LookupBlockIndex(hashBlock);
     if (!pi || !cs.ActiveChain().Contains(pi)) return 0;
     if (ppindex) *ppindex = pi;
@@ -263,7 +268,7 @@ CWallet::~CWallet() {
 void CWallet::Flush() { db->Write(std::string("orderposnext"), nOrderPosNext, true); }
 
 bool CWallet::Load(std::string& err, bool& firstRun) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     firstRun = db->IsEmpty();
     KVIterator it(db.get());
     it.SeekToFirst();
@@ -386,7 +391,7 @@ bool CWallet::Load(std::string& err, bool& firstRun) {
 }
 
 bool CWallet::BackupWallet(const std::string& dest) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Flush();
     KVStore out(dest, false, true);
     KVBatch b;
@@ -416,7 +421,7 @@ bool CWallet::WriteKeyRecords(const CPubKey& pub, const CKey* key, const std::ve
 }
 
 bool CWallet::AddKeyPubKey(const CKey& key, const CPubKey& pubkey) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     if (!mapKeyMetadata.count(pubkey.GetID())) {
         CKeyMetadata m;
         m.nCreateTime = GetTime();
@@ -433,7 +438,7 @@ bool CWallet::AddKeyPubKey(const CKey& key, const CPubKey& pubkey) {
 
 bool CWallet::AddCryptedKey(const CPubKey& pubkey, const std::vector<unsigned char>& crypted) {
     if (!CCryptoKeyStore::AddCryptedKey(pubkey, crypted)) return false;
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     return WriteKeyRecords(pubkey, nullptr, &crypted);
 }
 
@@ -458,7 +463,7 @@ bool CWallet::AddWatchOnly(const CScript& dest, int64_t nCreateTime) {
 }
 
 bool CWallet::RemoveWatchOnly(const CScript& dest) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     if (!CBasicKeyStore::RemoveWatchOnly(dest)) return false;
     KVBatch b;
     b.Erase(K("watchs", dest));
@@ -486,7 +491,7 @@ CPubKey CWallet::DeriveNewChildKey(CKeyMetadata& metadata, CKey& secret) {
 }
 
 CPubKey CWallet::GenerateNewKey() {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     CKey secret;
     CKeyMetadata metadata;
     metadata.nCreateTime = GetTime();
@@ -509,7 +514,7 @@ CPubKey CWallet::GenerateNewHDMasterKey() {
     metadata.hdKeypath = "m";
     metadata.hdMasterKeyID = pub.GetID();
     {
-        std::lock_guard<std::recursive_mutex> l(cs_wallet);
+        WalletLock l(*this);
         mapKeyMetadata[pub.GetID()] = metadata;
         if (!AddKeyPubKey(key, pub)) throw std::runtime_error("CWallet::GenerateNewHDMasterKey: AddKeyPubKey failed");
     }
@@ -517,7 +522,7 @@ CPubKey CWallet::GenerateNewHDMasterKey() {
 }
 
 bool CWallet::SetHDMasterKey(const CPubKey& pub) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     CHDChain c;
     c.masterKeyID = pub.GetID();
     hdChain = c;
@@ -525,7 +530,7 @@ bool CWallet::SetHDMasterKey(const CPubKey& pub) {
 }
 
 bool CWallet::NewKeyPool() {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     KVBatch b;
     for (int64_t i : setKeyPool) b.Erase(K("pool", i));
     db->WriteBatch(b, true);
@@ -536,7 +541,7 @@ bool CWallet::NewKeyPool() {
 }
 
 bool CWallet::TopUpKeyPool(unsigned int kpSize) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     if (IsLocked()) return false;
     const unsigned int nTarget =
         kpSize > 0 ? kpSize : (unsigned int)std::max<int64_t>(gArgs.GetArg("-keypool", (int64_t)DEFAULT_KEYPOOL_SIZE), 0);
@@ -554,7 +559,7 @@ bool CWallet::TopUpKeyPool(unsigned int kpSize) {
 void CWallet::ReserveKeyFromKeyPool(int64_t& nIndex, CKeyPool& keypool) {
     nIndex = -1;
     keypool.vchPubKey = CPubKey();
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     if (!IsLocked()) TopUpKeyPool();
     if (setKeyPool.empty()) return;
     nIndex = *setKeyPool.begin();
@@ -566,12 +571,12 @@ void CWallet::ReserveKeyFromKeyPool(int64_t& nIndex, CKeyPool& keypool) {
 void CWallet::KeepKey(int64_t nIndex) { db->Erase(K("pool", nIndex)); }
 
 void CWallet::ReturnKey(int64_t nIndex) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     setKeyPool.insert(nIndex);
 }
 
 bool CWallet::GetKeyFromPool(CPubKey& result) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     int64_t nIndex = 0;
     CKeyPool kp;
     ReserveKeyFromKeyPool(nIndex, kp);
@@ -586,7 +591,7 @@ bool CWallet::GetKeyFromPool(CPubKey& result) {
 }
 
 int64_t CWallet::GetOldestKeyPoolTime() {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     if (setKeyPool.empty()) return GetTime();
     CKeyPool kp;
     if (!db->Read(K("pool", *setKeyPool.begin()), kp)) return GetTime();
@@ -609,7 +614,7 @@ bool CWallet::EncryptWallet(const std::string& passphrase) {
     if (!crypter.SetKeyFromPassphrase(passphrase, mk.vchSalt, mk.nDeriveIterations, mk.nDerivationMethod)) return false;
     if (!crypter.Encrypt(masterKey, mk.vchCryptedKey)) return false;
     {
-        std::lock_guard<std::recursive_mutex> l(cs_wallet);
+        WalletLock l(*this);
         mapMasterKeys[++nMasterKeyMaxID] = mk;
         db->Write(K("mkey", nMasterKeyMaxID), mk, true);
         std::set<CKeyID> plainIds;
@@ -634,7 +639,7 @@ bool CWallet::EncryptWallet(const std::string& passphrase) {
 bool CWallet::Unlock(const std::string& passphrase) {
     CCrypter crypter;
     CKeyingMaterial masterKey;
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     for (const auto& kv : mapMasterKeys) {
         if (!crypter.SetKeyFromPassphrase(passphrase, kv.second.vchSalt, kv.second.nDeriveIterations,
                                           kv.second.nDerivationMethod))
@@ -647,7 +652,7 @@ bool CWallet::Unlock(const std::string& passphrase) {
 
 bool CWallet::ChangeWalletPassphrase(const std::string& oldPass, const std::string& newPass) {
     const bool wasLocked = IsLocked();
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Lock();
     CCrypter crypter;
     CKeyingMaterial masterKey;
@@ -677,7 +682,7 @@ int64_t CWallet::IncOrderPosNext() {
 }
 
 const CWalletTx* CWallet::GetWalletTx(const uint256& hash) const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     auto it = mapWallet.find(hash);
     return it == mapWallet.end() ? nullptr : &it->second;
 }
@@ -704,7 +709,7 @@ bool CWallet::IsSpent(const uint256& hash, unsigned int n) const {
 }
 
 bool CWallet::AddToWallet(const CWalletTx& wtxIn, bool) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     const uint256 hash = wtxIn.GetHash();
     auto ret = mapWallet.insert({hash, wtxIn});
     CWalletTx& wtx = ret.first->second;
@@ -752,7 +757,7 @@ bool CWallet::AddToWallet(const CWalletTx& wtxIn, bool) {
 bool CWallet::AddToWalletIfInvolvingMe(const CTransactionRef& ptx, const CBlockIndex* pIndex, int posInBlock,
                                        bool fUpdate) {
     const CTransaction& tx = *ptx;
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     if (pIndex) {
         for (const CTxIn& in : tx.vin) {
             auto range = mapTxSpends.equal_range(in.prevout);
@@ -776,7 +781,7 @@ bool CWallet::AddToWalletIfInvolvingMe(const CTransactionRef& ptx, const CBlockI
 }
 
 bool CWallet::MarkConflicted(const uint256& hashBlock, const uint256& hashTx) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     const CBlockIndex* pi = chainstate ? chainstate->LookupBlockIndex(hashBlock) : nullptr;
     if (!pi) return false;
     std::set<uint256> todo{hashTx}, done;
@@ -801,7 +806,7 @@ bool CWallet::MarkConflicted(const uint256& hashBlock, const uint256& hashTx) {
 }
 
 bool CWallet::AbandonTransaction(const uint256& hashTx) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     auto it = mapWallet.find(hashTx);
     if (it == mapWallet.end()) return false;
     if (it->second.GetDepthInMainChain() != 0 || it->second.InMempool()) return false;
@@ -828,7 +833,7 @@ bool CWallet::AbandonTransaction(const uint256& hashTx) {
 }
 
 void CWallet::SyncTransaction(const CTransactionRef& tx, const CBlockIndex* pindex, int posInBlock) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     AddToWalletIfInvolvingMe(tx, pindex, posInBlock, true);
 }
 
@@ -836,13 +841,13 @@ void CWallet::TransactionAddedToMempool(const CTransactionRef& tx) { SyncTransac
 
 void CWallet::BlockConnected(const std::shared_ptr<const CBlock>& block, const CBlockIndex* pindex,
                              const std::vector<CTransactionRef>& conflicted) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     for (const CTransactionRef& t : conflicted) SyncTransaction(t);
     for (size_t i = 0; i < block->vtx.size(); i++) SyncTransaction(block->vtx[i], pindex, (int)i);
 }
 
 void CWallet::BlockDisconnected(const std::shared_ptr<const CBlock>& block) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     for (const CTransactionRef& t : block->vtx) SyncTransaction(t);
 }
 
@@ -850,7 +855,7 @@ void CWallet::SetBestChain(const CBlockLocator& loc) { db->Write(std::string("be
 
 std::vector<uint256> CWallet::ResendWalletTransactionsBefore(int64_t nTime) {
     std::vector<uint256> result;
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     std::multimap<unsigned int, CWalletTx*> sorted;
     for (auto& kv : mapWallet) {
         if (kv.second.nTimeReceived > nTime) continue;
@@ -875,8 +880,8 @@ void CWallet::ResendWalletTransactions(int64_t nBestBlockTime) {
 
 void CWallet::ReacceptWalletTransactions() {
     if (!fBroadcastTransactions || !chainstate) return;
-    std::lock_guard<std::recursive_mutex> lm(chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    std::lock_guard<CCriticalSection> lm(chainstate->cs());
+    WalletLock l(*this);
     std::map<int64_t, CWalletTx*> mapSorted;
     for (auto& kv : mapWallet) {
         CWalletTx& wtx = kv.second;
@@ -896,9 +901,9 @@ bool CWallet::ScanForWalletTransactions(const CBlockIndex* pindex, bool fUpdate,
     while (pindex) {
         CBlock block;
         {
-            std::lock_guard<std::recursive_mutex> lm(chainstate->cs());
+            std::lock_guard<CCriticalSection> lm(chainstate->cs());
             if (!chainstate->ReadBlock(block, pindex, false)) break;
-            std::lock_guard<std::recursive_mutex> l(cs_wallet);
+            WalletLock l(*this);
             for (size_t i = 0; i < block.vtx.size(); i++)
                 if (AddToWalletIfInvolvingMe(block.vtx[i], pindex, (int)i, fUpdate)) found++;
             pindex = chainstate->ActiveChain().Next(pindex);
@@ -910,7 +915,7 @@ bool CWallet::ScanForWalletTransactions(const CBlockIndex* pindex, bool fUpdate,
 }
 
 bool CWallet::AddAccountingEntry(const CAccountingEntry& entryIn) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     CAccountingEntry e = entryIn;
     e.nEntryNo = nAccountingEntryNumber++;
     if (!db->Write(K("acentry", std::make_pair(e.strAccount, e.nEntryNo)), e)) return false;
@@ -922,7 +927,7 @@ bool CWallet::AddAccountingEntry(const CAccountingEntry& entryIn) {
 
 // ------------------------------------------------------------------ ownership
 isminetype CWallet::IsMine(const CTxIn& txin) const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     auto it = mapWallet.find(txin.prevout.hash);
     if (it != mapWallet.end() && txin.prevout.n < it->second.tx->vout.size())
         return IsMine(it->second.tx->vout[txin.prevout.n]);
@@ -937,7 +942,7 @@ bool CWallet::IsMine(const CTransaction& tx) const {
 bool CWallet::IsFromMe(const CTransaction& tx) const { return GetDebit(tx, ISMINE_ALL) > 0; }
 
 Amount CWallet::GetDebit(const CTxIn& txin, const isminefilter& filter) const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     auto it = mapWallet.find(txin.prevout.hash);
     if (it != mapWallet.end() && txin.prevout.n < it->second.tx->vout.size())
         if (IsMine(it->second.tx->vout[txin.prevout.n]) & filter) return it->second.tx->vout[txin.prevout.n].nValue;
@@ -961,7 +966,7 @@ bool CWallet::IsChange(const CTxOut& txout) const {
     if (IsMine(txout)) {
         CTxDestination d;
         if (!ExtractDestination(txout.scriptPubKey, d)) return true;
-        std::lock_guard<std::recursive_mutex> l(cs_wallet);
+        WalletLock l(*this);
         if (!mapAddressBook.count(d)) return true;
     }
     return false;
@@ -969,14 +974,14 @@ bool CWallet::IsChange(const CTxOut& txout) const {
 Amount CWallet::GetChange(const CTxOut& txout) const { return IsChange(txout) ? txout.nValue : 0; }
 
 Amount CWallet::GetBalance() const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Amount n = 0;
     for (const auto& kv : mapWallet)
         if (kv.second.IsTrusted()) n += kv.second.GetAvailableCredit();
     return n;
 }
 Amount CWallet::GetUnconfirmedBalance() const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Amount n = 0;
     for (const auto& kv : mapWallet)
         if (!kv.second.IsTrusted() && kv.second.GetDepthInMainChain() == 0 && kv.second.InMempool())
@@ -984,20 +989,20 @@ Amount CWallet::GetUnconfirmedBalance() const {
     return n;
 }
 Amount CWallet::GetImmatureBalance() const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Amount n = 0;
     for (const auto& kv : mapWallet) n += kv.second.GetImmatureCredit();
     return n;
 }
 Amount CWallet::GetWatchOnlyBalance() const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Amount n = 0;
     for (const auto& kv : mapWallet)
         if (kv.second.IsTrusted()) n += kv.second.GetAvailableWatchOnlyCredit();
     return n;
 }
 Amount CWallet::GetUnconfirmedWatchOnlyBalance() const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Amount n = 0;
     for (const auto& kv : mapWallet)
         if (!kv.second.IsTrusted() && kv.second.GetDepthInMainChain() == 0 && kv.second.InMempool())
@@ -1005,14 +1010,14 @@ Amount CWallet::GetUnconfirmedWatchOnlyBalance() const {
     return n;
 }
 Amount CWallet::GetImmatureWatchOnlyBalance() const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Amount n = 0;
     for (const auto& kv : mapWallet) n += kv.second.GetImmatureWatchOnlyCredit();
     return n;
 }
 
 Amount CWallet::GetAccountBalance(const std::string& strAccount, int nMinDepth, const isminefilter& filter) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     Amount nBalance = 0;
     for (const auto& kv : mapWallet) {
         const CWalletTx& wtx = kv.second;
@@ -1041,7 +1046,7 @@ Amount CWallet::GetAccountBalance(const std::string& strAccount, int nMinDepth, 
 }
 
 std::set<CTxDestination> CWallet::GetAccountAddresses(const std::string& strAccount) const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     std::set<CTxDestination> r;
     for (const auto& kv : mapAddressBook)
         if (kv.second.name == strAccount) r.insert(kv.first);
@@ -1050,7 +1055,7 @@ std::set<CTxDestination> CWallet::GetAccountAddresses(const std::string& strAcco
 
 std::map<CTxDestination, Amount> CWallet::GetAddressBalances() {
     std::map<CTxDestination, Amount> balances;
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     for (const auto& kv : mapWallet) {
         const CWalletTx& wtx = kv.second;
         if (!wtx.IsTrusted()) continue;
@@ -1069,7 +1074,7 @@ std::map<CTxDestination, Amount> CWallet::GetAddressBalances() {
 }
 
 std::set<std::set<CTxDestination>> CWallet::GetAddressGroupings() {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     std::set<std::set<CTxDestination>> groupings;
     for (const auto& kv : mapWallet) {
         const CWalletTx& wtx = kv.second;
@@ -1133,7 +1138,7 @@ std::set<std::set<CTxDestination>> CWallet::GetAddressGroupings() {
 void CWallet::AvailableCoins(std::vector<COutput>& vCoins, bool fOnlyConfirmed, const CCoinControl* coinControl,
                              bool fIncludeZeroValue) const {
     vCoins.clear();
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     const int height = chainstate ? chainstate->Height() : 0;
     for (const auto& kv : mapWallet) {
         const CWalletTx& wtx = kv.second;
@@ -1335,8 +1340,8 @@ bool CWallet::CreateTransaction(const std::vector<CRecipient>& vecSend, CWalletT
     wtxNew.fTimeReceivedIsTxTime = true;
     wtxNew.pwallet = this;
     CMutableTransaction txNew;
-    std::lock_guard<std::recursive_mutex> lm(chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    std::lock_guard<CCriticalSection> lm(chainstate->cs());
+    WalletLock l(*this);
     // anti fee-sniping: lock to the current height, sometimes a bit earlier
     txNew.nLockTime = (uint32_t)chainstate->Height();
     if (GetRandInt(10) == 0) txNew.nLockTime = (uint32_t)std::max(0, (int)txNew.nLockTime - GetRandInt(100));
@@ -1460,8 +1465,8 @@ bool CWallet::CreateTransaction(const std::vector<CRecipient>& vecSend, CWalletT
 }
 
 bool CWallet::CommitTransaction(CWalletTx& wtxNew, CReserveKey& reservekey, CValidationState& state) {
-    std::lock_guard<std::recursive_mutex> lm(chainstate->cs());
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    std::lock_guard<CCriticalSection> lm(chainstate->cs());
+    WalletLock l(*this);
     LogPrintf("CommitTransaction:\n%s", wtxNew.tx->ToString().c_str());
     reservekey.KeepKey();
     wtxNew.fFromMe = true;
@@ -1516,28 +1521,28 @@ bool CWallet::FundTransaction(CMutableTransaction& tx, Amount& nFeeRet, bool ove
 }
 
 void CWallet::LockCoin(const COutPoint& o) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     setLockedCoins.insert(o);
 }
 void CWallet::UnlockCoin(const COutPoint& o) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     setLockedCoins.erase(o);
 }
 void CWallet::UnlockAllCoins() {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     setLockedCoins.clear();
 }
 bool CWallet::IsLockedCoin(const uint256& hash, unsigned int n) const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     return setLockedCoins.count(COutPoint(hash, n)) > 0;
 }
 std::vector<COutPoint> CWallet::ListLockedCoins() const {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     return std::vector<COutPoint>(setLockedCoins.begin(), setLockedCoins.end());
 }
 
 bool CWallet::SetAddressBook(const CTxDestination& address, const std::string& strName, const std::string& purpose) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     CAddressBookData& d = mapAddressBook[address];
     d.name = strName;
     if (!purpose.empty()) d.purpose = purpose;
@@ -1548,7 +1553,7 @@ bool CWallet::SetAddressBook(const CTxDestination& address, const std::string& s
 }
 
 bool CWallet::DelAddressBook(const CTxDestination& address) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     KVBatch b;
     for (const auto& kv : mapAddressBook[address].destdata) b.Erase(K("destdata", std::make_pair(DestKey{address}, kv.first)));
     mapAddressBook.erase(address);
@@ -1558,7 +1563,7 @@ bool CWallet::DelAddressBook(const CTxDestination& address) {
 }
 
 bool CWallet::GetAccountPubkey(CPubKey& pubKey, const std::string& strAccount, bool bForceNew) {
-    std::lock_guard<std::recursive_mutex> l(cs_wallet);
+    WalletLock l(*this);
     CPubKey cur;
     const bool have = db->Read(K("acc", strAccount), cur);
     bool keyUsed = false;

@@ -403,7 +403,7 @@ public:
     void SetBestChain(const CBlockLocator& loc) override;
     void ResendWalletTransactions(int64_t nBestBlockTime) override;
 
-    mutable std::recursive_mutex cs_wallet;
+    mutable CCriticalSection cs_wallet{"cs_wallet"};
     Chainstate* chainstate = nullptr;
     CTxMemPool* mempool = nullptr;
     CFeeRate payTxFee{DEFAULT_TRANSACTION_FEE};
@@ -430,6 +430,17 @@ private:
     int64_t nLastResend = 0;
     uint64_t nAccountingEntryNumber = 0;
     friend class CWalletTx;
+};
+
+// Lock order cs_main -> cs_wallet (reference LOCK2(cs_main, pwallet->cs_wallet)): wallet
+// code reads chain depth under cs_wallet, so every wallet critical section takes cs_main
+// first when the wallet is attached to a chainstate.
+class WalletLock {
+public:
+    explicit WalletLock(const CWallet& w);
+
+private:
+    std::unique_lock<CCriticalSection> m, l;
 };
 
 CWallet* GetWallet();

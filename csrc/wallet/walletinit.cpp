@@ -82,7 +82,7 @@ static bool LoadOneWallet(NodeContext& node, const std::string& name, std::strin
     // rescan from the wallet's best block (or genesis) to the tip
     const CBlockIndex* start = nullptr;
     {
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        std::lock_guard<CCriticalSection> l(cs.cs());
         CBlockLocator loc;
         if (!gArgs.GetBoolArg("-rescan", false) && !gArgs.GetBoolArg("-zapwallettxes", false) &&
             w->DB().Read(std::string("bestblock"), loc)) {
@@ -96,7 +96,7 @@ static bool LoadOneWallet(NodeContext& node, const std::string& name, std::strin
     if (start && start != cs.Tip()) {
         LogPrintf("Rescanning last %i blocks (from block %i)...\n", cs.Height() - start->nHeight, start->nHeight);
         w->ScanForWalletTransactions(start, true);
-        std::lock_guard<std::recursive_mutex> l(cs.cs());
+        std::lock_guard<CCriticalSection> l(cs.cs());
         w->SetBestChain(cs.ActiveChain().GetLocator());
     }
     w->ReacceptWalletTransactions();
@@ -137,7 +137,7 @@ bool StartWallet(NodeContext& node, std::string& err) {
         obj.pushKV("paytxfee", ValueFromAmount(w->payTxFee.GetFeePerK()));
     };
     g_walletDescribeAddress = [w](const CTxDestination& d, UniValue& ret) {
-        std::lock_guard<std::recursive_mutex> l(w->cs_wallet);
+        WalletLock l(*w);
         const isminetype mine = IsMine(*w, d);
         ret.pushKV("ismine", (mine & ISMINE_SPENDABLE) != 0);
         ret.pushKV("iswatchonly", (mine & ISMINE_WATCH_ONLY) != 0);

@@ -441,3 +441,10 @@ def test_message_hash(native):
     msg = b"hello"
     exp = sha256d(bytes([len(magic)]) + magic + bytes([len(msg)]) + msg)
     assert native.message_hash("hello") == exp
+
+
+def test_lockorder_detector(native):
+    # first order a->b is recorded silently; the reverse b->a is reported (reference sync.cpp
+    # potential_deadlock_detected)
+    first, total = native.lockorder_probe()
+    assert (first, total) == (0, 1)
