@@ -39,6 +39,7 @@ CORELIB    := build/libbcpcore.a
 CONSLIB    := lib/libbcpconsensus.so
 
 .PHONY: all pyext tools clean kernels conslib
+.DEFAULT_GOAL := all
 conslib: $(CONSLIB)
 all: pyext tools conslib
 pyext: $(PYEXT)

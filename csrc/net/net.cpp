@@ -1,4 +1,5 @@
 #include "net/net.h"
+#include "node/ui_interface.h"
 #include "consensus/params.h"
 #include "consensus/tx_verify.h"
 #include "crypto/hashes.h"
@@ -441,6 +442,7 @@ void CConnman::SetNetworkActive(bool active) {
     LogPrintf("SetNetworkActive: %s\n", active ? "true" : "false");
     if (fNetworkActive == active) return;
     fNetworkActive = active;
+    uiInterface.NotifyNetworkActiveChanged(active);
     if (!active) {
         std::lock_guard<CCriticalSection> l(cs_vNodes);
         for (CNode* p : vNodes) p->fDisconnect = true;
@@ -785,7 +787,10 @@ void CConnman::ThreadSocketHandler() {
             std::lock_guard<CCriticalSection> l(cs_vNodes);
             n = vNodes.size();
         }
-        if (n != nPrevNodeCount) nPrevNodeCount = n;
+        if (n != nPrevNodeCount) {
+            nPrevNodeCount = n;
+            uiInterface.NotifyNumConnectionsChanged((int)n);
+        }
 
         // ---- poll
         std::vector<struct pollfd> fds;
@@ -1130,17 +1135,20 @@ void CConnman::Ban(const CSubNet& sub, BanReason reason, int64_t bantime, bool s
     std::lock_guard<CCriticalSection> l(cs_vNodes);
     for (CNode* p : vNodes)
         if (sub.Match(p->addr)) p->fDisconnect = true;
+    uiInterface.BannedListChanged();
     if (reason == BanReasonManuallyAdded) DumpData();
 }
 
 bool CConnman::Unban(const CNetAddr& addr) { return Unban(CSubNet(addr)); }
 bool CConnman::Unban(const CSubNet& sub) {
     if (!banman.Unban(sub)) return false;
+    uiInterface.BannedListChanged();
     DumpData();
     return true;
 }
 void CConnman::ClearBanned() {
     banman.ClearBanned();
+    uiInterface.BannedListChanged();
     DumpData();
 }
 

@@ -4,6 +4,7 @@
 // FindFilesToPrune :3914, PruneOneBlockFile :3831, and the ReplayBlocks crash-recovery
 // of the head-blocks marker written by CCoinsViewDB::BatchWrite.
 #include "node/validation.h"
+#include "node/ui_interface.h"
 #include "consensus/pow.h"
 #include "node/signals.h"
 #include "util/strencodings.h"
@@ -221,7 +222,14 @@ bool Chainstate::VerifyDB(int nCheckLevel, int nCheckDepth) {
     CBlockIndex* pindexFailure = nullptr;
     int nGoodTransactions = 0;
     CValidationState state;
+    struct ProgressDone {
+        ~ProgressDone() { uiInterface.ShowProgress("", 100); }
+    } progressDone;
+    uiInterface.ShowProgress("Verifying blocks...", 0);
     for (CBlockIndex* pindex = chainActive.Tip(); pindex && pindex->pprev; pindex = pindex->pprev) {
+        const int pct = std::max(1, std::min(99, (int)(((double)(chainActive.Height() - pindex->nHeight)) /
+                                                        (double)nCheckDepth * (nCheckLevel >= 4 ? 50 : 100))));
+        uiInterface.ShowProgress("Verifying blocks...", pct);
         if (pindex->nHeight < chainActive.Height() - nCheckDepth) break;
         if (PruneMode() && !(pindex->nStatus & BLOCK_HAVE_DATA)) break;
         CBlock block;
@@ -258,6 +266,9 @@ bool Chainstate::VerifyDB(int nCheckLevel, int nCheckDepth) {
     if (nCheckLevel >= 4) {
         CBlockIndex* pindex = pindexState;
         while (pindex != chainActive.Tip()) {
+            uiInterface.ShowProgress("Verifying blocks...",
+                                     std::max(1, std::min(99, 100 - (int)(((double)(chainActive.Height() - pindex->nHeight)) /
+                                                                          (double)nCheckDepth * 50))));
             pindex = chainActive.Next(pindex);
             CBlock block;
             if (!ReadBlockFromDisk(block, pindex, params)) return error("VerifyDB(): *** ReadBlockFromDisk failed");

@@ -1,4 +1,5 @@
 #include "node/init.h"
+#include "node/ui_interface.h"
 #include "consensus/params.h"
 #include "kernels/gpu_api.h"
 #include "node/node.h"
@@ -45,6 +46,10 @@ std::string HelpMessage() {
         {"-par=<n>", "Number of script verification threads (0 = auto)"},
         {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
         {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 256)"},
+        {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
+        {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
+        {"-blocknotify=<cmd>", "Execute command when the best block changes (%s in cmd is replaced by block hash)"},
+        {"-alertnotify=<cmd>", "Execute command when a relevant alert is received or we see a really long fork (%s in cmd is replaced by message)"},
         {"-txindex", "Maintain a full transaction index (default: 0)"},
         {"-prune=<n>", "Reduce storage by pruning old blocks (MiB target, >= 550)"},
         {"-reindex", "Rebuild chain state and block index from the blk*.dat files on disk"},
@@ -180,6 +185,8 @@ int AppMain(int argc, char* argv[]) {
     LogPrintf("\n\n\n\n\n");
     LogPrintf("%s version %s (MI355X)\n", CLIENT_NAME, FormatFullVersion().c_str());
     LogPrintf("Using data directory %s\n", datadir.c_str());
+    noui_connect();
+    uiInterface.InitMessage.connect(SetRPCWarmupStatus);
 
     {
         const std::string pidfile = datadir + "/" + gArgs.GetArg("-pid", "bitcoincashplusd.pid");
@@ -214,10 +221,12 @@ int AppMain(int argc, char* argv[]) {
     SetUseCashAddr(gArgs.GetBoolArg("-usecashaddr", true));
     if (!ParseFeeArg("-minrelaytxfee", minRelayTxFee) || !ParseFeeArg("-dustrelayfee", dustRelayFee) ||
         !ParseFeeArg("-incrementalrelayfee", incrementalRelayFee)) {
-        LogPrintf("Error: invalid fee amount argument\n");
+        InitError("Invalid fee amount argument");
         return 1;
     }
     SetGpuSigThreshold((size_t)gArgs.GetArg("-gpusigthreshold", (int64_t)GetGpuSigThreshold()));
+    InitSignatureCache(gArgs.GetArg("-maxsigcachesize", (int64_t)DEFAULT_MAX_SIG_CACHE_SIZE));
+    InitScriptExecutionCache(gArgs.GetArg("-maxscriptcachesize", (int64_t)DEFAULT_MAX_SCRIPT_CACHE_SIZE));
     const bool useGpu = gArgs.GetBoolArg("-gpu", true) && gpu::GpuAvailable();
     LogPrintf("GPU acceleration: %s\n", useGpu ? gpu::DeviceName(0).c_str() : "disabled");
 
@@ -250,19 +259,18 @@ int AppMain(int argc, char* argv[]) {
         http.reset(new HTTPServer(ho));
         std::string err;
         if (!http->Start(err)) {
-            LogPrintf("Error: %s\n", err.c_str());
-            fprintf(stderr, "Error: %s\n", err.c_str());
+            InitError(err);
             return 1;
         }
         if (!StartHTTPRPC(*http, datadir, err)) {
-            fprintf(stderr, "Error: %s\n", err.c_str());
+            InitError(err);
             return 1;
         }
         if (gArgs.GetBoolArg("-rest", false)) StartREST(*http);
     }
 
     // ---- chainstate
-    SetRPCWarmupStatus("Loading block index...");
+    uiInterface.InitMessage("Loading block index...");
     const bool reindex = gArgs.GetBoolArg("-reindex", false) || gArgs.GetBoolArg("-reindex-chainstate", false);
     std::string err;
     std::unique_ptr<NodeContext> node;
@@ -272,43 +280,41 @@ int AppMain(int argc, char* argv[]) {
         SetNode(node.get());
         node->scheduler.reset(new Scheduler());
         if (reindex) {
-            SetRPCWarmupStatus("Reindexing blocks...");
+            uiInterface.InitMessage("Reindexing blocks...");
             if (!node->chainstate->Reindex()) {
-                LogPrintf("Error: reindex failed\n");
+                InitError("Reindex failed");
                 return 1;
             }
         } else {
             if (!node->chainstate->LoadBlockIndex(err) || !node->chainstate->InitBlockIndex(err)) {
-                LogPrintf("Error: %s\n", err.c_str());
-                fprintf(stderr, "Error: %s\n", err.c_str());
+                InitError(err);
                 return 1;
             }
         }
-        SetRPCWarmupStatus("Verifying blocks...");
+        uiInterface.InitMessage("Verifying blocks...");
         if (!node->chainstate->RewindBlockIndex()) LogPrintf("Warning: RewindBlockIndex failed\n");
         if (!node->chainstate->VerifyDB((int)gArgs.GetArg("-checklevel", (int64_t)DEFAULT_CHECKLEVEL),
                                         (int)gArgs.GetArg("-checkblocks", (int64_t)DEFAULT_CHECKBLOCKS))) {
-            LogPrintf("Error: corrupted block database detected; restart with -reindex\n");
-            fprintf(stderr, "Error: Corrupted block database detected. Please restart with -reindex.\n");
+            InitError("Corrupted block database detected. Please restart with -reindex.");
             return 1;
         }
     }
     if (gArgs.GetBoolArg("-persistmempool", true)) {
-        SetRPCWarmupStatus("Loading mempool...");
+        uiInterface.InitMessage("Loading mempool...");
         node->chainstate->LoadMempool(datadir + "/mempool.dat");
     }
-    SetRPCWarmupStatus("Loading wallet...");
+    uiInterface.InitMessage("Loading wallet...");
     if (!StartWallet(*node, err)) {
-        fprintf(stderr, "Error: %s\n", err.c_str());
+        InitError(err);
         return 1;
     }
-    SetRPCWarmupStatus("Starting network threads...");
+    uiInterface.InitMessage("Starting network threads...");
     if (!StartNetwork(*node, err)) {
-        fprintf(stderr, "Error: %s\n", err.c_str());
+        InitError(err);
         return 1;
     }
     if (!StartZMQ(*node, err)) {
-        fprintf(stderr, "Error: %s\n", err.c_str());
+        InitError(err);
         return 1;
     }
     // periodic flush + mempool expiry
@@ -320,13 +326,22 @@ int AppMain(int argc, char* argv[]) {
             }
         },
         60 * 1000);
+    // -blocknotify (reference init.cpp BlockNotifyCallback): %s = new tip hash
+    if (gArgs.IsArgSet("-blocknotify"))
+        uiInterface.NotifyBlockTip.connect([](bool ibd, const CBlockIndex* tip) {
+            if (ibd || !tip) return;
+            std::string cmd = gArgs.GetArg("-blocknotify", "");
+            ReplaceAll(cmd, "%s", tip->GetBlockHash().GetHex());
+            RunCommandAsync(cmd);
+        });
     SetRPCWarmupFinished();
-    LogPrintf("init message: Done loading\n");
+    uiInterface.InitMessage("Done loading");
 
     while (!g_signalled.load() && !ShutdownRequested()) MilliSleep(200);
 
     // ---- shutdown (reference init.cpp Shutdown(): RPC, network, wallet, mempool dump, flush)
     LogPrintf("Shutdown: In progress...\n");
+    uiInterface.NotifyBlockTip.disconnect_all();
     if (http) http->Stop();
     StopHTTPRPC(datadir);
     StopZMQ(*node);

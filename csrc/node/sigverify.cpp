@@ -8,7 +8,10 @@
 
 namespace bcp {
 
-SignatureCache::SignatureCache(size_t n) : maxEntries(n) { GetRandBytes(nonce.begin(), 32); }
+SignatureCache::SignatureCache() {
+    GetRandBytes(nonce.begin(), 32);
+    set.setup_bytes((size_t)DEFAULT_MAX_SIG_CACHE_SIZE << 20);
+}
 
 uint256 SignatureCache::Entry(const uint256& sighash, const std::vector<unsigned char>& sig,
                               const std::vector<unsigned char>& pubkey) const {
@@ -18,25 +21,16 @@ uint256 SignatureCache::Entry(const uint256& sighash, const std::vector<unsigned
     h.Finalize(r.begin());
     return r;
 }
-bool SignatureCache::Get(const uint256& e, bool erase) {
-    std::lock_guard<std::mutex> l(cs);
-    auto it = set.find(e);
-    if (it == set.end()) return false;
-    if (erase) set.erase(it);
-    return true;
-}
-void SignatureCache::Set(const uint256& e) {
-    std::lock_guard<std::mutex> l(cs);
-    if (set.size() >= maxEntries) set.erase(set.begin()); // random-ish eviction (hash order)
-    set.insert(e);
-}
-size_t SignatureCache::Size() const {
-    std::lock_guard<std::mutex> l(cs);
-    return set.size();
-}
 SignatureCache& GetSignatureCache() {
     static SignatureCache c;
     return c;
+}
+size_t InitSignatureCache(int64_t mib) {
+    mib = std::min(std::max<int64_t>(0, mib), MAX_MAX_SIG_CACHE_SIZE);
+    const size_t n = GetSignatureCache().SetupBytes((size_t)mib << 20);
+    LogPrintf("Using %zu MiB out of %zu requested for signature cache, able to store %zu elements\n",
+              (n * sizeof(uint256)) >> 20, (size_t)mib, n);
+    return n;
 }
 
 static std::atomic<size_t> g_gpuThreshold{256};

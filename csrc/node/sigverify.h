@@ -6,32 +6,37 @@
 // one batch: on the GPU when available and the batch is large enough, else on the pool.
 #pragma once
 #include "script/interpreter.h"
+#include "util/cuckoocache.h"
 #include "util/util.h"
 
 #include <unordered_set>
 
 namespace bcp {
 
+static const unsigned DEFAULT_MAX_SIG_CACHE_SIZE = 32;    // MiB (reference sigcache.h:16)
+static const int64_t MAX_MAX_SIG_CACHE_SIZE = 16384;        // MiB
+static const unsigned DEFAULT_MAX_SCRIPT_CACHE_SIZE = 32; // MiB (reference scriptcache.h:17)
+static const int64_t MAX_MAX_SCRIPT_CACHE_SIZE = 16384;
+
+// Salted cuckoo set of verified (sighash, pubkey, sig) triples.
 class SignatureCache {
 public:
-    explicit SignatureCache(size_t maxEntries = 1 << 20);
-    bool Get(const uint256& entry, bool erase);
-    void Set(const uint256& entry);
+    SignatureCache();
+    bool Get(const uint256& entry, bool erase) const { return set.contains(entry, erase); }
+    void Set(const uint256& entry) { set.insert(entry); }
     uint256 Entry(const uint256& sighash, const std::vector<unsigned char>& sig,
                   const std::vector<unsigned char>& pubkey) const;
-    void SetMaxEntries(size_t n) { maxEntries = n; }
-    size_t Size() const;
+    size_t SetupBytes(size_t bytes) { return set.setup_bytes(bytes); }
+    size_t Capacity() const { return set.capacity(); }
+    size_t Size() const { return set.count_live(); }
 
 private:
-    struct H {
-        size_t operator()(const uint256& u) const { return (size_t)u.GetUint64(0); }
-    };
     uint256 nonce;
-    size_t maxEntries;
-    mutable std::mutex cs;
-    std::unordered_set<uint256, H> set;
+    SharedCuckooSet set;
 };
 SignatureCache& GetSignatureCache();
+// -maxsigcachesize / -maxscriptcachesize (MiB); returns element capacities.
+size_t InitSignatureCache(int64_t mib);
 
 struct SigVerifyStats {
     uint64_t gpu_batches = 0, gpu_sigs = 0, cpu_sigs = 0, cache_hits = 0;

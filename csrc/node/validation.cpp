@@ -1,6 +1,7 @@
 // Chainstate engine: block/header acceptance, connect/disconnect, activation.
 // See validation.h for the parity map.
 #include "node/validation.h"
+#include "node/ui_interface.h"
 #include "consensus/merkle.h"
 #include "consensus/pow.h"
 #include "node/policy.h"
@@ -28,37 +29,50 @@ std::string FormatStateMessage(const CValidationState& state) {
                      state.GetRejectCode());
 }
 
+// Reference validation.cpp AlertNotify: UI alert + -alertnotify=<cmd> with the
+// sanitized message single-quoted in place of %s.
+void AlertNotify(const std::string& strMessage) {
+    uiInterface.NotifyAlertChanged();
+    std::string cmd = gArgs.GetArg("-alertnotify", "");
+    if (cmd.empty()) return;
+    std::string safe = SanitizeString(strMessage);
+    safe = safe.substr(0, 200);
+    ReplaceAll(cmd, "%s", "'" + safe + "'");
+    RunCommandAsync(cmd);
+}
+
 // ------------------------------------------------------------------ block-level caches
 // Script execution cache: (txid, flags) validated with all inputs (reference
 // src/script/scriptcache.cpp). Filled by mempool acceptance, consumed by ConnectBlock.
 namespace {
 struct ScriptCache {
-    std::mutex m;
-    std::unordered_set<uint256, Uint256Hasher> set;
+    SharedCuckooSet set;
     uint256 nonce;
-    ScriptCache() { GetRandBytes(nonce.begin(), 32); }
+    ScriptCache() {
+        GetRandBytes(nonce.begin(), 32);
+        set.setup_bytes((size_t)DEFAULT_MAX_SCRIPT_CACHE_SIZE << 20);
+    }
     uint256 Key(const CTransaction& tx, uint32_t flags) {
         uint256 r;
         CSHA256().Write(nonce.begin(), 32).Write(tx.GetHash().begin(), 32).Write((const unsigned char*)&flags, 4).Finalize(r.begin());
         return r;
     }
-    bool Has(const uint256& k, bool erase) {
-        std::lock_guard<std::mutex> l(m);
-        auto it = set.find(k);
-        if (it == set.end()) return false;
-        if (erase) set.erase(it);
-        return true;
-    }
-    void Add(const uint256& k) {
-        std::lock_guard<std::mutex> l(m);
-        if (set.size() > 500000) set.erase(set.begin());
-        set.insert(k);
-    }
+    bool Has(const uint256& k, bool erase) { return set.contains(k, erase); }
+    void Add(const uint256& k) { set.insert(k); }
 };
 ScriptCache& GetScriptCache() {
     static ScriptCache c;
     return c;
 }
+} // namespace
+size_t InitScriptExecutionCache(int64_t mib) {
+    mib = std::min(std::max<int64_t>(0, mib), MAX_MAX_SCRIPT_CACHE_SIZE);
+    const size_t n = GetScriptCache().set.setup_bytes((size_t)mib << 20);
+    LogPrintf("Using %zu MiB out of %zu requested for script execution cache, able to store %zu elements\n",
+              (n * sizeof(uint256)) >> 20, (size_t)mib, n);
+    return n;
+}
+namespace {
 
 // Block validation checker: script logic on the CPU pool, ECDSA deferred to a batch,
 // eager checks served from the signature cache when possible.
@@ -360,7 +374,10 @@ void Chainstate::NotifyHeaderTip() {
             pindexHeaderOld = pindexHeader;
         }
     }
-    if (fNotify) GetMainSignals().NotifyHeaderTip(pindexHeader, ibd);
+    if (fNotify) {
+        GetMainSignals().NotifyHeaderTip(pindexHeader, ibd);
+        uiInterface.NotifyHeaderTip(ibd, pindexHeader);
+    }
 }
 
 bool Chainstate::ProcessNewBlockHeaders(const std::vector<CBlockHeader>& headers, CValidationState& state,
@@ -948,8 +965,14 @@ void Chainstate::UpdateTip(CBlockIndex* pindexNew) {
                 ++nUpgraded;
             pindex = pindex->pprev;
         }
-        if (nUpgraded > 100 / 2)
+        if (nUpgraded > 100 / 2) {
             strMiscWarning = "Warning: Unknown block versions being mined! It's possible unknown rules are in effect";
+            static bool fWarned = false;
+            if (!fWarned) {
+                AlertNotify(strMiscWarning);
+                fWarned = true;
+            }
+        }
     }
     LogPrintf("UpdateTip: new best=%s height=%d version=0x%08x log2_work=%.8g tx=%lu date='%lld' cache=%.1fMiB(%utxo)\n",
               chainActive.Tip()->GetBlockHash().ToString().c_str(), chainActive.Height(), chainActive.Tip()->nVersion,
@@ -1148,7 +1171,10 @@ bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<cons
                 GetMainSignals().BlockConnected(pb.second, pb.first, conflicted);
             }
         }
-        if (pindexFork != pindexNewTip) GetMainSignals().UpdatedBlockTip(pindexNewTip, pindexFork, fInitialDownload);
+        if (pindexFork != pindexNewTip) {
+            GetMainSignals().UpdatedBlockTip(pindexNewTip, pindexFork, fInitialDownload);
+            uiInterface.NotifyBlockTip(fInitialDownload, pindexNewTip);
+        }
     } while (pindexNewTip != pindexMostWork);
     CheckBlockIndex();
     if (!FlushStateToDisk(state, FLUSH_STATE_PERIODIC)) return false;

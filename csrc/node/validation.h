@@ -86,6 +86,11 @@ struct MempoolAcceptResult {
     Amount fee = 0;
 };
 
+// -maxscriptcachesize (MiB): resize the script-execution cache; returns its capacity.
+size_t InitScriptExecutionCache(int64_t mib);
+// UI alert + -alertnotify command.
+void AlertNotify(const std::string& strMessage);
+
 class Chainstate {
 public:
     Chainstate(const CChainParams& params, const ChainstateOptions& opts);

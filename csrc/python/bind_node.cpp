@@ -1,14 +1,118 @@
 // Python bindings: embedded node (chainstate + mempool + RPC dispatch) for tests and
 // tools. The same CRPCTable serves the HTTP JSON-RPC server of bcpd.
 #include "node/node.h"
+#include "node/ui_interface.h"
 #include "python/bind.h"
 #include "rpc/server.h"
+#include "util/cuckoocache.h"
 #include "util/util.h"
+
+#include <deque>
+#include <map>
 
 namespace bcp {
 namespace py {
 
 static std::unique_ptr<NodeContext> g_pynode;
+
+// UI signal observer for tests: counts emissions per signal and remembers the last
+// values (connected on ui_track_start, removed on ui_track_stop).
+struct UITracker {
+    std::mutex m;
+    std::map<std::string, int> counts;
+    std::vector<std::string> initMessages;
+    int lastTipHeight = -1, lastHeaderHeight = -1, lastConnections = -1, lastProgress = -1;
+    std::vector<std::pair<std::function<void()>, int>> conns;
+    void bump(const char* name) {
+        std::lock_guard<std::mutex> l(m);
+        counts[name]++;
+    }
+};
+static UITracker g_ui;
+
+// Deterministic key stream for the cache simulations (splitmix64).
+struct SimRng {
+    uint64_t x;
+    uint64_t next() {
+        uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+        z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+        z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+        return z ^ (z >> 31);
+    }
+    uint256 key() {
+        uint256 k;
+        for (int i = 0; i < 4; ++i) {
+            const uint64_t v = next();
+            memcpy(k.begin() + 8 * i, &v, 8);
+        }
+        return k;
+    }
+};
+
+// Cache behaviour simulations mirroring reference src/test/cuckoocache_tests.cpp.
+static double CuckooHitRate(size_t megabytes, double load) {
+    CuckooHashSet set;
+    const size_t cap = set.setup_bytes(megabytes << 20);
+    const size_t n = (size_t)(load * cap);
+    SimRng r{1};
+    std::vector<uint256> keys(n);
+    for (auto& k : keys) k = r.key();
+    for (auto& k : keys) set.insert(k);
+    size_t hits = 0;
+    for (auto& k : keys) hits += set.contains(k, false);
+    return (double)hits / (double)n;
+}
+
+// Insert 1x capacity; erase the first quarter; insert half a capacity more. Returns
+// (hit rate of erased quarter, of the un-erased second quarter, of the fresh half).
+static std::vector<double> CuckooErase(size_t megabytes) {
+    CuckooHashSet set;
+    const size_t cap = set.setup_bytes(megabytes << 20);
+    SimRng r{2};
+    std::vector<uint256> keys(cap + cap / 2);
+    for (auto& k : keys) k = r.key();
+    for (size_t i = 0; i < cap; ++i) set.insert(keys[i]);
+    for (size_t i = 0; i < cap / 2; ++i) set.contains(keys[i], true);
+    for (size_t i = cap; i < keys.size(); ++i) set.insert(keys[i]);
+    size_t erased = 0, stale = 0, fresh = 0;
+    for (size_t i = 0; i < cap / 2; ++i) erased += set.contains(keys[i], false);
+    for (size_t i = cap / 2; i < cap; ++i) stale += set.contains(keys[i], false);
+    for (size_t i = cap; i < keys.size(); ++i) fresh += set.contains(keys[i], false);
+    return {erased / double(cap / 2), stale / double(cap / 2), fresh / double(keys.size() - cap)};
+}
+
+// Sliding window of "blocks": each inserts block_size keys and later consumes the
+// first and last quarter of them. Returns (min window hit rate, fraction of windows
+// under 99.9%).
+static std::vector<double> CuckooGenerations(size_t megabytes, double load) {
+    CuckooHashSet set;
+    const size_t cap = set.setup_bytes(megabytes << 20);
+    const uint32_t BLOCK = 10000, WINDOW = 60, POP = (BLOCK / WINDOW) / 2;
+    const size_t total = (size_t)(load * cap) / BLOCK;
+    SimRng r{3};
+    std::deque<std::vector<uint256>> window;
+    double minHit = 1.0;
+    size_t loose = 0;
+    for (size_t b = 0; b < total; ++b) {
+        if (window.size() == WINDOW) window.pop_front();
+        std::vector<uint256> ins(BLOCK), reads;
+        for (auto& k : ins) k = r.key();
+        reads.insert(reads.end(), ins.begin(), ins.begin() + BLOCK / 4);
+        reads.insert(reads.end(), ins.end() - BLOCK / 4, ins.end());
+        for (auto& k : ins) set.insert(k);
+        window.push_back(std::move(reads));
+        size_t count = 0;
+        for (auto& w : window)
+            for (uint32_t j = 0; j < POP; ++j) {
+                count += set.contains(w.back(), true);
+                w.pop_back();
+            }
+        const double hit = (double)count / double(window.size() * POP);
+        minHit = std::min(minHit, hit);
+        loose += hit < 0.999;
+    }
+    return {minHit, (double)loose / (double)total};
+}
 
 void bind_node(pyb::module_& m) {
     m.def(
@@ -41,6 +145,65 @@ void bind_node(pyb::module_& m) {
     });
     m.def("node_running", []() { return (bool)g_pynode; });
     // Lock-order detector probe (reference DEBUG_LOCKORDER): a->b then b->a in one thread.
+    m.def("ui_track_start", []() {
+        {
+            std::lock_guard<std::mutex> l(g_ui.m);
+            g_ui.counts.clear();
+            g_ui.initMessages.clear();
+        }
+        auto add = [](auto& sig, auto fn) {
+            const int id = sig.connect(fn);
+            g_ui.conns.emplace_back([&sig, id] { sig.disconnect(id); }, id);
+        };
+        add(uiInterface.NotifyBlockTip, [](bool, const CBlockIndex* p) {
+            g_ui.bump("NotifyBlockTip");
+            g_ui.lastTipHeight = p ? p->nHeight : -1;
+        });
+        add(uiInterface.NotifyHeaderTip, [](bool, const CBlockIndex* p) {
+            g_ui.bump("NotifyHeaderTip");
+            g_ui.lastHeaderHeight = p ? p->nHeight : -1;
+        });
+        add(uiInterface.InitMessage, [](const std::string& s) {
+            g_ui.bump("InitMessage");
+            std::lock_guard<std::mutex> l(g_ui.m);
+            g_ui.initMessages.push_back(s);
+        });
+        add(uiInterface.ShowProgress, [](const std::string&, int p) {
+            g_ui.bump("ShowProgress");
+            g_ui.lastProgress = p;
+        });
+        add(uiInterface.NotifyNumConnectionsChanged, [](int n) {
+            g_ui.bump("NotifyNumConnectionsChanged");
+            g_ui.lastConnections = n;
+        });
+        add(uiInterface.NotifyNetworkActiveChanged, [](bool) { g_ui.bump("NotifyNetworkActiveChanged"); });
+        add(uiInterface.BannedListChanged, []() { g_ui.bump("BannedListChanged"); });
+        add(uiInterface.NotifyAlertChanged, []() { g_ui.bump("NotifyAlertChanged"); });
+        add(uiInterface.LoadWallet, [](CWallet*) { g_ui.bump("LoadWallet"); });
+        add(uiInterface.ThreadSafeMessageBox, [](const std::string&, const std::string&, unsigned) {
+            g_ui.bump("ThreadSafeMessageBox");
+            return true;
+        });
+    });
+    m.def("ui_track_stop", []() {
+        for (auto& c : g_ui.conns) c.first();
+        g_ui.conns.clear();
+    });
+    m.def("ui_track_counts", []() {
+        std::lock_guard<std::mutex> l(g_ui.m);
+        pyb::dict d;
+        for (auto& kv : g_ui.counts) d[pyb::str(kv.first)] = kv.second;
+        d["lastTipHeight"] = g_ui.lastTipHeight;
+        d["lastHeaderHeight"] = g_ui.lastHeaderHeight;
+        d["lastProgress"] = g_ui.lastProgress;
+        d["initMessages"] = g_ui.initMessages;
+        return d;
+    });
+    m.def("ui_init_message", [](const std::string& s) { uiInterface.InitMessage(s); });
+    m.def("ui_init_error", [](const std::string& s) { return InitError(s); });
+    m.def("cuckoo_hit_rate", &CuckooHitRate, pyb::arg("megabytes"), pyb::arg("load"));
+    m.def("cuckoo_erase", &CuckooErase, pyb::arg("megabytes"));
+    m.def("cuckoo_generations", &CuckooGenerations, pyb::arg("megabytes") = 32, pyb::arg("load") = 10.0);
     m.def("lockorder_probe", []() {
         const uint64_t before = LockOrderViolations();
         const bool was = LockOrderChecking();

@@ -8,6 +8,7 @@
 #include <cstring>
 #include <fstream>
 #include <pthread.h>
+#include <thread>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -491,4 +492,22 @@ void Scheduler::Loop() {
     }
 }
 
+} // namespace bcp
+
+namespace bcp {
+void ReplaceAll(std::string& s, const std::string& from, const std::string& to) {
+    if (from.empty()) return;
+    size_t p = 0;
+    while ((p = s.find(from, p)) != std::string::npos) {
+        s.replace(p, from.size(), to);
+        p += to.size();
+    }
+}
+
+void RunCommand(const std::string& cmd) {
+    const int r = std::system(cmd.c_str());
+    if (r != 0) LogPrintf("runCommand error: system(%s) returned %d\n", cmd.c_str(), r);
+}
+
+void RunCommandAsync(const std::string& cmd) { std::thread([cmd] { RunCommand(cmd); }).detach(); }
 } // namespace bcp

@@ -60,6 +60,12 @@ void LogPrintCat(uint32_t cat, const char* fmt, ...) __attribute__((format(print
     } while (0)
 bool error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 void ShrinkDebugFile();
+// Replace every occurrence of `from` in `s` (boost::replace_all in the reference).
+void ReplaceAll(std::string& s, const std::string& from, const std::string& to);
+// Run a shell command (reference util.cpp runCommand); the async form runs it on a
+// detached thread so notification hooks never block validation.
+void RunCommand(const std::string& cmd);
+void RunCommandAsync(const std::string& cmd);
 
 // ---------------------------------------------------------------- args / config
 class ArgsManager {

@@ -1,4 +1,5 @@
 #include "wallet/wallet.h"
+#include "node/ui_interface.h"
 #include "consensus/params.h"
 #include "consensus/tx_verify.h"
 #include "node/policy.h"
@@ -747,9 +748,8 @@ bool CWallet::AddToWallet(const CWalletTx& wtxIn, bool) {
     const std::string cmd = gArgs.GetArg("-walletnotify", "");
     if (!cmd.empty() && (fInsertedNew || fUpdated)) {
         std::string c = cmd;
-        const size_t p = c.find("%s");
-        if (p != std::string::npos) c.replace(p, 2, hash.GetHex());
-        std::thread([c] { (void)!std::system(c.c_str()); }).detach();
+        ReplaceAll(c, "%s", hash.GetHex());
+        RunCommandAsync(c);
     }
     return true;
 }
@@ -898,7 +898,18 @@ bool CWallet::ScanForWalletTransactions(const CBlockIndex* pindex, bool fUpdate,
     if (!chainstate) return false;
     int found = 0;
     const int64_t start = GetTimeMillis();
+    int tipHeight = 0;
+    {
+        std::lock_guard<CCriticalSection> lm(chainstate->cs());
+        tipHeight = std::max(1, chainstate->Height());
+    }
+    const int firstHeight = pindex ? pindex->nHeight : 0;
+    uiInterface.ShowProgress("Rescanning...", 0);
     while (pindex) {
+        if (pindex->nHeight % 100 == 0)
+            uiInterface.ShowProgress("Rescanning...",
+                                     std::max(1, std::min(99, (int)(100.0 * (pindex->nHeight - firstHeight) /
+                                                                    std::max(1, tipHeight - firstHeight)))));
         CBlock block;
         {
             std::lock_guard<CCriticalSection> lm(chainstate->cs());
@@ -909,6 +920,7 @@ bool CWallet::ScanForWalletTransactions(const CBlockIndex* pindex, bool fUpdate,
             pindex = chainstate->ActiveChain().Next(pindex);
         }
     }
+    uiInterface.ShowProgress("Rescanning...", 100);
     if (pnFound) *pnFound = found;
     LogPrintf("Rescan completed in %15dms (%d wallet txs)\n", (int)(GetTimeMillis() - start), found);
     return true;

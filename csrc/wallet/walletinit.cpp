@@ -4,6 +4,7 @@
 // -paytxfee/-txconfirmtarget; and the wallet hooks used by generate/getinfo/validateaddress).
 #include "node/node.h"
 #include "node/txmempool.h"
+#include "node/ui_interface.h"
 #include "node/validation.h"
 #include "rpc/server.h"
 #include "util/strencodings.h"
@@ -93,6 +94,7 @@ static bool LoadOneWallet(NodeContext& node, const std::string& name, std::strin
         if (start && start != cs.Tip()) start = cs.ActiveChain().Next(start) ? start : nullptr;
     }
     GetMainSignals().Register(w.get());
+    uiInterface.LoadWallet(w.get());
     if (start && start != cs.Tip()) {
         LogPrintf("Rescanning last %i blocks (from block %i)...\n", cs.Height() - start->nHeight, start->nHeight);
         w->ScanForWalletTransactions(start, true);
