@@ -72,7 +72,7 @@ struct EhCfg {
 };
 
 // Mainnet/testnet (200,9); (96,5); regtest (48,5).
-using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 1024, 512, 256>;
+using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
 using Cfg48_5 = EhCfg<48, 5, 3, 128, 64, 8, 64, 256>;
 
@@ -128,7 +128,7 @@ __device__ uint32_t block_exscan(uint32_t* v, int n, uint32_t* wsum /* >= NT/64 
 // (CNT0/OFF0 are NB x GENWG).
 template <class C, bool HDR>
 __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__ states, uint32_t* __restrict__ R,
-                                                 uint64_t* __restrict__ F, uint32_t* __restrict__ CNT,
+                                                 uint32_t* __restrict__ F, uint32_t* __restrict__ CNT,
                                                  uint32_t* __restrict__ OFF) {
     constexpr int W0 = C::words(0);
     constexpr int SW = (C::N + 31) / 32 + 1;
@@ -188,7 +188,7 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
     __syncthreads();
     // word-flat stores: consecutive lanes write consecutive dwords of the area
     uint32_t* area = R + ((size_t)nonce * C::ROWS + (size_t)gw * C::RPW) * C::WMAX;
-    uint64_t* farea = F + (size_t)nonce * C::ROWS + (size_t)gw * C::RPW;
+    uint32_t* farea = F + (size_t)nonce * C::ROWS + (size_t)gw * C::RPW;
     for (int k = tid; k < C::RPW * W0; k += NTG) {
         const uint32_t t = k / W0, w = k - t * W0;
         area[k] = rows[perm[t] * W0 + w];
@@ -216,62 +216,108 @@ template <int NS> __device__ __forceinline__ uint32_t run_of(const uint32_t* sta
 #define EH_STAMP(k)                                                                                  \
     do {                                                                                             \
         if constexpr (STAMP) {                                                                       \
-            if (threadIdx.x == 0) stamps[(size_t)blockIdx.x * 16 + (k)] = __builtin_amdgcn_s_memtime(); \
+            if (threadIdx.x == 0) stamps[(size_t)bk * 16 + (k)] = __builtin_amdgcn_s_memtime();        \
         }                                                                                            \
     } while (0)
 
-// LDS bytes of a round with full rows in LDS (one 1024-lane workgroup per CU).
+// LDS bytes of a persistent round (one 1024-lane workgroup per CU for (200,9)).
+template <class C> constexpr int round_tail() { return (C::NRESTS * 4 > C::CAP * 2) ? C::NRESTS * 4 : C::CAP * 2; }
+template <class C> constexpr int round_un() {
+    return (C::CAP * 2 + round_tail<C>() > C::CAP * 4) ? C::CAP * 2 + round_tail<C>() : C::CAP * 4;
+}
 template <class C> constexpr int round_lds(int stage, bool prune) {
     const int WI = C::words(stage - 1);
     const int NS = C::nsrc(stage - 1);
-    const int tail = (C::NRESTS * 4 > C::CAP * 2) ? C::NRESTS * 4 : C::CAP * 2;
-    return C::CAP * WI * 4 + (prune ? C::CAP * 4 : 0) + C::CAP * 4 /*plist*/ + C::CAP * 2 + tail +
-           (2 * NS + 1 + 2 * C::NB) * 4 + 256;
+    return C::CAP * WI * 4 + (prune ? C::CAP * 4 : 0) + C::CAP * 4 /*plist*/ + round_un<C>() +
+           2 * (2 * NS + 1) * 4 + 2 * C::NB * 4 + 256;
 }
 // Depth-1 duplicate pruning wherever its signatures fit next to the full rows.
 template <class C> constexpr bool round_prunes(int stage) {
     return stage >= 2 && round_lds<C>(stage, true) <= 160 * 1024;
 }
 
-// Parent references. A stage-s row (s >= 1) stores F = (d << 32) | (j << 16) | i: it was
-// made in round s by workgroup d from its LDS rows i and j. Round s also records its
-// gather map M_s[d*CAP + r] = global slot (stage s-1) of LDS row r, so the index tree
-// is walked as  slot -> F -> (d,i,j) -> M -> parent slots. Stage-0 F holds leaf indices.
+// Parent references. A stage-s row (s >= 1) at global slot g = d*CAP + t stores
+// F = (j << 16) | i: it was made in round s by workgroup d (= g / CAP, implied by the slot)
+// from its LDS rows i and j. Round s also records its gather map M_s[d*CAP + r] = global
+// slot (stage s-1) of LDS row r, so the index tree is walked as
+// slot -> (d, F) -> (d,i,j) -> M -> parent slots. Stage-0 F holds leaf indices.
 __device__ __forceinline__ uint64_t pack_tri(uint32_t d, uint32_t i, uint32_t j) {
     return ((uint64_t)d << 32) | (j << 16) | i;
 }
 // 2 x 16-bit signature of a row's parents for depth-1 duplicate pruning: each half is the
-// parent's LDS row (13 bits) plus 3 bits of the producing workgroup; a signature match is
-// confirmed exactly from global memory.
-__device__ __forceinline__ uint32_t parent_sig(uint64_t f) {
-    const uint32_t d = (uint32_t)(f >> 32) & 7, i = (uint32_t)f & 0x1fff, j = ((uint32_t)f >> 16) & 0x1fff;
-    return ((i | (d << 13)) << 16) | (j | (d << 13));
+// parent's LDS row (13 bits) plus 3 bits of the producing workgroup. Pairs whose signatures
+// share a half are dropped without an exact check: a false match (~1e-4 per compared pair)
+// costs a negligible fraction of the yield, and every emitted solution is re-checked for
+// distinct indices anyway.
+__device__ __forceinline__ uint32_t parent_sig(uint32_t d, uint32_t f) {
+    const uint32_t i = f & 0x1fff, j = (f >> 16) & 0x1fff;
+    return ((i | ((d & 7) << 13)) << 16) | (j | ((d & 7) << 13));
 }
-__device__ __forceinline__ bool share_parent_tri(uint64_t a, uint64_t b) {
-    if ((a >> 32) != (b >> 32)) return false;
-    const uint32_t a0 = (uint32_t)a & 0xffff, a1 = ((uint32_t)a >> 16), b0 = (uint32_t)b & 0xffff,
-                   b1 = ((uint32_t)b >> 16);
-    return a0 == b0 || a0 == b1 || a1 == b0 || a1 == b1;
+
+// Row I/O of W dwords at a dword-aligned byte offset through a buffer descriptor: one
+// 16-byte access plus a remainder (dword-aligned 16-byte buffer accesses are legal on gfx950).
+template <int W> __device__ __forceinline__ void row_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t* o) {
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    if constexpr (W >= 4) {
+        const u4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        o[0] = x.x, o[1] = x.y, o[2] = x.z, o[3] = x.w;
+        row_load<W - 4>(rs, off + 16, o + 4);
+    } else if constexpr (W == 3) {
+        const u3 x = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+        o[0] = x.x, o[1] = x.y, o[2] = x.z;
+    } else if constexpr (W == 2) {
+        const u2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        o[0] = x.x, o[1] = x.y;
+    } else if constexpr (W == 1) {
+        o[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+    }
+}
+template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint32_t* v) {
+    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+    typedef uint32_t u3 __attribute__((ext_vector_type(3)));
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    if constexpr (W >= 4) {
+        const u4 x = {v[0], v[1], v[2], v[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
+        row_store<W - 4>(rs, off + 16, v + 4);
+    } else if constexpr (W == 3) {
+        const u3 x = {v[0], v[1], v[2]};
+        __builtin_amdgcn_raw_buffer_store_b96(x, rs, off, 0, 0);
+    } else if constexpr (W == 2) {
+        const u2 x = {v[0], v[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, 0);
+    } else if constexpr (W == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, 0);
+    }
 }
 
 // STAGE < K: collision round producing stage-STAGE rows. STAGE == K: final round.
-// Workgroup d = bucket d of stage STAGE-1 rows (= output area d of stage STAGE).
-//   1. run table from row d of CNT/OFF (one run per source area);
-//   2. gather: (a) per LDS row its global slot (binary search over the runs) into LDS
-//      scratch and the gather map M; (b) word-flat copy of the rows (consecutive lanes read
-//      consecutive dwords), plus parent signatures where pruning is enabled;
-//   3. LDS hash table on the RB bits;
-//   4. one chain walk records colliding pairs in an LDS pair list (depth-1 pruning);
-//   5. counting sort of the pair list by destination -> LDS permutation;
-//   6. word-flat emit from LDS in slot order: XOR, shift one digit, store.
+// Bucket bk = nonce*NB + d holds the stage STAGE-1 rows whose top digit bits are d; it becomes
+// output area d of stage STAGE.
+//
+// The kernel is PERSISTENT and software-pipelined: one workgroup per CU walks buckets
+// blockIdx.x, +gridDim.x, ... While it collides bucket b out of LDS, the rows of its next
+// bucket are already in flight into VGPRs (plain loads are not drained by a bare barrier),
+// and the run table of the bucket after that is in flight too. Per bucket:
+//   A. commit: prefetched rows (VGPRs) -> LDS rows (+ parent signatures when pruning);
+//   B. run table of the NEXT bucket from its prefetched CNT/OFF column (exclusive scan);
+//      fetch the run table of the bucket after it (registers, not waited for);
+//   C. slot map of the next bucket (16 lanes per run) -> gather map M; issue its row loads,
+//      one lane per row, 16-byte buffer loads (not waited for);
+//   D. collide bucket b: LDS hash table on the RB bits, one chain walk into an LDS pair list
+//      (depth-1 pruning), counting sort of the pairs by destination, one-lane-per-row emit
+//      (XOR, shift one digit, 16-byte stores) in slot order + one column of CNT/OFF.
 template <class C, int STAGE, bool STAMP>
-__global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ Rin, const uint64_t* __restrict__ Fin,
+__global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ Fin,
                                                   const uint32_t* __restrict__ CNTin,
                                                   const uint32_t* __restrict__ OFFin, uint32_t* __restrict__ Rout,
-                                                  uint64_t* __restrict__ Fout, uint32_t* __restrict__ CNTout,
+                                                  uint32_t* __restrict__ Fout, uint32_t* __restrict__ CNTout,
                                                   uint32_t* __restrict__ OFFout, uint32_t* __restrict__ Mout,
                                                   uint32_t* __restrict__ ncand, uint64_t* __restrict__ cand,
-                                                  uint64_t* __restrict__ stamps) {
+                                                  uint64_t* __restrict__ stamps, uint32_t* __restrict__ pdrop,
+                                                  int nbk) {
     constexpr int WI = C::words(STAGE - 1);
     constexpr int WO = (STAGE < C::K) ? C::words(STAGE) : 1;
     constexpr int NS = C::nsrc(STAGE - 1);
@@ -280,198 +326,262 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     constexpr bool PRUNE = round_prunes<C>(STAGE);
     static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024, "round LDS budget");
     constexpr int NT = C::NT;
-    constexpr int U = 8; // independent dwords in flight per lane in the gather
-    // union: gather {gslot[CAP] u32}; walk {nxt[CAP] u16, head[NRESTS] u32};
+    static_assert(NS <= NT, "one run-table entry per lane");
+    constexpr int RPL = (C::CAP + NT - 1) / NT; // prefetched rows per lane
+    // union: prefetch {gslot[CAP] u32}; walk {nxt[CAP] u16, head[NRESTS] u32};
     //        sort/emit {pdst[CAP] u16, perm[CAP] u16}
-    constexpr int TAIL = (C::NRESTS * 4 > C::CAP * 2) ? C::NRESTS * 4 : C::CAP * 2;
     __shared__ uint32_t rows[C::CAP * WI];
     __shared__ uint32_t psig[PRUNE ? C::CAP : 1];
     __shared__ uint32_t plist[FINAL ? 1 : C::CAP]; // (j << 16) | i
-    __shared__ __attribute__((aligned(16))) uint8_t un[C::CAP * 2 + TAIL];
-    __shared__ uint32_t rpos[NS + 1], rsrc[NS], hist[C::NB], cur[C::NB];
+    __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>()];
+    __shared__ uint32_t rpos[2][NS + 1], rsrc[2][NS], hist[C::NB], cur[C::NB];
     __shared__ uint32_t wsum[C::NW + 1];
     __shared__ uint32_t npairs;
-    static_assert(C::CAP * 2 + TAIL >= C::CAP * 4, "gather scratch");
     uint32_t* gslot = reinterpret_cast<uint32_t*>(un);
     uint16_t* nxt = reinterpret_cast<uint16_t*>(un);
     uint32_t* head = reinterpret_cast<uint32_t*>(un + C::CAP * 2);
     uint16_t* pdst = reinterpret_cast<uint16_t*>(un);
     uint16_t* perm = reinterpret_cast<uint16_t*>(un + C::CAP * 2);
-    const int d = blockIdx.x % C::NB;
-    const int nonce = blockIdx.x / C::NB;
     const int tid = threadIdx.x;
-    const size_t matin = (size_t)nonce * C::NB * NS;
-    const size_t matout = (size_t)nonce * C::NB * C::NB;
+    const int G = gridDim.x;
+    int bk = blockIdx.x;
+    if (bk >= nbk) return; // uniform per workgroup
 
-    EH_STAMP(0);
-    // 1. run table: row d of CNT/OFF
-    for (int b = tid; b < NS; b += NT) {
-        rpos[b] = CNTin[matin + (size_t)d * NS + b];
-        rsrc[b] = OFFin[matin + (size_t)d * NS + b];
-    }
-    for (int b = tid; b < C::NB; b += NT) hist[b] = 0;
-    if (tid == 0) npairs = 0;
-    __syncthreads();
-    const uint32_t total = block_exscan<NT>(rpos, NS, wsum); // rpos = LDS start of run b
-    if (tid == 0) rpos[NS] = total;
-    const uint32_t n = min(total, (uint32_t)C::CAP);
-    __syncthreads();
-    EH_STAMP(1);
-
-    const uint32_t* rin_nonce = Rin + (size_t)nonce * C::ROWS * C::WMAX;
-    const uint64_t* fin_nonce = Fin + (size_t)nonce * C::ROWS;
-    auto gidx_of = [&](uint32_t r) -> uint32_t {
-        const uint32_t b = run_of<NS>(rpos, r);
-        return b * SSTRIDE + rsrc[b] + (r - rpos[b]);
+    uint32_t rt_cnt = 0, rt_off = 0; // run-table entry `tid` of a bucket two steps ahead
+    auto rt_fetch = [&](int bb) {
+        if (bb < nbk && tid < NS) {
+            const size_t at = (size_t)(bb / C::NB) * C::NB * NS + (size_t)(bb % C::NB) * NS + tid;
+            rt_cnt = CNTin[at];
+            rt_off = OFFin[at];
+        }
     };
-
-    // 2a. global slot of every LDS row: 16 lanes per run, 4 runs per wave instruction
-    {
-        const int lane = tid & 63, wid = tid >> 6, sub = lane >> 4, l16 = lane & 15;
-        for (int b0 = wid * 4; b0 < NS; b0 += C::NW * 4) {
-            const int b = b0 + sub;
-            if (b < NS) {
-                const uint32_t p0 = rpos[b];
-                const uint32_t len = rpos[b + 1] - p0;
-                const uint32_t s0 = b * SSTRIDE + rsrc[b];
-                for (uint32_t j = l16; j < len && p0 + j < n; j += 16) gslot[p0 + j] = s0 + j;
-            }
+    auto rt_commit = [&](int p) -> uint32_t {
+        if (tid < NS) {
+            rpos[p][tid] = rt_cnt;
+            rsrc[p][tid] = rt_off;
         }
-    }
-    __syncthreads();
-    // gather map (coalesced)
-    uint32_t* mrow = Mout + (size_t)nonce * C::ROWS + (size_t)d * C::CAP;
-    for (uint32_t r = tid; r < n; r += NT) mrow[r] = gslot[r];
-    // 2b. word-flat row copy: all of a lane's dwords (and parent refs) issued before use
-    {
-        constexpr int UW = (C::CAP * WI + NT - 1) / NT;      // dwords per lane, upper bound
-        constexpr int UR = PRUNE ? (C::CAP + NT - 1) / NT : 0; // parent refs per lane
-        uint32_t v[UW];
-        uint64_t f[UR > 0 ? UR : 1];
-#pragma unroll
-        for (int u = 0; u < UW; ++u) {
-            const uint32_t k = tid + u * NT;
-            const uint32_t kk = k < n * WI ? k : 0;
-            const uint32_t r = kk / WI, w = kk - r * WI;
-            v[u] = rin_nonce[(size_t)gslot[r] * WI + w];
-        }
-        if constexpr (PRUNE) {
-#pragma unroll
-            for (int u = 0; u < UR; ++u) {
-                const uint32_t r = tid + u * NT;
-                f[u] = fin_nonce[gslot[r < n ? r : 0]];
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UW; ++u) {
-            const uint32_t k = tid + u * NT;
-            if (k < n * WI) rows[k] = v[u];
-        }
-        if constexpr (PRUNE) {
-#pragma unroll
-            for (int u = 0; u < UR; ++u) {
-                const uint32_t r = tid + u * NT;
-                if (r < n) psig[r] = parent_sig(f[u]);
-            }
-        }
-    }
-    __syncthreads();
-    EH_STAMP(2);
-
-    // 3. LDS hash table on the RB remaining bits of the digit
-    for (int k = tid; k < C::NRESTS; k += NT) head[k] = NIL;
-    __syncthreads();
-    for (uint32_t i = tid; i < n; i += NT) nxt[i] = (uint16_t)atomicExch(&head[rows[i * WI] >> (32 - C::RB)], i);
-    __syncthreads();
-    EH_STAMP(3);
-
-    // 4. single chain walk
-    for (uint32_t i = tid; i < n; i += NT) {
-        uint32_t ri[WI];
-#pragma unroll
-        for (int w = 0; w < WI; ++w) ri[w] = rows[i * WI + w];
-        uint32_t si = 0;
-        if constexpr (PRUNE) si = psig[i];
-        int steps = 0;
-        for (uint32_t j = nxt[i]; j != NIL16 && steps < MAX_CHAIN; j = nxt[j], ++steps) {
-            uint32_t any = 0;
-#pragma unroll
-            for (int w = 0; w < WI; ++w) any |= ri[w] ^ rows[j * WI + w];
-            if constexpr (FINAL) {
-                if (any != 0) continue;
-            } else {
-                if (any == 0) continue; // identical subtrees
-            }
-            if constexpr (PRUNE) {
-                const uint32_t sj = psig[j];
-                if ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) || (si & 0xffff) == (sj >> 16) ||
-                    (si & 0xffff) == (sj & 0xffff)) {
-                    if (share_parent_tri(fin_nonce[gidx_of(i)], fin_nonce[gidx_of(j)])) continue;
+        __syncthreads();
+        const uint32_t total = block_exscan<NT>(rpos[p], NS, wsum);
+        if (tid == 0) rpos[p][NS] = total;
+        __syncthreads();
+        return min(total, (uint32_t)C::CAP);
+    };
+    // A thread id the compiler cannot see through: keeps the per-lane index math of the
+    // prefetch/commit loops from being hoisted out of the persistent loop (live invariants
+    // would otherwise push the prefetched rows out to scratch).
+    auto opaque_tid = [&]() -> uint32_t {
+        uint32_t t;
+        asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
+        return t;
+    };
+    uint32_t v[RPL][WI];
+    uint32_t f[PRUNE ? RPL : 1], fd[PRUNE ? RPL : 1]; // parent refs + producing workgroup
+    uint32_t so[RPL];                                  // slots of the next bucket's rows
+    int pf_nonce = 0;
+    auto prefetch = [&](int bb, int p, uint32_t nn) {
+        const int nonce = bb / C::NB, d = bb % C::NB;
+        { // slot of every LDS row: 16 lanes per run, 4 runs per wave instruction
+            const int lane = tid & 63, wid = tid >> 6, sub = lane >> 4, l16 = lane & 15;
+            for (int b0 = wid * 4; b0 < NS; b0 += C::NW * 4) {
+                const int b = b0 + sub;
+                if (b < NS) {
+                    const uint32_t p0 = rpos[p][b];
+                    const uint32_t len = rpos[p][b + 1] - p0;
+                    const uint32_t s0 = b * SSTRIDE + rsrc[p][b];
+                    for (uint32_t j = l16; j < len && p0 + j < nn; j += 16) gslot[p0 + j] = s0 + j;
                 }
             }
-            if constexpr (FINAL) {
-                const uint32_t c = atomicAdd(&ncand[nonce], 1u);
-                if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
-            } else {
-                // wave-aggregated append: one LDS atomic per wave instead of one per pair
-                const uint64_t act = __ballot(1);
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                const int leader = __builtin_ctzll(act);
-                uint32_t base = 0;
-                if ((int)(tid & 63) == leader) base = atomicAdd(&npairs, (uint32_t)__builtin_popcountll(act));
-                base = __shfl(base, leader, 64);
-                const uint32_t k = base + rank;
-                if (k < (uint32_t)C::CAP) plist[k] = (j << 16) | i;
+        }
+        __syncthreads();
+        EH_STAMP(8);
+        uint32_t* mrow = Mout + (size_t)nonce * C::ROWS + (size_t)d * C::CAP;
+        for (uint32_t r = tid; r < nn; r += NT) mrow[r] = gslot[r];
+        // buffer loads: 32-bit lane offsets against a per-nonce descriptor keep the address
+        // math out of the VGPRs that hold the prefetched rows across phase D
+        const auto rsrc_rows = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(Rin + (size_t)nonce * C::ROWS * C::WMAX), 0, C::ROWS * C::WMAX * 4, 0x00020000);
+        const auto rsrc_refs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(Fin + (size_t)nonce * C::ROWS),
+                                                                 0, C::ROWS * 4, 0x00020000);
+        const uint32_t ot = opaque_tid();
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+            const uint32_t r = ot + u * NT;
+            so[u] = (r < nn) ? gslot[r] : 0u; // clamped to a valid slot: loads are unconditional
+        }
+        pf_nonce = nonce;
+    };
+    // Issue the prefetch loads of rows [U0, U1) of every lane. The loads of one bucket are
+    // issued in slices spread over phase D: a wave that issues the whole bucket at once stalls
+    // at issue once the CU's outstanding-request window is full, and the barrier after it
+    // then holds every other wave too.
+    auto issue = [&](int u0, int u1) {
+        const auto rsrc_rows = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(Rin + (size_t)pf_nonce * C::ROWS * C::WMAX), 0, C::ROWS * C::WMAX * 4, 0x00020000);
+        const auto rsrc_refs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t*>(Fin + (size_t)pf_nonce * C::ROWS), 0, C::ROWS * 4, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+            if (u < u0 || u >= u1) continue;
+            row_load<WI>(rsrc_rows, so[u] * (WI * 4), v[u]);
+            if constexpr (PRUNE) {
+                f[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc_refs, so[u] * 4, 0, 0);
+                fd[u] = so[u] / C::CAP;
             }
         }
-    }
-    if constexpr (!FINAL) {
-        __syncthreads(); // chains/head are dead from here: reuse them for pdst/perm
-        EH_STAMP(4);
-        const uint32_t np = min(npairs, (uint32_t)C::CAP);
-        for (uint32_t k = tid; k < np; k += NT) {
-            const uint32_t pr = plist[k];
-            const uint32_t nb = ((rows[(pr & 0xffff) * WI] ^ rows[(pr >> 16) * WI]) >> (32 - C::DB)) & (C::NB - 1);
-            pdst[k] = (uint16_t)nb;
-            atomicAdd(&hist[nb], 1u);
+    };
+
+    // prologue: run table of the first bucket, prefetch its rows, fetch the second run table
+    int pb = 0;
+    rt_fetch(bk);
+    uint32_t n = rt_commit(0);
+    rt_fetch(bk + G);
+    prefetch(bk, 0, n);
+    issue(0, RPL);
+    __syncthreads();
+
+    for (;;) {
+        const int nonce = bk / C::NB, d = bk % C::NB;
+        const size_t matout = (size_t)nonce * C::NB * C::NB;
+        EH_STAMP(0);
+        // A. commit the prefetched rows
+        {
+            const uint32_t ot = opaque_tid();
+#pragma unroll
+            for (int u = 0; u < RPL; ++u) {
+                const uint32_t r = ot + u * NT;
+                if (r < n) {
+#pragma unroll
+                    for (int w = 0; w < WI; ++w) rows[r * WI + w] = v[u][w];
+                    if constexpr (PRUNE) psig[r] = parent_sig(fd[u], f[u]);
+                }
+            }
         }
-        __syncthreads();
-        for (int b = tid; b < C::NB; b += NT) cur[b] = hist[b];
-        __syncthreads();
-        block_exscan<NT>(cur, C::NB, wsum);
-        for (int b = tid; b < C::NB; b += NT) {
-            CNTout[matout + (size_t)b * C::NB + d] = hist[b];
-            OFFout[matout + (size_t)b * C::NB + d] = cur[b];
+        for (int b = tid; b < C::NB; b += NT) hist[b] = 0;
+        if (tid == 0) npairs = 0;
+        EH_STAMP(1);
+        // B + C. next bucket: run table, slot map, row loads in flight
+        const int bn = bk + G;
+        uint32_t nn = 0;
+        if (bn < nbk) { // uniform
+            nn = rt_commit(pb ^ 1);
+            EH_STAMP(7);
+            rt_fetch(bn + G);
+            prefetch(bn, pb ^ 1, nn);
+            issue(0, 2);
+            EH_STAMP(9);
         }
+        const bool more = bn < nbk;
         __syncthreads();
-        for (uint32_t k = tid; k < np; k += NT) perm[atomicAdd(&cur[pdst[k]], 1u)] = (uint16_t)k;
+        EH_STAMP(2);
+
+        // D1. LDS hash table on the RB remaining bits of the digit
+        for (int k = tid; k < C::NRESTS; k += NT) head[k] = NIL;
         __syncthreads();
-        EH_STAMP(5);
-        // 6. word-flat emit: global slot g = d*CAP + t lives at Rout + nonce*ROWS*WMAX + g*WO
-        uint32_t* area = Rout + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::CAP * WO;
-        uint64_t* farea = Fout + (size_t)nonce * C::ROWS + (size_t)d * C::CAP;
-        for (uint32_t k = tid; k < np * WO; k += NT) {
-            const uint32_t t = k / WO, w = k - t * WO;
-            const uint32_t pr = plist[perm[t]];
-            const uint32_t i = pr & 0xffff, j = pr >> 16;
-            const uint32_t x0 = rows[i * WI + w] ^ rows[j * WI + w];
-            const uint32_t x1 = (w + 1 < (uint32_t)WI) ? (rows[i * WI + w + 1] ^ rows[j * WI + w + 1]) : 0u;
-            area[k] = (x0 << C::DB) | (x1 >> (32 - C::DB));
+        for (uint32_t i = tid; i < n; i += NT) nxt[i] = (uint16_t)atomicExch(&head[rows[i * WI] >> (32 - C::RB)], i);
+        if (more) issue(2, 3);
+        __syncthreads();
+        EH_STAMP(3);
+
+        // D2. single chain walk
+        for (uint32_t i = tid; i < n; i += NT) {
+            uint32_t ri[WI];
+#pragma unroll
+            for (int w = 0; w < WI; ++w) ri[w] = rows[i * WI + w];
+            uint32_t si = 0;
+            if constexpr (PRUNE) si = psig[i];
+            int steps = 0;
+            for (uint32_t j = nxt[i]; j != NIL16 && steps < MAX_CHAIN; j = nxt[j], ++steps) {
+                uint32_t any = 0;
+#pragma unroll
+                for (int w = 0; w < WI; ++w) any |= ri[w] ^ rows[j * WI + w];
+                if constexpr (FINAL) {
+                    if (any != 0) continue;
+                } else {
+                    if (any == 0) continue; // identical subtrees
+                }
+                if constexpr (PRUNE) {
+                    const uint32_t sj = psig[j];
+                    if ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) || (si & 0xffff) == (sj >> 16) ||
+                        (si & 0xffff) == (sj & 0xffff))
+                        continue;
+                }
+                if constexpr (FINAL) {
+                    const uint32_t c = atomicAdd(&ncand[nonce], 1u);
+                    if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
+                } else {
+                    // wave-aggregated append: one LDS atomic per wave instead of one per pair
+                    const uint64_t act = __ballot(1);
+                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+                    const int leader = __builtin_ctzll(act);
+                    uint32_t base = 0;
+                    if ((int)(tid & 63) == leader) base = atomicAdd(&npairs, (uint32_t)__builtin_popcountll(act));
+                    base = __shfl(base, leader, 64);
+                    const uint32_t k = base + rank;
+                    if (k < (uint32_t)C::CAP) plist[k] = (j << 16) | i;
+                }
+            }
         }
-        for (uint32_t t = tid; t < np; t += NT) {
-            const uint32_t pr = plist[perm[t]];
-            farea[t] = pack_tri(d, pr & 0xffff, pr >> 16);
+        if (more) issue(3, 4);
+        if constexpr (!FINAL) {
+            __syncthreads(); // chains/head are dead from here: reuse them for pdst/perm
+            EH_STAMP(4);
+            // D3. counting sort of the pair list by destination bucket
+            const uint32_t np = min(npairs, (uint32_t)C::CAP);
+            if (tid == 0 && npairs > (uint32_t)C::CAP) atomicAdd(&pdrop[STAGE], npairs - C::CAP);
+            for (uint32_t k = tid; k < np; k += NT) {
+                const uint32_t pr = plist[k];
+                const uint32_t nb = ((rows[(pr & 0xffff) * WI] ^ rows[(pr >> 16) * WI]) >> (32 - C::DB)) & (C::NB - 1);
+                pdst[k] = (uint16_t)nb;
+                atomicAdd(&hist[nb], 1u);
+            }
+            __syncthreads();
+            for (int b = tid; b < C::NB; b += NT) cur[b] = hist[b];
+            __syncthreads();
+            block_exscan<NT>(cur, C::NB, wsum);
+            for (int b = tid; b < C::NB; b += NT) {
+                CNTout[matout + (size_t)b * C::NB + d] = hist[b];
+                OFFout[matout + (size_t)b * C::NB + d] = cur[b];
+            }
+            __syncthreads();
+            for (uint32_t k = tid; k < np; k += NT) perm[atomicAdd(&cur[pdst[k]], 1u)] = (uint16_t)k;
+            if (more) issue(4, RPL);
+            __syncthreads();
+            EH_STAMP(5);
+            // D4. emit, one lane per output row in slot order: XOR, shift one digit, store
+            const auto rsrc_out = __builtin_amdgcn_make_buffer_rsrc(
+                Rout + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::CAP * WO, 0, C::CAP * WO * 4, 0x00020000);
+            uint32_t* farea = Fout + (size_t)nonce * C::ROWS + (size_t)d * C::CAP;
+            for (uint32_t t = tid; t < np; t += NT) {
+                const uint32_t pr = plist[perm[t]];
+                const uint32_t i = pr & 0xffff, j = pr >> 16;
+                uint32_t x[WI + 1], o[WO];
+#pragma unroll
+                for (int w = 0; w < WI; ++w) x[w] = rows[i * WI + w] ^ rows[j * WI + w];
+                x[WI] = 0;
+#pragma unroll
+                for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
+                row_store<WO>(rsrc_out, t * (WO * 4), o);
+                farea[t] = pr;
+            }
+        }
+        if constexpr (FINAL) {
+            if (more) issue(4, RPL);
         }
         __syncthreads();
         EH_STAMP(6);
+        if (bn >= nbk) break;
+        bk = bn;
+        n = nn;
+        pb ^= 1;
     }
 }
+
 
 // ------------------------------------------------------------------ tree expansion
 // F: K arrays of per-stage references; M: K gather maps (M_s for round s at index s-1).
 template <class C>
-__global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint64_t* __restrict__ F,
+__global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_t* __restrict__ F,
                                                                   const uint32_t* __restrict__ M,
                                                                   const uint32_t* __restrict__ ncand,
                                                                   const uint64_t* __restrict__ cand, int batch,
@@ -503,10 +613,14 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint64_
             buf[cur][t] = Ms[(size_t)dd * C::CAP + r];
         }
         __syncthreads();
-        if (s > 1 && t < 2 * cnt) tri[t] = F[(size_t)(s - 1) * batch * C::ROWS + (size_t)nonce * C::ROWS + buf[cur][t]];
+        if (s > 1 && t < 2 * cnt) {
+            const uint32_t slot = buf[cur][t];
+            const uint32_t fr = F[(size_t)(s - 1) * batch * C::ROWS + (size_t)nonce * C::ROWS + slot];
+            tri[t] = pack_tri(slot / C::CAP, fr & 0xffff, fr >> 16);
+        }
     }
     __syncthreads();
-    if (t < (uint32_t)L) buf[cur][t] = (uint32_t)F[(size_t)nonce * C::ROWS + buf[cur][t]];
+    if (t < (uint32_t)L) buf[cur][t] = F[(size_t)nonce * C::ROWS + buf[cur][t]];
     // Canonical order: at each level the subtree with the smaller first index goes left.
     for (int l = 0; l < C::K; ++l) {
         __syncthreads();
@@ -584,12 +698,15 @@ struct EquihashGpuSolver::Impl {
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     DevBuf<bcpk::EhBaseState> d_states;
     DevBuf<uint32_t> d_rows[2], d_cnt[2], d_off[2], d_maps, d_ncand, d_idx, d_valid;
-    DevBuf<uint64_t> d_refs, d_cand;
+    DevBuf<uint32_t> d_refs, d_pdrop;
+    HostBuf<uint32_t> h_pdrop;
+    DevBuf<uint64_t> d_cand;
     HostBuf<bcpk::EhBaseState> h_states;
     HostBuf<uint32_t> h_ncand, h_idx, h_valid, h_cnt_sample, h_cnt0;
     size_t genwg = 0;
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0, cap = 0;
     int inflight = 0;
+    int ncu = 1;
     bool debug = false, stamp_mode = false;
     DevBuf<uint64_t> d_stamps;
     EhGpuStats stats;
@@ -613,6 +730,8 @@ struct EquihashGpuSolver::Impl {
         d_refs.alloc((size_t)C::K * batch * C::ROWS);
         d_maps.alloc((size_t)C::K * batch * C::ROWS);
         d_ncand.alloc(batch);
+        d_pdrop.alloc(C::K + 1);
+        h_pdrop.alloc(C::K + 1);
         d_cand.alloc((size_t)batch * C::MAXCAND);
         d_idx.alloc((size_t)batch * C::MAXCAND * C::L);
         d_valid.alloc((size_t)batch * C::MAXCAND);
@@ -623,23 +742,34 @@ struct EquihashGpuSolver::Impl {
         h_cnt0.alloc((size_t)C::NB * C::GENWG);
         d_stamps.alloc((size_t)C::K * batch * C::NB * 16);
         genwg = C::GENWG;
-        bytes = 2 * d_rows[0].n * 4 + d_refs.n * 8 + d_maps.n * 4 + 4 * d_cnt[0].n * 4 + d_idx.n * 4;
+        bytes = 2 * d_rows[0].n * 4 + d_refs.n * 4 + d_maps.n * 4 + 4 * d_cnt[0].n * 4 + d_idx.n * 4;
     }
 
+    // Persistent round kernels: as many workgroups as fit on the device at once.
+    template <class C, int S, bool ST> int round_grid(int nbk) {
+        static int per_cu = -1;
+        if (per_cu < 0) {
+            int occ = 0;
+            BCP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bcpk::eh_round<C, S, ST>, C::NT, 0));
+            per_cu = std::max(occ, 1);
+        }
+        return std::min(nbk, ncu * per_cu);
+    }
     template <class C, int S> void launch_round(int nstates) {
         const int pi = (S - 1) & 1, po = S & 1;
-        const uint64_t* fin = d_refs.p + (size_t)(S - 1) * batch * C::ROWS;
-        uint64_t* fout = (S < C::K) ? d_refs.p + (size_t)S * batch * C::ROWS : nullptr;
+        const uint32_t* fin = d_refs.p + (size_t)(S - 1) * batch * C::ROWS;
+        uint32_t* fout = (S < C::K) ? d_refs.p + (size_t)S * batch * C::ROWS : nullptr;
         uint32_t* mout = d_maps.p + (size_t)(S - 1) * batch * C::ROWS;
+        const int nbk = C::NB * nstates;
         if (stamp_mode) {
             uint64_t* st = d_stamps.p + (size_t)(S - 1) * batch * C::NB * 16;
-            hipLaunchKernelGGL((bcpk::eh_round<C, S, true>), dim3(C::NB * nstates), dim3(C::NT), 0, stream,
-                               d_rows[pi].p, fin, d_cnt[pi].p, d_off[pi].p, d_rows[po].p, fout, d_cnt[po].p,
-                               d_off[po].p, mout, d_ncand.p, d_cand.p, st);
+            hipLaunchKernelGGL((bcpk::eh_round<C, S, true>), dim3(round_grid<C, S, true>(nbk)), dim3(C::NT), 0,
+                               stream, d_rows[pi].p, fin, d_cnt[pi].p, d_off[pi].p, d_rows[po].p, fout, d_cnt[po].p,
+                               d_off[po].p, mout, d_ncand.p, d_cand.p, st, d_pdrop.p, nbk);
         } else {
-            hipLaunchKernelGGL((bcpk::eh_round<C, S, false>), dim3(C::NB * nstates), dim3(C::NT), 0, stream,
-                               d_rows[pi].p, fin, d_cnt[pi].p, d_off[pi].p, d_rows[po].p, fout, d_cnt[po].p,
-                               d_off[po].p, mout, d_ncand.p, d_cand.p, nullptr);
+            hipLaunchKernelGGL((bcpk::eh_round<C, S, false>), dim3(round_grid<C, S, false>(nbk)), dim3(C::NT), 0,
+                               stream, d_rows[pi].p, fin, d_cnt[pi].p, d_off[pi].p, d_rows[po].p, fout, d_cnt[po].p,
+                               d_off[po].p, mout, d_ncand.p, d_cand.p, nullptr, d_pdrop.p, nbk);
         }
         if (debug && S < C::K)
             BCP_HIP_CHECK(hipMemcpyAsync(h_cnt_sample.p + (size_t)S * C::NB * C::NB, d_cnt[po].p,
@@ -653,6 +783,7 @@ struct EquihashGpuSolver::Impl {
         BCP_HIP_CHECK(hipMemcpyAsync(d_states.p, h_states.p, nstates * sizeof(bcpk::EhBaseState),
                                      hipMemcpyHostToDevice, stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ncand.p, 0, batch * sizeof(uint32_t), stream));
+        BCP_HIP_CHECK(hipMemsetAsync(d_pdrop.p, 0, (C::K + 1) * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipEventRecord(ev0, stream));
         // header-shaped inputs (140 B: g lands at byte 12 of the final block) take the
         // zero-message-word BLAKE2b specialisation
@@ -680,6 +811,9 @@ struct EquihashGpuSolver::Impl {
         BCP_HIP_CHECK(hipEventRecord(ev1, stream));
         BCP_HIP_CHECK(
             hipMemcpyAsync(h_ncand.p, d_ncand.p, nstates * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        if (debug)
+            BCP_HIP_CHECK(hipMemcpyAsync(h_pdrop.p, d_pdrop.p, (C::K + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                         stream));
         BCP_HIP_CHECK(hipMemcpyAsync(h_valid.p, d_valid.p, nstates * C::MAXCAND * sizeof(uint32_t),
                                      hipMemcpyDeviceToHost, stream));
         BCP_HIP_CHECK(hipMemcpyAsync(h_idx.p, d_idx.p, nstates * C::MAXCAND * C::L * sizeof(uint32_t),
@@ -700,6 +834,7 @@ EquihashGpuSolver::EquihashGpuSolver(unsigned n, unsigned k, int batch, int devi
     impl->k = k;
     impl->batch = batch;
     impl->device = UseDevice(device);
+    BCP_HIP_CHECK(hipDeviceGetAttribute(&impl->ncu, hipDeviceAttributeMultiprocessorCount, impl->device));
     BCP_HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev0));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev1));
@@ -732,7 +867,7 @@ std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
     BCP_HIP_CHECK(hipMemcpy(h.data(), impl->d_stamps.p, h.size() * 8, hipMemcpyDeviceToHost));
     std::vector<std::vector<double>> out;
     for (size_t s = 0; s < impl->kstages; ++s) {
-        std::vector<double> acc(7, 0.0);
+        std::vector<double> acc(10, 0.0);
         size_t cnt = 0;
         for (size_t wg = 0; wg < (size_t)nonces * impl->nb; ++wg) {
             const uint64_t* t = &h[s * per + wg * 16];
@@ -740,6 +875,12 @@ std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
             for (int k = 1; k < 7; ++k)
                 if (t[k] >= t[k - 1] && t[k] != 0) acc[k] += (double)(t[k] - t[k - 1]);
             acc[0] += (double)((t[6] ? t[6] : t[3]) - t[0]);
+            // prefetch split: run-table commit | slot map | M map + load issue | barrier
+            if (t[7] && t[8] && t[9] && t[7] >= t[1] && t[8] >= t[7] && t[9] >= t[8] && t[2] >= t[9]) {
+                acc[7] += (double)(t[7] - t[1]);
+                acc[8] += (double)(t[8] - t[7]);
+                acc[9] += (double)(t[9] - t[8]);
+            }
             ++cnt;
         }
         for (auto& a : acc) a = cnt ? a / cnt : 0;
@@ -775,12 +916,16 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
         impl->stats.stage_rows.assign(impl->kstages, 0);
         impl->stats.stage_dropped.assign(impl->kstages, 0);
         impl->stats.stage_maxfill.assign(impl->kstages, 0);
+        impl->stats.stage_top.assign(impl->kstages, {});
+        impl->stats.pair_dropped.assign(impl->h_pdrop.p, impl->h_pdrop.p + impl->kstages + 1);
         for (size_t s = 0; s < impl->kstages; ++s) {
             const size_t ns = s == 0 ? impl->genwg : NB;
             const uint32_t* m = s == 0 ? impl->h_cnt0.p : impl->h_cnt_sample.p + s * NB * NB;
+            std::vector<uint64_t> fills;
             for (size_t dd = 0; dd < NB; ++dd) {
                 uint64_t fill = 0;
                 for (size_t src = 0; src < ns; ++src) fill += m[dd * ns + src];
+                fills.push_back(fill);
                 impl->stats.stage_rows[s] += fill;
                 impl->stats.stage_maxfill[s] = std::max<uint64_t>(impl->stats.stage_maxfill[s], fill);
                 if (fill > impl->cap) {
@@ -788,6 +933,9 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
                     impl->stats.dropped_rows += fill - impl->cap;
                 }
             }
+            std::sort(fills.rbegin(), fills.rend());
+            fills.resize(std::min<size_t>(fills.size(), 8));
+            impl->stats.stage_top[s] = fills;
         }
     }
     std::vector<std::vector<std::vector<uint32_t>>> out(ns);

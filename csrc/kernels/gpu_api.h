@@ -40,6 +40,8 @@ struct EhGpuStats {
     uint64_t dropped_rows = 0;   // rows lost to bucket overflow (debug mode, nonce 0 of each batch)
     double gpu_ms = 0;
     std::vector<uint64_t> stage_rows, stage_dropped, stage_maxfill; // debug mode, last batch
+    std::vector<std::vector<uint64_t>> stage_top;
+    std::vector<uint64_t> pair_dropped;                              // debug: pair-list overflow per round (batch total)                    // debug: 8 fullest buckets per stage
 };
 
 // Batched Equihash solver: one launch sequence solves `batch` nonces at once

@@ -89,6 +89,8 @@ void bind_gpu(pyb::module_& m) {
                  d["stage_rows"] = st.stage_rows;
                  d["stage_dropped"] = st.stage_dropped;
                  d["stage_maxfill"] = st.stage_maxfill;
+                 d["stage_top"] = st.stage_top;
+                 d["pair_dropped"] = st.pair_dropped;
                  return d;
              })
         .def("reset_stats", &gpu::EquihashGpuSolver::ResetStats)

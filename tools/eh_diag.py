@@ -73,7 +73,7 @@ def phases():
         sts.append(st)
     s.solve(sts)
     s.solve(sts)
-    names = ["total", "runtable", "gather", "hash", "walk", "sort", "emit"]
+    names = ["total", "commit", "prefetch", "hash", "walk", "sort", "emit", "pf_runtable", "pf_slotmap", "pf_issue"]
     for stage, ph in enumerate(s.phase_cycles(4)):
         print(json.dumps({"round": stage + 1, **{n: round(v) for n, v in zip(names, ph)}}))
 
