@@ -40,7 +40,8 @@
 
 namespace bcpk {
 
-template <int N_, int K_, int BB_, int CAP_, int NT_, int GENWG_, int NTG_, int MAXCAND_>
+template <int N_, int K_, int BB_, int CAP_, int NT_, int GENWG_, int NTG_, int MAXCAND_, int CAP4_ = CAP_,
+          int CAP3_ = CAP_>
 struct EhCfg {
     static constexpr int N = N_, K = K_;
     static constexpr int DB = N / (K + 1);           // digit bits
@@ -48,7 +49,13 @@ struct EhCfg {
     static constexpr int RB = DB - BB_;              // in-bucket collision bits
     static constexpr int NB = 1 << BB_;              // buckets (= output areas of rounds 1..K-1)
     static constexpr int NRESTS = 1 << RB;
-    static constexpr int CAP = CAP_;                 // row slots per area / LDS rows per bucket
+    // LDS row capacity of a round by the width of the rows it reads: the narrow late rounds
+    // hold more rows (their buckets and pair lists overflow most, from duplicate subtrees)
+    static constexpr int CAP = CAP_;                 // rounds reading >= 5-word rows
+    static constexpr int cap(int round) {
+        return words(round - 1) >= 5 ? CAP_ : words(round - 1) == 4 ? CAP4_ : CAP3_;
+    }
+    static constexpr int AREA = CAP_ > CAP4_ ? (CAP_ > CAP3_ ? CAP_ : CAP3_) : (CAP4_ > CAP3_ ? CAP4_ : CAP3_);
     static constexpr int NT = NT_;                   // threads per round workgroup
     static constexpr int NW = NT_ / 64;
     static constexpr int INIT = 1 << (DB + 1);
@@ -63,34 +70,38 @@ struct EhCfg {
     static constexpr int words(int stage) { return (bits(stage) + 31) / 32; }
     static constexpr int WMAX = words(0);
     static constexpr int nsrc(int stage) { return stage == 0 ? GENWG_ : NB; } // areas holding stage rows
-    static constexpr size_t ROWS = (size_t)NB * CAP; // slots per stage per nonce (>= GENWG*RPW)
+    static constexpr size_t ROWS = (size_t)NB * AREA; // slots per stage per nonce (>= GENWG*RPW)
     static_assert((size_t)GENWG_ * RPW <= ROWS && RPW * GENWG_ == INIT, "generation areas");
     static_assert(RB > 0 && DB < 32, "digit geometry");
-    static_assert(CAP < 65535 && RPW < 65535, "u16 indices");
+    static_assert(AREA < 8192 && RPW < 65535, "u16 indices, 13-bit parent signatures");
     static_assert(NT_ % 64 == 0 && 4 * NT_ >= GENWG_ && 4 * NT_ >= NB && 4 * NTG_ >= NB, "workgroup shape");
     static_assert(words(K - 1) == 1, "final round keeps whole rows in one LDS word");
 };
 
 // Mainnet/testnet (200,9); (96,5); regtest (48,5).
-using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256>;
+using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
-using Cfg48_5 = EhCfg<48, 5, 3, 128, 64, 8, 64, 256>;
+using Cfg48_5 = EhCfg<48, 5, 3, 256, 64, 8, 64, 256>;
 
 constexpr uint32_t NIL16 = 0xffffu;
 constexpr uint32_t NIL = 0xffffffffu;
 constexpr int MAX_CHAIN = 48;
 
-// Block-wide exclusive scan of n (<= 4*NT) values in LDS `v`, in place. Returns the total.
-template <int NT>
-__device__ uint32_t block_exscan(uint32_t* v, int n, uint32_t* wsum /* >= NT/64 + 1 */) {
+// Block-wide scans over n (<= MAXPER*NT) values in LDS `v`, in place; each thread owns `per`
+// consecutive entries, waves scan with shuffles, wave totals are combined through `wsum`
+// (>= NT/64 + 1 entries).
+// Exclusive sum (entries of type T: u32, or u16 when every prefix fits). Returns the total.
+template <int NT, int MAXPER = 4, class T = uint32_t>
+__device__ uint32_t block_exscan(T* v, int n, uint32_t* wsum) {
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int per = (n + NT - 1) / NT; // each thread owns `per` consecutive entries
-    uint32_t local[4] = {0, 0, 0, 0};
+    const int per = (n + NT - 1) / NT;
+    uint32_t local[MAXPER];
     uint32_t s = 0;
-    for (int q = 0; q < per; ++q) {
+#pragma unroll
+    for (int q = 0; q < MAXPER; ++q) {
         const int i = tid * per + q;
-        local[q] = (i < n) ? v[i] : 0u;
+        local[q] = (q < per && i < n) ? (uint32_t)v[i] : 0u;
         s += local[q];
     }
     uint32_t x = s; // wave inclusive scan
@@ -112,14 +123,57 @@ __device__ uint32_t block_exscan(uint32_t* v, int n, uint32_t* wsum /* >= NT/64 
     }
     __syncthreads();
     uint32_t base = wsum[wid] + x - s;
-    for (int q = 0; q < per; ++q) {
+#pragma unroll
+    for (int q = 0; q < MAXPER; ++q) {
         const int i = tid * per + q;
-        if (i < n) v[i] = base;
+        if (q < per && i < n) v[i] = (T)base;
         base += local[q];
     }
     const uint32_t total = wsum[NW];
     __syncthreads();
     return total;
+}
+
+// Inclusive prefix maximum (entries u32 or u16).
+template <int NT, int MAXPER = 4, class T = uint32_t>
+__device__ void block_maxscan(T* v, int n, uint32_t* wsum) {
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int per = (n + NT - 1) / NT;
+    uint32_t local[MAXPER];
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < MAXPER; ++q) {
+        const int i = tid * per + q;
+        local[q] = (q < per && i < n) ? (uint32_t)v[i] : 0u;
+        s = max(s, local[q]);
+    }
+    uint32_t x = s;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x = max(x, y);
+    }
+    const uint32_t excl = __shfl_up(x, 1, 64);
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < NW; ++w) {
+            const uint32_t t = wsum[w];
+            wsum[w] = acc;
+            acc = max(acc, t);
+        }
+    }
+    __syncthreads();
+    uint32_t run = max(wsum[wid], lane ? excl : 0u);
+#pragma unroll
+    for (int q = 0; q < MAXPER; ++q) {
+        const int i = tid * per + q;
+        run = max(run, local[q]);
+        if (q < per && i < n) v[i] = (T)run;
+    }
+    __syncthreads();
 }
 
 // ------------------------------------------------------------------ stage 0
@@ -221,14 +275,21 @@ template <int NS> __device__ __forceinline__ uint32_t run_of(const uint32_t* sta
     } while (0)
 
 // LDS bytes of a persistent round (one 1024-lane workgroup per CU for (200,9)).
-template <class C> constexpr int round_tail() { return (C::NRESTS * 4 > C::CAP * 2) ? C::NRESTS * 4 : C::CAP * 2; }
-template <class C> constexpr int round_un() {
-    return (C::CAP * 2 + round_tail<C>() > C::CAP * 4) ? C::CAP * 2 + round_tail<C>() : C::CAP * 4;
+// Phase-D union (bytes): walk {sidx[CAP] u16, bend[NRESTS] u32, offp[CAP] u16};
+// prefetch {gslot[CAP] u32}.
+template <class C> constexpr int un_walk_bend(int cap) { return (cap * 2 + 3) / 4 * 4; }
+template <class C> constexpr int un_walk_offp(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
+template <class C> constexpr int round_un(int cap) {
+    const int walk = un_walk_offp<C>(cap) + cap * 2;
+    const int pref = cap * 4;
+    return walk > pref ? walk : pref;
 }
 template <class C> constexpr int round_lds(int stage, bool prune) {
     const int WI = C::words(stage - 1);
     const int NS = C::nsrc(stage - 1);
-    return C::CAP * WI * 4 + (prune ? C::CAP * 4 : 0) + C::CAP * 4 /*plist*/ + round_un<C>() +
+    const int cap = C::cap(stage);
+    const int marks = stage == C::K ? 0 : (C::AREA + C::NT - 1) / C::NT * C::NT * 2;
+    return cap * WI * 4 + (prune ? cap * 4 : 0) + marks + round_un<C>(cap) +
            2 * (2 * NS + 1) * 4 + 2 * C::NB * 4 + 256;
 }
 // Depth-1 duplicate pruning wherever its signatures fit next to the full rows.
@@ -236,19 +297,18 @@ template <class C> constexpr bool round_prunes(int stage) {
     return stage >= 2 && round_lds<C>(stage, true) <= 160 * 1024;
 }
 
-// Parent references. A stage-s row (s >= 1) at global slot g = d*CAP + t stores
-// F = (j << 16) | i: it was made in round s by workgroup d (= g / CAP, implied by the slot)
-// from its LDS rows i and j. Round s also records its gather map M_s[d*CAP + r] = global
+// Parent references. A stage-s row (s >= 1) at global slot g = d*AREA + t stores
+// F = (j << 16) | i: it was made in round s by workgroup d (= g / AREA, implied by the slot)
+// from its LDS rows i and j. Round s also records its gather map M_s[d*AREA + r] = global
 // slot (stage s-1) of LDS row r, so the index tree is walked as
 // slot -> (d, F) -> (d,i,j) -> M -> parent slots. Stage-0 F holds leaf indices.
 __device__ __forceinline__ uint64_t pack_tri(uint32_t d, uint32_t i, uint32_t j) {
     return ((uint64_t)d << 32) | (j << 16) | i;
 }
 // 2 x 16-bit signature of a row's parents for depth-1 duplicate pruning: each half is the
-// parent's LDS row (13 bits) plus 3 bits of the producing workgroup. Pairs whose signatures
-// share a half are dropped without an exact check: a false match (~1e-4 per compared pair)
-// costs a negligible fraction of the yield, and every emitted solution is re-checked for
-// distinct indices anyway.
+// parent's LDS row (13 bits) plus 3 bits of the producing workgroup. A half shared by two rows
+// is confirmed exactly by comparing the full producing workgroups (from the run table): a
+// signature-only prune would drop ~1e-4 of all pairs, ~6% of the solutions (511 pairs each).
 __device__ __forceinline__ uint32_t parent_sig(uint32_t d, uint32_t f) {
     const uint32_t i = f & 0x1fff, j = (f >> 16) & 0x1fff;
     return ((i | ((d & 7) << 13)) << 16) | (j | ((d & 7) << 13));
@@ -306,9 +366,10 @@ template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_
 //      fetch the run table of the bucket after it (registers, not waited for);
 //   C. slot map of the next bucket (16 lanes per run) -> gather map M; issue its row loads,
 //      one lane per row, 16-byte buffer loads (not waited for);
-//   D. collide bucket b: LDS hash table on the RB bits, one chain walk into an LDS pair list
-//      (depth-1 pruning), counting sort of the pairs by destination, one-lane-per-row emit
-//      (XOR, shift one digit, 16-byte stores) in slot order + one column of CNT/OFF.
+//   D. collide bucket b: counting sort of the rows by their RB bits, atomic-free pair
+//      enumeration (scan + max-scan, one lane per pair; depth-1 pruning), counting sort of the
+//      pairs by destination, one-lane-per-row emit (XOR, shift one digit, 16-byte stores) in
+//      slot order + one column of CNT/OFF.
 template <class C, int STAGE, bool STAMP>
 __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ Fin,
                                                   const uint32_t* __restrict__ CNTin,
@@ -321,27 +382,27 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     constexpr int WI = C::words(STAGE - 1);
     constexpr int WO = (STAGE < C::K) ? C::words(STAGE) : 1;
     constexpr int NS = C::nsrc(STAGE - 1);
-    constexpr int SSTRIDE = (STAGE == 1) ? C::RPW : C::CAP; // slots per source area
+    constexpr int CAP = C::cap(STAGE);                        // LDS rows / pair-list entries
+    constexpr int SSTRIDE = (STAGE == 1) ? C::RPW : C::AREA; // slots per source area
     constexpr bool FINAL = STAGE == C::K;
     constexpr bool PRUNE = round_prunes<C>(STAGE);
     static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024, "round LDS budget");
     constexpr int NT = C::NT;
     static_assert(NS <= NT, "one run-table entry per lane");
-    constexpr int RPL = (C::CAP + NT - 1) / NT; // prefetched rows per lane
-    // union: prefetch {gslot[CAP] u32}; walk {nxt[CAP] u16, head[NRESTS] u32};
-    //        sort/emit {pdst[CAP] u16, perm[CAP] u16}
-    __shared__ uint32_t rows[C::CAP * WI];
-    __shared__ uint32_t psig[PRUNE ? C::CAP : 1];
-    __shared__ uint32_t plist[FINAL ? 1 : C::CAP]; // (j << 16) | i
-    __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>()];
+    constexpr int RPL = (CAP + NT - 1) / NT; // prefetched rows per lane
+    // `un` is the phase-D union described at round_un().
+    __shared__ uint32_t rows[CAP * WI];
+    __shared__ uint32_t psig[PRUNE ? CAP : 1];
+    constexpr int MP = FINAL ? 1 : (C::AREA + NT - 1) / NT; // pairs per lane (registers)
+    constexpr int MPR = (CAP + NT - 1) / NT;                  // LDS rows per lane (scans)
+    __shared__ uint16_t pmark[FINAL ? 1 : MP * NT];           // pair index -> first sorted position
+    __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(CAP)];
     __shared__ uint32_t rpos[2][NS + 1], rsrc[2][NS], hist[C::NB], cur[C::NB];
     __shared__ uint32_t wsum[C::NW + 1];
-    __shared__ uint32_t npairs;
     uint32_t* gslot = reinterpret_cast<uint32_t*>(un);
-    uint16_t* nxt = reinterpret_cast<uint16_t*>(un);
-    uint32_t* head = reinterpret_cast<uint32_t*>(un + C::CAP * 2);
-    uint16_t* pdst = reinterpret_cast<uint16_t*>(un);
-    uint16_t* perm = reinterpret_cast<uint16_t*>(un + C::CAP * 2);
+    uint16_t* sidx = reinterpret_cast<uint16_t*>(un);
+    uint32_t* bend = reinterpret_cast<uint32_t*>(un + un_walk_bend<C>(CAP));
+    uint16_t* offp = reinterpret_cast<uint16_t*>(un + un_walk_offp<C>(CAP));
     const int tid = threadIdx.x;
     const int G = gridDim.x;
     int bk = blockIdx.x;
@@ -364,7 +425,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         const uint32_t total = block_exscan<NT>(rpos[p], NS, wsum);
         if (tid == 0) rpos[p][NS] = total;
         __syncthreads();
-        return min(total, (uint32_t)C::CAP);
+        return min(total, (uint32_t)CAP);
     };
     // A thread id the compiler cannot see through: keeps the per-lane index math of the
     // prefetch/commit loops from being hoisted out of the persistent loop (live invariants
@@ -394,7 +455,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         }
         __syncthreads();
         EH_STAMP(8);
-        uint32_t* mrow = Mout + (size_t)nonce * C::ROWS + (size_t)d * C::CAP;
+        uint32_t* mrow = Mout + (size_t)nonce * C::ROWS + (size_t)d * C::AREA;
         for (uint32_t r = tid; r < nn; r += NT) mrow[r] = gslot[r];
         // buffer loads: 32-bit lane offsets against a per-nonce descriptor keep the address
         // math out of the VGPRs that hold the prefetched rows across phase D
@@ -425,7 +486,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             row_load<WI>(rsrc_rows, so[u] * (WI * 4), v[u]);
             if constexpr (PRUNE) {
                 f[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc_refs, so[u] * 4, 0, 0);
-                fd[u] = so[u] / C::CAP;
+                fd[u] = so[u] / C::AREA;
             }
         }
     };
@@ -457,7 +518,6 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             }
         }
         for (int b = tid; b < C::NB; b += NT) hist[b] = 0;
-        if (tid == 0) npairs = 0;
         EH_STAMP(1);
         // B + C. next bucket: run table, slot map, row loads in flight
         const int bn = bk + G;
@@ -474,86 +534,125 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         __syncthreads();
         EH_STAMP(2);
 
-        // D1. LDS hash table on the RB remaining bits of the digit
-        for (int k = tid; k < C::NRESTS; k += NT) head[k] = NIL;
+        // global slot (stage STAGE-1) of LDS row r of the current bucket, from its run table
+        auto slot_of = [&](uint32_t r) -> uint32_t {
+            const uint32_t b = run_of<NS>(rpos[pb], r);
+            return b * SSTRIDE + rsrc[pb][b] + (r - rpos[pb][b]);
+        };
+        // D1. counting sort of the rows by their RB key: sidx = row ids grouped by key,
+        //     bend[key] = end of the key's group
+        auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WI] >> (32 - C::RB); };
+        for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
         __syncthreads();
-        for (uint32_t i = tid; i < n; i += NT) nxt[i] = (uint16_t)atomicExch(&head[rows[i * WI] >> (32 - C::RB)], i);
+        for (uint32_t i = tid; i < n; i += NT) atomicAdd(&bend[key_of(i)], 1u);
+        __syncthreads();
+        block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
+        for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
         if (more) issue(2, 3);
         __syncthreads();
         EH_STAMP(3);
 
-        // D2. single chain walk
-        for (uint32_t i = tid; i < n; i += NT) {
-            uint32_t ri[WI];
-#pragma unroll
-            for (int w = 0; w < WI; ++w) ri[w] = rows[i * WI + w];
-            uint32_t si = 0;
-            if constexpr (PRUNE) si = psig[i];
-            int steps = 0;
-            for (uint32_t j = nxt[i]; j != NIL16 && steps < MAX_CHAIN; j = nxt[j], ++steps) {
-                uint32_t any = 0;
-#pragma unroll
-                for (int w = 0; w < WI; ++w) any |= ri[w] ^ rows[j * WI + w];
-                if constexpr (FINAL) {
-                    if (any != 0) continue;
-                } else {
-                    if (any == 0) continue; // identical subtrees
-                }
-                if constexpr (PRUNE) {
-                    const uint32_t sj = psig[j];
-                    if ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) || (si & 0xffff) == (sj >> 16) ||
-                        (si & 0xffff) == (sj & 0xffff))
-                        continue;
-                }
-                if constexpr (FINAL) {
+        if constexpr (FINAL) {
+            // D2 (final round). Candidates are pairs equal on ALL remaining bits: each sorted
+            // position scans the rest of its key group (a few rows). No pair list, so a bucket's
+            // pair count is not capped (a capped list here silently lost solutions).
+            static_assert(WI == 1, "final-round rows are one word");
+            for (uint32_t p = tid; p < n; p += NT) {
+                const uint32_t i = sidx[p], ri = rows[i], e = bend[ri >> (32 - C::RB)];
+                for (uint32_t q = p + 1; q < e; ++q) {
+                    const uint32_t j = sidx[q];
+                    if (rows[j] != ri) continue;
+                    if constexpr (PRUNE) {
+                        const uint32_t si = psig[i], sj = psig[j];
+                        if ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) || (si & 0xffff) == (sj >> 16) ||
+                            (si & 0xffff) == (sj & 0xffff))
+                            if (slot_of(i) / C::AREA == slot_of(j) / C::AREA) continue;
+                    }
                     const uint32_t c = atomicAdd(&ncand[nonce], 1u);
                     if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
-                } else {
-                    // wave-aggregated append: one LDS atomic per wave instead of one per pair
-                    const uint64_t act = __ballot(1);
-                    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
-                    const int leader = __builtin_ctzll(act);
-                    uint32_t base = 0;
-                    if ((int)(tid & 63) == leader) base = atomicAdd(&npairs, (uint32_t)__builtin_popcountll(act));
-                    base = __shfl(base, leader, 64);
-                    const uint32_t k = base + rank;
-                    if (k < (uint32_t)C::CAP) plist[k] = (j << 16) | i;
                 }
             }
-        }
-        if (more) issue(3, 4);
-        if constexpr (!FINAL) {
-            __syncthreads(); // chains/head are dead from here: reuse them for pdst/perm
-            EH_STAMP(4);
-            // D3. counting sort of the pair list by destination bucket
-            const uint32_t np = min(npairs, (uint32_t)C::CAP);
-            if (tid == 0 && npairs > (uint32_t)C::CAP) atomicAdd(&pdrop[STAGE], npairs - C::CAP);
-            for (uint32_t k = tid; k < np; k += NT) {
-                const uint32_t pr = plist[k];
-                const uint32_t nb = ((rows[(pr & 0xffff) * WI] ^ rows[(pr >> 16) * WI]) >> (32 - C::DB)) & (C::NB - 1);
-                pdst[k] = (uint16_t)nb;
-                atomicAdd(&hist[nb], 1u);
+            if (more) issue(3, 4);
+        } else {
+            // D2. atomic-free pair enumeration. Sorted position p pairs with every later position
+            //     of its group: c_p = bend[key] - p - 1 pairs, first pair index offp[p] (exclusive
+            //     scan). A mark p at each group's first pair index, spread by an inclusive
+            //     max-scan, tells every pair index k its p; q = p + 1 + (k - offp[p]). Pairs live
+            //     in registers (MP per lane: up to MP*NT per bucket, above the row capacity:
+            //     capped pair lists lost ~9% of the solutions); identical subtrees and pairs that
+            //     share a parent are dropped.
+            // c_p is capped at 14 so every prefix fits the u16 offsets (a key group of 16+ rows is
+            // ~1e-8 likely; it only loses a few pairs)
+            for (uint32_t p = tid; p < n; p += NT) offp[p] = (uint16_t)min(bend[key_of(sidx[p])] - p - 1, 14u);
+            __syncthreads();
+            const uint32_t P = block_exscan<NT, MPR>(offp, (int)n, wsum);
+            const uint32_t Pc = min(P, (uint32_t)(MP * NT));
+            if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT);
+            for (uint32_t k = tid; k < Pc; k += NT) pmark[k] = 0;
+            __syncthreads();
+            for (uint32_t p = tid; p < n; p += NT) {
+                const uint32_t o = offp[p], e = (p + 1 < n) ? offp[p + 1] : P;
+                if (e > o && o < Pc) pmark[o] = (uint16_t)p;
             }
             __syncthreads();
+            block_maxscan<NT, MP>(pmark, (int)Pc, wsum);
+            uint32_t pv[MP], pd[MP];
+#pragma unroll
+            for (int u = 0; u < MP; ++u) {
+                const uint32_t k = tid + u * NT;
+                pv[u] = NIL;
+                pd[u] = 0;
+                if (k < Pc) {
+                    const uint32_t p = pmark[k], q = p + 1 + (k - offp[p]);
+                    const uint32_t i = sidx[p], j = sidx[q];
+                    uint32_t any = 0;
+#pragma unroll
+                    for (int w = 0; w < WI; ++w) any |= rows[i * WI + w] ^ rows[j * WI + w];
+                    bool keep = any != 0; // drop pairs of identical subtrees
+                    if constexpr (PRUNE) {
+                        const uint32_t si = psig[i], sj = psig[j];
+                        if (keep && ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) ||
+                                     (si & 0xffff) == (sj >> 16) || (si & 0xffff) == (sj & 0xffff))) {
+                            // signature hit (a shared parent, or ~1e-4 by chance): parents are
+                            // shared only if both rows were made by the same workgroup
+                            if (slot_of(i) / C::AREA == slot_of(j) / C::AREA) keep = false;
+                        }
+                    }
+                    if (keep) {
+                        pv[u] = (j << 16) | i;
+                        pd[u] = ((rows[i * WI] ^ rows[j * WI]) >> (32 - C::DB)) & (C::NB - 1); // destination
+                        atomicAdd(&hist[pd[u]], 1u);
+                    }
+                }
+            }
+            if (more) issue(3, 4);
+            __syncthreads();
+            EH_STAMP(4);
+            // D3. output runs by destination bucket: exclusive scan of the counts -> one column
+            //     of CNT/OFF; each pair then takes the next slot of its destination's run
             for (int b = tid; b < C::NB; b += NT) cur[b] = hist[b];
             __syncthreads();
-            block_exscan<NT>(cur, C::NB, wsum);
+            const uint32_t np = block_exscan<NT>(cur, C::NB, wsum);
             for (int b = tid; b < C::NB; b += NT) {
                 CNTout[matout + (size_t)b * C::NB + d] = hist[b];
                 OFFout[matout + (size_t)b * C::NB + d] = cur[b];
             }
-            __syncthreads();
-            for (uint32_t k = tid; k < np; k += NT) perm[atomicAdd(&cur[pdst[k]], 1u)] = (uint16_t)k;
+            // slot -> pair table in the (now dead) walk/prefetch union
+            uint32_t* spair = reinterpret_cast<uint32_t*>(un);
+            static_assert(round_un<C>(CAP) >= C::AREA * 4, "slot table fits the union");
+#pragma unroll
+            for (int u = 0; u < MP; ++u)
+                if (pv[u] != NIL) spair[atomicAdd(&cur[pd[u]], 1u)] = pv[u];
             if (more) issue(4, RPL);
             __syncthreads();
             EH_STAMP(5);
-            // D4. emit, one lane per output row in slot order: XOR, shift one digit, store
+            // D4. emit, one lane per output row in slot order (coalesced): XOR, shift one
+            //     digit, store
             const auto rsrc_out = __builtin_amdgcn_make_buffer_rsrc(
-                Rout + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::CAP * WO, 0, C::CAP * WO * 4, 0x00020000);
-            uint32_t* farea = Fout + (size_t)nonce * C::ROWS + (size_t)d * C::CAP;
+                Rout + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::AREA * WO, 0, C::AREA * WO * 4, 0x00020000);
+            uint32_t* farea = Fout + (size_t)nonce * C::ROWS + (size_t)d * C::AREA;
             for (uint32_t t = tid; t < np; t += NT) {
-                const uint32_t pr = plist[perm[t]];
+                const uint32_t pr = spair[t];
                 const uint32_t i = pr & 0xffff, j = pr >> 16;
                 uint32_t x[WI + 1], o[WO];
 #pragma unroll
@@ -610,13 +709,13 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
             const uint64_t tr = tri[t >> 1];
             const uint32_t dd = (uint32_t)(tr >> 32);
             const uint32_t r = (t & 1) ? (((uint32_t)tr >> 16) & 0xffff) : ((uint32_t)tr & 0xffff);
-            buf[cur][t] = Ms[(size_t)dd * C::CAP + r];
+            buf[cur][t] = Ms[(size_t)dd * C::AREA + r];
         }
         __syncthreads();
         if (s > 1 && t < 2 * cnt) {
             const uint32_t slot = buf[cur][t];
             const uint32_t fr = F[(size_t)(s - 1) * batch * C::ROWS + (size_t)nonce * C::ROWS + slot];
-            tri[t] = pack_tri(slot / C::CAP, fr & 0xffff, fr >> 16);
+            tri[t] = pack_tri(slot / C::AREA, fr & 0xffff, fr >> 16);
         }
     }
     __syncthreads();
@@ -704,7 +803,8 @@ struct EquihashGpuSolver::Impl {
     HostBuf<bcpk::EhBaseState> h_states;
     HostBuf<uint32_t> h_ncand, h_idx, h_valid, h_cnt_sample, h_cnt0;
     size_t genwg = 0;
-    size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0, cap = 0;
+    size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
+    std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
     int inflight = 0;
     int ncu = 1;
     bool debug = false, stamp_mode = false;
@@ -717,7 +817,8 @@ struct EquihashGpuSolver::Impl {
         L = C::L;
         maxcand = C::MAXCAND;
         nb = C::NB;
-        cap = C::CAP;
+        caps.clear();
+        for (int r = 1; r <= C::K; ++r) caps.push_back(C::cap(r));
         kstages = C::K;
         d_states.alloc(batch);
         h_states.alloc(batch);
@@ -784,6 +885,7 @@ struct EquihashGpuSolver::Impl {
                                      hipMemcpyHostToDevice, stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ncand.p, 0, batch * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_pdrop.p, 0, (C::K + 1) * sizeof(uint32_t), stream));
+        if (debug) BCP_HIP_CHECK(hipMemsetAsync(d_refs.p, 0xff, d_refs.n * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipEventRecord(ev0, stream));
         // header-shaped inputs (140 B: g lands at byte 12 of the final block) take the
         // zero-message-word BLAKE2b specialisation
@@ -889,6 +991,20 @@ std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
     return out;
 }
 void EquihashGpuSolver::ResetStats() { impl->stats = EhGpuStats(); }
+
+// Debug: parent refs F (K stages) then gather maps M (K rounds) of nonce 0 of the last batch,
+// each ROWS slots; with SetDebug(true) never-written F slots read 0xffffffff.
+std::vector<uint32_t> EquihashGpuSolver::DebugDump() {
+    BCP_HIP_CHECK(hipSetDevice(impl->device));
+    BCP_HIP_CHECK(hipStreamSynchronize(impl->stream));
+    const size_t R = impl->rows, K = impl->kstages, B = impl->batch;
+    std::vector<uint32_t> out(2 * K * R);
+    for (size_t s = 0; s < K; ++s) {
+        BCP_HIP_CHECK(hipMemcpy(out.data() + s * R, impl->d_refs.p + s * B * R, R * 4, hipMemcpyDeviceToHost));
+        BCP_HIP_CHECK(hipMemcpy(out.data() + (K + s) * R, impl->d_maps.p + s * B * R, R * 4, hipMemcpyDeviceToHost));
+    }
+    return out;
+}
 size_t EquihashGpuSolver::DeviceBytes() const { return impl->bytes; }
 
 void EquihashGpuSolver::Launch(const std::vector<EhBaseState>& states) {
@@ -928,9 +1044,9 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
                 fills.push_back(fill);
                 impl->stats.stage_rows[s] += fill;
                 impl->stats.stage_maxfill[s] = std::max<uint64_t>(impl->stats.stage_maxfill[s], fill);
-                if (fill > impl->cap) {
-                    impl->stats.stage_dropped[s] += fill - impl->cap;
-                    impl->stats.dropped_rows += fill - impl->cap;
+                if (fill > impl->caps[s]) {
+                    impl->stats.stage_dropped[s] += fill - impl->caps[s];
+                    impl->stats.dropped_rows += fill - impl->caps[s];
                 }
             }
             std::sort(fills.rbegin(), fills.rend());
@@ -939,6 +1055,14 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
         }
     }
     std::vector<std::vector<std::vector<uint32_t>>> out(ns);
+    if (impl->debug) {
+        impl->stats.debug_cands.clear();
+        const uint32_t nc = std::min<uint32_t>(impl->h_ncand.p[0], (uint32_t)impl->maxcand);
+        for (uint32_t c = 0; c < nc; ++c) {
+            const uint32_t* p = impl->h_idx.p + (size_t)c * impl->L;
+            impl->stats.debug_cands.emplace_back(p, p + impl->L);
+        }
+    }
     for (int nn = 0; nn < ns; ++nn) {
         uint32_t nc = std::min<uint32_t>(impl->h_ncand.p[nn], (uint32_t)impl->maxcand);
         impl->stats.candidates += nc;

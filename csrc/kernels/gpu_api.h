@@ -41,7 +41,8 @@ struct EhGpuStats {
     double gpu_ms = 0;
     std::vector<uint64_t> stage_rows, stage_dropped, stage_maxfill; // debug mode, last batch
     std::vector<std::vector<uint64_t>> stage_top;
-    std::vector<uint64_t> pair_dropped;                              // debug: pair-list overflow per round (batch total)                    // debug: 8 fullest buckets per stage
+    std::vector<uint64_t> pair_dropped;
+    std::vector<std::vector<uint32_t>> debug_cands;                  // debug: every candidate of nonce 0 (valid or not)                              // debug: pair-list overflow per round (batch total)                    // debug: 8 fullest buckets per stage
 };
 
 // Batched Equihash solver: one launch sequence solves `batch` nonces at once
@@ -63,6 +64,7 @@ public:
     const EhGpuStats& Stats() const;
     void SetDebug(bool on);   // collect per-stage bucket statistics (extra D2H copies)
     void SetStampMode(bool on); // diagnostic: launch phase-timestamped round kernels
+    std::vector<uint32_t> DebugDump(); // diagnostic: parent refs + gather maps of nonce 0
     std::vector<std::vector<double>> PhaseCycles(int nonces);
     void ResetStats();
     size_t DeviceBytes() const;

@@ -91,11 +91,13 @@ void bind_gpu(pyb::module_& m) {
                  d["stage_maxfill"] = st.stage_maxfill;
                  d["stage_top"] = st.stage_top;
                  d["pair_dropped"] = st.pair_dropped;
+                 d["debug_cands"] = st.debug_cands;
                  return d;
              })
         .def("reset_stats", &gpu::EquihashGpuSolver::ResetStats)
         .def("set_debug", &gpu::EquihashGpuSolver::SetDebug)
         .def("set_stamp_mode", &gpu::EquihashGpuSolver::SetStampMode)
+        .def("debug_dump", &gpu::EquihashGpuSolver::DebugDump)
         .def("phase_cycles", &gpu::EquihashGpuSolver::PhaseCycles);
 
     m.def(
