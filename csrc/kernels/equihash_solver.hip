@@ -637,6 +637,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                 CNTout[matout + (size_t)b * C::NB + d] = hist[b];
                 OFFout[matout + (size_t)b * C::NB + d] = cur[b];
             }
+            __syncthreads(); // every OFF column entry is read before cur[] is advanced
             // slot -> pair table in the (now dead) walk/prefetch union
             uint32_t* spair = reinterpret_cast<uint32_t*>(un);
             static_assert(round_un<C>(CAP) >= C::AREA * 4, "slot table fits the union");
