@@ -210,10 +210,25 @@ void CNode::PushBlockHash(const uint256& hash) {
     vBlockHashesToAnnounce.push_back(hash);
 }
 
+limitedmap<uint256, int64_t> mapAlreadyAskedFor(MAX_INV_SZ);
+std::mutex cs_mapAlreadyAskedFor;
+
 void CNode::AskFor(const CInv& inv) {
     std::lock_guard<std::mutex> l(cs_inventory);
-    if (mapAskFor.size() > MAX_INV_SZ) return;
-    mapAskFor.insert({GetTimeMicros(), inv});
+    if (mapAskFor.size() > MAX_INV_SZ || setAskFor.size() > MAX_INV_SZ) return;
+    if (!setAskFor.insert(inv.hash).second) return; // already queued from this peer
+    // each further peer asked for the same hash waits 2 minutes longer, so one slow or lying
+    // peer delays but never blocks relay; request times are kept strictly increasing
+    static int64_t nLastTime = 0;
+    std::lock_guard<std::mutex> la(cs_mapAlreadyAskedFor);
+    int64_t nNow = GetTimeMicros() - 1000000;
+    nNow = std::max(nNow, ++nLastTime);
+    nLastTime = nNow;
+    auto it = mapAlreadyAskedFor.find(inv.hash);
+    const int64_t nRequestTime = std::max(it != mapAlreadyAskedFor.end() ? it->second + 2 * 60 * 1000000 : 0, nNow);
+    if (it != mapAlreadyAskedFor.end()) mapAlreadyAskedFor.update(it, nRequestTime);
+    else mapAlreadyAskedFor.insert({inv.hash, nRequestTime});
+    mapAskFor.insert({nRequestTime, inv});
 }
 
 void CNode::CopyStats(CNodeStats& st) const {

@@ -9,6 +9,7 @@
 // Design: a poll(2) socket thread (no select FD_SETSIZE cap) and one message thread
 // that round-robins peers, both event-driven by a condition variable.
 #pragma once
+#include "util/limitedmap.h"
 #include "consensus/merkleblock.h"
 #include "crypto/hashes.h"
 #include "keys/key.h"
@@ -31,6 +32,11 @@
 #include <vector>
 
 namespace bcp {
+
+// txid -> earliest time (us) any peer may be asked for it; staggers requests for the same
+// transaction across peers by 2 minutes each (reference net.cpp mapAlreadyAskedFor).
+extern limitedmap<uint256, int64_t> mapAlreadyAskedFor;
+extern std::mutex cs_mapAlreadyAskedFor;
 
 typedef int64_t NodeId;
 class CConnman;
@@ -179,6 +185,7 @@ public:
     std::vector<uint256> vInventoryBlockToSend;
     std::vector<uint256> vBlockHashesToAnnounce;
     std::multimap<int64_t, CInv> mapAskFor;
+    std::set<uint256> setAskFor; // hashes queued in mapAskFor (one request per hash per peer)
     bool fSendMempool = false;
     int64_t nNextInvSend = 0;
     std::atomic<int64_t> timeLastMempoolReq{0};

@@ -1205,6 +1205,11 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
             for (auto it = pfrom->mapAskFor.begin(); it != pfrom->mapAskFor.end();)
                 if (it->second.hash == inv.hash) it = pfrom->mapAskFor.erase(it);
                 else ++it;
+            pfrom->setAskFor.erase(inv.hash);
+        }
+        {
+            std::lock_guard<std::mutex> la(cs_mapAlreadyAskedFor);
+            mapAlreadyAskedFor.erase(inv.hash);
         }
         if (!AlreadyHave(inv) && cs->AcceptToMemoryPool(state, ptx, true, &fMissingInputs)) {
             RelayTransaction(tx);
@@ -1959,7 +1964,12 @@ bool PeerLogicValidation::SendMessages(CNode* pto, std::atomic<bool>& interrupt)
                     I.Push(pto, msgMaker.Make(NetMsgType::GETDATA, vGetData));
                     vGetData.clear();
                 }
+            } else {
+                // got it already: other peers need not be asked
+                std::lock_guard<std::mutex> la(cs_mapAlreadyAskedFor);
+                mapAlreadyAskedFor.erase(inv.hash);
             }
+            pto->setAskFor.erase(inv.hash);
             pto->mapAskFor.erase(pto->mapAskFor.begin());
         }
     }
@@ -1972,6 +1982,8 @@ bool PeerLogicValidation::SendMessages(CNode* pto, std::atomic<bool>& interrupt)
         Amount currentFilter = I.pool->GetMinFee((size_t)maxmempool).GetFeePerK();
         const int64_t timeNow = GetTimeMicros();
         if (timeNow > pto->nextSendTimeFeeFilter) {
+            static FeeFilterRounder filterRounder(minRelayTxFee);
+            currentFilter = filterRounder.round(currentFilter);
             currentFilter = std::max(currentFilter, minRelayTxFee.GetFeePerK());
             if (currentFilter != pto->lastSentFeeFilter) {
                 I.Push(pto, msgMaker.Make(NetMsgType::FEEFILTER, (int64_t)currentFilter));

@@ -1,4 +1,5 @@
 #include "node/coins.h"
+#include "util/memusage.h"
 #include "keys/key.h"
 #include "secp256k1/secp256k1.h"
 
@@ -135,9 +136,8 @@ SaltedOutpointHasher::SaltedOutpointHasher() {
 CCoinsViewCache::CCoinsViewCache(CCoinsView* b) : CCoinsViewBacked(b) {}
 
 size_t CCoinsViewCache::DynamicMemoryUsage() const {
-    // node overhead (~ key + entry + bucket pointer) plus script heap usage
-    return cacheCoins.size() * (sizeof(COutPoint) + sizeof(CCoinsCacheEntry) + 2 * sizeof(void*)) +
-           cacheCoins.bucket_count() * sizeof(void*) + cachedCoinsUsage;
+    // hash-table nodes and buckets plus the scripts' heap buffers (reference coins.cpp)
+    return memusage::DynamicUsage(cacheCoins) + cachedCoinsUsage;
 }
 
 CCoinsMap::iterator CCoinsViewCache::FetchCoin(const COutPoint& outpoint) const {

@@ -78,7 +78,9 @@ public:
     bool IsCoinBase() const { return fCoinBase; }
     uint32_t GetHeight() const { return nHeight; }
     const CTxOut& GetTxOut() const { return out; }
-    size_t DynamicMemoryUsage() const { return out.scriptPubKey.capacity(); }
+    size_t DynamicMemoryUsage() const {
+        return out.scriptPubKey.capacity() ? ((out.scriptPubKey.capacity() + 8 + 15) & ~(size_t)15) : 0;
+    }
 
     template <typename S> void Serialize(S& s) const {
         WriteVarInt(s, (uint64_t)nHeight * 2 + (fCoinBase ? 1 : 0));

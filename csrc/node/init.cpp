@@ -49,6 +49,8 @@ std::string HelpMessage() {
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
         {"-blocknotify=<cmd>", "Execute command when the best block changes (%s in cmd is replaced by block hash)"},
+        {"-disablesafemode", "Disable safemode, override a real safe mode event (default: 0)"},
+        {"-testsafemode", "Force safe mode (default: 0)"},
         {"-alertnotify=<cmd>", "Execute command when a relevant alert is received or we see a really long fork (%s in cmd is replaced by message)"},
         {"-txindex", "Maintain a full transaction index (default: 0)"},
         {"-prune=<n>", "Reduce storage by pruning old blocks (MiB target, >= 550)"},
@@ -299,6 +301,7 @@ int AppMain(int argc, char* argv[]) {
             return 1;
         }
     }
+    if (node->mempool && node->mempool->Estimator()) node->mempool->Estimator()->Read(datadir + "/fee_estimates.dat");
     if (gArgs.GetBoolArg("-persistmempool", true)) {
         uiInterface.InitMessage("Loading mempool...");
         node->chainstate->LoadMempool(datadir + "/mempool.dat");
@@ -347,6 +350,7 @@ int AppMain(int argc, char* argv[]) {
     StopZMQ(*node);
     StopNetwork(*node);
     if (gArgs.GetBoolArg("-persistmempool", true)) node->chainstate->DumpMempool(datadir + "/mempool.dat");
+    if (node->mempool && node->mempool->Estimator()) node->mempool->Estimator()->Write(datadir + "/fee_estimates.dat");
     StopWallet(*node);
     if (node->scheduler) node->scheduler->Stop();
     node->chainstate->Shutdown();

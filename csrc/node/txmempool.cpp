@@ -1,21 +1,30 @@
 #include "node/txmempool.h"
+#include "keys/key.h"
 #include "consensus/tx_verify.h"
 #include "node/policy.h"
 #include "node/signals.h"
 #include "util/strencodings.h"
 #include "util/util.h"
+#include "util/memusage.h"
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
 #include <deque>
 #include <stdexcept>
 
 namespace bcp {
 
 // ------------------------------------------------------------------ entry
+// Heap usage of a transaction (reference core_memusage.h RecursiveDynamicUsage): the tx object
+// in its make_shared block, its vin/vout arrays, and every script's byte buffer.
 static size_t TxUsage(const CTransaction& tx) {
-    // heap usage estimate: serialized bytes plus per-vector overheads
-    return tx.GetTotalSize() + 64 * (tx.vin.size() + tx.vout.size()) + 128;
+    size_t mem = memusage::MallocUsage(sizeof(CTransaction) + 2 * sizeof(long) + sizeof(void*)) +
+                 memusage::DynamicUsage(tx.vin) + memusage::DynamicUsage(tx.vout);
+    for (const CTxIn& in : tx.vin) mem += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(in.scriptSig));
+    for (const CTxOut& out : tx.vout)
+        mem += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(out.scriptPubKey));
+    return mem;
 }
 
 CTxMemPoolEntry::CTxMemPoolEntry(const CTransactionRef& t, Amount fee, int64_t time, double priority,
@@ -164,7 +173,7 @@ void CTxMemPool::addUnchecked(const uint256& hash, const CTxMemPoolEntry& entry,
     const CTransaction& tx = newit->second->GetTx();
     std::set<uint256> setParentTransactions;
     for (const CTxIn& in : tx.vin) {
-        mapNextTx[in.prevout] = &tx;
+        mapNextTx.insert(std::make_pair(&in.prevout, &tx));
         setParentTransactions.insert(in.prevout.hash);
     }
     for (const uint256& ph : setParentTransactions) {
@@ -177,7 +186,7 @@ void CTxMemPool::addUnchecked(const uint256& hash, const CTxMemPoolEntry& entry,
     totalTxSize += entry.GetTxSize();
     if (minerPolicyEstimator)
         minerPolicyEstimator->processTransaction(hash, CFeeRate(entry.GetFee(), entry.GetTxSize()), entry.GetHeight(),
-                                                 validFeeEstimate);
+                                                 validFeeEstimate, entry.GetPriority(entry.GetHeight()));
 }
 
 void CTxMemPool::CalculateDescendants(txiter entryit, setEntries& setDescendants) {
@@ -464,7 +473,7 @@ void CTxMemPool::UpdateTransactionsFromBlock(const std::vector<uint256>& vHashes
         if (it == mapTx.end()) continue;
         setEntries setChildren;
         auto iter = mapNextTx.lower_bound(COutPoint(*hit, 0));
-        for (; iter != mapNextTx.end() && iter->first.hash == *hit; ++iter) {
+        for (; iter != mapNextTx.end() && iter->first->hash == *hit; ++iter) {
             auto childIter = mapTx.find(iter->second->GetHash());
             if (childIter == mapTx.end()) continue;
             if (setChildren.insert(childIter).second && !setAlreadyIncluded.count(childIter->first)) {
@@ -641,8 +650,12 @@ uint64_t CTxMemPool::GetTotalTxSize() const {
 }
 size_t CTxMemPool::DynamicMemoryUsage() const {
     std::lock_guard<CCriticalSection> l(cs);
-    return mapTx.size() * (sizeof(CTxMemPoolEntry) + 96) + mapNextTx.size() * 80 + mapLinks.size() * 128 +
-           mapDeltas.size() * 64 + cachedInnerUsage;
+    // index nodes + entries + link sets (reference CTxMemPool::DynamicMemoryUsage)
+    size_t links = 0;
+    for (const auto& l : mapLinks) links += memusage::DynamicUsage(l.second.parents) + memusage::DynamicUsage(l.second.children);
+    return memusage::DynamicUsage(mapTx) + mapTx.size() * memusage::MallocUsage(sizeof(CTxMemPoolEntry)) +
+           memusage::MallocUsage(sizeof(memusage::stl_tree_node) + 2 * sizeof(void*)) * mapNextTx.size() +
+           memusage::DynamicUsage(mapLinks) + links + memusage::DynamicUsage(mapDeltas) + cachedInnerUsage;
 }
 unsigned CTxMemPool::GetTransactionsUpdated() const {
     std::lock_guard<CCriticalSection> l(cs);
@@ -711,23 +724,64 @@ bool CCoinsViewMemPool::HaveCoin(const COutPoint& outpoint) const {
 }
 
 // ------------------------------------------------------------------ fee estimator
-CBlockPolicyEstimator::CBlockPolicyEstimator() {
-    for (double b = 1000; b <= 1e7; b *= 1.1) buckets.push_back(b);
+// Reference policy/fees.cpp: per-bucket exponentially decayed (0.998/block) counts of how many
+// blocks transactions took to confirm; an estimate for a target is the lowest bucket group
+// (scanning from the top, grouping until enough data) whose in-target confirmation rate is
+// >= 95%. Fee rates bucket from 1000 to 1e7 sat/kB, priorities from 1e6 to 1e16, 1.1x / 2x apart.
+static const double MIN_FEE_BUCKET = 1000, MAX_FEE_BUCKET = 1e7, FEE_SPACING = 1.1;
+static const double MIN_PRI_BUCKET = 1e6, MAX_PRI_BUCKET = 1e16, PRI_SPACING = 2;
+static const double DECAY = 0.998, MIN_SUCCESS = 0.95, SUFFICIENT_TXS = 1.0;
+static const uint32_t FEE_ESTIMATES_VERSION = 170001;
+
+void CBlockPolicyEstimator::Stats::Init(double lo, double hi, double spacing) {
+    buckets.clear();
+    for (double b = lo; b <= hi; b *= spacing) buckets.push_back(b);
     buckets.push_back(1e99);
     confAvg.assign(MAX_TARGET + 1, std::vector<double>(buckets.size(), 0.0));
     txAvg.assign(buckets.size(), 0.0);
 }
-int CBlockPolicyEstimator::BucketFor(const CFeeRate& r) const {
-    const double v = (double)r.GetFeePerK();
-    return (int)(std::lower_bound(buckets.begin(), buckets.end(), v) - buckets.begin());
+int CBlockPolicyEstimator::Stats::BucketFor(double v) const {
+    const int b = (int)(std::lower_bound(buckets.begin(), buckets.end(), v) - buckets.begin());
+    return std::min(b, (int)buckets.size() - 1);
+}
+void CBlockPolicyEstimator::Stats::Decay(double d) {
+    for (auto& row : confAvg)
+        for (double& x : row) x *= d;
+    for (double& x : txAvg) x *= d;
+}
+void CBlockPolicyEstimator::Stats::Record(int blocks, int bucket) {
+    for (int t = std::max(1, blocks); t <= MAX_TARGET; t++) confAvg[t][bucket] += 1;
+    txAvg[bucket] += 1;
+}
+double CBlockPolicyEstimator::Stats::Estimate(int confTarget, double minValue) const {
+    if (confTarget < 1 || confTarget > MAX_TARGET) return -1;
+    double nConf = 0, nTotal = 0;
+    int best = -1;
+    for (int b = (int)buckets.size() - 1; b >= 0; b--) {
+        nConf += confAvg[confTarget][b];
+        nTotal += txAvg[b];
+        if (nTotal >= SUFFICIENT_TXS) {
+            if (nConf / nTotal >= MIN_SUCCESS) best = b;
+            else break;
+            nConf = nTotal = 0;
+        }
+    }
+    if (best < 0) return -1;
+    const double v = best < (int)buckets.size() - 1 ? buckets[best] : buckets[buckets.size() - 2];
+    return std::max(v, minValue);
+}
+
+CBlockPolicyEstimator::CBlockPolicyEstimator() {
+    feeStats.Init(MIN_FEE_BUCKET, MAX_FEE_BUCKET, FEE_SPACING);
+    priStats.Init(MIN_PRI_BUCKET, MAX_PRI_BUCKET, PRI_SPACING);
 }
 void CBlockPolicyEstimator::processTransaction(const uint256& txid, const CFeeRate& rate, unsigned height,
-                                               bool valid) {
+                                               bool valid, double priority) {
     if (!valid) return;
     std::lock_guard<std::mutex> l(cs);
-    int b = BucketFor(rate);
-    if (b >= (int)buckets.size()) b = (int)buckets.size() - 1;
-    mapTracked[txid] = Tracked{height, b};
+    // fee payers are tracked by fee rate; zero-fee txs with a meaningful priority by priority
+    if (rate.GetFeePerK() > 0) mapTracked[txid] = Tracked{height, feeStats.BucketFor((double)rate.GetFeePerK()), false};
+    else if (priority >= MIN_PRI_BUCKET) mapTracked[txid] = Tracked{height, priStats.BucketFor(priority), true};
 }
 void CBlockPolicyEstimator::removeTx(const uint256& txid) {
     std::lock_guard<std::mutex> l(cs);
@@ -737,37 +791,20 @@ void CBlockPolicyEstimator::processBlock(unsigned height, const std::vector<uint
     std::lock_guard<std::mutex> l(cs);
     if (height <= bestHeight) return;
     bestHeight = height;
-    const double decay = 0.998;
-    for (auto& row : confAvg)
-        for (double& x : row) x *= decay;
-    for (double& x : txAvg) x *= decay;
+    feeStats.Decay(DECAY);
+    priStats.Decay(DECAY);
     for (const uint256& h : confirmed) {
         auto it = mapTracked.find(h);
         if (it == mapTracked.end()) continue;
         const int blocks = std::max(1, (int)height - (int)it->second.height);
-        for (int t = blocks; t <= MAX_TARGET; t++) confAvg[t][it->second.bucket] += 1;
-        txAvg[it->second.bucket] += 1;
+        (it->second.priority ? priStats : feeStats).Record(blocks, it->second.bucket);
         mapTracked.erase(it);
     }
 }
 CFeeRate CBlockPolicyEstimator::estimateFee(int confTarget) const {
     std::lock_guard<std::mutex> l(cs);
-    if (confTarget < 1 || confTarget > MAX_TARGET) return CFeeRate(0);
-    // scan from high to low fee rates, grouping buckets until enough data; keep the
-    // lowest group whose confirmation rate within target is >= 95%
-    double nConf = 0, nTotal = 0;
-    int best = -1;
-    for (int b = (int)buckets.size() - 1; b >= 0; b--) {
-        nConf += confAvg[confTarget][b];
-        nTotal += txAvg[b];
-        if (nTotal >= 1.0) {
-            if (nConf / nTotal >= 0.95) best = b;
-            else break;
-            nConf = nTotal = 0;
-        }
-    }
-    if (best < 0) return CFeeRate(0);
-    return CFeeRate((Amount)(best < (int)buckets.size() - 1 ? buckets[best] : buckets[buckets.size() - 2]));
+    const double v = feeStats.Estimate(confTarget, 0);
+    return CFeeRate(v < 0 ? 0 : (Amount)v);
 }
 CFeeRate CBlockPolicyEstimator::estimateSmartFee(int confTarget, int* answerFoundAtTarget) const {
     for (int t = std::max(1, confTarget); t <= MAX_TARGET; t++) {
@@ -779,6 +816,102 @@ CFeeRate CBlockPolicyEstimator::estimateSmartFee(int confTarget, int* answerFoun
     }
     if (answerFoundAtTarget) *answerFoundAtTarget = MAX_TARGET;
     return CFeeRate(0);
+}
+double CBlockPolicyEstimator::estimatePriority(int confTarget) const {
+    std::lock_guard<std::mutex> l(cs);
+    return priStats.Estimate(confTarget, 0);
+}
+double CBlockPolicyEstimator::estimateSmartPriority(int confTarget, int* answerFoundAtTarget) const {
+    for (int t = std::max(1, confTarget); t <= MAX_TARGET; t++) {
+        const double p = estimatePriority(t);
+        if (p >= 0) {
+            if (answerFoundAtTarget) *answerFoundAtTarget = t;
+            return p;
+        }
+    }
+    if (answerFoundAtTarget) *answerFoundAtTarget = MAX_TARGET;
+    return -1;
+}
+
+bool CBlockPolicyEstimator::Write(const std::string& path) const {
+    std::vector<unsigned char> out;
+    {
+        std::lock_guard<std::mutex> l(cs);
+        VectorWriter w(out, SER_DISK, PROTOCOL_VERSION);
+        auto wd = [&](double x) { // doubles as their IEEE-754 bit patterns
+            uint64_t u;
+            memcpy(&u, &x, 8);
+            w << u;
+        };
+        w << FEE_ESTIMATES_VERSION << bestHeight;
+        for (const Stats* st : {&feeStats, &priStats}) {
+            w << (uint64_t)st->buckets.size();
+            for (double b : st->buckets) wd(b);
+            for (const auto& row : st->confAvg)
+                for (double x : row) wd(x);
+            for (double x : st->txAvg) wd(x);
+        }
+    }
+    const std::string tmp = path + ".new";
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) return false;
+    const bool ok = fwrite(out.data(), 1, out.size(), f) == out.size();
+    fclose(f);
+    return ok && rename(tmp.c_str(), path.c_str()) == 0;
+}
+
+bool CBlockPolicyEstimator::Read(const std::string& path) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    std::vector<unsigned char> data;
+    unsigned char buf[65536];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof(buf), f)) > 0) data.insert(data.end(), buf, buf + n);
+    fclose(f);
+    try {
+        SpanReader r(data.data(), data.size(), SER_DISK, PROTOCOL_VERSION);
+        auto rd = [&](double& x) {
+            uint64_t u;
+            r >> u;
+            memcpy(&x, &u, 8);
+        };
+        uint32_t version;
+        unsigned height;
+        r >> version >> height;
+        if (version != FEE_ESTIMATES_VERSION) return false;
+        Stats loaded[2];
+        for (Stats& st : loaded) {
+            uint64_t nb;
+            r >> nb;
+            if (nb == 0 || nb > 1000) throw std::runtime_error("bad bucket count");
+            st.buckets.resize(nb);
+            for (double& b : st.buckets) rd(b);
+            st.confAvg.assign(MAX_TARGET + 1, std::vector<double>(nb));
+            for (auto& row : st.confAvg)
+                for (double& x : row) rd(x);
+            st.txAvg.resize(nb);
+            for (double& x : st.txAvg) rd(x);
+        }
+        std::lock_guard<std::mutex> l(cs);
+        feeStats = loaded[0];
+        priStats = loaded[1];
+        bestHeight = height;
+    } catch (const std::exception& e) {
+        LogPrintf("CBlockPolicyEstimator::Read(): unable to read policy estimator data (non-fatal): %s\n", e.what());
+        return false;
+    }
+    return true;
+}
+
+FeeFilterRounder::FeeFilterRounder(const CFeeRate& minIncrementalFee) {
+    const double minFeeLimit = std::max((double)1, (double)minIncrementalFee.GetFeePerK() / 2);
+    feeset.insert(0);
+    for (double b = minFeeLimit; b <= MAX_FEE_BUCKET; b *= FEE_SPACING) feeset.insert(b);
+}
+Amount FeeFilterRounder::round(Amount currentMinFee) {
+    auto it = feeset.lower_bound((double)currentMinFee);
+    if ((it != feeset.begin() && GetRand(3) != 0) || it == feeset.end()) --it;
+    return (Amount)*it;
 }
 
 } // namespace bcp

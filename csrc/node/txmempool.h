@@ -13,6 +13,8 @@
 #include "primitives/transaction.h"
 #include "util/sync.h"
 
+#include "util/indirectmap.h"
+
 #include <map>
 #include <memory>
 #include <mutex>
@@ -91,26 +93,53 @@ struct TxMempoolInfo {
 class CBlockPolicyEstimator {
 public:
     CBlockPolicyEstimator();
-    void processTransaction(const uint256& txid, const CFeeRate& rate, unsigned height, bool validForEstimation);
+    // priority < 0: not tracked for priority (reference fees.h priStats; free txs with
+    // priority are tracked there, fee payers in feeStats)
+    void processTransaction(const uint256& txid, const CFeeRate& rate, unsigned height, bool validForEstimation,
+                            double priority = -1);
     void processBlock(unsigned height, const std::vector<uint256>& confirmedTxids);
     void removeTx(const uint256& txid);
     CFeeRate estimateFee(int confTarget) const;
     CFeeRate estimateSmartFee(int confTarget, int* answerFoundAtTarget) const;
-    double estimatePriority(int) const { return -1; }
+    double estimatePriority(int confTarget) const;
+    double estimateSmartPriority(int confTarget, int* answerFoundAtTarget) const;
+    // fee_estimates.dat (reference CBlockPolicyEstimator::Write/Read, txmempool.cpp:954-990)
+    bool Write(const std::string& path) const;
+    bool Read(const std::string& path);
 
 private:
+    // One decayed confirmation table over value buckets (fee rate in sat/kB, or priority).
+    struct Stats {
+        std::vector<double> buckets;              // upper bucket bounds
+        std::vector<std::vector<double>> confAvg; // [target][bucket] decayed confirmed counts
+        std::vector<double> txAvg;                // [bucket] decayed totals
+        void Init(double lo, double hi, double spacing);
+        int BucketFor(double v) const;
+        void Decay(double d);
+        void Record(int blocks, int bucket);
+        double Estimate(int confTarget, double minValue) const;
+    };
     struct Tracked {
         unsigned height;
         int bucket;
+        bool priority; // tracked in priStats instead of feeStats
     };
-    int BucketFor(const CFeeRate& r) const;
-    std::vector<double> buckets;                    // fee-rate bucket boundaries (sat/kB)
-    std::vector<std::vector<double>> confAvg;       // [target][bucket] decayed confirmed counts
-    std::vector<double> txAvg;                      // [bucket] decayed totals
+    Stats feeStats, priStats;
     std::map<uint256, Tracked> mapTracked;
     unsigned bestHeight = 0;
     static const int MAX_TARGET = 25;
     mutable std::mutex cs;
+};
+
+// Rounds the fee filter we announce to peers to a coarse, randomized bucket so the exact
+// mempool minimum fee does not fingerprint the node (reference policy/fees.h FeeFilterRounder).
+class FeeFilterRounder {
+public:
+    explicit FeeFilterRounder(const CFeeRate& minIncrementalFee);
+    Amount round(Amount currentMinFee);
+
+private:
+    std::set<double> feeset;
 };
 
 class CTxMemPool {
@@ -181,7 +210,7 @@ public:
     void setSanityCheck(double dFrequency) { nCheckFrequency = (uint32_t)(dFrequency * 4294967295.0); }
     CBlockPolicyEstimator* Estimator() { return minerPolicyEstimator; }
 
-    std::map<COutPoint, const CTransaction*> mapNextTx;
+    indirectmap<COutPoint, const CTransaction*> mapNextTx; // keys point into the spending txs
 
 private:
     struct Links {

@@ -2,6 +2,7 @@
 // See validation.h for the parity map.
 #include "node/validation.h"
 #include "node/ui_interface.h"
+#include "node/warnings.h"
 #include "consensus/merkle.h"
 #include "consensus/pow.h"
 #include "node/policy.h"
@@ -955,7 +956,7 @@ void Chainstate::UpdateTip(CBlockIndex* pindexNew) {
     chainActive.SetTip(pindexNew);
     if (mempool) mempool->AddTransactionsUpdated(1);
     cvBlockChange.notify_all();
-    strMiscWarning.clear();
+    std::string strWarning;
     if (!IsInitialBlockDownload()) {
         int nUpgraded = 0;
         const CBlockIndex* pindex = chainActive.Tip();
@@ -966,14 +967,15 @@ void Chainstate::UpdateTip(CBlockIndex* pindexNew) {
             pindex = pindex->pprev;
         }
         if (nUpgraded > 100 / 2) {
-            strMiscWarning = "Warning: Unknown block versions being mined! It's possible unknown rules are in effect";
+            strWarning = "Warning: Unknown block versions being mined! It's possible unknown rules are in effect";
             static bool fWarned = false;
             if (!fWarned) {
-                AlertNotify(strMiscWarning);
+                AlertNotify(strWarning);
                 fWarned = true;
             }
         }
     }
+    bcp::SetMiscWarning(strWarning);
     LogPrintf("UpdateTip: new best=%s height=%d version=0x%08x log2_work=%.8g tx=%lu date='%lld' cache=%.1fMiB(%utxo)\n",
               chainActive.Tip()->GetBlockHash().ToString().c_str(), chainActive.Height(), chainActive.Tip()->nVersion,
               std::log(chainActive.Tip()->nChainWork.getdouble()) / std::log(2.0),
@@ -1070,6 +1072,57 @@ void Chainstate::InvalidChainFound(CBlockIndex* pindexNew) {
     if (!pindexBestInvalid || pindexNew->nChainWork > pindexBestInvalid->nChainWork) pindexBestInvalid = pindexNew;
     LogPrintf("InvalidChainFound: invalid block=%s height=%d\n", pindexNew->GetBlockHash().ToString().c_str(),
               pindexNew->nHeight);
+    CheckForkWarningConditions();
+}
+
+// Large-fork / invalid-chain warnings (reference validation.cpp:1203-1297): a competing branch
+// that forked within the last 72 blocks and carries 7+ blocks' worth of work past the fork
+// point, or an invalid chain 6+ blocks' worth ahead of our tip, raises a warning (which also
+// turns on RPC safe mode) and fires -alertnotify once.
+void Chainstate::CheckForkWarningConditions() {
+    const CBlockIndex* tip = chainActive.Tip();
+    if (!tip || IsInitialBlockDownload()) return;
+    if (pindexBestForkTip && chainActive.Height() - pindexBestForkTip->nHeight >= 72) pindexBestForkTip = nullptr;
+    if (pindexBestForkTip ||
+        (pindexBestInvalid && pindexBestInvalid->nChainWork > tip->nChainWork + GetBlockProof(*tip) * 6)) {
+        if (!bcp::GetLargeWorkForkFound() && pindexBestForkBase) {
+            AlertNotify("Warning: Large-work fork detected, forking after block " +
+                        pindexBestForkBase->phashBlock->ToString());
+        }
+        if (pindexBestForkTip && pindexBestForkBase) {
+            LogPrintf("CheckForkWarningConditions: Warning: Large valid fork found\n  forking the chain at height %d "
+                      "(%s)\n  lasting to height %d (%s).\n",
+                      pindexBestForkBase->nHeight, pindexBestForkBase->phashBlock->ToString().c_str(),
+                      pindexBestForkTip->nHeight, pindexBestForkTip->phashBlock->ToString().c_str());
+            bcp::SetLargeWorkForkFound(true);
+        } else {
+            LogPrintf("CheckForkWarningConditions: Warning: Found invalid chain at least ~6 blocks longer than our "
+                      "best chain.\n");
+            bcp::SetLargeWorkInvalidChainFound(true);
+        }
+    } else {
+        bcp::SetLargeWorkForkFound(false);
+        bcp::SetLargeWorkInvalidChainFound(false);
+    }
+}
+
+std::string Chainstate::Warnings() const { return bcp::GetWarnings("statusbar"); }
+
+void Chainstate::CheckForkWarningConditionsOnNewFork(CBlockIndex* pindexNewForkTip) {
+    CBlockIndex* pfork = pindexNewForkTip;
+    CBlockIndex* plonger = chainActive.Tip();
+    while (pfork && pfork != plonger) {
+        while (plonger && plonger->nHeight > pfork->nHeight) plonger = plonger->pprev;
+        if (pfork == plonger) break;
+        pfork = pfork->pprev;
+    }
+    if (pfork && (!pindexBestForkTip || pindexNewForkTip->nHeight > pindexBestForkTip->nHeight) &&
+        pindexNewForkTip->nChainWork - pfork->nChainWork > GetBlockProof(*pfork) * 7 &&
+        chainActive.Height() - pindexNewForkTip->nHeight < 72) {
+        pindexBestForkTip = pindexNewForkTip;
+        pindexBestForkBase = pfork;
+    }
+    CheckForkWarningConditions();
 }
 
 void Chainstate::InvalidBlockFound(CBlockIndex* pindex, const CValidationState& state) {
@@ -1110,6 +1163,7 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
                             trace)) {
                 if (state.IsInvalid()) {
                     if (!state.CorruptionPossible()) InvalidChainFound(vpindexToConnect.front());
+                    CheckForkWarningConditionsOnNewFork(vpindexToConnect.back());
                     state = CValidationState();
                     fInvalidFound = true;
                     fContinue = false;

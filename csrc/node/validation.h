@@ -183,7 +183,7 @@ public:
     WorkerPool& Pool() { return *pool; }
     bool UseGpu() const { return opts.useGpu; }
     void SetUseGpu(bool v) { opts.useGpu = v; }
-    const std::string& Warnings() const { return strMiscWarning; }
+    std::string Warnings() const; // bcp::GetWarnings("statusbar")
     // block-change notification for RPC long-poll / waitfornewblock
     void WaitForBlockChange(int64_t timeoutMillis, const uint256& from);
     std::condition_variable_any& BlockChangeCV() { return cvBlockChange; }
@@ -249,6 +249,8 @@ private:
     CChain chainActive;
     CBlockIndex* pindexBestHeader = nullptr;
     CBlockIndex* pindexBestInvalid = nullptr;
+    void CheckForkWarningConditions();
+    void CheckForkWarningConditionsOnNewFork(CBlockIndex* pindexNewForkTip);
     CBlockIndex* pindexBestForkTip = nullptr;
     CBlockIndex* pindexBestForkBase = nullptr;
     std::set<CBlockIndex*, WorkComparator> setBlockIndexCandidates;
@@ -266,7 +268,6 @@ private:
     mutable std::atomic<bool> latchToFalse{false};
     int64_t nLastWrite = 0, nLastFlush = 0, nLastSetChain = 0;
     std::atomic<int64_t> nLastConnectMicros{0};
-    std::string strMiscWarning;
 
     std::unique_ptr<CBlockTreeDB> pblocktree;
     std::unique_ptr<CCoinsViewDB> pcoinsdbview;

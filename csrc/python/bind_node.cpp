@@ -5,6 +5,9 @@
 #include "python/bind.h"
 #include "rpc/server.h"
 #include "util/cuckoocache.h"
+#include "util/indirectmap.h"
+#include "util/limitedmap.h"
+#include "util/memusage.h"
 #include "util/util.h"
 
 #include <deque>
@@ -201,6 +204,44 @@ void bind_node(pyb::module_& m) {
     });
     m.def("ui_init_message", [](const std::string& s) { uiInterface.InitMessage(s); });
     m.def("ui_init_error", [](const std::string& s) { return InitError(s); });
+    // container utilities (reference limitedmap.h / indirectmap.h / memusage.h), exposed for tests
+    using LMap = limitedmap<int64_t, int64_t>;
+    pyb::class_<LMap>(m, "LimitedMap")
+        .def(pyb::init<size_t>())
+        .def("insert", [](LMap& l, int64_t k, int64_t v) { l.insert({k, v}); })
+        .def("erase", [](LMap& l, int64_t k) { l.erase(k); })
+        .def("update", [](LMap& l, int64_t k, int64_t v) {
+            auto it = l.find(k);
+            if (it == l.end()) throw pyb::key_error("no such key");
+            l.update(it, v);
+        })
+        .def("get", [](const LMap& l, int64_t k) -> pyb::object {
+            auto it = l.find(k);
+            return it == l.end() ? pyb::object(pyb::none()) : pyb::object(pyb::int_(it->second));
+        })
+        .def("set_max_size", [](LMap& l, size_t n) { return l.max_size(n); })
+        .def("__len__", &LMap::size)
+        .def("keys", [](const LMap& l) {
+            std::vector<int64_t> k;
+            for (const auto& kv : l) k.push_back(kv.first);
+            return k;
+        });
+    m.def("indirectmap_probe", [](const std::vector<int64_t>& values) {
+        // keys live in `values`; the map orders and finds them by value, not by address
+        indirectmap<int64_t, size_t> im;
+        for (size_t i = 0; i < values.size(); ++i) im.insert(std::make_pair(&values[i], i));
+        std::vector<int64_t> order;
+        for (const auto& kv : im) order.push_back(*kv.first);
+        const int64_t probe = values.empty() ? 0 : values[0];
+        auto it = im.find(probe);
+        return pyb::make_tuple(order, it == im.end() ? -1 : (int64_t)it->second, (int64_t)im.count(probe));
+    });
+    m.def("malloc_usage", &memusage::MallocUsage);
+    m.def("memusage_vector_u8", [](size_t cap) {
+        std::vector<unsigned char> v;
+        v.reserve(cap);
+        return memusage::DynamicUsage(v);
+    });
     m.def("cuckoo_hit_rate", &CuckooHitRate, pyb::arg("megabytes"), pyb::arg("load"));
     m.def("cuckoo_erase", &CuckooErase, pyb::arg("megabytes"));
     m.def("cuckoo_generations", &CuckooGenerations, pyb::arg("megabytes") = 32, pyb::arg("load") = 10.0);

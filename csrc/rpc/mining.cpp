@@ -352,7 +352,11 @@ static UniValue estimatefee(const JSONRPCRequest& req) {
     if (feeRate == CFeeRate(0)) return -1.0;
     return ValueFromAmount(feeRate.GetFeePerK());
 }
-static UniValue estimatepriority(const JSONRPCRequest& req) { return -1.0; }
+static UniValue estimatepriority(const JSONRPCRequest& req) {
+    int nBlocks = req.params[0].get_int();
+    if (nBlocks < 1) nBlocks = 1;
+    return Node().mempool->Estimator()->estimatePriority(nBlocks);
+}
 static UniValue estimatesmartfee(const JSONRPCRequest& req) {
     const int nBlocks = req.params[0].get_int();
     UniValue result(UniValue::VOBJ);
@@ -364,8 +368,10 @@ static UniValue estimatesmartfee(const JSONRPCRequest& req) {
 }
 static UniValue estimatesmartpriority(const JSONRPCRequest& req) {
     UniValue result(UniValue::VOBJ);
-    result.pushKV("priority", -1.0);
-    result.pushKV("blocks", req.params[0].get_int());
+    int answerFound = 0;
+    const double priority = Node().mempool->Estimator()->estimateSmartPriority(req.params[0].get_int(), &answerFound);
+    result.pushKV("priority", priority);
+    result.pushKV("blocks", answerFound);
     return result;
 }
 

@@ -1,4 +1,5 @@
 #include "rpc/server.h"
+#include "node/warnings.h"
 #include "keys/key.h"
 #include "util/strencodings.h"
 #include "util/util.h"
@@ -126,6 +127,7 @@ UniValue CRPCTable::execute(const JSONRPCRequest& request) const {
         ThrowRPC(RPC_IN_WARMUP, status);
     const CRPCCommand* pcmd = (*this)[request.strMethod];
     if (!pcmd) ThrowRPC(RPC_METHOD_NOT_FOUND, "Method not found");
+    if (!pcmd->okSafeMode) bcp::ObserveSafeMode();
     try {
         if (request.params.isObject()) return pcmd->actor(transformNamedArguments(request, pcmd->argNames));
         return pcmd->actor(request);

@@ -6,6 +6,7 @@
 // CCheckQueueSpeed, CoinSelection, RIPEMD160, SHA1, SHA256, SHA512, SHA256_32b,
 // SipHash_32b, FastRandom_32bit/1bit, LockedPool, MempoolEviction, RollingBloom) plus
 // MI355X batches (SHA256d64 batch, Merkle root, ECDSA batch verify) when a GPU is visible.
+#include <unistd.h>
 #include "consensus/merkle.h"
 #include "consensus/merkleblock.h"
 #include "consensus/params.h"
@@ -371,6 +372,15 @@ int main(int argc, char* argv[]) {
     if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help")) {
         printf("Usage: bench_bcp [-filter=<regex>] [-time=<seconds per bench>] [-list] [-datadir=bench/data]\n");
         return 0;
+    }
+    { // default: <dir of the binary>/../bench/data, so the working directory does not matter
+        char exe[4096];
+        const ssize_t len = readlink("/proc/self/exe", exe, sizeof(exe) - 1);
+        if (len > 0) {
+            std::string p(exe, (size_t)len);
+            p = p.substr(0, p.find_last_of('/'));
+            g_dataDir = p + "/../bench/data";
+        }
     }
     g_dataDir = gArgs.GetArg("-datadir", g_dataDir);
     const std::regex filter(gArgs.GetArg("-filter", ".*"));

@@ -149,3 +149,45 @@ def test_rpc_warmup_and_stop_via_cli(tmp_path):
     assert n.proc.returncode == 0
     with pytest.raises((ConnectionError, OSError, RPCError)):
         n.rpc.getblockcount()
+
+
+def test_safe_mode(tmp_path):
+    """-testsafemode raises a warning: commands not marked okSafeMode fail with
+    RPC_FORBIDDEN_BY_SAFE_MODE (-2); -disablesafemode overrides (reference warnings.cpp,
+    rpc/server.cpp ObserveSafeMode)."""
+    n = BcpdProcess(str(tmp_path / "sm"), extra_args=["-gpu=0", "-testsafemode"])
+    n.start()
+    try:
+        assert "testsafemode" in n.rpc.getinfo()["errors"]
+        assert "testsafemode" in n.rpc.getblockchaininfo()["warnings"]
+        n.rpc.getblockcount()  # okSafeMode
+        with pytest.raises(RPCError) as e:
+            n.rpc.sendrawtransaction("00")
+        assert e.value.code == -2 and "Safe mode" in str(e.value)
+    finally:
+        n.stop()
+    n = BcpdProcess(str(tmp_path / "sm2"), extra_args=["-gpu=0", "-testsafemode", "-disablesafemode"])
+    n.start()
+    try:
+        with pytest.raises(RPCError) as e:
+            n.rpc.sendrawtransaction("00")
+        assert e.value.code != -2
+    finally:
+        n.stop()
+
+
+def test_fee_estimates_persist(tmp_path):
+    """fee_estimates.dat is written at shutdown and read back at startup (reference
+    CBlockPolicyEstimator::Write/Read); estimatepriority/estimatesmartpriority answer."""
+    n = BcpdProcess(str(tmp_path / "fe"), extra_args=["-gpu=0"])
+    n.start()
+    n.rpc.generate(3)
+    assert n.rpc.estimatepriority(2) == -1
+    sp = n.rpc.estimatesmartpriority(2)
+    assert sp["priority"] == -1 and sp["blocks"] >= 2
+    n.stop()
+    found = [os.path.join(d, f) for d, _, fs in os.walk(str(tmp_path / "fe")) for f in fs if f == "fee_estimates.dat"]
+    assert found and os.path.getsize(found[0]) > 100
+    n.start()
+    assert n.rpc.estimatefee(2) == -1
+    n.stop()
