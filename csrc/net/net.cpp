@@ -1,4 +1,5 @@
 #include "net/net.h"
+#include "net/netbase.h"
 #include "node/ui_interface.h"
 #include "consensus/params.h"
 #include "consensus/tx_verify.h"
@@ -507,42 +508,47 @@ CNode* CConnman::ConnectNode(CAddress addrConnect, const char* pszDest) {
     }
     LogPrint(BCLog::NET, "trying connection %s lastseen=%.1fhrs\n", pszDest ? pszDest : addrConnect.ToString().c_str(),
              pszDest ? 0.0 : (double)(GetAdjustedTime() - addrConnect.nTime) / 3600.0);
-    if (pszDest) {
-        std::vector<CService> resolved;
-        if (Lookup(pszDest, resolved, Params().GetDefaultPort(), true, 256) && !resolved.empty()) {
-            addrConnect = CAddress(resolved[GetRand(resolved.size())], NODE_NONE);
-            if (!addrConnect.IsValid()) return nullptr;
-            std::lock_guard<CCriticalSection> l(cs_vNodes);
-            if (FindNode((CService)addrConnect)) {
-                LogPrintf("Failed to open new connection, already connected\n");
+    const int timeoutMs = (int)gArgs.GetArg("-timeout", (int64_t)5000);
+    int fd = -1;
+    bool proxyConnectionFailed = false;
+    proxyType nameProxy;
+    if (pszDest && GetNameProxy(nameProxy)) {
+        // -proxy set: hand the name to the proxy, never resolve it locally
+        int port = Params().GetDefaultPort();
+        std::string host;
+        SplitHostPort(pszDest, port, host);
+        fd = ConnectThroughProxy(nameProxy, host, (uint16_t)port, timeoutMs, &proxyConnectionFailed);
+        if (fd >= 0) {
+            CService svc = LookupNumeric(host, port);
+            if (!svc.IsValid()) svc = nameProxy.proxy; // the peer's address stays unknown to us
+            addrConnect = CAddress(svc, NODE_NONE);
+        }
+    } else {
+        if (pszDest) {
+            std::vector<CService> resolved;
+            if (Lookup(pszDest, resolved, Params().GetDefaultPort(), true, 256) && !resolved.empty()) {
+                addrConnect = CAddress(resolved[GetRand(resolved.size())], NODE_NONE);
+                if (!addrConnect.IsValid()) return nullptr;
+                std::lock_guard<CCriticalSection> l(cs_vNodes);
+                if (FindNode((CService)addrConnect)) {
+                    LogPrintf("Failed to open new connection, already connected\n");
+                    return nullptr;
+                }
+            } else {
                 return nullptr;
             }
-        } else {
-            return nullptr;
         }
+        if (!IsReachable(addrConnect)) return nullptr; // -onlynet excludes this network
+        proxyType proxy;
+        if (GetProxy(addrConnect.GetNetwork(), proxy))
+            fd = ConnectThroughProxy(proxy, addrConnect.ToStringIP(), addrConnect.GetPort(), timeoutMs,
+                                     &proxyConnectionFailed);
+        else if (!addrConnect.IsTor()) // onion peers are only reachable through a proxy
+            fd = ConnectDirectly(addrConnect, timeoutMs);
     }
-    struct sockaddr_storage ss;
-    socklen_t len = sizeof(ss);
-    if (!addrConnect.GetSockAddr((struct sockaddr*)&ss, &len)) return nullptr;
-    const int fd = socket(((struct sockaddr*)&ss)->sa_family, SOCK_STREAM, IPPROTO_TCP);
-    if (fd < 0) return nullptr;
-    int one = 1;
-    setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-    SetNonBlocking(fd);
-    int rc = connect(fd, (struct sockaddr*)&ss, len);
-    if (rc != 0 && errno == EINPROGRESS) {
-        struct pollfd pfd = {fd, POLLOUT, 0};
-        rc = poll(&pfd, 1, (int)gArgs.GetArg("-timeout", (int64_t)5000));
-        int soerr = 0;
-        socklen_t sl = sizeof(soerr);
-        if (rc == 1 && getsockopt(fd, SOL_SOCKET, SO_ERROR, &soerr, &sl) == 0 && soerr == 0)
-            rc = 0;
-        else
-            rc = -1;
-    }
-    if (rc != 0) {
-        close(fd);
-        addrman.Attempt(addrConnect, true);
+    if (fd < 0) {
+        // a dead proxy says nothing about the peer: do not count it as a failed attempt
+        if (!proxyConnectionFailed && !pszDest) addrman.Attempt(addrConnect, true);
         return nullptr;
     }
     addrman.Attempt(addrConnect, false);
@@ -1021,6 +1027,7 @@ void CConnman::ThreadOpenConnections() {
         for (int nTries = 0; !interruptNet && nTries < 100; nTries++) {
             CAddrInfo a = addrman.Select(fFeeler);
             if (!a.IsValid() || setConnected.count(a.GetGroup()) || IsLocalAddr(a)) break;
+            if (IsLimited(a.GetNetwork())) continue; // -onlynet / no proxy for this network
             if ((a.nServices & nRelevantServices) != nRelevantServices) continue;
             if (nANow - a.nLastTry < 600 && nTries < 30) continue;
             if (a.GetPort() != Params().GetDefaultPort() && nTries < 50) continue;

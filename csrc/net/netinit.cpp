@@ -3,6 +3,7 @@
 // -maxconnections/-maxuploadtarget/-peerbloomfilters handling and CConnman::Start).
 #include "net/net.h"
 #include "net/net_processing.h"
+#include "net/netbase.h"
 #include "node/node.h"
 #include "node/txmempool.h"
 #include "node/validation.h"
@@ -45,13 +46,69 @@ std::string NetHelp() {
         {"-listenonion", "Automatically create Tor hidden service (default: 1)"},
         {"-torcontrol=<ip>:<port>", "Tor control port to use if onion listening enabled (default: 127.0.0.1:9051)"},
         {"-torpassword=<pass>", "Tor control port password (default: empty)"},
+        {"-proxy=<ip:port>", "Connect through SOCKS5 proxy"},
+        {"-onion=<ip:port>", "Use separate SOCKS5 proxy to reach peers via Tor hidden services (default: -proxy)"},
+        {"-proxyrandomize", "Randomize credentials for every proxy connection. This enables Tor stream isolation (default: 1)"},
+        {"-onlynet=<net>", "Only connect to nodes in network <net> (ipv4, ipv6 or onion)"},
     };
     for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);
     return s;
 }
 
+// -onlynet / -proxy / -onion (reference init.cpp AppInitMain step 6)
+static bool SetupProxies(std::string& err) {
+    ClearProxies();
+    const std::vector<std::string> onlynets = gArgs.GetArgs("-onlynet");
+    if (!onlynets.empty()) {
+        bool allow[NET_MAX] = {};
+        for (const std::string& n : onlynets) {
+            const Network net = ParseNetwork(n);
+            if (net == NET_UNROUTABLE) {
+                err = "Unknown network specified in -onlynet: '" + n + "'";
+                return false;
+            }
+            allow[net] = true;
+        }
+        for (int n = NET_IPV4; n < NET_MAX; ++n) SetLimited((Network)n, !allow[n]);
+    }
+    const bool randomize = gArgs.GetBoolArg("-proxyrandomize", true);
+    const std::string proxyArg = gArgs.GetArg("-proxy", "");
+    if (!proxyArg.empty() && proxyArg != "0") {
+        CService svc = LookupNumeric(proxyArg, 9050);
+        if (!svc.IsValid()) {
+            err = "Invalid -proxy address: '" + proxyArg + "'";
+            return false;
+        }
+        proxyType p;
+        p.proxy = svc;
+        p.randomize_credentials = randomize;
+        SetProxy(NET_IPV4, p);
+        SetProxy(NET_IPV6, p);
+        SetProxy(NET_TOR, p);
+        SetNameProxy(p);
+    }
+    const std::string onionArg = gArgs.GetArg("-onion", "");
+    if (onionArg == "0") {
+        SetLimited(NET_TOR); // -onion=0: no onion peers at all
+    } else if (!onionArg.empty()) {
+        CService svc = LookupNumeric(onionArg, 9050);
+        if (!svc.IsValid()) {
+            err = "Invalid -onion address: '" + onionArg + "'";
+            return false;
+        }
+        proxyType p;
+        p.proxy = svc;
+        p.randomize_credentials = randomize;
+        SetProxy(NET_TOR, p); // reachability of onion peers stays as -onlynet decided
+    } else if (proxyArg.empty() || proxyArg == "0") {
+        SetLimited(NET_TOR); // no proxy that could reach .onion
+    }
+    return true;
+}
+
 bool StartNetwork(NodeContext& node, std::string& err) {
     const CChainParams& params = *node.params;
+    if (!SetupProxies(err)) return false;
     CConnman::Options o;
     std::vector<std::string> connect = gArgs.GetArgs("-connect");
     const bool connectDisabled = connect.size() == 1 && connect[0] == "0";

@@ -7,6 +7,7 @@
 #include "node/node.h"
 #include "node/policy.h"
 #include "rpc/server.h"
+#include "net/netbase.h"
 #include "util/strencodings.h"
 
 namespace bcp {
@@ -169,13 +170,15 @@ static UniValue getnetworkinfo(const JSONRPCRequest& req) {
         obj.pushKV("connections", (int64_t)c->GetNodeCount(CONNECTIONS_ALL));
     }
     UniValue nets(UniValue::VARR);
-    for (const char* n : {"ipv4", "ipv6", "onion"}) {
+    for (Network net : {NET_IPV4, NET_IPV6, NET_TOR}) {
         UniValue o(UniValue::VOBJ);
-        o.pushKV("name", n);
-        o.pushKV("limited", false);
-        o.pushKV("reachable", std::string(n) != "onion");
-        o.pushKV("proxy", "");
-        o.pushKV("proxy_randomize_credentials", false);
+        proxyType proxy;
+        const bool haveProxy = GetProxy(net, proxy);
+        o.pushKV("name", GetNetworkName(net));
+        o.pushKV("limited", IsLimited(net));
+        o.pushKV("reachable", IsReachable(net));
+        o.pushKV("proxy", haveProxy ? proxy.proxy.ToStringIPPort() : std::string());
+        o.pushKV("proxy_randomize_credentials", haveProxy && proxy.randomize_credentials);
         nets.push_back(o);
     }
     obj.pushKV("networks", nets);
