@@ -63,8 +63,14 @@ def test_seeder_crawls_and_answers(tmp_path):
         assert soa and soa[0][0] == 6
         rc, _ = dns_query(dns_port, "other.example", 1)
         assert rc == 5  # REFUSED
-        time.sleep(1.5)
-        text = open(dump).read()
+        text = ""
+        deadline = time.time() + 20  # the dumper writes every -dumpinterval seconds
+        while time.time() < deadline:
+            if os.path.exists(dump):
+                text = open(dump).read()
+                if f"127.0.0.1:{node.p2p_port}" in text:
+                    break
+            time.sleep(0.3)
         assert f"127.0.0.1:{node.p2p_port}" in text and "/Bitcoin Cash Plus:" in text
     finally:
         p.terminate()
