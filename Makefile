@@ -77,6 +77,20 @@ $(CONSLIB): build/obj/consensuslib/bitcoinconsensus.o $(CORELIB)
 	@mkdir -p lib
 	$(CXX) -shared -o $@ $< $(CORELIB) $(LDLIBS)
 
+# Host-side sanitizer build of the fuzz harness (reference --enable-asan/--enable-ubsan):
+# every CPU source rebuilt with ASan+UBSan, the gfx950 kernel objects linked as they are
+# (GPU code is never sanitized here).  `make asan` -> bin/bcp-fuzz-asan
+ASAN_FLAGS := -fsanitize=address,undefined -fno-omit-frame-pointer -O1 -g
+ASAN_OBJS  := $(patsubst csrc/%.cpp,build/asan/%.o,$(CORE_SRCS) $(GPU_HOST) csrc/tools/bcp-fuzz.cpp)
+.PHONY: asan
+asan: bin/bcp-fuzz-asan
+build/asan/%.o: csrc/%.cpp
+	@mkdir -p $(dir $@)
+	$(CXX) $(filter-out -O2,$(CXXFLAGS)) $(ASAN_FLAGS) -MMD -MP -c $< -o $@
+bin/bcp-fuzz-asan: $(ASAN_OBJS) $(HIP_OBJS)
+	@mkdir -p bin
+	$(CXX) $(ASAN_FLAGS) -o $@ $^ $(LDLIBS)
+
 clean:
 	rm -rf build bin lib bitcoincashplus_amd/_bcpnative*.so
 

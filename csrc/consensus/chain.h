@@ -162,6 +162,9 @@ public:
         ::bcp::Unserialize(s, nSolution);
     }
     CBlockHeader GetHeader() const;
+    // hash of the stored header (reference CDiskBlockIndex::GetBlockHash, chain.h:441): a
+    // freshly read entry has no phashBlock yet
+    uint256 GetBlockHash() const { return GetHeader().GetHash(); }
 };
 
 class CChain {

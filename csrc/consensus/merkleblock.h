@@ -17,8 +17,8 @@ enum bloomflags { BLOOM_UPDATE_NONE = 0, BLOOM_UPDATE_ALL = 1, BLOOM_UPDATE_P2PU
 
 class CBloomFilter {
 public:
-    static const unsigned int MAX_BLOOM_FILTER_SIZE = 36000; // bytes
-    static const unsigned int MAX_HASH_FUNCS = 50;
+    static constexpr unsigned int MAX_BLOOM_FILTER_SIZE = 36000; // bytes
+    static constexpr unsigned int MAX_HASH_FUNCS = 50;
     CBloomFilter() : isFull(true), isEmpty(false), nHashFuncs(0), nTweak(0), nFlags(0) {}
     CBloomFilter(unsigned nElements, double nFPRate, unsigned nTweak, unsigned char nFlags);
     void insert(const std::vector<unsigned char>& vKey);

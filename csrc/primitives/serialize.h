@@ -303,7 +303,7 @@ public:
     void read(char* p, size_t n) {
         if (n == 0) return;
         if (nReadPos + n > vch.size()) throw ser_error("DataStream::read(): end of data");
-        memcpy(p, vch.data() + nReadPos, n);
+        if (n) memcpy(p, vch.data() + nReadPos, n);
         nReadPos += n;
         if (nReadPos == vch.size()) { nReadPos = 0; vch.clear(); }
     }
@@ -335,6 +335,7 @@ public:
     int GetVersion() const { return nVersion; }
     void read(char* dst, size_t k) {
         if (pos + k > n) throw ser_error("SpanReader::read(): end of data");
+        if (k == 0) return; // an empty vector's data() may be null: memcpy(null, ..., 0) is UB
         memcpy(dst, p + pos, k);
         pos += k;
     }
