@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "8")))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "32")))
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
     args = ap.parse_args()
 
@@ -50,7 +50,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    solver = native.EquihashGpuSolver(200, 9, args.batch, local_rank)
+    # two solvers, double-buffered: while the GPU runs batch s, the host decodes batch s-1
+    solvers = [native.EquihashGpuSolver(200, 9, args.batch, local_rank) for _ in range(2)]
+    solver = solvers[0]
     # Template: CEquihashInput of a mainnet-shaped header (108 B), random-ish but fixed.
     header = bytes((i * 37 + 11) & 0xFF for i in range(108))
 
@@ -65,20 +67,27 @@ def main():
         return sts
 
     for w in range(args.warmup):
-        solver.solve(states_for(1_000_000 + w))
-    solver.reset_stats()
+        solvers[w % 2].solve(states_for(1_000_000 + w))
+    for sv in solvers:
+        sv.reset_stats()
     all_states = [states_for(s) for s in range(args.steps)]
     sols_kept = []
 
     barrier()
     t0 = time.perf_counter()
     nsol = 0
-    for s in range(args.steps):
-        res = solver.solve(all_states[s])
-        for b, sols in enumerate(res):
-            nsol += len(sols)
-            if s < 2:
-                sols_kept.extend((all_states[s][b], x) for x in sols)
+    pending = None  # (step, solver) launched but not yet collected
+    for s in range(args.steps + 1):
+        if s < args.steps:
+            solvers[s % 2].launch(all_states[s])
+        if pending is not None:
+            ps, psolver = pending
+            res = psolver.collect()
+            for b, sols in enumerate(res):
+                nsol += len(sols)
+                if ps < 2:
+                    sols_kept.extend((all_states[ps][b], x) for x in sols)
+        pending = (s, solvers[s % 2]) if s < args.steps else None
     barrier()
     dt = time.perf_counter() - t0
 
@@ -99,7 +108,7 @@ def main():
         if not verified:
             raise SystemExit("bench: GPU verifier rejected solver output")
 
-    st = solver.stats()
+    st = solvers[0].stats()
     if rank == 0:
         value = total_sols / max_dt
         nonces = args.steps * args.batch * world

@@ -36,7 +36,24 @@ __device__ __constant__ static const uint8_t kB2Sigma[12][16] = {
     {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15},
     {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3}};
 
-__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 64-bit rotate right as two 32-bit funnel shifts (v_alignbit_b32): the generic shift/or form
+// compiles to two 64-bit shifts plus two ORs. n is a compile-time constant at every call site
+// (32 is a plain half swap).
+__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    uint32_t rlo, rhi;
+    if (n == 32) {
+        rlo = hi;
+        rhi = lo;
+    } else if (n < 32) {
+        rlo = __builtin_amdgcn_alignbit(hi, lo, n);
+        rhi = __builtin_amdgcn_alignbit(lo, hi, n);
+    } else {
+        rlo = __builtin_amdgcn_alignbit(lo, hi, n - 32);
+        rhi = __builtin_amdgcn_alignbit(hi, lo, n - 32);
+    }
+    return ((uint64_t)rhi << 32) | rlo;
+}
 
 #define BCPK_B2G(a, b, c, d, x, y)       \
     a = a + b + (x);                     \
