@@ -438,7 +438,8 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     uint32_t v[RPL][WI];
     uint32_t f[PRUNE ? RPL : 1], fd[PRUNE ? RPL : 1]; // parent refs + producing workgroup
     uint32_t so[RPL];                                  // slots of the next bucket's rows
-    int pf_nonce = 0;
+    int pf_nonce = 0, pf_d = 0;
+    uint32_t pf_n = 0;
     auto prefetch = [&](int bb, int p, uint32_t nn) {
         const int nonce = bb / C::NB, d = bb % C::NB;
         { // slot of every LDS row: 16 lanes per run, 4 runs per wave instruction
@@ -455,8 +456,6 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         }
         __syncthreads();
         EH_STAMP(8);
-        uint32_t* mrow = Mout + (size_t)nonce * C::ROWS + (size_t)d * C::AREA;
-        for (uint32_t r = tid; r < nn; r += NT) mrow[r] = gslot[r];
         // buffer loads: 32-bit lane offsets against a per-nonce descriptor keep the address
         // math out of the VGPRs that hold the prefetched rows across phase D
         const auto rsrc_rows = __builtin_amdgcn_make_buffer_rsrc(
@@ -470,6 +469,19 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             so[u] = (r < nn) ? gslot[r] : 0u; // clamped to a valid slot: loads are unconditional
         }
         pf_nonce = nonce;
+        pf_d = d;
+        pf_n = nn;
+    };
+    // Gather map of the prefetched bucket, from the slots held in registers: written late in
+    // phase D, where its stores do not compete with the prefetch loads for the CU's queue.
+    auto write_map = [&]() {
+        uint32_t* mrow = Mout + (size_t)pf_nonce * C::ROWS + (size_t)pf_d * C::AREA;
+        const uint32_t ot = opaque_tid();
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+            const uint32_t r = ot + u * NT;
+            if (r < pf_n) mrow[r] = so[u];
+        }
     };
     // Issue the prefetch loads of rows [U0, U1) of every lane. The loads of one bucket are
     // issued in slices spread over phase D: a wave that issues the whole bucket at once stalls
@@ -498,6 +510,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     rt_fetch(bk + G);
     prefetch(bk, 0, n);
     issue(0, RPL);
+    write_map();
     __syncthreads();
 
     for (;;) {
@@ -605,10 +618,14 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                 if (k < Pc) {
                     const uint32_t p = pmark[k], q = p + 1 + (k - offp[p]);
                     const uint32_t i = sidx[p], j = sidx[q];
-                    uint32_t any = 0;
+                    const uint32_t x0 = rows[i * WI] ^ rows[j * WI];
+                    // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the
+                    // pairs, so the remaining words are read only when it matches
+                    bool keep = x0 != 0;
+                    if (!keep) {
 #pragma unroll
-                    for (int w = 0; w < WI; ++w) any |= rows[i * WI + w] ^ rows[j * WI + w];
-                    bool keep = any != 0; // drop pairs of identical subtrees
+                        for (int w = 1; w < WI; ++w) keep |= rows[i * WI + w] != rows[j * WI + w];
+                    }
                     if constexpr (PRUNE) {
                         const uint32_t si = psig[i], sj = psig[j];
                         if (keep && ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) ||
@@ -620,7 +637,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                     }
                     if (keep) {
                         pv[u] = (j << 16) | i;
-                        pd[u] = ((rows[i * WI] ^ rows[j * WI]) >> (32 - C::DB)) & (C::NB - 1); // destination
+                        pd[u] = (x0 >> (32 - C::DB)) & (C::NB - 1); // destination bucket
                         atomicAdd(&hist[pd[u]], 1u);
                     }
                 }
@@ -668,6 +685,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         if constexpr (FINAL) {
             if (more) issue(4, RPL);
         }
+        if (more) write_map();
         __syncthreads();
         EH_STAMP(6);
         if (bn >= nbk) break;
