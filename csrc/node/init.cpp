@@ -1,4 +1,6 @@
 #include "node/init.h"
+
+#include <thread>
 #include "node/ui_interface.h"
 #include "consensus/params.h"
 #include "kernels/gpu_api.h"
@@ -49,6 +51,7 @@ std::string HelpMessage() {
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
         {"-blocknotify=<cmd>", "Execute command when the best block changes (%s in cmd is replaced by block hash)"},
+        {"-loadblock=<file>", "Imports blocks from external blk000??.dat file on startup"},
         {"-disablesafemode", "Disable safemode, override a real safe mode event (default: 0)"},
         {"-testsafemode", "Force safe mode (default: 0)"},
         {"-alertnotify=<cmd>", "Execute command when a relevant alert is received or we see a really long fork (%s in cmd is replaced by message)"},
@@ -306,6 +309,43 @@ int AppMain(int argc, char* argv[]) {
         uiInterface.InitMessage("Loading mempool...");
         node->chainstate->LoadMempool(datadir + "/mempool.dat");
     }
+    // Block import (reference init.cpp ThreadImport :974-1046): <datadir>/bootstrap.dat (then
+    // renamed to bootstrap.dat.old) and every -loadblock=<file>, on a background thread so RPC
+    // and the network come up meanwhile; blocks are accepted, stored and connected as usual.
+    std::vector<std::pair<std::string, bool>> importFiles; // (path, is <datadir>/bootstrap.dat)
+    {
+        const std::string boot = datadir + "/bootstrap.dat";
+        FILE* f = fopen(boot.c_str(), "rb");
+        if (f) {
+            fclose(f);
+            importFiles.emplace_back(boot, true);
+        }
+    }
+    for (const std::string& f : gArgs.GetArgs("-loadblock")) importFiles.emplace_back(f, false);
+    std::thread importThread;
+    if (!importFiles.empty()) {
+        importThread = std::thread([files = importFiles, cs = node->chainstate.get()] {
+            RenameThread("bcp-loadblk");
+            for (const auto& item : files) {
+                const std::string& path = item.first;
+                FILE* f = fopen(path.c_str(), "rb");
+                if (!f) {
+                    LogPrintf("Warning: Could not open blocks file %s\n", path.c_str());
+                    continue;
+                }
+                LogPrintf("Importing blocks file %s...\n", path.c_str());
+                cs->LoadExternalBlockFile(f); // closes nothing: we own f
+                fclose(f);
+                if (item.second) {
+                    const std::string old = path + ".old";
+                    if (rename(path.c_str(), old.c_str()) == 0) LogPrintf("Renamed %s to %s\n", path.c_str(), old.c_str());
+                }
+            }
+            CValidationState state;
+            cs->ActivateBestChain(state);
+            LogPrintf("Block import finished\n");
+        });
+    }
     uiInterface.InitMessage("Loading wallet...");
     if (!StartWallet(*node, err)) {
         InitError(err);
@@ -344,6 +384,7 @@ int AppMain(int argc, char* argv[]) {
 
     // ---- shutdown (reference init.cpp Shutdown(): RPC, network, wallet, mempool dump, flush)
     LogPrintf("Shutdown: In progress...\n");
+    if (importThread.joinable()) importThread.join();
     uiInterface.NotifyBlockTip.disconnect_all();
     if (http) http->Stop();
     StopHTTPRPC(datadir);

@@ -77,3 +77,24 @@ def test_zmq_block_and_tx_notifications(tmp_path):
         assert msg[0] == b"hashtx" and msg[1].hex() == n.rpc.getblock(h)["tx"][0]
     finally:
         n.stop()
+
+
+def test_contrib_zmq_sub_client(tmp_path):
+    """contrib/zmq/zmq_sub.py (reference contrib/zmq/zmq_sub.py) subscribes and decodes."""
+    import importlib.util
+    import time
+    spec = importlib.util.spec_from_file_location(
+        "zmq_sub", os.path.join(os.path.dirname(BIN_DIR), "contrib", "zmq", "zmq_sub.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    port = free_port()
+    n = BcpdProcess(str(tmp_path / "z"), extra_args=["-gpu=0", f"-zmqpubhashblock=tcp://127.0.0.1:{port}"])
+    n.start()
+    try:
+        sub = mod.ZmtpSubscriber("127.0.0.1", port, [b"hashblock"], timeout=20)
+        time.sleep(0.3)
+        h = n.rpc.generate(1)[0]
+        line = mod.describe(sub.recv_multipart())
+        assert line == f"hashblock #0: {h}"
+    finally:
+        n.stop()
