@@ -229,6 +229,20 @@ int AppMain(int argc, char* argv[]) {
         InitError("Invalid fee amount argument");
         return 1;
     }
+    // excessive block size vs the legacy 1MB limit and the mining limit (reference init.cpp
+    // AppInitParameterInteraction :1413-1424, config.cpp SetMaxBlockSize)
+    {
+        const int64_t ebs = gArgs.GetArg("-excessiveblocksize", (int64_t)DEFAULT_MAX_BLOCK_SIZE);
+        if (ebs <= (int64_t)LEGACY_MAX_BLOCK_SIZE) {
+            InitError("Excessive block size must be > 1,000,000 bytes (1MB)");
+            return 1;
+        }
+        if (gArgs.GetArg("-blockmaxsize", (int64_t)DEFAULT_MAX_GENERATED_BLOCK_SIZE) > ebs) {
+            InitError("Max generated block size (blockmaxsize) cannot exceed the excessive block size "
+                      "(excessiveblocksize)");
+            return 1;
+        }
+    }
     SetGpuSigThreshold((size_t)gArgs.GetArg("-gpusigthreshold", (int64_t)GetGpuSigThreshold()));
     InitSignatureCache(gArgs.GetArg("-maxsigcachesize", (int64_t)DEFAULT_MAX_SIG_CACHE_SIZE));
     InitScriptExecutionCache(gArgs.GetArg("-maxscriptcachesize", (int64_t)DEFAULT_MAX_SCRIPT_CACHE_SIZE));
