@@ -952,7 +952,7 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         }
         LogPrintf("receive version message: %s: version %d, blocks=%d, us=%s, peer=%d%s\n", cleanSubVer.c_str(),
                   pfrom->nVersion.load(), pfrom->nStartingHeight.load(), addrMe.ToString().c_str(), (int)pfrom->GetId(),
-                  pfrom->fInbound ? "" : (", peeraddr=" + pfrom->addr.ToString()).c_str());
+                  fLogIPs ? (", peeraddr=" + pfrom->addr.ToString()).c_str() : "");
         const int64_t nTimeOffset = nTime - GetTime();
         pfrom->nTimeOffset = nTimeOffset;
         AddTimeData(pfrom->addr.ToStringIP(), nTimeOffset);

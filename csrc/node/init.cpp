@@ -3,6 +3,7 @@
 #include <thread>
 #include "node/ui_interface.h"
 #include "consensus/params.h"
+#include "consensus/versionbits.h"
 #include "kernels/gpu_api.h"
 #include "node/node.h"
 #include "node/policy.h"
@@ -51,6 +52,7 @@ std::string HelpMessage() {
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
         {"-blocknotify=<cmd>", "Execute command when the best block changes (%s in cmd is replaced by block hash)"},
+        {"-bip9params=<deployment>:<start>:<end>", "Use given start/end times for specified version bits deployment (regtest-only)"},
         {"-loadblock=<file>", "Imports blocks from external blk000??.dat file on startup"},
         {"-disablesafemode", "Disable safemode, override a real safe mode event (default: 0)"},
         {"-testsafemode", "Force safe mode (default: 0)"},
@@ -87,6 +89,9 @@ std::string HelpMessage() {
         {"-rpcservertimeout=<n>", "Timeout during HTTP requests (default: 30)"},
         {"-debug=<category>", "Output debugging information (net, mempool, http, bench, rpc, gpu, ...)"},
         {"-printtoconsole", "Send trace/debug info to console instead of debug.log file"},
+        {"-logtimestamps", "Prepend debug output with timestamp (default: 1)"},
+        {"-logtimemicros", "Add microsecond precision to debug timestamps (default: 0)"},
+        {"-logips", "Include IP addresses in debug output (default: 0)"},
         {"-shrinkdebugfile", "Shrink debug.log file on client startup (default: 1)"},
         {"-checkblockindex", "Do a full consistency check of the block index (regtest default)"},
         {"-checkmempool=<n>", "Run checks every <n> transactions"},
@@ -158,6 +163,36 @@ int AppMain(int argc, char* argv[]) {
         return 1;
     }
     SelectParams(chain);
+    // -bip9params=deployment:start:end, regtest only (reference chainparams.cpp:474
+    // UpdateRegtestBIP9Parameters + init.cpp parsing)
+    for (const std::string& p : gArgs.GetArgs("-bip9params")) {
+        if (chain != "regtest") {
+            fprintf(stderr, "Error: BIP9 parameters may only be overridden on regtest.\n");
+            return 1;
+        }
+        const size_t a = p.find(':'), b = a == std::string::npos ? a : p.find(':', a + 1);
+        int64_t nStart = 0, nTimeout = 0;
+        if (b == std::string::npos || !ParseInt64(p.substr(a + 1, b - a - 1), &nStart) ||
+            !ParseInt64(p.substr(b + 1), &nTimeout)) {
+            fprintf(stderr, "Error: Version bits parameters malformed, expecting deployment:start:end\n");
+            return 1;
+        }
+        const std::string name = p.substr(0, a);
+        bool found = false;
+        for (int j = 0; j < (int)Consensus::MAX_VERSION_BITS_DEPLOYMENTS; ++j) {
+            if (name == VersionBitsDeploymentInfo[j].name) {
+                Params(chain).UpdateVersionBitsParameters((Consensus::DeploymentPos)j, nStart, nTimeout);
+                found = true;
+                LogPrintf("Setting BIP9 activation parameters for %s to start=%lld, timeout=%lld\n", name.c_str(),
+                          (long long)nStart, (long long)nTimeout);
+                break;
+            }
+        }
+        if (!found) {
+            fprintf(stderr, "Error: Invalid deployment (%s)\n", name.c_str());
+            return 1;
+        }
+    }
     const std::string datadir = GetDataDir(true);
     TryCreateDirectories(datadir);
 
@@ -183,7 +218,9 @@ int AppMain(int argc, char* argv[]) {
         LogInit(datadir + "/debug.log", false);
         ShrinkDebugFile();
     }
-    LogInit(console ? "" : datadir + "/debug.log", console);
+    LogInit(console ? "" : datadir + "/debug.log", console, gArgs.GetBoolArg("-logtimestamps", true));
+    LogSetTimeMicros(gArgs.GetBoolArg("-logtimemicros", false));
+    fLogIPs = gArgs.GetBoolArg("-logips", false);
     for (const std::string& c : gArgs.GetArgs("-debug"))
         if (!LogEnableCategory(c)) LogPrintf("Unsupported logging category -debug=%s.\n", c.c_str());
     for (const std::string& c : gArgs.GetArgs("-debugexclude")) LogDisableCategory(c);

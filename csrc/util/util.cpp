@@ -72,6 +72,7 @@ struct LogState {
     std::string path;
     bool console = false;
     bool timestamps = true;
+    bool micros = false;
     bool startedNewLine = true;
     std::atomic<uint32_t> categories{0};
 };
@@ -111,6 +112,8 @@ std::string VFormat(const char* fmt, va_list ap) {
 }
 } // namespace
 
+bool fLogIPs = false;
+void LogSetTimeMicros(bool on) { L().micros = on; }
 void LogInit(const std::string& path, bool console, bool timestamps) {
     LogState& s = L();
     std::lock_guard<std::mutex> l(s.m);
@@ -158,7 +161,7 @@ void LogPrintStr(const std::string& str) {
         gmtime_r(&t, &tmv);
         char buf[64];
         strftime(buf, sizeof(buf), "%Y-%m-%d %H:%M:%S", &tmv);
-        out = strprintf("%s.%06d ", buf, (int)(us % 1000000));
+        out = s.micros ? strprintf("%s.%06d ", buf, (int)(us % 1000000)) : std::string(buf) + " ";
     }
     out += str;
     s.startedNewLine = !str.empty() && str.back() == '\n';

@@ -45,6 +45,8 @@ enum LogFlags : uint32_t {
 };
 }
 void LogInit(const std::string& debugLogPath, bool printToConsole, bool logTimestamps = true);
+void LogSetTimeMicros(bool on); // -logtimemicros: microsecond timestamps
+extern bool fLogIPs;            // -logips: include peer IP addresses in debug output
 void LogShutdown();
 bool LogEnableCategory(const std::string& name); // "net", "1"/"all"
 bool LogDisableCategory(const std::string& name);

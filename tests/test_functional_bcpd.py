@@ -191,3 +191,26 @@ def test_fee_estimates_persist(tmp_path):
     n.start()
     assert n.rpc.estimatefee(2) == -1
     n.stop()
+
+
+def test_bip9params_and_log_flags(tmp_path):
+    """-bip9params overrides a deployment's window on regtest (reference chainparams.cpp:474);
+    -logtimemicros/-logips are accepted; -bip9params is rejected off regtest."""
+    n = BcpdProcess(str(tmp_path / "b9"), extra_args=["-gpu=0", "-bip9params=csv:999999999999:999999999999",
+                                                        "-logtimemicros", "-logips"])
+    n.start()
+    try:
+        n.rpc.generate(300)  # two full 144-block periods
+        assert n.rpc.getblockchaininfo()["bip9_softforks"]["csv"]["status"] == "defined"
+    finally:
+        n.stop()
+    d = BcpdProcess(str(tmp_path / "b9x"), extra_args=["-gpu=0", "-bip9params=nosuchfork:0:1"])
+    with pytest.raises(RuntimeError):
+        d.start()
+    m = BcpdProcess(str(tmp_path / "b9y"), extra_args=["-gpu=0"])
+    m.start()
+    try:
+        m.rpc.generate(300)  # default regtest window: csv moves past "defined"
+        assert m.rpc.getblockchaininfo()["bip9_softforks"]["csv"]["status"] != "defined"
+    finally:
+        m.stop()
