@@ -16,6 +16,8 @@ namespace bcp {
 extern std::function<void(const uint256&)> g_relayTransaction;
 
 void StartTorControl(NodeContext& node, int listenPort);
+void StartMapPort(int port);
+void StopMapPort();
 void StopTorControl();
 
 static std::unique_ptr<CConnman> g_connman;
@@ -49,6 +51,7 @@ std::string NetHelp() {
         {"-proxy=<ip:port>", "Connect through SOCKS5 proxy"},
         {"-onion=<ip:port>", "Use separate SOCKS5 proxy to reach peers via Tor hidden services (default: -proxy)"},
         {"-proxyrandomize", "Randomize credentials for every proxy connection. This enables Tor stream isolation (default: 1)"},
+        {"-upnp", "Use UPnP to map the listening port (default: 0)"},
         {"-onlynet=<net>", "Only connect to nodes in network <net> (ipv4, ipv6 or onion)"},
     };
     for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);
@@ -184,6 +187,7 @@ bool StartNetwork(NodeContext& node, std::string& err) {
         return false;
     }
     StartTorControl(node, port);
+    if (gArgs.GetBoolArg("-upnp", false) && o.fListen) StartMapPort(port);
     LogPrintf("Network started: listen=%d port=%d services=%llx\n", (int)o.fListen, port,
               (unsigned long long)o.nLocalServices);
     return true;
@@ -191,6 +195,7 @@ bool StartNetwork(NodeContext& node, std::string& err) {
 
 void StopNetwork(NodeContext& node) {
     if (!g_connman) return;
+    StopMapPort();
     StopTorControl();
     g_relayTransaction = nullptr;
     g_connman->Interrupt();
