@@ -79,7 +79,8 @@ class FakeIGD:
 
 def test_upnp_maps_and_unmaps_port(tmp_path):
     igd = FakeIGD()
-    n = BcpdProcess(str(tmp_path / "u"), extra_args=["-gpu=0", "-upnp", f"-upnpdiscover=127.0.0.1:{igd.ssdp_port}"])
+    n = BcpdProcess(str(tmp_path / "u"), extra_args=["-gpu=0", "-upnp", "-discover=1",
+                                                       f"-upnpdiscover=127.0.0.1:{igd.ssdp_port}"])
     n.start()
     try:
         end = time.time() + 30
