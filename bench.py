@@ -41,9 +41,17 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     require_gpu("bench.py")
-    torch.cuda.set_device(local_rank)
+    # one rank per GPU over RCCL ("nccl"); BCP_DIST_BACKEND=gloo + ranks sharing a GPU is the
+    # rehearsal mode for the multi-rank path on a 1-GPU box (CPU-side reductions)
+    backend = os.environ.get("BCP_DIST_BACKEND", "nccl")
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group(backend)
+    red_dev = "cuda" if backend == "nccl" else "cpu"
 
     def barrier():
         if world > 1:
@@ -51,7 +59,7 @@ def main():
         torch.cuda.synchronize()
 
     # two solvers, double-buffered: while the GPU runs batch s, the host decodes batch s-1
-    solvers = [native.EquihashGpuSolver(200, 9, args.batch, local_rank) for _ in range(2)]
+    solvers = [native.EquihashGpuSolver(200, 9, args.batch, device) for _ in range(2)]
     solver = solvers[0]
     # Template: CEquihashInput of a mainnet-shaped header (108 B), random-ish but fixed.
     header = bytes((i * 37 + 11) & 0xFF for i in range(108))
@@ -91,7 +99,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
 
-    t = torch.tensor([float(nsol), dt], dtype=torch.float64, device="cuda")
+    t = torch.tensor([float(nsol), dt], dtype=torch.float64, device=red_dev)
     if world > 1:
         tot = t.clone()
         dist.all_reduce(tot[:1], op=dist.ReduceOp.SUM)
@@ -103,7 +111,7 @@ def main():
 
     verified = None
     if args.verify and sols_kept:
-        ok = native.eh_verify_batch_gpu(200, 9, [a for a, _ in sols_kept], [b for _, b in sols_kept], local_rank)
+        ok = native.eh_verify_batch_gpu(200, 9, [a for a, _ in sols_kept], [b for _, b in sols_kept], device)
         verified = bool(all(ok))
         if not verified:
             raise SystemExit("bench: GPU verifier rejected solver output")
