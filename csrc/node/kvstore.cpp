@@ -162,6 +162,83 @@ bool KVStore::Replay() {
     return true;
 }
 
+std::map<std::string, std::string> KVStore::Salvage(const std::string& dir, uint64_t* skipped) {
+    std::map<std::string, std::string> out;
+    if (skipped) *skipped = 0;
+    const std::string path = dir + "/kv.log";
+    const int f = ::open(path.c_str(), O_RDONLY);
+    if (f < 0) return out;
+    struct stat st;
+    if (fstat(f, &st) != 0) {
+        ::close(f);
+        return out;
+    }
+    std::vector<unsigned char> log((size_t)st.st_size);
+    const bool read_ok = log.empty() || PreadAll(f, log.data(), log.size(), 0);
+    ::close(f);
+    if (!read_ok) return out;
+    size_t off = 0;
+    while (off + 12 <= log.size()) {
+        uint32_t magic, len, crc;
+        memcpy(&magic, &log[off], 4);
+        memcpy(&len, &log[off + 4], 4);
+        memcpy(&crc, &log[off + 8], 4);
+        const bool framed = magic == BATCH_MAGIC && off + 12 + (uint64_t)len <= log.size() &&
+                            Crc32c(&log[off + 12], len) == crc;
+        std::vector<KVBatch::Op> ops;
+        bool ok = framed;
+        if (framed) {
+            const unsigned char* p = &log[off + 12];
+            const unsigned char* end = p + len;
+            while (ok && p < end) {
+                const uint8_t op = *p++;
+                uint64_t klen, vlen = 0;
+                if (!GetVar(p, end, klen) || (uint64_t)(end - p) < klen) {
+                    ok = false;
+                    break;
+                }
+                std::string key((const char*)p, klen);
+                p += klen;
+                if (op == OP_PUT) {
+                    if (!GetVar(p, end, vlen) || (uint64_t)(end - p) < vlen) {
+                        ok = false;
+                        break;
+                    }
+                    ops.push_back({true, std::move(key), std::string((const char*)p, vlen)});
+                    p += vlen;
+                } else if (op == OP_DEL) {
+                    ops.push_back({false, std::move(key), std::string()});
+                } else {
+                    ok = false;
+                }
+            }
+        }
+        if (ok) { // apply the whole batch in log order
+            for (auto& o : ops) {
+                if (o.put)
+                    out[o.key] = std::move(o.value);
+                else
+                    out.erase(o.key);
+            }
+            off += 12 + len;
+            continue;
+        }
+        // damaged: resynchronise on the next batch header
+        size_t next = off + 1;
+        while (next + 4 <= log.size()) {
+            uint32_t m;
+            memcpy(&m, &log[next], 4);
+            if (m == BATCH_MAGIC) break;
+            ++next;
+        }
+        if (next + 4 > log.size()) next = log.size();
+        if (skipped) *skipped += next - off;
+        off = next;
+    }
+    if (skipped && off < log.size()) *skipped += log.size() - off;
+    return out;
+}
+
 bool KVStore::WriteBatch(KVBatch& batch, bool fSync) {
     if (batch.ops.empty()) return true;
     std::lock_guard<std::mutex> l(cs);

@@ -132,6 +132,12 @@ public:
     std::unique_ptr<KVIterator> NewIterator() const { return std::unique_ptr<KVIterator>(new KVIterator(this)); }
     void Compact(); // rewrite the log with live records only
     uint64_t LogBytes() const { return logSize; }
+    // Salvage (reference CDBEnv::Salvage / CWalletDB::Recover): scan a store's log without
+    // trusting its structure — every batch whose header and CRC check out is replayed, damaged
+    // stretches are skipped by searching for the next batch header (instead of truncating the
+    // rest of the log as Replay does). Returns the latest value of every live key; `skipped`
+    // counts the damaged bytes.
+    static std::map<std::string, std::string> Salvage(const std::string& dir, uint64_t* skipped = nullptr);
 
 private:
     friend class KVIterator;

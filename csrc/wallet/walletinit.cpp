@@ -10,7 +10,9 @@
 #include "util/strencodings.h"
 #include "wallet/wallet.h"
 
+#include <cstdio>
 #include <functional>
+#include <sys/stat.h>
 
 namespace bcp {
 
@@ -29,6 +31,7 @@ std::string WalletHelp() {
         {"-mintxfee=<amt>", "Fees (in BCP/kB) smaller than this are considered zero fee for transaction creation (default: 0.00001)"},
         {"-paytxfee=<amt>", "Fee (in BCP/kB) to add to transactions you send (default: 0.00)"},
         {"-rescan", "Rescan the block chain for missing wallet transactions on startup"},
+        {"-salvagewallet", "Attempt to recover private keys from a corrupt wallet on startup"},
         {"-spendzeroconfchange", "Spend unconfirmed change when sending transactions (default: 1)"},
         {"-txconfirmtarget=<n>", "If paytxfee is not set, include enough fee so transactions begin confirmation within n blocks (default: 6)"},
         {"-usehd", "Use hierarchical deterministic key generation (HD) after BIP32. Only has effect during wallet creation/first start (default: 1)"},
@@ -41,9 +44,50 @@ std::string WalletHelp() {
     return s;
 }
 
+// -salvagewallet (reference CWalletDB::Recover): move the damaged store aside as
+// <name>.<time>.bak, recover every intact batch from its log, and keep only the key records
+// (private/encrypted keys, master keys, key metadata, HD chain); transactions come back
+// through the rescan that -salvagewallet implies.
+static bool SalvageWallet(const std::string& path, std::string& err) {
+    struct stat st;
+    if (stat(path.c_str(), &st) != 0) return true; // nothing to salvage
+    const std::string bak = strprintf("%s.%lld.bak", path.c_str(), (long long)GetTime());
+    if (rename(path.c_str(), bak.c_str()) != 0) {
+        err = "Failed to rename " + path + " to " + bak;
+        return false;
+    }
+    uint64_t skipped = 0;
+    const std::map<std::string, std::string> recs = KVStore::Salvage(bak, &skipped);
+    KVStore fresh(path, false, true);
+    KVBatch b;
+    size_t kept = 0;
+    for (const auto& kv : recs) {
+        std::string type;
+        try {
+            SpanReader r((const unsigned char*)kv.first.data(), kv.first.size(), SER_DISK, PROTOCOL_VERSION);
+            r >> type;
+        } catch (const std::exception&) {
+            continue;
+        }
+        if (type == "key" || type == "wkey" || type == "mkey" || type == "ckey" || type == "keymeta" ||
+            type == "hdchain") {
+            b.WriteRaw(kv.first, kv.second);
+            ++kept;
+        }
+    }
+    if (!fresh.WriteBatch(b, true)) {
+        err = "Salvage: writing the recovered wallet failed";
+        return false;
+    }
+    LogPrintf("Salvage(aggressive) found %u records, kept %u key records, skipped %u damaged bytes\n",
+              (unsigned)recs.size(), (unsigned)kept, (unsigned)skipped);
+    return true;
+}
+
 static bool LoadOneWallet(NodeContext& node, const std::string& name, std::string& err) {
     Chainstate& cs = *node.chainstate;
     const std::string path = node.datadir + "/" + name;
+    if (gArgs.GetBoolArg("-salvagewallet", false) && !SalvageWallet(path, err)) return false;
     std::unique_ptr<CWallet> w(new CWallet(name, path, false));
     bool firstRun = false;
     if (!w->Load(err, firstRun)) return false;
@@ -86,6 +130,7 @@ static bool LoadOneWallet(NodeContext& node, const std::string& name, std::strin
         std::lock_guard<CCriticalSection> l(cs.cs());
         CBlockLocator loc;
         if (!gArgs.GetBoolArg("-rescan", false) && !gArgs.GetBoolArg("-zapwallettxes", false) &&
+            !gArgs.GetBoolArg("-salvagewallet", false) &&
             w->DB().Read(std::string("bestblock"), loc)) {
             start = cs.FindForkInGlobalIndex(loc);
         } else {
