@@ -117,6 +117,8 @@ __device__ __forceinline__ void fe_mul_small(fe& r, const fe& a, uint32_t m) {
     fe_cond_sub_p(r, (uint32_t)f);
 }
 
+__device__ __forceinline__ void fe_reduce512(fe& r, const uint32_t (&t)[16]);
+
 // 512-bit product reduced mod p.
 __device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) {
     uint32_t t[16];
@@ -133,6 +135,47 @@ __device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) {
         }
         t[i + 8] = (uint32_t)carry;
     }
+    fe_reduce512(r, t);
+}
+
+// Squaring: the 28 cross products a_i*a_j (i<j) once, doubled with a 1-bit shift, plus the 8
+// diagonal squares — 36 32x32 multiplies instead of the 64 of fe_mul. Point doubling and the
+// inversion/sqrt ladders are mostly squarings.
+__device__ __forceinline__ void fe_sqr(fe& r, const fe& a) {
+    uint32_t t[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) t[i] = 0;
+#pragma unroll
+    for (int i = 0; i < 7; i++) {
+        uint64_t carry = 0;
+#pragma unroll
+        for (int j = i + 1; j < 8; j++) {
+            const uint64_t p = (uint64_t)a.v[i] * a.v[j] + t[i + j] + carry;
+            t[i + j] = (uint32_t)p;
+            carry = p >> 32;
+        }
+        t[i + 8] = (uint32_t)carry;
+    }
+    t[15] = t[14] >> 31;
+#pragma unroll
+    for (int i = 14; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
+    t[0] <<= 1;
+    uint64_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        const uint64_t sq = (uint64_t)a.v[i] * a.v[i];
+        c += (uint64_t)t[2 * i] + (uint32_t)sq;
+        t[2 * i] = (uint32_t)c;
+        c >>= 32;
+        c += (uint64_t)t[2 * i + 1] + (sq >> 32);
+        t[2 * i + 1] = (uint32_t)c;
+        c >>= 32;
+    }
+    fe_reduce512(r, t);
+}
+
+// 512-bit value t (t < 2^512) reduced mod p.
+__device__ __forceinline__ void fe_reduce512(fe& r, const uint32_t (&t)[16]) {
     // lo + hi * (2^32 + 977)
     uint32_t u[9];
     uint64_t c = 0;
@@ -185,7 +228,6 @@ __device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) {
     fe_cond_sub_p(r, 0);
 }
 
-__device__ __forceinline__ void fe_sqr(fe& r, const fe& a) { fe_mul(r, a, a); }
 
 __device__ __forceinline__ void fe_sqr_n(fe& r, const fe& a, int n) {
     fe_sqr(r, a);
