@@ -544,14 +544,24 @@ __device__ __forceinline__ void store_be32(unsigned char* b, const fe& a) {
 }
 
 // One lane per signature: scalar checks, s^-1, u1, u2, wNAF(u2), r+n.
-__global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs, int n) {
+// Reads the packed host arrays (msg 32 B, compact sig 64 B, compressed key 33 B per
+// signature: 129 B uploaded instead of a 272 B Job) and builds the Job on the device.
+__global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs, const unsigned char* __restrict__ msg,
+                                                         const unsigned char* __restrict__ sig,
+                                                         const unsigned char* __restrict__ pub, int n) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= n) return;
     Job& J = jobs[idx];
+    const unsigned char* sg = sig + (size_t)idx * 64;
+    const unsigned char* pk = pub + (size_t)idx * 33;
+#pragma unroll
+    for (int i = 0; i < 32; i++) J.r[i] = sg[i];
+#pragma unroll
+    for (int i = 0; i < 33; i++) J.pub[i] = pk[i];
     fe r, s, z;
-    load_be32(r, J.r);
-    load_be32(s, J.rn);
-    load_be32(z, J.u1);
+    load_be32(r, sg);
+    load_be32(s, sg + 32);
+    load_be32(z, msg + (size_t)idx * 32);
     const bool ok = sc_lt_n(r) && sc_lt_n(s) && !fe_is_zero(r) && !fe_is_zero(s);
     if (!sc_lt_n(z)) sc_sub_n(z); // z < 2^256 < 2n
     fe one;
@@ -767,6 +777,7 @@ struct State {
     std::mutex m;
     Job* d_jobs = nullptr;
     uint8_t* d_out = nullptr;
+    unsigned char* d_in = nullptr; // packed msg32 | sig64 | pub33 arrays, cap entries each
     size_t cap = 0;
     hipStream_t stream = nullptr;
 };
@@ -808,27 +819,26 @@ std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, c
     State& st = S();
     std::call_once(st.once, InitTable);
 
-    // host: copy r, s, z, pubkey; all scalar arithmetic runs in ecdsa_prep_kernel
-    std::vector<Job> jobs(n);
-    for (size_t i = 0; i < n; i++) {
-        Job& J = jobs[i];
-        memset(&J, 0, sizeof(J));
-        memcpy(J.u1, &msg32[i * 32], 32);
-        memcpy(J.r, &sig64[i * 64], 32);
-        memcpy(J.rn, &sig64[i * 64 + 32], 32);
-        memcpy(J.pub, &pub33[i * 33], 33);
-    }
-
+    // host: upload the packed z / (r,s) / key arrays; the prep kernel builds the Jobs and does
+    // all scalar arithmetic
     std::lock_guard<std::mutex> l(st.m);
     if (st.cap < n) {
         if (st.d_jobs) BCP_HIP_CHECK(hipFree(st.d_jobs));
         if (st.d_out) BCP_HIP_CHECK(hipFree(st.d_out));
+        if (st.d_in) BCP_HIP_CHECK(hipFree(st.d_in));
         st.cap = std::max<size_t>(n, 4096);
         BCP_HIP_CHECK(hipMalloc(&st.d_jobs, st.cap * sizeof(Job)));
         BCP_HIP_CHECK(hipMalloc(&st.d_out, st.cap));
+        BCP_HIP_CHECK(hipMalloc(&st.d_in, st.cap * 129));
     }
-    BCP_HIP_CHECK(hipMemcpyAsync(st.d_jobs, jobs.data(), n * sizeof(Job), hipMemcpyHostToDevice, st.stream));
-    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st.stream, st.d_jobs, (int)n);
+    unsigned char* d_msg = st.d_in;
+    unsigned char* d_sig = d_msg + st.cap * 32;
+    unsigned char* d_pub = d_sig + st.cap * 64;
+    BCP_HIP_CHECK(hipMemcpyAsync(d_msg, msg32.data(), n * 32, hipMemcpyHostToDevice, st.stream));
+    BCP_HIP_CHECK(hipMemcpyAsync(d_sig, sig64.data(), n * 64, hipMemcpyHostToDevice, st.stream));
+    BCP_HIP_CHECK(hipMemcpyAsync(d_pub, pub33.data(), n * 33, hipMemcpyHostToDevice, st.stream));
+    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st.stream, st.d_jobs,
+                       (const unsigned char*)d_msg, (const unsigned char*)d_sig, (const unsigned char*)d_pub, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
     const int grid = (int)((n + WG - 1) / WG);
     hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, st.stream, st.d_jobs, st.d_gtab, st.d_out, (int)n);
