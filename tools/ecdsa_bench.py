@@ -25,7 +25,7 @@ assert all(r)
 if b.gpu_available():
     nat.ecdsa_verify_batch(items[:256], use_gpu=True)  # warm-up (table upload, code load)
     for size in (1024, 8192, n, 4 * n):
-        r, ms = nat.ecdsa_verify_batch(items[:size], use_gpu=True)
+        r, ms = nat.ecdsa_verify_batch(items[:size], use_gpu=True, threads=min(16, os.cpu_count() or 8))
         assert all(r), "GPU rejected a valid signature"
         out[f"gpu_sig_per_s_{size}"] = size / ms * 1e3
 print(json.dumps(out))
