@@ -1,6 +1,9 @@
 """End-to-end regtest chain through the C++ node (reference test/functional/bcp_hardfork.py:
 mine past BCPHeight=3000 so blocks switch to the 140-byte header + Equihash(48,5),
-then getblocktemplate reports height 3001)."""
+then getblocktemplate reports height 3001).
+
+Every test only assumes what the module fixture guarantees (a chain of at least 101 blocks),
+so the module runs in any order and under pytest-xdist's per-test distribution."""
 import pytest
 
 from bitcoincashplus_amd.node.embedded import EmbeddedNode, RPCError
@@ -10,21 +13,25 @@ from bitcoincashplus_amd.node.embedded import EmbeddedNode, RPCError
 def node(tmp_path_factory):
     d = tmp_path_factory.mktemp("regtest")
     n = EmbeddedNode("regtest", str(d), gpu=False)
+    assert n.getblockcount() == 0
+    n.generate(101)
     yield n
     n.stop()
 
 
 def test_genesis(node):
-    assert node.getblockcount() == 0
-    assert node.getbestblockhash() == "0f9188f13cb7b2c71f2a335e3a4fc328bf5beb436012afca590b1a11466e2206"
+    assert node.getblockhash(0) == "0f9188f13cb7b2c71f2a335e3a4fc328bf5beb436012afca590b1a11466e2206"
 
 
 def test_generate_prefork(node):
-    hashes = node.generate(101)
-    assert len(hashes) == 101
-    assert node.getblockcount() == 101
+    start = node.getblockcount()
+    if start >= 2999:
+        pytest.skip("chain already past the fork")
+    hashes = node.generate(3)
+    assert len(hashes) == 3
+    assert node.getblockcount() == start + 3
     blk = node.getblock(hashes[-1])
-    assert blk["height"] == 101
+    assert blk["height"] == start + 3
     assert blk["solution"] == ""
     hdr_hex = node.getblockheader(hashes[-1], False)
     assert len(hdr_hex) == 160  # legacy 80-byte header before the fork
@@ -32,23 +39,27 @@ def test_generate_prefork(node):
 
 def test_utxo_and_info(node):
     info = node.getblockchaininfo()
-    assert info["chain"] == "regtest" and info["blocks"] == 101 and info["bcpheight"] == 3000
+    assert info["chain"] == "regtest" and info["blocks"] >= 101 and info["bcpheight"] == 3000
     ts = node.gettxoutsetinfo()
-    assert ts["height"] == 101 and ts["txouts"] >= 101
+    assert ts["height"] == info["blocks"] and ts["txouts"] >= 101
 
 
 def test_fork_transition_equihash(node):
-    node.generate(3000 - node.getblockcount() - 1)
-    assert node.getblockcount() == 2999
-    tmpl = node.getblocktemplate()
-    assert tmpl["height"] == 3000 and tmpl["equihash"] == "48,5"
-    h = node.generate(2)
-    blk = node.getblock(h[0])
+    if node.getblockcount() < 2999:
+        node.generate(2999 - node.getblockcount())
+        assert node.getblockcount() == 2999
+        tmpl = node.getblocktemplate()
+        assert tmpl["height"] == 3000 and tmpl["equihash"] == "48,5"
+    start = node.getblockcount()
+    node.generate(2)
+    h = node.getblockhash(3000)
+    blk = node.getblock(h)
     assert blk["height"] == 3000
     assert len(blk["solution"]) > 0  # Equihash(48,5) solution present
-    hdr_hex = node.getblockheader(h[0], False)
+    hdr_hex = node.getblockheader(h, False)
     assert len(hdr_hex) > 280  # 140-byte header + solution
-    assert node.getblocktemplate()["height"] == 3002
+    assert len(node.getblockheader(node.getblockhash(2999), False)) == 160  # legacy below the fork
+    assert node.getblocktemplate()["height"] == start + 3
 
 
 def test_invalidate_reconsider(node):
