@@ -1,9 +1,11 @@
 #include "consensus/pow.h"
 #include "consensus/equihash.h"
 #include "kernels/gpu_api.h"
+#include "util/util.h"
 
 #include <algorithm>
 #include <atomic>
+#include <stdexcept>
 
 namespace bcp {
 
@@ -120,17 +122,28 @@ std::vector<bool> CheckEquihashSolutions(const std::vector<const CBlockHeader*>&
     const EquihashParams ep(params.EquihashN(), params.EquihashK());
     std::vector<bool> out(headers.size(), false);
     if (headers.empty()) return out;
-    if (allow_gpu && headers.size() >= 4 && gpu::GpuAvailable()) {
-        std::vector<gpu::EhBaseState> states;
-        std::vector<std::vector<unsigned char>> sols;
-        states.reserve(headers.size());
-        for (const CBlockHeader* h : headers) {
-            states.push_back(gpu::MakeEhBaseState(EquihashStateFor(h, ep)));
-            sols.push_back(h->nSolution);
+    static std::atomic<int> gpuFailures{0};
+    if (allow_gpu && headers.size() >= 4 && gpuFailures.load() < 3 && (GpuFaultInjection() || gpu::GpuAvailable())) {
+        // A device failure must not leave headers neither accepted nor rejected: log it and
+        // verify the same batch on the CPU. Three consecutive failures turn the GPU path off.
+        try {
+            if (GpuFaultInjection()) throw std::runtime_error("injected GPU Equihash-verify fault");
+            std::vector<gpu::EhBaseState> states;
+            std::vector<std::vector<unsigned char>> sols;
+            states.reserve(headers.size());
+            for (const CBlockHeader* h : headers) {
+                states.push_back(gpu::MakeEhBaseState(EquihashStateFor(h, ep)));
+                sols.push_back(h->nSolution);
+            }
+            std::vector<uint8_t> r = gpu::EquihashVerifyBatch(ep.N, ep.K, states, sols);
+            for (size_t i = 0; i < r.size(); ++i) out[i] = r[i] != 0;
+            gpuFailures = 0;
+            return out;
+        } catch (const std::exception& e) {
+            const int f = ++gpuFailures;
+            LogPrintf("GPU Equihash verification failed (%s); verifying %zu headers on the CPU%s\n", e.what(),
+                      headers.size(), f >= 3 ? " (GPU path now disabled)" : "");
         }
-        std::vector<uint8_t> r = gpu::EquihashVerifyBatch(ep.N, ep.K, states, sols);
-        for (size_t i = 0; i < r.size(); ++i) out[i] = r[i] != 0;
-        return out;
     }
     for (size_t i = 0; i < headers.size(); ++i) out[i] = EhIsValidSolution(ep, EquihashStateFor(headers[i], ep), headers[i]->nSolution);
     return out;

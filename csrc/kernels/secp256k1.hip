@@ -771,6 +771,9 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
     out[idx] = (ok && match && J.scalar_ok) ? 1 : 0;
 }
 
+// Device-resident verifier state, one per HIP device: the generator comb table, the
+// stream and the grow-only job/input buffers all belong to the device they were
+// allocated on, so a call for device d never touches another device's pointers.
 struct State {
     std::once_flag once;
     uint32_t* d_gtab = nullptr;
@@ -781,12 +784,15 @@ struct State {
     size_t cap = 0;
     hipStream_t stream = nullptr;
 };
-State& S() {
-    static State s;
-    return s;
+constexpr int MAX_DEVICES = 64;
+State& S(int device) {
+    static State s[MAX_DEVICES];
+    if (device < 0 || device >= MAX_DEVICES) throw std::runtime_error("EcdsaVerifyBatch: device id out of range");
+    return s[device];
 }
 
-void InitTable() {
+// Builds the table on the current device (the caller made `st`'s device current).
+void InitTable(State& st) {
     // 32 x 256 affine points, 8 LE limbs for x then y
     const std::vector<secp::Ge>& t = secp::generator_table();
     std::vector<uint32_t> h(32 * 256 * 16, 0);
@@ -802,9 +808,9 @@ void InitTable() {
             h[e * 16 + 8 + k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
         }
     }
-    BCP_HIP_CHECK(hipMalloc(&S().d_gtab, h.size() * 4));
-    BCP_HIP_CHECK(hipMemcpy(S().d_gtab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    BCP_HIP_CHECK(hipStreamCreateWithFlags(&S().stream, hipStreamNonBlocking));
+    BCP_HIP_CHECK(hipMalloc(&st.d_gtab, h.size() * 4));
+    BCP_HIP_CHECK(hipMemcpy(st.d_gtab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    BCP_HIP_CHECK(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
 }
 
 } // namespace
@@ -815,9 +821,10 @@ std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, c
     if (sig64.size() != n * 64 || pub33.size() != n * 33) throw std::invalid_argument("EcdsaVerifyBatch: sizes");
     std::vector<uint8_t> result(n, 0);
     if (n == 0) return result;
-    UseDevice(device);
-    State& st = S();
-    std::call_once(st.once, InitTable);
+    const int dev = UseDevice(device);
+    State& st = S(dev);
+    // a throwing init leaves the once_flag unset, so the next call retries it
+    std::call_once(st.once, [&] { InitTable(st); });
 
     // host: upload the packed z / (r,s) / key arrays; the prep kernel builds the Jobs and does
     // all scalar arithmetic

@@ -48,7 +48,8 @@ std::string HelpMessage() {
         {"-dbcache=<n>", "Set database cache size in megabytes (default: 450)"},
         {"-par=<n>", "Number of script verification threads (0 = auto)"},
         {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
-        {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 256)"},
+        {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 1024)"},
+        {"-gpufaultinjection", "(testing) make every validation GPU batch fail so the CPU fallback runs (default: 0)"},
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
         {"-blocknotify=<cmd>", "Execute command when the best block changes (%s in cmd is replaced by block hash)"},
@@ -283,8 +284,10 @@ int AppMain(int argc, char* argv[]) {
     SetGpuSigThreshold((size_t)gArgs.GetArg("-gpusigthreshold", (int64_t)GetGpuSigThreshold()));
     InitSignatureCache(gArgs.GetArg("-maxsigcachesize", (int64_t)DEFAULT_MAX_SIG_CACHE_SIZE));
     InitScriptExecutionCache(gArgs.GetArg("-maxscriptcachesize", (int64_t)DEFAULT_MAX_SCRIPT_CACHE_SIZE));
-    const bool useGpu = gArgs.GetBoolArg("-gpu", true) && gpu::GpuAvailable();
-    LogPrintf("GPU acceleration: %s\n", useGpu ? gpu::DeviceName(0).c_str() : "disabled");
+    SetGpuFaultInjection(gArgs.GetBoolArg("-gpufaultinjection", false));
+    const bool useGpu = gArgs.GetBoolArg("-gpu", true) && (GpuFaultInjection() || gpu::GpuAvailable());
+    LogPrintf("GPU acceleration: %s%s\n", !useGpu ? "disabled" : gpu::GpuAvailable() ? gpu::DeviceName(0).c_str() : "none",
+              GpuFaultInjection() ? " (fault injection: every GPU batch fails)" : "");
 
     // ---- RPC server starts in warmup so clients get RPC_IN_WARMUP while loading
     RegisterAllRPCCommands(tableRPC);

@@ -274,7 +274,7 @@ static bool SolveLegacy(CBlock& block, const Consensus::Params& cp, uint64_t& nM
     for (int i = 0; i < 4096 && nMaxTries > 0; i++) {
         if (CheckProofOfWork(block.GetHash(cp), block.nBits, false, cp)) return true;
         if (cancel && cancel->load()) return false;
-        ++n32;
+        if (++n32 == 0) block.nTime++;
         WriteLE32(block.nNonce.begin(), n32);
         --nMaxTries;
         std::lock_guard<std::mutex> l(g_minerMutex);
@@ -284,7 +284,7 @@ static bool SolveLegacy(CBlock& block, const Consensus::Params& cp, uint64_t& nM
         while (nMaxTries > 0) {
             if (CheckProofOfWork(block.GetHash(cp), block.nBits, false, cp)) return true;
             if (cancel && cancel->load()) return false;
-            ++n32;
+            if (++n32 == 0) block.nTime++; // nonce space wrapped: new header
             WriteLE32(block.nNonce.begin(), n32);
             --nMaxTries;
         }
@@ -293,29 +293,37 @@ static bool SolveLegacy(CBlock& block, const Consensus::Params& cp, uint64_t& nM
     arith_uint256 target;
     target.SetCompact(block.nBits);
     const uint256 t = ArithToUint256(target);
+    // Scan [n32, 2^32) in chunks; when the 32-bit nonce space is used up, bump nTime (a new
+    // header) and start again from 0, so no nonce is scanned twice for the same header.
+    const uint64_t NONCE_SPACE = 1ull << 32;
     while (nMaxTries > 0) {
         std::vector<unsigned char> hdr = SerializeToBytes(static_cast<const CBlockHeader&>(block), SER_NETWORK,
                                                           PROTOCOL_VERSION | SERIALIZE_BLOCK_LEGACY);
-        const uint64_t count = std::min<uint64_t>(nMaxTries, 1ull << 30);
+        const uint64_t count = std::min<uint64_t>({nMaxTries, 1ull << 30, NONCE_SPACE - n32});
         const int64_t t0 = GetTimeMicros();
         const int64_t found = gpu::Sha256dScanNonces(hdr.data(), t.begin(), n32, count);
+        const uint64_t scanned = found >= 0 ? (uint64_t)found - n32 + 1 : count;
         {
             std::lock_guard<std::mutex> l(g_minerMutex);
             g_minerStats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
-            g_minerStats.sha_nonces += count;
+            g_minerStats.sha_nonces += scanned;
         }
+        nMaxTries -= std::min<uint64_t>(nMaxTries, scanned);
         if (found >= 0) {
             WriteLE32(block.nNonce.begin(), (uint32_t)found);
-            nMaxTries -= std::min<uint64_t>(nMaxTries, (uint32_t)found - n32 + 1);
-            return CheckProofOfWork(block.GetHash(cp), block.nBits, false, cp);
+            if (CheckProofOfWork(block.GetHash(cp), block.nBits, false, cp)) return true;
+            LogPrintf("SolveLegacy: GPU nonce %u failed the CPU proof-of-work recheck; scanning on\n",
+                      (uint32_t)found);
         }
-        nMaxTries -= count;
-        n32 += (uint32_t)count;
-        if (cancel && cancel->load()) return false;
-        if (n32 == 0) {
-            // nonce space exhausted: bump the time and restart
+        const uint64_t next = (uint64_t)n32 + scanned;
+        if (next >= NONCE_SPACE) {
             block.nTime++;
+            n32 = 0;
+        } else {
+            n32 = (uint32_t)next;
         }
+        WriteLE32(block.nNonce.begin(), n32);
+        if (cancel && cancel->load()) return false;
     }
     return false;
 }

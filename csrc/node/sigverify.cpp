@@ -33,9 +33,20 @@ size_t InitSignatureCache(int64_t mib) {
     return n;
 }
 
-static std::atomic<size_t> g_gpuThreshold{256};
+static std::atomic<size_t> g_gpuThreshold{DEFAULT_GPU_SIG_THRESHOLD};
 void SetGpuSigThreshold(size_t n) { g_gpuThreshold = n; }
 size_t GetGpuSigThreshold() { return g_gpuThreshold.load(); }
+
+// Device failures (allocation, launch, fault) never decide a block's validity: the batch
+// is re-verified on the CPU. After MAX_GPU_SIG_FAILURES consecutive failures the GPU
+// path is switched off for the rest of the process.
+static std::atomic<int> g_gpuFailures{0};
+static std::atomic<bool> g_gpuDisabled{false};
+void ResetGpuSigFailures() {
+    g_gpuFailures = 0;
+    g_gpuDisabled = false;
+}
+bool GpuSigPathDisabled() { return g_gpuDisabled.load(); }
 
 static std::mutex g_statsMutex;
 static SigVerifyStats g_stats;
@@ -90,6 +101,7 @@ std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*
         for (size_t j = 0; j < n; j++) prep(j);
     for (size_t j = 0; j < n; j++)
         if (!hostOk[j]) pub[j * 33] = 2; // keep device input well-formed; result masked below
+    if (GpuFaultInjection()) throw std::runtime_error("injected GPU signature-verify fault");
     std::vector<uint8_t> res = gpu::EcdsaVerifyBatch(msg, sig, pub);
     for (size_t j = 0; j < n; j++) res[j] &= hostOk[j];
     return res;
@@ -111,21 +123,38 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
     bool ok = true;
     const size_t n = todo.size();
     if (n > 0) {
-        const bool gpu = useGpu && n >= g_gpuThreshold.load() && gpu::GpuAvailable();
+        bool gpu = useGpu && !g_gpuDisabled.load() && n >= g_gpuThreshold.load() &&
+                   (GpuFaultInjection() || gpu::GpuAvailable());
         const int64_t t0 = GetTimeMicros();
         if (gpu) {
             std::vector<const DeferredSigCheck*> ptrs(n);
             for (size_t j = 0; j < n; j++) ptrs[j] = &checks[todo[j]];
-            std::vector<uint8_t> res = GpuVerifyDeferred(ptrs, pool);
-            for (size_t j = 0; j < n; j++) {
-                if (!res[j]) ok = false;
-                else if (cacheStore) cache.Set(entries[todo[j]]);
+            std::vector<uint8_t> res;
+            try {
+                res = GpuVerifyDeferred(ptrs, pool);
+                g_gpuFailures = 0;
+            } catch (const std::exception& e) {
+                const int fails = ++g_gpuFailures;
+                LogPrintf("GPU signature verification failed (%s); re-verifying %zu signatures on the CPU\n",
+                          e.what(), n);
+                if (fails >= MAX_GPU_SIG_FAILURES && !g_gpuDisabled.exchange(true))
+                    LogPrintf("GPU signature verification disabled after %d consecutive failures\n", fails);
+                std::lock_guard<std::mutex> l(g_statsMutex);
+                g_stats.gpu_failures++;
+                gpu = false;
             }
-            std::lock_guard<std::mutex> l(g_statsMutex);
-            g_stats.gpu_batches++;
-            g_stats.gpu_sigs += n;
-            g_stats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
-        } else {
+            if (gpu) {
+                for (size_t j = 0; j < n; j++) {
+                    if (!res[j]) ok = false;
+                    else if (cacheStore) cache.Set(entries[todo[j]]);
+                }
+                std::lock_guard<std::mutex> l(g_statsMutex);
+                g_stats.gpu_batches++;
+                g_stats.gpu_sigs += n;
+                g_stats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
+            }
+        }
+        if (!gpu) {
             std::atomic<bool> allOk{true};
             auto work = [&](size_t j) {
                 if (!allOk.load(std::memory_order_relaxed)) return;

@@ -39,9 +39,15 @@ SignatureCache& GetSignatureCache();
 size_t InitSignatureCache(int64_t mib);
 
 struct SigVerifyStats {
-    uint64_t gpu_batches = 0, gpu_sigs = 0, cpu_sigs = 0, cache_hits = 0;
+    uint64_t gpu_batches = 0, gpu_sigs = 0, cpu_sigs = 0, cache_hits = 0, gpu_failures = 0;
     double gpu_ms = 0, cpu_ms = 0;
 };
+
+// Smallest batch sent to the GPU (-gpusigthreshold). Below it the CPU pool is faster:
+// profiles/ecdsa_crossover.md measures the crossover on MI355X.
+static const size_t DEFAULT_GPU_SIG_THRESHOLD = 1024;
+// Consecutive device failures after which the GPU signature path is turned off.
+static const int MAX_GPU_SIG_FAILURES = 3;
 
 // Verify all checks; returns true iff every one is valid. cacheStore: remember
 // successes (mempool acceptance); block validation erases consumed entries.
@@ -49,8 +55,10 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
                            bool cacheErase);
 // Device verification of the given checks (no cache); result[i] = 1 iff valid.
 std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool);
-void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path (default 256)
+void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path
 size_t GetGpuSigThreshold();
+void ResetGpuSigFailures();
+bool GpuSigPathDisabled();
 SigVerifyStats GetSigVerifyStats();
 
 // TransactionSignatureChecker that consults/updates the signature cache.

@@ -191,6 +191,22 @@ void bind_consensus(pyb::module_& m) {
         r >> h;
         return CheckEquihashSolution(&h, Params(chain));
     });
+    // Batched header check (CheckEquihashSolutions): GPU for >= 4 headers, CPU fallback on device errors.
+    m.def(
+        "check_equihash_headers",
+        [](const std::vector<pyb::bytes>& hs, const std::string& chain, bool allow_gpu) {
+            std::vector<CBlockHeader> headers(hs.size());
+            for (size_t i = 0; i < hs.size(); ++i) {
+                std::vector<unsigned char> v = to_vec(hs[i]);
+                SpanReader r(v.data(), v.size(), SER_NETWORK, PROTOCOL_VERSION);
+                r >> headers[i];
+            }
+            std::vector<const CBlockHeader*> ptrs;
+            for (auto& h : headers) ptrs.push_back(&h);
+            pyb::gil_scoped_release nogil;
+            return CheckEquihashSolutions(ptrs, Params(chain), allow_gpu);
+        },
+        pyb::arg("headers"), pyb::arg("chain") = "regtest", pyb::arg("allow_gpu") = true);
     m.def("tx_decode", [](const pyb::bytes& b) {
         std::vector<unsigned char> v = to_vec(b);
         SpanReader r(v.data(), v.size(), SER_NETWORK, PROTOCOL_VERSION);

@@ -207,6 +207,40 @@ void bind_gpu(pyb::module_& m) {
             return pyb::make_tuple(out, ms);
         },
         pyb::arg("items"), pyb::arg("use_gpu") = true, pyb::arg("threads") = 8);
+
+    // Block-validation entry point (BatchVerifySignatures): cache-less, GPU when the batch
+    // reaches the threshold, CPU fallback when the device path throws. Returns all-valid.
+    m.def(
+        "sig_batch_verify",
+        [](const std::vector<std::tuple<pyb::bytes, pyb::bytes, pyb::bytes>>& items, bool use_gpu, int threads) {
+            std::vector<DeferredSigCheck> checks(items.size());
+            for (size_t i = 0; i < items.size(); i++) {
+                checks[i].pubkey = to_vec(std::get<0>(items[i]));
+                checks[i].sig = to_vec(std::get<1>(items[i]));
+                auto m32 = to_vec(std::get<2>(items[i]));
+                if (m32.size() != 32) throw std::invalid_argument("msg32");
+                memcpy(checks[i].sighash.begin(), m32.data(), 32);
+            }
+            pyb::gil_scoped_release nogil;
+            WorkerPool pool(std::max(1, threads));
+            return BatchVerifySignatures(checks, &pool, use_gpu, false, false);
+        },
+        pyb::arg("items"), pyb::arg("use_gpu") = true, pyb::arg("threads") = 4);
+    m.def("set_gpu_fault_injection", &SetGpuFaultInjection);
+    m.def("set_gpu_sig_threshold", &SetGpuSigThreshold);
+    m.def("get_gpu_sig_threshold", &GetGpuSigThreshold);
+    m.def("reset_gpu_sig_failures", &ResetGpuSigFailures);
+    m.def("gpu_sig_path_disabled", &GpuSigPathDisabled);
+    m.def("sig_verify_stats", []() {
+        const SigVerifyStats s = GetSigVerifyStats();
+        pyb::dict d;
+        d["gpu_batches"] = s.gpu_batches;
+        d["gpu_sigs"] = s.gpu_sigs;
+        d["cpu_sigs"] = s.cpu_sigs;
+        d["cache_hits"] = s.cache_hits;
+        d["gpu_failures"] = s.gpu_failures;
+        return d;
+    });
 }
 
 } // namespace py

@@ -112,6 +112,8 @@ static UniValue getgpuinfo(const JSONRPCRequest& req) {
     sv.pushKV("gpu_ms", s.gpu_ms);
     sv.pushKV("cpu_ms", s.cpu_ms);
     sv.pushKV("gpu_threshold", (uint64_t)GetGpuSigThreshold());
+    sv.pushKV("gpu_failures", (uint64_t)s.gpu_failures);
+    sv.pushKV("gpu_disabled", GpuSigPathDisabled());
     obj.pushKV("sigverify", sv);
     return obj;
 }

@@ -514,3 +514,9 @@ void RunCommand(const std::string& cmd) {
 
 void RunCommandAsync(const std::string& cmd) { std::thread([cmd] { RunCommand(cmd); }).detach(); }
 } // namespace bcp
+
+namespace bcp {
+static std::atomic<bool> g_gpuFaultInjection{false};
+void SetGpuFaultInjection(bool on) { g_gpuFaultInjection = on; }
+bool GpuFaultInjection() { return g_gpuFaultInjection.load(); }
+} // namespace bcp

@@ -106,6 +106,10 @@ bool RenameOver(const std::string& src, const std::string& dst);
 bool FileCommit(FILE* file);
 void RenameThread(const char* name);
 int GetNumCores();
+// -gpufaultinjection (tests only): every GPU batch issued by validation throws, as a failed
+// hipMalloc or launch would, so the CPU fallback paths can be exercised on any host.
+void SetGpuFaultInjection(bool on);
+bool GpuFaultInjection();
 std::string FormatFullVersion();
 std::string FormatSubVersion(const std::string& name, int nClientVersion, const std::vector<std::string>& comments);
 static const int CLIENT_VERSION = 170000; // 0.17.0

@@ -73,3 +73,45 @@ def test_gpu_batch_edge_scalars(native):
             items.append((native.ec_pubkey_create(sec, True), native.ec_sign(sec, m), m))
     res, _ = native.ecdsa_verify_batch(items, use_gpu=True)
     assert all(res)
+
+
+def _edge_scalar_items(native):
+    """DER signatures whose r or s sit on the scalar-range boundaries (0, 1, n-1, n, n+1,
+    2^256-1) plus message hashes >= n. The lax-DER parse on the host and the range checks and
+    z reduction in ecdsa_prep_kernel must agree with CPubKey::Verify on every one."""
+    n = ref.N
+    sec = (0x1234567 * 0x9E3779B97F4A7C15).to_bytes(32, "big")
+    pub = native.ec_pubkey_create(sec, True)
+    msgs = [b"\xff" * 32, n.to_bytes(32, "big"), (n + 5).to_bytes(32, "big"), b"\x00" * 32,
+            hashlib.sha256(b"edge").digest()]
+    edges = [0, 1, n - 1, n, n + 1, 2**256 - 1]
+    items = []
+    for m in msgs:
+        good = native.ec_sign(sec, m)
+        items.append((pub, good, m))  # valid, with z >= n for the first three messages
+        rlen = good[3]
+        r_good = int.from_bytes(good[4:4 + rlen], "big")
+        off = 4 + rlen
+        s_good = int.from_bytes(good[off + 2:off + 2 + good[off + 1]], "big")
+        for e in edges:
+            items.append((pub, ref.der_encode(e, s_good), m))
+            items.append((pub, ref.der_encode(r_good, e), m))
+        items.append((pub, ref.der_encode(r_good, n - s_good), m))  # high-S twin: normalised, valid
+        if r_good + n < 2**256:
+            items.append((pub, ref.der_encode(r_good + n, s_good), m))  # x(R)+n form of r: out of range
+    return items
+
+
+def test_cpu_edge_scalars(native):
+    items = _edge_scalar_items(native)
+    res, _ = native.ecdsa_verify_batch(items, use_gpu=False)
+    # the valid signature and its high-S twin verify for every message; nothing else does
+    assert sum(res) == 2 * 5
+
+
+@pytest.mark.gpu
+def test_gpu_edge_scalars_match_cpu(native):
+    items = _edge_scalar_items(native)
+    cpu, _ = native.ecdsa_verify_batch(items, use_gpu=False)
+    gpu, _ = native.ecdsa_verify_batch(items, use_gpu=True)
+    assert gpu == cpu
