@@ -2,30 +2,32 @@
 // CPU BasicSolve/OptimisedSolve (reference src/crypto/equihash.cpp:332-722,
 // called from generateBlocks src/rpc/mining.cpp:161-199).
 //
-// Design: an atomic-free, bucket-sorted Wagner solver with parent pointers.
+// Design: a bucket-sorted Wagner solver with parent pointers and contiguous buckets.
 //
 //  * Rows are bucketed on the top BB bits of the current digit (NB = 2^BB buckets,
-//    ~INIT/NB rows each; (200,9): 512 buckets x 4096 rows).
-//  * Every kernel launch is "one workgroup per bucket". A workgroup owns an output
-//    AREA of CAP row slots. Instead of a global atomic per emitted row (memory-side
-//    atomics across the 8 XCDs measured ~15 G/s, which dominated round time in the
-//    first version), each workgroup counting-sorts its outputs by destination bucket
-//    IN LDS and writes
-//      - the rows into its own area, grouped by destination bucket,
-//      - one column of the NB x NB count/offset matrices CNT[dest][src], OFF[dest][src].
-//    The next round's workgroup `d` reads row d of those matrices and gathers its NB
-//    contiguous runs (lane per row) straight into LDS. Outputs are permuted in LDS so
-//    each workgroup writes its area in slot order (lane-consecutive, coalesced stores).
-//  * Collisions on the remaining RB = DB-BB bits of the digit are found with an LDS
-//    hash table (atomicExch chain heads); each row keeps a 64-bit parent reference
-//    (global slot of both parents), so nothing ever carries index lists.
+//    ~INIT/NB rows each; (200,9): 512 buckets x 4096 rows). Every stage keeps each bucket
+//    CONTIGUOUS in its own area of AREA row slots.
+//  * Every kernel works "one workgroup per bucket". A producer workgroup counting-sorts its
+//    output rows by destination bucket in LDS, then claims one run per destination with ONE
+//    device-scope atomicAdd on that bucket's fill counter (a 512-lane, 2 KB contiguous wave
+//    instruction set per workgroup, issued as soon as the histogram is known so its latency
+//    hides behind the scan and scatter), and writes its rows into the claimed runs. The
+//    consumer round then reads its bucket as one contiguous block (16-byte loads, lane-flat,
+//    straight into LDS): no run tables, slot maps or per-row gather maps.
+//  * Collisions on the remaining RB = DB-BB bits of the digit are found by a counting sort of
+//    the bucket on those bits and an atomic-free pair enumeration (scan + max-scan); each output
+//    row keeps a 64-bit parent triple (producing bucket, LDS row i, LDS row j), so nothing ever
+//    carries index lists: the parents of a stage-s row are the stage-(s-1) slots
+//    bucket*AREA + i and bucket*AREA + j.
 //  * Depth-1 duplicate pruning: pairs whose rows share a parent are dropped.
-//  * Final round: pairs equal on all remaining bits are candidates; eh_expand walks
-//    the K levels of parent references, canonicalises subtree order (reference
-//    IsValidSolution ordering rule) and rejects repeated indices (LDS bitonic sort).
+//  * Final round: pairs equal on all remaining bits are candidates; eh_expand walks the K levels
+//    of parent triples, canonicalises subtree order (reference IsValidSolution ordering rule)
+//    and rejects repeated indices (LDS bitonic sort).
+//  * Block scans use DPP row shifts/broadcasts inside a wave and one LDS word per wave
+//    across waves: two barriers per scan, no ds_bpermute traffic.
 //
-// Memory traffic per row per round: one coalesced gather, one area write, one 8-byte
-// reference write. No global atomics except the (rare) candidate append.
+// Memory traffic per row per round: one contiguous read, one row write into a claimed run,
+// one 8-byte parent-triple write.
 #include <hip/hip_runtime.h>
 
 #include "crypto/hashes.h"
@@ -47,7 +49,7 @@ struct EhCfg {
     static constexpr int DB = N / (K + 1);           // digit bits
     static constexpr int BB = BB_;                   // bucket bits
     static constexpr int RB = DB - BB_;              // in-bucket collision bits
-    static constexpr int NB = 1 << BB_;              // buckets (= output areas of rounds 1..K-1)
+    static constexpr int NB = 1 << BB_;              // buckets (= areas of every stage)
     static constexpr int NRESTS = 1 << RB;
     // LDS row capacity of a round by the width of the rows it reads: the narrow late rounds
     // hold more rows (their buckets and pair lists overflow most, from duplicate subtrees)
@@ -59,7 +61,7 @@ struct EhCfg {
     static constexpr int NT = NT_;                   // threads per round workgroup
     static constexpr int NW = NT_ / 64;
     static constexpr int INIT = 1 << (DB + 1);
-    static constexpr int GENWG = GENWG_;             // generation workgroups (= stage-0 areas)
+    static constexpr int GENWG = GENWG_;             // generation workgroups per nonce
     static constexpr int NTG = NTG_;                 // threads per generation workgroup
     static constexpr int RPW = INIT / GENWG_;        // rows per generation workgroup
     static constexpr int IPH = 512 / N;
@@ -69,12 +71,11 @@ struct EhCfg {
     static constexpr int bits(int stage) { return N - stage * DB - BB_; }
     static constexpr int words(int stage) { return (bits(stage) + 31) / 32; }
     static constexpr int WMAX = words(0);
-    static constexpr int nsrc(int stage) { return stage == 0 ? GENWG_ : NB; } // areas holding stage rows
-    static constexpr size_t ROWS = (size_t)NB * AREA; // slots per stage per nonce (>= GENWG*RPW)
-    static_assert((size_t)GENWG_ * RPW <= ROWS && RPW * GENWG_ == INIT, "generation areas");
+    static constexpr size_t ROWS = (size_t)NB * AREA; // slots per stage per nonce
+    static_assert(RPW * GENWG_ == INIT && RPW < 65535, "generation split");
     static_assert(RB > 0 && DB < 32, "digit geometry");
-    static_assert(AREA < 8192 && RPW < 65535, "u16 indices, 13-bit parent signatures");
-    static_assert(NT_ % 64 == 0 && 4 * NT_ >= GENWG_ && 4 * NT_ >= NB && 4 * NTG_ >= NB, "workgroup shape");
+    static_assert(AREA < 8192, "13-bit LDS row indices in parent triples and signatures");
+    static_assert(NT_ % 64 == 0 && NT_ <= 1024 && NB <= NT_ && NB <= NTG_ && NT_ / 64 <= 64, "workgroup shape");
     static_assert(words(K - 1) == 1, "final round keeps whole rows in one LDS word");
 };
 
@@ -83,62 +84,79 @@ using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
 using Cfg48_5 = EhCfg<48, 5, 3, 256, 64, 8, 64, 256>;
 
-constexpr uint32_t NIL16 = 0xffffu;
 constexpr uint32_t NIL = 0xffffffffu;
-constexpr int MAX_CHAIN = 48;
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u3v __attribute__((ext_vector_type(3)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 
-// Block-wide scans over n (<= MAXPER*NT) values in LDS `v`, in place; each thread owns `per`
-// consecutive entries, waves scan with shuffles, wave totals are combined through `wsum`
-// (>= NT/64 + 1 entries).
-// Exclusive sum (entries of type T: u32, or u16 when every prefix fits). Returns the total.
-template <int NT, int MAXPER = 4, class T = uint32_t>
-__device__ uint32_t block_exscan(T* v, int n, uint32_t* wsum) {
+// ------------------------------------------------------------------ wave / block scans
+// DPP controls (GFX9 encoding): row_shr:n = 0x110|n, row_bcast:15 = 0x142, row_bcast:31 = 0x143,
+// wave_shr:1 = 0x138. Lanes whose source is outside the row / disabled keep `old` (= 0, the
+// identity of both + and max over unsigned values). All lanes of the wave must be active.
+template <int CTRL, int ROWMASK = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROWMASK, 0xf, false);
+}
+// Inclusive wave-wide sum (MAX = false) or max (MAX = true).
+template <bool MAX> __device__ __forceinline__ uint32_t wave_incl(uint32_t x) {
+    auto op = [](uint32_t a, uint32_t b) -> uint32_t { return MAX ? (a > b ? a : b) : a + b; };
+    x = op(x, dpp0<0x111>(x));
+    x = op(x, dpp0<0x112>(x));
+    x = op(x, dpp0<0x114>(x));
+    x = op(x, dpp0<0x118>(x));
+    x = op(x, dpp0<0x142, 0xa>(x));
+    x = op(x, dpp0<0x143, 0xc>(x));
+    return x;
+}
+
+// Block-wide exclusive sum over n (<= MAXPER*NT) values: src[i] -> dst[i] (src may be dst);
+// thread t owns `per` consecutive entries. Wave totals go through `wsum` (>= NT/64 entries);
+// every wave combines them itself, so the scan costs two barriers (the second makes dst
+// visible and frees wsum). Returns the total.
+template <int NT, int MAXPER = 4, class TS = uint32_t, class TD = TS>
+__device__ uint32_t block_exscan(const TS* src, TD* dst, int n, uint32_t* wsum) {
     constexpr int NW = NT / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int per = (n + NT - 1) / NT;
     uint32_t local[MAXPER];
     uint32_t s = 0;
 #pragma unroll
     for (int q = 0; q < MAXPER; ++q) {
         const int i = tid * per + q;
-        local[q] = (q < per && i < n) ? (uint32_t)v[i] : 0u;
+        local[q] = (q < per && i < n) ? (uint32_t)src[i] : 0u;
         s += local[q];
     }
-    uint32_t x = s; // wave inclusive scan
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
+    const uint32_t x = wave_incl<false>(s);
+    if (NW > 1) {
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
     }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t t = wsum[w];
-            wsum[w] = acc;
-            acc += t;
-        }
-        wsum[NW] = acc;
-    }
-    __syncthreads();
-    uint32_t base = wsum[wid] + x - s;
+    const uint32_t wt = (NW > 1 && lane < NW) ? wsum[lane] : 0u;
+    const uint32_t ws = wave_incl<false>(wt);
+    const uint32_t before = NW > 1 ? __builtin_amdgcn_readlane(ws, wid) - __builtin_amdgcn_readlane(wt, wid) : 0u;
+    const uint32_t total = NW > 1 ? __builtin_amdgcn_readlane(ws, NW - 1) : __builtin_amdgcn_readlane(x, 63);
+    uint32_t base = before + x - s;
 #pragma unroll
     for (int q = 0; q < MAXPER; ++q) {
         const int i = tid * per + q;
-        if (q < per && i < n) v[i] = (T)base;
+        if (q < per && i < n) dst[i] = (TD)base;
         base += local[q];
     }
-    const uint32_t total = wsum[NW];
     __syncthreads();
     return total;
 }
+template <int NT, int MAXPER = 4, class T = uint32_t>
+__device__ uint32_t block_exscan(T* v, int n, uint32_t* wsum) {
+    return block_exscan<NT, MAXPER, T, T>(v, v, n, wsum);
+}
 
-// Inclusive prefix maximum (entries u32 or u16).
+// Inclusive prefix maximum in place (entries u32 or u16); two barriers.
 template <int NT, int MAXPER = 4, class T = uint32_t>
 __device__ void block_maxscan(T* v, int n, uint32_t* wsum) {
     constexpr int NW = NT / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int per = (n + NT - 1) / NT;
     uint32_t local[MAXPER];
     uint32_t s = 0;
@@ -148,25 +166,16 @@ __device__ void block_maxscan(T* v, int n, uint32_t* wsum) {
         local[q] = (q < per && i < n) ? (uint32_t)v[i] : 0u;
         s = max(s, local[q]);
     }
-    uint32_t x = s;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x = max(x, y);
+    const uint32_t x = wave_incl<true>(s);
+    const uint32_t excl = dpp0<0x138>(x); // wave_shr:1 -> lane l sees lane l-1 (lane 0: 0)
+    if (NW > 1) {
+        if (lane == 63) wsum[wid] = x;
+        __syncthreads();
     }
-    const uint32_t excl = __shfl_up(x, 1, 64);
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t acc = 0;
-        for (int w = 0; w < NW; ++w) {
-            const uint32_t t = wsum[w];
-            wsum[w] = acc;
-            acc = max(acc, t);
-        }
-    }
-    __syncthreads();
-    uint32_t run = max(wsum[wid], lane ? excl : 0u);
+    const uint32_t wt = (NW > 1 && lane < NW) ? wsum[lane] : 0u;
+    const uint32_t ws = wave_incl<true>(wt);
+    const uint32_t before = (NW > 1 && wid > 0) ? __builtin_amdgcn_readlane(ws, wid - 1) : 0u;
+    uint32_t run = max(before, excl);
 #pragma unroll
     for (int q = 0; q < MAXPER; ++q) {
         const int i = tid * per + q;
@@ -176,21 +185,44 @@ __device__ void block_maxscan(T* v, int n, uint32_t* wsum) {
     __syncthreads();
 }
 
+// Row I/O of W dwords at a dword-aligned byte offset through a buffer descriptor: one
+// 16-byte access plus a remainder (dword-aligned 16-byte buffer accesses are legal on gfx950).
+template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint32_t* v) {
+    if constexpr (W >= 4) {
+        const u4v x = {v[0], v[1], v[2], v[3]};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
+        row_store<W - 4>(rs, off + 16, v + 4);
+    } else if constexpr (W == 3) {
+        const u3v x = {v[0], v[1], v[2]};
+        __builtin_amdgcn_raw_buffer_store_b96(x, rs, off, 0, 0);
+    } else if constexpr (W == 2) {
+        const u2v x = {v[0], v[1]};
+        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, 0);
+    } else if constexpr (W == 1) {
+        __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, 0);
+    }
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+
 // ------------------------------------------------------------------ stage 0
-// Generation workgroup gw hashes rows [gw*RPW, (gw+1)*RPW), counting-sorts them by bucket in
-// LDS and writes its area in slot order (lane-consecutive stores) + column gw of CNT/OFF
-// (CNT0/OFF0 are NB x GENWG).
+// Generation workgroup gw of a nonce hashes rows [gw*RPW, (gw+1)*RPW), counting-sorts them by
+// bucket in LDS, claims one run per destination bucket (device-scope atomicAdd on the stage-0
+// fill counters CTR0[nonce][NB]) and writes every row into its run; the leaf index of each
+// slot goes to LEAF.
 template <class C, bool HDR>
 __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__ states, uint32_t* __restrict__ R,
-                                                 uint32_t* __restrict__ F, uint32_t* __restrict__ CNT,
-                                                 uint32_t* __restrict__ OFF) {
+                                                 uint32_t* __restrict__ LEAF, uint32_t* __restrict__ CTR0) {
     constexpr int W0 = C::words(0);
     constexpr int SW = (C::N + 31) / 32 + 1;
     constexpr int NTG = C::NTG;
+    constexpr uint32_t OCAP = C::cap(1);
     __shared__ uint32_t rows[C::RPW * W0];
     __shared__ uint16_t dst[C::RPW];
     __shared__ uint16_t perm[C::RPW];
-    __shared__ uint32_t hist[C::NB], cur[C::NB];
+    __shared__ uint32_t hist[C::NB], cur[C::NB], base[C::NB];
     __shared__ uint32_t wsum[NTG / 64 + 1];
     const int gw = blockIdx.x % C::GENWG;
     const int nonce = blockIdx.x / C::GENWG;
@@ -228,41 +260,47 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
         }
     }
     __syncthreads();
-    for (int i = tid; i < C::NB; i += NTG) cur[i] = hist[i];
-    __syncthreads();
-    block_exscan<NTG>(cur, C::NB, wsum); // cur = run offsets inside area gw
-    uint32_t* cntp = CNT + (size_t)nonce * C::NB * C::GENWG;
-    uint32_t* offp = OFF + (size_t)nonce * C::NB * C::GENWG;
-    for (int i = tid; i < C::NB; i += NTG) {
-        cntp[(size_t)i * C::GENWG + gw] = hist[i];
-        offp[(size_t)i * C::GENWG + gw] = cur[i];
-    }
-    __syncthreads();
+    // claim the runs; the returned bases are used only after the scan and the scatter
+    uint32_t myb = 0;
+    if (tid < C::NB && hist[tid]) myb = atomicAdd(&CTR0[(size_t)nonce * C::NB + tid], hist[tid]);
+    block_exscan<NTG>(hist, cur, C::NB, wsum); // cur = run offsets inside this workgroup's sorted order
     for (int li = tid; li < C::RPW; li += NTG) perm[atomicAdd(&cur[dst[li]], 1u)] = (uint16_t)li;
+    if (tid < C::NB) base[tid] = myb;
     __syncthreads();
-    // word-flat stores: consecutive lanes write consecutive dwords of the area
-    uint32_t* area = R + ((size_t)nonce * C::ROWS + (size_t)gw * C::RPW) * C::WMAX;
-    uint32_t* farea = F + (size_t)nonce * C::ROWS + (size_t)gw * C::RPW;
-    for (int k = tid; k < C::RPW * W0; k += NTG) {
-        const uint32_t t = k / W0, w = k - t * W0;
-        area[k] = rows[perm[t] * W0 + w];
+    const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * W0 * 4));
+    uint32_t* leaf = LEAF + (size_t)nonce * C::ROWS;
+    for (int t = tid; t < C::RPW; t += NTG) {
+        const uint32_t li = perm[t], d = dst[li];
+        const uint32_t pos = base[d] + (uint32_t)t - (cur[d] - hist[d]);
+        if (pos < OCAP) {
+            uint32_t o[W0];
+#pragma unroll
+            for (int w = 0; w < W0; ++w) o[w] = rows[li * W0 + w];
+            const uint32_t slot = d * C::AREA + pos;
+            row_store<W0>(rs, slot * (W0 * 4), o);
+            leaf[slot] = r0 + li;
+        }
     }
-    for (int t = tid; t < C::RPW; t += NTG) farea[t] = r0 + perm[t];
 }
 
 // ------------------------------------------------------------------ stages 1..K
-__device__ __forceinline__ bool share_parent(uint64_t a, uint64_t b) {
-    const uint32_t a0 = (uint32_t)(a >> 32), a1 = (uint32_t)a, b0 = (uint32_t)(b >> 32), b1 = (uint32_t)b;
-    return a0 == b0 || a0 == b1 || a1 == b0 || a1 == b1;
+// Parent triple of a stage-s row (s >= 1): (producing bucket << 32) | (j << 16) | i; its parents
+// are the stage-(s-1) slots bucket*AREA + i and bucket*AREA + j.
+__device__ __forceinline__ uint64_t pack_tri(uint32_t d, uint32_t i, uint32_t j) {
+    return ((uint64_t)d << 32) | (j << 16) | i;
 }
-
-// index of the run holding LDS row r: last b with start[b] <= r (start is non-decreasing)
-template <int NS> __device__ __forceinline__ uint32_t run_of(const uint32_t* start, uint32_t r) {
-    uint32_t lo = 0;
-#pragma unroll
-    for (uint32_t step = NS / 2; step > 0; step >>= 1)
-        if (start[lo + step] <= r) lo += step;
-    return lo;
+// 2 x 16-bit signature of a row's parents for depth-1 duplicate pruning: each half is the
+// parent's LDS row (13 bits) plus 3 bits of the producing bucket. A half shared by two rows is
+// confirmed exactly by comparing the full producing buckets: a signature-only prune would drop
+// ~1e-4 of all pairs, ~6% of the solutions (511 pairs each).
+__device__ __forceinline__ uint32_t parent_sig(uint64_t tri) {
+    const uint32_t d = (uint32_t)(tri >> 32), f = (uint32_t)tri;
+    const uint32_t i = f & 0x1fff, j = (f >> 16) & 0x1fff;
+    return ((i | ((d & 7) << 13)) << 16) | (j | ((d & 7) << 13));
+}
+__device__ __forceinline__ bool sig_hit(uint32_t si, uint32_t sj) {
+    return (si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) || (si & 0xffff) == (sj >> 16) ||
+           (si & 0xffff) == (sj & 0xffff);
 }
 
 // Diagnostic builds (STAMP) record s_memtime at each phase boundary (thread 0, after the
@@ -274,159 +312,76 @@ template <int NS> __device__ __forceinline__ uint32_t run_of(const uint32_t* sta
         }                                                                                            \
     } while (0)
 
-// LDS bytes of a persistent round (one 1024-lane workgroup per CU for (200,9)).
-// Phase-D union (bytes): walk {sidx[CAP] u16, bend[NRESTS] u32, offp[CAP] u16};
-// prefetch {gslot[CAP] u32}.
+// LDS bytes of a round. Phase-D union `un` (bytes): {sidx[CAP] u16, bend[NRESTS] u32,
+// offp[CAP] u16} during the collision search, the slot -> pair table spair[AREA] u32 after it.
 template <class C> constexpr int un_walk_bend(int cap) { return (cap * 2 + 3) / 4 * 4; }
 template <class C> constexpr int un_walk_offp(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
 template <class C> constexpr int round_un(int cap) {
     const int walk = un_walk_offp<C>(cap) + cap * 2;
-    const int pref = cap * 4;
-    return walk > pref ? walk : pref;
+    return walk > C::AREA * 4 ? walk : C::AREA * 4;
 }
 template <class C> constexpr int round_lds(int stage, bool prune) {
     const int WI = C::words(stage - 1);
-    const int NS = C::nsrc(stage - 1);
     const int cap = C::cap(stage);
     const int marks = stage == C::K ? 0 : (C::AREA + C::NT - 1) / C::NT * C::NT * 2;
-    return cap * WI * 4 + (prune ? cap * 4 : 0) + marks + round_un<C>(cap) +
-           2 * (2 * NS + 1) * 4 + 2 * C::NB * 4 + 256;
+    return (cap * WI + 3) / 4 * 16 + (prune ? cap * 6 : 0) + marks + round_un<C>(cap) + 3 * C::NB * 4 + 512;
 }
 // Depth-1 duplicate pruning wherever its signatures fit next to the full rows.
 template <class C> constexpr bool round_prunes(int stage) {
     return stage >= 2 && round_lds<C>(stage, true) <= 160 * 1024;
 }
 
-// Parent references. A stage-s row (s >= 1) at global slot g = d*AREA + t stores
-// F = (j << 16) | i: it was made in round s by workgroup d (= g / AREA, implied by the slot)
-// from its LDS rows i and j. Round s also records its gather map M_s[d*AREA + r] = global
-// slot (stage s-1) of LDS row r, so the index tree is walked as
-// slot -> (d, F) -> (d,i,j) -> M -> parent slots. Stage-0 F holds leaf indices.
-__device__ __forceinline__ uint64_t pack_tri(uint32_t d, uint32_t i, uint32_t j) {
-    return ((uint64_t)d << 32) | (j << 16) | i;
-}
-// 2 x 16-bit signature of a row's parents for depth-1 duplicate pruning: each half is the
-// parent's LDS row (13 bits) plus 3 bits of the producing workgroup. A half shared by two rows
-// is confirmed exactly by comparing the full producing workgroups (from the run table): a
-// signature-only prune would drop ~1e-4 of all pairs, ~6% of the solutions (511 pairs each).
-__device__ __forceinline__ uint32_t parent_sig(uint32_t d, uint32_t f) {
-    const uint32_t i = f & 0x1fff, j = (f >> 16) & 0x1fff;
-    return ((i | ((d & 7) << 13)) << 16) | (j | ((d & 7) << 13));
-}
-
-// Row I/O of W dwords at a dword-aligned byte offset through a buffer descriptor: one
-// 16-byte access plus a remainder (dword-aligned 16-byte buffer accesses are legal on gfx950).
-template <int W> __device__ __forceinline__ void row_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t* o) {
-    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-    typedef uint32_t u3 __attribute__((ext_vector_type(3)));
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    if constexpr (W >= 4) {
-        const u4 x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
-        o[0] = x.x, o[1] = x.y, o[2] = x.z, o[3] = x.w;
-        row_load<W - 4>(rs, off + 16, o + 4);
-    } else if constexpr (W == 3) {
-        const u3 x = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
-        o[0] = x.x, o[1] = x.y, o[2] = x.z;
-    } else if constexpr (W == 2) {
-        const u2 x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
-        o[0] = x.x, o[1] = x.y;
-    } else if constexpr (W == 1) {
-        o[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
-    }
-}
-template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint32_t* v) {
-    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-    typedef uint32_t u3 __attribute__((ext_vector_type(3)));
-    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
-    if constexpr (W >= 4) {
-        const u4 x = {v[0], v[1], v[2], v[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
-        row_store<W - 4>(rs, off + 16, v + 4);
-    } else if constexpr (W == 3) {
-        const u3 x = {v[0], v[1], v[2]};
-        __builtin_amdgcn_raw_buffer_store_b96(x, rs, off, 0, 0);
-    } else if constexpr (W == 2) {
-        const u2 x = {v[0], v[1]};
-        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, 0);
-    } else if constexpr (W == 1) {
-        __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, 0);
-    }
-}
-
 // STAGE < K: collision round producing stage-STAGE rows. STAGE == K: final round.
-// Bucket bk = nonce*NB + d holds the stage STAGE-1 rows whose top digit bits are d; it becomes
-// output area d of stage STAGE.
+// Bucket bk = nonce*NB + d holds the stage STAGE-1 rows whose top digit bits are d (area d of
+// that stage, CTRin[bk] rows).
 //
 // The kernel is PERSISTENT and software-pipelined: one workgroup per CU walks buckets
 // blockIdx.x, +gridDim.x, ... While it collides bucket b out of LDS, the rows of its next
-// bucket are already in flight into VGPRs (plain loads are not drained by a bare barrier),
-// and the run table of the bucket after that is in flight too. Per bucket:
-//   A. commit: prefetched rows (VGPRs) -> LDS rows (+ parent signatures when pruning);
-//   B. run table of the NEXT bucket from its prefetched CNT/OFF column (exclusive scan);
-//      fetch the run table of the bucket after it (registers, not waited for);
-//   C. slot map of the next bucket (16 lanes per run) -> gather map M; issue its row loads,
-//      one lane per row, 16-byte buffer loads (not waited for);
-//   D. collide bucket b: counting sort of the rows by their RB bits, atomic-free pair
-//      enumeration (scan + max-scan, one lane per pair; depth-1 pruning), counting sort of the
-//      pairs by destination, one-lane-per-row emit (XOR, shift one digit, 16-byte stores) in
-//      slot order + one column of CNT/OFF.
+// bucket are in flight into VGPRs (16-byte lane-flat loads of the contiguous area, issued in
+// slices across the phases; plain loads are not drained by a bare barrier). Per bucket:
+//   A. commit: prefetched words (VGPRs) -> LDS rows (+ parent signatures when pruning);
+//      issue the first slice of the next bucket's loads;
+//   D1. counting sort of the rows by their RB bits;
+//   D2. atomic-free pair enumeration (scan + max-scan, one lane per pair; depth-1 pruning);
+//   D3. destination histogram -> one atomicAdd per destination bucket claims this bucket's
+//       runs there; counting sort of the pairs by destination;
+//   D4. one-lane-per-row emit (XOR, shift one digit, 16-byte stores) into the claimed runs,
+//       plus the parent triples.
 template <class C, int STAGE, bool STAMP>
-__global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ Fin,
-                                                  const uint32_t* __restrict__ CNTin,
-                                                  const uint32_t* __restrict__ OFFin, uint32_t* __restrict__ Rout,
-                                                  uint32_t* __restrict__ Fout, uint32_t* __restrict__ CNTout,
-                                                  uint32_t* __restrict__ OFFout, uint32_t* __restrict__ Mout,
+__global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ Rin, const uint64_t* __restrict__ Pin,
+                                                  const uint32_t* __restrict__ CTRin, uint32_t* __restrict__ Rout,
+                                                  uint64_t* __restrict__ Pout, uint32_t* __restrict__ CTRout,
                                                   uint32_t* __restrict__ ncand, uint64_t* __restrict__ cand,
                                                   uint64_t* __restrict__ stamps, uint32_t* __restrict__ pdrop,
                                                   int nbk) {
     constexpr int WI = C::words(STAGE - 1);
     constexpr int WO = (STAGE < C::K) ? C::words(STAGE) : 1;
-    constexpr int NS = C::nsrc(STAGE - 1);
     constexpr int CAP = C::cap(STAGE);                        // LDS rows / pair-list entries
-    constexpr int SSTRIDE = (STAGE == 1) ? C::RPW : C::AREA; // slots per source area
     constexpr bool FINAL = STAGE == C::K;
     constexpr bool PRUNE = round_prunes<C>(STAGE);
     static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024, "round LDS budget");
     constexpr int NT = C::NT;
-    static_assert(NS <= NT, "one run-table entry per lane");
-    constexpr int RPL = (CAP + NT - 1) / NT; // prefetched rows per lane
-    // `un` is the phase-D union described at round_un().
-    __shared__ uint32_t rows[CAP * WI];
-    __shared__ uint32_t psig[PRUNE ? CAP : 1];
+    constexpr int NV = (CAP * WI + 4 * NT - 1) / (4 * NT); // 16-byte prefetch vectors per lane
+    constexpr int RPL = (CAP + NT - 1) / NT;                // prefetched parent triples per lane
+    constexpr int SL = (NV + 3) / 4;                        // prefetch slice (vectors per phase)
     constexpr int MP = FINAL ? 1 : (C::AREA + NT - 1) / NT; // pairs per lane (registers)
-    constexpr int MPR = (CAP + NT - 1) / NT;                  // LDS rows per lane (scans)
+    constexpr int MPR = (CAP + NT - 1) / NT;                 // LDS rows per lane (scans)
+    __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
+    __shared__ uint32_t psig[PRUNE ? CAP : 1];
+    __shared__ uint16_t pdw[PRUNE ? CAP : 1];                 // producing bucket of each row
     __shared__ uint16_t pmark[FINAL ? 1 : MP * NT];           // pair index -> first sorted position
     __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(CAP)];
-    __shared__ uint32_t rpos[2][NS + 1], rsrc[2][NS], hist[C::NB], cur[C::NB];
+    __shared__ uint32_t hist[C::NB], cur[C::NB], base[C::NB];
     __shared__ uint32_t wsum[C::NW + 1];
-    uint32_t* gslot = reinterpret_cast<uint32_t*>(un);
     uint16_t* sidx = reinterpret_cast<uint16_t*>(un);
     uint32_t* bend = reinterpret_cast<uint32_t*>(un + un_walk_bend<C>(CAP));
     uint16_t* offp = reinterpret_cast<uint16_t*>(un + un_walk_offp<C>(CAP));
+    uint32_t* spair = reinterpret_cast<uint32_t*>(un);
     const int tid = threadIdx.x;
     const int G = gridDim.x;
     int bk = blockIdx.x;
     if (bk >= nbk) return; // uniform per workgroup
 
-    uint32_t rt_cnt = 0, rt_off = 0; // run-table entry `tid` of a bucket two steps ahead
-    auto rt_fetch = [&](int bb) {
-        if (bb < nbk && tid < NS) {
-            const size_t at = (size_t)(bb / C::NB) * C::NB * NS + (size_t)(bb % C::NB) * NS + tid;
-            rt_cnt = CNTin[at];
-            rt_off = OFFin[at];
-        }
-    };
-    auto rt_commit = [&](int p) -> uint32_t {
-        if (tid < NS) {
-            rpos[p][tid] = rt_cnt;
-            rsrc[p][tid] = rt_off;
-        }
-        __syncthreads();
-        const uint32_t total = block_exscan<NT>(rpos[p], NS, wsum);
-        if (tid == 0) rpos[p][NS] = total;
-        __syncthreads();
-        return min(total, (uint32_t)CAP);
-    };
     // A thread id the compiler cannot see through: keeps the per-lane index math of the
     // prefetch/commit loops from being hoisted out of the persistent loop (live invariants
     // would otherwise push the prefetched rows out to scratch).
@@ -435,133 +390,90 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
         return t;
     };
-    uint32_t v[RPL][WI];
-    uint32_t f[PRUNE ? RPL : 1], fd[PRUNE ? RPL : 1]; // parent refs + producing workgroup
-    uint32_t so[RPL];                                  // slots of the next bucket's rows
-    int pf_nonce = 0, pf_d = 0;
+    u4v nx[NV];
+    uint64_t nf[PRUNE ? RPL : 1];
+    int pf_bk = bk;
     uint32_t pf_n = 0;
-    auto prefetch = [&](int bb, int p, uint32_t nn) {
-        const int nonce = bb / C::NB, d = bb % C::NB;
-        { // slot of every LDS row: 16 lanes per run, 4 runs per wave instruction
-            const int lane = tid & 63, wid = tid >> 6, sub = lane >> 4, l16 = lane & 15;
-            for (int b0 = wid * 4; b0 < NS; b0 += C::NW * 4) {
-                const int b = b0 + sub;
-                if (b < NS) {
-                    const uint32_t p0 = rpos[p][b];
-                    const uint32_t len = rpos[p][b + 1] - p0;
-                    const uint32_t s0 = b * SSTRIDE + rsrc[p][b];
-                    for (uint32_t j = l16; j < len && p0 + j < nn; j += 16) gslot[p0 + j] = s0 + j;
+    // Issue prefetch vectors [u0, u1) of bucket pf_bk (and its parent triples with the first slice).
+    auto issue = [&](int u0, int u1) {
+        const int nonce = pf_bk / C::NB, d = pf_bk % C::NB;
+        const auto rs = buf_rsrc(Rin + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::AREA * WI, CAP * WI * 4);
+        const uint32_t ot = opaque_tid();
+        const uint32_t lim = pf_n * WI;
+#pragma unroll
+        for (int u = 0; u < NV; ++u) {
+            if (u < u0 || u >= u1) continue;
+            const uint32_t k = 4 * (ot + u * NT);
+            if (k < lim) nx[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 4, 0, 0);
+        }
+        if constexpr (PRUNE) {
+            if (u0 == 0) {
+                const auto rp = buf_rsrc(Pin + (size_t)nonce * C::ROWS + (size_t)d * C::AREA, CAP * 8);
+#pragma unroll
+                for (int u = 0; u < RPL; ++u) {
+                    const uint32_t r = ot + u * NT;
+                    if (r < pf_n) {
+                        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rp, r * 8, 0, 0);
+                        nf[u] = ((uint64_t)x.y << 32) | x.x;
+                    }
                 }
             }
         }
-        __syncthreads();
-        EH_STAMP(8);
-        // buffer loads: 32-bit lane offsets against a per-nonce descriptor keep the address
-        // math out of the VGPRs that hold the prefetched rows across phase D
-        const auto rsrc_rows = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(Rin + (size_t)nonce * C::ROWS * C::WMAX), 0, C::ROWS * C::WMAX * 4, 0x00020000);
-        const auto rsrc_refs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(Fin + (size_t)nonce * C::ROWS),
-                                                                 0, C::ROWS * 4, 0x00020000);
-        const uint32_t ot = opaque_tid();
-#pragma unroll
-        for (int u = 0; u < RPL; ++u) {
-            const uint32_t r = ot + u * NT;
-            so[u] = (r < nn) ? gslot[r] : 0u; // clamped to a valid slot: loads are unconditional
-        }
-        pf_nonce = nonce;
-        pf_d = d;
-        pf_n = nn;
-    };
-    // Gather map of the prefetched bucket, from the slots held in registers: written late in
-    // phase D, where its stores do not compete with the prefetch loads for the CU's queue.
-    auto write_map = [&]() {
-        uint32_t* mrow = Mout + (size_t)pf_nonce * C::ROWS + (size_t)pf_d * C::AREA;
-        const uint32_t ot = opaque_tid();
-#pragma unroll
-        for (int u = 0; u < RPL; ++u) {
-            const uint32_t r = ot + u * NT;
-            if (r < pf_n) mrow[r] = so[u];
-        }
-    };
-    // Issue the prefetch loads of rows [U0, U1) of every lane. The loads of one bucket are
-    // issued in slices spread over phase D: a wave that issues the whole bucket at once stalls
-    // at issue once the CU's outstanding-request window is full, and the barrier after it
-    // then holds every other wave too.
-    auto issue = [&](int u0, int u1) {
-        const auto rsrc_rows = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(Rin + (size_t)pf_nonce * C::ROWS * C::WMAX), 0, C::ROWS * C::WMAX * 4, 0x00020000);
-        const auto rsrc_refs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<uint32_t*>(Fin + (size_t)pf_nonce * C::ROWS), 0, C::ROWS * 4, 0x00020000);
-#pragma unroll
-        for (int u = 0; u < RPL; ++u) {
-            if (u < u0 || u >= u1) continue;
-            row_load<WI>(rsrc_rows, so[u] * (WI * 4), v[u]);
-            if constexpr (PRUNE) {
-                f[u] = __builtin_amdgcn_raw_buffer_load_b32(rsrc_refs, so[u] * 4, 0, 0);
-                fd[u] = so[u] / C::AREA;
-            }
-        }
     };
 
-    // prologue: run table of the first bucket, prefetch its rows, fetch the second run table
-    int pb = 0;
-    rt_fetch(bk);
-    uint32_t n = rt_commit(0);
-    rt_fetch(bk + G);
-    prefetch(bk, 0, n);
-    issue(0, RPL);
-    write_map();
-    __syncthreads();
+    // prologue: first bucket in flight, fill of the second known
+    uint32_t n = min(CTRin[bk], (uint32_t)CAP);
+    pf_n = n;
+    issue(0, NV);
+    uint32_t fill_next = (bk + G < nbk) ? CTRin[bk + G] : 0u;
 
     for (;;) {
         const int nonce = bk / C::NB, d = bk % C::NB;
-        const size_t matout = (size_t)nonce * C::NB * C::NB;
         EH_STAMP(0);
-        // A. commit the prefetched rows
+        // A. commit the prefetched bucket (lane-flat 16-byte LDS stores: conflict-free)
         {
             const uint32_t ot = opaque_tid();
+            const uint32_t lim = n * WI;
 #pragma unroll
-            for (int u = 0; u < RPL; ++u) {
-                const uint32_t r = ot + u * NT;
-                if (r < n) {
+            for (int u = 0; u < NV; ++u) {
+                const uint32_t k = 4 * (ot + u * NT);
+                if (k < lim) *reinterpret_cast<u4v*>(&rows[k]) = nx[u];
+            }
+            if constexpr (PRUNE) {
 #pragma unroll
-                    for (int w = 0; w < WI; ++w) rows[r * WI + w] = v[u][w];
-                    if constexpr (PRUNE) psig[r] = parent_sig(fd[u], f[u]);
+                for (int u = 0; u < RPL; ++u) {
+                    const uint32_t r = ot + u * NT;
+                    if (r < n) {
+                        psig[r] = parent_sig(nf[u]);
+                        pdw[r] = (uint16_t)(nf[u] >> 32);
+                    }
                 }
             }
         }
         for (int b = tid; b < C::NB; b += NT) hist[b] = 0;
+        for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
         EH_STAMP(1);
-        // B + C. next bucket: run table, slot map, row loads in flight
         const int bn = bk + G;
+        const bool more = bn < nbk; // uniform
         uint32_t nn = 0;
-        if (bn < nbk) { // uniform
-            nn = rt_commit(pb ^ 1);
-            EH_STAMP(7);
-            rt_fetch(bn + G);
-            prefetch(bn, pb ^ 1, nn);
-            issue(0, 2);
-            EH_STAMP(9);
+        if (more) {
+            nn = min(fill_next, (uint32_t)CAP);
+            pf_bk = bn;
+            pf_n = nn;
+            issue(0, SL);
+            fill_next = (bn + G < nbk) ? CTRin[bn + G] : 0u;
         }
-        const bool more = bn < nbk;
         __syncthreads();
         EH_STAMP(2);
 
-        // global slot (stage STAGE-1) of LDS row r of the current bucket, from its run table
-        auto slot_of = [&](uint32_t r) -> uint32_t {
-            const uint32_t b = run_of<NS>(rpos[pb], r);
-            return b * SSTRIDE + rsrc[pb][b] + (r - rpos[pb][b]);
-        };
         // D1. counting sort of the rows by their RB key: sidx = row ids grouped by key,
         //     bend[key] = end of the key's group
         auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WI] >> (32 - C::RB); };
-        for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
-        __syncthreads();
         for (uint32_t i = tid; i < n; i += NT) atomicAdd(&bend[key_of(i)], 1u);
         __syncthreads();
         block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
         for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
-        if (more) issue(2, 3);
+        if (more) issue(SL, 2 * SL);
         __syncthreads();
         EH_STAMP(3);
 
@@ -576,16 +488,13 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                     const uint32_t j = sidx[q];
                     if (rows[j] != ri) continue;
                     if constexpr (PRUNE) {
-                        const uint32_t si = psig[i], sj = psig[j];
-                        if ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) || (si & 0xffff) == (sj >> 16) ||
-                            (si & 0xffff) == (sj & 0xffff))
-                            if (slot_of(i) / C::AREA == slot_of(j) / C::AREA) continue;
+                        if (sig_hit(psig[i], psig[j]) && pdw[i] == pdw[j]) continue;
                     }
                     const uint32_t c = atomicAdd(&ncand[nonce], 1u);
                     if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
                 }
             }
-            if (more) issue(3, 4);
+            if (more) issue(2 * SL, NV);
         } else {
             // D2. atomic-free pair enumeration. Sorted position p pairs with every later position
             //     of its group: c_p = bend[key] - p - 1 pairs, first pair index offp[p] (exclusive
@@ -597,12 +506,11 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             // c_p is capped at 14 so every prefix fits the u16 offsets (a key group of 16+ rows is
             // ~1e-8 likely; it only loses a few pairs)
             for (uint32_t p = tid; p < n; p += NT) offp[p] = (uint16_t)min(bend[key_of(sidx[p])] - p - 1, 14u);
+            for (uint32_t k = tid; k < (uint32_t)(MP * NT); k += NT) pmark[k] = 0;
             __syncthreads();
             const uint32_t P = block_exscan<NT, MPR>(offp, (int)n, wsum);
             const uint32_t Pc = min(P, (uint32_t)(MP * NT));
             if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT);
-            for (uint32_t k = tid; k < Pc; k += NT) pmark[k] = 0;
-            __syncthreads();
             for (uint32_t p = tid; p < n; p += NT) {
                 const uint32_t o = offp[p], e = (p + 1 < n) ? offp[p + 1] : P;
                 if (e > o && o < Pc) pmark[o] = (uint16_t)p;
@@ -627,13 +535,9 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                         for (int w = 1; w < WI; ++w) keep |= rows[i * WI + w] != rows[j * WI + w];
                     }
                     if constexpr (PRUNE) {
-                        const uint32_t si = psig[i], sj = psig[j];
-                        if (keep && ((si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) ||
-                                     (si & 0xffff) == (sj >> 16) || (si & 0xffff) == (sj & 0xffff))) {
-                            // signature hit (a shared parent, or ~1e-4 by chance): parents are
-                            // shared only if both rows were made by the same workgroup
-                            if (slot_of(i) / C::AREA == slot_of(j) / C::AREA) keep = false;
-                        }
+                        // signature hit (a shared parent, or ~1e-4 by chance): parents are
+                        // shared only if both rows were made by the same bucket
+                        if (keep && sig_hit(psig[i], psig[j]) && pdw[i] == pdw[j]) keep = false;
                     }
                     if (keep) {
                         pv[u] = (j << 16) | i;
@@ -642,33 +546,27 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                     }
                 }
             }
-            if (more) issue(3, 4);
+            if (more) issue(2 * SL, 3 * SL);
             __syncthreads();
             EH_STAMP(4);
-            // D3. output runs by destination bucket: exclusive scan of the counts -> one column
-            //     of CNT/OFF; each pair then takes the next slot of its destination's run
-            for (int b = tid; b < C::NB; b += NT) cur[b] = hist[b];
-            __syncthreads();
-            const uint32_t np = block_exscan<NT>(cur, C::NB, wsum);
-            for (int b = tid; b < C::NB; b += NT) {
-                CNTout[matout + (size_t)b * C::NB + d] = hist[b];
-                OFFout[matout + (size_t)b * C::NB + d] = cur[b];
-            }
-            __syncthreads(); // every OFF column entry is read before cur[] is advanced
-            // slot -> pair table in the (now dead) walk/prefetch union
-            uint32_t* spair = reinterpret_cast<uint32_t*>(un);
-            static_assert(round_un<C>(CAP) >= C::AREA * 4, "slot table fits the union");
+            // D3. claim this bucket's runs in the destination areas (device-scope atomics whose
+            //     latency hides behind the scan and the scatter), then sort the pairs by
+            //     destination: each pair takes the next LDS slot of its destination's run
+            uint32_t myb = 0;
+            if (tid < C::NB && hist[tid]) myb = atomicAdd(&CTRout[(size_t)nonce * C::NB + tid], hist[tid]);
+            const uint32_t np = block_exscan<NT>(hist, cur, C::NB, wsum);
 #pragma unroll
             for (int u = 0; u < MP; ++u)
                 if (pv[u] != NIL) spair[atomicAdd(&cur[pd[u]], 1u)] = pv[u];
-            if (more) issue(4, RPL);
+            if (tid < C::NB) base[tid] = myb;
+            if (more) issue(3 * SL, NV);
             __syncthreads();
             EH_STAMP(5);
-            // D4. emit, one lane per output row in slot order (coalesced): XOR, shift one
-            //     digit, store
-            const auto rsrc_out = __builtin_amdgcn_make_buffer_rsrc(
-                Rout + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::AREA * WO, 0, C::AREA * WO * 4, 0x00020000);
-            uint32_t* farea = Fout + (size_t)nonce * C::ROWS + (size_t)d * C::AREA;
+            // D4. emit, one lane per output row in destination order: XOR, shift one digit,
+            //     store into the claimed run (rows past the next round's capacity are dropped)
+            constexpr uint32_t OCAP = C::cap(STAGE + 1 <= C::K ? STAGE + 1 : C::K);
+            const auto rs_out = buf_rsrc(Rout + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * WO * 4));
+            uint64_t* pout = Pout + (size_t)nonce * C::ROWS;
             for (uint32_t t = tid; t < np; t += NT) {
                 const uint32_t pr = spair[t];
                 const uint32_t i = pr & 0xffff, j = pr >> 16;
@@ -676,31 +574,31 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
 #pragma unroll
                 for (int w = 0; w < WI; ++w) x[w] = rows[i * WI + w] ^ rows[j * WI + w];
                 x[WI] = 0;
+                const uint32_t b = (x[0] >> (32 - C::DB)) & (C::NB - 1);
+                const uint32_t pos = base[b] + t - (cur[b] - hist[b]);
+                if (pos < OCAP) {
 #pragma unroll
-                for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
-                row_store<WO>(rsrc_out, t * (WO * 4), o);
-                farea[t] = pr;
+                    for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
+                    const uint32_t slot = b * C::AREA + pos;
+                    row_store<WO>(rs_out, slot * (WO * 4), o);
+                    pout[slot] = pack_tri(d, i, j);
+                }
             }
         }
-        if constexpr (FINAL) {
-            if (more) issue(4, RPL);
-        }
-        if (more) write_map();
         __syncthreads();
         EH_STAMP(6);
-        if (bn >= nbk) break;
+        if (!more) break;
         bk = bn;
         n = nn;
-        pb ^= 1;
     }
 }
 
 
 // ------------------------------------------------------------------ tree expansion
-// F: K arrays of per-stage references; M: K gather maps (M_s for round s at index s-1).
+// LEAF: stage-0 leaf index per slot; P: K-1 arrays of stage-1..K-1 parent triples.
 template <class C>
-__global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_t* __restrict__ F,
-                                                                  const uint32_t* __restrict__ M,
+__global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_t* __restrict__ LEAF,
+                                                                  const uint64_t* __restrict__ P,
                                                                   const uint32_t* __restrict__ ncand,
                                                                   const uint64_t* __restrict__ cand, int batch,
                                                                   uint32_t* __restrict__ out_idx,
@@ -719,26 +617,22 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
         dup = 0;
     }
     int cur = 0;
-    // level s: 2^(K-s) triples of round s -> 2^(K-s+1) stage-(s-1) slots
+    // level s: 2^(K-s) triples of round s -> 2^(K-s+1) stage-(s-1) slots -> their triples
     for (int s = C::K; s >= 1; --s) {
         __syncthreads();
         const uint32_t cnt = 1u << (C::K - s);
-        const uint32_t* Ms = M + (size_t)(s - 1) * batch * C::ROWS + (size_t)nonce * C::ROWS;
         if (t < 2 * cnt) {
             const uint64_t tr = tri[t >> 1];
             const uint32_t dd = (uint32_t)(tr >> 32);
             const uint32_t r = (t & 1) ? (((uint32_t)tr >> 16) & 0xffff) : ((uint32_t)tr & 0xffff);
-            buf[cur][t] = Ms[(size_t)dd * C::AREA + r];
+            buf[cur][t] = dd * C::AREA + r;
         }
         __syncthreads();
-        if (s > 1 && t < 2 * cnt) {
-            const uint32_t slot = buf[cur][t];
-            const uint32_t fr = F[(size_t)(s - 1) * batch * C::ROWS + (size_t)nonce * C::ROWS + slot];
-            tri[t] = pack_tri(slot / C::AREA, fr & 0xffff, fr >> 16);
-        }
+        if (s > 1 && t < 2 * cnt)
+            tri[t] = P[(size_t)(s - 2) * batch * C::ROWS + (size_t)nonce * C::ROWS + buf[cur][t]];
     }
     __syncthreads();
-    if (t < (uint32_t)L) buf[cur][t] = F[(size_t)nonce * C::ROWS + buf[cur][t]];
+    if (t < (uint32_t)L) buf[cur][t] = LEAF[(size_t)nonce * C::ROWS + buf[cur][t]];
     // Canonical order: at each level the subtree with the smaller first index goes left.
     for (int l = 0; l < C::K; ++l) {
         __syncthreads();
@@ -815,13 +709,10 @@ struct EquihashGpuSolver::Impl {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     DevBuf<bcpk::EhBaseState> d_states;
-    DevBuf<uint32_t> d_rows[2], d_cnt[2], d_off[2], d_maps, d_ncand, d_idx, d_valid;
-    DevBuf<uint32_t> d_refs, d_pdrop;
-    HostBuf<uint32_t> h_pdrop;
-    DevBuf<uint64_t> d_cand;
+    DevBuf<uint32_t> d_rows[2], d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop;
+    DevBuf<uint64_t> d_par, d_cand;
     HostBuf<bcpk::EhBaseState> h_states;
-    HostBuf<uint32_t> h_ncand, h_idx, h_valid, h_cnt_sample, h_cnt0;
-    size_t genwg = 0;
+    HostBuf<uint32_t> h_ncand, h_idx, h_valid, h_ctr0, h_pdrop;
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
     int inflight = 0;
@@ -841,14 +732,10 @@ struct EquihashGpuSolver::Impl {
         kstages = C::K;
         d_states.alloc(batch);
         h_states.alloc(batch);
-        for (int p = 0; p < 2; ++p) {
-            d_rows[p].alloc((size_t)batch * C::ROWS * C::WMAX);
-            const size_t m = (size_t)C::NB * std::max(C::NB, C::GENWG);
-            d_cnt[p].alloc((size_t)batch * m);
-            d_off[p].alloc((size_t)batch * m);
-        }
-        d_refs.alloc((size_t)C::K * batch * C::ROWS);
-        d_maps.alloc((size_t)C::K * batch * C::ROWS);
+        for (int p = 0; p < 2; ++p) d_rows[p].alloc((size_t)batch * C::ROWS * C::WMAX);
+        d_ctr.alloc((size_t)C::K * batch * C::NB);
+        d_leaf.alloc((size_t)batch * C::ROWS);
+        d_par.alloc((size_t)(C::K - 1) * batch * C::ROWS);
         d_ncand.alloc(batch);
         d_pdrop.alloc(C::K + 1);
         h_pdrop.alloc(C::K + 1);
@@ -858,11 +745,9 @@ struct EquihashGpuSolver::Impl {
         h_ncand.alloc(batch);
         h_idx.alloc((size_t)batch * C::MAXCAND * C::L);
         h_valid.alloc((size_t)batch * C::MAXCAND);
-        h_cnt_sample.alloc((size_t)C::K * C::NB * C::NB);
-        h_cnt0.alloc((size_t)C::NB * C::GENWG);
+        h_ctr0.alloc((size_t)C::K * C::NB);
         d_stamps.alloc((size_t)C::K * batch * C::NB * 16);
-        genwg = C::GENWG;
-        bytes = 2 * d_rows[0].n * 4 + d_refs.n * 4 + d_maps.n * 4 + 4 * d_cnt[0].n * 4 + d_idx.n * 4;
+        bytes = 2 * d_rows[0].n * 4 + d_par.n * 8 + d_leaf.n * 4 + d_ctr.n * 4 + d_idx.n * 4;
     }
 
     // Persistent round kernels: as many workgroups as fit on the device at once.
@@ -876,24 +761,22 @@ struct EquihashGpuSolver::Impl {
         return std::min(nbk, ncu * per_cu);
     }
     template <class C, int S> void launch_round(int nstates) {
-        const int pi = (S - 1) & 1, po = S & 1;
-        const uint32_t* fin = d_refs.p + (size_t)(S - 1) * batch * C::ROWS;
-        uint32_t* fout = (S < C::K) ? d_refs.p + (size_t)S * batch * C::ROWS : nullptr;
-        uint32_t* mout = d_maps.p + (size_t)(S - 1) * batch * C::ROWS;
+        const uint32_t* rin = d_rows[(S - 1) & 1].p;
+        uint32_t* rout = d_rows[S & 1].p;
+        const uint64_t* pin = S >= 2 ? d_par.p + (size_t)(S - 2) * batch * C::ROWS : nullptr;
+        uint64_t* pout = S < C::K ? d_par.p + (size_t)(S - 1) * batch * C::ROWS : nullptr;
+        const uint32_t* cin = d_ctr.p + (size_t)(S - 1) * batch * C::NB;
+        uint32_t* cout = S < C::K ? d_ctr.p + (size_t)S * batch * C::NB : nullptr;
         const int nbk = C::NB * nstates;
         if (stamp_mode) {
             uint64_t* st = d_stamps.p + (size_t)(S - 1) * batch * C::NB * 16;
             hipLaunchKernelGGL((bcpk::eh_round<C, S, true>), dim3(round_grid<C, S, true>(nbk)), dim3(C::NT), 0,
-                               stream, d_rows[pi].p, fin, d_cnt[pi].p, d_off[pi].p, d_rows[po].p, fout, d_cnt[po].p,
-                               d_off[po].p, mout, d_ncand.p, d_cand.p, st, d_pdrop.p, nbk);
+                               stream, rin, pin, cin, rout, pout, cout, d_ncand.p, d_cand.p, st, d_pdrop.p, nbk);
         } else {
             hipLaunchKernelGGL((bcpk::eh_round<C, S, false>), dim3(round_grid<C, S, false>(nbk)), dim3(C::NT), 0,
-                               stream, d_rows[pi].p, fin, d_cnt[pi].p, d_off[pi].p, d_rows[po].p, fout, d_cnt[po].p,
-                               d_off[po].p, mout, d_ncand.p, d_cand.p, nullptr, d_pdrop.p, nbk);
+                               stream, rin, pin, cin, rout, pout, cout, d_ncand.p, d_cand.p, nullptr, d_pdrop.p,
+                               nbk);
         }
-        if (debug && S < C::K)
-            BCP_HIP_CHECK(hipMemcpyAsync(h_cnt_sample.p + (size_t)S * C::NB * C::NB, d_cnt[po].p,
-                                         (size_t)C::NB * C::NB * 4, hipMemcpyDeviceToHost, stream));
     }
     template <class C, int... S> void launch_rounds(int nstates, std::integer_sequence<int, S...>) {
         (launch_round<C, S + 1>(nstates), ...);
@@ -904,7 +787,11 @@ struct EquihashGpuSolver::Impl {
                                      hipMemcpyHostToDevice, stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ncand.p, 0, batch * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_pdrop.p, 0, (C::K + 1) * sizeof(uint32_t), stream));
-        if (debug) BCP_HIP_CHECK(hipMemsetAsync(d_refs.p, 0xff, d_refs.n * sizeof(uint32_t), stream));
+        BCP_HIP_CHECK(hipMemsetAsync(d_ctr.p, 0, d_ctr.n * sizeof(uint32_t), stream));
+        if (debug) {
+            BCP_HIP_CHECK(hipMemsetAsync(d_leaf.p, 0xff, d_leaf.n * sizeof(uint32_t), stream));
+            BCP_HIP_CHECK(hipMemsetAsync(d_par.p, 0xff, d_par.n * sizeof(uint64_t), stream));
+        }
         BCP_HIP_CHECK(hipEventRecord(ev0, stream));
         // header-shaped inputs (140 B: g lands at byte 12 of the final block) take the
         // zero-message-word BLAKE2b specialisation
@@ -916,25 +803,25 @@ struct EquihashGpuSolver::Impl {
         }
         if (hdr)
             hipLaunchKernelGGL((bcpk::eh_gen<C, true>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
-                               d_states.p, d_rows[0].p, d_refs.p, d_cnt[0].p, d_off[0].p);
+                               d_states.p, d_rows[0].p, d_leaf.p, d_ctr.p);
         else
             hipLaunchKernelGGL((bcpk::eh_gen<C, false>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
-                               d_states.p, d_rows[0].p, d_refs.p, d_cnt[0].p, d_off[0].p);
-        if (debug) { // stage-0 fill per destination bucket, folded to NB x NB-shaped sums on the host
-            BCP_HIP_CHECK(hipMemcpyAsync(h_cnt0.p, d_cnt[0].p, (size_t)C::NB * C::GENWG * 4,
-                                         hipMemcpyDeviceToHost, stream));
-        }
+                               d_states.p, d_rows[0].p, d_leaf.p, d_ctr.p);
         launch_rounds<C>((int)nstates, std::make_integer_sequence<int, C::K>{});
         constexpr int EB = C::L < 64 ? 64 : C::L;
-        hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND * nstates), dim3(EB), 0, stream, d_refs.p,
-                           d_maps.p, d_ncand.p, d_cand.p, batch, d_idx.p, d_valid.p);
+        hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND * nstates), dim3(EB), 0, stream, d_leaf.p,
+                           d_par.p, d_ncand.p, d_cand.p, batch, d_idx.p, d_valid.p);
         BCP_HIP_CHECK(hipGetLastError());
         BCP_HIP_CHECK(hipEventRecord(ev1, stream));
         BCP_HIP_CHECK(
             hipMemcpyAsync(h_ncand.p, d_ncand.p, nstates * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        if (debug)
+        if (debug) { // per-stage fills of nonce 0's buckets, and pair-list overflow
+            for (int s = 0; s < C::K; ++s)
+                BCP_HIP_CHECK(hipMemcpyAsync(h_ctr0.p + (size_t)s * C::NB, d_ctr.p + (size_t)s * batch * C::NB,
+                                             C::NB * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
             BCP_HIP_CHECK(hipMemcpyAsync(h_pdrop.p, d_pdrop.p, (C::K + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                          stream));
+        }
         BCP_HIP_CHECK(hipMemcpyAsync(h_valid.p, d_valid.p, nstates * C::MAXCAND * sizeof(uint32_t),
                                      hipMemcpyDeviceToHost, stream));
         BCP_HIP_CHECK(hipMemcpyAsync(h_idx.p, d_idx.p, nstates * C::MAXCAND * C::L * sizeof(uint32_t),
@@ -979,7 +866,9 @@ const EhGpuStats& EquihashGpuSolver::Stats() const { return impl->stats; }
 void EquihashGpuSolver::SetDebug(bool on) { impl->debug = on; }
 void EquihashGpuSolver::SetStampMode(bool on) { impl->stamp_mode = on; }
 
-// Mean cycles per phase per round (diagnostic stamp builds): [stage][phase delta].
+// Mean cycles per phase per round (diagnostic stamp builds): [stage][phase delta], deltas
+// 1..6 = commit, next-bucket issue + barrier, key sort, pair enumeration, claim + pair sort, emit;
+// [0] = whole bucket.
 std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
     BCP_HIP_CHECK(hipSetDevice(impl->device));
     BCP_HIP_CHECK(hipStreamSynchronize(impl->stream));
@@ -988,20 +877,14 @@ std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
     BCP_HIP_CHECK(hipMemcpy(h.data(), impl->d_stamps.p, h.size() * 8, hipMemcpyDeviceToHost));
     std::vector<std::vector<double>> out;
     for (size_t s = 0; s < impl->kstages; ++s) {
-        std::vector<double> acc(10, 0.0);
+        std::vector<double> acc(7, 0.0);
         size_t cnt = 0;
         for (size_t wg = 0; wg < (size_t)nonces * impl->nb; ++wg) {
             const uint64_t* t = &h[s * per + wg * 16];
             if (t[0] == 0) continue;
             for (int k = 1; k < 7; ++k)
                 if (t[k] >= t[k - 1] && t[k] != 0) acc[k] += (double)(t[k] - t[k - 1]);
-            acc[0] += (double)((t[6] ? t[6] : t[3]) - t[0]);
-            // prefetch split: run-table commit | slot map | M map + load issue | barrier
-            if (t[7] && t[8] && t[9] && t[7] >= t[1] && t[8] >= t[7] && t[9] >= t[8] && t[2] >= t[9]) {
-                acc[7] += (double)(t[7] - t[1]);
-                acc[8] += (double)(t[8] - t[7]);
-                acc[9] += (double)(t[9] - t[8]);
-            }
+            acc[0] += (double)(t[6] - t[0]);
             ++cnt;
         }
         for (auto& a : acc) a = cnt ? a / cnt : 0;
@@ -1011,17 +894,18 @@ std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
 }
 void EquihashGpuSolver::ResetStats() { impl->stats = EhGpuStats(); }
 
-// Debug: parent refs F (K stages) then gather maps M (K rounds) of nonce 0 of the last batch,
-// each ROWS slots; with SetDebug(true) never-written F slots read 0xffffffff.
-std::vector<uint32_t> EquihashGpuSolver::DebugDump() {
+// Debug: nonce 0 of the last batch, K arrays of ROWS slots: stage-0 leaf indices (zero-extended),
+// then the parent triples of stages 1..K-1; with SetDebug(true) never-written slots read all-ones.
+std::vector<uint64_t> EquihashGpuSolver::DebugDump() {
     BCP_HIP_CHECK(hipSetDevice(impl->device));
     BCP_HIP_CHECK(hipStreamSynchronize(impl->stream));
     const size_t R = impl->rows, K = impl->kstages, B = impl->batch;
-    std::vector<uint32_t> out(2 * K * R);
-    for (size_t s = 0; s < K; ++s) {
-        BCP_HIP_CHECK(hipMemcpy(out.data() + s * R, impl->d_refs.p + s * B * R, R * 4, hipMemcpyDeviceToHost));
-        BCP_HIP_CHECK(hipMemcpy(out.data() + (K + s) * R, impl->d_maps.p + s * B * R, R * 4, hipMemcpyDeviceToHost));
-    }
+    std::vector<uint64_t> out(K * R);
+    std::vector<uint32_t> leaf(R);
+    BCP_HIP_CHECK(hipMemcpy(leaf.data(), impl->d_leaf.p, R * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < R; ++i) out[i] = leaf[i];
+    for (size_t s = 1; s < K; ++s)
+        BCP_HIP_CHECK(hipMemcpy(out.data() + s * R, impl->d_par.p + (s - 1) * B * R, R * 8, hipMemcpyDeviceToHost));
     return out;
 }
 size_t EquihashGpuSolver::DeviceBytes() const { return impl->bytes; }
@@ -1046,7 +930,8 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
     impl->stats.gpu_ms += ms;
     impl->stats.nonces += ns;
     if (impl->debug) {
-        // nonce 0: per stage, rows offered to each destination bucket vs its LDS capacity
+        // nonce 0: per stage, rows offered to each bucket (its fill counter) vs the LDS capacity
+        // of the round that reads it
         const size_t NB = impl->nb;
         impl->stats.stage_rows.assign(impl->kstages, 0);
         impl->stats.stage_dropped.assign(impl->kstages, 0);
@@ -1054,12 +939,9 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
         impl->stats.stage_top.assign(impl->kstages, {});
         impl->stats.pair_dropped.assign(impl->h_pdrop.p, impl->h_pdrop.p + impl->kstages + 1);
         for (size_t s = 0; s < impl->kstages; ++s) {
-            const size_t ns = s == 0 ? impl->genwg : NB;
-            const uint32_t* m = s == 0 ? impl->h_cnt0.p : impl->h_cnt_sample.p + s * NB * NB;
             std::vector<uint64_t> fills;
             for (size_t dd = 0; dd < NB; ++dd) {
-                uint64_t fill = 0;
-                for (size_t src = 0; src < ns; ++src) fill += m[dd * ns + src];
+                const uint64_t fill = impl->h_ctr0.p[s * NB + dd];
                 fills.push_back(fill);
                 impl->stats.stage_rows[s] += fill;
                 impl->stats.stage_maxfill[s] = std::max<uint64_t>(impl->stats.stage_maxfill[s], fill);

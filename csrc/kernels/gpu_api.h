@@ -64,7 +64,7 @@ public:
     const EhGpuStats& Stats() const;
     void SetDebug(bool on);   // collect per-stage bucket statistics (extra D2H copies)
     void SetStampMode(bool on); // diagnostic: launch phase-timestamped round kernels
-    std::vector<uint32_t> DebugDump(); // diagnostic: parent refs + gather maps of nonce 0
+    std::vector<uint64_t> DebugDump(); // diagnostic: leaf indices + parent triples of nonce 0
     std::vector<std::vector<double>> PhaseCycles(int nonces);
     void ResetStats();
     size_t DeviceBytes() const;

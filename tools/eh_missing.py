@@ -17,15 +17,15 @@ GEOM = {(48, 5): (8, 256), (96, 5): (128, 1280), (200, 9): (512, 5120)}  # (NB, 
 
 
 def trace_missing(dump, n, k, idx):
-    """Follow one missing solution up the GPU's tree: at each stage, find the slots holding its
-    subtrees (by parent-slot pairs) and report the first stage where one is absent."""
+    """Follow one missing solution up the GPU's tree: at each stage, find the slot holding each of
+    its subtrees (by parent-slot pairs) and report the first stage where one is absent.
+    dump: K arrays of ROWS slots: stage-0 leaf indices, then the parent triples
+    (bucket << 32 | j << 16 | i) of stages 1..K-1; never-written slots are all-ones."""
     import numpy as np
     nb, area = GEOM[(n, k)]
     rows = nb * area
     d = np.asarray(dump, dtype=np.uint64)
     F = [d[s * rows:(s + 1) * rows] for s in range(k)]
-    M = [d[(k + s) * rows:(k + s + 1) * rows] for s in range(k)]
-    # stage 0: leaf -> slot
     f0 = F[0]
     valid = f0 != 0xFFFFFFFF
     leaf_slot = {int(v): int(sl) for sl, v in zip(np.nonzero(valid)[0], f0[valid])}
@@ -35,12 +35,13 @@ def trace_missing(dump, n, k, idx):
         return
     for s in range(1, k):
         f = F[s]
-        g = np.nonzero(f != 0xFFFFFFFF)[0]
-        fi, fj = (f[g] & np.uint64(0xFFFF)).astype(np.int64), (f[g] >> np.uint64(16)).astype(np.int64)
-        dd = g.astype(np.int64) // area
-        p1 = M[s - 1][dd * area + fi]
-        p2 = M[s - 1][dd * area + fj]
-        lo, hi = np.minimum(p1, p2), np.maximum(p1, p2)
+        g = np.nonzero(f != np.uint64(0xFFFFFFFFFFFFFFFF))[0]
+        fv = f[g]
+        dd = (fv >> np.uint64(32)).astype(np.int64)
+        fi = (fv & np.uint64(0xFFFF)).astype(np.int64)
+        fj = ((fv >> np.uint64(16)) & np.uint64(0xFFFF)).astype(np.int64)
+        p1, p2 = dd * area + fi, dd * area + fj
+        lo, hi = np.minimum(p1, p2).astype(np.uint64), np.maximum(p1, p2).astype(np.uint64)
         keys = (lo << np.uint64(32)) | hi
         order = np.argsort(keys)
         sk = keys[order]
