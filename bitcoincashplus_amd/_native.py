@@ -22,7 +22,17 @@ except Exception:  # pragma: no cover - torch is part of the image
 _HERE = os.path.dirname(os.path.abspath(__file__))
 
 try:
-    native = importlib.import_module("bitcoincashplus_amd._bcpnative")
+    _alt = os.environ.get("BCP_NATIVE_PATH")
+    if _alt:  # A/B benchmarking: load another build of the same extension (tools/ab_bench.py)
+        import importlib.machinery
+        import importlib.util
+        _spec = importlib.util.spec_from_file_location(
+            "bitcoincashplus_amd._bcpnative", _alt,
+            loader=importlib.machinery.ExtensionFileLoader("bitcoincashplus_amd._bcpnative", _alt))
+        native = importlib.util.module_from_spec(_spec)
+        _spec.loader.exec_module(native)
+    else:
+        native = importlib.import_module("bitcoincashplus_amd._bcpnative")
 except ImportError as e:  # pragma: no cover
     raise ImportError(
         "bitcoincashplus_amd native extension not built: run `make -j8` in "

@@ -85,6 +85,7 @@ using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
 using Cfg48_5 = EhCfg<48, 5, 3, 256, 64, 8, 64, 256>;
 
 constexpr uint32_t NIL = 0xffffffffu;
+constexpr uint32_t OOB = 0x80000000u; // buffer offset past every descriptor's range: access dropped
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
 typedef uint32_t u3v __attribute__((ext_vector_type(3)));
 typedef uint32_t u4v __attribute__((ext_vector_type(4)));
@@ -112,9 +113,10 @@ template <bool MAX> __device__ __forceinline__ uint32_t wave_incl(uint32_t x) {
 // Block-wide exclusive sum over n (<= MAXPER*NT) values: src[i] -> dst[i] (src may be dst);
 // thread t owns `per` consecutive entries. Wave totals go through `wsum` (>= NT/64 entries);
 // every wave combines them itself, so the scan costs two barriers (the second makes dst
-// visible and frees wsum). Returns the total.
+// visible and frees wsum). Returns the total; `mine` (optional) receives the exclusive prefix of
+// the thread's first entry.
 template <int NT, int MAXPER = 4, class TS = uint32_t, class TD = TS>
-__device__ uint32_t block_exscan(const TS* src, TD* dst, int n, uint32_t* wsum) {
+__device__ uint32_t block_exscan(const TS* src, TD* dst, int n, uint32_t* wsum, uint32_t* mine = nullptr) {
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -137,6 +139,7 @@ __device__ uint32_t block_exscan(const TS* src, TD* dst, int n, uint32_t* wsum) 
     const uint32_t before = NW > 1 ? __builtin_amdgcn_readlane(ws, wid) - __builtin_amdgcn_readlane(wt, wid) : 0u;
     const uint32_t total = NW > 1 ? __builtin_amdgcn_readlane(ws, NW - 1) : __builtin_amdgcn_readlane(x, 63);
     uint32_t base = before + x - s;
+    if (mine) *mine = base;
 #pragma unroll
     for (int q = 0; q < MAXPER; ++q) {
         const int i = tid * per + q;
@@ -203,6 +206,24 @@ template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_
     }
 }
 
+// x = LDS row i XOR LDS row j (rows of WI words): 8-byte LDS reads when rows are 8-byte aligned
+// (even WI). Rows are random here, so every read is bank-conflict bound; a ds_read_b64 spreads its
+// lanes over 64 banks where a ds_read2_b32 pays two 32-bank conflict rounds.
+template <int WI> __device__ __forceinline__ void lds_row_xor(const uint32_t* rows, uint32_t i, uint32_t j, uint32_t* x) {
+    if constexpr (WI % 2 == 0) {
+        const u2v* r2 = reinterpret_cast<const u2v*>(rows);
+#pragma unroll
+        for (int w = 0; w < WI / 2; ++w) {
+            const u2v a = r2[i * (WI / 2) + w], b = r2[j * (WI / 2) + w];
+            x[2 * w] = a.x ^ b.x;
+            x[2 * w + 1] = a.y ^ b.y;
+        }
+    } else {
+#pragma unroll
+        for (int w = 0; w < WI; ++w) x[w] = rows[i * WI + w] ^ rows[j * WI + w];
+    }
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
 }
@@ -261,17 +282,17 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
     }
     __syncthreads();
     // claim the runs; the returned bases are used only after the scan and the scatter
-    uint32_t myb = 0;
+    uint32_t myb = 0, start = 0;
     if (tid < C::NB && hist[tid]) myb = atomicAdd(&CTR0[(size_t)nonce * C::NB + tid], hist[tid]);
-    block_exscan<NTG>(hist, cur, C::NB, wsum); // cur = run offsets inside this workgroup's sorted order
+    block_exscan<NTG>(hist, cur, C::NB, wsum, &start); // cur = run offsets inside this workgroup's sorted order
     for (int li = tid; li < C::RPW; li += NTG) perm[atomicAdd(&cur[dst[li]], 1u)] = (uint16_t)li;
-    if (tid < C::NB) base[tid] = myb;
+    if (tid < C::NB) base[tid] = myb - start; // sorted position t of bucket d -> run position base[d] + t
     __syncthreads();
     const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * W0 * 4));
     uint32_t* leaf = LEAF + (size_t)nonce * C::ROWS;
     for (int t = tid; t < C::RPW; t += NTG) {
         const uint32_t li = perm[t], d = dst[li];
-        const uint32_t pos = base[d] + (uint32_t)t - (cur[d] - hist[d]);
+        const uint32_t pos = base[d] + (uint32_t)t;
         if (pos < OCAP) {
             uint32_t o[W0];
 #pragma unroll
@@ -363,7 +384,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     constexpr int NT = C::NT;
     constexpr int NV = (CAP * WI + 4 * NT - 1) / (4 * NT); // 16-byte prefetch vectors per lane
     constexpr int RPL = (CAP + NT - 1) / NT;                // prefetched parent triples per lane
-    constexpr int SL = (NV + 3) / 4;                        // prefetch slice (vectors per phase)
+    constexpr int SL = (NV + 2) / 3;                        // prefetch slice (vectors per phase)
     constexpr int MP = FINAL ? 1 : (C::AREA + NT - 1) / NT; // pairs per lane (registers)
     constexpr int MPR = (CAP + NT - 1) / NT;                 // LDS rows per lane (scans)
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
@@ -395,6 +416,11 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     int pf_bk = bk;
     uint32_t pf_n = 0;
     // Issue prefetch vectors [u0, u1) of bucket pf_bk (and its parent triples with the first slice).
+    // Every vector-memory instruction of the loop body is issued unconditionally (lanes with nothing
+    // to move use an out-of-range buffer offset, which the descriptor's range check drops), so the
+    // compiler can count the outstanding operations and wait for the prefetched words with a
+    // precise vmcnt(N) instead of vmcnt(0): a vmcnt(0) at the commit would wait for the acks of the
+    // previous bucket's emit stores as well.
     auto issue = [&](int u0, int u1) {
         const int nonce = pf_bk / C::NB, d = pf_bk % C::NB;
         const auto rs = buf_rsrc(Rin + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::AREA * WI, CAP * WI * 4);
@@ -404,7 +430,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         for (int u = 0; u < NV; ++u) {
             if (u < u0 || u >= u1) continue;
             const uint32_t k = 4 * (ot + u * NT);
-            if (k < lim) nx[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, k * 4, 0, 0);
+            nx[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < lim ? k * 4 : OOB, 0, 0);
         }
         if constexpr (PRUNE) {
             if (u0 == 0) {
@@ -412,10 +438,8 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
 #pragma unroll
                 for (int u = 0; u < RPL; ++u) {
                     const uint32_t r = ot + u * NT;
-                    if (r < pf_n) {
-                        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rp, r * 8, 0, 0);
-                        nf[u] = ((uint64_t)x.y << 32) | x.x;
-                    }
+                    const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rp, r < pf_n ? r * 8 : OOB, 0, 0);
+                    nf[u] = ((uint64_t)x.y << 32) | x.x;
                 }
             }
         }
@@ -425,6 +449,18 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     uint32_t n = min(CTRin[bk], (uint32_t)CAP);
     pf_n = n;
     issue(0, NV);
+    if constexpr (!FINAL) {
+        // As many (dropped) stores as one emit issues: the compiler's wait counts at the loop head
+        // take the minimum over the entry and back edges; with these, both edges see the prefetch
+        // loads followed by MP emit store groups, so the commit waits for its loads only.
+        const auto rs_out = buf_rsrc(Rout, 0), rs_par = buf_rsrc(Pout, 0);
+        const uint32_t z[WO] = {};
+#pragma unroll
+        for (int u = 0; u < MP; ++u) { // distinct offsets: identical stores would be merged
+            row_store<WO>(rs_out, OOB + 256 * u, z);
+            __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rs_par, OOB + 256 * u, 0, 0);
+        }
+    }
     uint32_t fill_next = (bk + G < nbk) ? CTRin[bk + G] : 0u;
 
     for (;;) {
@@ -455,14 +491,11 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         EH_STAMP(1);
         const int bn = bk + G;
         const bool more = bn < nbk; // uniform
-        uint32_t nn = 0;
-        if (more) {
-            nn = min(fill_next, (uint32_t)CAP);
-            pf_bk = bn;
-            pf_n = nn;
-            issue(0, SL);
-            fill_next = (bn + G < nbk) ? CTRin[bn + G] : 0u;
-        }
+        const uint32_t nn = more ? min(fill_next, (uint32_t)CAP) : 0u;
+        pf_bk = more ? bn : bk;
+        pf_n = nn;
+        issue(0, SL); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
+        fill_next = (bn + G < nbk) ? CTRin[bn + G] : 0u;
         __syncthreads();
         EH_STAMP(2);
 
@@ -473,7 +506,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         __syncthreads();
         block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
         for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
-        if (more) issue(SL, 2 * SL);
+        issue(SL, 2 * SL);
         __syncthreads();
         EH_STAMP(3);
 
@@ -494,7 +527,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                     if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
                 }
             }
-            if (more) issue(2 * SL, NV);
+            issue(2 * SL, NV);
         } else {
             // D2. atomic-free pair enumeration. Sorted position p pairs with every later position
             //     of its group: c_p = bend[key] - p - 1 pairs, first pair index offp[p] (exclusive
@@ -510,7 +543,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             __syncthreads();
             const uint32_t P = block_exscan<NT, MPR>(offp, (int)n, wsum);
             const uint32_t Pc = min(P, (uint32_t)(MP * NT));
-            if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT);
+            if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT); // rare
             for (uint32_t p = tid; p < n; p += NT) {
                 const uint32_t o = offp[p], e = (p + 1 < n) ? offp[p + 1] : P;
                 if (e > o && o < Pc) pmark[o] = (uint16_t)p;
@@ -546,43 +579,45 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                     }
                 }
             }
-            if (more) issue(2 * SL, 3 * SL);
             __syncthreads();
             EH_STAMP(4);
             // D3. claim this bucket's runs in the destination areas (device-scope atomics whose
             //     latency hides behind the scan and the scatter), then sort the pairs by
             //     destination: each pair takes the next LDS slot of its destination's run
             uint32_t myb = 0;
-            if (tid < C::NB && hist[tid]) myb = atomicAdd(&CTRout[(size_t)nonce * C::NB + tid], hist[tid]);
-            const uint32_t np = block_exscan<NT>(hist, cur, C::NB, wsum);
+            if (tid < C::NB) myb = atomicAdd(&CTRout[(size_t)nonce * C::NB + tid], hist[tid]); // wave-uniform branch
+            issue(2 * SL, NV); // after the claim: waiting for its return then skips these loads
+            uint32_t start = 0; // thread b < NB: first LDS slot of destination b (NB <= NT: one entry each)
+            const uint32_t np = block_exscan<NT>(hist, cur, C::NB, wsum, &start);
 #pragma unroll
             for (int u = 0; u < MP; ++u)
                 if (pv[u] != NIL) spair[atomicAdd(&cur[pd[u]], 1u)] = pv[u];
-            if (tid < C::NB) base[tid] = myb;
-            if (more) issue(3 * SL, NV);
+            if (tid < C::NB) base[tid] = myb - start; // LDS slot t of destination b -> run position base[b] + t
             __syncthreads();
             EH_STAMP(5);
             // D4. emit, one lane per output row in destination order: XOR, shift one digit,
             //     store into the claimed run (rows past the next round's capacity are dropped)
             constexpr uint32_t OCAP = C::cap(STAGE + 1 <= C::K ? STAGE + 1 : C::K);
             const auto rs_out = buf_rsrc(Rout + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * WO * 4));
-            uint64_t* pout = Pout + (size_t)nonce * C::ROWS;
-            for (uint32_t t = tid; t < np; t += NT) {
-                const uint32_t pr = spair[t];
+            const auto rs_par = buf_rsrc(Pout + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 8));
+#pragma unroll
+            for (int u = 0; u < MP; ++u) { // fixed trip count, unconditional stores (see issue())
+                const uint32_t t = tid + u * NT;
+                const uint32_t pr = t < np ? spair[t] : 0u;
                 const uint32_t i = pr & 0xffff, j = pr >> 16;
                 uint32_t x[WI + 1], o[WO];
-#pragma unroll
-                for (int w = 0; w < WI; ++w) x[w] = rows[i * WI + w] ^ rows[j * WI + w];
+                lds_row_xor<WI>(rows, i, j, x);
                 x[WI] = 0;
                 const uint32_t b = (x[0] >> (32 - C::DB)) & (C::NB - 1);
-                const uint32_t pos = base[b] + t - (cur[b] - hist[b]);
-                if (pos < OCAP) {
+                const uint32_t pos = base[b] + t;
+                const bool ok = t < np && pos < OCAP;
+                const uint32_t slot = b * C::AREA + pos;
 #pragma unroll
-                    for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
-                    const uint32_t slot = b * C::AREA + pos;
-                    row_store<WO>(rs_out, slot * (WO * 4), o);
-                    pout[slot] = pack_tri(d, i, j);
-                }
+                for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
+                row_store<WO>(rs_out, ok ? slot * (WO * 4) : OOB, o);
+                const uint64_t tri = pack_tri(d, i, j);
+                const u2v tv = {(uint32_t)tri, (uint32_t)(tri >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b64(tv, rs_par, ok ? slot * 8 : OOB, 0, 0);
             }
         }
         __syncthreads();
