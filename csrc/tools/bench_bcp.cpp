@@ -8,12 +8,16 @@
 // MI355X batches (SHA256d64 batch, Merkle root, ECDSA batch verify) when a GPU is visible.
 #include <unistd.h>
 #include "consensus/merkle.h"
+#include "consensus/tx_verify.h"
 #include "consensus/merkleblock.h"
 #include "consensus/params.h"
 #include "crypto/hashes.h"
 #include "kernels/gpu_api.h"
 #include "keys/key.h"
 #include "node/coins.h"
+#include "node/miner.h"
+#include "script/sign.h"
+#include "script/standard.h"
 #include "node/sigverify.h"
 #include "node/txmempool.h"
 #include "node/validation.h"
@@ -357,6 +361,29 @@ static void GpuMerkle(State& st) {
 }
 static bench::Reg reg_GpuMerkle("GPU_MerkleRoot_1M", GpuMerkle);
 
+// Merkle roots at the sizes of real blocks: ~21k transactions fill 8 MB with 2-in/2-out P2PKH
+// spends; 1M leaves bound the largest block.
+static void MerkleBench(State& st, size_t n, bool gpuPath) {
+    if (gpuPath && !gpu::GpuAvailable()) return;
+    std::vector<unsigned char> leaves(32 * n);
+    for (size_t i = 0; i < leaves.size(); i++) leaves[i] = (unsigned char)(i * 131 + 7);
+    std::vector<uint256> v(n);
+    for (size_t i = 0; i < n; i++) memcpy(v[i].begin(), leaves.data() + 32 * i, 32);
+    while (st.KeepRunning()) {
+        bool mut = false;
+        if (gpuPath) gpu::MerkleRoot(leaves, &mut);
+        else ComputeMerkleRoot(v, &mut);
+    }
+}
+static bench::Reg reg_GpuMerkle21k("GPU_MerkleRoot_21k", [](State& st) { MerkleBench(st, 21001, true); });
+static bench::Reg reg_CpuMerkle21k("CPU_MerkleRoot_21k", [](State& st) { MerkleBench(st, 21001, false); });
+
+static void CpuSha256d64(State& st) {
+    std::vector<unsigned char> data(64 * (1 << 20), 1), out(32 * (1 << 20));
+    while (st.KeepRunning()) Sha256d64(out.data(), data.data(), 1u << 20);
+}
+static bench::Reg reg_CpuSha("CPU_SHA256d64_1M", CpuSha256d64);
+
 static void CpuMerkle(State& st) {
     std::vector<uint256> leaves(1 << 20);
     for (size_t i = 0; i < leaves.size(); i++) *(uint64_t*)leaves[i].begin() = i;
@@ -366,6 +393,144 @@ static void CpuMerkle(State& st) {
     }
 }
 static bench::Reg reg_CpuMerkle("CPU_MerkleRoot_1M", CpuMerkle);
+
+// ---- 8 MB block connect (BASELINE.md "block connect time for an 8 MB block"): a regtest chain
+// in a memory-only chainstate, 21,000 signed 2-in/2-out P2PKH transactions (42,000 FORKID
+// signatures, ~7.9 MB) in one block on top of it, then Chainstate::TestBlockValidity (CheckBlock +
+// contextual checks + ConnectBlock with every script and signature checked, nothing cached)
+// per iteration. _GPU batches the ECDSA checks on the MI355X; _CPU keeps them on the worker pool.
+namespace {
+struct BigBlockFixture {
+    std::unique_ptr<Chainstate> cs;
+    CTxMemPool pool;
+    CBlock block;
+    size_t nSigs = 0, nBytes = 0;
+    bool ok = false;
+};
+
+CBlock MakeBlock(Chainstate& cs, CTxMemPool& pool, const CScript& spk, const std::vector<CTransactionRef>& txs) {
+    BlockAssembler::Options o;
+    BlockAssembler ba(cs, &pool, o);
+    std::unique_ptr<CBlockTemplate> t = ba.CreateNewBlock(spk);
+    CBlock b = t->block;
+    unsigned extra = 0;
+    IncrementExtraNonce(&b, cs.Tip(), extra, cs.MaxBlockSize()); // BIP34 height in the coinbase
+    for (const auto& tx : txs) b.vtx.push_back(tx);
+    b.hashMerkleRoot = BlockMerkleRoot(b);
+    uint64_t tries = 1u << 24;
+    if (!SolveBlock(b, Params(), tries, false)) throw std::runtime_error("bench: SolveBlock failed");
+    return b;
+}
+
+BigBlockFixture& BigBlock() {
+    static BigBlockFixture f;
+    static bool built = false;
+    if (built) return f;
+    built = true;
+    SelectParams("regtest");
+    ChainstateOptions o;
+    o.memoryOnly = true;
+    o.useGpu = gpu::GpuAvailable();
+    o.scriptThreads = std::min(16, std::max(2, GetNumCores()));
+    f.cs.reset(new Chainstate(Params(), o));
+    std::string err;
+    if (!f.cs->InitBlockIndex(err)) throw std::runtime_error("bench: " + err);
+    f.cs->SetMempool(&f.pool);
+    CBasicKeyStore ks;
+    CKey key;
+    key.MakeNewKey(true);
+    ks.AddKey(key);
+    const CScript spk = GetScriptForDestination(key.GetPubKey().GetID());
+    const uint32_t hashType = SIGHASH_ALL | SIGHASH_FORKID;
+    const int NFAN = 24, NOUT = 1750, NTX = 21000; // 42,000 outputs
+    std::vector<CTransactionRef> coinbases;
+    auto connect = [&](const CBlock& b) {
+        bool fNew = false;
+        CValidationState st;
+        if (!f.cs->ProcessNewBlock(std::make_shared<const CBlock>(b), true, &fNew, &st)) {
+            fprintf(stderr, "height %d txs %zu size %zu cb-sigops %llu\n", f.cs->Height(), b.vtx.size(),
+                    GetSerializeSize(b, PROTOCOL_VERSION), (unsigned long long)GetSigOpCountWithoutP2SH(*b.vtx[0]));
+            throw std::runtime_error("bench: ProcessNewBlock: " + FormatStateMessage(st));
+        }
+    };
+    for (int h = 0; h < 100 + NFAN; h++) {
+        CBlock b = MakeBlock(*f.cs, f.pool, spk, {});
+        coinbases.push_back(b.vtx[0]);
+        connect(b);
+    }
+    // fan-out: NFAN matured coinbases -> NFAN * NOUT P2PKH outputs
+    std::vector<CTransactionRef> fan;
+    for (int c = 0; c < NFAN; c++) {
+        const CTransaction& cb = *coinbases[c];
+        CMutableTransaction m;
+        m.vin.resize(1);
+        m.vin[0].prevout = COutPoint(cb.GetHash(), 0);
+        const Amount each = (cb.vout[0].nValue - 100000) / NOUT;
+        for (int k = 0; k < NOUT; k++) m.vout.push_back(CTxOut(each, spk));
+        if (!SignSignature(ks, cb.vout[0].scriptPubKey, m, 0, cb.vout[0].nValue, hashType))
+            throw std::runtime_error("bench: fan-out signing failed");
+        fan.push_back(MakeTransactionRef(std::move(m)));
+    }
+    // 8 fan-out transactions per block: a P2PKH output is one sigop in 34 bytes, so an output-only
+    // block would exceed the 20,000-sigops-per-MB budget
+    for (int c0 = 0; c0 < NFAN; c0 += 8)
+        connect(MakeBlock(*f.cs, f.pool, spk, std::vector<CTransactionRef>(fan.begin() + c0, fan.begin() + c0 + 8)));
+    // the big block: NTX transactions, 2 inputs and 2 outputs each, signed on the worker pool
+    std::vector<CMutableTransaction> txs(NTX);
+    WorkerPool wp(std::min(16, std::max(2, GetNumCores())));
+    std::atomic<bool> signFail{false};
+    wp.ParallelFor(NTX, [&](size_t t) {
+        CMutableTransaction& m = txs[t];
+        Amount in = 0;
+        for (int k = 0; k < 2; k++) {
+            const size_t u = 2 * t + k;
+            const CTransaction& ft = *fan[u / NOUT];
+            m.vin.emplace_back();
+            m.vin.back().prevout = COutPoint(ft.GetHash(), (uint32_t)(u % NOUT));
+            in += ft.vout[u % NOUT].nValue;
+        }
+        m.vout.push_back(CTxOut(in / 2 - 500, spk));
+        m.vout.push_back(CTxOut(in / 2 - 500, spk));
+        for (int k = 0; k < 2; k++) {
+            const size_t u = 2 * t + k;
+            const CTxOut& prev = fan[u / NOUT]->vout[u % NOUT];
+            if (!SignSignature(ks, prev.scriptPubKey, m, k, prev.nValue, hashType)) signFail = true;
+        }
+    }, 64);
+    if (signFail) throw std::runtime_error("bench: signing failed");
+    std::vector<CTransactionRef> refs;
+    for (auto& m : txs) refs.push_back(MakeTransactionRef(std::move(m)));
+    f.block = MakeBlock(*f.cs, f.pool, spk, refs);
+    f.nSigs = 2 * (size_t)NTX;
+    f.nBytes = GetSerializeSize(f.block, PROTOCOL_VERSION);
+    f.ok = true;
+    fprintf(stderr, "# big block: %zu txs, %zu signatures, %zu bytes, on height %d\n", f.block.vtx.size(), f.nSigs,
+            f.nBytes, f.cs->Height());
+    return f;
+}
+
+void ConnectBigBlock(State& st, bool useGpu) {
+    BigBlockFixture& f = BigBlock();
+    const size_t thr = GetGpuSigThreshold();
+    SetGpuSigThreshold(useGpu ? DEFAULT_GPU_SIG_THRESHOLD : SIZE_MAX);
+    while (st.KeepRunning()) {
+        CValidationState state;
+        if (!f.cs->TestBlockValidity(state, f.block, f.cs->Tip(), false, true)) {
+            fprintf(stderr, "TestBlockValidity failed: %s\n", state.GetRejectReason().c_str());
+            exit(1);
+        }
+    }
+    SetGpuSigThreshold(thr);
+}
+} // namespace
+
+static void ConnectBlock8MB_CPU(State& st) { ConnectBigBlock(st, false); }
+static void ConnectBlock8MB_GPU(State& st) {
+    if (!gpu::GpuAvailable()) return;
+    ConnectBigBlock(st, true);
+}
+BENCHMARK(ConnectBlock8MB_CPU);
+BENCHMARK(ConnectBlock8MB_GPU);
 
 int main(int argc, char* argv[]) {
     gArgs.ParseParameters(argc, argv);
