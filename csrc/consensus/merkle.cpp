@@ -7,7 +7,9 @@
 
 namespace bcp {
 
-static std::atomic<size_t> g_gpu_merkle_threshold{(size_t)-1};
+// Blocks with at least this many transactions hash their merkle tree on the GPU when one is
+// visible: 0.18 ms vs 11 ms on one CPU core at 21k leaves (profiles/block_connect_r2.md).
+static std::atomic<size_t> g_gpu_merkle_threshold{2048};
 void SetGpuMerkleThreshold(size_t n) { g_gpu_merkle_threshold = n; }
 
 // One level: pairs (2i, 2i+1), odd tail duplicated. The tail pair is "impure" if its right
@@ -41,9 +43,13 @@ uint256 ComputeMerkleRoot(const std::vector<uint256>& leaves, bool* mutated) {
         std::vector<unsigned char> flat(leaves.size() * 32);
         for (size_t i = 0; i < leaves.size(); ++i) memcpy(&flat[32 * i], leaves[i].begin(), 32);
         bool mut = false;
-        std::vector<unsigned char> root = gpu::MerkleRoot(flat, &mut);
-        if (mutated) *mutated = mut;
-        return uint256(root);
+        try {
+            std::vector<unsigned char> root = gpu::MerkleRoot(flat, &mut);
+            if (mutated) *mutated = mut;
+            return uint256(root);
+        } catch (const std::exception&) {
+            // a device error must not decide validity: recompute on the CPU
+        }
     }
     return MerkleLevels(leaves, mutated);
 }

@@ -112,12 +112,20 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
     if (checks.empty()) return true;
     SignatureCache& cache = GetSignatureCache();
     std::vector<uint256> entries(checks.size());
+    std::vector<uint8_t> hit(checks.size());
     std::vector<size_t> todo;
     todo.reserve(checks.size());
     uint64_t hits = 0;
-    for (size_t i = 0; i < checks.size(); i++) {
+    // cache keys are one SHA-256 each: on the pool (the cache takes concurrent lookups)
+    auto probe = [&](size_t i) {
         entries[i] = cache.Entry(checks[i].sighash, checks[i].sig, checks[i].pubkey);
-        if (cache.Get(entries[i], cacheErase)) hits++;
+        hit[i] = cache.Get(entries[i], cacheErase);
+    };
+    if (pool && checks.size() >= 1024) pool->ParallelFor(checks.size(), probe, 256);
+    else
+        for (size_t i = 0; i < checks.size(); i++) probe(i);
+    for (size_t i = 0; i < checks.size(); i++) {
+        if (hit[i]) hits++;
         else todo.push_back(i);
     }
     bool ok = true;

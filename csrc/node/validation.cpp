@@ -13,6 +13,7 @@
 #include "util/strencodings.h"
 
 #include <algorithm>
+#include <thread>
 #include <deque>
 #include <unistd.h>
 #include <cassert>
@@ -232,12 +233,31 @@ bool Chainstate::CheckBlock(const CBlock& block, CValidationState& state, bool f
                                        state.GetDebugMessage().c_str()));
     uint64_t nSigOps = 0;
     const uint64_t nMaxSigOpsCount = GetMaxBlockSigOpsCount(currentBlockSize);
-    for (size_t i = 0; i < block.vtx.size(); i++) {
+    // Large blocks: the per-transaction checks run on the pool, then an in-order scan reports
+    // the first failure exactly as the serial loop would (re-running that transaction's check
+    // for its reject reason).
+    const size_t ntx = block.vtx.size();
+    std::vector<uint32_t> txSigOps;
+    std::vector<uint8_t> txOk;
+    if (pool && ntx >= 512) {
+        txSigOps.resize(ntx);
+        txOk.assign(ntx, 1);
+        pool->ParallelFor(
+            ntx,
+            [&](size_t i) {
+                const CTransaction& tx = *block.vtx[i];
+                txSigOps[i] = (uint32_t)GetSigOpCountWithoutP2SH(tx);
+                CValidationState st;
+                if (i > 0 && !CheckRegularTransaction(tx, st, false)) txOk[i] = 0;
+            },
+            64);
+    }
+    for (size_t i = 0; i < ntx; i++) {
         const CTransaction& tx = *block.vtx[i];
-        nSigOps += GetSigOpCountWithoutP2SH(tx);
+        nSigOps += txSigOps.empty() ? GetSigOpCountWithoutP2SH(tx) : txSigOps[i];
         if (nSigOps > nMaxSigOpsCount)
             return state.DoS(100, false, REJECT_INVALID, "bad-blk-sigops", false, "out-of-bounds SigOpCount");
-        if (i > 0 && !CheckRegularTransaction(tx, state, false))
+        if (i > 0 && (txOk.empty() || !txOk[i]) && !CheckRegularTransaction(tx, state, false))
             return state.Invalid(false, state.GetRejectCode(), state.GetRejectReason(),
                                  strprintf("Transaction check failed (txid %s) %s", tx.GetHash().ToString().c_str(),
                                            state.GetDebugMessage().c_str()));
@@ -697,12 +717,65 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     std::vector<std::pair<uint256, CDiskTxPos>> vPos;
     vPos.reserve(block.vtx.size());
     blockundo.vtxundo.reserve(block.vtx.size() - 1);
-    std::vector<std::unique_ptr<PrecomputedTransactionData>> txdatas(block.vtx.size());
-    std::vector<ScriptJob> jobs;
-    std::vector<uint256> scriptCacheKeys;
+    const size_t ntx = block.vtx.size();
     ScriptCache& sc = GetScriptCache();
 
-    for (size_t i = 0; i < block.vtx.size(); i++) {
+    // Per-transaction work that needs no coins runs on the pool first: the BIP143-style sighash
+    // midstates (PrecomputedTransactionData), the script-cache key and the serialized size.
+    std::vector<std::unique_ptr<PrecomputedTransactionData>> txdatas(ntx);
+    std::vector<uint256> scKeys(ntx);
+    std::vector<uint32_t> txSizes(ntx);
+    size_t maxJobs = 0;
+    for (size_t i = 1; i < ntx; i++) maxJobs += block.vtx[i]->vin.size();
+    pool->ParallelFor(
+        ntx,
+        [&](size_t i) {
+            const CTransaction& tx = *block.vtx[i];
+            txSizes[i] = (uint32_t)GetSerializeSize(tx, PROTOCOL_VERSION);
+            if (i == 0 || !fScriptChecks) return;
+            scKeys[i] = sc.Key(tx, flags);
+            txdatas[i].reset(new PrecomputedTransactionData(tx));
+        },
+        64);
+
+    // Script checks overlap the UTXO pass (reference CCheckQueue: the master keeps connecting
+    // while workers run the queued CScriptChecks, src/validation.cpp:2011-2127). The loop below
+    // publishes jobs into a pre-sized array; the pool's threads (driven from a helper thread, the
+    // ParallelFor caller) execute them as they appear, deferring every ECDSA check into a
+    // per-job sink for the batch verifier.
+    std::vector<ScriptJob> jobs(maxJobs);
+    std::vector<std::vector<DeferredSigCheck>> sinks(maxJobs);
+    std::atomic<size_t> nProduced{0}, nextJob{0};
+    std::atomic<bool> doneProducing{false}, anyFail{false};
+    auto runJobs = [&](size_t) {
+        for (;;) {
+            const size_t k = nextJob.fetch_add(1, std::memory_order_relaxed);
+            while (k >= nProduced.load(std::memory_order_acquire)) {
+                if (doneProducing.load(std::memory_order_acquire) && k >= nProduced.load(std::memory_order_acquire))
+                    return;
+                std::this_thread::yield();
+            }
+            if (anyFail.load(std::memory_order_relaxed)) continue;
+            const ScriptJob& J = jobs[k];
+            BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k]);
+            ScriptError err;
+            if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, J.scriptPubKey, flags, checker, &err)) anyFail = true;
+        }
+    };
+    std::thread scriptThread;
+    if (fScriptChecks && maxJobs > 0)
+        scriptThread = std::thread([&]() { pool->ParallelFor((size_t)pool->Size(), runJobs, 1); });
+    // every return below stops and joins the script workers first
+    struct JoinOnExit {
+        std::atomic<bool>& done;
+        std::thread& th;
+        ~JoinOnExit() {
+            done.store(true, std::memory_order_release);
+            if (th.joinable()) th.join();
+        }
+    } joinOnExit{doneProducing, scriptThread};
+
+    for (size_t i = 0; i < ntx; i++) {
         const CTransaction& tx = *block.vtx[i];
         nInputs += (int)tx.vin.size();
         if (!tx.IsCoinBase()) {
@@ -726,15 +799,15 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
                 return error("ConnectBlock(): CheckTxInputs on %s failed with %s", tx.GetHash().ToString().c_str(),
                              FormatStateMessage(state).c_str());
             if (fScriptChecks) {
-                const uint256 key = sc.Key(tx, flags);
                 // transactions fully validated under these flags in the mempool skip re-execution
-                if (!sc.Has(key, !fJustCheck)) {
-                    txdatas[i].reset(new PrecomputedTransactionData(tx));
+                if (!sc.Has(scKeys[i], !fJustCheck)) {
+                    size_t n = nProduced.load(std::memory_order_relaxed);
                     for (size_t j = 0; j < tx.vin.size(); j++) {
                         const Coin& coin = view.AccessCoin(tx.vin[j].prevout);
-                        jobs.push_back(ScriptJob{&tx, (unsigned)j, coin.GetTxOut().scriptPubKey, coin.GetTxOut().nValue,
-                                                 txdatas[i].get()});
+                        jobs[n + j] = ScriptJob{&tx, (unsigned)j, coin.GetTxOut().scriptPubKey, coin.GetTxOut().nValue,
+                                                txdatas[i].get()};
                     }
+                    nProduced.store(n + tx.vin.size(), std::memory_order_release);
                 }
             }
         }
@@ -750,7 +823,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
         }
         AddCoins(view, tx, pindex->nHeight);
         vPos.push_back(std::make_pair(tx.GetHash(), pos));
-        pos.nTxOffset += (unsigned)GetSerializeSize(tx, PROTOCOL_VERSION);
+        pos.nTxOffset += txSizes[i];
     }
     const int64_t nTime2 = GetTimeMicros();
 
@@ -761,32 +834,19 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
                                (long long)block.vtx[0]->GetValueOut(), (long long)blockReward),
                          REJECT_INVALID, "bad-cb-amount");
 
-    // ---- scripts on the CPU pool, ECDSA batched (GPU when large enough)
-    if (!jobs.empty()) {
-        std::vector<std::vector<DeferredSigCheck>> sinks(jobs.size());
-        std::vector<uint8_t> scriptOk(jobs.size(), 1);
-        std::atomic<bool> anyFail{false};
-        pool->ParallelFor(
-            jobs.size(),
-            [&](size_t k) {
-                if (anyFail.load(std::memory_order_relaxed)) return;
-                const ScriptJob& J = jobs[k];
-                BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k]);
-                ScriptError err;
-                if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, J.scriptPubKey, flags, checker, &err)) {
-                    scriptOk[k] = 0;
-                    anyFail = true;
-                }
-            },
-            4);
+    // ---- remaining scripts, then one ECDSA batch (GPU when large enough)
+    doneProducing.store(true, std::memory_order_release);
+    if (scriptThread.joinable()) scriptThread.join();
+    const size_t nJobs = nProduced.load();
+    if (nJobs > 0) {
         bool ok = !anyFail.load();
         if (ok) {
             size_t total = 0;
-            for (auto& s : sinks) total += s.size();
+            for (size_t k = 0; k < nJobs; k++) total += sinks[k].size();
             std::vector<DeferredSigCheck> all;
             all.reserve(total);
-            for (auto& s : sinks)
-                for (auto& c : s) all.push_back(std::move(c));
+            for (size_t k = 0; k < nJobs; k++)
+                for (auto& c : sinks[k]) all.push_back(std::move(c));
             ok = BatchVerifySignatures(all, pool.get(), opts.useGpu, false, !fJustCheck);
         }
         // Before the fork script failures do not invalidate blocks (reference validation.cpp:2121-2126).
@@ -795,7 +855,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     }
     const int64_t nTime4 = GetTimeMicros();
     LogPrint(BCLog::BENCH, "    - Connect %u txs (%d inputs, %zu script jobs): %.2fms, verify %.2fms\n",
-             (unsigned)block.vtx.size(), nInputs, jobs.size(), 0.001 * (nTime2 - nTimeStart), 0.001 * (nTime4 - nTime2));
+             (unsigned)block.vtx.size(), nInputs, nJobs, 0.001 * (nTime2 - nTimeStart), 0.001 * (nTime4 - nTime2));
     if (fJustCheck) return true;
 
     if (pindex->GetUndoPos().IsNull() || !pindex->IsValid(BLOCK_VALID_SCRIPTS)) {

@@ -51,7 +51,7 @@ def test_sha256d_batch(native):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 13, 100, 1000, 4097])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 8, 13, 100, 1000, 1024, 1025, 2047, 4097, 21001])
 def test_merkle_root(native, n):
     leaves = [os.urandom(32) for _ in range(n)]
     root, mut = native.merkle_root_gpu(b"".join(leaves))
@@ -67,6 +67,10 @@ def test_merkle_mutation(native):
     r1, m1 = native.merkle_root_gpu(b"".join([a, b, c]))
     r2, m2 = native.merkle_root_gpu(b"".join([a, b, c, c]))
     assert r1 == r2 and not m1 and m2
+    # the same in a tree deep enough to go through the wide levels and the one-workgroup tail
+    big = [os.urandom(32) for _ in range(3001)]
+    for leaves in (big, big + [big[-1]], big[:2048] + big[:2048]):
+        assert native.merkle_root_gpu(b"".join(leaves)) == merkle_ref(leaves)
 
 
 @pytest.mark.gpu
