@@ -5,6 +5,7 @@
 #include "consensus/params.h"
 #include "consensus/versionbits.h"
 #include "kernels/gpu_api.h"
+#include "node/miner.h"
 #include "node/node.h"
 #include "node/policy.h"
 #include "node/sigverify.h"
@@ -49,6 +50,7 @@ std::string HelpMessage() {
         {"-par=<n>", "Number of script verification threads (0 = auto)"},
         {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
         {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 1024)"},
+        {"-gpudevices=<list>", "Comma-separated GPU indices the built-in Equihash miner runs on, one host thread per device (default: all visible)"},
         {"-gpufaultinjection", "(testing) make every validation GPU batch fail so the CPU fallback runs (default: 0)"},
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
@@ -282,6 +284,19 @@ int AppMain(int argc, char* argv[]) {
         }
     }
     SetGpuSigThreshold((size_t)gArgs.GetArg("-gpusigthreshold", (int64_t)GetGpuSigThreshold()));
+    if (gArgs.IsArgSet("-gpudevices")) {
+        std::vector<int> devs;
+        for (const std::string& tok : SplitString(gArgs.GetArg("-gpudevices", ""), ',')) {
+            if (tok.empty()) continue;
+            int64_t d = 0;
+            if (!ParseInt64(tok, &d) || d < 0) {
+                InitError("Invalid -gpudevices entry: " + tok);
+                return 1;
+            }
+            devs.push_back((int)d);
+        }
+        SetMinerGpuDevices(devs);
+    }
     InitSignatureCache(gArgs.GetArg("-maxsigcachesize", (int64_t)DEFAULT_MAX_SIG_CACHE_SIZE));
     InitScriptExecutionCache(gArgs.GetArg("-maxscriptcachesize", (int64_t)DEFAULT_MAX_SCRIPT_CACHE_SIZE));
     SetGpuFaultInjection(gArgs.GetBoolArg("-gpufaultinjection", false));

@@ -1,4 +1,6 @@
 #include "node/miner.h"
+
+#include <thread>
 #include "consensus/equihash.h"
 #include "crypto/common.h"
 #include "consensus/merkle.h"
@@ -255,16 +257,123 @@ MinerStats GetMinerStats() {
 }
 
 namespace {
-struct GpuSolverCache {
-    std::mutex m;
-    std::unique_ptr<gpu::EquihashGpuSolver> solver;
-    unsigned n = 0, k = 0;
+// Two solvers per (device, N, K), kept across blocks: (200,9) at batch 32 holds ~9 GiB each.
+struct DeviceMiner {
+    int device;
+    unsigned n, k;
+    std::mutex busy;
+    std::unique_ptr<gpu::EquihashGpuSolver> s[2];
 };
-GpuSolverCache& SolverCache() {
-    static GpuSolverCache c;
-    return c;
+std::mutex g_devMinersMutex;
+std::vector<std::unique_ptr<DeviceMiner>> g_devMiners;
+std::vector<int> g_minerDevices;
+
+DeviceMiner& GetDeviceMiner(int device, unsigned n, unsigned k) {
+    std::lock_guard<std::mutex> l(g_devMinersMutex);
+    for (auto& d : g_devMiners)
+        if (d->device == device && d->n == n && d->k == k) return *d;
+    std::unique_ptr<DeviceMiner> d(new DeviceMiner);
+    d->device = device;
+    d->n = n;
+    d->k = k;
+    const int batch = n == 200 ? 32 : 16;
+    for (auto& s : d->s) s.reset(new gpu::EquihashGpuSolver(n, k, batch, device));
+    g_devMiners.push_back(std::move(d));
+    return *g_devMiners.back();
 }
 } // namespace
+
+void SetMinerGpuDevices(const std::vector<int>& devices) {
+    std::lock_guard<std::mutex> l(g_devMinersMutex);
+    g_minerDevices = devices;
+}
+std::vector<int> GetMinerGpuDevices() {
+    std::vector<int> d;
+    {
+        std::lock_guard<std::mutex> l(g_devMinersMutex);
+        d = g_minerDevices;
+    }
+    if (d.empty())
+        for (int i = 0; i < gpu::DeviceCount(); i++) d.push_back(i);
+    return d;
+}
+
+EhSearchResult EquihashSearchGpu(unsigned n, unsigned k, const std::vector<unsigned char>& equihashInput,
+                                 const uint256& nonce0, uint64_t maxNonces,
+                                 const std::function<bool(const uint256&, const std::vector<unsigned char>&)>& accept,
+                                 std::vector<int> devices, const std::atomic<bool>* cancel) {
+    if (devices.empty()) devices = GetMinerGpuDevices();
+    if (devices.empty()) throw std::runtime_error("EquihashSearchGpu: no GPU device");
+    const EquihashParams ep(n, k);
+    CBlake2b base = EhInitialiseState(ep);
+    base.Write(equihashInput.data(), equihashInput.size());
+    const arith_uint256 n0 = UintToArith256(nonce0);
+    std::atomic<uint64_t> next{0}, nNonces{0}, nSols{0};
+    std::atomic<bool> stop{false};
+    std::mutex resMutex;
+    EhSearchResult res;
+    std::string firstError;
+    auto worker = [&](int device) {
+        try {
+            DeviceMiner& dm = GetDeviceMiner(device, n, k);
+            std::lock_guard<std::mutex> busy(dm.busy);
+            const int B = dm.s[0]->Batch();
+            std::vector<uint256> pend[2];
+            auto launch = [&](int slot) -> bool {
+                if (stop.load() || (cancel && cancel->load())) return false;
+                const uint64_t start = next.fetch_add((uint64_t)B);
+                if (start >= maxNonces) return false;
+                const int nb = (int)std::min<uint64_t>((uint64_t)B, maxNonces - start);
+                std::vector<gpu::EhBaseState> states(nb);
+                pend[slot].resize(nb);
+                for (int b = 0; b < nb; b++) {
+                    pend[slot][b] = ArithToUint256(n0 + arith_uint256(start + 1 + (uint64_t)b));
+                    CBlake2b st = base;
+                    st.Write(pend[slot][b].begin(), 32);
+                    states[b] = gpu::MakeEhBaseState(st);
+                }
+                dm.s[slot]->Launch(states);
+                return true;
+            };
+            auto collect = [&](int slot) {
+                const auto sols = dm.s[slot]->Collect();
+                nNonces += pend[slot].size();
+                for (size_t b = 0; b < sols.size(); b++)
+                    for (const auto& idx : sols[b]) {
+                        nSols++;
+                        if (stop.load()) continue;
+                        std::vector<unsigned char> minimal = GetMinimalFromIndices(idx, ep.N / (ep.K + 1));
+                        if (!accept(pend[slot][b], minimal)) continue;
+                        std::lock_guard<std::mutex> l(resMutex);
+                        if (!res.found) {
+                            res.found = true;
+                            res.nonce = pend[slot][b];
+                            res.solution = std::move(minimal);
+                        }
+                        stop = true;
+                    }
+            };
+            bool inflight[2] = {launch(0), false};
+            for (int cur = 0;; cur ^= 1) { // launch the next batch, then decode the running one
+                inflight[cur ^ 1] = launch(cur ^ 1);
+                if (inflight[cur]) collect(cur);
+                inflight[cur] = false;
+                if (!inflight[cur ^ 1]) break;
+            }
+        } catch (const std::exception& e) {
+            std::lock_guard<std::mutex> l(resMutex);
+            if (firstError.empty()) firstError = e.what();
+            stop = true;
+        }
+    };
+    std::vector<std::thread> threads;
+    for (int d : devices) threads.emplace_back(worker, d);
+    for (auto& t : threads) t.join();
+    res.nonces = nNonces.load();
+    res.solutions = nSols.load();
+    if (!res.found && !firstError.empty()) throw std::runtime_error("EquihashSearchGpu: " + firstError);
+    return res;
+}
 
 static bool SolveLegacy(CBlock& block, const Consensus::Params& cp, uint64_t& nMaxTries, bool useGpu,
                         const std::atomic<bool>* cancel) {
@@ -341,49 +450,28 @@ static bool SolveEquihash(CBlock& block, const CChainParams& params, uint64_t& n
     };
     const bool gpuOk = useGpu && ep.N >= 96 && gpu::GpuAvailable();
     if (gpuOk) {
-        GpuSolverCache& sc = SolverCache();
-        std::lock_guard<std::mutex> l(sc.m);
-        if (!sc.solver || sc.n != ep.N || sc.k != ep.K) {
-            sc.solver.reset(new gpu::EquihashGpuSolver(ep.N, ep.K, ep.N == 200 ? 8 : 16));
-            sc.n = ep.N;
-            sc.k = ep.K;
+        const CBlockHeader hdr = block.GetBlockHeader();
+        auto accept = [&](const uint256& nonce, const std::vector<unsigned char>& soln) {
+            CBlockHeader h = hdr; // thread-safe: each candidate hashes its own copy
+            h.nNonce = nonce;
+            h.nSolution = soln;
+            return CheckProofOfWork(h.GetHash(cp), h.nBits, true, cp);
+        };
+        const int64_t t0 = GetTimeMicros();
+        const EhSearchResult r = EquihashSearchGpu(ep.N, ep.K, input, block.nNonce, nMaxTries, accept, {}, cancel);
+        {
+            std::lock_guard<std::mutex> ls(g_minerMutex);
+            g_minerStats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
+            g_minerStats.eh_nonces += r.nonces;
+            g_minerStats.eh_solutions += r.solutions;
         }
-        const int batch = sc.solver->Batch();
-        while (nMaxTries > 0) {
-            const int nb = (int)std::min<uint64_t>(nMaxTries, (uint64_t)batch);
-            std::vector<gpu::EhBaseState> states;
-            std::vector<uint256> nonces;
-            arith_uint256 nn = UintToArith256(block.nNonce);
-            for (int b = 0; b < nb; b++) {
-                nn += 1;
-                const uint256 nonce = ArithToUint256(nn);
-                CBlake2b st = base;
-                st.Write(nonce.begin(), 32);
-                states.push_back(gpu::MakeEhBaseState(st));
-                nonces.push_back(nonce);
-            }
-            const int64_t t0 = GetTimeMicros();
-            auto sols = sc.solver->Solve(states);
-            {
-                std::lock_guard<std::mutex> ls(g_minerMutex);
-                g_minerStats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
-                g_minerStats.eh_nonces += nb;
-            }
-            nMaxTries -= nb;
-            for (int b = 0; b < nb; b++) {
-                for (const auto& idx : sols[b]) {
-                    block.nNonce = nonces[b];
-                    std::vector<unsigned char> minimal = GetMinimalFromIndices(idx, ep.N / (ep.K + 1));
-                    {
-                        std::lock_guard<std::mutex> ls(g_minerMutex);
-                        g_minerStats.eh_solutions++;
-                    }
-                    if (tryState(minimal)) return true;
-                }
-            }
-            block.nNonce = nonces.back();
-            if (cancel && cancel->load()) return false;
+        nMaxTries -= std::min(nMaxTries, r.nonces);
+        if (r.found) {
+            block.nNonce = r.nonce;
+            block.nSolution = r.solution;
+            return true;
         }
+        block.nNonce = ArithToUint256(UintToArith256(block.nNonce) + arith_uint256(r.nonces));
         return false;
     }
     while (nMaxTries > 0) {

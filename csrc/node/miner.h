@@ -15,6 +15,7 @@
 #include "primitives/block.h"
 
 #include <atomic>
+#include <functional>
 #include <memory>
 
 namespace bcp {
@@ -77,6 +78,25 @@ struct MinerStats {
 bool SolveBlock(CBlock& block, const CChainParams& params, uint64_t& nMaxTries, bool useGpu,
                 const std::atomic<bool>* cancel = nullptr);
 MinerStats GetMinerStats();
+
+// Multi-GPU Equihash search (the built-in miner's post-fork path). Every selected device runs
+// two solvers double-buffered on its own host thread; nonces come from one shared counter, so the
+// devices sweep disjoint ranges nonce0+1, nonce0+2, ... (nonce-space data parallelism, SURVEY
+// §2.3). `accept` is called concurrently from the device threads for every solution found and
+// must be thread-safe; the first accepted one ends the search on all devices.
+struct EhSearchResult {
+    bool found = false;
+    uint256 nonce;                        // nonce of the accepted solution
+    std::vector<unsigned char> solution;  // minimal encoding
+    uint64_t nonces = 0, solutions = 0;   // instances solved / solutions seen (all devices)
+};
+EhSearchResult EquihashSearchGpu(unsigned n, unsigned k, const std::vector<unsigned char>& equihashInput,
+                                 const uint256& nonce0, uint64_t maxNonces,
+                                 const std::function<bool(const uint256&, const std::vector<unsigned char>&)>& accept,
+                                 std::vector<int> devices = {}, const std::atomic<bool>* cancel = nullptr);
+// -gpudevices: devices used by the miner (empty: every visible device).
+void SetMinerGpuDevices(const std::vector<int>& devices);
+std::vector<int> GetMinerGpuDevices();
 
 // generate / generatetoaddress core: mines nGenerate blocks on the active chain.
 std::vector<uint256> GenerateBlocks(Chainstate& chainstate, CTxMemPool* mempool, const CScript& coinbaseScript,

@@ -2,6 +2,7 @@
 #include "consensus/equihash.h"
 #include "kernels/gpu_api.h"
 #include "python/bind.h"
+#include "node/miner.h"
 #include "node/sigverify.h"
 #include "secp256k1/secp256k1.h"
 
@@ -99,6 +100,34 @@ void bind_gpu(pyb::module_& m) {
         .def("set_stamp_mode", &gpu::EquihashGpuSolver::SetStampMode)
         .def("debug_dump", &gpu::EquihashGpuSolver::DebugDump)
         .def("phase_cycles", &gpu::EquihashGpuSolver::PhaseCycles);
+
+    // Multi-GPU Equihash search of the built-in miner (EquihashSearchGpu) with an accept-all target:
+    // returns the first solution found in nonces nonce0+1 .. nonce0+max_nonces (little-endian
+    // 256-bit arithmetic on the 32-byte nonce).
+    m.def(
+        "eh_search_gpu",
+        [](unsigned n, unsigned k, const pyb::bytes& input, const pyb::bytes& nonce0, uint64_t maxNonces,
+           const std::vector<int>& devices) {
+            const auto in = to_vec(input), n0 = to_vec(nonce0);
+            if (n0.size() != 32) throw std::invalid_argument("nonce0 must be 32 bytes");
+            uint256 start;
+            memcpy(start.begin(), n0.data(), 32);
+            EhSearchResult r;
+            {
+                pyb::gil_scoped_release rel;
+                r = EquihashSearchGpu(n, k, in, start, maxNonces,
+                                      [](const uint256&, const std::vector<unsigned char>&) { return true; }, devices);
+            }
+            pyb::dict d;
+            d["found"] = r.found;
+            d["nonce"] = to_bytes(r.nonce.begin(), 32);
+            d["solution"] = to_bytes(r.solution.data(), r.solution.size());
+            d["nonces"] = r.nonces;
+            d["solutions"] = r.solutions;
+            return d;
+        },
+        pyb::arg("n"), pyb::arg("k"), pyb::arg("input"), pyb::arg("nonce0"), pyb::arg("max_nonces"),
+        pyb::arg("devices") = std::vector<int>{});
 
     m.def(
         "eh_verify_batch_gpu",

@@ -201,3 +201,24 @@ def test_gpu_verify_batch(native, n, k):
     assert list(got) == expect
     cpu = [native.eh_is_valid_solution(n, k, st, s)[0] for st, s in zip(states, sols)]
     assert cpu == expect
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(96, 5), (200, 9)])
+def test_gpu_miner_search(native, n, k):
+    """The built-in miner's multi-GPU search (EquihashSearchGpu): every visible device, two
+    double-buffered solvers each; the accepted solution is valid for its nonce, which lies in
+    the searched range."""
+    body = bytes((i * 7 + 3) & 0xFF for i in range(108))
+    nonce0 = (5).to_bytes(32, "little")
+    r = native.eh_search_gpu(n, k, body, nonce0, 256)
+    assert r["found"]
+    nonce = int.from_bytes(r["nonce"], "little")
+    assert 6 <= nonce <= 5 + 256
+    assert r["nonces"] >= 1 and r["solutions"] >= 1
+    st = native.EquihashState(n, k)
+    st.update(body + r["nonce"])
+    assert native.eh_is_valid_solution(n, k, st, r["solution"])[0]
+    # explicit device list, and an exhausted range reports not found
+    r0 = native.eh_search_gpu(n, k, body, nonce0, 0, [0])
+    assert not r0["found"] and r0["nonces"] == 0
