@@ -120,7 +120,7 @@ __device__ __forceinline__ void fe_mul_small(fe& r, const fe& a, uint32_t m) {
 __device__ __forceinline__ void fe_reduce512(fe& r, const uint32_t (&t)[16]);
 
 // 512-bit product reduced mod p.
-__device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) {
+__device__ __forceinline__ void fe_mul_impl(fe& r, const fe& a, const fe& b) {
     uint32_t t[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) t[i] = 0;
@@ -141,7 +141,7 @@ __device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) {
 // Squaring: the 28 cross products a_i*a_j (i<j) once, doubled with a 1-bit shift, plus the 8
 // diagonal squares — 36 32x32 multiplies instead of the 64 of fe_mul. Point doubling and the
 // inversion/sqrt ladders are mostly squarings.
-__device__ __forceinline__ void fe_sqr(fe& r, const fe& a) {
+__device__ __forceinline__ void fe_sqr_impl(fe& r, const fe& a) {
     uint32_t t[16];
 #pragma unroll
     for (int i = 0; i < 16; i++) t[i] = 0;
@@ -173,6 +173,23 @@ __device__ __forceinline__ void fe_sqr(fe& r, const fe& a) {
     }
     fe_reduce512(r, t);
 }
+
+// Out-of-line multiply and square, arguments and result in VGPRs (by value: a by-reference
+// argument of a non-inlined function would go through scratch). Inlining every field operation
+// made the verify kernel ~460 KB of straight-line code: with one wave per SIMD the instruction
+// cache, not the multipliers, set its speed.
+__device__ __noinline__ fe fe_mul_v(fe a, fe b) {
+    fe r;
+    fe_mul_impl(r, a, b);
+    return r;
+}
+__device__ __noinline__ fe fe_sqr_v(fe a) {
+    fe r;
+    fe_sqr_impl(r, a);
+    return r;
+}
+__device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) { r = fe_mul_v(a, b); }
+__device__ __forceinline__ void fe_sqr(fe& r, const fe& a) { r = fe_sqr_v(a); }
 
 // 512-bit value t (t < 2^512) reduced mod p.
 __device__ __forceinline__ void fe_reduce512(fe& r, const uint32_t (&t)[16]) {
@@ -446,22 +463,28 @@ constexpr int WG = 128;
 constexpr int WNAF_W = 4;              // odd multiples 1,3,5,7
 constexpr int NPRE = 1 << (WNAF_W - 2); // 4
 
+constexpr int GLV_DIGITS = 132; // width-4 wNAF digits of a <= 129-bit GLV half (|k1|,|k2| < 2^129)
+
 struct Job {
     unsigned char u1[32];   // big-endian scalar for the G comb
     unsigned char r[32];    // big-endian r
     unsigned char rn[32];   // big-endian r + n (valid when rplusn_ok)
     unsigned char pub[33];  // compressed key
     unsigned char rplusn_ok;
-    unsigned char wnaf[130]; // u2 as width-4 wNAF, 2 signed nibbles per byte, digit b at wnaf[b>>1]
-    unsigned char nwnaf_lo, nwnaf_hi; // number of digits
-    unsigned char scalar_ok;          // set by the prep kernel: r, s in [1, n-1]
-    unsigned char pad[9];
+    // u2 = k1 + k2*lambda (mod n), |k1|, |k2| < 2^129 (GLV): width-4 wNAF of |k1| and |k2|,
+    // 2 signed nibbles per byte, digit b at wnaf[i][b>>1]; neg[i]: k_i < 0
+    unsigned char wnaf[2][GLV_DIGITS / 2];
+    unsigned char nwnaf[2]; // digits of each half
+    unsigned char neg[2];
+    unsigned char scalar_ok; // set by the prep kernel: r, s in [1, n-1]
+    unsigned char pad[5];
 };
 // Host-filled input to the prep kernel (u1 <- z, rn <- s before prep).
 static_assert(sizeof(Job) == 272, "job layout");
 
-__device__ __forceinline__ int wnaf_digit(const Job& J, int b) {
-    const int byte = J.wnaf[b >> 1];
+__device__ __forceinline__ int wnaf_digit(const Job& J, int h, int b) {
+    if (b >= J.nwnaf[h]) return 0;
+    const int byte = J.wnaf[h][b >> 1];
     const int nib = (b & 1) ? (byte >> 4) : (byte & 15);
     return nib >= 8 ? nib - 16 : nib;
 }
@@ -476,6 +499,106 @@ __device__ __constant__ uint32_t N_ONE_M[8] = {0x2FC9BEBF, 0x402DA173, 0x50B75FC
 __device__ __constant__ uint32_t N_MINUS_2[8] = {0xD036413F, 0xBFD25E8C, 0xAF48A03B, 0xBAAEDCE6,
                                                  0xFFFFFFFE, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF};
 constexpr uint32_t N_INV32 = 0x5588B13F; // -n^-1 mod 2^32
+
+// GLV endomorphism (secp256k1 has a cube root of unity lambda mod n with lambda*(x, y) =
+// (beta*x, y)): u2 = k1 + k2*lambda with ~128-bit k1, k2 halves the doublings of u2*Q.
+// Lattice basis (a1,b1), (a2,b2) of {(a,b): a + b*lambda = 0 mod n}; c1 = round(b2*k/n),
+// c2 = round(-b1*k/n) through g1 = round(2^384*b2/n), g2 = round(2^384*(-b1)/n);
+// k1 = k - c1*a1 - c2*a2, k2 = -c1*b1 - c2*b2 (exact integers, |k1|,|k2| < 2^129).
+// Derived and range-checked over 2e5 random scalars with Python integers.
+__device__ __constant__ uint32_t GLV_G1[8] = {0x45DBB031, 0xE893209A, 0x71E8CA7F, 0x3DAA8A14,
+                                              0x9284EB15, 0xE86C90E4, 0xA7D46BCD, 0x3086D221};
+__device__ __constant__ uint32_t GLV_G2[8] = {0x8AC47F71, 0x1571B4AE, 0x9DF506C6, 0x221208AC,
+                                              0x0ABFE4C4, 0x6F547FA9, 0x010E8828, 0xE4437ED6};
+__device__ __constant__ uint32_t GLV_A1[4] = {0x9284EB15, 0xE86C90E4, 0xA7D46BCD, 0x3086D221};
+__device__ __constant__ uint32_t GLV_B1N[4] = {0x0ABFE4C3, 0x6F547FA9, 0x010E8828, 0xE4437ED6}; // -b1
+__device__ __constant__ uint32_t GLV_A2[5] = {0x9D44CFD8, 0x57C1108D, 0xA8E2F3F6, 0x14CA50F7, 0x00000001};
+__device__ __constant__ uint32_t GLV_B2[4] = {0x9284EB15, 0xE86C90E4, 0xA7D46BCD, 0x3086D221};
+__device__ __constant__ uint32_t GLV_BETA[8] = {0x719501EE, 0xC1396C28, 0x12F58995, 0x9CF04975,
+                                                0xAC3434E9, 0x6E64479E, 0x657C0710, 0x7AE96A2B};
+
+// r[0 .. NA+NB) = a[0 .. NA) * b[0 .. NB) (plain integers, 32-bit limbs, little-endian)
+template <int NA, int NB>
+__device__ __forceinline__ void mul_wide(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+#pragma unroll
+    for (int i = 0; i < NA + NB; i++) r[i] = 0;
+#pragma unroll
+    for (int i = 0; i < NA; i++) {
+        uint64_t c = 0;
+#pragma unroll
+        for (int j = 0; j < NB; j++) {
+            c += (uint64_t)r[i + j] + (uint64_t)a[i] * b[j];
+            r[i + j] = (uint32_t)c;
+            c >>= 32;
+        }
+        r[i + NB] = (uint32_t)c;
+    }
+}
+// round(k * g / 2^384) for 256-bit k and g: the top 128 bits of the product plus the rounding bit
+__device__ __forceinline__ void mul_shift384(uint32_t (&c)[4], const fe& k, const uint32_t* g) {
+    uint32_t t[16];
+    mul_wide<8, 8>(t, k.v, g);
+    uint64_t carry = t[11] >> 31; // bit 383
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        carry += t[12 + i];
+        c[i] = (uint32_t)carry;
+        carry >>= 32;
+    }
+}
+// width-4 wNAF of a magnitude m (<= 5 limbs, < 2^130), LSB first into J-style nibble bytes
+__device__ __forceinline__ int wnaf4(unsigned char* out, const uint32_t (&m)[5]) {
+    uint32_t k[6];
+#pragma unroll
+    for (int i = 0; i < 5; i++) k[i] = m[i];
+    k[5] = 0;
+    int len = 0;
+    unsigned char cur = 0;
+    for (int b = 0; b < GLV_DIGITS; b++) {
+        int d = 0;
+        if (k[0] & 1) {
+            d = (int)(k[0] & 15);
+            if (d >= 8) d -= 16;
+            const uint32_t addend = (uint32_t)(-d);
+            const uint32_t ext = d > 0 ? 0xFFFFFFFFu : 0u;
+            uint64_t c = 0;
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                c += (uint64_t)k[i] + (i == 0 ? addend : ext);
+                k[i] = (uint32_t)c;
+                c >>= 32;
+            }
+            len = b + 1;
+        }
+        const unsigned char nib = (unsigned char)(d & 15);
+        if (b & 1) {
+            out[b >> 1] = cur | (unsigned char)(nib << 4);
+            cur = 0;
+        } else {
+            cur = nib;
+        }
+#pragma unroll
+        for (int i = 0; i < 5; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
+        k[5] >>= 1;
+    }
+    return len;
+}
+// 10-limb two's complement -> magnitude (5 limbs) and sign
+__device__ __forceinline__ bool abs10(uint32_t (&m)[5], uint32_t (&v)[10]) {
+    const bool neg = (v[9] >> 31) != 0;
+    if (neg) {
+        uint64_t c = 1;
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            c += (uint64_t)(~v[i]);
+            v[i] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 5; i++) m[i] = v[i];
+    return neg;
+}
 
 // a < n ?
 __device__ __forceinline__ bool sc_lt_n(const fe& a) {
@@ -611,51 +734,39 @@ __global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs,
         }
         store_be32(J.rn, rn);
     }
-    // width-4 wNAF of u2, LSB first, two signed nibbles per byte
-    uint32_t k[9];
+    // GLV split of u2, then width-4 wNAF of each half
+    uint32_t c1[4], c2[4];
+    mul_shift384(c1, u2, GLV_G1);
+    mul_shift384(c2, u2, GLV_G2);
+    uint32_t p1[8], p2[8], p3[8], p4[9], k1[10], k2[10];
+    mul_wide<4, 4>(p1, c1, GLV_B1N); // c1 * (-b1)
+    mul_wide<4, 4>(p2, c2, GLV_B2);  // c2 * b2
+    mul_wide<4, 4>(p3, c1, GLV_A1);  // c1 * a1
+    mul_wide<4, 5>(p4, c2, GLV_A2);  // c2 * a2
+    { // k2 = c1*(-b1) - c2*b2
+        uint64_t br = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) k[i] = u2.v[i];
-    k[8] = 0;
-    int len = 0;
-    unsigned char cur = 0;
-    for (int b = 0; b < 258; b++) {
-        uint32_t nz = 0;
-#pragma unroll
-        for (int i = 0; i < 9; i++) nz |= k[i];
-        if (!nz) {
-            if (b & 1) J.wnaf[b >> 1] = cur;
-            for (int q = (b + 1) >> 1; q < 130; q++) J.wnaf[q] = 0;
-            break;
+        for (int i = 0; i < 10; i++) {
+            const uint64_t d = (uint64_t)(i < 8 ? p1[i] : 0u) - (i < 8 ? p2[i] : 0u) - br;
+            k2[i] = (uint32_t)d;
+            br = (d >> 63) & 1;
         }
-        int d = 0;
-        if (k[0] & 1) {
-            d = (int)(k[0] & 15);
-            if (d >= 8) d -= 16;
-            // k -= d (two's complement add of -d with sign extension)
-            const uint32_t addend = (uint32_t)(-d);
-            const uint32_t ext = d > 0 ? 0xFFFFFFFFu : 0u;
-            uint64_t c = 0;
-#pragma unroll
-            for (int i = 0; i < 9; i++) {
-                c += (uint64_t)k[i] + (i == 0 ? addend : ext);
-                k[i] = (uint32_t)c;
-                c >>= 32;
-            }
-            len = b + 1;
-        }
-        const unsigned char nib = (unsigned char)(d & 15);
-        if (b & 1) {
-            J.wnaf[b >> 1] = cur | (unsigned char)(nib << 4);
-            cur = 0;
-        } else {
-            cur = nib;
-        }
-#pragma unroll
-        for (int i = 0; i < 8; i++) k[i] = (k[i] >> 1) | (k[i + 1] << 31);
-        k[8] >>= 1;
     }
-    J.nwnaf_lo = (unsigned char)(len & 0xff);
-    J.nwnaf_hi = (unsigned char)(len >> 8);
+    { // k1 = u2 - c1*a1 - c2*a2 (two subtrahends: the borrow reaches 2)
+        int64_t br = 0;
+#pragma unroll
+        for (int i = 0; i < 10; i++) {
+            const int64_t v = (int64_t)(i < 8 ? u2.v[i] : 0u) - (int64_t)(i < 8 ? p3[i] : 0u) -
+                              (int64_t)(i < 9 ? p4[i] : 0u) - br;
+            k1[i] = (uint32_t)v;
+            br = -(v >> 32); // arithmetic shift: 0, 1 or 2
+        }
+    }
+    uint32_t m1[5], m2[5];
+    J.neg[0] = abs10(m1, k1) ? 1 : 0;
+    J.neg[1] = abs10(m2, k2) ? 1 : 0;
+    J.nwnaf[0] = (unsigned char)wnaf4(J.wnaf[0], m1);
+    J.nwnaf[1] = (unsigned char)wnaf4(J.wnaf[1], m2);
 }
 
 __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
@@ -707,34 +818,42 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
         cur = nx;
     }
 
-    // ---- u2*Q by wNAF
-    const int len = J.nwnaf_lo | (J.nwnaf_hi << 8);
+    // ---- u2*Q = k1*Q + k2*(lambda Q), both halves by interleaved width-4 wNAF; lambda*Q's
+    //      multiples are Q's with X scaled by beta (same Y, Z)
+    const int len = max((int)J.nwnaf[0], (int)J.nwnaf[1]);
+    fe beta;
+#pragma unroll
+    for (int i = 0; i < 8; i++) beta.v[i] = GLV_BETA[i];
     gej acc;
     acc.inf = true;
     for (int b = len - 1; b >= 0; b--) {
         gej d;
         gej_double(d, acc);
         acc = d;
-        const int dg = wnaf_digit(J, b);
-        if (dg) {
-            const int m = (dg > 0 ? dg : -dg) >> 1;
-            gej p;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                p.x.v[k] = preX[m][k][tid];
-                p.y.v[k] = preY[m][k][tid];
-                p.z.v[k] = preZ[m][k][tid];
-            }
-            p.inf = false;
-            if (dg < 0) {
-                fe zero;
+        for (int h = 0; h < 2; h++) {
+            const int dg = wnaf_digit(J, h, b);
+            if (dg) {
+                const int m = (dg > 0 ? dg : -dg) >> 1;
+                gej p;
 #pragma unroll
-                for (int i = 0; i < 8; i++) zero.v[i] = 0;
-                fe_sub(p.y, zero, p.y);
+                for (int k = 0; k < 8; k++) {
+                    p.x.v[k] = preX[m][k][tid];
+                    p.y.v[k] = preY[m][k][tid];
+                    p.z.v[k] = preZ[m][k][tid];
+                }
+                p.inf = false;
+                if (h == 1) fe_mul(p.x, p.x, beta);
+                if ((dg < 0) != (J.neg[h] != 0)) {
+                    fe zero;
+#pragma unroll
+                    for (int i = 0; i < 8; i++) zero.v[i] = 0;
+                    fe_sub(p.y, zero, p.y);
+                }
+                gej s;
+                gej_add(s, acc, p);
+                acc = s;
             }
-            gej s;
-            gej_add(s, acc, p);
-            acc = s;
         }
     }
 
