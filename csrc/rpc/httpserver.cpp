@@ -301,6 +301,14 @@ static bool CheckUserAuthorized(const std::string& userpass, std::string& user) 
     return false;
 }
 
+// "Basic <base64 user:pass>" checked against the RPC credentials (also used by the web GUI).
+bool RPCAuthorizedHeader(const std::string& auth, std::string& user) {
+    if (auth.compare(0, 6, "Basic ") != 0) return false;
+    bool invalid = false;
+    std::vector<unsigned char> dec = DecodeBase64(TrimString(auth.substr(6)), &invalid);
+    return !invalid && CheckUserAuthorized(std::string(dec.begin(), dec.end()), user);
+}
+
 static bool HTTPReq_JSONRPC(const HTTPRequest& req, HTTPReply& rep) {
     if (req.method != "POST") {
         rep.status = 405;
@@ -315,10 +323,8 @@ static bool HTTPReq_JSONRPC(const HTTPRequest& req, HTTPReply& rep) {
         rep.body.clear();
         return false;
     }
-    bool invalid = false;
-    std::vector<unsigned char> dec = DecodeBase64(TrimString(auth.substr(6)), &invalid);
     std::string user;
-    if (invalid || !CheckUserAuthorized(std::string(dec.begin(), dec.end()), user)) {
+    if (!RPCAuthorizedHeader(auth, user)) {
         LogPrintf("ThreadRPCServer incorrect password attempt from %s\n", req.peer.c_str());
         MilliSleep(250); // deter brute-forcing
         rep.status = 401;

@@ -77,6 +77,9 @@ bool StartHTTPRPC(HTTPServer& server, const std::string& datadir, std::string& e
 void StopHTTPRPC(const std::string& datadir);
 // REST endpoints (rest.cpp).
 void StartREST(HTTPServer& server);
+// Browser wallet GUI at GET /gui (webgui.cpp), behind the RPC credentials.
+void StartWebGUI(HTTPServer& server);
+bool RPCAuthorizedHeader(const std::string& authorization, std::string& user);
 
 // Minimal blocking HTTP client (bcp-cli, tests).
 bool HTTPPost(const std::string& host, int port, const std::string& path, const std::string& auth,
