@@ -394,17 +394,26 @@ static void CpuMerkle(State& st) {
 }
 static bench::Reg reg_CpuMerkle("CPU_MerkleRoot_1M", CpuMerkle);
 
-// ---- 8 MB block connect (BASELINE.md "block connect time for an 8 MB block"): a regtest chain
-// past the BCP fork (Equihash(48,5) headers) in a memory-only chainstate, 21,000 signed 2-in/2-out P2PKH transactions (42,000 FORKID
-// signatures, ~7.9 MB) in one block on top of it, then Chainstate::TestBlockValidity (CheckBlock +
-// contextual checks + ConnectBlock with every script and signature checked, nothing cached)
-// per iteration. _GPU batches the ECDSA checks on the MI355X; _CPU keeps them on the worker pool.
+// ---- 8 MB block connect (BASELINE.md "block connect time for an 8 MB / 160k-sigop block"): a
+// regtest chain past the BCP fork (Equihash(48,5) headers) in a memory-only chainstate, one big
+// block on top of it, then Chainstate::TestBlockValidity (CheckBlock + contextual checks +
+// ConnectBlock with every script and signature checked, nothing cached) per iteration. _GPU
+// batches the ECDSA checks on the MI355X; _CPU keeps them on the worker pool.
+//   ConnectBlock8MB:             21,000 2-in/2-out P2PKH transactions (42,000 FORKID signatures,
+//                                7.83 MB), outputs P2PKH.
+//   ConnectBlock8MB_160kSigops:  the consensus worst case of an 8 MB block: 19,500 2-in/2-out
+//                                P2PKH transactions paying to P2SH (39,000 signatures, no sigops
+//                                of their own) plus 8 transactions of 198 P2SH inputs whose redeem
+//                                script is <pk> (2DUP CHECKSIGVERIFY) x100 CHECKSIG (201 ops, 101
+//                                accurately counted sigops each): 159,984 sigops of the 160,000
+//                                allowed (20,000 per started MB, reference src/consensus/consensus.h:
+//                                115,137-140), 198,984 signature checks in 7.8 MB.
 namespace {
 struct BigBlockFixture {
     std::unique_ptr<Chainstate> cs;
     CTxMemPool pool;
     CBlock block;
-    size_t nSigs = 0, nBytes = 0;
+    size_t nSigs = 0, nBytes = 0, nSigOps = 0;
     bool ok = false;
 };
 
@@ -422,11 +431,12 @@ CBlock MakeBlock(Chainstate& cs, CTxMemPool& pool, const CScript& spk, const std
     return b;
 }
 
-BigBlockFixture& BigBlock() {
-    static BigBlockFixture f;
-    static bool built = false;
-    if (built) return f;
-    built = true;
+BigBlockFixture& BigBlock(bool worstCase) {
+    static BigBlockFixture fx[2];
+    static bool built[2] = {false, false};
+    BigBlockFixture& f = fx[worstCase];
+    if (built[worstCase]) return f;
+    built[worstCase] = true;
     SelectParams("regtest");
     ChainstateOptions o;
     o.memoryOnly = true;
@@ -445,7 +455,17 @@ BigBlockFixture& BigBlock() {
     ks.AddKey(key);
     const CScript spk = GetScriptForDestination(key.GetPubKey().GetID());
     const uint32_t hashType = SIGHASH_ALL | SIGHASH_FORKID;
-    const int NFAN = 24, NOUT = 1750, NTX = 21000; // 42,000 outputs
+    // the worst-case redeem script and its P2SH output script
+    CScript redeem;
+    const CPubKey pub = key.GetPubKey();
+    redeem << std::vector<unsigned char>(pub.begin(), pub.end());
+    for (int i = 0; i < 100; i++) redeem << OP_2DUP << OP_CHECKSIGVERIFY;
+    redeem << OP_CHECKSIG;
+    const CScript spkSH = GetScriptForDestination(CScriptID(redeem));
+    const int NFAN = 24, NOUT = 1750;              // 42,000 P2PKH outputs to spend
+    const int NTX = worstCase ? 19500 : 21000;     // 2-in/2-out P2PKH spends in the big block
+    const int NSHTX = worstCase ? 8 : 0, NSHIN = 198; // P2SH spends: 198 x 101 sigops < 20,000 per tx
+    const CScript& bigOut = worstCase ? spkSH : spk;
     std::vector<CTransactionRef> coinbases;
     auto connect = [&](const CBlock& b) {
         bool fNew = false;
@@ -464,7 +484,7 @@ BigBlockFixture& BigBlock() {
         coinbases.push_back(b.vtx[0]);
         connect(b);
     }
-    // fan-out: NFAN matured coinbases -> NFAN * NOUT P2PKH outputs
+    // fan-out: NFAN matured coinbases -> NFAN * NOUT P2PKH outputs (+ one coinbase -> P2SH outputs)
     std::vector<CTransactionRef> fan;
     for (int c = 0; c < NFAN; c++) {
         const CTransaction& cb = *coinbases[c];
@@ -477,10 +497,25 @@ BigBlockFixture& BigBlock() {
             throw std::runtime_error("bench: fan-out signing failed");
         fan.push_back(MakeTransactionRef(std::move(m)));
     }
+    CTransactionRef shFan;
+    if (NSHTX) {
+        const CTransaction& cb = *coinbases[NFAN];
+        CMutableTransaction m;
+        m.vin.resize(1);
+        m.vin[0].prevout = COutPoint(cb.GetHash(), 0);
+        const Amount each = (cb.vout[0].nValue - 100000) / (NSHTX * NSHIN);
+        for (int k = 0; k < NSHTX * NSHIN; k++) m.vout.push_back(CTxOut(each, spkSH));
+        if (!SignSignature(ks, cb.vout[0].scriptPubKey, m, 0, cb.vout[0].nValue, hashType))
+            throw std::runtime_error("bench: P2SH fan-out signing failed");
+        shFan = MakeTransactionRef(std::move(m));
+    }
     // 8 fan-out transactions per block: a P2PKH output is one sigop in 34 bytes, so an output-only
     // block would exceed the 20,000-sigops-per-MB budget
-    for (int c0 = 0; c0 < NFAN; c0 += 8)
-        connect(MakeBlock(*f.cs, f.pool, spk, std::vector<CTransactionRef>(fan.begin() + c0, fan.begin() + c0 + 8)));
+    for (int c0 = 0; c0 < NFAN; c0 += 8) {
+        std::vector<CTransactionRef> v(fan.begin() + c0, fan.begin() + c0 + 8);
+        if (c0 == 0 && shFan) v.push_back(shFan);
+        connect(MakeBlock(*f.cs, f.pool, spk, v));
+    }
     // the big block: NTX transactions, 2 inputs and 2 outputs each, signed on the worker pool
     std::vector<CMutableTransaction> txs(NTX);
     WorkerPool wp(std::min(16, std::max(2, GetNumCores())));
@@ -495,8 +530,8 @@ BigBlockFixture& BigBlock() {
             m.vin.back().prevout = COutPoint(ft.GetHash(), (uint32_t)(u % NOUT));
             in += ft.vout[u % NOUT].nValue;
         }
-        m.vout.push_back(CTxOut(in / 2 - 500, spk));
-        m.vout.push_back(CTxOut(in / 2 - 500, spk));
+        m.vout.push_back(CTxOut(in / 2 - 500, bigOut));
+        m.vout.push_back(CTxOut(in / 2 - 500, bigOut));
         for (int k = 0; k < 2; k++) {
             const size_t u = 2 * t + k;
             const CTxOut& prev = fan[u / NOUT]->vout[u % NOUT];
@@ -504,19 +539,49 @@ BigBlockFixture& BigBlock() {
         }
     }, 64);
     if (signFail) throw std::runtime_error("bench: signing failed");
+    // the worst-case P2SH spends: scriptSig <sig> <redeem>, one signature checked 101 times
+    std::vector<CMutableTransaction> shTxs(NSHTX);
+    for (int t = 0; t < NSHTX; t++) {
+        CMutableTransaction& m = shTxs[t];
+        Amount in = 0;
+        for (int k = 0; k < NSHIN; k++) {
+            const uint32_t n = (uint32_t)(t * NSHIN + k);
+            m.vin.emplace_back();
+            m.vin.back().prevout = COutPoint(shFan->GetHash(), n);
+            in += shFan->vout[n].nValue;
+        }
+        m.vout.push_back(CTxOut(in - 10000, spkSH));
+        const CTransaction unsigned_tx(m);
+        const PrecomputedTransactionData txdata(unsigned_tx);
+        for (int k = 0; k < NSHIN; k++) {
+            const uint256 h = SignatureHash(redeem, unsigned_tx, k, hashType, shFan->vout[t * NSHIN + k].nValue,
+                                            &txdata);
+            std::vector<unsigned char> sig;
+            if (!key.Sign(h, sig)) throw std::runtime_error("bench: P2SH signing failed");
+            sig.push_back((unsigned char)hashType);
+            m.vin[k].scriptSig = CScript() << sig << std::vector<unsigned char>(redeem.begin(), redeem.end());
+        }
+    }
     std::vector<CTransactionRef> refs;
     for (auto& m : txs) refs.push_back(MakeTransactionRef(std::move(m)));
+    for (auto& m : shTxs) refs.push_back(MakeTransactionRef(std::move(m)));
     f.block = MakeBlock(*f.cs, f.pool, spk, refs);
-    f.nSigs = 2 * (size_t)NTX;
+    f.nSigs = 2 * (size_t)NTX + (size_t)NSHTX * NSHIN * 101;
     f.nBytes = GetSerializeSize(f.block, PROTOCOL_VERSION);
+    {
+        const CCoinsViewCache& view = f.cs->CoinsTip();
+        for (const auto& tx : f.block.vtx)
+            f.nSigOps += GetSigOpCountWithoutP2SH(*tx) + (tx->IsCoinBase() ? 0 : GetP2SHSigOpCount(*tx, view));
+    }
     f.ok = true;
-    fprintf(stderr, "# big block: %zu txs, %zu signatures, %zu bytes, on height %d\n", f.block.vtx.size(), f.nSigs,
-            f.nBytes, f.cs->Height());
+    fprintf(stderr, "# big block%s: %zu txs, %zu signature checks, %zu sigops (limit %llu), %zu bytes, on height %d\n",
+            worstCase ? " (160k sigops)" : "", f.block.vtx.size(), f.nSigs, f.nSigOps,
+            (unsigned long long)GetMaxBlockSigOpsCount(f.nBytes), f.nBytes, f.cs->Height());
     return f;
 }
 
-void ConnectBigBlock(State& st, bool useGpu) {
-    BigBlockFixture& f = BigBlock();
+void ConnectBigBlock(State& st, bool useGpu, bool worstCase) {
+    BigBlockFixture& f = BigBlock(worstCase);
     const size_t thr = GetGpuSigThreshold();
     SetGpuSigThreshold(useGpu ? DEFAULT_GPU_SIG_THRESHOLD : SIZE_MAX);
     const SigVerifyStats s0 = GetSigVerifyStats();
@@ -539,13 +604,20 @@ void ConnectBigBlock(State& st, bool useGpu) {
 }
 } // namespace
 
-static void ConnectBlock8MB_CPU(State& st) { ConnectBigBlock(st, false); }
+static void ConnectBlock8MB_CPU(State& st) { ConnectBigBlock(st, false, false); }
 static void ConnectBlock8MB_GPU(State& st) {
     if (!gpu::GpuAvailable()) return;
-    ConnectBigBlock(st, true);
+    ConnectBigBlock(st, true, false);
+}
+static void ConnectBlock8MB_160kSigops_CPU(State& st) { ConnectBigBlock(st, false, true); }
+static void ConnectBlock8MB_160kSigops_GPU(State& st) {
+    if (!gpu::GpuAvailable()) return;
+    ConnectBigBlock(st, true, true);
 }
 BENCHMARK(ConnectBlock8MB_CPU);
 BENCHMARK(ConnectBlock8MB_GPU);
+BENCHMARK(ConnectBlock8MB_160kSigops_CPU);
+BENCHMARK(ConnectBlock8MB_160kSigops_GPU);
 
 int main(int argc, char* argv[]) {
     gArgs.ParseParameters(argc, argv);
