@@ -770,7 +770,16 @@ bool TransactionSignatureChecker::PrepareSig(const valtype& sigIn, const CScript
     if (sigIn.empty()) return false;
     sigOut.assign(sigIn.begin(), sigIn.end() - 1);
     const uint32_t ht = sigIn.back();
+    if (memoValid && ht == memoHashType && flags == memoFlags && scriptCode == memoCode) {
+        sighash = memoSighash;
+        return true;
+    }
     sighash = SignatureHash(scriptCode, *txTo, nIn, ht, amount, txdata, flags);
+    memoCode = scriptCode;
+    memoHashType = ht;
+    memoFlags = flags;
+    memoSighash = sighash;
+    memoValid = true;
     return true;
 }
 

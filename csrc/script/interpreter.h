@@ -151,6 +151,15 @@ protected:
     unsigned int nIn;
     Amount amount;
     const PrecomputedTransactionData* txdata;
+
+private:
+    // Last digest computed by this checker: a script that checks signatures repeatedly under the
+    // same script code and hash type (e.g. a P2SH redeem script of many CHECKSIGVERIFYs) hashes
+    // the transaction once instead of once per check.
+    mutable CScript memoCode;
+    mutable uint32_t memoHashType = 0, memoFlags = 0;
+    mutable bool memoValid = false;
+    mutable uint256 memoSighash;
 };
 
 // One ECDSA verification recorded for later batch execution (GPU).
