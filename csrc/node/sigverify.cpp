@@ -13,10 +13,10 @@ SignatureCache::SignatureCache() {
     set.setup_bytes((size_t)DEFAULT_MAX_SIG_CACHE_SIZE << 20);
 }
 
-uint256 SignatureCache::Entry(const uint256& sighash, const std::vector<unsigned char>& sig,
-                              const std::vector<unsigned char>& pubkey) const {
+uint256 SignatureCache::Entry(const uint256& sighash, const unsigned char* sig, size_t sigLen,
+                              const unsigned char* pubkey, size_t pubLen) const {
     CSHA256 h;
-    h.Write(nonce.begin(), 32).Write(sighash.begin(), 32).Write(pubkey.data(), pubkey.size()).Write(sig.data(), sig.size());
+    h.Write(nonce.begin(), 32).Write(sighash.begin(), 32).Write(pubkey, pubLen).Write(sig, sigLen);
     uint256 r;
     h.Finalize(r.begin());
     return r;
@@ -82,7 +82,7 @@ std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*
         secp::sig_serialize_compact(&sig[j * 64], s);
         if (secp::sc_is_zero(s.r) || secp::sc_is_zero(s.s)) hostOk[j] = 0;
         memcpy(&msg[j * 32], c.sighash.begin(), 32);
-        const std::vector<unsigned char>& pk = c.pubkey;
+        const auto& pk = c.pubkey;
         if (pk.size() == 33 && (pk[0] == 2 || pk[0] == 3)) {
             memcpy(&pub[j * 33], pk.data(), 33);
         } else {
@@ -118,7 +118,8 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
     uint64_t hits = 0;
     // cache keys are one SHA-256 each: on the pool (the cache takes concurrent lookups)
     auto probe = [&](size_t i) {
-        entries[i] = cache.Entry(checks[i].sighash, checks[i].sig, checks[i].pubkey);
+        const DeferredSigCheck& c = checks[i];
+        entries[i] = cache.Entry(c.sighash, c.sig.data(), c.sig.size(), c.pubkey.data(), c.pubkey.size());
         hit[i] = cache.Get(entries[i], cacheErase);
     };
     if (pool && checks.size() >= 1024) pool->ParallelFor(checks.size(), probe, 256);

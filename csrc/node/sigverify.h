@@ -24,8 +24,12 @@ public:
     SignatureCache();
     bool Get(const uint256& entry, bool erase) const { return set.contains(entry, erase); }
     void Set(const uint256& entry) { set.insert(entry); }
+    uint256 Entry(const uint256& sighash, const unsigned char* sig, size_t sigLen, const unsigned char* pubkey,
+                  size_t pubLen) const;
     uint256 Entry(const uint256& sighash, const std::vector<unsigned char>& sig,
-                  const std::vector<unsigned char>& pubkey) const;
+                  const std::vector<unsigned char>& pubkey) const {
+        return Entry(sighash, sig.data(), sig.size(), pubkey.data(), pubkey.size());
+    }
     size_t SetupBytes(size_t bytes) { return set.setup_bytes(bytes); }
     size_t Capacity() const { return set.capacity(); }
     size_t Size() const { return set.count_live(); }

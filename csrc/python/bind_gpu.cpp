@@ -207,8 +207,9 @@ void bind_gpu(pyb::module_& m) {
         [](const std::vector<std::tuple<pyb::bytes, pyb::bytes, pyb::bytes>>& items, bool use_gpu, int threads) {
             std::vector<DeferredSigCheck> checks(items.size());
             for (size_t i = 0; i < items.size(); i++) {
-                checks[i].pubkey = to_vec(std::get<0>(items[i]));
-                checks[i].sig = to_vec(std::get<1>(items[i]));
+                if (!checks[i].pubkey.assign(to_vec(std::get<0>(items[i]))) ||
+                    !checks[i].sig.assign(to_vec(std::get<1>(items[i]))))
+                    throw std::invalid_argument("pubkey longer than 65 or signature longer than 72 bytes");
                 auto m32 = to_vec(std::get<2>(items[i]));
                 if (m32.size() != 32) throw std::invalid_argument("msg32");
                 memcpy(checks[i].sighash.begin(), m32.data(), 32);
@@ -244,8 +245,9 @@ void bind_gpu(pyb::module_& m) {
         [](const std::vector<std::tuple<pyb::bytes, pyb::bytes, pyb::bytes>>& items, bool use_gpu, int threads) {
             std::vector<DeferredSigCheck> checks(items.size());
             for (size_t i = 0; i < items.size(); i++) {
-                checks[i].pubkey = to_vec(std::get<0>(items[i]));
-                checks[i].sig = to_vec(std::get<1>(items[i]));
+                if (!checks[i].pubkey.assign(to_vec(std::get<0>(items[i]))) ||
+                    !checks[i].sig.assign(to_vec(std::get<1>(items[i]))))
+                    throw std::invalid_argument("pubkey longer than 65 or signature longer than 72 bytes");
                 auto m32 = to_vec(std::get<2>(items[i]));
                 if (m32.size() != 32) throw std::invalid_argument("msg32");
                 memcpy(checks[i].sighash.begin(), m32.data(), 32);

@@ -767,8 +767,14 @@ uint256 SignatureHash(const CScript& scriptCode, const CTransaction& txTo, unsig
 // ------------------------------------------------------------------ checkers
 bool TransactionSignatureChecker::PrepareSig(const valtype& sigIn, const CScript& scriptCode, uint32_t flags,
                                              valtype& sigOut, uint256& sighash) const {
-    if (sigIn.empty()) return false;
+    if (!SigDigest(sigIn, scriptCode, flags, sighash)) return false;
     sigOut.assign(sigIn.begin(), sigIn.end() - 1);
+    return true;
+}
+
+bool TransactionSignatureChecker::SigDigest(const valtype& sigIn, const CScript& scriptCode, uint32_t flags,
+                                            uint256& sighash) const {
+    if (sigIn.empty()) return false;
     const uint32_t ht = sigIn.back();
     if (memoValid && ht == memoHashType && flags == memoFlags && scriptCode == memoCode) {
         sighash = memoSighash;
@@ -801,10 +807,20 @@ bool DeferringSignatureChecker::CheckSig(const valtype& sigIn, const valtype& pu
                                          uint32_t flags, bool deferrable) const {
     if (!deferrable || !sink) return TransactionSignatureChecker::CheckSig(sigIn, pubkey, scriptCode, flags, false);
     if (pubkey.empty() || CPubKey::GetLen(pubkey[0]) != pubkey.size()) return false;
-    DeferredSigCheck c;
-    if (!PrepareSig(sigIn, scriptCode, flags, c.sig, c.sighash)) return false;
-    c.pubkey = pubkey;
-    sink->push_back(std::move(c));
+    // a signature or key too long for the inline record (only possible without STRICTENC) is
+    // checked right away
+    if (sigIn.empty()) return false;
+    if (sigIn.size() - 1 > decltype(DeferredSigCheck::sig)::capacity ||
+        pubkey.size() > decltype(DeferredSigCheck::pubkey)::capacity)
+        return TransactionSignatureChecker::CheckSig(sigIn, pubkey, scriptCode, flags, false);
+    sink->emplace_back();
+    DeferredSigCheck& c = sink->back();
+    if (!SigDigest(sigIn, scriptCode, flags, c.sighash)) {
+        sink->pop_back();
+        return false;
+    }
+    c.sig.assign(sigIn.data(), sigIn.size() - 1);
+    c.pubkey.assign(pubkey);
     return true;
 }
 

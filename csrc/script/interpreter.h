@@ -17,6 +17,7 @@
 #include "primitives/transaction.h"
 #include "script/script.h"
 
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -142,6 +143,9 @@ public:
     bool CheckSequence(const CScriptNum& nSequence) const override;
 
 protected:
+    // Digest for a signature with its hashtype byte (memoised); false if the signature is empty.
+    bool SigDigest(const std::vector<unsigned char>& sigIn, const CScript& scriptCode, uint32_t flags,
+                   uint256& sighash) const;
     // Computes the digest and splits off the hashtype; false if the signature is empty.
     bool PrepareSig(const std::vector<unsigned char>& sigIn, const CScript& scriptCode, uint32_t flags,
                     std::vector<unsigned char>& sigOut, uint256& sighash) const;
@@ -162,10 +166,30 @@ private:
     mutable uint256 memoSighash;
 };
 
+// Fixed-capacity byte string stored inline: a block's deferred checks (up to ~200k) are created
+// on the script workers and freed together after the batch, without two heap blocks each.
+template <size_t CAP> struct InlineBytes {
+    static constexpr size_t capacity = CAP;
+    uint8_t len = 0;
+    unsigned char buf[CAP];
+    const unsigned char* data() const { return buf; }
+    size_t size() const { return len; }
+    const unsigned char* begin() const { return buf; }
+    const unsigned char* end() const { return buf + len; }
+    unsigned char operator[](size_t i) const { return buf[i]; }
+    bool assign(const unsigned char* p, size_t n) {
+        if (n > CAP) return false;
+        memcpy(buf, p, n);
+        len = (uint8_t)n;
+        return true;
+    }
+    bool assign(const std::vector<unsigned char>& v) { return assign(v.data(), v.size()); }
+};
+
 // One ECDSA verification recorded for later batch execution (GPU).
 struct DeferredSigCheck {
-    std::vector<unsigned char> pubkey; // serialized (33/65 bytes)
-    std::vector<unsigned char> sig;    // DER, hashtype stripped
+    InlineBytes<65> pubkey; // serialized (33/65 bytes)
+    InlineBytes<72> sig;    // DER (strict DER is at most 72 bytes), hashtype stripped
     uint256 sighash;
 };
 

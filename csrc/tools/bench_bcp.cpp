@@ -614,6 +614,47 @@ static void ConnectBlock8MB_160kSigops_GPU(State& st) {
     if (!gpu::GpuAvailable()) return;
     ConnectBigBlock(st, true, true);
 }
+// Script evaluation of one worst-case P2SH input (<pk> (2DUP CHECKSIGVERIFY) x100 CHECKSIG, the
+// 160k-sigop block's redeem script) with every CHECKSIG deferred into a batch sink: the per-input
+// CPU cost that block validation pays before the batched ECDSA checks.
+static void ScriptP2SH101_Deferred(State& st) {
+    CKey key;
+    key.MakeNewKey(true);
+    const CPubKey pub = key.GetPubKey();
+    CScript redeem;
+    redeem << std::vector<unsigned char>(pub.begin(), pub.end());
+    for (int i = 0; i < 100; i++) redeem << OP_2DUP << OP_CHECKSIGVERIFY;
+    redeem << OP_CHECKSIG;
+    const CScript spk = GetScriptForDestination(CScriptID(redeem));
+    const uint32_t hashType = SIGHASH_ALL | SIGHASH_FORKID;
+    CMutableTransaction m;
+    m.vin.resize(1);
+    m.vin[0].prevout = COutPoint(uint256S("01"), 0);
+    m.vout.push_back(CTxOut(1000, spk));
+    const Amount amount = 2000;
+    {
+        const CTransaction u(m);
+        std::vector<unsigned char> sig;
+        key.Sign(SignatureHash(redeem, u, 0, hashType, amount), sig);
+        sig.push_back((unsigned char)hashType);
+        m.vin[0].scriptSig = CScript() << sig << std::vector<unsigned char>(redeem.begin(), redeem.end());
+    }
+    const CTransaction tx(m);
+    const PrecomputedTransactionData txdata(tx);
+    const uint32_t flags = MANDATORY_SCRIPT_VERIFY_FLAGS | SCRIPT_VERIFY_DERSIG;
+    std::vector<DeferredSigCheck> sink;
+    while (st.KeepRunning()) {
+        sink.clear();
+        DeferringSignatureChecker chk(&tx, 0, amount, &txdata, &sink);
+        ScriptError err;
+        if (!VerifyScript(tx.vin[0].scriptSig, spk, flags, chk, &err) || sink.size() != 101) {
+            fprintf(stderr, "ScriptP2SH101_Deferred: %s, %zu checks\n", ScriptErrorString(err), sink.size());
+            exit(1);
+        }
+    }
+}
+BENCHMARK(ScriptP2SH101_Deferred);
+
 BENCHMARK(ConnectBlock8MB_CPU);
 BENCHMARK(ConnectBlock8MB_GPU);
 BENCHMARK(ConnectBlock8MB_160kSigops_CPU);
