@@ -55,14 +55,34 @@ __device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) {
     return ((uint64_t)rhi << 32) | rlo;
 }
 
+// 64-bit add. BCP_B2_ADDC=1 spells it as a full-rate v_add_co/v_addc pair instead of the
+// single 64-bit v_lshl_add_u64 the compiler picks for gfx950 (A/B builds).
+#ifndef BCP_B2_ADDC
+#define BCP_B2_ADDC 0
+#endif
+__device__ __forceinline__ uint64_t add64(uint64_t a, uint64_t b) {
+#if BCP_B2_ADDC
+    uint32_t lo, hi;
+    asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\tv_addc_co_u32_e32 %1, vcc, %4, %5, vcc"
+        : "=&v"(lo), "=v"(hi)
+        : "v"((uint32_t)a), "v"((uint32_t)b), "v"((uint32_t)(a >> 32)), "v"((uint32_t)(b >> 32))
+        : "vcc");
+    return ((uint64_t)hi << 32) | lo;
+#else
+    return a + b;
+#endif
+}
+// a + m, where m is a compile-time zero for most message words of the header specialisation
+#define BCPK_ADDM(a, x) ((__builtin_constant_p(x) && (x) == 0) ? (a) : add64((a), (x)))
+
 #define BCPK_B2G(a, b, c, d, x, y)       \
-    a = a + b + (x);                     \
+    a = BCPK_ADDM(add64(a, b), (x));     \
     d = rotr64(d ^ a, 32);               \
-    c = c + d;                           \
+    c = add64(c, d);                     \
     b = rotr64(b ^ c, 24);               \
-    a = a + b + (y);                     \
+    a = BCPK_ADDM(add64(a, b), (y));     \
     d = rotr64(d ^ a, 16);               \
-    c = c + d;                           \
+    c = add64(c, d);                     \
     b = rotr64(b ^ c, 63);
 
 // Final-block compression with message m; writes the new chaining value to out.

@@ -40,6 +40,20 @@
 #include <stdexcept>
 #include <utility>
 
+// Generation kernel choice: BCP_EH_GEN_NTG > 0 selects eh_gen_reg with that many threads per
+// workgroup and BCP_EH_GEN_HPT hashes per thread, where the geometry allows ((200,9)); 0 selects
+// the LDS-sorted eh_gen everywhere (A/B builds, tools/build_variant.sh). 512 x 2 measured best
+// (profiles/equihash_r2_gen.md): 2.06 -> 1.75 ms per 32 nonces.
+#ifndef BCP_EH_GEN_NTG
+#define BCP_EH_GEN_NTG 512
+#endif
+#ifndef BCP_EH_GEN_HPT
+#define BCP_EH_GEN_HPT 2
+#endif
+#ifndef BCP_EH_GEN_WPE // minimum waves per SIMD the generation kernel's registers must allow
+#define BCP_EH_GEN_WPE 1
+#endif
+
 namespace bcpk {
 
 template <int N_, int K_, int BB_, int CAP_, int NT_, int GENWG_, int NTG_, int MAXCAND_, int CAP4_ = CAP_,
@@ -301,6 +315,85 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
             row_store<W0>(rs, slot * (W0 * 4), o);
             leaf[slot] = r0 + li;
         }
+    }
+}
+
+// Register-resident generation for configs whose rows split evenly over hashes (IPH | RPW):
+// every thread keeps the HPT*IPH rows it hashed in VGPRs, takes its rank inside this
+// workgroup's run of each row's bucket with an LDS atomicAdd (returning), and after the
+// run claims writes the rows straight from registers. LDS holds only the two 512-entry
+// tables, so several workgroups share a CU and one's hashing (VALU) overlaps another's
+// claim and scatter (memory) — the LDS-sorted eh_gen above holds a whole CU with its 118 KB
+// row buffer and runs those phases back to back.
+template <class C, int NTG, int HPT> struct GenReg {
+    static constexpr int RPT = HPT * C::IPH;            // rows per thread
+    static constexpr int RPW = NTG > 0 ? NTG * RPT : 1; // rows per workgroup
+    static constexpr bool OK = NTG > 0 && C::INIT % RPW == 0;
+    static constexpr int GWG = OK ? C::INIT / RPW : 1;  // workgroups per nonce
+};
+template <class C, bool HDR, int NTG, int HPT>
+__global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_WPE))) void eh_gen_reg(const EhBaseState* __restrict__ states, uint32_t* __restrict__ R,
+                                                  uint32_t* __restrict__ LEAF, uint32_t* __restrict__ CTR0) {
+    using G = GenReg<C, NTG, HPT>;
+    static_assert(G::OK, "register generation geometry");
+    constexpr int W0 = C::words(0);
+    constexpr int SW = (C::N + 31) / 32 + 1;
+    constexpr uint32_t OCAP = C::cap(1);
+    __shared__ uint32_t hist[C::NB], base[C::NB];
+    const int gw = blockIdx.x % G::GWG;
+    const int nonce = blockIdx.x / G::GWG;
+    const int tid = threadIdx.x;
+    const EhBaseState& bs = states[nonce];
+    for (int i = tid; i < C::NB; i += NTG) hist[i] = 0;
+    __syncthreads();
+    const uint32_t r0 = (uint32_t)gw * G::RPW;
+    const uint32_t g0 = r0 / C::IPH;
+    uint32_t rw[G::RPT][W0];
+    uint32_t rk[G::RPT]; // (rank within this workgroup's run << 16) | bucket
+#pragma unroll
+    for (int hh = 0; hh < HPT; ++hh) {
+        const uint32_t g = g0 + hh * NTG + tid;
+        uint64_t h[8];
+        if constexpr (HDR) eh_hash_g_hdr(bs, g, h);
+        else eh_hash_g(bs, g, h);
+#pragma unroll
+        for (int s = 0; s < C::IPH; ++s) {
+            uint32_t S[SW];
+#pragma unroll
+            for (int w = 0; w < SW; ++w) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int k = 4 * w + t;
+                    v = (v << 8) | ((k < C::NBYTES) ? digest_byte(h, s * C::NBYTES + k) : 0u);
+                }
+                S[w] = v;
+            }
+            const int q = hh * C::IPH + s;
+            const uint32_t d = S[0] >> (32 - C::BB);
+#pragma unroll
+            for (int w = 0; w < W0; ++w) rw[q][w] = (S[w] << C::BB) | (S[w + 1] >> (32 - C::BB));
+            rk[q] = (atomicAdd(&hist[d], 1u) << 16) | d;
+        }
+    }
+    __syncthreads();
+    // claim one run per destination bucket
+    for (int b = tid; b < C::NB; b += NTG) {
+        const uint32_t c = hist[b];
+        base[b] = c ? atomicAdd(&CTR0[(size_t)nonce * C::NB + b], c) : 0u;
+    }
+    __syncthreads();
+    const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * W0 * 4));
+    const auto rl = buf_rsrc(LEAF + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 4));
+#pragma unroll
+    for (int q = 0; q < G::RPT; ++q) {
+        const uint32_t d = rk[q] & 0xffff;
+        const uint32_t pos = base[d] + (rk[q] >> 16);
+        const uint32_t slot = d * C::AREA + pos;
+        const bool ok = pos < OCAP;
+        row_store<W0>(rs, ok ? slot * (W0 * 4) : OOB, rw[q]);
+        const uint32_t g = g0 + (q / C::IPH) * NTG + tid;
+        __builtin_amdgcn_raw_buffer_store_b32(g * C::IPH + (q % C::IPH), rl, ok ? slot * 4 : OOB, 0, 0);
     }
 }
 
@@ -637,7 +730,9 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
                                                                   const uint32_t* __restrict__ ncand,
                                                                   const uint64_t* __restrict__ cand, int batch,
                                                                   uint32_t* __restrict__ out_idx,
-                                                                  uint32_t* __restrict__ out_valid) {
+                                                                  uint32_t* __restrict__ out_valid,
+                                                                  uint32_t* __restrict__ nout,
+                                                                  uint32_t* __restrict__ out_list) {
     constexpr int L = C::L;
     __shared__ uint32_t buf[2][L];
     __shared__ uint64_t tri[L / 2 > 0 ? L / 2 : 1];
@@ -706,6 +801,18 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
     if (t + 1 < (uint32_t)L && buf[o][t] == buf[o][t + 1]) atomicOr(&dup, 1u);
     __syncthreads();
     if (t == 0) out_valid[nonce * C::MAXCAND + c] = dup ? 0u : 1u;
+    // Valid solutions are also appended to one compact list, (nonce, candidate, L indices) per
+    // entry, so the host copies a few KB per nonce instead of MAXCAND * L words.
+    if (dup) return; // uniform
+    __shared__ uint32_t slot;
+    if (t == 0) slot = atomicAdd(nout, 1u);
+    __syncthreads();
+    uint32_t* e = out_list + (size_t)slot * (L + 2);
+    if (t == 0) {
+        e[0] = nonce;
+        e[1] = c;
+    }
+    if (t < (uint32_t)L) e[2 + t] = buf[cur][t];
 }
 
 } // namespace bcpk
@@ -744,10 +851,11 @@ struct EquihashGpuSolver::Impl {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     DevBuf<bcpk::EhBaseState> d_states;
-    DevBuf<uint32_t> d_rows[2], d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop;
+    DevBuf<uint32_t> d_rows[2], d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
     DevBuf<uint64_t> d_par, d_cand;
     HostBuf<bcpk::EhBaseState> h_states;
-    HostBuf<uint32_t> h_ncand, h_idx, h_valid, h_ctr0, h_pdrop;
+    HostBuf<uint32_t> h_ncand, h_idx, h_ctr0, h_pdrop, h_nout, h_out;
+    size_t outq = 0; // compact-list entries copied back with every batch (more: a second copy)
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
     int inflight = 0;
@@ -778,8 +886,12 @@ struct EquihashGpuSolver::Impl {
         d_idx.alloc((size_t)batch * C::MAXCAND * C::L);
         d_valid.alloc((size_t)batch * C::MAXCAND);
         h_ncand.alloc(batch);
-        h_idx.alloc((size_t)batch * C::MAXCAND * C::L);
-        h_valid.alloc((size_t)batch * C::MAXCAND);
+        d_nout.alloc(1);
+        h_nout.alloc(1);
+        d_out.alloc((size_t)batch * C::MAXCAND * (C::L + 2));
+        h_out.alloc((size_t)batch * C::MAXCAND * (C::L + 2));
+        outq = std::min<size_t>((size_t)batch * 4 + 16, (size_t)batch * C::MAXCAND);
+        h_idx.alloc((size_t)C::MAXCAND * C::L);
         h_ctr0.alloc((size_t)C::K * C::NB);
         d_stamps.alloc((size_t)C::K * batch * C::NB * 16);
         bytes = 2 * d_rows[0].n * 4 + d_par.n * 8 + d_leaf.n * 4 + d_ctr.n * 4 + d_idx.n * 4;
@@ -821,6 +933,7 @@ struct EquihashGpuSolver::Impl {
         BCP_HIP_CHECK(hipMemcpyAsync(d_states.p, h_states.p, nstates * sizeof(bcpk::EhBaseState),
                                      hipMemcpyHostToDevice, stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ncand.p, 0, batch * sizeof(uint32_t), stream));
+        BCP_HIP_CHECK(hipMemsetAsync(d_nout.p, 0, sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_pdrop.p, 0, (C::K + 1) * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ctr.p, 0, d_ctr.n * sizeof(uint32_t), stream));
         if (debug) {
@@ -836,7 +949,18 @@ struct EquihashGpuSolver::Impl {
             hdr &= st.g_byte == 12;
             for (int w = 2; w < 16; ++w) hdr &= st.m[w] == 0;
         }
-        if (hdr)
+        constexpr bool reg = BCP_EH_GEN_NTG > 0 && bcpk::GenReg<C, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>::OK;
+        if constexpr (reg) {
+            using GR = bcpk::GenReg<C, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>;
+            if (hdr)
+                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, true, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>),
+                                   dim3(GR::GWG * nstates), dim3(BCP_EH_GEN_NTG), 0, stream, d_states.p,
+                                   d_rows[0].p, d_leaf.p, d_ctr.p);
+            else
+                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, false, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>),
+                                   dim3(GR::GWG * nstates), dim3(BCP_EH_GEN_NTG), 0, stream, d_states.p,
+                                   d_rows[0].p, d_leaf.p, d_ctr.p);
+        } else if (hdr)
             hipLaunchKernelGGL((bcpk::eh_gen<C, true>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
                                d_states.p, d_rows[0].p, d_leaf.p, d_ctr.p);
         else
@@ -845,7 +969,7 @@ struct EquihashGpuSolver::Impl {
         launch_rounds<C>((int)nstates, std::make_integer_sequence<int, C::K>{});
         constexpr int EB = C::L < 64 ? 64 : C::L;
         hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND * nstates), dim3(EB), 0, stream, d_leaf.p,
-                           d_par.p, d_ncand.p, d_cand.p, batch, d_idx.p, d_valid.p);
+                           d_par.p, d_ncand.p, d_cand.p, batch, d_idx.p, d_valid.p, d_nout.p, d_out.p);
         BCP_HIP_CHECK(hipGetLastError());
         BCP_HIP_CHECK(hipEventRecord(ev1, stream));
         BCP_HIP_CHECK(
@@ -857,10 +981,12 @@ struct EquihashGpuSolver::Impl {
             BCP_HIP_CHECK(hipMemcpyAsync(h_pdrop.p, d_pdrop.p, (C::K + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                          stream));
         }
-        BCP_HIP_CHECK(hipMemcpyAsync(h_valid.p, d_valid.p, nstates * C::MAXCAND * sizeof(uint32_t),
-                                     hipMemcpyDeviceToHost, stream));
-        BCP_HIP_CHECK(hipMemcpyAsync(h_idx.p, d_idx.p, nstates * C::MAXCAND * C::L * sizeof(uint32_t),
-                                     hipMemcpyDeviceToHost, stream));
+        BCP_HIP_CHECK(hipMemcpyAsync(h_nout.p, d_nout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        BCP_HIP_CHECK(hipMemcpyAsync(h_out.p, d_out.p, outq * (C::L + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                     stream));
+        if (debug) // every candidate of nonce 0, valid or not
+            BCP_HIP_CHECK(hipMemcpyAsync(h_idx.p, d_idx.p, C::MAXCAND * C::L * sizeof(uint32_t),
+                                         hipMemcpyDeviceToHost, stream));
     }
 };
 
@@ -991,6 +1117,11 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
         }
     }
     std::vector<std::vector<std::vector<uint32_t>>> out(ns);
+    const size_t ew = impl->L + 2; // compact-list entry: nonce, candidate, L indices
+    const size_t nout = impl->h_nout.p[0];
+    if (nout > impl->outq) // more valid solutions than the per-batch copy holds: fetch the rest
+        BCP_HIP_CHECK(hipMemcpy(impl->h_out.p + impl->outq * ew, impl->d_out.p + impl->outq * ew,
+                                (nout - impl->outq) * ew * sizeof(uint32_t), hipMemcpyDeviceToHost));
     if (impl->debug) {
         impl->stats.debug_cands.clear();
         const uint32_t nc = std::min<uint32_t>(impl->h_ncand.p[0], (uint32_t)impl->maxcand);
@@ -999,22 +1130,26 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
             impl->stats.debug_cands.emplace_back(p, p + impl->L);
         }
     }
-    for (int nn = 0; nn < ns; ++nn) {
-        uint32_t nc = std::min<uint32_t>(impl->h_ncand.p[nn], (uint32_t)impl->maxcand);
-        impl->stats.candidates += nc;
-        for (uint32_t c = 0; c < nc; ++c) {
-            if (!impl->h_valid.p[nn * impl->maxcand + c]) {
-                impl->stats.duplicates++;
-                continue;
-            }
-            const uint32_t* p = impl->h_idx.p + ((size_t)nn * impl->maxcand + c) * impl->L;
-            std::vector<uint32_t> v(p, p + impl->L);
-            bool seen = false;
-            for (auto& prev : out[nn]) seen |= (prev == v);
-            if (seen) continue;
-            out[nn].push_back(std::move(v));
-            impl->stats.solutions++;
-        }
+    uint64_t cands = 0;
+    for (int nn = 0; nn < ns; ++nn) cands += std::min<uint32_t>(impl->h_ncand.p[nn], (uint32_t)impl->maxcand);
+    impl->stats.candidates += cands;
+    impl->stats.duplicates += cands - nout;
+    // the list is in completion order: put every nonce's solutions in candidate order
+    std::vector<std::pair<uint64_t, const uint32_t*>> ents;
+    ents.reserve(nout);
+    for (size_t e = 0; e < nout; ++e) {
+        const uint32_t* p = impl->h_out.p + e * ew;
+        if (p[0] < (uint32_t)ns) ents.emplace_back(((uint64_t)p[0] << 32) | p[1], p + 2);
+    }
+    std::sort(ents.begin(), ents.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    for (const auto& en : ents) {
+        const int nn = (int)(en.first >> 32);
+        std::vector<uint32_t> v(en.second, en.second + impl->L);
+        bool seen = false;
+        for (auto& prev : out[nn]) seen |= (prev == v);
+        if (seen) continue;
+        out[nn].push_back(std::move(v));
+        impl->stats.solutions++;
     }
     return out;
 }
