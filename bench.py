@@ -14,6 +14,7 @@ Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
 Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 """
 import argparse
+import collections
 import json
 import os
 import struct
@@ -31,6 +32,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "32")))
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
+    ap.add_argument("--solvers", type=int, default=int(os.environ.get("BCP_EH_SOLVERS", "2")),
+                    help="solvers in flight per GPU (each its own stream and buffers)")
     args = ap.parse_args()
 
     import torch
@@ -58,8 +61,10 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
 
-    # two solvers, double-buffered: while the GPU runs batch s, the host decodes batch s-1
-    solvers = [native.EquihashGpuSolver(200, 9, args.batch, device) for _ in range(2)]
+    # several solvers in flight (default two, double-buffered): while the GPU runs batch s, the
+    # host decodes batch s-1, and one solver's kernels fill the other's tails
+    nsolv = max(1, args.solvers)
+    solvers = [native.EquihashGpuSolver(200, 9, args.batch, device) for _ in range(nsolv)]
     solver = solvers[0]
     # Template: CEquihashInput of a mainnet-shaped header (108 B), random-ish but fixed.
     header = bytes((i * 37 + 11) & 0xFF for i in range(108))
@@ -75,7 +80,7 @@ def main():
         return sts
 
     for w in range(args.warmup):
-        solvers[w % 2].solve(states_for(1_000_000 + w))
+        solvers[w % nsolv].solve(states_for(1_000_000 + w))
     for sv in solvers:
         sv.reset_stats()
     all_states = [states_for(s) for s in range(args.steps)]
@@ -84,18 +89,23 @@ def main():
     barrier()
     t0 = time.perf_counter()
     nsol = 0
-    pending = None  # (step, solver) launched but not yet collected
-    for s in range(args.steps + 1):
-        if s < args.steps:
-            solvers[s % 2].launch(all_states[s])
-        if pending is not None:
-            ps, psolver = pending
-            res = psolver.collect()
-            for b, sols in enumerate(res):
-                nsol += len(sols)
-                if ps < 2:
-                    sols_kept.extend((all_states[ps][b], x) for x in sols)
-        pending = (s, solvers[s % 2]) if s < args.steps else None
+    pending = collections.deque()  # (step, solver) launched but not yet collected
+
+    def collect():
+        nonlocal nsol
+        ps, psolver = pending.popleft()
+        for b, sols in enumerate(psolver.collect()):
+            nsol += len(sols)
+            if ps < 2:
+                sols_kept.extend((all_states[ps][b], x) for x in sols)
+
+    for s in range(args.steps):
+        if len(pending) == nsolv:  # this step's solver still holds an older batch
+            collect()
+        solvers[s % nsolv].launch(all_states[s])
+        pending.append((s, solvers[s % nsolv]))
+    while pending:
+        collect()
     barrier()
     dt = time.perf_counter() - t0
 
@@ -138,6 +148,7 @@ def main():
                 "global_batch": args.batch * world,
                 "seq_len": 2097152,
                 "parallelism": f"dp{world} (nonce-space)",
+                "solvers_in_flight": nsolv,
                 "nonces_per_sec": round(nonces / max_dt, 2),
                 "solutions_per_nonce": round(total_sols / max(nonces, 1), 3),
                 "verified": verified,
