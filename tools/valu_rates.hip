@@ -29,6 +29,10 @@ constexpr int ITERS = 2048;
 #define F_SDWA(i) "v_xor_b32_sdwa %" #i ", %" #i ", %8 dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0\n\t"
 #define F_PERM(i) "v_perm_b32 %" #i ", %" #i ", %8, %8\n\t"
 #define F_LSHR(i) "v_lshrrev_b32 %" #i ", 7, %" #i "\n\t"
+#define F_MULLO(i) "v_mul_lo_u32 %" #i ", %" #i ", %8\n\t"
+#define F_MULHI(i) "v_mul_hi_u32 %" #i ", %" #i ", %8\n\t"
+#define F_MAD24(i) "v_mad_u32_u24 %" #i ", %" #i ", %8, %8\n\t"
+#define F_MULHI24(i) "v_mul_hi_u32_u24 %" #i ", %" #i ", %8\n\t"
 #define F_XOR3(i) "v_lshl_or_b32 %" #i ", %" #i ", 3, %8\n\t"
 
 template <int OP> __global__ void bench(unsigned* out, unsigned seed) {
@@ -46,6 +50,31 @@ template <int OP> __global__ void bench(unsigned* out, unsigned seed) {
         if constexpr (OP == 6) OP8(F_PERM);
         if constexpr (OP == 7) OP8(F_LSHR);
         if constexpr (OP == 8) OP8(F_XOR3);
+        if constexpr (OP == 9) OP8(F_MULLO);
+        if constexpr (OP == 10) OP8(F_MULHI);
+        if constexpr (OP == 11) OP8(F_MAD24);
+        if constexpr (OP == 12) OP8(F_MULHI24);
+        if constexpr (OP == 13) { // 8 x v_mad_u64_u32 on 4 chains
+            asm volatile(
+                "v_mad_u64_u32 %0, vcc, %5, %4, %0\n\tv_mad_u64_u32 %1, vcc, %5, %4, %1\n\t"
+                "v_mad_u64_u32 %2, vcc, %5, %4, %2\n\tv_mad_u64_u32 %3, vcc, %5, %4, %3\n\t"
+                "v_mad_u64_u32 %0, vcc, %5, %4, %0\n\tv_mad_u64_u32 %1, vcc, %5, %4, %1\n\t"
+                "v_mad_u64_u32 %2, vcc, %5, %4, %2\n\tv_mad_u64_u32 %3, vcc, %5, %4, %3\n\t"
+                : "+v"(b[0]), "+v"(b[1]), "+v"(b[2]), "+v"(b[3])
+                : "v"(k), "v"(k ^ 5u)
+                : "vcc");
+        }
+        if constexpr (OP == 14) { // 8 x v_fma_f64 on 4 chains
+            double* d = reinterpret_cast<double*>(b);
+            const double kd = (double)k;
+            asm volatile(
+                "v_fma_f64 %0, %0, %4, %4\n\tv_fma_f64 %1, %1, %4, %4\n\t"
+                "v_fma_f64 %2, %2, %4, %4\n\tv_fma_f64 %3, %3, %4, %4\n\t"
+                "v_fma_f64 %0, %0, %4, %4\n\tv_fma_f64 %1, %1, %4, %4\n\t"
+                "v_fma_f64 %2, %2, %4, %4\n\tv_fma_f64 %3, %3, %4, %4\n\t"
+                : "+v"(d[0]), "+v"(d[1]), "+v"(d[2]), "+v"(d[3])
+                : "v"(kd));
+        }
         if constexpr (OP == 3) { // 8 x v_lshl_add_u64 (64-bit add) on 4 chains, twice
             asm volatile(
                 "v_lshl_add_u64 %0, %0, 0, %4\n\tv_lshl_add_u64 %1, %1, 0, %4\n\t"
@@ -84,12 +113,15 @@ int main() {
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
     const char* names[] = {"v_xor_b32",    "v_alignbit_b32", "v_add_u32",     "v_lshl_add_u64", "v_add_co+v_addc (pair)",
-                           "v_xor_b32_sdwa", "v_perm_b32",   "v_lshrrev_b32", "v_lshl_or_b32"};
+                           "v_xor_b32_sdwa", "v_perm_b32",   "v_lshrrev_b32", "v_lshl_or_b32",
+                           "v_mul_lo_u32", "v_mul_hi_u32", "v_mad_u32_u24", "v_mul_hi_u32_u24",
+                           "v_mad_u64_u32", "v_fma_f64"};
     void (*ks[])(unsigned*, unsigned) = {bench<0>, bench<1>, bench<2>, bench<3>, bench<4>,
-                                         bench<5>, bench<6>, bench<7>, bench<8>};
+                                         bench<5>, bench<6>, bench<7>, bench<8>, bench<9>,
+                                         bench<10>, bench<11>, bench<12>, bench<13>, bench<14>};
     for (int waves_per_simd = 1; waves_per_simd <= 8; waves_per_simd *= 2) {
         const int blocks = ncu * 4 * waves_per_simd, threads = 64;
-        for (int op = 0; op < 9; ++op) {
+        for (int op = 0; op < 15; ++op) {
             auto k = ks[op];
             hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, out, 1u);
             CK(hipEventRecord(e0));
