@@ -26,8 +26,14 @@
 //  * Block scans use DPP row shifts/broadcasts inside a wave and one LDS word per wave
 //    across waves: two barriers per scan, no ds_bpermute traffic.
 //
-// Memory traffic per row per round: one contiguous read, one row write into a claimed run,
-// one 8-byte parent-triple write.
+// Memory layout (BCP_EH_MERGED, default): every stage has its own slot array and a stage-s
+// slot holds the row followed by its parent triple, so the emit writes one contiguous slot per
+// output row (one store stream instead of a row stream plus a parent stream: the separate 8-byte
+// parent stores cost 40-50% of the emit phase, profiles/equihash_r2_gen.md) and a pruning round
+// gets the parents with the rows. Keeping all K stage arrays costs 51 words per slot per nonce
+// (≈17 GB per 32-nonce solver, against 288 GB of HBM); the parents must outlive the rows anyway
+// for the final expansion. Per row per round: one contiguous slot read, one slot write into a
+// claimed run.
 #include <hip/hip_runtime.h>
 
 #include "crypto/hashes.h"
@@ -49,6 +55,12 @@
 #endif
 #ifndef BCP_EH_GEN_HPT
 #define BCP_EH_GEN_HPT 2
+#endif
+#ifndef BCP_EH_MERGED // 1: each stage-s slot holds the row AND its parent triple (one store stream)
+#define BCP_EH_MERGED 1
+#endif
+#ifndef BCP_EH_EXP_NOPARENT // timing experiment only: emit stores no parent triples (no solutions)
+#define BCP_EH_EXP_NOPARENT 0
 #endif
 #ifndef BCP_EH_GEN_WPE // minimum waves per SIMD the generation kernel's registers must allow
 #define BCP_EH_GEN_WPE 1
@@ -85,6 +97,8 @@ struct EhCfg {
     static constexpr int bits(int stage) { return N - stage * DB - BB_; }
     static constexpr int words(int stage) { return (bits(stage) + 31) / 32; }
     static constexpr int WMAX = words(0);
+    // words per slot of stage s: the row, plus (s >= 1, merged layout) its parent triple
+    static constexpr int sw(int stage) { return stage == 0 || !BCP_EH_MERGED ? words(stage) : words(stage) + 2; }
     static constexpr size_t ROWS = (size_t)NB * AREA; // slots per stage per nonce
     static_assert(RPW * GENWG_ == INIT && RPW < 65535, "generation split");
     static_assert(RB > 0 && DB < 32, "digit geometry");
@@ -217,6 +231,22 @@ template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_
         __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, 0);
     } else if constexpr (W == 1) {
         __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, 0);
+    }
+}
+
+template <int W> __device__ __forceinline__ void row_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t* v) {
+    if constexpr (W >= 4) {
+        const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
+        row_load<W - 4>(rs, off + 16, v + 4);
+    } else if constexpr (W == 3) {
+        const u3v x = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+        v[0] = x.x, v[1] = x.y, v[2] = x.z;
+    } else if constexpr (W == 2) {
+        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        v[0] = x.x, v[1] = x.y;
+    } else if constexpr (W == 1) {
+        v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
     }
 }
 
@@ -480,8 +510,15 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     constexpr int SL = (NV + 2) / 3;                        // prefetch slice (vectors per phase)
     constexpr int MP = FINAL ? 1 : (C::AREA + NT - 1) / NT; // pairs per lane (registers)
     constexpr int MPR = (CAP + NT - 1) / NT;                 // LDS rows per lane (scans)
+    // Merged layout: a stage-s slot is its row followed by its parent triple (2 words); rows are
+    // prefetched one per lane (RPL per lane) and the parent words go straight to psig/pdw.
+    constexpr bool MG = BCP_EH_MERGED;
+    constexpr int SWI = C::sw(STAGE - 1);                  // words per input slot
+    constexpr int SWO = STAGE < C::K ? C::sw(STAGE) : 1;   // words per output slot
+    constexpr int NI = MG ? RPL : NV;                      // prefetch units per lane
+    constexpr int SLI = MG ? (RPL + 2) / 3 : SL;           // prefetch slice (units per phase)
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
-    __shared__ uint32_t psig[PRUNE ? CAP : 1];
+    __shared__ uint32_t psig[PRUNE ? CAP : 1];                // merged: the parent's (j << 16) | i
     __shared__ uint16_t pdw[PRUNE ? CAP : 1];                 // producing bucket of each row
     __shared__ uint16_t pmark[FINAL ? 1 : MP * NT];           // pair index -> first sorted position
     __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(CAP)];
@@ -504,8 +541,9 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
         return t;
     };
-    u4v nx[NV];
-    uint64_t nf[PRUNE ? RPL : 1];
+    u4v nx[MG ? 1 : NV];
+    uint64_t nf[PRUNE && !MG ? RPL : 1];
+    uint32_t nr[MG ? RPL : 1][MG ? SWI : 1];
     int pf_bk = bk;
     uint32_t pf_n = 0;
     // Issue prefetch vectors [u0, u1) of bucket pf_bk (and its parent triples with the first slice).
@@ -516,6 +554,16 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     // previous bucket's emit stores as well.
     auto issue = [&](int u0, int u1) {
         const int nonce = pf_bk / C::NB, d = pf_bk % C::NB;
+        if constexpr (MG) {
+            const auto rs = buf_rsrc(Rin + ((size_t)nonce * C::ROWS + (size_t)d * C::AREA) * SWI, CAP * SWI * 4);
+            const uint32_t ot = opaque_tid();
+#pragma unroll
+            for (int u = 0; u < RPL; ++u) {
+                if (u < u0 || u >= u1) continue;
+                const uint32_t r = ot + u * NT;
+                row_load<SWI>(rs, r < pf_n ? r * (SWI * 4) : OOB, nr[u]);
+            }
+        } else {
         const auto rs = buf_rsrc(Rin + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::AREA * WI, CAP * WI * 4);
         const uint32_t ot = opaque_tid();
         const uint32_t lim = pf_n * WI;
@@ -536,22 +584,23 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                 }
             }
         }
+        }
     };
 
     // prologue: first bucket in flight, fill of the second known
     uint32_t n = min(CTRin[bk], (uint32_t)CAP);
     pf_n = n;
-    issue(0, NV);
+    issue(0, NI);
     if constexpr (!FINAL) {
         // As many (dropped) stores as one emit issues: the compiler's wait counts at the loop head
         // take the minimum over the entry and back edges; with these, both edges see the prefetch
         // loads followed by MP emit store groups, so the commit waits for its loads only.
         const auto rs_out = buf_rsrc(Rout, 0), rs_par = buf_rsrc(Pout, 0);
-        const uint32_t z[WO] = {};
+        const uint32_t z[SWO] = {};
 #pragma unroll
         for (int u = 0; u < MP; ++u) { // distinct offsets: identical stores would be merged
-            row_store<WO>(rs_out, OOB + 256 * u, z);
-            __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rs_par, OOB + 256 * u, 0, 0);
+            row_store<SWO>(rs_out, OOB + 256 * u, z);
+            if constexpr (!MG) __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rs_par, OOB + 256 * u, 0, 0);
         }
     }
     uint32_t fill_next = (bk + G < nbk) ? CTRin[bk + G] : 0u;
@@ -560,7 +609,27 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         const int nonce = bk / C::NB, d = bk % C::NB;
         EH_STAMP(0);
         // A. commit the prefetched bucket (lane-flat 16-byte LDS stores: conflict-free)
-        {
+        if constexpr (MG) {
+            const uint32_t ot = opaque_tid();
+#pragma unroll
+            for (int u = 0; u < RPL; ++u) {
+                const uint32_t r = ot + u * NT;
+                if (r < n) {
+                    if constexpr (WI % 2 == 0) {
+#pragma unroll
+                        for (int w = 0; w < WI; w += 2)
+                            *reinterpret_cast<u2v*>(&rows[r * WI + w]) = u2v{nr[u][w], nr[u][w + 1]};
+                    } else {
+#pragma unroll
+                        for (int w = 0; w < WI; ++w) rows[r * WI + w] = nr[u][w];
+                    }
+                    if constexpr (PRUNE) {
+                        psig[r] = nr[u][WI];
+                        pdw[r] = (uint16_t)nr[u][WI + 1];
+                    }
+                }
+            }
+        } else {
             const uint32_t ot = opaque_tid();
             const uint32_t lim = n * WI;
 #pragma unroll
@@ -587,7 +656,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         const uint32_t nn = more ? min(fill_next, (uint32_t)CAP) : 0u;
         pf_bk = more ? bn : bk;
         pf_n = nn;
-        issue(0, SL); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
+        issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
         fill_next = (bn + G < nbk) ? CTRin[bn + G] : 0u;
         __syncthreads();
         EH_STAMP(2);
@@ -599,7 +668,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         __syncthreads();
         block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
         for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
-        issue(SL, 2 * SL);
+        issue(SLI, 2 * SLI);
         __syncthreads();
         EH_STAMP(3);
 
@@ -620,7 +689,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                     if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
                 }
             }
-            issue(2 * SL, NV);
+            issue(2 * SLI, NI);
         } else {
             // D2. atomic-free pair enumeration. Sorted position p pairs with every later position
             //     of its group: c_p = bend[key] - p - 1 pairs, first pair index offp[p] (exclusive
@@ -679,7 +748,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             //     destination: each pair takes the next LDS slot of its destination's run
             uint32_t myb = 0;
             if (tid < C::NB) myb = atomicAdd(&CTRout[(size_t)nonce * C::NB + tid], hist[tid]); // wave-uniform branch
-            issue(2 * SL, NV); // after the claim: waiting for its return then skips these loads
+            issue(2 * SLI, NI); // after the claim: waiting for its return then skips these loads
             uint32_t start = 0; // thread b < NB: first LDS slot of destination b (NB <= NT: one entry each)
             const uint32_t np = block_exscan<NT>(hist, cur, C::NB, wsum, &start);
 #pragma unroll
@@ -691,7 +760,8 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             // D4. emit, one lane per output row in destination order: XOR, shift one digit,
             //     store into the claimed run (rows past the next round's capacity are dropped)
             constexpr uint32_t OCAP = C::cap(STAGE + 1 <= C::K ? STAGE + 1 : C::K);
-            const auto rs_out = buf_rsrc(Rout + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * WO * 4));
+            const auto rs_out = MG ? buf_rsrc(Rout + (size_t)nonce * C::ROWS * SWO, (uint32_t)(C::ROWS * SWO * 4))
+                                   : buf_rsrc(Rout + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * WO * 4));
             const auto rs_par = buf_rsrc(Pout + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 8));
 #pragma unroll
             for (int u = 0; u < MP; ++u) { // fixed trip count, unconditional stores (see issue())
@@ -707,10 +777,21 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                 const uint32_t slot = b * C::AREA + pos;
 #pragma unroll
                 for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
-                row_store<WO>(rs_out, ok ? slot * (WO * 4) : OOB, o);
                 const uint64_t tri = pack_tri(d, i, j);
-                const u2v tv = {(uint32_t)tri, (uint32_t)(tri >> 32)};
-                __builtin_amdgcn_raw_buffer_store_b64(tv, rs_par, ok ? slot * 8 : OOB, 0, 0);
+                if constexpr (MG) {
+                    uint32_t ov[SWO];
+#pragma unroll
+                    for (int w = 0; w < WO; ++w) ov[w] = o[w];
+                    ov[WO] = (uint32_t)tri;
+                    ov[WO + 1] = (uint32_t)(tri >> 32);
+                    row_store<SWO>(rs_out, ok ? slot * (SWO * 4) : OOB, ov);
+                } else {
+                    row_store<WO>(rs_out, ok ? slot * (WO * 4) : OOB, o);
+                    const u2v tv = {(uint32_t)tri, (uint32_t)(tri >> 32)};
+#if !BCP_EH_EXP_NOPARENT
+                    __builtin_amdgcn_raw_buffer_store_b64(tv, rs_par, ok ? slot * 8 : OOB, 0, 0);
+#endif
+                }
             }
         }
         __syncthreads();
@@ -723,10 +804,14 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
 
 
 // ------------------------------------------------------------------ tree expansion
+// Merged layout: the stage arrays (stage s slot = row, parent triple) passed by value.
+struct EhStages {
+    const uint32_t* r[16];
+};
 // LEAF: stage-0 leaf index per slot; P: K-1 arrays of stage-1..K-1 parent triples.
 template <class C>
 __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_t* __restrict__ LEAF,
-                                                                  const uint64_t* __restrict__ P,
+                                                                  const uint64_t* __restrict__ P, EhStages st,
                                                                   const uint32_t* __restrict__ ncand,
                                                                   const uint64_t* __restrict__ cand, int batch,
                                                                   uint32_t* __restrict__ out_idx,
@@ -758,8 +843,14 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
             buf[cur][t] = dd * C::AREA + r;
         }
         __syncthreads();
-        if (s > 1 && t < 2 * cnt)
-            tri[t] = P[(size_t)(s - 2) * batch * C::ROWS + (size_t)nonce * C::ROWS + buf[cur][t]];
+        if (s > 1 && t < 2 * cnt) {
+            if constexpr (BCP_EH_MERGED) { // stage s-1 slot: row words, then the parent triple
+                const uint32_t* q = st.r[s - 1] + ((size_t)nonce * C::ROWS + buf[cur][t]) * C::sw(s - 1) + C::words(s - 1);
+                tri[t] = ((uint64_t)q[1] << 32) | q[0];
+            } else {
+                tri[t] = P[(size_t)(s - 2) * batch * C::ROWS + (size_t)nonce * C::ROWS + buf[cur][t]];
+            }
+        }
     }
     __syncthreads();
     if (t < (uint32_t)L) buf[cur][t] = LEAF[(size_t)nonce * C::ROWS + buf[cur][t]];
@@ -853,11 +944,13 @@ struct EquihashGpuSolver::Impl {
     DevBuf<bcpk::EhBaseState> d_states;
     DevBuf<uint32_t> d_rows[2], d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
     DevBuf<uint64_t> d_par, d_cand;
+    DevBuf<uint32_t> d_rst[16]; // merged layout: stage-s slot arrays (s = 0..K-1)
     HostBuf<bcpk::EhBaseState> h_states;
     HostBuf<uint32_t> h_ncand, h_idx, h_ctr0, h_pdrop, h_nout, h_out;
     size_t outq = 0; // compact-list entries copied back with every batch (more: a second copy)
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
+    std::vector<size_t> slot_words, row_words; // per stage
     int inflight = 0;
     int ncu = 1;
     bool debug = false, stamp_mode = false;
@@ -872,13 +965,24 @@ struct EquihashGpuSolver::Impl {
         nb = C::NB;
         caps.clear();
         for (int r = 1; r <= C::K; ++r) caps.push_back(C::cap(r));
+        slot_words.clear();
+        row_words.clear();
+        for (int st = 0; st < C::K; ++st) {
+            slot_words.push_back(C::sw(st));
+            row_words.push_back(C::words(st));
+        }
         kstages = C::K;
         d_states.alloc(batch);
         h_states.alloc(batch);
-        for (int p = 0; p < 2; ++p) d_rows[p].alloc((size_t)batch * C::ROWS * C::WMAX);
+        static_assert(C::K <= 16, "stage arrays");
+        if (BCP_EH_MERGED) {
+            for (int s = 0; s < C::K; ++s) d_rst[s].alloc((size_t)batch * C::ROWS * C::sw(s));
+        } else {
+            for (int p = 0; p < 2; ++p) d_rows[p].alloc((size_t)batch * C::ROWS * C::WMAX);
+        }
         d_ctr.alloc((size_t)C::K * batch * C::NB);
         d_leaf.alloc((size_t)batch * C::ROWS);
-        d_par.alloc((size_t)(C::K - 1) * batch * C::ROWS);
+        if (!BCP_EH_MERGED) d_par.alloc((size_t)(C::K - 1) * batch * C::ROWS);
         d_ncand.alloc(batch);
         d_pdrop.alloc(C::K + 1);
         h_pdrop.alloc(C::K + 1);
@@ -895,6 +999,7 @@ struct EquihashGpuSolver::Impl {
         h_ctr0.alloc((size_t)C::K * C::NB);
         d_stamps.alloc((size_t)C::K * batch * C::NB * 16);
         bytes = 2 * d_rows[0].n * 4 + d_par.n * 8 + d_leaf.n * 4 + d_ctr.n * 4 + d_idx.n * 4;
+        for (int s = 0; s < C::K; ++s) bytes += d_rst[s].n * 4;
     }
 
     // Persistent round kernels: as many workgroups as fit on the device at once.
@@ -908,10 +1013,10 @@ struct EquihashGpuSolver::Impl {
         return std::min(nbk, ncu * per_cu);
     }
     template <class C, int S> void launch_round(int nstates) {
-        const uint32_t* rin = d_rows[(S - 1) & 1].p;
-        uint32_t* rout = d_rows[S & 1].p;
-        const uint64_t* pin = S >= 2 ? d_par.p + (size_t)(S - 2) * batch * C::ROWS : nullptr;
-        uint64_t* pout = S < C::K ? d_par.p + (size_t)(S - 1) * batch * C::ROWS : nullptr;
+        const uint32_t* rin = BCP_EH_MERGED ? d_rst[S - 1].p : d_rows[(S - 1) & 1].p;
+        uint32_t* rout = BCP_EH_MERGED ? (S < C::K ? d_rst[S].p : nullptr) : d_rows[S & 1].p;
+        const uint64_t* pin = !BCP_EH_MERGED && S >= 2 ? d_par.p + (size_t)(S - 2) * batch * C::ROWS : nullptr;
+        uint64_t* pout = !BCP_EH_MERGED && S < C::K ? d_par.p + (size_t)(S - 1) * batch * C::ROWS : nullptr;
         const uint32_t* cin = d_ctr.p + (size_t)(S - 1) * batch * C::NB;
         uint32_t* cout = S < C::K ? d_ctr.p + (size_t)S * batch * C::NB : nullptr;
         const int nbk = C::NB * nstates;
@@ -938,7 +1043,9 @@ struct EquihashGpuSolver::Impl {
         BCP_HIP_CHECK(hipMemsetAsync(d_ctr.p, 0, d_ctr.n * sizeof(uint32_t), stream));
         if (debug) {
             BCP_HIP_CHECK(hipMemsetAsync(d_leaf.p, 0xff, d_leaf.n * sizeof(uint32_t), stream));
-            BCP_HIP_CHECK(hipMemsetAsync(d_par.p, 0xff, d_par.n * sizeof(uint64_t), stream));
+            if (d_par.n) BCP_HIP_CHECK(hipMemsetAsync(d_par.p, 0xff, d_par.n * sizeof(uint64_t), stream));
+            for (int s = 1; s < C::K; ++s)
+                if (d_rst[s].n) BCP_HIP_CHECK(hipMemsetAsync(d_rst[s].p, 0xff, d_rst[s].n * sizeof(uint32_t), stream));
         }
         BCP_HIP_CHECK(hipEventRecord(ev0, stream));
         // header-shaped inputs (140 B: g lands at byte 12 of the final block) take the
@@ -949,27 +1056,31 @@ struct EquihashGpuSolver::Impl {
             hdr &= st.g_byte == 12;
             for (int w = 2; w < 16; ++w) hdr &= st.m[w] == 0;
         }
+        uint32_t* r0 = BCP_EH_MERGED ? d_rst[0].p : d_rows[0].p;
         constexpr bool reg = BCP_EH_GEN_NTG > 0 && bcpk::GenReg<C, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>::OK;
         if constexpr (reg) {
             using GR = bcpk::GenReg<C, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>;
             if (hdr)
                 hipLaunchKernelGGL((bcpk::eh_gen_reg<C, true, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>),
                                    dim3(GR::GWG * nstates), dim3(BCP_EH_GEN_NTG), 0, stream, d_states.p,
-                                   d_rows[0].p, d_leaf.p, d_ctr.p);
+                                   r0, d_leaf.p, d_ctr.p);
             else
                 hipLaunchKernelGGL((bcpk::eh_gen_reg<C, false, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>),
                                    dim3(GR::GWG * nstates), dim3(BCP_EH_GEN_NTG), 0, stream, d_states.p,
-                                   d_rows[0].p, d_leaf.p, d_ctr.p);
+                                   r0, d_leaf.p, d_ctr.p);
         } else if (hdr)
             hipLaunchKernelGGL((bcpk::eh_gen<C, true>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
-                               d_states.p, d_rows[0].p, d_leaf.p, d_ctr.p);
+                               d_states.p, r0, d_leaf.p, d_ctr.p);
         else
             hipLaunchKernelGGL((bcpk::eh_gen<C, false>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
-                               d_states.p, d_rows[0].p, d_leaf.p, d_ctr.p);
+                               d_states.p, r0, d_leaf.p, d_ctr.p);
         launch_rounds<C>((int)nstates, std::make_integer_sequence<int, C::K>{});
         constexpr int EB = C::L < 64 ? 64 : C::L;
+        bcpk::EhStages stages{};
+        for (int s = 0; s < C::K; ++s) stages.r[s] = d_rst[s].p;
+        if (!BCP_EH_EXP_NOPARENT) // timing experiment builds store no parents: nothing to expand
         hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND * nstates), dim3(EB), 0, stream, d_leaf.p,
-                           d_par.p, d_ncand.p, d_cand.p, batch, d_idx.p, d_valid.p, d_nout.p, d_out.p);
+                           d_par.p, stages, d_ncand.p, d_cand.p, batch, d_idx.p, d_valid.p, d_nout.p, d_out.p);
         BCP_HIP_CHECK(hipGetLastError());
         BCP_HIP_CHECK(hipEventRecord(ev1, stream));
         BCP_HIP_CHECK(
@@ -1066,7 +1177,14 @@ std::vector<uint64_t> EquihashGpuSolver::DebugDump() {
     BCP_HIP_CHECK(hipMemcpy(leaf.data(), impl->d_leaf.p, R * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < R; ++i) out[i] = leaf[i];
     for (size_t s = 1; s < K; ++s)
-        BCP_HIP_CHECK(hipMemcpy(out.data() + s * R, impl->d_par.p + (s - 1) * B * R, R * 8, hipMemcpyDeviceToHost));
+        if (impl->d_par.n) {
+            BCP_HIP_CHECK(hipMemcpy(out.data() + s * R, impl->d_par.p + (s - 1) * B * R, R * 8, hipMemcpyDeviceToHost));
+        } else { // merged layout: the triple follows the row in every stage-s slot of nonce 0
+            const size_t sw = impl->slot_words[s], w = impl->row_words[s];
+            std::vector<uint32_t> buf(R * sw);
+            BCP_HIP_CHECK(hipMemcpy(buf.data(), impl->d_rst[s].p, R * sw * 4, hipMemcpyDeviceToHost));
+            for (size_t i = 0; i < R; ++i) out[s * R + i] = ((uint64_t)buf[i * sw + w + 1] << 32) | buf[i * sw + w];
+        }
     return out;
 }
 size_t EquihashGpuSolver::DeviceBytes() const { return impl->bytes; }

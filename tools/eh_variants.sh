@@ -13,7 +13,8 @@ for b in $(ls ab); do
     export BCP_NATIVE_PATH=$PWD/ab/$b/$EXT
     timeout -k 10 200 python -u tools/eh_crosscheck.py --nonces 2 > "$O/x200_$b.log" 2>&1
     timeout -k 10 100 python -u tools/eh_crosscheck.py --n 96 --k 5 --nonces 16 > "$O/x96_$b.log" 2>&1
-    echo "$b $(grep -h -o '"missing": [0-9]*, "extra": [0-9]*' "$O/x200_$b.log" "$O/x96_$b.log" | tr '\n' ' ')"
+    timeout -k 10 100 python -u tools/eh_crosscheck.py --n 48 --k 5 --nonces 32 > "$O/x48_$b.log" 2>&1
+    echo "$b $(grep -h -o '"missing": [0-9]*, "extra": [0-9]*'  "$O/x200_$b.log" "$O/x96_$b.log" "$O/x48_$b.log" | tr '\n' ' ')"
     timeout -k 10 100 python3 tools/eh_serial.py > "$O/ser_$b.log" 2>&1
     echo "$b serial $(tail -n 1 "$O/ser_$b.log")"
 done
