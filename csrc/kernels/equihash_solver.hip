@@ -59,6 +59,15 @@
 #ifndef BCP_EH_MERGED // 1: each stage-s slot holds the row AND its parent triple (one store stream)
 #define BCP_EH_MERGED 1
 #endif
+#ifndef BCP_EH_LEAF_SLOT // 1 (merged layout): a stage-0 slot holds the row and its leaf index
+#define BCP_EH_LEAF_SLOT 0 // measured neutral (round 1 reads 7-word slots), profiles/equihash_r2_gen.md
+#endif
+#ifndef BCP_EH_SLOT_ALIGN // merged layout: slot widths rounded up to a multiple of this many words
+#define BCP_EH_SLOT_ALIGN 1 // 2 and 4 measured slower (more bytes, no alignment gain)
+#endif
+#ifndef BCP_EH_ROWONLY_LOAD // merged layout: non-pruning rounds skip the parent words of a slot
+#define BCP_EH_ROWONLY_LOAD 1
+#endif
 #ifndef BCP_EH_EXP_NOPARENT // timing experiment only: emit stores no parent triples (no solutions)
 #define BCP_EH_EXP_NOPARENT 0
 #endif
@@ -98,7 +107,12 @@ struct EhCfg {
     static constexpr int words(int stage) { return (bits(stage) + 31) / 32; }
     static constexpr int WMAX = words(0);
     // words per slot of stage s: the row, plus (s >= 1, merged layout) its parent triple
-    static constexpr int sw(int stage) { return stage == 0 || !BCP_EH_MERGED ? words(stage) : words(stage) + 2; }
+    static constexpr bool LEAFSLOT = BCP_EH_MERGED && BCP_EH_LEAF_SLOT;
+    static constexpr int sw(int stage) {
+        return !BCP_EH_MERGED ? words(stage)
+                              : ((stage == 0 ? words(0) + (LEAFSLOT ? 1 : 0) : words(stage) + 2) + BCP_EH_SLOT_ALIGN - 1) /
+                                    BCP_EH_SLOT_ALIGN * BCP_EH_SLOT_ALIGN;
+    }
     static constexpr size_t ROWS = (size_t)NB * AREA; // slots per stage per nonce
     static_assert(RPW * GENWG_ == INIT && RPW < 65535, "generation split");
     static_assert(RB > 0 && DB < 32, "digit geometry");
@@ -332,18 +346,20 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
     for (int li = tid; li < C::RPW; li += NTG) perm[atomicAdd(&cur[dst[li]], 1u)] = (uint16_t)li;
     if (tid < C::NB) base[tid] = myb - start; // sorted position t of bucket d -> run position base[d] + t
     __syncthreads();
-    const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * W0 * 4));
-    uint32_t* leaf = LEAF + (size_t)nonce * C::ROWS;
+    constexpr int SW0 = C::sw(0);
+    const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * SW0, (uint32_t)(C::ROWS * SW0 * 4));
+    uint32_t* leaf = C::LEAFSLOT ? nullptr : LEAF + (size_t)nonce * C::ROWS;
     for (int t = tid; t < C::RPW; t += NTG) {
         const uint32_t li = perm[t], d = dst[li];
         const uint32_t pos = base[d] + (uint32_t)t;
         if (pos < OCAP) {
-            uint32_t o[W0];
+            uint32_t o[SW0 > W0 ? SW0 : W0 + 1] = {};
 #pragma unroll
             for (int w = 0; w < W0; ++w) o[w] = rows[li * W0 + w];
+            o[W0] = r0 + li;
             const uint32_t slot = d * C::AREA + pos;
-            row_store<W0>(rs, slot * (W0 * 4), o);
-            leaf[slot] = r0 + li;
+            row_store<SW0>(rs, slot * (SW0 * 4), o);
+            if constexpr (!C::LEAFSLOT) leaf[slot] = r0 + li;
         }
     }
 }
@@ -413,17 +429,27 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
         base[b] = c ? atomicAdd(&CTR0[(size_t)nonce * C::NB + b], c) : 0u;
     }
     __syncthreads();
-    const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * W0 * 4));
-    const auto rl = buf_rsrc(LEAF + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 4));
+    constexpr int SW0 = C::sw(0);
+    const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * SW0, (uint32_t)(C::ROWS * SW0 * 4));
+    const auto rl = buf_rsrc(C::LEAFSLOT ? R : LEAF + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 4));
 #pragma unroll
     for (int q = 0; q < G::RPT; ++q) {
         const uint32_t d = rk[q] & 0xffff;
         const uint32_t pos = base[d] + (rk[q] >> 16);
         const uint32_t slot = d * C::AREA + pos;
         const bool ok = pos < OCAP;
-        row_store<W0>(rs, ok ? slot * (W0 * 4) : OOB, rw[q]);
         const uint32_t g = g0 + (q / C::IPH) * NTG + tid;
-        __builtin_amdgcn_raw_buffer_store_b32(g * C::IPH + (q % C::IPH), rl, ok ? slot * 4 : OOB, 0, 0);
+        const uint32_t li = g * C::IPH + (q % C::IPH); // leaf index
+        if constexpr (C::LEAFSLOT) {
+            uint32_t o[SW0 > W0 ? SW0 : W0 + 1] = {};
+#pragma unroll
+            for (int w = 0; w < W0; ++w) o[w] = rw[q][w];
+            o[W0] = li;
+            row_store<SW0>(rs, ok ? slot * (SW0 * 4) : OOB, o);
+        } else {
+            row_store<W0>(rs, ok ? slot * (SW0 * 4) : OOB, rw[q]);
+            __builtin_amdgcn_raw_buffer_store_b32(li, rl, ok ? slot * 4 : OOB, 0, 0);
+        }
     }
 }
 
@@ -543,7 +569,9 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     };
     u4v nx[MG ? 1 : NV];
     uint64_t nf[PRUNE && !MG ? RPL : 1];
-    uint32_t nr[MG ? RPL : 1][MG ? SWI : 1];
+    // (a round that does not prune loads only the row words of each slot)
+    constexpr int LWI = MG ? (PRUNE ? SWI : (BCP_EH_ROWONLY_LOAD ? WI : SWI)) : 1;
+    uint32_t nr[MG ? RPL : 1][LWI];
     int pf_bk = bk;
     uint32_t pf_n = 0;
     // Issue prefetch vectors [u0, u1) of bucket pf_bk (and its parent triples with the first slice).
@@ -561,7 +589,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             for (int u = 0; u < RPL; ++u) {
                 if (u < u0 || u >= u1) continue;
                 const uint32_t r = ot + u * NT;
-                row_load<SWI>(rs, r < pf_n ? r * (SWI * 4) : OOB, nr[u]);
+                row_load<LWI>(rs, r < pf_n ? r * (SWI * 4) : OOB, nr[u]);
             }
         } else {
         const auto rs = buf_rsrc(Rin + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::AREA * WI, CAP * WI * 4);
@@ -779,7 +807,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                 for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
                 const uint64_t tri = pack_tri(d, i, j);
                 if constexpr (MG) {
-                    uint32_t ov[SWO];
+                    uint32_t ov[SWO] = {};
 #pragma unroll
                     for (int w = 0; w < WO; ++w) ov[w] = o[w];
                     ov[WO] = (uint32_t)tri;
@@ -853,7 +881,12 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
         }
     }
     __syncthreads();
-    if (t < (uint32_t)L) buf[cur][t] = LEAF[(size_t)nonce * C::ROWS + buf[cur][t]];
+    if (t < (uint32_t)L) {
+        if constexpr (C::LEAFSLOT)
+            buf[cur][t] = st.r[0][((size_t)nonce * C::ROWS + buf[cur][t]) * C::sw(0) + C::words(0)];
+        else
+            buf[cur][t] = LEAF[(size_t)nonce * C::ROWS + buf[cur][t]];
+    }
     // Canonical order: at each level the subtree with the smaller first index goes left.
     for (int l = 0; l < C::K; ++l) {
         __syncthreads();
@@ -951,6 +984,7 @@ struct EquihashGpuSolver::Impl {
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
     std::vector<size_t> slot_words, row_words; // per stage
+    size_t leaf_slot_words = 0;                 // > 0: stage-0 slots carry the leaf index last
     int inflight = 0;
     int ncu = 1;
     bool debug = false, stamp_mode = false;
@@ -981,7 +1015,8 @@ struct EquihashGpuSolver::Impl {
             for (int p = 0; p < 2; ++p) d_rows[p].alloc((size_t)batch * C::ROWS * C::WMAX);
         }
         d_ctr.alloc((size_t)C::K * batch * C::NB);
-        d_leaf.alloc((size_t)batch * C::ROWS);
+        if (!C::LEAFSLOT) d_leaf.alloc((size_t)batch * C::ROWS);
+        leaf_slot_words = C::LEAFSLOT ? C::sw(0) : 0;
         if (!BCP_EH_MERGED) d_par.alloc((size_t)(C::K - 1) * batch * C::ROWS);
         d_ncand.alloc(batch);
         d_pdrop.alloc(C::K + 1);
@@ -1042,9 +1077,9 @@ struct EquihashGpuSolver::Impl {
         BCP_HIP_CHECK(hipMemsetAsync(d_pdrop.p, 0, (C::K + 1) * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ctr.p, 0, d_ctr.n * sizeof(uint32_t), stream));
         if (debug) {
-            BCP_HIP_CHECK(hipMemsetAsync(d_leaf.p, 0xff, d_leaf.n * sizeof(uint32_t), stream));
+            if (d_leaf.n) BCP_HIP_CHECK(hipMemsetAsync(d_leaf.p, 0xff, d_leaf.n * sizeof(uint32_t), stream));
             if (d_par.n) BCP_HIP_CHECK(hipMemsetAsync(d_par.p, 0xff, d_par.n * sizeof(uint64_t), stream));
-            for (int s = 1; s < C::K; ++s)
+            for (int s = 0; s < C::K; ++s)
                 if (d_rst[s].n) BCP_HIP_CHECK(hipMemsetAsync(d_rst[s].p, 0xff, d_rst[s].n * sizeof(uint32_t), stream));
         }
         BCP_HIP_CHECK(hipEventRecord(ev0, stream));
@@ -1174,7 +1209,14 @@ std::vector<uint64_t> EquihashGpuSolver::DebugDump() {
     const size_t R = impl->rows, K = impl->kstages, B = impl->batch;
     std::vector<uint64_t> out(K * R);
     std::vector<uint32_t> leaf(R);
-    BCP_HIP_CHECK(hipMemcpy(leaf.data(), impl->d_leaf.p, R * 4, hipMemcpyDeviceToHost));
+    if (impl->leaf_slot_words) {
+        const size_t sw = impl->leaf_slot_words;
+        std::vector<uint32_t> buf(R * sw);
+        BCP_HIP_CHECK(hipMemcpy(buf.data(), impl->d_rst[0].p, R * sw * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < R; ++i) leaf[i] = buf[i * sw + impl->row_words[0]];
+    } else {
+        BCP_HIP_CHECK(hipMemcpy(leaf.data(), impl->d_leaf.p, R * 4, hipMemcpyDeviceToHost));
+    }
     for (size_t i = 0; i < R; ++i) out[i] = leaf[i];
     for (size_t s = 1; s < K; ++s)
         if (impl->d_par.n) {
