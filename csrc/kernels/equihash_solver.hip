@@ -68,6 +68,9 @@
 #ifndef BCP_EH_ROWONLY_LOAD // merged layout: non-pruning rounds skip the parent words of a slot
 #define BCP_EH_ROWONLY_LOAD 1
 #endif
+#ifndef BCP_EH_COMPACT_PARENT // 1 (merged layout): one parent word where the row has 3 spare bits
+#define BCP_EH_COMPACT_PARENT 1
+#endif
 #ifndef BCP_EH_EXP_NOPARENT // timing experiment only: emit stores no parent triples (no solutions)
 #define BCP_EH_EXP_NOPARENT 0
 #endif
@@ -108,9 +111,16 @@ struct EhCfg {
     static constexpr int WMAX = words(0);
     // words per slot of stage s: the row, plus (s >= 1, merged layout) its parent triple
     static constexpr bool LEAFSLOT = BCP_EH_MERGED && BCP_EH_LEAF_SLOT;
+    // Compact parents: the triple (d, i, j) as ONE word (i, j: 13 bits each, 6 bits of d) plus the
+    // top 3 bits of d in the low (padding) bits of the row's last word, where the row has them.
+    static constexpr bool cp(int stage) {
+        return BCP_EH_MERGED && BCP_EH_COMPACT_PARENT && stage >= 1 && stage < K &&
+               32 * words(stage) - bits(stage) >= 3 && NB <= 512;
+    }
     static constexpr int sw(int stage) {
         return !BCP_EH_MERGED ? words(stage)
-                              : ((stage == 0 ? words(0) + (LEAFSLOT ? 1 : 0) : words(stage) + 2) + BCP_EH_SLOT_ALIGN - 1) /
+                              : ((stage == 0 ? words(0) + (LEAFSLOT ? 1 : 0) : words(stage) + (cp(stage) ? 1 : 2)) +
+                                 BCP_EH_SLOT_ALIGN - 1) /
                                     BCP_EH_SLOT_ALIGN * BCP_EH_SLOT_ALIGN;
     }
     static constexpr size_t ROWS = (size_t)NB * AREA; // slots per stage per nonce
@@ -459,6 +469,15 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
 __device__ __forceinline__ uint64_t pack_tri(uint32_t d, uint32_t i, uint32_t j) {
     return ((uint64_t)d << 32) | (j << 16) | i;
 }
+// Compact parent word: i | j << 16 with bits 13-15 / 29-31 holding d's bits 0-2 / 3-5; d's bits
+// 6-8 ride in the low 3 bits of the row's last word (EhCfg::cp).
+__device__ __forceinline__ uint32_t cpack(uint32_t d, uint32_t i, uint32_t j) {
+    return i | (j << 16) | ((d & 7) << 13) | (((d >> 3) & 7) << 29);
+}
+__host__ __device__ __forceinline__ uint32_t cunpack_d(uint32_t pw, uint32_t lastword) {
+    return ((pw >> 13) & 7) | (((pw >> 29) & 7) << 3) | ((lastword & 7) << 6);
+}
+inline uint32_t cunpack_d_host(uint32_t pw, uint32_t lastword) { return cunpack_d(pw, lastword); }
 // 2 x 16-bit signature of a row's parents for depth-1 duplicate pruning: each half is the
 // parent's LDS row (13 bits) plus 3 bits of the producing bucket. A half shared by two rows is
 // confirmed exactly by comparing the full producing buckets: a signature-only prune would drop
@@ -643,6 +662,11 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             for (int u = 0; u < RPL; ++u) {
                 const uint32_t r = ot + u * NT;
                 if (r < n) {
+                    uint32_t lbits = 0;
+                    if constexpr (C::cp(STAGE - 1)) { // d's top bits out of the row's padding
+                        lbits = nr[u][WI - 1];
+                        nr[u][WI - 1] &= ~7u;
+                    }
                     if constexpr (WI % 2 == 0) {
 #pragma unroll
                         for (int w = 0; w < WI; w += 2)
@@ -652,8 +676,13 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                         for (int w = 0; w < WI; ++w) rows[r * WI + w] = nr[u][w];
                     }
                     if constexpr (PRUNE) {
-                        psig[r] = nr[u][WI];
-                        pdw[r] = (uint16_t)nr[u][WI + 1];
+                        if constexpr (C::cp(STAGE - 1)) {
+                            psig[r] = nr[u][WI] & 0x1fff1fffu;
+                            pdw[r] = (uint16_t)cunpack_d(nr[u][WI], lbits);
+                        } else {
+                            psig[r] = nr[u][WI];
+                            pdw[r] = (uint16_t)nr[u][WI + 1];
+                        }
                     }
                 }
             }
@@ -810,8 +839,13 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                     uint32_t ov[SWO] = {};
 #pragma unroll
                     for (int w = 0; w < WO; ++w) ov[w] = o[w];
-                    ov[WO] = (uint32_t)tri;
-                    ov[WO + 1] = (uint32_t)(tri >> 32);
+                    if constexpr (C::cp(STAGE)) {
+                        ov[WO - 1] |= (d >> 6) & 7;
+                        ov[WO] = cpack(d, i, j);
+                    } else {
+                        ov[WO] = (uint32_t)tri;
+                        ov[WO + 1] = (uint32_t)(tri >> 32);
+                    }
                     row_store<SWO>(rs_out, ok ? slot * (SWO * 4) : OOB, ov);
                 } else {
                     row_store<WO>(rs_out, ok ? slot * (WO * 4) : OOB, o);
@@ -874,7 +908,10 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
         if (s > 1 && t < 2 * cnt) {
             if constexpr (BCP_EH_MERGED) { // stage s-1 slot: row words, then the parent triple
                 const uint32_t* q = st.r[s - 1] + ((size_t)nonce * C::ROWS + buf[cur][t]) * C::sw(s - 1) + C::words(s - 1);
-                tri[t] = ((uint64_t)q[1] << 32) | q[0];
+                if (C::cp(s - 1))
+                    tri[t] = ((uint64_t)cunpack_d(q[0], q[-1]) << 32) | (q[0] & 0x1fff1fffu);
+                else
+                    tri[t] = ((uint64_t)q[1] << 32) | q[0];
             } else {
                 tri[t] = P[(size_t)(s - 2) * batch * C::ROWS + (size_t)nonce * C::ROWS + buf[cur][t]];
             }
@@ -984,7 +1021,8 @@ struct EquihashGpuSolver::Impl {
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
     std::vector<size_t> slot_words, row_words; // per stage
-    size_t leaf_slot_words = 0;                 // > 0: stage-0 slots carry the leaf index last
+    size_t leaf_slot_words = 0;
+    std::vector<bool> compact;                  // per stage: compact parent word                 // > 0: stage-0 slots carry the leaf index last
     int inflight = 0;
     int ncu = 1;
     bool debug = false, stamp_mode = false;
@@ -1000,9 +1038,11 @@ struct EquihashGpuSolver::Impl {
         caps.clear();
         for (int r = 1; r <= C::K; ++r) caps.push_back(C::cap(r));
         slot_words.clear();
+        compact.clear();
         row_words.clear();
         for (int st = 0; st < C::K; ++st) {
             slot_words.push_back(C::sw(st));
+            compact.push_back(C::cp(st));
             row_words.push_back(C::words(st));
         }
         kstages = C::K;
@@ -1225,7 +1265,11 @@ std::vector<uint64_t> EquihashGpuSolver::DebugDump() {
             const size_t sw = impl->slot_words[s], w = impl->row_words[s];
             std::vector<uint32_t> buf(R * sw);
             BCP_HIP_CHECK(hipMemcpy(buf.data(), impl->d_rst[s].p, R * sw * 4, hipMemcpyDeviceToHost));
-            for (size_t i = 0; i < R; ++i) out[s * R + i] = ((uint64_t)buf[i * sw + w + 1] << 32) | buf[i * sw + w];
+            for (size_t i = 0; i < R; ++i) {
+                const uint32_t* q = &buf[i * sw + w];
+                out[s * R + i] = impl->compact[s] ? ((uint64_t)bcpk::cunpack_d_host(q[0], q[-1]) << 32) | (q[0] & 0x1fff1fffu)
+                                                  : ((uint64_t)q[1] << 32) | q[0];
+            }
         }
     return out;
 }
