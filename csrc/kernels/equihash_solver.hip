@@ -1267,8 +1267,12 @@ std::vector<uint64_t> EquihashGpuSolver::DebugDump() {
             BCP_HIP_CHECK(hipMemcpy(buf.data(), impl->d_rst[s].p, R * sw * 4, hipMemcpyDeviceToHost));
             for (size_t i = 0; i < R; ++i) {
                 const uint32_t* q = &buf[i * sw + w];
-                out[s * R + i] = impl->compact[s] ? ((uint64_t)bcpk::cunpack_d_host(q[0], q[-1]) << 32) | (q[0] & 0x1fff1fffu)
-                                                  : ((uint64_t)q[1] << 32) | q[0];
+                if (impl->compact[s] && q[0] == 0xffffffffu) // never written (SetDebug fill): no row index is 0x1fff
+                    out[s * R + i] = ~0ull;
+                else
+                    out[s * R + i] = impl->compact[s]
+                                         ? ((uint64_t)bcpk::cunpack_d_host(q[0], q[-1]) << 32) | (q[0] & 0x1fff1fffu)
+                                         : ((uint64_t)q[1] << 32) | q[0];
             }
         }
     return out;

@@ -141,6 +141,32 @@ def test_gpu_solver_matches_cpu(native, n, k):
 
 
 @pytest.mark.gpu
+def test_gpu_solver_tree_dump_96_5(native):
+    """SetDebug + DebugDump decode the slot arrays (rows with compact or two-word parent triples):
+    every written stage-s (s >= 1) slot names a producing bucket < NB and two LDS rows < AREA of
+    it, every written stage-0 slot a leaf index < 2^(DB+1); never-written slots read all-ones."""
+    n, k, nb, area = 96, 5, 128, 1280
+    solver = native.EquihashGpuSolver(n, k, 1)
+    solver.set_debug(True)
+    st = native.EquihashState(n, k)
+    st.update(header_input(3, b"dump"))
+    sols = solver.solve([st])[0]
+    for s_ in sols:
+        assert native.eh_is_valid_solution(n, k, st, s_)[0]
+    dump = solver.debug_dump()
+    rows = len(dump) // k
+    assert rows == nb * area
+    leaves = [x for x in dump[:rows] if x != 0xFFFFFFFF]
+    assert len(leaves) > rows // 2 and max(leaves) < 1 << (n // (k + 1) + 1)
+    for stage in range(1, k):
+        tri = [x for x in dump[stage * rows:(stage + 1) * rows] if x != (1 << 64) - 1]
+        assert len(tri) > rows // 4, stage
+        for x in tri:
+            d, i, j = x >> 32, x & 0xFFFF, (x >> 16) & 0xFFFF
+            assert d < nb and i < area and j < area and i != j, (stage, hex(x))
+
+
+@pytest.mark.gpu
 def test_gpu_solver_200_9(native):
     solver = native.EquihashGpuSolver(200, 9, 2)
     states = []
