@@ -25,7 +25,7 @@ for b in $(ls "$GRAFT_REPO_ROOT/ab"); do
 done
 cd "$GRAFT_REPO_ROOT"
 unset BCP_NATIVE_PATH
-timeout -k 10 500 python -u tools/ab_bench.py --reps 3 ab/*/$EXT > "$O/ab.log" 2>&1
+timeout -k 10 500 python -u tools/ab_bench.py --reps ${REPS:-3} ab/*/$EXT > "$O/ab.log" 2>&1
 tail -n 6 "$O/ab.log"
 # PMC pass over the serial run of the first build (generation + rounds)
 if [ -n "$PMC_BUILD" ]; then
