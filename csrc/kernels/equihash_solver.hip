@@ -71,6 +71,15 @@
 #ifndef BCP_EH_COMPACT_PARENT // 1 (merged layout): one parent word where the row has 3 spare bits
 #define BCP_EH_COMPACT_PARENT 1
 #endif
+#ifndef BCP_EH_ST_CPOL // cache-policy bits of the slot stores (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
+#define BCP_EH_ST_CPOL 0
+#endif
+#ifndef BCP_EH_LD_CPOL // cache-policy bits of the slot loads
+#define BCP_EH_LD_CPOL 0
+#endif
+#ifndef BCP_EH_XCD_MAP // 1: every kernel of a nonce runs on one XCD (nonce % 8), so the run writes
+#define BCP_EH_XCD_MAP 1  //    of a nonce meet in one L2 (batches that are a multiple of 8 nonces)
+#endif
 #ifndef BCP_EH_EXP_NOPARENT // timing experiment only: emit stores no parent triples (no solutions)
 #define BCP_EH_EXP_NOPARENT 0
 #endif
@@ -245,32 +254,32 @@ __device__ void block_maxscan(T* v, int n, uint32_t* wsum) {
 template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint32_t* v) {
     if constexpr (W >= 4) {
         const u4v x = {v[0], v[1], v[2], v[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, BCP_EH_ST_CPOL);
         row_store<W - 4>(rs, off + 16, v + 4);
     } else if constexpr (W == 3) {
         const u3v x = {v[0], v[1], v[2]};
-        __builtin_amdgcn_raw_buffer_store_b96(x, rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b96(x, rs, off, 0, BCP_EH_ST_CPOL);
     } else if constexpr (W == 2) {
         const u2v x = {v[0], v[1]};
-        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, BCP_EH_ST_CPOL);
     } else if constexpr (W == 1) {
-        __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, BCP_EH_ST_CPOL);
     }
 }
 
 template <int W> __device__ __forceinline__ void row_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t* v) {
     if constexpr (W >= 4) {
-        const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
+        const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, BCP_EH_LD_CPOL);
         v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
         row_load<W - 4>(rs, off + 16, v + 4);
     } else if constexpr (W == 3) {
-        const u3v x = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
+        const u3v x = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, BCP_EH_LD_CPOL);
         v[0] = x.x, v[1] = x.y, v[2] = x.z;
     } else if constexpr (W == 2) {
-        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
+        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, BCP_EH_LD_CPOL);
         v[0] = x.x, v[1] = x.y;
     } else if constexpr (W == 1) {
-        v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
+        v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, BCP_EH_LD_CPOL);
     }
 }
 
@@ -294,6 +303,24 @@ template <int WI> __device__ __forceinline__ void lds_row_xor(const uint32_t* ro
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, uint32_t bytes) {
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, bytes, 0x00020000);
+}
+
+// XCD-aware work mapping. Workgroups are dispatched round-robin over the 8 XCDs (workgroup b
+// on XCD b % 8), and each XCD has its own L2. A producer writes runs into every destination
+// bucket of its nonce; a 128-byte line at a run boundary is shared by two producers. With all
+// workgroups of a nonce on the same XCD those partial lines merge in one L2 before they are
+// written back (non-temporal stores, which skip the L2 merge, measured 2x slower).
+constexpr int NXCD = 8;
+// it-th bucket of workgroup b among nbk = NB * nonces buckets (grid G); -1 when done.
+template <int NB> __device__ __forceinline__ int xcd_bucket(int b, int it, int G, int nbk) {
+    const int nonces = nbk / NB;
+    if (!BCP_EH_XCD_MAP || G % NXCD || nonces % NXCD) {
+        const int bk = b + it * G;
+        return bk < nbk ? bk : -1;
+    }
+    const int x = b % NXCD, j = b / NXCD + it * (G / NXCD);
+    if (j >= NB * (nonces / NXCD)) return -1;
+    return (x + NXCD * (j / NB)) * NB + j % NB;
 }
 
 // ------------------------------------------------------------------ stage 0
@@ -396,8 +423,13 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     constexpr int SW = (C::N + 31) / 32 + 1;
     constexpr uint32_t OCAP = C::cap(1);
     __shared__ uint32_t hist[C::NB], base[C::NB];
-    const int gw = blockIdx.x % G::GWG;
-    const int nonce = blockIdx.x / G::GWG;
+    int gw = blockIdx.x % G::GWG;
+    int nonce = blockIdx.x / G::GWG;
+    if (BCP_EH_XCD_MAP && (gridDim.x / G::GWG) % NXCD == 0) { // nonce n's workgroups on XCD n % 8
+        const int x = blockIdx.x % NXCD, j = blockIdx.x / NXCD;
+        gw = j % G::GWG;
+        nonce = x + NXCD * (j / G::GWG);
+    }
     const int tid = threadIdx.x;
     const EhBaseState& bs = states[nonce];
     for (int i = tid; i < C::NB; i += NTG) hist[i] = 0;
@@ -575,8 +607,9 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     uint32_t* spair = reinterpret_cast<uint32_t*>(un);
     const int tid = threadIdx.x;
     const int G = gridDim.x;
-    int bk = blockIdx.x;
-    if (bk >= nbk) return; // uniform per workgroup
+    int it = 0;
+    int bk = xcd_bucket<C::NB>(blockIdx.x, 0, G, nbk);
+    if (bk < 0) return; // uniform per workgroup
 
     // A thread id the compiler cannot see through: keeps the per-lane index math of the
     // prefetch/commit loops from being hoisted out of the persistent loop (live invariants
@@ -650,7 +683,8 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             if constexpr (!MG) __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rs_par, OOB + 256 * u, 0, 0);
         }
     }
-    uint32_t fill_next = (bk + G < nbk) ? CTRin[bk + G] : 0u;
+    const int bk1 = xcd_bucket<C::NB>(blockIdx.x, 1, G, nbk);
+    uint32_t fill_next = bk1 >= 0 ? CTRin[bk1] : 0u;
 
     for (;;) {
         const int nonce = bk / C::NB, d = bk % C::NB;
@@ -708,13 +742,14 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         for (int b = tid; b < C::NB; b += NT) hist[b] = 0;
         for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
         EH_STAMP(1);
-        const int bn = bk + G;
-        const bool more = bn < nbk; // uniform
+        const int bn = xcd_bucket<C::NB>(blockIdx.x, it + 1, G, nbk);
+        const bool more = bn >= 0; // uniform
         const uint32_t nn = more ? min(fill_next, (uint32_t)CAP) : 0u;
         pf_bk = more ? bn : bk;
         pf_n = nn;
         issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
-        fill_next = (bn + G < nbk) ? CTRin[bn + G] : 0u;
+        const int bn2 = xcd_bucket<C::NB>(blockIdx.x, it + 2, G, nbk);
+        fill_next = bn2 >= 0 ? CTRin[bn2] : 0u;
         __syncthreads();
         EH_STAMP(2);
 
@@ -860,6 +895,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         EH_STAMP(6);
         if (!more) break;
         bk = bn;
+        ++it;
         n = nn;
     }
 }

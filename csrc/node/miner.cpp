@@ -257,7 +257,8 @@ MinerStats GetMinerStats() {
 }
 
 namespace {
-// Two solvers per (device, N, K), kept across blocks: (200,9) at batch 32 holds ~9 GiB each.
+// Two solvers per (device, N, K), kept across blocks: (200,9) at batch 32 holds ~17 GiB each
+// (one slot array per stage, csrc/kernels/equihash_solver.hip).
 struct DeviceMiner {
     int device;
     unsigned n, k;
