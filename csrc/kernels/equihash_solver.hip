@@ -80,6 +80,9 @@
 #ifndef BCP_EH_XCD_MAP // 1: every kernel of a nonce runs on one XCD (nonce % 8), so the run writes
 #define BCP_EH_XCD_MAP 1  //    of a nonce meet in one L2 (batches that are a multiple of 8 nonces)
 #endif
+#ifndef BCP_EH_PF_SLICES // merged layout: the next bucket's rows are prefetched in this many slices
+#define BCP_EH_PF_SLICES 3
+#endif
 #ifndef BCP_EH_EXP_NOPARENT // timing experiment only: emit stores no parent triples (no solutions)
 #define BCP_EH_EXP_NOPARENT 0
 #endif
@@ -593,7 +596,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     constexpr int SWI = C::sw(STAGE - 1);                  // words per input slot
     constexpr int SWO = STAGE < C::K ? C::sw(STAGE) : 1;   // words per output slot
     constexpr int NI = MG ? RPL : NV;                      // prefetch units per lane
-    constexpr int SLI = MG ? (RPL + 2) / 3 : SL;           // prefetch slice (units per phase)
+    constexpr int SLI = MG ? (RPL + BCP_EH_PF_SLICES - 1) / BCP_EH_PF_SLICES : SL; // prefetch slice (units per phase)
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
     __shared__ uint32_t psig[PRUNE ? CAP : 1];                // merged: the parent's (j << 16) | i
     __shared__ uint16_t pdw[PRUNE ? CAP : 1];                 // producing bucket of each row
