@@ -460,6 +460,9 @@ __device__ __forceinline__ bool fe_lt_p(const fe& a) {
 }
 
 constexpr int WG = 128;
+#ifndef BCP_ECDSA_REGULAR // 1: regular window-3 recoding of the GLV halves (uniform additions)
+#define BCP_ECDSA_REGULAR 1
+#endif
 constexpr int WNAF_W = 4;              // odd multiples 1,3,5,7
 constexpr int NPRE = 1 << (WNAF_W - 2); // 4
 
@@ -477,7 +480,7 @@ struct Job {
     unsigned char nwnaf[2]; // digits of each half
     unsigned char neg[2];
     unsigned char scalar_ok; // set by the prep kernel: r, s in [1, n-1]
-    unsigned char pad[5];
+    unsigned char pad[5];    // regular recoding: pad[0], pad[1] = half 0 / 1 was even (encoded as k + 1)
 };
 // Host-filled input to the prep kernel (u1 <- z, rn <- s before prep).
 static_assert(sizeof(Job) == 272, "job layout");
@@ -583,6 +586,47 @@ __device__ __forceinline__ int wnaf4(unsigned char* out, const uint32_t (&m)[5])
     }
     return len;
 }
+// Regular signed-digit recoding with window 3 (BCP_ECDSA_REGULAR): an odd magnitude m < 2^130
+// becomes exactly REG_DIGITS digits, every one odd in [-7, 7] (never zero), m = sum d_i 8^i:
+// d = (m mod 16) - 8, m = (m - d) / 8 for the low digits, the remaining 1..7 on top. Every lane
+// then adds at the same positions, so a wave runs 2 x 44 point additions instead of one at
+// almost every bit (a width-4 wNAF digit is nonzero somewhere among 64 lanes at nearly every
+// position, and the divergent branch costs the whole wave).
+constexpr int REG_DIGITS = 44;
+__device__ __forceinline__ void regw3(unsigned char* out, const uint32_t (&m)[5]) {
+    uint32_t k[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) k[i] = m[i];
+    unsigned char cur = 0;
+    for (int b = 0; b < REG_DIGITS; b++) {
+        int d;
+        if (b == REG_DIGITS - 1) {
+            d = (int)k[0]; // 1..7
+        } else {
+            d = (int)(k[0] & 15) - 8;
+            // k -= d (k - d = 8 mod 16), then k >>= 3
+            const uint32_t addend = (uint32_t)(-d), ext = d > 0 ? 0xFFFFFFFFu : 0u;
+            uint64_t c = 0;
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                c += (uint64_t)k[i] + (i == 0 ? addend : ext);
+                k[i] = (uint32_t)c;
+                c >>= 32;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) k[i] = (k[i] >> 3) | (k[i + 1] << 29);
+            k[4] >>= 3;
+        }
+        const unsigned char nib = (unsigned char)(d & 15);
+        if (b & 1) {
+            out[b >> 1] = cur | (unsigned char)(nib << 4);
+            cur = 0;
+        } else {
+            cur = nib;
+        }
+    }
+}
+
 // 10-limb two's complement -> magnitude (5 limbs) and sign
 __device__ __forceinline__ bool abs10(uint32_t (&m)[5], uint32_t (&v)[10]) {
     const bool neg = (v[9] >> 31) != 0;
@@ -765,8 +809,22 @@ __global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs,
     uint32_t m1[5], m2[5];
     J.neg[0] = abs10(m1, k1) ? 1 : 0;
     J.neg[1] = abs10(m2, k2) ? 1 : 0;
+#if BCP_ECDSA_REGULAR
+    // an even half k is encoded as k + 1 and corrected by one subtraction of its point
+    auto make_odd = [](uint32_t (&m)[5]) -> unsigned char {
+        if (m[0] & 1) return 0;
+        m[0] |= 1; // even: + 1 never carries
+        return 1;
+    };
+    J.pad[0] = make_odd(m1);
+    J.pad[1] = make_odd(m2);
+    regw3(J.wnaf[0], m1);
+    regw3(J.wnaf[1], m2);
+    J.nwnaf[0] = J.nwnaf[1] = (unsigned char)REG_DIGITS;
+#else
     J.nwnaf[0] = (unsigned char)wnaf4(J.wnaf[0], m1);
     J.nwnaf[1] = (unsigned char)wnaf4(J.wnaf[1], m2);
+#endif
 }
 
 __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
@@ -820,12 +878,56 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
 
     // ---- u2*Q = k1*Q + k2*(lambda Q), both halves by interleaved width-4 wNAF; lambda*Q's
     //      multiples are Q's with X scaled by beta (same Y, Z)
-    const int len = max((int)J.nwnaf[0], (int)J.nwnaf[1]);
     fe beta;
 #pragma unroll
     for (int i = 0; i < 8; i++) beta.v[i] = GLV_BETA[i];
     gej acc;
     acc.inf = true;
+    // signed multiple dg (odd, |dg| <= 7) of half h's point: m = |dg| >> 1 indexes Q, 3Q, 5Q, 7Q;
+    // half 1 scales X by beta; the sign combines the digit's and the GLV half's (J.neg)
+    auto add_multiple = [&](int h, int dg) {
+        const int m = (dg > 0 ? dg : -dg) >> 1;
+        gej p;
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            p.x.v[k] = preX[m][k][tid];
+            p.y.v[k] = preY[m][k][tid];
+            p.z.v[k] = preZ[m][k][tid];
+        }
+        p.inf = false;
+        if (h == 1) fe_mul(p.x, p.x, beta);
+        if ((dg < 0) != (J.neg[h] != 0)) {
+            fe zero;
+#pragma unroll
+            for (int i = 0; i < 8; i++) zero.v[i] = 0;
+            fe_sub(p.y, zero, p.y);
+        }
+        gej s;
+        gej_add(s, acc, p);
+        acc = s;
+    };
+#if BCP_ECDSA_REGULAR
+    // ---- u2*Q = k1*Q + k2*(lambda Q): 44 regular window-3 digits per half, the same
+    //      positions in every lane (3 doublings + 2 additions per digit, no divergence)
+    for (int b = REG_DIGITS - 1; b >= 0; b--) {
+        if (b < REG_DIGITS - 1) {
+#pragma unroll
+            for (int t = 0; t < 3; t++) {
+                gej d;
+                gej_double(d, acc);
+                acc = d;
+            }
+        }
+        add_multiple(0, wnaf_digit(J, 0, b));
+        add_multiple(1, wnaf_digit(J, 1, b));
+    }
+    // halves that were even were encoded as k + 1: subtract their point once
+    for (int h = 0; h < 2; h++)
+        if (J.pad[h]) add_multiple(h, -1);
+#else
+    // ---- u2*Q = k1*Q + k2*(lambda Q), both halves by interleaved width-4 wNAF; lambda*Q's
+    //      multiples are Q's with X scaled by beta (same Y, Z)
+    const int len = max((int)J.nwnaf[0], (int)J.nwnaf[1]);
     for (int b = len - 1; b >= 0; b--) {
         gej d;
         gej_double(d, acc);
@@ -833,29 +935,10 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
 #pragma unroll
         for (int h = 0; h < 2; h++) {
             const int dg = wnaf_digit(J, h, b);
-            if (dg) {
-                const int m = (dg > 0 ? dg : -dg) >> 1;
-                gej p;
-#pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    p.x.v[k] = preX[m][k][tid];
-                    p.y.v[k] = preY[m][k][tid];
-                    p.z.v[k] = preZ[m][k][tid];
-                }
-                p.inf = false;
-                if (h == 1) fe_mul(p.x, p.x, beta);
-                if ((dg < 0) != (J.neg[h] != 0)) {
-                    fe zero;
-#pragma unroll
-                    for (int i = 0; i < 8; i++) zero.v[i] = 0;
-                    fe_sub(p.y, zero, p.y);
-                }
-                gej s;
-                gej_add(s, acc, p);
-                acc = s;
-            }
+            if (dg) add_multiple(h, dg);
         }
     }
+#endif
 
     // ---- + u1*G via byte-window comb table (affine, 16 words per entry)
     for (int i = 0; i < 32; i++) {

@@ -49,7 +49,7 @@ std::string HelpMessage() {
         {"-dbcache=<n>", "Set database cache size in megabytes (default: 450)"},
         {"-par=<n>", "Number of script verification threads (0 = auto)"},
         {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
-        {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 1024)"},
+        {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 512)"},
         {"-gpudevices=<list>", "Comma-separated GPU indices the built-in Equihash miner runs on, one host thread per device (default: all visible)"},
         {"-gpufaultinjection", "(testing) make every validation GPU batch fail so the CPU fallback runs (default: 0)"},
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},

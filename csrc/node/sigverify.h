@@ -48,8 +48,9 @@ struct SigVerifyStats {
 };
 
 // Smallest batch sent to the GPU (-gpusigthreshold). Below it the CPU pool is faster:
-// profiles/ecdsa_crossover.md measures the crossover on MI355X.
-static const size_t DEFAULT_GPU_SIG_THRESHOLD = 1024;
+// profiles/ecdsa_r2_regular.md measures the crossover on MI355X (between 256 and 512 signatures
+// with the regular-recoding verify kernel; it was 1024 before, profiles/ecdsa_crossover.md).
+static const size_t DEFAULT_GPU_SIG_THRESHOLD = 512;
 // Consecutive device failures after which the GPU signature path is turned off.
 static const int MAX_GPU_SIG_FAILURES = 3;
 
