@@ -265,6 +265,47 @@ __device__ __forceinline__ bool fe_eq(const fe& a, const fe& b) {
     return o == 0;
 }
 
+// x223 = a^(2^223 - 1), with x2 = a^3 and x22 = a^(2^22 - 1) on the way (libsecp256k1 chain).
+__device__ void fe_chain223(fe& x223, fe& x22, fe& x2, const fe& a) {
+    fe x3, x6, x9, x11, x44, x88, x176, x220;
+    fe_sqr(x2, a);
+    fe_mul(x2, x2, a);
+    fe_sqr(x3, x2);
+    fe_mul(x3, x3, a);
+    fe_sqr_n(x6, x3, 3);
+    fe_mul(x6, x6, x3);
+    fe_sqr_n(x9, x6, 3);
+    fe_mul(x9, x9, x3);
+    fe_sqr_n(x11, x9, 2);
+    fe_mul(x11, x11, x2);
+    fe_sqr_n(x22, x11, 11);
+    fe_mul(x22, x22, x11);
+    fe_sqr_n(x44, x22, 22);
+    fe_mul(x44, x44, x22);
+    fe_sqr_n(x88, x44, 44);
+    fe_mul(x88, x88, x44);
+    fe_sqr_n(x176, x88, 88);
+    fe_mul(x176, x176, x88);
+    fe_sqr_n(x220, x176, 44);
+    fe_mul(x220, x220, x44);
+    fe_sqr_n(x223, x220, 3);
+    fe_mul(x223, x223, x3);
+}
+
+// r = a^(p-2) = 1/a (a != 0): the p-2 blocks of ones are 223, 22, 1, 2, 1 bits long.
+__device__ void fe_inv(fe& r, const fe& a) {
+    fe x223, x22, x2, t1;
+    fe_chain223(x223, x22, x2, a);
+    fe_sqr_n(t1, x223, 23);
+    fe_mul(t1, t1, x22);
+    fe_sqr_n(t1, t1, 5);
+    fe_mul(t1, t1, a);
+    fe_sqr_n(t1, t1, 3);
+    fe_mul(t1, t1, x2);
+    fe_sqr_n(t1, t1, 2);
+    fe_mul(r, t1, a);
+}
+
 // r = a^((p+1)/4); returns whether r^2 == a (libsecp256k1 addition chain).
 __device__ __forceinline__ bool fe_sqrt(fe& r, const fe& a) {
     fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t1;
@@ -460,6 +501,9 @@ __device__ __forceinline__ bool fe_lt_p(const fe& a) {
 }
 
 constexpr int WG = 128;
+#ifndef BCP_ECDSA_AFFINE_TABLE // 1: the Q multiples are made affine (one batched inversion), LDS holds
+#define BCP_ECDSA_AFFINE_TABLE 1 //    X and Y only and every table addition is a mixed one
+#endif
 #ifndef BCP_ECDSA_REGULAR // 1: regular window-3 recoding of the GLV halves (uniform additions)
 #define BCP_ECDSA_REGULAR 1
 #endif
@@ -830,7 +874,8 @@ __global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs,
 __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
                                                           uint8_t* __restrict__ out, int n) {
     // word-major layout: lane-consecutive words -> conflict-free LDS access
-    __shared__ uint32_t preX[NPRE][8][WG], preY[NPRE][8][WG], preZ[NPRE][8][WG];
+    constexpr bool AFF = BCP_ECDSA_AFFINE_TABLE;
+    __shared__ uint32_t preX[NPRE][8][WG], preY[NPRE][8][WG], preZ[AFF ? 1 : NPRE][8][AFF ? 1 : WG];
     const int tid = threadIdx.x;
     const int idx = blockIdx.x * WG + tid;
     if (idx >= n) return;
@@ -864,16 +909,49 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
     gej q2;
     gej_double(q2, q1);
     gej cur = q1;
-    for (int m = 0; m < NPRE; m++) {
+    if constexpr (AFF) {
+        // Q, 3Q, 5Q, 7Q in Jacobian, then all four Z inverted with one inversion (Montgomery's
+        // trick) and stored affine: x = X/Z^2, y = Y/Z^3
+        gej mult[NPRE];
+        mult[0] = q1;
 #pragma unroll
-        for (int k = 0; k < 8; k++) {
-            preX[m][k][tid] = cur.x.v[k];
-            preY[m][k][tid] = cur.y.v[k];
-            preZ[m][k][tid] = cur.z.v[k];
+        for (int m = 1; m < NPRE; m++) gej_add(mult[m], mult[m - 1], q2);
+        fe pre[NPRE], inv;
+        pre[0] = mult[0].z;
+#pragma unroll
+        for (int m = 1; m < NPRE; m++) fe_mul(pre[m], pre[m - 1], mult[m].z);
+        fe_inv(inv, pre[NPRE - 1]);
+#pragma unroll
+        for (int m = NPRE - 1; m >= 0; m--) {
+            fe zi, zi2, zi3, ax, ay;
+            if (m > 0) {
+                fe_mul(zi, inv, pre[m - 1]);
+                fe_mul(inv, inv, mult[m].z);
+            } else {
+                zi = inv;
+            }
+            fe_sqr(zi2, zi);
+            fe_mul(zi3, zi2, zi);
+            fe_mul(ax, mult[m].x, zi2);
+            fe_mul(ay, mult[m].y, zi3);
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                preX[m][k][tid] = ax.v[k];
+                preY[m][k][tid] = ay.v[k];
+            }
         }
-        gej nx;
-        gej_add(nx, cur, q2);
-        cur = nx;
+    } else {
+        for (int m = 0; m < NPRE; m++) {
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                preX[m][k][tid] = cur.x.v[k];
+                preY[m][k][tid] = cur.y.v[k];
+                preZ[m][k][tid] = cur.z.v[k];
+            }
+            gej nx;
+            gej_add(nx, cur, q2);
+            cur = nx;
+        }
     }
 
     // ---- u2*Q = k1*Q + k2*(lambda Q), both halves by interleaved width-4 wNAF; lambda*Q's
@@ -892,7 +970,7 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
         for (int k = 0; k < 8; k++) {
             p.x.v[k] = preX[m][k][tid];
             p.y.v[k] = preY[m][k][tid];
-            p.z.v[k] = preZ[m][k][tid];
+            if constexpr (!AFF) p.z.v[k] = preZ[m][k][tid];
         }
         p.inf = false;
         if (h == 1) fe_mul(p.x, p.x, beta);
@@ -903,7 +981,10 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
             fe_sub(p.y, zero, p.y);
         }
         gej s;
-        gej_add(s, acc, p);
+        if constexpr (AFF)
+            gej_add_ge(s, acc, p.x, p.y);
+        else
+            gej_add(s, acc, p);
         acc = s;
     };
 #if BCP_ECDSA_REGULAR
