@@ -19,7 +19,7 @@ PY_EXT     := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_
 CXXFLAGS   := -std=c++17 $(OPT) -g1 -fPIC -Wall -Wno-unused-function -Wno-sign-compare -Icsrc -pthread
 HIPFLAGS   := -std=c++17 $(OPT) -fPIC --offload-arch=$(GPU_ARCH) -Icsrc -munsafe-fp-atomics \
               -Wno-unused-result -Wno-unused-variable -Wno-pass-failed
-LDLIBS     := -L$(ROCM)/lib -lamdhip64 -pthread -ldl -Wl,-rpath,$(ROCM)/lib
+LDLIBS     := -L$(ROCM)/lib -lamdhip64 -lcrypto -pthread -ldl -Wl,-rpath,$(ROCM)/lib
 
 CORE_SRCS  := $(wildcard csrc/crypto/*.cpp csrc/primitives/*.cpp csrc/consensus/*.cpp \
                 csrc/script/*.cpp csrc/secp256k1/*.cpp csrc/util/*.cpp csrc/node/*.cpp \

@@ -22,6 +22,7 @@ void bind_gpu(pyb::module_& m);
 void bind_consensus(pyb::module_& m);
 void bind_script(pyb::module_& m);
 void bind_node(pyb::module_& m);
+void bind_payments(pyb::module_& m);
 
 } // namespace py
 } // namespace bcp

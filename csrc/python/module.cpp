@@ -10,4 +10,5 @@ PYBIND11_MODULE(_bcpnative, m) {
     bcp::py::bind_consensus(m);
     bcp::py::bind_script(m);
     bcp::py::bind_node(m);
+    bcp::py::bind_payments(m);
 }

@@ -37,7 +37,10 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 <label><input type="checkbox" id="sendsub"> subtract fee from amount</label>
 <div>Comment</div><input class="wide" id="sendcomment">
 <div id="passrow" style="display:none">Wallet passphrase <input type="password" id="sendpass"></div>
-<p><button class="act" onclick="doSend()">Send</button> <span id="sendres"></span></p></div></section>
+<p><button class="act" onclick="doSend()">Send</button> <span id="sendres"></span></p></div>
+<div class="card"><div>BIP70 payment request (hex or base64)</div><textarea class="wide" id="preq" rows="3"></textarea>
+<p><button onclick="checkReq()">Check</button> <button class="act" onclick="payReq()">Pay request</button> <span id="preqres"></span></p>
+<div id="preqinfo"></div></div></section>
 <section id="receive"><div class="card">Label <input id="rcvlabel"> <button class="act" onclick="newAddr()">New address</button>
 <p class="mono big" id="newaddr"></p></div>
 <div class="card"><b>Receiving addresses</b><table><thead><tr><th>Address</th><th>Label</th><th>Received</th><th>Conf.</th></tr></thead><tbody id="rcvlist"></tbody></table></div></section>
@@ -91,6 +94,17 @@ async function doSend(){
     $("sendres").innerHTML="<span class='ok'>sent "+esc(txid)+"</span>";$("sendpass").value="";
   }catch(e){ if(e.code==-13) $("passrow").style.display="block";
     $("sendres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function checkReq(){$("preqres").textContent="";
+  try{const r=await rpc("decodepaymentrequest",[$("preq").value.trim()]);
+    const who=r.merchant?"<span class='ok'>"+esc(r.merchant)+"</span>":"<span class='err'>unauthenticated"+(r.merchant_error?" ("+esc(r.merchant_error)+")":"")+"</span>";
+    $("preqinfo").innerHTML="Merchant: "+who+"<br>Memo: "+esc(r.memo)+"<br>Pay: "+r.outputs.map(o=>esc(o.address||o.script)+" "+amt(o.amount)).join(", ")+
+      (r.network_ok?"":"<br><span class='err'>network "+esc(r.network)+" does not match</span>")+(r.expired?"<br><span class='err'>expired</span>":"");
+  }catch(e){$("preqres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function payReq(){$("preqres").textContent="";
+  try{const pass=$("sendpass").value; if(pass) await rpc("walletpassphrase",[pass,60]);
+    const r=await rpc("sendpaymentrequest",[$("preq").value.trim()]);
+    $("preqres").innerHTML="<span class='ok'>paid "+esc(r.txid)+(r.payment_url?" (send the Payment to "+esc(r.payment_url)+")":"")+"</span>";
+  }catch(e){ if(e.code==-13) $("passrow").style.display="block"; $("preqres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
 async function newAddr(){try{$("newaddr").textContent=await rpc("getnewaddress",[$("rcvlabel").value]);refresh("receive");}
   catch(e){$("newaddr").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
 async function doGenerate(){$("genres").textContent="mining…";

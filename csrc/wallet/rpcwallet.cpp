@@ -18,6 +18,7 @@
 #include "rpc/core_io.h"
 #include "rpc/server.h"
 #include "util/strencodings.h"
+#include "wallet/paymentrequest.h"
 #include "wallet/wallet.h"
 
 #include <fstream>
@@ -1363,6 +1364,148 @@ static UniValue removeprunedfunds(const JSONRPCRequest& req) {
     return UniValue::NullUniValue;
 }
 
+// ---- BIP70 payment requests (reference src/qt/paymentserver.cpp processPaymentRequest :579-690,
+// PaymentServer::fetchPaymentACK :692-760; the Qt dialog flow becomes two RPCs here).
+static payments::PaymentRequestPlus ParsePaymentRequestParam(const UniValue& v, bool* sizeOk = nullptr) {
+    const std::string in = v.get_str();
+    std::vector<unsigned char> raw;
+    if (IsHex(in)) {
+        raw = ParseHex(in);
+    } else {
+        bool invalid = false;
+        raw = DecodeBase64(in, &invalid);
+        if (invalid) ThrowRPC(RPC_DESERIALIZATION_ERROR, "Payment request is neither hex nor base64");
+    }
+    if (sizeOk) *sizeOk = payments::VerifySize((int64_t)raw.size());
+    else if (!payments::VerifySize((int64_t)raw.size()))
+        ThrowRPC(RPC_INVALID_PARAMETER, strprintf("Payment request too large (%u bytes, allowed %d bytes)",
+                                                  (unsigned)raw.size(), (int)payments::BIP70_MAX_PAYMENTREQUEST_SIZE));
+    payments::PaymentRequestPlus pr;
+    if (!pr.parse(std::string(raw.begin(), raw.end())))
+        ThrowRPC(RPC_DESERIALIZATION_ERROR, "Payment request is not initialized (parse error)");
+    return pr;
+}
+
+static payments::CertStore RootCertStore() {
+    payments::CertStore cs;
+    std::string err;
+    if (!payments::LoadRootCertificates(gArgs.GetArg("-rootcertificates", "-system-"), cs, err))
+        ThrowRPC(RPC_MISC_ERROR, err);
+    cs.allow_self_signed_root = gArgs.GetBoolArg("-allowselfsignedrootcertificates", payments::DEFAULT_SELFSIGNED_ROOTCERTS);
+    return cs;
+}
+
+static UniValue decodepaymentrequest(const JSONRPCRequest& req) {
+    if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "decodepaymentrequest \"request\"");
+    bool sizeOk = true;
+    const payments::PaymentRequestPlus pr = ParsePaymentRequestParam(req.params[0], &sizeOk);
+    const payments::PaymentDetails& d = pr.getDetails();
+    UniValue r(UniValue::VOBJ);
+    r.pushKV("payment_details_version", (int64_t)pr.getRequest().payment_details_version);
+    r.pushKV("pki_type", pr.getRequest().pki_type);
+    std::string merchant, merr;
+    if (pr.getRequest().pki_type != "none") {
+        if (!pr.getMerchant(RootCertStore(), merchant, &merr)) r.pushKV("merchant_error", merr);
+    }
+    r.pushKV("merchant", merchant);
+    r.pushKV("network", d.network);
+    r.pushKV("network_ok", payments::VerifyNetwork(d, P().NetworkIDString()));
+    r.pushKV("time", (int64_t)d.time);
+    if (d.has_expires) r.pushKV("expires", (int64_t)d.expires);
+    r.pushKV("expired", payments::VerifyExpired(d, GetTime()));
+    r.pushKV("size_ok", sizeOk);
+    r.pushKV("memo", d.memo);
+    r.pushKV("payment_url", d.payment_url);
+    r.pushKV("merchant_data", HexStr(d.merchant_data.begin(), d.merchant_data.end()));
+    UniValue outs(UniValue::VARR);
+    Amount total = 0;
+    bool amountsOk = true;
+    for (const auto& [script, amount] : pr.getPayTo()) {
+        UniValue o(UniValue::VOBJ);
+        o.pushKV("amount", ValueFromAmount(amount));
+        o.pushKV("amount_ok", payments::VerifyAmount(amount));
+        amountsOk &= payments::VerifyAmount(amount);
+        total += amount;
+        CTxDestination dest;
+        if (ExtractDestination(script, dest)) o.pushKV("address", EncodeDestination(dest, P()));
+        o.pushKV("script", HexStr(script.begin(), script.end()));
+        o.pushKV("dust", IsDust(CTxOut(amount, script), dustRelayFee));
+        outs.push_back(o);
+    }
+    r.pushKV("outputs", outs);
+    r.pushKV("total_ok", amountsOk && payments::VerifyAmount(total));
+    return r;
+}
+
+static UniValue sendpaymentrequest(const JSONRPCRequest& req) {
+    CWallet& w = Wallet(req);
+    if (req.params.size() < 1 || req.params.size() > 2) ThrowRPC(RPC_INVALID_PARAMS, "sendpaymentrequest \"request\" ( \"memo\" )");
+    const payments::PaymentRequestPlus pr = ParsePaymentRequestParam(req.params[0]);
+    const payments::PaymentDetails& d = pr.getDetails();
+    if (!payments::VerifyNetwork(d, P().NetworkIDString()))
+        ThrowRPC(RPC_INVALID_PARAMETER, "Payment request rejected: network doesn't match client network");
+    if (payments::VerifyExpired(d, GetTime())) ThrowRPC(RPC_INVALID_PARAMETER, "Payment request rejected: expired");
+    std::string merchant;
+    if (pr.getRequest().pki_type != "none") {
+        std::string merr;
+        if (!pr.getMerchant(RootCertStore(), merchant, &merr))
+            ThrowRPC(RPC_INVALID_PARAMETER, "Payment request rejected: merchant authentication failed: " + merr);
+    }
+    std::vector<CRecipient> vecSend;
+    Amount total = 0;
+    for (const auto& [script, amount] : pr.getPayTo()) {
+        if (!payments::VerifyAmount(amount)) ThrowRPC(RPC_INVALID_PARAMETER, "Payment request rejected: invalid amount");
+        if (IsDust(CTxOut(amount, script), dustRelayFee))
+            ThrowRPC(RPC_INVALID_PARAMETER, "Requested payment amount is too small (considered dust)");
+        total += amount;
+        if (!payments::VerifyAmount(total)) ThrowRPC(RPC_INVALID_PARAMETER, "Payment request rejected: invalid amount");
+        vecSend.push_back({script, amount, false});
+    }
+    if (vecSend.empty()) ThrowRPC(RPC_INVALID_PARAMETER, "Payment request has no outputs");
+    EnsureWalletIsUnlocked(w);
+    CWalletTx wtx;
+    if (!d.memo.empty()) wtx.mapValue["PaymentRequest"] = d.memo;
+    if (!merchant.empty()) wtx.mapValue["to"] = merchant;
+    CReserveKey rk(&w);
+    Amount fee = 0;
+    int changePos = -1;
+    std::string err;
+    if (!w.CreateTransaction(vecSend, wtx, rk, fee, changePos, err)) ThrowRPC(RPC_WALLET_INSUFFICIENT_FUNDS, err);
+    CValidationState state;
+    if (!w.CommitTransaction(wtx, rk, state))
+        ThrowRPC(RPC_WALLET_ERROR, "Transaction commit failed:: " + state.GetRejectReason());
+    // BIP70 Payment for the merchant's payment_url: merchant_data echoed, the signed
+    // transaction, and a fresh refund address.
+    payments::Payment pay;
+    pay.has_merchant_data = d.has_merchant_data;
+    pay.merchant_data = d.merchant_data;
+    const std::string txhex = EncodeHexTx(*wtx.tx);
+    const std::vector<unsigned char> txraw = ParseHex(txhex);
+    pay.transactions.emplace_back(txraw.begin(), txraw.end());
+    CPubKey refundKey;
+    if (w.GetKeyFromPool(refundKey)) {
+        const CScript s = GetScriptForDestination(CTxDestination(refundKey.GetID()));
+        payments::Output o;
+        o.has_script = true;
+        o.script.assign(s.begin(), s.end());
+        pay.refund_to.push_back(o);
+    }
+    if (req.params.size() > 1 && !req.params[1].isNull() && !req.params[1].get_str().empty()) {
+        pay.has_memo = true;
+        pay.memo = req.params[1].get_str();
+    }
+    const std::string payment = payments::SerializePayment(pay);
+    UniValue r(UniValue::VOBJ);
+    r.pushKV("txid", wtx.GetHash().GetHex());
+    r.pushKV("merchant", merchant);
+    r.pushKV("amount", ValueFromAmount(total));
+    r.pushKV("fee", ValueFromAmount(fee));
+    r.pushKV("payment_url", d.payment_url);
+    r.pushKV("payment", HexStr(payment.begin(), payment.end()));
+    r.pushKV("payment_mimetype", payments::BIP71_MIMETYPE_PAYMENT);
+    return r;
+}
+
 void RegisterWalletRPCCommands(CRPCTable& t) {
     const CRPCCommand cmds[] = {
         {"rawtransactions", "fundrawtransaction", fundrawtransaction, false, {"hexstring", "options"}, "fundrawtransaction \"hexstring\" ( options )\nAdd inputs to a transaction until it has enough in value to meet its out value."},
@@ -1370,6 +1513,8 @@ void RegisterWalletRPCCommands(CRPCTable& t) {
         {"wallet", "abandontransaction", abandontransaction, false, {"txid"}, "abandontransaction \"txid\"\nMark in-wallet transaction <txid> as abandoned."},
         {"wallet", "addmultisigaddress", addmultisigaddress, true, {"nrequired", "keys", "account"}, "addmultisigaddress nrequired [\"key\",...] ( \"account\" )\nAdd a nrequired-to-sign multisignature address to the wallet."},
         {"wallet", "backupwallet", backupwallet, true, {"destination"}, "backupwallet \"destination\"\nSafely copies current wallet file to destination."},
+        {"wallet", "decodepaymentrequest", decodepaymentrequest, true, {"request"}, "decodepaymentrequest \"request\"\nDecode and check a BIP70 payment request (hex or base64): merchant authentication, network, expiry, amounts."},
+        {"wallet", "sendpaymentrequest", sendpaymentrequest, false, {"request", "memo"}, "sendpaymentrequest \"request\" ( \"memo\" )\nPay a BIP70 payment request and return the BIP70 Payment message for its payment_url."},
         {"wallet", "dumpprivkey", dumpprivkey, true, {"address"}, "dumpprivkey \"address\"\nReveals the private key corresponding to 'address'."},
         {"wallet", "dumpwallet", dumpwallet, true, {"filename"}, "dumpwallet \"filename\"\nDumps all wallet keys in a human-readable format."},
         {"wallet", "encryptwallet", encryptwallet, true, {"passphrase"}, "encryptwallet \"passphrase\"\nEncrypts the wallet with 'passphrase'."},

@@ -37,6 +37,8 @@ std::string WalletHelp() {
         {"-usehd", "Use hierarchical deterministic key generation (HD) after BIP32. Only has effect during wallet creation/first start (default: 1)"},
         {"-wallet=<file>", "Specify wallet store (within data directory) (default: wallet.dat)"},
         {"-walletbroadcast", "Make the wallet broadcast transactions (default: 1)"},
+        {"-rootcertificates=<file>", "Root certificates for BIP70 payment request merchant authentication, PEM or DER (default: -system-)"},
+        {"-allowselfsignedrootcertificates", "Accept a self-signed merchant certificate in BIP70 payment requests (default: 0)"},
         {"-walletnotify=<cmd>", "Execute command when a wallet transaction changes (%s in cmd is replaced by TxID)"},
         {"-zapwallettxes", "Delete all wallet transactions and only recover those parts of the blockchain through -rescan on startup"},
     };
