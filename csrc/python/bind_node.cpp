@@ -3,6 +3,7 @@
 #include "node/node.h"
 #include "node/ui_interface.h"
 #include "python/bind.h"
+#include "rpc/console.h"
 #include "rpc/server.h"
 #include "util/cuckoocache.h"
 #include "util/indirectmap.h"
@@ -262,6 +263,22 @@ void bind_node(pyb::module_& m) {
         SetLockOrderChecking(was, true);
         return pyb::make_tuple(mid - before, LockOrderViolations() - before);
     });
+    // RPC console line parser with a Python executor: executor(method, [str args]) returns the
+    // call's result as JSON text (None: parse and filter only). Returns (result, filtered).
+    m.def(
+        "console_parse",
+        [](const std::string& line, pyb::object executor) {
+            std::string result, filtered;
+            ConsoleExecutor exec = [&](const std::string& method, const std::vector<std::string>& args) {
+                const std::string js = executor(method, args).cast<std::string>();
+                UniValue v;
+                if (!v.read(js)) throw std::invalid_argument("executor must return JSON");
+                return v;
+            };
+            RPCParseCommandLine(result, line, executor.is_none() ? nullptr : &exec, &filtered);
+            return pyb::make_tuple(result, filtered);
+        },
+        pyb::arg("line"), pyb::arg("executor") = pyb::none());
     // JSON in, JSON out: {"result": ..., "error": ...}
     m.def("rpc_json", [](const std::string& method, const std::string& paramsJson) {
         std::string out;

@@ -3,6 +3,7 @@
 // setmocktime, echo, echojson), src/rpc/server.cpp (help, stop, uptime) and
 // src/rpc/abc.cpp (getexcessiveblock/setexcessiveblock, :77).
 #include "keys/key.h"
+#include "rpc/console.h"
 #include "node/node.h"
 #include "node/policy.h"
 #include "node/sigverify.h"
@@ -246,8 +247,37 @@ static UniValue setexcessiveblock(const JSONRPCRequest& req) {
     return "Excessive Block set to " + std::to_string(ebs) + " bytes.";
 }
 
+// Console line execution for the browser GUI console (reference Qt RPCConsole::RPCExecuteCommandLine):
+// nested calls, [key] result queries, and the history-filtered form of the line.
+static UniValue execconsole(const JSONRPCRequest& req) {
+    if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "execconsole \"line\"");
+    const std::string line = req.params[0].get_str();
+    UniValue r(UniValue::VOBJ);
+    std::string filtered, result;
+    // the history form is computed without executing, so it exists even when execution fails
+    try {
+        std::string dummy;
+        RPCParseCommandLine(dummy, line, nullptr, &filtered);
+    } catch (const std::runtime_error&) {
+        filtered = IsSensitiveConsoleCommand(line.substr(0, line.find_first_of(" (\t"))) ? "" : line;
+    }
+    const ConsoleExecutor exec = [](const std::string& m, const std::vector<std::string>& a) {
+        if (m == "execconsole") ThrowRPC(RPC_INVALID_PARAMETER, "execconsole cannot be nested");
+        return ConsoleExecuteRPC(m, a);
+    };
+    try {
+        RPCParseCommandLine(result, line, &exec);
+    } catch (const std::runtime_error& e) {
+        ThrowRPC(RPC_PARSE_ERROR, e.what());
+    }
+    r.pushKV("result", result);
+    r.pushKV("filtered", filtered);
+    return r;
+}
+
 void RegisterMiscRPCCommands(CRPCTable& t) {
     const CRPCCommand cmds[] = {
+        {"hidden", "execconsole", execconsole, true, {"line"}, "execconsole \"line\"\nRun one RPC console line (nested calls such as getblock(getbestblockhash())[tx][0]); returns the result and the history-filtered line."},
         {"control", "help", help, true, {"command"}, "help ( \"command\" )\nList all commands, or get help for a specified command."},
         {"control", "stop", stop, true, {}, "stop\nStop Bitcoin Cash Plus server."},
         {"control", "uptime", uptime, true, {}, "uptime\nReturns the total uptime of the server."},

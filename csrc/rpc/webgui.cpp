@@ -111,19 +111,18 @@ async function doGenerate(){$("genres").textContent="mining…";
   try{const h=await rpc("generate",[Number($("gencount").value)]);$("genres").innerHTML="<span class='ok'>"+h.length+" block(s)</span>";refresh("mining");}
   catch(e){$("genres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
 const hist=[];let hpos=0;
-function parseArgs(s){const out=[];const re=/"((?:[^"\\]|\\.)*)"|(\S+)/g;let m;
-  while((m=re.exec(s))){const tok=m[1]!==undefined?m[1]:m[2];
-    if(m[1]!==undefined){out.push(tok);continue;}
-    try{out.push(JSON.parse(tok));}catch(_){out.push(tok);}}
-  return out;}
 $("conin").addEventListener("keydown",async ev=>{
   if(ev.key=="ArrowUp"&&hpos>0){$("conin").value=hist[--hpos];return;}
   if(ev.key=="ArrowDown"&&hpos<hist.length){hpos++;$("conin").value=hist[hpos]||"";return;}
   if(ev.key!="Enter") return;
-  const line=$("conin").value.trim(); if(!line) return; hist.push(line);hpos=hist.length;$("conin").value="";
-  const [m,...args]=parseArgs(line); let text;
-  try{const r=await rpc(String(m),args);text=typeof r=="string"?r:JSON.stringify(r,null,2);}catch(e){text="error "+e.code+": "+e.message;}
-  $("conout").textContent+="> "+line+"\n"+text+"\n\n";$("conout").scrollTop=1e9;});
+  const line=$("conin").value.trim(); if(!line) return; $("conin").value="";
+  let text,shown=line;
+  // the node parses the line (nested calls, [key] queries) and returns the history-safe form
+  try{const r=await rpc("execconsole",[line]);text=r.result;shown=r.filtered;}catch(e){text="error "+e.code+": "+e.message;}
+  // a line that failed to parse still keeps secrets out of the history
+  if(/^(importprivkey|importmulti|signmessagewithprivkey|signrawtransaction|walletpassphrase|walletpassphrasechange|encryptwallet)\b/i.test(shown)&&shown==line) shown=shown.split(/[ (]/)[0]+"(…)";
+  hist.push(shown);hpos=hist.length;
+  $("conout").textContent+="> "+shown+"\n"+text+"\n\n";$("conout").scrollTop=1e9;});
 show("overview");setInterval(()=>refresh(),5000);
 </script></body></html>
 )BCPGUI";
