@@ -1,5 +1,6 @@
 // Python bindings: BIP70 payment protocol (wallet/paymentrequest.h) for tests.
 #include "python/bind.h"
+#include "wallet/bitcoinuri.h"
 #include "wallet/paymentrequest.h"
 
 namespace bcp {
@@ -110,6 +111,30 @@ void bind_payments(pyb::module_& m) {
         q.signature = std::string(sig);
         q.has_signature = true;
         return pyb::bytes(SerializePaymentRequest(q));
+    });
+    // BIP21 URIs: (ok, address, amount, label, message, r)
+    m.def("parse_bitcoin_uri", [](const std::string& scheme, const std::string& uri) {
+        SendCoinsRecipient r;
+        const bool ok = ParseBitcoinURI(scheme, uri, &r);
+        return pyb::make_tuple(ok, r.address, r.amount, r.label, r.message, r.paymentRequestUrl);
+    });
+    m.def(
+        "format_bitcoin_uri",
+        [](const std::string& address, Amount amount, const std::string& label, const std::string& message,
+           bool useCashAddr) {
+            SendCoinsRecipient r;
+            r.address = address;
+            r.amount = amount;
+            r.label = label;
+            r.message = message;
+            return FormatBitcoinURI(r, useCashAddr);
+        },
+        pyb::arg("address"), pyb::arg("amount") = 0, pyb::arg("label") = "", pyb::arg("message") = "",
+        pyb::arg("use_cashaddr") = true);
+    m.def("parse_coin_amount", [](const std::string& t) -> pyb::object {
+        Amount a;
+        if (!ParseCoinAmount(t, &a)) return pyb::none();
+        return pyb::cast(a);
     });
     // Payment / PaymentACK round trips (what sendpaymentrequest hands back for payment_url).
     m.def("payment_decode", [](const pyb::bytes& data) {

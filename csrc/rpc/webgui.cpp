@@ -89,6 +89,10 @@ async function refresh(id){current=id||current;
 async function doSend(){
   $("sendres").textContent="";
   try{
+    const to=$("sendto").value.trim();
+    if(to.includes(":")&&to.includes("?")){const u=await rpc("parsebitcoinuri",[to]);$("sendto").value=u.address;
+      if(u.amount>0)$("sendamt").value=u.amount; if(u.message)$("sendcomment").value=u.message;
+      $("sendres").innerHTML="<span class='ok'>filled from URI — check and press Send</span>";return;}
     const pass=$("sendpass").value; if(pass) await rpc("walletpassphrase",[pass,60]);
     const txid=await rpc("sendtoaddress",[$("sendto").value.trim(),Number($("sendamt").value),$("sendcomment").value,"",$("sendsub").checked]);
     $("sendres").innerHTML="<span class='ok'>sent "+esc(txid)+"</span>";$("sendpass").value="";
@@ -105,7 +109,8 @@ async function payReq(){$("preqres").textContent="";
     const r=await rpc("sendpaymentrequest",[$("preq").value.trim()]);
     $("preqres").innerHTML="<span class='ok'>paid "+esc(r.txid)+(r.payment_url?" (send the Payment to "+esc(r.payment_url)+")":"")+"</span>";
   }catch(e){ if(e.code==-13) $("passrow").style.display="block"; $("preqres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
-async function newAddr(){try{$("newaddr").textContent=await rpc("getnewaddress",[$("rcvlabel").value]);refresh("receive");}
+async function newAddr(){try{const a=await rpc("getnewaddress",[$("rcvlabel").value]);
+  $("newaddr").textContent=a+"  "+await rpc("formatbitcoinuri",[a,null,$("rcvlabel").value]);refresh("receive");}
   catch(e){$("newaddr").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
 async function doGenerate(){$("genres").textContent="mining…";
   try{const h=await rpc("generate",[Number($("gencount").value)]);$("genres").innerHTML="<span class='ok'>"+h.length+" block(s)</span>";refresh("mining");}

@@ -18,6 +18,7 @@
 #include "rpc/core_io.h"
 #include "rpc/server.h"
 #include "util/strencodings.h"
+#include "wallet/bitcoinuri.h"
 #include "wallet/paymentrequest.h"
 #include "wallet/wallet.h"
 
@@ -1506,6 +1507,36 @@ static UniValue sendpaymentrequest(const JSONRPCRequest& req) {
     return r;
 }
 
+// ---- BIP21 URIs (reference src/qt/guiutil.cpp parseBitcoinURI / formatBitcoinURI; the GUI's
+// send and receive pages use these).
+static UniValue parsebitcoinuri(const JSONRPCRequest& req) {
+    if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "parsebitcoinuri \"uri\"");
+    SendCoinsRecipient r;
+    const std::string uri = req.params[0].get_str();
+    if (!ParseBitcoinURI(BitcoinURIScheme(true), uri, &r) && !ParseBitcoinURI(BitcoinURIScheme(false), uri, &r))
+        ThrowRPC(RPC_INVALID_PARAMETER, "Invalid or unsupported payment URI");
+    UniValue o(UniValue::VOBJ);
+    o.pushKV("address", r.address);
+    o.pushKV("isvalid", DecodeDestination(r.address, P()).IsValid());
+    o.pushKV("amount", ValueFromAmount(r.amount));
+    o.pushKV("label", r.label);
+    o.pushKV("message", r.message);
+    if (!r.paymentRequestUrl.empty()) o.pushKV("r", r.paymentRequestUrl);
+    return o;
+}
+
+static UniValue formatbitcoinuri(const JSONRPCRequest& req) {
+    if (req.params.size() < 1 || req.params.size() > 4)
+        ThrowRPC(RPC_INVALID_PARAMS, "formatbitcoinuri \"address\" ( amount \"label\" \"message\" )");
+    SendCoinsRecipient r;
+    const CTxDestination d = ParseDest(req.params[0].get_str());
+    r.address = EncodeDestination(d, P());
+    if (req.params.size() > 1 && !req.params[1].isNull()) r.amount = AmountFromValue(req.params[1]);
+    if (req.params.size() > 2 && !req.params[2].isNull()) r.label = req.params[2].get_str();
+    if (req.params.size() > 3 && !req.params[3].isNull()) r.message = req.params[3].get_str();
+    return FormatBitcoinURI(r, UseCashAddr());
+}
+
 void RegisterWalletRPCCommands(CRPCTable& t) {
     const CRPCCommand cmds[] = {
         {"rawtransactions", "fundrawtransaction", fundrawtransaction, false, {"hexstring", "options"}, "fundrawtransaction \"hexstring\" ( options )\nAdd inputs to a transaction until it has enough in value to meet its out value."},
@@ -1515,6 +1546,8 @@ void RegisterWalletRPCCommands(CRPCTable& t) {
         {"wallet", "backupwallet", backupwallet, true, {"destination"}, "backupwallet \"destination\"\nSafely copies current wallet file to destination."},
         {"wallet", "decodepaymentrequest", decodepaymentrequest, true, {"request"}, "decodepaymentrequest \"request\"\nDecode and check a BIP70 payment request (hex or base64): merchant authentication, network, expiry, amounts."},
         {"wallet", "sendpaymentrequest", sendpaymentrequest, false, {"request", "memo"}, "sendpaymentrequest \"request\" ( \"memo\" )\nPay a BIP70 payment request and return the BIP70 Payment message for its payment_url."},
+        {"wallet", "parsebitcoinuri", parsebitcoinuri, true, {"uri"}, "parsebitcoinuri \"uri\"\nSplit a BIP21 payment URI into address, amount, label, message (and BIP72 r)."},
+        {"wallet", "formatbitcoinuri", formatbitcoinuri, true, {"address", "amount", "label", "message"}, "formatbitcoinuri \"address\" ( amount \"label\" \"message\" )\nBuild a BIP21 payment URI."},
         {"wallet", "dumpprivkey", dumpprivkey, true, {"address"}, "dumpprivkey \"address\"\nReveals the private key corresponding to 'address'."},
         {"wallet", "dumpwallet", dumpwallet, true, {"filename"}, "dumpwallet \"filename\"\nDumps all wallet keys in a human-readable format."},
         {"wallet", "encryptwallet", encryptwallet, true, {"passphrase"}, "encryptwallet \"passphrase\"\nEncrypts the wallet with 'passphrase'."},

@@ -1,0 +1,77 @@
+"""BIP21 payment URIs (csrc/wallet/bitcoinuri.{h,cpp}, RPC parsebitcoinuri / formatbitcoinuri).
+
+Parity: reference src/qt/test/uritests.cpp (uriTestsBase58, uriTestsCashAddr, uriTestFormatURI)
+— the same URIs and expected fields, with the main-chain scheme "bitcoincashplus".
+"""
+import pytest
+
+from bitcoincashplus_amd import native
+
+SCHEME = "bitcoincashplus"
+B58 = "175tWpb8K1S7NmH4Zx6rewF9WQrcZv245W"
+CASH = "qqqprqq976hvnqkeajpc33u5rt92xw5vm5ylgfku0f"
+
+
+def parse(uri):
+    ok, addr, amount, label, message, r = native.parse_bitcoin_uri(SCHEME, uri)
+    return ok, addr, amount, label, message
+
+
+@pytest.mark.parametrize("addr,expect", [(B58, B58), (CASH, f"{SCHEME}:{CASH}")])
+def test_reference_uris(addr, expect):
+    if addr == B58:  # no scheme at all
+        assert not parse(f"{addr}?req-dontexist=")[0]
+    assert not parse(f"{SCHEME}:{addr}?req-dontexist=")[0]
+    assert parse(f"{SCHEME}:{addr}?dontexist=") == (True, expect, 0, "", "")
+    assert parse(f"{SCHEME}:{addr}?label=Wikipedia Example Address") == (True, expect, 0, "Wikipedia Example Address", "")
+    assert parse(f"{SCHEME}:{addr}?amount=0.001")[2] == 100000
+    assert parse(f"{SCHEME}:{addr}?amount=1.001")[2] == 100100000
+    ok, a, amt, label, _ = parse(f"{SCHEME}:{addr}?amount=100&label=Wikipedia Example")
+    assert ok and a == expect and amt == 10000000000 and label == "Wikipedia Example"
+    ok, a, _, label, msg = parse(f"{SCHEME}:{addr}?message=Wikipedia Example Address")
+    assert ok and a == expect and label == "" and msg == "Wikipedia Example Address"
+    ok, a, _, label, _ = parse(f"{SCHEME}://{addr}?message=Wikipedia Example Address")
+    assert ok and a == expect and label == ""
+    assert parse(f"{SCHEME}:{addr}?req-message=Wikipedia Example Address")[0]
+    assert not parse(f"{SCHEME}:{addr}?amount=1,000&label=Wikipedia Example")[0]
+    assert not parse(f"{SCHEME}:{addr}?amount=1,000.0&label=Wikipedia Example")[0]
+
+
+def test_uri_details():
+    assert not parse(f"bitcoin:{B58}")[0]                     # wrong scheme
+    assert parse(f"BitcoinCashPlus:{B58}")[0]                  # schemes are case-insensitive
+    assert parse(f"{SCHEME}:{B58}/")[1] == B58                 # trailing slash from an OS handler
+    assert parse(f"{SCHEME}:{B58}?label=a%20b%26c")[3] == "a b&c"
+    assert not parse(f"{SCHEME}:{B58}?amount=0.123456789")[0]  # more than 8 decimals
+    assert parse(f"{SCHEME}:{B58}?amount=")[2] == 0
+    assert native.parse_bitcoin_uri(SCHEME, f"{SCHEME}:{B58}?r=https://m.example/req")[5] == "https://m.example/req"
+    assert native.parse_coin_amount("21000000") == 21000000 * 10**8
+    assert native.parse_coin_amount("1 000.5") == 100050000000
+    assert native.parse_coin_amount("99999999999.00000000") is None  # > 18 digits: beyond 63 bits
+    assert native.parse_coin_amount("-1") is None
+
+
+def test_format_uri():
+    assert native.format_bitcoin_uri(f"{SCHEME}:{CASH}", message="test") == f"{SCHEME}:{CASH}?message=test"
+    assert native.format_bitcoin_uri("CGXa8qa2kKjkmAYjHFsS5j6y4KNbKfNfUS", message="test", use_cashaddr=False) == \
+        f"{SCHEME}:CGXa8qa2kKjkmAYjHFsS5j6y4KNbKfNfUS?message=test"
+    uri = native.format_bitcoin_uri(f"{SCHEME}:{CASH}", 100100000, "shop & co", "order 5")
+    assert uri == f"{SCHEME}:{CASH}?amount=1.001&label=shop%20%26%20co&message=order%205"
+    assert parse(uri) == (True, f"{SCHEME}:{CASH}", 100100000, "shop & co", "order 5")
+
+
+@pytest.mark.functional
+def test_uri_rpcs(tmp_path):
+    from bitcoincashplus_amd.node.process import BcpdProcess
+
+    n = BcpdProcess(str(tmp_path / "n"), extra_args=["-gpu=0", "-keypool=5"])
+    n.start()
+    try:
+        addr = n.rpc.getnewaddress()
+        uri = n.rpc.formatbitcoinuri(addr, 1.5, "me", "for coffee")
+        assert uri.startswith(addr + "?amount=1.5&label=me&message=for%20coffee")
+        r = n.rpc.parsebitcoinuri(uri)
+        assert r["address"] == addr and r["isvalid"] and float(r["amount"]) == 1.5
+        assert r["label"] == "me" and r["message"] == "for coffee"
+    finally:
+        n.stop()
