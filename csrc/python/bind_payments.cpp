@@ -1,5 +1,6 @@
 // Python bindings: BIP70 payment protocol (wallet/paymentrequest.h) for tests.
 #include "python/bind.h"
+#include "keys/key.h"
 #include "wallet/bitcoinuri.h"
 #include "wallet/paymentrequest.h"
 
@@ -131,6 +132,21 @@ void bind_payments(pyb::module_& m) {
         },
         pyb::arg("address"), pyb::arg("amount") = 0, pyb::arg("label") = "", pyb::arg("message") = "",
         pyb::arg("use_cashaddr") = true);
+    m.def("validate_address_input", [](std::string input) {
+        const AddressInputState st = ValidateAddressInput(input);
+        return pyb::make_tuple(st == AddressInputState::Invalid ? "invalid"
+                               : st == AddressInputState::Intermediate ? "intermediate" : "acceptable", input);
+    });
+    m.def(
+        "dummy_address", [](bool cash, const std::string& chain) { return DummyAddress(Params(chain), cash); },
+        pyb::arg("use_cashaddr"), pyb::arg("chain") = "main");
+    m.def(
+        "to_current_encoding",
+        [](const std::string& a, bool cash, const std::string& chain) { return ToCurrentEncoding(a, Params(chain), cash); },
+        pyb::arg("address"), pyb::arg("use_cashaddr"), pyb::arg("chain") = "main");
+    m.def("is_valid_destination", [](const std::string& a, const std::string& chain) {
+        return IsValidDestinationString(a, Params(chain));
+    }, pyb::arg("address"), pyb::arg("chain") = "main");
     m.def("parse_coin_amount", [](const std::string& t) -> pyb::object {
         Amount a;
         if (!ParseCoinAmount(t, &a)) return pyb::none();

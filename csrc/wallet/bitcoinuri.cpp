@@ -142,4 +142,49 @@ std::string FormatBitcoinURI(const SendCoinsRecipient& info, bool useCashAddr) {
     return ret;
 }
 
+AddressInputState ValidateAddressInput(std::string& input) {
+    if (input.empty()) return AddressInputState::Intermediate;
+    std::string kept;
+    for (size_t i = 0; i < input.size();) {
+        const unsigned char c = (unsigned char)input[i];
+        // U+200B ZERO WIDTH SPACE (e2 80 8b), U+FEFF ZERO WIDTH NO-BREAK SPACE (ef bb bf)
+        if (input.compare(i, 3, "\xe2\x80\x8b") == 0 || input.compare(i, 3, "\xef\xbb\xbf") == 0) {
+            i += 3;
+            continue;
+        }
+        if (std::isspace(c)) {
+            i++;
+            continue;
+        }
+        kept += (char)c;
+        i++;
+    }
+    input = kept;
+    for (unsigned char c : input)
+        if (!(std::isalnum(c) && c < 0x80) && c != ':') return AddressInputState::Invalid;
+    return AddressInputState::Acceptable;
+}
+
+std::string DummyAddress(const CChainParams& params, bool useCashAddr) {
+    static const std::vector<unsigned char> data = {0x3a, 0x91, 0x07, 0xc4, 0x5e, 0x2b, 0xd8, 0x60, 0x19, 0xf3,
+                                                    0x44, 0xa7, 0x0c, 0x82, 0x6d, 0xe5, 0x31, 0x9b, 0x58, 0x0f};
+    const CTxDestination d{CKeyID(uint160(data))};
+    std::string addr = useCashAddr ? EncodeCashAddr(d, params) : EncodeLegacyAddr(d, params);
+    // change the last character until the checksum no longer matches
+    static const std::string alphabet = "qpzry9x8gf2tvdw0s3jn54khce6mua7l";
+    const char orig = addr.back();
+    for (char c : alphabet) {
+        if (c == orig) continue;
+        addr.back() = c;
+        if (!IsValidDestinationString(addr, params)) break;
+    }
+    return addr;
+}
+
+std::string ToCurrentEncoding(const std::string& addr, const CChainParams& params, bool useCashAddr) {
+    const CTxDestination d = DecodeDestination(addr, params);
+    if (!d.IsValid()) return addr;
+    return useCashAddr ? EncodeCashAddr(d, params) : EncodeLegacyAddr(d, params);
+}
+
 } // namespace bcp

@@ -7,6 +7,7 @@
 // formatbitcoinuri) and the tests.
 #pragma once
 
+#include "consensus/params.h"
 #include "primitives/amount.h"
 
 #include <string>
@@ -34,5 +35,16 @@ std::string BitcoinURIScheme(bool useCashAddr);
 bool ParseBitcoinURI(const std::string& scheme, const std::string& uri, SendCoinsRecipient* out);
 
 std::string FormatBitcoinURI(const SendCoinsRecipient& info, bool useCashAddr);
+
+// Address entry helpers of the send form (reference src/qt/bitcoinaddressvalidator.cpp
+// BitcoinAddressEntryValidator::validate, src/qt/guiutil.cpp DummyAddress and
+// ToCurrentEncoding, tested by bitcoinaddressvalidatortests.cpp and guiutiltests.cpp).
+enum class AddressInputState { Invalid, Intermediate, Acceptable };
+// Drops whitespace and zero-width spaces from `input` (UTF-8), then accepts only [0-9A-Za-z:].
+AddressInputState ValidateAddressInput(std::string& input);
+// A plausible-looking placeholder address that is not valid, in the selected encoding.
+std::string DummyAddress(const CChainParams& params, bool useCashAddr);
+// A valid address re-encoded in the selected encoding; anything else unchanged.
+std::string ToCurrentEncoding(const std::string& addr, const CChainParams& params, bool useCashAddr);
 
 } // namespace bcp

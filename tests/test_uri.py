@@ -75,3 +75,30 @@ def test_uri_rpcs(tmp_path):
         assert r["label"] == "me" and r["message"] == "for coffee"
     finally:
         n.stop()
+
+
+def test_address_entry_validator():
+    """reference bitcoinaddressvalidatortests.cpp inputTests"""
+    v = native.validate_address_input
+    assert v("")[0] == "intermediate"
+    for ok in ("BIIC", "BITCOINCASHH", "BITC", "BITCOINCASHPLUS:QP", "bitcoincashplus:qp", "bItCoInCaShPlUs:Qp",
+               "BBBBBBBBBBBBBB"):
+        assert v(ok)[0] == "acceptable", ok
+    assert v("%")[0] == "invalid"
+    # whitespace and zero-width spaces are stripped, not rejected
+    assert v(" bitcoincashplus:​qp \t﻿") == ("acceptable", "bitcoincashplus:qp")
+
+
+def test_dummy_address_and_current_encoding():
+    """reference guiutiltests.cpp dummyAddressTest / toCurrentEncodingTest"""
+    for cash in (False, True):
+        d = native.dummy_address(cash)
+        assert d and not native.is_valid_destination(d)
+    assert native.dummy_address(True).startswith("bitcoincashplus:")
+    cash_addr = "bitcoincashplus:qqqprqq976hvnqkeajpc33u5rt92xw5vm5ylgfku0f"
+    b58 = "CGUFXy9eQgs3eunVAEqFdS9tnkEcgLw9VD"
+    assert native.to_current_encoding("garbage", True) == "garbage"
+    assert native.to_current_encoding(cash_addr, True) == cash_addr
+    assert native.to_current_encoding(b58, True) == cash_addr
+    assert native.to_current_encoding(cash_addr, False) == b58
+    assert native.to_current_encoding(b58, False) == b58
