@@ -44,7 +44,13 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 <section id="receive"><div class="card">Label <input id="rcvlabel"> <button class="act" onclick="newAddr()">New address</button>
 <p class="mono big" id="newaddr"></p></div>
 <div class="card"><b>Receiving addresses</b><table><thead><tr><th>Address</th><th>Label</th><th>Received</th><th>Conf.</th></tr></thead><tbody id="rcvlist"></tbody></table></div></section>
-<section id="transactions"><div class="card"><table><thead><tr><th>Date</th><th>Type</th><th>Address</th><th>Amount</th><th>Conf.</th><th>Txid</th></tr></thead><tbody id="txlist"></tbody></table></div></section>
+<section id="transactions"><div class="card"><button onclick="exportCsv()">Export CSV</button></div><div class="card"><table><thead><tr><th>Date</th><th>Type</th><th>Address</th><th>Amount</th><th>Conf.</th><th>Txid</th></tr></thead><tbody id="txlist"></tbody></table></div></section>
+<section id="signverify"><div class="card"><b>Sign message</b><div>Address</div><input class="wide" id="smaddr">
+<div>Message</div><textarea class="wide" id="smmsg" rows="3"></textarea>
+<p><button class="act" onclick="signMsg()">Sign</button></p><p class="mono" id="smsig"></p></div>
+<div class="card"><b>Verify message</b><div>Address</div><input class="wide" id="vmaddr">
+<div>Message</div><textarea class="wide" id="vmmsg" rows="3"></textarea><div>Signature</div><input class="wide" id="vmsig">
+<p><button class="act" onclick="verifyMsg()">Verify</button> <span id="vmres"></span></p></div></section>
 <section id="peers"><div class="card"><table><thead><tr><th>Address</th><th>Client</th><th>Version</th><th>Direction</th><th>Height</th><th>Sent</th><th>Recv</th><th>Ping ms</th></tr></thead><tbody id="peerlist"></tbody></table></div></section>
 <section id="mining"><div class="card"><table><tbody id="mininfo"></tbody></table></div>
 <div class="card"><table><tbody id="gpuinfo"></tbody></table></div>
@@ -54,7 +60,7 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 <input class="wide mono" id="conin" placeholder="method arg1 arg2 …  (e.g. getblockchaininfo, getblockhash 10; ↑/↓ history)"></div></section>
 </main>
 <script>
-const TABS=[["overview","Overview"],["send","Send"],["receive","Receive"],["transactions","Transactions"],["peers","Peers"],["mining","Mining"],["console","Console"]];
+const TABS=[["overview","Overview"],["send","Send"],["receive","Receive"],["transactions","Transactions"],["signverify","Sign / verify"],["peers","Peers"],["mining","Mining"],["console","Console"]];
 let rpcId=0;
 async function rpc(method,params=[]){
   const r=await fetch("/",{method:"POST",credentials:"same-origin",headers:{"Content-Type":"application/json"},
@@ -109,6 +115,18 @@ async function payReq(){$("preqres").textContent="";
     const r=await rpc("sendpaymentrequest",[$("preq").value.trim()]);
     $("preqres").innerHTML="<span class='ok'>paid "+esc(r.txid)+(r.payment_url?" (send the Payment to "+esc(r.payment_url)+")":"")+"</span>";
   }catch(e){ if(e.code==-13) $("passrow").style.display="block"; $("preqres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function signMsg(){try{const pass=$("sendpass").value; if(pass) await rpc("walletpassphrase",[pass,60]);
+  $("smsig").textContent=await rpc("signmessage",[$("smaddr").value.trim(),$("smmsg").value]);}
+  catch(e){$("smsig").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function verifyMsg(){try{const ok=await rpc("verifymessage",[$("vmaddr").value.trim(),$("vmsig").value.trim(),$("vmmsg").value]);
+  $("vmres").innerHTML=ok?"<span class='ok'>message verified</span>":"<span class='err'>signature does not match</span>";}
+  catch(e){$("vmres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function exportCsv(){const txs=await rpc("listtransactions",["*",100000]);
+  const q=v=>'"'+String(v??"").replace(/"/g,'""')+'"';
+  const lines=[["Confirmed","Date","Type","Label","Address","Amount","ID"].map(q).join(",")].concat(txs.map(t=>
+    [t.confirmations>0,new Date(t.time*1000).toISOString(),t.category,t.label||t.account||"",t.address||"",t.amount,t.txid].map(q).join(",")));
+  const a=document.createElement("a");a.href=URL.createObjectURL(new Blob([lines.join("\n")],{type:"text/csv"}));
+  a.download="transactions.csv";a.click();}
 async function newAddr(){try{const a=await rpc("getnewaddress",[$("rcvlabel").value]);
   $("newaddr").textContent=a+"  "+await rpc("formatbitcoinuri",[a,null,$("rcvlabel").value]);refresh("receive");}
   catch(e){$("newaddr").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
