@@ -37,7 +37,9 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 <label><input type="checkbox" id="sendsub"> subtract fee from amount</label>
 <div>Comment</div><input class="wide" id="sendcomment">
 <div id="passrow" style="display:none">Wallet passphrase <input type="password" id="sendpass"></div>
-<p><button class="act" onclick="doSend()">Send</button> <span id="sendres"></span></p></div>
+<p><button class="act" onclick="doSend()">Send</button> <span id="sendres"></span></p>
+<details id="cc"><summary>Coin control</summary><p><button onclick="loadCoins()">List coins</button> Change address <input class="wide" id="ccchange"></p>
+<table><thead><tr><th></th><th>Amount</th><th>Address</th><th>Conf.</th><th>Output</th></tr></thead><tbody id="cclist"></tbody></table></details></div>
 <div class="card"><div>BIP70 payment request (hex or base64)</div><textarea class="wide" id="preq" rows="3"></textarea>
 <p><button onclick="checkReq()">Check</button> <button class="act" onclick="payReq()">Pay request</button> <span id="preqres"></span></p>
 <div id="preqinfo"></div></div></section>
@@ -100,6 +102,10 @@ async function doSend(){
       if(u.amount>0)$("sendamt").value=u.amount; if(u.message)$("sendcomment").value=u.message;
       $("sendres").innerHTML="<span class='ok'>filled from URI — check and press Send</span>";return;}
     const pass=$("sendpass").value; if(pass) await rpc("walletpassphrase",[pass,60]);
+    const picked=[...document.querySelectorAll(".ccpick:checked")].map(c=>({txid:c.dataset.txid,vout:Number(c.dataset.vout)}));
+    if(picked.length){const to=$("sendto").value.trim(),amts={};amts[to]=Number($("sendamt").value);
+      const r=await rpc("sendwithcoincontrol",[amts,picked,$("ccchange").value.trim(),$("sendsub").checked?[to]:[]]);
+      $("sendres").innerHTML="<span class='ok'>sent "+esc(r.txid)+" (fee "+amt(r.fee)+")</span>";$("sendpass").value="";loadCoins();return;}
     const txid=await rpc("sendtoaddress",[$("sendto").value.trim(),Number($("sendamt").value),$("sendcomment").value,"",$("sendsub").checked]);
     $("sendres").innerHTML="<span class='ok'>sent "+esc(txid)+"</span>";$("sendpass").value="";
   }catch(e){ if(e.code==-13) $("passrow").style.display="block";
@@ -127,6 +133,9 @@ async function exportCsv(){const txs=await rpc("listtransactions",["*",100000]);
     [t.confirmations>0,new Date(t.time*1000).toISOString(),t.category,t.label||t.account||"",t.address||"",t.amount,t.txid].map(q).join(",")));
   const a=document.createElement("a");a.href=URL.createObjectURL(new Blob([lines.join("\n")],{type:"text/csv"}));
   a.download="transactions.csv";a.click();}
+async function loadCoins(){const u=await rpc("listunspent",[0]);
+  $("cclist").innerHTML=u.map(c=>"<tr><td><input type='checkbox' class='ccpick' data-txid='"+esc(c.txid)+"' data-vout='"+c.vout+"'></td><td>"+amt(c.amount)+
+    "</td><td class='mono'>"+esc(c.address||"")+"</td><td>"+c.confirmations+"</td><td class='mono'>"+esc(c.txid.slice(0,16))+"…:"+c.vout+"</td></tr>").join("");}
 async function newAddr(){try{const a=await rpc("getnewaddress",[$("rcvlabel").value]);
   $("newaddr").textContent=a+"  "+await rpc("formatbitcoinuri",[a,null,$("rcvlabel").value]);refresh("receive");}
   catch(e){$("newaddr").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}

@@ -1537,6 +1537,63 @@ static UniValue formatbitcoinuri(const JSONRPCRequest& req) {
     return FormatBitcoinURI(r, UseCashAddr());
 }
 
+// Coin control send (reference Qt SendCoinsDialog + CoinControlDialog: pay recipients from
+// exactly the selected outputs, optional custom change address), used by the GUI send page.
+static UniValue sendwithcoincontrol(const JSONRPCRequest& req) {
+    CWallet& w = Wallet(req);
+    if (req.params.size() < 2 || req.params.size() > 4)
+        ThrowRPC(RPC_INVALID_PARAMS, "sendwithcoincontrol {\"address\":amount,...} [{\"txid\":\"id\",\"vout\":n},...] ( \"changeaddress\" [\"address\",...] )");
+    const UniValue sendTo = req.params[0].get_obj();
+    const UniValue inputs = req.params[1].get_array();
+    CCoinControl cc;
+    cc.fAllowOtherInputs = false;
+    for (size_t i = 0; i < inputs.size(); i++) {
+        const UniValue& o = inputs[i].get_obj();
+        const int vout = find_value(o, "vout").get_int();
+        if (vout < 0) ThrowRPC(RPC_INVALID_PARAMETER, "Invalid parameter, vout must be positive");
+        COutPoint op;
+        op.hash = ParseHashO(o, "txid");
+        op.n = (uint32_t)vout;
+        cc.setSelected.insert(op);
+    }
+    if (cc.setSelected.empty()) ThrowRPC(RPC_INVALID_PARAMETER, "No inputs selected");
+    if (req.params.size() > 2 && !req.params[2].isNull() && !req.params[2].get_str().empty()) {
+        cc.destChange = DecodeDestination(req.params[2].get_str(), P());
+        if (!cc.destChange.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid change address");
+    }
+    UniValue subtractFrom(UniValue::VARR);
+    if (req.params.size() > 3 && !req.params[3].isNull()) subtractFrom = req.params[3].get_array();
+    std::vector<CRecipient> vecSend;
+    std::set<CTxDestination> seen;
+    for (const std::string& name : sendTo.getKeys()) {
+        const CTxDestination d = DecodeDestination(name, P());
+        if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin Cash Plus address: " + name);
+        if (!seen.insert(d).second) ThrowRPC(RPC_INVALID_PARAMETER, "Invalid parameter, duplicated address: " + name);
+        const Amount nAmount = AmountFromValue(sendTo[name]);
+        if (nAmount <= 0) ThrowRPC(RPC_TYPE_ERROR, "Invalid amount for send");
+        bool fSub = false;
+        for (size_t i = 0; i < subtractFrom.size(); i++)
+            if (subtractFrom[i].get_str() == name) fSub = true;
+        vecSend.push_back({GetScriptForDestination(d), nAmount, fSub});
+    }
+    if (vecSend.empty()) ThrowRPC(RPC_INVALID_PARAMETER, "No recipients");
+    EnsureWalletIsUnlocked(w);
+    CWalletTx wtx;
+    CReserveKey rk(&w);
+    Amount fee = 0;
+    int changePos = -1;
+    std::string err;
+    if (!w.CreateTransaction(vecSend, wtx, rk, fee, changePos, err, &cc)) ThrowRPC(RPC_WALLET_INSUFFICIENT_FUNDS, err);
+    CValidationState state;
+    if (!w.CommitTransaction(wtx, rk, state))
+        ThrowRPC(RPC_WALLET_ERROR, "Transaction commit failed:: " + state.GetRejectReason());
+    UniValue r(UniValue::VOBJ);
+    r.pushKV("txid", wtx.GetHash().GetHex());
+    r.pushKV("fee", ValueFromAmount(fee));
+    r.pushKV("changepos", changePos);
+    return r;
+}
+
 void RegisterWalletRPCCommands(CRPCTable& t) {
     const CRPCCommand cmds[] = {
         {"rawtransactions", "fundrawtransaction", fundrawtransaction, false, {"hexstring", "options"}, "fundrawtransaction \"hexstring\" ( options )\nAdd inputs to a transaction until it has enough in value to meet its out value."},
@@ -1548,6 +1605,7 @@ void RegisterWalletRPCCommands(CRPCTable& t) {
         {"wallet", "sendpaymentrequest", sendpaymentrequest, false, {"request", "memo"}, "sendpaymentrequest \"request\" ( \"memo\" )\nPay a BIP70 payment request and return the BIP70 Payment message for its payment_url."},
         {"wallet", "parsebitcoinuri", parsebitcoinuri, true, {"uri"}, "parsebitcoinuri \"uri\"\nSplit a BIP21 payment URI into address, amount, label, message (and BIP72 r)."},
         {"wallet", "formatbitcoinuri", formatbitcoinuri, true, {"address", "amount", "label", "message"}, "formatbitcoinuri \"address\" ( amount \"label\" \"message\" )\nBuild a BIP21 payment URI."},
+        {"wallet", "sendwithcoincontrol", sendwithcoincontrol, false, {"amounts", "inputs", "changeaddress", "subtractfeefrom"}, "sendwithcoincontrol {\"address\":amount,...} [{\"txid\":\"id\",\"vout\":n},...] ( \"changeaddress\" [\"address\",...] )\nSend to recipients spending only the selected outputs (coin control)."},
         {"wallet", "dumpprivkey", dumpprivkey, true, {"address"}, "dumpprivkey \"address\"\nReveals the private key corresponding to 'address'."},
         {"wallet", "dumpwallet", dumpwallet, true, {"filename"}, "dumpwallet \"filename\"\nDumps all wallet keys in a human-readable format."},
         {"wallet", "encryptwallet", encryptwallet, true, {"passphrase"}, "encryptwallet \"passphrase\"\nEncrypts the wallet with 'passphrase'."},

@@ -255,3 +255,29 @@ def test_watchonly_and_accounts(tmp_path):
         assert D(n.rpc.getwalletinfo()["paytxfee"]) == D("0.001")
     finally:
         n.stop()
+
+
+def test_coin_control_send(tmp_path):
+    """Coin control (reference Qt CoinControlDialog + SendCoinsDialog, CCoinControl with
+    fAllowOtherInputs = false): only the selected outputs are spent, change goes to the chosen
+    address."""
+    n = BcpdProcess(str(tmp_path / "cc"), extra_args=["-gpu=0", "-keypool=5"])
+    n.start()
+    try:
+        n.rpc.generate(103)
+        coins = sorted(n.rpc.listunspent(), key=lambda c: (c["txid"], c["vout"]))
+        assert len(coins) >= 3
+        pick = coins[0]
+        dest, change = n.rpc.getnewaddress(), n.rpc.getnewaddress()
+        r = n.rpc.sendwithcoincontrol({dest: 1}, [{"txid": pick["txid"], "vout": pick["vout"]}], change)
+        tx = n.rpc.decoderawtransaction(n.rpc.gettransaction(r["txid"])["hex"])
+        assert [(i["txid"], i["vout"]) for i in tx["vin"]] == [(pick["txid"], pick["vout"])]
+        outs = {o["scriptPubKey"]["addresses"][0]: o["value"] for o in tx["vout"]}
+        assert D(outs[dest]) == D(1) and change in outs
+        assert D(outs[change]) == D(pick["amount"]) - 1 - D(r["fee"])
+        # more than the selected coin holds: refused, although the wallet could pay it
+        other = coins[1]
+        with pytest.raises(RPCError):
+            n.rpc.sendwithcoincontrol({dest: float(D(other["amount"]) + 1)}, [{"txid": other["txid"], "vout": other["vout"]}])
+    finally:
+        n.stop()

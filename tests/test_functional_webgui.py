@@ -41,7 +41,7 @@ def test_webgui(tmp_path):
         # every method the page calls is registered (help errors on unknown commands)
         methods = set(re.findall(r'rpc\("([a-z]+)"', page))
         assert {"getbalance", "sendtoaddress", "getnewaddress", "listtransactions", "getpeerinfo",
-                "getmininginfo", "generate", "decodepaymentrequest", "sendpaymentrequest", "execconsole", "parsebitcoinuri", "formatbitcoinuri", "signmessage", "verifymessage"} <= methods
+                "getmininginfo", "generate", "decodepaymentrequest", "sendpaymentrequest", "execconsole", "parsebitcoinuri", "formatbitcoinuri", "signmessage", "verifymessage", "sendwithcoincontrol", "listunspent"} <= methods
         for m in sorted(methods):
             assert m in n.rpc.help(m), m
 
