@@ -14,5 +14,5 @@ mkdir -p "$D" ab/"$NAME"
 cp build/libbcpcore.a "$D/libbcpcore.a"
 ar r "$D/libbcpcore.a" "$D/equihash_solver.o"
 g++ -shared -o ab/"$NAME"/_bcpnative"$EXT" build/obj/python/*.o -Wl,--whole-archive "$D/libbcpcore.a" \
-    -Wl,--no-whole-archive -L/opt/rocm/lib -lamdhip64 -pthread -ldl -Wl,-rpath,/opt/rocm/lib
+    -Wl,--no-whole-archive -L/opt/rocm/lib -lamdhip64 -lcrypto -pthread -ldl -Wl,-rpath,/opt/rocm/lib
 echo "built ab/$NAME/_bcpnative$EXT"
