@@ -11,21 +11,61 @@ so scaling is weak; ranks take disjoint nonce ranges (nonce-space data
 parallelism) and the solution counts are summed with an RCCL all-reduce.
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
-Multi-GPU: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+`--gpus N` always drives N GPUs, one process per GPU over RCCL:
+* launched by torchrun (WORLD_SIZE set): WORLD_SIZE must equal N;
+* launched directly with N > 1: this process counts the visible devices (without
+  initialising HIP), refuses N > visible, and starts
+  `python -m torch.distributed.run --nproc-per-node N ...` as a child, exiting
+  with its status (the parent never touches the GPU).
+
+After timing, every solution of every timed step is re-checked by the GPU batch
+verifier (a rejection fails the run), and the mean solutions per nonce must be
+>= 1.85 (Equihash(200,9) yields ~1.88 per nonce; a lower figure means the solver
+lost rows).
 """
 import argparse
 import collections
 import json
 import os
+import socket
 import struct
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+MIN_SOLUTIONS_PER_NONCE = 1.85
 
-def main():
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def visible_gpus() -> int:
+    """Device count without initialising the HIP runtime (torch's count is a sysfs/env
+    probe on this image), so a launcher parent may still spawn children safely."""
+    import torch
+    return int(torch.cuda.device_count())
+
+
+def launch_ranks(argv, gpus: int, launcher=None) -> int:
+    """Start one rank per GPU under torch.distributed.run; returns the child's status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return (launcher or subprocess.call)(cmd, env=env)
+
+
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -34,20 +74,67 @@ def main():
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
     ap.add_argument("--solvers", type=int, default=int(os.environ.get("BCP_EH_SOLVERS", "2")),
                     help="solvers in flight per GPU (each its own stream and buffers)")
-    args = ap.parse_args()
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launcher: ranks rendezvous over gloo, all-reduce, "
+                         "report n_gpus; no GPU work and no metric")
+    return ap.parse_args(argv)
 
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench: --gpus must be >= 1")
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    rehearsal = os.environ.get("BCP_DIST_BACKEND", "nccl") != "nccl"
+    if world == 0:
+        # not under torchrun: this process is the launcher for N > 1
+        nvis = visible_gpus()
+        if args.gpus > nvis and not (rehearsal or args.dry_run):
+            raise SystemExit(f"bench: --gpus {args.gpus} but only {nvis} GPU(s) visible")
+        if args.gpus > 1:
+            sys.exit(launch_ranks(argv, args.gpus))
+        world = 1
+    elif world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dry_run(world)
+    else:
+        run(args, world)
+
+
+def dry_run(world):
+    """Exercise the rank launch and the collective path without a GPU."""
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([1.0, float(rank)], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(t[0]),
+                          "rank_sum": int(t[1])}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run(args, world):
     import torch
     import torch.distributed as dist
     from bitcoincashplus_amd import native, require_gpu
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     require_gpu("bench.py")
     # one rank per GPU over RCCL ("nccl"); BCP_DIST_BACKEND=gloo + ranks sharing a GPU is the
     # rehearsal mode for the multi-rank path on a 1-GPU box (CPU-side reductions)
     backend = os.environ.get("BCP_DIST_BACKEND", "nccl")
-    device = local_rank % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if backend == "nccl" and local_rank >= ndev:
+        raise SystemExit(f"bench: rank {rank} (local {local_rank}) has no GPU of its own ({ndev} visible)")
+    device = local_rank % max(1, ndev)
     torch.cuda.set_device(device)
     if world > 1:
         if backend == "nccl":
@@ -65,7 +152,6 @@ def main():
     # host decodes batch s-1, and one solver's kernels fill the other's tails
     nsolv = max(1, args.solvers)
     solvers = [native.EquihashGpuSolver(200, 9, args.batch, device) for _ in range(nsolv)]
-    solver = solvers[0]
     # Template: CEquihashInput of a mainnet-shaped header (108 B), random-ish but fixed.
     header = bytes((i * 37 + 11) & 0xFF for i in range(108))
 
@@ -84,7 +170,7 @@ def main():
     for sv in solvers:
         sv.reset_stats()
     all_states = [states_for(s) for s in range(args.steps)]
-    sols_kept = []
+    sols_kept = []  # (state, solution) for EVERY solution of every timed step
 
     barrier()
     t0 = time.perf_counter()
@@ -96,8 +182,7 @@ def main():
         ps, psolver = pending.popleft()
         for b, sols in enumerate(psolver.collect()):
             nsol += len(sols)
-            if ps < 2:
-                sols_kept.extend((all_states[ps][b], x) for x in sols)
+            sols_kept.extend((all_states[ps][b], x) for x in sols)
 
     for s in range(args.steps):
         if len(pending) == nsolv:  # this step's solver still holds an older batch
@@ -109,27 +194,34 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
 
-    t = torch.tensor([float(nsol), dt], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        tot = t.clone()
-        dist.all_reduce(tot[:1], op=dist.ReduceOp.SUM)
-        mx = t.clone()
-        dist.all_reduce(mx[1:], op=dist.ReduceOp.MAX)
-        total_sols, max_dt = float(tot[0]), float(mx[1])
-    else:
-        total_sols, max_dt = nsol, dt
-
+    # verification happens after the timed region: every solution found in every step
     verified = None
+    nbad = 0
     if args.verify and sols_kept:
         ok = native.eh_verify_batch_gpu(200, 9, [a for a, _ in sols_kept], [b for _, b in sols_kept], device)
-        verified = bool(all(ok))
-        if not verified:
-            raise SystemExit("bench: GPU verifier rejected solver output")
+        nbad = sum(1 for x in ok if not x)
+        verified = nbad == 0
+
+    t = torch.tensor([float(nsol), dt, float(nbad)], dtype=torch.float64, device=red_dev)
+    if world > 1:
+        tot = t.clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        total_sols, max_dt, total_bad = float(tot[0]), float(mx[1]), float(tot[2])
+    else:
+        total_sols, max_dt, total_bad = float(nsol), dt, float(nbad)
+    if total_bad:
+        raise SystemExit(f"bench: GPU verifier rejected {int(total_bad)} solver solution(s)")
+    nonces = args.steps * args.batch * world
+    per_nonce = total_sols / max(nonces, 1)
+    if per_nonce < MIN_SOLUTIONS_PER_NONCE:
+        raise SystemExit(f"bench: solver recall too low: {per_nonce:.3f} solutions/nonce "
+                         f"< {MIN_SOLUTIONS_PER_NONCE}")
 
     st = solvers[0].stats()
     if rank == 0:
         value = total_sols / max_dt
-        nonces = args.steps * args.batch * world
         out = {
             "metric": "equihash_200_9_solutions_per_sec",
             "value": round(value, 2),
@@ -150,12 +242,13 @@ def main():
                 "parallelism": f"dp{world} (nonce-space)",
                 "solvers_in_flight": nsolv,
                 "nonces_per_sec": round(nonces / max_dt, 2),
-                "solutions_per_nonce": round(total_sols / max(nonces, 1), 3),
+                "solutions_per_nonce": round(per_nonce, 3),
                 "verified": verified,
+                "verified_solutions": int(total_sols) if verified else 0,
                 "rank0_dropped_rows_sampled": st["dropped_rows_sampled"],
             },
         }
-        print(json.dumps(out))
+        print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

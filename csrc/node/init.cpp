@@ -82,7 +82,7 @@ std::string HelpMessage() {
         {"-usecashaddr", "Use Cash Address for destination encoding (default: 1)"},
         {"-server", "Accept command line and JSON-RPC commands (default: 1 for bcpd)"},
         {"-rest", "Accept public REST requests (default: 0)"},
-        {"-webgui", "Serve the browser wallet GUI at http://<rpcbind>:<rpcport>/gui to authenticated RPC users (default: 1)"},
+        {"-webgui", "Serve the browser wallet GUI at http://<rpcbind>:<rpcport>/gui to authenticated RPC users (default: 0)"},
         {"-rpcbind=<addr>[:port]", "Bind to given address to listen for JSON-RPC connections"},
         {"-rpcport=<port>", "Listen for JSON-RPC connections on <port> (default: 8332 / testnet and regtest 18332)"},
         {"-rpcallowip=<ip>", "Allow JSON-RPC connections from specified source (IP or subnet)"},
@@ -342,7 +342,7 @@ int AppMain(int argc, char* argv[]) {
             return 1;
         }
         if (gArgs.GetBoolArg("-rest", false)) StartREST(*http);
-        if (gArgs.GetBoolArg("-webgui", true)) StartWebGUI(*http);
+        if (gArgs.GetBoolArg("-webgui", false)) StartWebGUI(*http);
     }
 
     // ---- chainstate

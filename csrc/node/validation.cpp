@@ -129,6 +129,7 @@ Chainstate::Chainstate(const CChainParams& p, const ChainstateOptions& o) : para
     int threads = opts.scriptThreads <= 0 ? GetNumCores() : opts.scriptThreads;
     threads = std::max(1, std::min(threads, MAX_SCRIPTCHECK_THREADS));
     pool.reset(new WorkerPool(threads));
+    scriptQueue.reset(new CheckQueue(threads - 1)); // the connecting thread is the last worker
     fReindex = opts.wipe;
 }
 
@@ -740,40 +741,27 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
 
     // Script checks overlap the UTXO pass (reference CCheckQueue: the master keeps connecting
     // while workers run the queued CScriptChecks, src/validation.cpp:2011-2127). The loop below
-    // publishes jobs into a pre-sized array; the pool's threads (driven from a helper thread, the
-    // ParallelFor caller) execute them as they appear, deferring every ECDSA check into a
-    // per-job sink for the batch verifier.
+    // publishes jobs into a pre-sized array; the script queue's own threads execute them as they
+    // appear (sleeping while none are available), deferring every ECDSA check into a per-job sink
+    // for the batch verifier. Nothing in the UTXO loop may wait on the queue's threads.
     std::vector<ScriptJob> jobs(maxJobs);
     std::vector<std::vector<DeferredSigCheck>> sinks(maxJobs);
-    std::atomic<size_t> nProduced{0}, nextJob{0};
-    std::atomic<bool> doneProducing{false}, anyFail{false};
-    auto runJobs = [&](size_t) {
-        for (;;) {
-            const size_t k = nextJob.fetch_add(1, std::memory_order_relaxed);
-            while (k >= nProduced.load(std::memory_order_acquire)) {
-                if (doneProducing.load(std::memory_order_acquire) && k >= nProduced.load(std::memory_order_acquire))
-                    return;
-                std::this_thread::yield();
-            }
-            if (anyFail.load(std::memory_order_relaxed)) continue;
+    std::atomic<bool> anyFail{false};
+    size_t nProduced = 0;
+    const bool queued = fScriptChecks && maxJobs > 0;
+    if (queued)
+        scriptQueue->Begin([&](size_t k) {
+            if (anyFail.load(std::memory_order_relaxed)) return;
             const ScriptJob& J = jobs[k];
             BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k]);
             ScriptError err;
             if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, J.scriptPubKey, flags, checker, &err)) anyFail = true;
-        }
-    };
-    std::thread scriptThread;
-    if (fScriptChecks && maxJobs > 0)
-        scriptThread = std::thread([&]() { pool->ParallelFor((size_t)pool->Size(), runJobs, 1); });
-    // every return below stops and joins the script workers first
-    struct JoinOnExit {
-        std::atomic<bool>& done;
-        std::thread& th;
-        ~JoinOnExit() {
-            done.store(true, std::memory_order_release);
-            if (th.joinable()) th.join();
-        }
-    } joinOnExit{doneProducing, scriptThread};
+        });
+    // every return below drains and closes the session first (jobs/sinks outlive it)
+    struct CompleteOnExit {
+        CheckQueue& q;
+        ~CompleteOnExit() { q.Complete(); }
+    } completeOnExit{*scriptQueue};
 
     for (size_t i = 0; i < ntx; i++) {
         const CTransaction& tx = *block.vtx[i];
@@ -801,13 +789,13 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
             if (fScriptChecks) {
                 // transactions fully validated under these flags in the mempool skip re-execution
                 if (!sc.Has(scKeys[i], !fJustCheck)) {
-                    size_t n = nProduced.load(std::memory_order_relaxed);
                     for (size_t j = 0; j < tx.vin.size(); j++) {
                         const Coin& coin = view.AccessCoin(tx.vin[j].prevout);
-                        jobs[n + j] = ScriptJob{&tx, (unsigned)j, coin.GetTxOut().scriptPubKey, coin.GetTxOut().nValue,
-                                                txdatas[i].get()};
+                        jobs[nProduced + j] = ScriptJob{&tx, (unsigned)j, coin.GetTxOut().scriptPubKey,
+                                                        coin.GetTxOut().nValue, txdatas[i].get()};
                     }
-                    nProduced.store(n + tx.vin.size(), std::memory_order_release);
+                    nProduced += tx.vin.size();
+                    scriptQueue->Publish(nProduced);
                 }
             }
         }
@@ -835,9 +823,8 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
                          REJECT_INVALID, "bad-cb-amount");
 
     // ---- remaining scripts, then one ECDSA batch (GPU when large enough)
-    doneProducing.store(true, std::memory_order_release);
-    if (scriptThread.joinable()) scriptThread.join();
-    const size_t nJobs = nProduced.load();
+    scriptQueue->Complete();
+    const size_t nJobs = nProduced;
     if (nJobs > 0) {
         bool ok = !anyFail.load();
         if (ok) {

@@ -30,6 +30,7 @@
 #include "consensus/versionbits.h"
 #include "node/coins.h"
 #include "node/txdb.h"
+#include "util/checkqueue.h"
 #include "util/util.h"
 
 #include <atomic>
@@ -273,6 +274,7 @@ private:
     std::unique_ptr<CCoinsViewDB> pcoinsdbview;
     std::unique_ptr<CCoinsViewCache> pcoinsTip;
     std::unique_ptr<WorkerPool> pool;
+    std::unique_ptr<CheckQueue> scriptQueue; // ConnectBlock script checks (reference CCheckQueue)
     VersionBitsCache versionbitscache;
     CTxMemPool* mempool = nullptr;
 };

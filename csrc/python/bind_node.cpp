@@ -5,13 +5,19 @@
 #include "python/bind.h"
 #include "rpc/console.h"
 #include "rpc/server.h"
+#include "util/checkqueue.h"
 #include "util/cuckoocache.h"
 #include "util/indirectmap.h"
 #include "util/limitedmap.h"
 #include "util/memusage.h"
 #include "util/util.h"
 
+#include <sys/resource.h>
+
+#include <atomic>
+#include <chrono>
 #include <deque>
+#include <thread>
 #include <map>
 
 namespace bcp {
@@ -148,6 +154,42 @@ void bind_node(pyb::module_& m) {
         g_pynode.reset();
     });
     m.def("node_running", []() { return (bool)g_pynode; });
+    // CheckQueue exercise (reference src/test/checkqueue_tests.cpp): publishes `total` jobs in
+    // steps of `step` with `idle_ms` pauses in between; returns (sum of run indices, jobs run,
+    // jobs run by workers, process CPU seconds spent while the session sat idle).
+    m.def(
+        "checkqueue_run",
+        [](int workers, size_t total, size_t step, int idle_ms) {
+            pyb::gil_scoped_release rel;
+            auto res = std::make_tuple((uint64_t)0, (uint64_t)0, (size_t)0, 0.0);
+            CheckQueue q(workers);
+            std::atomic<uint64_t> sum{0}, cnt{0};
+            auto cpu = []() {
+                struct rusage ru;
+                getrusage(RUSAGE_SELF, &ru);
+                return ru.ru_utime.tv_sec + ru.ru_stime.tv_sec + 1e-6 * (ru.ru_utime.tv_usec + ru.ru_stime.tv_usec);
+            };
+            double idleCpu = 0;
+            for (int rep = 0; rep < 2; rep++) { // two sessions on the same queue
+                q.Begin([&](size_t k) {
+                    sum += k;
+                    cnt++;
+                });
+                for (size_t p = 0; p < total;) {
+                    p = std::min(total, p + step);
+                    q.Publish(p);
+                    if (idle_ms > 0) {
+                        const double c0 = cpu();
+                        std::this_thread::sleep_for(std::chrono::milliseconds(idle_ms));
+                        idleCpu += cpu() - c0;
+                    }
+                }
+                q.Complete();
+            }
+            res = std::make_tuple((uint64_t)sum, (uint64_t)cnt, q.WorkerJobs(), idleCpu);
+            return res; // converted to a Python tuple after the GIL is re-acquired
+        },
+        pyb::arg("workers"), pyb::arg("total"), pyb::arg("step"), pyb::arg("idle_ms") = 0);
     // Lock-order detector probe (reference DEBUG_LOCKORDER): a->b then b->a in one thread.
     m.def("ui_track_start", []() {
         {

@@ -69,6 +69,8 @@ private:
     const ConsoleExecutor* exec;
     size_t pos = 0;
     int sensitiveDepth = 0; // > 0 inside the arguments of a sensitive command
+    int callDepth = 0;      // nested calls: bounded so a hostile line cannot exhaust the stack
+    static constexpr int MAX_CALL_DEPTH = 64;
     std::vector<std::pair<size_t, size_t>> ranges;
 
     static bool IsSpace(char c) { return c == ' ' || c == '\t'; }
@@ -157,6 +159,11 @@ private:
     }
 
     UniValue Call(const std::string& name, size_t nameEnd, bool top) {
+        if (++callDepth > MAX_CALL_DEPTH) Syntax();
+        struct DepthGuard {
+            int& d;
+            ~DepthGuard() { --d; }
+        } guard{callDepth};
         const bool opens = sensitiveDepth == 0 && IsSensitiveConsoleCommand(name);
         if (opens || sensitiveDepth > 0) sensitiveDepth++;
         std::vector<std::string> args;
@@ -188,7 +195,8 @@ private:
             if (r.isArray()) {
                 for (char ch : key)
                     if (!std::isdigit((unsigned char)ch)) throw std::runtime_error("Invalid result query");
-                const size_t i = (size_t)std::stoull(key);
+                // an index longer than any array is simply out of range (no stoull overflow)
+                const size_t i = key.size() > 18 ? SIZE_MAX : (size_t)std::stoull(key);
                 if (i < r.size()) sub = r[i];
             } else if (r.isObject()) {
                 sub = find_value(r, key);

@@ -309,10 +309,44 @@ bool RPCAuthorizedHeader(const std::string& auth, std::string& user) {
     return !invalid && CheckUserAuthorized(std::string(dec.begin(), dec.end()), user);
 }
 
+// Cross-site request guard. Command-line and library clients never send an Origin header;
+// browsers always do on a POST. A browser request is served only if it comes from the page this
+// server itself serves (Origin == http://<Host>), is declared JSON, and carries the custom
+// X-Requested-With header that a cross-site "simple" request (form/text-plain POST) cannot set.
+// This keeps another site open in the same browser from riding on Basic credentials the browser
+// cached for the web GUI (which the reference's native Qt wallet never puts in a browser).
+bool BrowserRequestAllowed(const HTTPRequest& req, std::string& why) {
+    const std::string origin = req.Header("origin");
+    if (origin.empty()) return true;
+    const std::string host = req.Header("host");
+    if (host.empty() || (origin != "http://" + host && origin != "https://" + host)) {
+        why = "cross-origin request refused";
+        return false;
+    }
+    const std::string ct = ToLower(req.Header("content-type"));
+    if (ct.compare(0, 16, "application/json") != 0) {
+        why = "browser requests must be application/json";
+        return false;
+    }
+    if (req.Header("x-requested-with").empty()) {
+        why = "browser requests must carry X-Requested-With";
+        return false;
+    }
+    return true;
+}
+
 static bool HTTPReq_JSONRPC(const HTTPRequest& req, HTTPReply& rep) {
     if (req.method != "POST") {
         rep.status = 405;
         rep.body = "JSONRPC server handles only POST requests";
+        rep.contentType = "text/plain";
+        return false;
+    }
+    std::string why;
+    if (!BrowserRequestAllowed(req, why)) {
+        LogPrintf("ThreadRPCServer refused browser request from %s: %s\n", req.peer.c_str(), why.c_str());
+        rep.status = 403;
+        rep.body = why;
         rep.contentType = "text/plain";
         return false;
     }

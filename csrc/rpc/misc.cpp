@@ -258,7 +258,7 @@ static UniValue execconsole(const JSONRPCRequest& req) {
     try {
         std::string dummy;
         RPCParseCommandLine(dummy, line, nullptr, &filtered);
-    } catch (const std::runtime_error&) {
+    } catch (const std::exception&) {
         filtered = IsSensitiveConsoleCommand(line.substr(0, line.find_first_of(" (\t"))) ? "" : line;
     }
     const ConsoleExecutor exec = [](const std::string& m, const std::vector<std::string>& a) {

@@ -65,7 +65,7 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 const TABS=[["overview","Overview"],["send","Send"],["receive","Receive"],["transactions","Transactions"],["signverify","Sign / verify"],["peers","Peers"],["mining","Mining"],["console","Console"]];
 let rpcId=0;
 async function rpc(method,params=[]){
-  const r=await fetch("/",{method:"POST",credentials:"same-origin",headers:{"Content-Type":"application/json"},
+  const r=await fetch("/",{method:"POST",credentials:"same-origin",headers:{"Content-Type":"application/json","X-Requested-With":"bcp-webgui"},
     body:JSON.stringify({jsonrpc:"1.0",id:++rpcId,method:method,params:params})});
   const j=await r.json(); if(j.error) throw j.error; return j.result;}
 const $=id=>document.getElementById(id);

@@ -424,7 +424,8 @@ void WorkerPool::ParallelFor(size_t n, const std::function<void(size_t)>& fn, si
         for (size_t i = 0; i < n; i++) fn(i);
         return;
     }
-    static std::mutex serialize; // one job at a time per process
+    // one job at a time per pool (a nested ParallelFor on the same pool from inside fn would
+    // deadlock; fn may use another pool)
     std::lock_guard<std::mutex> one(serialize);
     {
         std::lock_guard<std::mutex> l(m);

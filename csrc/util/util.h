@@ -128,7 +128,7 @@ public:
 private:
     void Loop();
     std::vector<std::thread> threads;
-    std::mutex m;
+    std::mutex m, serialize;
     std::condition_variable cv, cvDone;
     const std::function<void(size_t)>* job = nullptr;
     size_t jobN = 0, grainSz = 1;

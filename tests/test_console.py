@@ -78,6 +78,19 @@ def test_syntax_errors():
         run("a(getblockchaininfo(True))")
 
 
+def test_hostile_lines():
+    """Deep nesting is a syntax error, not a stack overflow (with or without execution), and an
+    array index longer than any array is out of range, not an uncaught std::out_of_range."""
+    deep = "a(" * 100000
+    with pytest.raises(RuntimeError, match="Invalid Syntax"):
+        run(deep)
+    with pytest.raises(RuntimeError, match="Invalid Syntax"):
+        native.console_parse(deep)
+    assert run("getbestblockhash(" * 60 + ")" * 60) == "00ab"  # 60 levels are still fine
+    assert run("getblock(getbestblockhash())[tx][99999999999999999999]") == "null"
+    assert run("getblock(getbestblockhash())[tx][1]") == "ffee"
+
+
 def test_history_filter():
     assert filtered("importprivkey") == "importprivkey(…)"
     assert filtered("signmessagewithprivkey abc") == "signmessagewithprivkey(…)"

@@ -137,7 +137,7 @@ def test_gpu_solver_matches_cpu(native, n, k):
         found += len(g)
         # the GPU may drop rows on bucket overflow but must not invent solutions
         assert set(g) <= c or not c
-    assert found >= 0.8 * sum(len(c) for c in cpu)
+    assert found >= 0.97 * sum(len(c) for c in cpu)
 
 
 @pytest.mark.gpu
@@ -168,29 +168,49 @@ def test_gpu_solver_tree_dump_96_5(native):
 
 @pytest.mark.gpu
 def test_gpu_solver_200_9(native):
-    solver = native.EquihashGpuSolver(200, 9, 2)
+    """Recall pinned against the CPU reference solver over 16 mainnet-parameter nonces: the GPU
+    never reports a solution the CPU does not find, and finds at least 97% of the CPU's
+    (measured: 54 of 54 over 32 nonces, gpurun_out r3a/recall.json)."""
+    import concurrent.futures as cf
     states = []
-    for nonce in range(4):
+    for nonce in range(16):
         st = native.EquihashState(200, 9)
         st.update(header_input(nonce, b"main"))
         states.append(st)
-    res = solver.solve(states[:2]) + solver.solve(states[2:])
+    with cf.ThreadPoolExecutor(8) as ex:  # the binding releases the GIL
+        cpu = list(ex.map(lambda st: set(native.eh_solve_cpu(200, 9, st)[0]), states))
+    solver = native.EquihashGpuSolver(200, 9, 8)
+    res = solver.solve(states[:8]) + solver.solve(states[8:])
     total = 0
-    for st, sols in zip(states, res):
+    for st, sols, c in zip(states, res, cpu):
         for s in sols:
             assert len(s) == 1344
             assert native.eh_is_valid_solution(200, 9, st, s)[0]
+            assert s in c
         total += len(sols)
-    assert total >= 2  # ~1.9 solutions per nonce expected
-    # cross-check against the CPU reference solver: never a solution the CPU does not
-    # find; bucket-capacity drops make the GPU miss a few (these 4 nonces hold 14
-    # CPU solutions, unusually many of them sharing subtrees; the GPU finds 10-12)
-    cpu_total = 0
-    for st, sols in zip(states, res):
-        cpu, _ = native.eh_solve_cpu(200, 9, st)
-        assert set(sols) <= set(cpu)
-        cpu_total += len(cpu)
-    assert total >= 0.6 * cpu_total
+    cpu_total = sum(map(len, cpu))
+    assert cpu_total >= 16  # ~1.7-1.9 per nonce
+    assert total >= 0.97 * cpu_total, (total, cpu_total)
+
+
+@pytest.mark.gpu
+def test_gpu_solver_recall_small(native):
+    """(48,5) / (96,5): GPU recall >= 0.97 of the CPU solver over 64 nonces."""
+    for n, k in [(48, 5), (96, 5)]:
+        solver = native.EquihashGpuSolver(n, k, 16)
+        cpu_total = gpu_total = 0
+        for b0 in range(0, 64, 16):
+            states = []
+            for nonce in range(b0, b0 + 16):
+                st = native.EquihashState(n, k)
+                st.update(header_input(nonce, b"recall"))
+                states.append(st)
+            for st, g in zip(states, solver.solve(states)):
+                c = set(native.eh_solve_cpu(n, k, st)[0])
+                assert set(g) <= c
+                cpu_total += len(c)
+                gpu_total += len(g)
+        assert cpu_total > 0 and gpu_total >= 0.97 * cpu_total, (n, k, gpu_total, cpu_total)
 
 
 @pytest.mark.gpu

@@ -12,19 +12,19 @@ from bitcoincashplus_amd.node.process import BcpdProcess
 pytestmark = pytest.mark.functional
 
 
-def _get(port, path, auth=None, method="GET"):
+def _get(port, path, auth=None, method="GET", headers=None, body=None):
     c = http.client.HTTPConnection("127.0.0.1", port, timeout=30)
-    h = {}
+    h = dict(headers or {})
     if auth:
         h["Authorization"] = "Basic " + base64.b64encode(auth.encode()).decode()
-    c.request(method, path, headers=h)
+    c.request(method, path, body=body, headers=h)
     r = c.getresponse()
     body = r.read()
     return r.status, dict(r.getheaders()), body
 
 
 def test_webgui(tmp_path):
-    n = BcpdProcess(str(tmp_path / "g"), extra_args=["-gpu=0"])
+    n = BcpdProcess(str(tmp_path / "g"), extra_args=["-gpu=0", "-webgui=1"])
     n.start()
     try:
         st, hdr, _ = _get(n.rpcport, "/gui")
@@ -72,11 +72,40 @@ def test_webgui(tmp_path):
     finally:
         n.stop()
 
-    # -webgui=0 turns the page off
-    m = BcpdProcess(str(tmp_path / "h"), extra_args=["-gpu=0", "-webgui=0"])
+    # the page is off by default
+    m = BcpdProcess(str(tmp_path / "h"), extra_args=["-gpu=0"])
     m.start()
     try:
         st, _, _ = _get(m.rpcport, "/gui", auth="rt:rtpass")
         assert st == 404
     finally:
         m.stop()
+
+
+def test_rpc_refuses_cross_site_browser_requests(tmp_path):
+    """A browser on another site may hold Basic credentials cached for the GUI: a cross-origin
+    "simple" POST (text/plain, no custom header) must not reach the RPC table, while the GUI's
+    own same-origin JSON request and non-browser clients (no Origin) are served."""
+    n = BcpdProcess(str(tmp_path / "c"), extra_args=["-gpu=0", "-webgui=1"])
+    n.start()
+    try:
+        body = '{"method":"getblockcount","params":[],"id":1}'
+        host = f"127.0.0.1:{n.rpcport}"
+        cases = [
+            ({"Origin": "http://evil.example", "Content-Type": "text/plain"}, 403),
+            ({"Origin": "http://evil.example", "Content-Type": "application/json",
+              "X-Requested-With": "x"}, 403),
+            ({"Origin": "http://" + host, "Content-Type": "text/plain", "X-Requested-With": "x"}, 403),
+            ({"Origin": "http://" + host, "Content-Type": "application/json"}, 403),
+            ({"Origin": "null", "Content-Type": "application/json", "X-Requested-With": "x"}, 403),
+            ({"Origin": "http://" + host, "Content-Type": "application/json",
+              "X-Requested-With": "bcp-webgui"}, 200),
+            ({"Content-Type": "text/plain"}, 200),  # curl / bcp-cli style, no Origin
+        ]
+        for hdr, want in cases:
+            st, _, out = _get(n.rpcport, "/", auth="rt:rtpass", method="POST", headers=hdr, body=body)
+            assert st == want, (hdr, st, out)
+            if want == 200:
+                assert b'"result":0' in out.replace(b" ", b"")
+    finally:
+        n.stop()
