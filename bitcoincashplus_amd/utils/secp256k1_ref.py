@@ -133,6 +133,19 @@ def der_encode(r: int, s: int) -> bytes:
     return b"\x30" + bytes([len(body)]) + body
 
 
+def der_decode(sig: bytes):
+    """(r, s) of a strict DER signature (as produced by der_encode / the node's signer)."""
+    if len(sig) < 8 or sig[0] != 0x30 or sig[2] != 0x02:
+        raise ValueError("not a DER signature")
+    lr = sig[3]
+    r = int.from_bytes(sig[4:4 + lr], "big")
+    off = 4 + lr
+    if sig[off] != 0x02:
+        raise ValueError("not a DER signature")
+    ls = sig[off + 1]
+    return r, int.from_bytes(sig[off + 2:off + 2 + ls], "big")
+
+
 def verify(pub: bytes, r: int, s: int, msg32: bytes, require_low_s=True) -> bool:
     Q = parse_pubkey(pub)
     if Q is None or not (0 < r < N and 0 < s < N):

@@ -1,6 +1,7 @@
 #include "consensus/pow.h"
 #include "consensus/equihash.h"
 #include "kernels/gpu_api.h"
+#include "node/gpuverify.h"
 #include "util/util.h"
 
 #include <algorithm>
@@ -129,13 +130,14 @@ std::vector<bool> CheckEquihashSolutions(const std::vector<const CBlockHeader*>&
         try {
             if (GpuFaultInjection()) throw std::runtime_error("injected GPU Equihash-verify fault");
             std::vector<gpu::EhBaseState> states;
-            std::vector<std::vector<unsigned char>> sols;
+            std::vector<const std::vector<unsigned char>*> sols;
             states.reserve(headers.size());
             for (const CBlockHeader* h : headers) {
                 states.push_back(gpu::MakeEhBaseState(EquihashStateFor(h, ep)));
-                sols.push_back(h->nSolution);
+                sols.push_back(&h->nSolution);
             }
-            std::vector<uint8_t> r = gpu::EquihashVerifyBatch(ep.N, ep.K, states, sols);
+            // sharded across the validation GPUs (node/gpuverify.h)
+            std::vector<uint8_t> r = GpuVerifyService::Instance().Equihash(ep.N, ep.K, states, sols);
             for (size_t i = 0; i < r.size(); ++i) out[i] = r[i] != 0;
             gpuFailures = 0;
             return out;

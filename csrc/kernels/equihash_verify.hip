@@ -18,6 +18,10 @@
 #include "kernels/hip_util.h"
 
 #include <cstring>
+#include <memory>
+#include <mutex>
+
+#include <cstring>
 #include <stdexcept>
 
 namespace bcpk {
@@ -131,45 +135,94 @@ __global__ __launch_bounds__(C::NTH) void eh_verify(const EhBaseState* __restric
 namespace bcp {
 namespace gpu {
 
+// Stages n (state, solution) pairs through the lane's pinned buffers: one H2D copy of the
+// packed states + solutions, one kernel (one workgroup per solution), one D2H copy.
 template <class C>
-static std::vector<uint8_t> verify_impl(const std::vector<EhBaseState>& states,
-                                        const std::vector<std::vector<unsigned char>>& sols, int device) {
-    UseDevice(device);
-    const size_t n = states.size();
-    std::vector<uint8_t> result(n, 0);
-    if (n == 0) return result;
-    std::vector<uint8_t> packed(n * C::SOLW, 0);
+static void verify_lane(LaneState& L, const EhBaseState* states, const std::vector<unsigned char>* const* sols,
+                        size_t n, uint8_t* result) {
+    if (n == 0) return;
+    BCP_HIP_CHECK(hipSetDevice(L.device));
+    const size_t sb = n * sizeof(EhBaseState), pb = n * C::SOLW;
+    unsigned char* h_in = L.Host(0, sb + pb);
+    uint8_t* h_ok = L.Host(1, n);
+    memcpy(h_in, states, sb);
     std::vector<char> lenok(n, 0);
     for (size_t i = 0; i < n; ++i) {
-        if (sols[i].size() == (size_t)C::SOLW) {
-            memcpy(&packed[i * C::SOLW], sols[i].data(), C::SOLW);
+        unsigned char* dst = h_in + sb + i * C::SOLW;
+        if (sols[i]->size() == (size_t)C::SOLW) {
+            memcpy(dst, sols[i]->data(), C::SOLW);
             lenok[i] = 1;
+        } else {
+            memset(dst, 0, C::SOLW);
         }
     }
-    DevBuf<bcpk::EhBaseState> d_states(n);
-    DevBuf<uint8_t> d_sols(packed.size()), d_ok(n);
-    hipStream_t s;
-    BCP_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    BCP_HIP_CHECK(hipMemcpyAsync(d_states.p, states.data(), n * sizeof(EhBaseState), hipMemcpyHostToDevice, s));
-    BCP_HIP_CHECK(hipMemcpyAsync(d_sols.p, packed.data(), packed.size(), hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL((bcpk::eh_verify<C>), dim3(n), dim3(C::NTH), 0, s, d_states.p, d_sols.p, d_ok.p);
+    unsigned char* d_in = L.Dev(0, sb + pb);
+    uint8_t* d_ok = L.Dev(1, n);
+    BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, sb + pb, hipMemcpyHostToDevice, L.stream));
+    hipLaunchKernelGGL((bcpk::eh_verify<C>), dim3(n), dim3(C::NTH), 0, L.stream,
+                       reinterpret_cast<const bcpk::EhBaseState*>(d_in), (const uint8_t*)(d_in + sb), d_ok);
     BCP_HIP_CHECK(hipGetLastError());
-    BCP_HIP_CHECK(hipMemcpyAsync(result.data(), d_ok.p, n, hipMemcpyDeviceToHost, s));
-    BCP_HIP_CHECK(hipStreamSynchronize(s));
-    BCP_HIP_CHECK(hipStreamDestroy(s));
-    for (size_t i = 0; i < n; ++i)
-        if (!lenok[i]) result[i] = 0; // reference: invalid solution length
-    return result;
+    BCP_HIP_CHECK(hipMemcpyAsync(h_ok, d_ok, n, hipMemcpyDeviceToHost, L.stream));
+    BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
+    for (size_t i = 0; i < n; ++i) result[i] = lenok[i] ? h_ok[i] : 0; // reference: invalid solution length
+    L.batches++;
+    L.items += n;
+}
+
+VerifyLane::VerifyLane(int device, bool highPriority) : impl(new Impl) {
+    impl->device = UseDevice(device);
+    int least = 0, greatest = 0;
+    BCP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    impl->priority = highPriority ? greatest : least;
+    BCP_HIP_CHECK(hipStreamCreateWithPriority(&impl->stream, hipStreamNonBlocking, impl->priority));
+}
+VerifyLane::~VerifyLane() {
+    if (impl && impl->stream) {
+        (void)hipSetDevice(impl->device);
+        (void)hipStreamSynchronize(impl->stream);
+        (void)hipStreamDestroy(impl->stream);
+    }
+}
+int VerifyLane::Device() const { return impl->device; }
+int VerifyLane::Priority() const { return impl->priority; }
+uint64_t VerifyLane::Batches() const { return impl->batches; }
+uint64_t VerifyLane::Items() const { return impl->items; }
+
+void VerifyLane::Equihash(unsigned N, unsigned K, const EhBaseState* states,
+                          const std::vector<unsigned char>* const* sols, size_t n, uint8_t* result) {
+    if (N == 200 && K == 9) return verify_lane<bcpk::EvCfg<200, 9>>(*impl, states, sols, n, result);
+    if (N == 96 && K == 5) return verify_lane<bcpk::EvCfg<96, 5>>(*impl, states, sols, n, result);
+    if (N == 48 && K == 5) return verify_lane<bcpk::EvCfg<48, 5>>(*impl, states, sols, n, result);
+    if (N == 96 && K == 3) return verify_lane<bcpk::EvCfg<96, 3>>(*impl, states, sols, n, result);
+    throw std::invalid_argument("EquihashVerifyBatch: unsupported (N,K)");
+}
+
+// One default (normal-priority) lane per device for the plain batch API.
+static VerifyLane& DefaultLane(int device, std::unique_lock<std::mutex>& hold) {
+    static std::mutex m;
+    static std::unique_ptr<VerifyLane> lanes[64];
+    static std::mutex use[64];
+    const int dev = UseDevice(device);
+    if (dev >= 64) throw std::runtime_error("device index out of range");
+    {
+        std::lock_guard<std::mutex> l(m);
+        if (!lanes[dev]) lanes[dev].reset(new VerifyLane(dev, false));
+    }
+    hold = std::unique_lock<std::mutex>(use[dev]);
+    return *lanes[dev];
 }
 
 std::vector<uint8_t> EquihashVerifyBatch(unsigned n, unsigned k, const std::vector<EhBaseState>& states,
                                          const std::vector<std::vector<unsigned char>>& solutions, int device) {
     if (states.size() != solutions.size()) throw std::invalid_argument("states/solutions size mismatch");
-    if (n == 200 && k == 9) return verify_impl<bcpk::EvCfg<200, 9>>(states, solutions, device);
-    if (n == 96 && k == 5) return verify_impl<bcpk::EvCfg<96, 5>>(states, solutions, device);
-    if (n == 48 && k == 5) return verify_impl<bcpk::EvCfg<48, 5>>(states, solutions, device);
-    if (n == 96 && k == 3) return verify_impl<bcpk::EvCfg<96, 3>>(states, solutions, device);
-    throw std::invalid_argument("EquihashVerifyBatch: unsupported (N,K)");
+    std::vector<uint8_t> result(states.size(), 0);
+    if (states.empty()) return result;
+    std::vector<const std::vector<unsigned char>*> ptrs(solutions.size());
+    for (size_t i = 0; i < solutions.size(); ++i) ptrs[i] = &solutions[i];
+    std::unique_lock<std::mutex> hold;
+    VerifyLane& lane = DefaultLane(device, hold);
+    lane.Equihash(n, k, states.data(), ptrs.data(), states.size(), result.data());
+    return result;
 }
 
 bool GpuAvailable() {

@@ -103,5 +103,36 @@ int64_t Sha256dScanNonces(const unsigned char header80[80], const unsigned char 
 std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
                                       const std::vector<unsigned char>& pub33, int device = -1);
 
+// --------------------------------------------------------------- verification lanes
+// A verification lane is one device plus one HIP stream (created at the device's greatest
+// priority when `highPriority`, so a validation batch is scheduled ahead of the persistent
+// solver kernels the miner keeps on the same device) plus grow-only pinned host staging and
+// device buffers that every batch reuses (one H2D and one D2H copy per batch, no pageable
+// transfers, no per-batch allocation). A lane is driven by one thread at a time; the node's
+// GpuVerifyService gives each lane its own service thread (csrc/node/gpuverify.h).
+class VerifyLane {
+public:
+    VerifyLane(int device, bool highPriority);
+    ~VerifyLane();
+    VerifyLane(const VerifyLane&) = delete;
+    VerifyLane& operator=(const VerifyLane&) = delete;
+    int Device() const;
+    int Priority() const;
+    // Same contract as EcdsaVerifyBatch: n packed jobs, result[i] = 1 iff valid.
+    void Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33, size_t n,
+               uint8_t* result);
+    // Same contract as EquihashVerifyBatch for n (state, solution) pairs; a solution of the
+    // wrong length is rejected.
+    void Equihash(unsigned N, unsigned K, const EhBaseState* states, const std::vector<unsigned char>* const* sols,
+                  size_t n, uint8_t* result);
+    // Batches and items this lane has run (service statistics).
+    uint64_t Batches() const;
+    uint64_t Items() const;
+    struct Impl;
+
+private:
+    std::unique_ptr<Impl> impl;
+};
+
 } // namespace gpu
 } // namespace bcp

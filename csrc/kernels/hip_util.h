@@ -2,6 +2,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "kernels/gpu_api.h"
+
 #include <stdexcept>
 #include <string>
 
@@ -64,6 +66,28 @@ template <typename T> struct HostBuf {
     }
     ~HostBuf() { release(); }
 };
+
+// Per-lane execution state (VerifyLane::Impl, gpu_api.h): a stream and grow-only staging.
+// Slots index independent buffers so one batch can stage several arrays.
+struct LaneState {
+    int device = 0;
+    int priority = 0;
+    hipStream_t stream = nullptr;
+    static constexpr int SLOTS = 4;
+    HostBuf<unsigned char> host[SLOTS];
+    DevBuf<unsigned char> dev[SLOTS];
+    uint64_t batches = 0, items = 0;
+    unsigned char* Host(int slot, size_t bytes) {
+        if (host[slot].n < bytes) host[slot].alloc(bytes + bytes / 2);
+        return host[slot].p;
+    }
+    unsigned char* Dev(int slot, size_t bytes) {
+        if (dev[slot].n < bytes) dev[slot].alloc(bytes + bytes / 2);
+        return dev[slot].p;
+    }
+};
+
+struct VerifyLane::Impl : LaneState {};
 
 } // namespace gpu
 } // namespace bcp

@@ -1054,28 +1054,20 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
     out[idx] = (ok && match && J.scalar_ok) ? 1 : 0;
 }
 
-// Device-resident verifier state, one per HIP device: the generator comb table, the
-// stream and the grow-only job/input buffers all belong to the device they were
-// allocated on, so a call for device d never touches another device's pointers.
-struct State {
+// Generator comb table, one per HIP device (read-only once built, shared by every lane).
+struct Table {
     std::once_flag once;
     uint32_t* d_gtab = nullptr;
-    std::mutex m;
-    Job* d_jobs = nullptr;
-    uint8_t* d_out = nullptr;
-    unsigned char* d_in = nullptr; // packed msg32 | sig64 | pub33 arrays, cap entries each
-    size_t cap = 0;
-    hipStream_t stream = nullptr;
 };
 constexpr int MAX_DEVICES = 64;
-State& S(int device) {
-    static State s[MAX_DEVICES];
+Table& T(int device) {
+    static Table t[MAX_DEVICES];
     if (device < 0 || device >= MAX_DEVICES) throw std::runtime_error("EcdsaVerifyBatch: device id out of range");
-    return s[device];
+    return t[device];
 }
 
-// Builds the table on the current device (the caller made `st`'s device current).
-void InitTable(State& st) {
+// Builds the table on the current device (the caller made `tb`'s device current).
+void InitTable(Table& tb) {
     // 32 x 256 affine points, 8 LE limbs for x then y
     const std::vector<secp::Ge>& t = secp::generator_table();
     std::vector<uint32_t> h(32 * 256 * 16, 0);
@@ -1091,50 +1083,64 @@ void InitTable(State& st) {
             h[e * 16 + 8 + k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
         }
     }
-    BCP_HIP_CHECK(hipMalloc(&st.d_gtab, h.size() * 4));
-    BCP_HIP_CHECK(hipMemcpy(st.d_gtab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
-    BCP_HIP_CHECK(hipStreamCreateWithFlags(&st.stream, hipStreamNonBlocking));
+    BCP_HIP_CHECK(hipMalloc(&tb.d_gtab, h.size() * 4));
+    BCP_HIP_CHECK(hipMemcpy(tb.d_gtab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
 }
 
 } // namespace
 
+// Host: pack z / (r,s) / key into the lane's pinned staging (one H2D copy); the prep kernel builds
+// the Jobs and does all scalar arithmetic; one D2H copy of the verdicts.
+void VerifyLane::Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33, size_t n,
+                       uint8_t* result) {
+    if (n == 0) return;
+    LaneState& L = *impl;
+    BCP_HIP_CHECK(hipSetDevice(L.device));
+    Table& tb = T(L.device);
+    // a throwing init leaves the once_flag unset, so the next call retries it
+    std::call_once(tb.once, [&] { InitTable(tb); });
+    unsigned char* h_in = L.Host(0, n * 129);
+    uint8_t* h_out = L.Host(1, n);
+    memcpy(h_in, msg32, n * 32);
+    memcpy(h_in + n * 32, sig64, n * 64);
+    memcpy(h_in + n * 96, pub33, n * 33);
+    unsigned char* d_in = L.Dev(0, n * 129);
+    Job* d_jobs = reinterpret_cast<Job*>(L.Dev(1, n * sizeof(Job)));
+    uint8_t* d_out = L.Dev(2, n);
+    BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, n * 129, hipMemcpyHostToDevice, L.stream));
+    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, L.stream, d_jobs,
+                       (const unsigned char*)d_in, (const unsigned char*)(d_in + n * 32),
+                       (const unsigned char*)(d_in + n * 96), (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+    const int grid = (int)((n + WG - 1) / WG);
+    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, L.stream, d_jobs, tb.d_gtab, d_out, (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+    BCP_HIP_CHECK(hipMemcpyAsync(h_out, d_out, n, hipMemcpyDeviceToHost, L.stream));
+    BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
+    memcpy(result, h_out, n);
+    L.batches++;
+    L.items += n;
+}
+
 std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
                                       const std::vector<unsigned char>& pub33, int device) {
     const size_t n = msg32.size() / 32;
-    if (sig64.size() != n * 64 || pub33.size() != n * 33) throw std::invalid_argument("EcdsaVerifyBatch: sizes");
+    if (msg32.size() != n * 32 || sig64.size() != n * 64 || pub33.size() != n * 33)
+        throw std::invalid_argument("EcdsaVerifyBatch: sizes");
     std::vector<uint8_t> result(n, 0);
     if (n == 0) return result;
+    // one normal-priority lane per device for the plain batch API
+    static std::mutex m;
+    static std::unique_ptr<VerifyLane> lanes[MAX_DEVICES];
+    static std::mutex use[MAX_DEVICES];
     const int dev = UseDevice(device);
-    State& st = S(dev);
-    // a throwing init leaves the once_flag unset, so the next call retries it
-    std::call_once(st.once, [&] { InitTable(st); });
-
-    // host: upload the packed z / (r,s) / key arrays; the prep kernel builds the Jobs and does
-    // all scalar arithmetic
-    std::lock_guard<std::mutex> l(st.m);
-    if (st.cap < n) {
-        if (st.d_jobs) BCP_HIP_CHECK(hipFree(st.d_jobs));
-        if (st.d_out) BCP_HIP_CHECK(hipFree(st.d_out));
-        if (st.d_in) BCP_HIP_CHECK(hipFree(st.d_in));
-        st.cap = std::max<size_t>(n, 4096);
-        BCP_HIP_CHECK(hipMalloc(&st.d_jobs, st.cap * sizeof(Job)));
-        BCP_HIP_CHECK(hipMalloc(&st.d_out, st.cap));
-        BCP_HIP_CHECK(hipMalloc(&st.d_in, st.cap * 129));
+    if (dev >= MAX_DEVICES) throw std::runtime_error("EcdsaVerifyBatch: device id out of range");
+    {
+        std::lock_guard<std::mutex> l(m);
+        if (!lanes[dev]) lanes[dev].reset(new VerifyLane(dev, false));
     }
-    unsigned char* d_msg = st.d_in;
-    unsigned char* d_sig = d_msg + st.cap * 32;
-    unsigned char* d_pub = d_sig + st.cap * 64;
-    BCP_HIP_CHECK(hipMemcpyAsync(d_msg, msg32.data(), n * 32, hipMemcpyHostToDevice, st.stream));
-    BCP_HIP_CHECK(hipMemcpyAsync(d_sig, sig64.data(), n * 64, hipMemcpyHostToDevice, st.stream));
-    BCP_HIP_CHECK(hipMemcpyAsync(d_pub, pub33.data(), n * 33, hipMemcpyHostToDevice, st.stream));
-    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st.stream, st.d_jobs,
-                       (const unsigned char*)d_msg, (const unsigned char*)d_sig, (const unsigned char*)d_pub, (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    const int grid = (int)((n + WG - 1) / WG);
-    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, st.stream, st.d_jobs, st.d_gtab, st.d_out, (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    BCP_HIP_CHECK(hipMemcpyAsync(result.data(), st.d_out, n, hipMemcpyDeviceToHost, st.stream));
-    BCP_HIP_CHECK(hipStreamSynchronize(st.stream));
+    std::lock_guard<std::mutex> hold(use[dev]);
+    lanes[dev]->Ecdsa(msg32.data(), sig64.data(), pub33.data(), n, result.data());
     return result;
 }
 

@@ -1,0 +1,216 @@
+#include "node/gpuverify.h"
+
+#include "util/util.h"
+
+#include <algorithm>
+#include <atomic>
+#include <exception>
+#include <stdexcept>
+
+namespace bcp {
+
+GpuVerifyService& GpuVerifyService::Instance() {
+    static GpuVerifyService s;
+    return s;
+}
+
+GpuVerifyService::~GpuVerifyService() { Shutdown(); }
+
+void GpuVerifyService::Shutdown() {
+    std::vector<std::shared_ptr<Lane>> old;
+    {
+        std::lock_guard<std::mutex> l(m);
+        old.swap(lanes);
+        lanesStale = true;
+    }
+    for (auto& L : old) {
+        {
+            std::lock_guard<std::mutex> l(L->m);
+            L->stop = true;
+        }
+        L->cv.notify_all();
+        if (L->th.joinable()) L->th.join();
+    }
+}
+
+void GpuVerifyService::SetDevices(const std::vector<int>& devs) {
+    std::lock_guard<std::mutex> l(m);
+    devices = devs;
+    lanesStale = true;
+}
+
+std::vector<int> GpuVerifyService::Devices() const {
+    std::lock_guard<std::mutex> l(m);
+    if (!devices.empty()) return devices;
+    if (gpu::GpuAvailable()) return {0};
+    return {};
+}
+
+std::vector<int> GpuVerifyService::ConfiguredDevices() const {
+    std::lock_guard<std::mutex> l(m);
+    return devices;
+}
+
+void GpuVerifyService::SetMinShard(size_t ecdsa, size_t equihash) {
+    std::lock_guard<std::mutex> l(m);
+    minShardEcdsa = std::max<size_t>(1, ecdsa);
+    minShardEquihash = std::max<size_t>(1, equihash);
+}
+
+void GpuVerifyService::LaneLoop(Lane* L) {
+    RenameThread(("bcp-gpuverify" + std::to_string(L->device)).c_str());
+    try {
+        L->gl.reset(new gpu::VerifyLane(L->device, /*highPriority=*/true));
+        L->priority = L->gl->Priority();
+    } catch (const std::exception& e) {
+        L->initError = e.what();
+    }
+    for (;;) {
+        std::function<void()> task;
+        {
+            std::unique_lock<std::mutex> l(L->m);
+            L->cv.wait(l, [&] { return L->stop || !L->q.empty(); });
+            if (L->q.empty()) break; // stop requested and nothing queued
+            task = std::move(L->q.front());
+            L->q.pop_front();
+        }
+        task(); // tasks check L->gl / initError themselves (see RunSharded)
+    }
+    L->gl.reset();
+}
+
+std::vector<std::shared_ptr<GpuVerifyService::Lane>> GpuVerifyService::AcquireLanes() {
+    std::vector<std::shared_ptr<Lane>> retire;
+    std::vector<std::shared_ptr<Lane>> cur;
+    {
+        std::lock_guard<std::mutex> l(m);
+        if (lanesStale) {
+            std::vector<int> devs = devices;
+            if (devs.empty() && gpu::GpuAvailable()) devs = {0};
+            retire.swap(lanes);
+            for (int d : devs) {
+                auto L = std::make_shared<Lane>();
+                L->device = d;
+                L->th = std::thread(LaneLoop, L.get());
+                lanes.push_back(L);
+            }
+            lanesStale = false;
+        }
+        cur = lanes;
+    }
+    for (auto& L : retire) { // old lanes finish what they hold, then exit
+        {
+            std::lock_guard<std::mutex> l(L->m);
+            L->stop = true;
+        }
+        L->cv.notify_all();
+        if (L->th.joinable()) L->th.join();
+    }
+    return cur;
+}
+
+void GpuVerifyService::RunSharded(size_t n, size_t minShard,
+                                  const std::function<void(gpu::VerifyLane&, size_t, size_t)>& fn) {
+    std::vector<std::shared_ptr<Lane>> ls = AcquireLanes();
+    if (ls.empty()) throw std::runtime_error("GpuVerifyService: no validation GPU");
+    const size_t shards = std::max<size_t>(1, std::min(ls.size(), n / minShard));
+    struct Latch {
+        std::mutex m;
+        std::condition_variable cv;
+        size_t left;
+        std::exception_ptr err;
+    } latch;
+    latch.left = shards;
+    if (shards > 1) {
+        std::lock_guard<std::mutex> l(m);
+        sharded++;
+    }
+    const size_t base = n / shards, extra = n % shards;
+    size_t lo = 0;
+    for (size_t s = 0; s < shards; s++) {
+        const size_t hi = lo + base + (s < extra ? 1 : 0);
+        Lane* L = ls[s].get();
+        auto task = [&fn, &latch, L, lo, hi]() {
+            std::exception_ptr e;
+            try {
+                if (!L->gl) throw std::runtime_error("GPU verify lane on device " + std::to_string(L->device) +
+                                                     " unavailable: " + L->initError);
+                fn(*L->gl, lo, hi);
+                L->batches++;
+                L->items += hi - lo;
+            } catch (...) {
+                e = std::current_exception();
+            }
+            std::lock_guard<std::mutex> l(latch.m);
+            if (e && !latch.err) latch.err = e;
+            if (--latch.left == 0) latch.cv.notify_all();
+        };
+        bool queued = false;
+        {
+            std::lock_guard<std::mutex> l(L->m);
+            if (!L->stop) { // a lane retired by a concurrent SetDevices takes no new work
+                L->q.push_back(task);
+                queued = true;
+            }
+        }
+        if (queued) {
+            L->cv.notify_one();
+        } else {
+            std::lock_guard<std::mutex> l(latch.m);
+            if (!latch.err) latch.err = std::make_exception_ptr(std::runtime_error("GPU verify lane retired"));
+            --latch.left;
+        }
+        lo = hi;
+    }
+    std::unique_lock<std::mutex> l(latch.m);
+    latch.cv.wait(l, [&] { return latch.left == 0; });
+    if (latch.err) std::rethrow_exception(latch.err);
+}
+
+std::vector<uint8_t> GpuVerifyService::Ecdsa(const unsigned char* msg32, const unsigned char* sig64,
+                                             const unsigned char* pub33, size_t n) {
+    std::vector<uint8_t> out(n, 0);
+    if (n == 0) return out;
+    size_t minShard;
+    {
+        std::lock_guard<std::mutex> l(m);
+        minShard = minShardEcdsa;
+    }
+    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi) {
+        lane.Ecdsa(msg32 + lo * 32, sig64 + lo * 64, pub33 + lo * 33, hi - lo, out.data() + lo);
+    });
+    return out;
+}
+
+std::vector<uint8_t> GpuVerifyService::Equihash(unsigned N, unsigned K, const std::vector<gpu::EhBaseState>& states,
+                                                const std::vector<const std::vector<unsigned char>*>& sols) {
+    if (states.size() != sols.size()) throw std::invalid_argument("GpuVerifyService::Equihash: sizes");
+    const size_t n = states.size();
+    std::vector<uint8_t> out(n, 0);
+    if (n == 0) return out;
+    size_t minShard;
+    {
+        std::lock_guard<std::mutex> l(m);
+        minShard = minShardEquihash;
+    }
+    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi) {
+        lane.Equihash(N, K, states.data() + lo, sols.data() + lo, hi - lo, out.data() + lo);
+    });
+    return out;
+}
+
+uint64_t GpuVerifyService::ShardedBatches() const {
+    std::lock_guard<std::mutex> l(m);
+    return sharded;
+}
+
+std::vector<GpuVerifyService::LaneStats> GpuVerifyService::Stats() const {
+    std::vector<LaneStats> out;
+    std::lock_guard<std::mutex> l(m);
+    for (const auto& L : lanes) {
+        out.push_back(LaneStats{L->device, L->priority.load(), L->batches.load(), L->items.load()});
+    }
+    return out;
+}
+
+} // namespace bcp

@@ -1,0 +1,92 @@
+// GPU verification service: the node's validation batches (ECDSA signatures of a block, the
+// Equihash solutions of a HEADERS message) sharded across the node's validation GPUs.
+//
+// Parity: reference src/checkqueue.h:27-164 (CCheckQueue: the master splits a block's script
+// checks across -par threads and AND-reduces the verdicts) and src/validation.cpp:2011-2127
+// (ConnectBlock's control.Add / control.Wait). The MI355X equivalent:
+//  * one service thread per lane owns the lane's HIP stream (created at the device's greatest
+//    stream priority, so a validation batch is scheduled ahead of the miner's persistent solver
+//    kernels on a shared device) and its pinned staging buffers (gpu::VerifyLane);
+//  * a batch is split into contiguous shards, one per lane, that run concurrently on their
+//    devices; per-item verdicts are gathered in order (the caller AND-reduces);
+//  * -gpuvalidationdevices selects the devices (default: device 0); the built-in miner leaves
+//    those devices alone whenever other GPUs are available (miner.cpp GetMinerGpuDevices);
+//  * a lane failure fails the whole call (the caller re-verifies on the CPU: a device fault
+//    must never decide validity).
+// A device may be listed twice (two lanes on one GPU, two streams): the test suite uses that
+// to exercise the sharded path on a one-GPU box.
+#pragma once
+#include "kernels/gpu_api.h"
+
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace bcp {
+
+class GpuVerifyService {
+public:
+    static GpuVerifyService& Instance();
+    ~GpuVerifyService();
+
+    // Validation devices (duplicates allowed: one lane each). Empty = default ({0} when a GPU
+    // is visible). Takes effect for the next batch; running batches finish on the old lanes.
+    void SetDevices(const std::vector<int>& devices);
+    std::vector<int> Devices() const;           // resolved list
+    std::vector<int> ConfiguredDevices() const; // as set (empty: default)
+    // Smallest shard worth a lane of its own (items); below 2x this a batch stays on one lane.
+    void SetMinShard(size_t ecdsa, size_t equihash);
+
+    // result[i] = 1 iff job i is valid (gpu::EcdsaVerifyBatch contract, packed arrays).
+    std::vector<uint8_t> Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33,
+                               size_t n);
+    // result[i] = 1 iff solution i is valid for state i.
+    std::vector<uint8_t> Equihash(unsigned N, unsigned K, const std::vector<gpu::EhBaseState>& states,
+                                  const std::vector<const std::vector<unsigned char>*>& sols);
+
+    struct LaneStats {
+        int device;
+        int priority;
+        uint64_t batches, items;
+    };
+    std::vector<LaneStats> Stats() const;
+    uint64_t ShardedBatches() const;
+    // Stops the service threads (process shutdown; later calls restart them).
+    void Shutdown();
+
+private:
+    GpuVerifyService() = default;
+    struct Lane {
+        int device = 0;
+        std::unique_ptr<gpu::VerifyLane> gl; // created on the lane's own thread
+        std::thread th;
+        std::mutex m;
+        std::condition_variable cv;
+        std::deque<std::function<void()>> q;
+        bool stop = false;
+        std::string initError;
+        std::atomic<int> priority{0};
+        std::atomic<uint64_t> batches{0}, items{0};
+    };
+    static void LaneLoop(Lane* L);
+    std::vector<std::shared_ptr<Lane>> AcquireLanes();
+    // Runs fn(lane, lo, hi) for the shards of [0, n) and waits; rethrows the first failure.
+    void RunSharded(size_t n, size_t minShard,
+                    const std::function<void(gpu::VerifyLane&, size_t, size_t)>& fn);
+
+    mutable std::mutex m;
+    std::vector<int> devices;
+    std::vector<std::shared_ptr<Lane>> lanes;
+    bool lanesStale = true;
+    size_t minShardEcdsa = 256, minShardEquihash = 32;
+    uint64_t sharded = 0;
+};
+
+} // namespace bcp

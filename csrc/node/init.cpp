@@ -5,6 +5,7 @@
 #include "consensus/params.h"
 #include "consensus/versionbits.h"
 #include "kernels/gpu_api.h"
+#include "node/gpuverify.h"
 #include "node/miner.h"
 #include "node/node.h"
 #include "node/policy.h"
@@ -51,6 +52,7 @@ std::string HelpMessage() {
         {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
         {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 512)"},
         {"-gpudevices=<list>", "Comma-separated GPU indices the built-in Equihash miner runs on, one host thread per device (default: all visible)"},
+        {"-gpuvalidationdevices=<list>", "Comma-separated GPU indices that verify block signatures and header solutions, one high-priority stream and service thread each; batches are sharded across them. When set, the built-in miner leaves these devices alone if others are available (default: device 0, shared with the miner)"},
         {"-gpufaultinjection", "(testing) make every validation GPU batch fail so the CPU fallback runs (default: 0)"},
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
@@ -297,6 +299,19 @@ int AppMain(int argc, char* argv[]) {
             devs.push_back((int)d);
         }
         SetMinerGpuDevices(devs);
+    }
+    if (gArgs.IsArgSet("-gpuvalidationdevices")) {
+        std::vector<int> devs;
+        for (const std::string& tok : SplitString(gArgs.GetArg("-gpuvalidationdevices", ""), ',')) {
+            if (tok.empty()) continue;
+            int64_t d = 0;
+            if (!ParseInt64(tok, &d) || d < 0 || d >= 64) {
+                InitError("Invalid -gpuvalidationdevices entry: " + tok);
+                return 1;
+            }
+            devs.push_back((int)d);
+        }
+        GpuVerifyService::Instance().SetDevices(devs);
     }
     InitSignatureCache(gArgs.GetArg("-maxsigcachesize", (int64_t)DEFAULT_MAX_SIG_CACHE_SIZE));
     InitScriptExecutionCache(gArgs.GetArg("-maxscriptcachesize", (int64_t)DEFAULT_MAX_SCRIPT_CACHE_SIZE));

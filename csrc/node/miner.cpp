@@ -1,4 +1,5 @@
 #include "node/miner.h"
+#include "node/gpuverify.h"
 
 #include <thread>
 #include "consensus/equihash.h"
@@ -294,8 +295,17 @@ std::vector<int> GetMinerGpuDevices() {
         std::lock_guard<std::mutex> l(g_devMinersMutex);
         d = g_minerDevices;
     }
-    if (d.empty())
-        for (int i = 0; i < gpu::DeviceCount(); i++) d.push_back(i);
+    if (d.empty()) {
+        // default: every visible device except the explicitly configured validation devices,
+        // unless that would leave none (then the miner shares them; validation lanes run at the
+        // device's greatest stream priority, csrc/node/gpuverify.h)
+        const std::vector<int> val = GpuVerifyService::Instance().ConfiguredDevices();
+        const int cnt = gpu::DeviceCount();
+        for (int i = 0; i < cnt; i++)
+            if (std::find(val.begin(), val.end(), i) == val.end()) d.push_back(i);
+        if (d.empty())
+            for (int i = 0; i < cnt; i++) d.push_back(i);
+    }
     return d;
 }
 
@@ -449,7 +459,7 @@ static bool SolveEquihash(CBlock& block, const CChainParams& params, uint64_t& n
         block.nSolution = soln;
         return CheckProofOfWork(block.GetHash(cp), block.nBits, true, cp);
     };
-    const bool gpuOk = useGpu && ep.N >= 96 && gpu::GpuAvailable();
+    const bool gpuOk = useGpu && gpu::GpuAvailable(); // (48,5) too: 0.086 vs 0.109 ms per nonce batch, profiles/baseline_metrics_r2s4.md
     if (gpuOk) {
         const CBlockHeader hdr = block.GetBlockHeader();
         auto accept = [&](const uint256& nonce, const std::vector<unsigned char>& soln) {

@@ -1,5 +1,6 @@
 #include "node/sigverify.h"
 #include "kernels/gpu_api.h"
+#include "node/gpuverify.h"
 #include "keys/key.h"
 #include "secp256k1/secp256k1.h"
 
@@ -102,7 +103,8 @@ std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*
     for (size_t j = 0; j < n; j++)
         if (!hostOk[j]) pub[j * 33] = 2; // keep device input well-formed; result masked below
     if (GpuFaultInjection()) throw std::runtime_error("injected GPU signature-verify fault");
-    std::vector<uint8_t> res = gpu::EcdsaVerifyBatch(msg, sig, pub);
+    // sharded across the validation GPUs by the verify service (one high-priority lane each)
+    std::vector<uint8_t> res = GpuVerifyService::Instance().Ecdsa(msg.data(), sig.data(), pub.data(), n);
     for (size_t j = 0; j < n; j++) res[j] &= hostOk[j];
     return res;
 }

@@ -1,6 +1,7 @@
 // Python bindings for the CDNA4 kernels (csrc/kernels/*.hip).
 #include "consensus/equihash.h"
 #include "kernels/gpu_api.h"
+#include "node/gpuverify.h"
 #include "python/bind.h"
 #include "node/miner.h"
 #include "node/sigverify.h"
@@ -257,6 +258,61 @@ void bind_gpu(pyb::module_& m) {
             return BatchVerifySignatures(checks, &pool, use_gpu, false, false);
         },
         pyb::arg("items"), pyb::arg("use_gpu") = true, pyb::arg("threads") = 4);
+    // GPU verification service (node/gpuverify.h): validation devices / lanes and the sharded
+    // batch paths the node uses (ConnectBlock's ECDSA batch, HEADERS Equihash batches).
+    m.def("gpu_verify_set_devices", [](const std::vector<int>& d) { GpuVerifyService::Instance().SetDevices(d); });
+    m.def("gpu_verify_devices", []() { return GpuVerifyService::Instance().Devices(); });
+    m.def("gpu_verify_set_min_shard", [](size_t ecdsa, size_t eh) {
+        GpuVerifyService::Instance().SetMinShard(ecdsa, eh);
+    });
+    m.def("gpu_verify_shutdown", []() {
+        pyb::gil_scoped_release nogil;
+        GpuVerifyService::Instance().Shutdown();
+    });
+    m.def("gpu_verify_stats", []() {
+        pyb::list lanes;
+        for (const auto& L : GpuVerifyService::Instance().Stats()) {
+            pyb::dict d;
+            d["device"] = L.device;
+            d["priority"] = L.priority;
+            d["batches"] = L.batches;
+            d["items"] = L.items;
+            lanes.append(d);
+        }
+        pyb::dict out;
+        out["lanes"] = lanes;
+        out["sharded_batches"] = GpuVerifyService::Instance().ShardedBatches();
+        return out;
+    });
+    // packed inputs (msg32 | sig64 compact low-S | pub33 compressed), as gpu::EcdsaVerifyBatch
+    m.def("gpu_verify_ecdsa_packed", [](const pyb::bytes& msg, const pyb::bytes& sig, const pyb::bytes& pub) {
+        auto mv = to_vec(msg), sv = to_vec(sig), pv = to_vec(pub);
+        const size_t n = mv.size() / 32;
+        if (mv.size() != n * 32 || sv.size() != n * 64 || pv.size() != n * 33)
+            throw std::invalid_argument("gpu_verify_ecdsa_packed: sizes");
+        std::vector<uint8_t> r;
+        {
+            pyb::gil_scoped_release nogil;
+            r = GpuVerifyService::Instance().Ecdsa(mv.data(), sv.data(), pv.data(), n);
+        }
+        return std::vector<bool>(r.begin(), r.end());
+    });
+    m.def("gpu_verify_equihash", [](unsigned n, unsigned k, const std::vector<CBlake2b>& sts,
+                                    const std::vector<pyb::bytes>& sols) {
+        auto bs = states_from(sts);
+        std::vector<std::vector<unsigned char>> v;
+        for (auto& b : sols) v.push_back(to_vec(b));
+        std::vector<const std::vector<unsigned char>*> ptrs;
+        for (auto& x : v) ptrs.push_back(&x);
+        std::vector<uint8_t> r;
+        {
+            pyb::gil_scoped_release nogil;
+            r = GpuVerifyService::Instance().Equihash(n, k, bs, ptrs);
+        }
+        return std::vector<bool>(r.begin(), r.end());
+    });
+    m.def("get_miner_gpu_devices", &GetMinerGpuDevices);
+    m.def("set_miner_gpu_devices", &SetMinerGpuDevices);
     m.def("set_gpu_fault_injection", &SetGpuFaultInjection);
     m.def("set_gpu_sig_threshold", &SetGpuSigThreshold);
     m.def("get_gpu_sig_threshold", &GetGpuSigThreshold);

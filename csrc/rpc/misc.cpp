@@ -14,6 +14,8 @@
 #include "script/sign.h"
 #include "script/standard.h"
 #include "kernels/gpu_api.h"
+#include "node/gpuverify.h"
+#include "node/miner.h"
 #include "util/lockedpool.h"
 #include "util/strencodings.h"
 
@@ -116,6 +118,26 @@ static UniValue getgpuinfo(const JSONRPCRequest& req) {
     sv.pushKV("gpu_failures", (uint64_t)s.gpu_failures);
     sv.pushKV("gpu_disabled", GpuSigPathDisabled());
     obj.pushKV("sigverify", sv);
+    // validation lanes (node/gpuverify.h): devices, stream priority, work done per lane
+    GpuVerifyService& svc = GpuVerifyService::Instance();
+    UniValue vd(UniValue::VARR);
+    for (int d : svc.Devices()) vd.push_back(d);
+    obj.pushKV("validation_devices", vd);
+    UniValue lanes(UniValue::VARR);
+    for (const auto& L : svc.Stats()) {
+        UniValue o(UniValue::VOBJ);
+        o.pushKV("device", L.device);
+        o.pushKV("stream_priority", L.priority);
+        o.pushKV("batches", L.batches);
+        o.pushKV("items", L.items);
+        lanes.push_back(o);
+    }
+    obj.pushKV("validation_lanes", lanes);
+    obj.pushKV("sharded_batches", svc.ShardedBatches());
+    UniValue md(UniValue::VARR);
+    if (avail)
+        for (int d : GetMinerGpuDevices()) md.push_back(d);
+    obj.pushKV("miner_devices", md);
     return obj;
 }
 
