@@ -146,7 +146,7 @@ struct EhCfg {
 // Mainnet/testnet (200,9); (96,5); regtest (48,5).
 using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
-using Cfg48_5 = EhCfg<48, 5, 3, 256, 64, 8, 64, 256>;
+using Cfg48_5 = EhCfg<48, 5, 3, 512, 64, 8, 64, 256>; // 512-slot areas: 8 pairs per lane (a 256-pair list overflowed on duplicate-heavy nonces)
 
 constexpr uint32_t NIL = 0xffffffffu;
 constexpr uint32_t OOB = 0x80000000u; // buffer offset past every descriptor's range: access dropped

@@ -13,7 +13,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-GEOM = {(48, 5): (8, 256), (96, 5): (128, 1280), (200, 9): (512, 5120)}  # (NB, AREA)
+GEOM = {(48, 5): (8, 512), (96, 5): (128, 1280), (200, 9): (512, 5120)}  # (NB, AREA)
 
 
 def trace_missing(dump, n, k, idx):
@@ -64,12 +64,15 @@ def main():
     ap.add_argument("--n", type=int, default=48)
     ap.add_argument("--k", type=int, default=5)
     ap.add_argument("--nonces", default="10,25")
+    ap.add_argument("--salt", default="main")
+    ap.add_argument("--scan", type=int, default=0, help="scan nonces 0..SCAN-1 and trace every miss")
     args = ap.parse_args()
     from bitcoincashplus_amd import native
     from bitcoincashplus_amd.utils import equihash_ref as R
     cbl = args.n // (args.k + 1)
-    for nonce in [int(x) for x in args.nonces.split(",")]:
-        d = bytes(b"main" + bytes(104)) + struct.pack("<I", nonce) + bytes(28)
+    nonces = range(args.scan) if args.scan else [int(x) for x in args.nonces.split(",")]
+    for nonce in nonces:
+        d = (args.salt.encode() + bytes(108))[:108] + struct.pack("<I", nonce) + bytes(28)
         st = native.EquihashState(args.n, args.k)
         st.update(d)
         cpu = native.eh_solve_cpu(args.n, args.k, st)[0]
@@ -77,6 +80,8 @@ def main():
         solver.set_debug(True)
         gpu = solver.solve([st])[0]
         cands = [tuple(c) for c in solver.stats()["debug_cands"]]
+        if args.scan and set(cpu) <= set(gpu):
+            continue
         print(f"nonce {nonce}: cpu {len(cpu)} gpu {len(gpu)} candidates {len(cands)} "
               f"pair_dropped {solver.stats()['pair_dropped']} dropped {solver.stats()['stage_dropped']}")
         sets = None
