@@ -1445,7 +1445,9 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         std::shared_ptr<CBlock> pblock = std::make_shared<CBlock>();
         vRecv >> *pblock;
         LogPrint(BCLog::NET, "received block %s peer=%d\n", pblock->GetHash().ToString().c_str(), (int)pfrom->GetId());
-        bool forceProcessing = false;
+        // whitelisted peers may push blocks unrequested outside IBD (reference
+        // src/net_processing.cpp BLOCK handler: fWhitelisted && !IsInitialBlockDownload())
+        bool forceProcessing = pfrom->fWhitelisted && !cs->IsInitialBlockDownload();
         const uint256 hash = pblock->GetHash();
         {
             std::lock_guard<CCriticalSection> l(csMain());
