@@ -60,8 +60,15 @@ def create_block(prev_hash: int, coinbase: CTransaction, ntime: int, height: int
     b.nHeight = height
     b.vtx = [coinbase] + list(txs)
     b.hashMerkleRoot = b.calc_merkle_root()
+    if b.is_new_format():  # placeholder of the solution's size, so sizes are final before solving
+        b.nSolution = bytes(solution_width(*REGTEST_EQUIHASH))
     b.calc_sha256()
     return b
+
+
+def solution_width(n: int, k: int) -> int:
+    """Bytes of a minimal Equihash solution: 2^K indices of N/(K+1)+1 bits."""
+    return (1 << k) * (n // (k + 1) + 1) // 8
 
 
 def solve(block: CBlock, equihash=REGTEST_EQUIHASH, max_tries: int = 1 << 20) -> CBlock:

@@ -390,6 +390,11 @@ class CBlock(CBlockHeader):
         count = tx_count_bytes if tx_count_bytes is not None else ser_compact_size(len(self.vtx))
         return self.serialize_header(legacy) + count + b"".join(t.serialize() for t in self.vtx)
 
+    def consensus_size(self) -> int:
+        """Size the node's CheckBlock limits: the legacy layout before the fork, the new one after
+        (reference src/validation.cpp:3267-3279)."""
+        return len(self.serialize(legacy=not self.is_new_format()))
+
     def get_merkle_root(self, hashes: List[bytes]) -> int:
         while len(hashes) > 1:
             nxt = []

@@ -134,11 +134,11 @@ def run_fullblock_suite(n, postfork: bool):
     # ---- a block of exactly LEGACY_MAX_BLOCK_SIZE (1 MB)
     tip(15); b23 = block(23, spend=out[6])
     tx = CTransaction()
-    pad = LEGACY_MAX_BLOCK_SIZE - len(b23.serialize()) - 69
+    pad = LEGACY_MAX_BLOCK_SIZE - b23.consensus_size() - 69
     tx.vout.append(CTxOut(0, CScript([b"\x00" * pad])))
     tx.vin.append(CTxIn(COutPoint(b23.vtx[1].calc_sha256(), 0)))
     b23 = update_block(23, [tx])
-    assert len(b23.serialize()) == LEGACY_MAX_BLOCK_SIZE
+    assert b23.consensus_size() == LEGACY_MAX_BLOCK_SIZE
     accepted(); save()
 
     # ---- coinbase scriptSig length: 2..100
@@ -389,14 +389,14 @@ def run_fullblock_suite(n, postfork: bool):
     # ---- a bloated (non-canonical) tx-count varint does not poison the canonical block
     tip(60); b64a = block("64a", spend=out[18])
     tx = CTransaction()
-    pad = LEGACY_MAX_BLOCK_SIZE - len(b64a.serialize()) - 69
+    pad = LEGACY_MAX_BLOCK_SIZE - b64a.consensus_size() - 69
     tx.vout.append(CTxOut(0, CScript([b"\x00" * pad])))
     tx.vin.append(CTxIn(COutPoint(b64a.vtx[1].calc_sha256(), 0)))
     b64a = update_block("64a", [tx])
     from bitcoincashplus_amd.testing.messages import msg_block
     bloated = b"\xff" + len(b64a.vtx).to_bytes(8, "little")
     raw = b64a.serialize(legacy=peer.legacy, tx_count_bytes=bloated)
-    assert len(raw) == LEGACY_MAX_BLOCK_SIZE + 8
+    assert len(raw) == len(b64a.serialize(legacy=peer.legacy)) + 8
     peer.send(msg_block(raw=raw))
     peer.sync_with_ping()
     B.blocks[64] = b64a
