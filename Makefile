@@ -28,20 +28,24 @@ GPU_HOST   := $(wildcard csrc/gpu/*.cpp)
 HIP_SRCS   := $(wildcard csrc/kernels/*.hip)
 PY_SRCS    := $(wildcard csrc/python/*.cpp)
 TOOL_SRCS  := $(wildcard csrc/tools/*.cpp)
+TEST_SRCS  := $(wildcard csrc/test/*.cpp)
 
 CORE_OBJS  := $(patsubst csrc/%.cpp,build/obj/%.o,$(CORE_SRCS) $(GPU_HOST))
 HIP_OBJS   := $(patsubst csrc/%.hip,build/obj/%.o,$(HIP_SRCS))
 PY_OBJS    := $(patsubst csrc/%.cpp,build/obj/%.o,$(PY_SRCS))
 TOOLS      := $(patsubst csrc/tools/%.cpp,bin/%,$(TOOL_SRCS))
+TEST_OBJS  := $(patsubst csrc/%.cpp,build/obj/%.o,$(TEST_SRCS))
+UNITTEST   := bin/test_bcp
 
 PYEXT      := bitcoincashplus_amd/_bcpnative$(PY_EXT)
 CORELIB    := build/libbcpcore.a
 CONSLIB    := lib/libbcpconsensus.so
 
-.PHONY: all pyext tools clean kernels conslib
+.PHONY: all pyext tools clean kernels conslib unittest
 .DEFAULT_GOAL := all
 conslib: $(CONSLIB)
-all: pyext tools conslib
+all: pyext tools conslib unittest
+unittest: $(UNITTEST)
 pyext: $(PYEXT)
 kernels: $(HIP_OBJS)
 tools: $(TOOLS)
@@ -68,6 +72,11 @@ $(PYEXT): $(PY_OBJS) $(CORELIB)
 bin/%: build/obj/tools/%.o $(CORELIB)
 	@mkdir -p bin
 	$(CXX) -rdynamic -o $@ $< -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS)
+
+# native unit suites (reference src/test/ -> test_bitcoin); run by tests/test_unit_native.py
+$(UNITTEST): $(TEST_OBJS) $(CORELIB)
+	@mkdir -p bin
+	$(CXX) -rdynamic -o $@ $(TEST_OBJS) -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS)
 
 build/obj/tools/%.o: csrc/tools/%.cpp
 	@mkdir -p $(dir $@)

@@ -105,9 +105,11 @@ ReadStatus PartiallyDownloadedBlock::FillBlock(CBlock& block, const std::vector<
     header.SetNull();
     txn_available.clear();
     if (vtx_missing.size() != tx_missing_offset) return READ_STATUS_INVALID;
-    // a wrong short-id match shows up as a merkle mismatch: treat it as a failed (not invalid) read
+    // A wrong short-id match shows up as a merkle mismatch or a duplicated transaction: corruption
+    // is possible, so the read failed rather than the block being invalid (reference
+    // blockencodings.cpp FillBlock: CheckBlock + CorruptionPossible -> READ_STATUS_FAILED).
     bool mutated = false;
-    if (BlockMerkleRoot(block, &mutated) != block.hashMerkleRoot || mutated) return READ_STATUS_CHECKBLOCK_FAILED;
+    if (BlockMerkleRoot(block, &mutated) != block.hashMerkleRoot || mutated) return READ_STATUS_FAILED;
     LogPrint(BCLog::CMPCTBLOCK, "Successfully reconstructed block %s with %zu txn prefilled, %zu txn from mempool "
                                 "(incl at least %zu from extra pool) and %zu txn requested\n",
              block.GetHash().ToString().c_str(), prefilled_count, mempool_count, extra_count, vtx_missing.size());

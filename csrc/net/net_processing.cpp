@@ -1406,8 +1406,9 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
                 MarkBlockAsReceived(resp.blockhash);
                 MisbehavingLocked(pfrom->GetId(), 100, "invalid compact block/non-matching block transactions");
                 return true;
-            } else if (status == READ_STATUS_FAILED || status == READ_STATUS_CHECKBLOCK_FAILED) {
-                // short-id collision or mismatch: fetch the full block
+            } else if (status == READ_STATUS_FAILED) {
+                // possible short-id collision (merkle mismatch): fetch the full block
+                // (reference net_processing.cpp BLOCKTXN; CHECKBLOCK_FAILED is processed below)
                 std::vector<CInv> invs{CInv(MSG_BLOCK, resp.blockhash)};
                 Push(pfrom, msgMaker.Make(NetMsgType::GETDATA, invs));
             } else {

@@ -2,7 +2,7 @@
 
 Golden values come from the reference's own unit tests (cited per test) and from
 independent Python oracles (hashlib, bitcoincashplus_amd.utils.secp256k1_ref).
-Reference JSON vectors are read as plain JSON from /root/reference when mounted.
+Reference JSON vectors are vendored as plain JSON under tests/data/vectors/.
 """
 import hashlib
 import json
@@ -13,7 +13,7 @@ import pytest
 
 from bitcoincashplus_amd.utils import secp256k1_ref as ref
 
-REF_DATA = "/root/reference/src/test/data"
+REF_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "vectors")  # vendored from reference src/test/data
 
 
 def sha256d(b):

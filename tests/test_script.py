@@ -3,14 +3,14 @@
 script_tests.json  -> reference src/test/script_tests.cpp:1073 (script_json_test)
 sighash.json       -> reference src/test/sighash_tests.cpp:172 (sighash_from_data)
 tx_valid/invalid   -> reference src/test/transaction_tests.cpp:38-215
-The JSON files are read (as data) from the mounted reference tree.
+The JSON files are the reference's, vendored as data under tests/data/vectors/.
 """
 import json
 import os
 
 import pytest
 
-REF_DATA = "/root/reference/src/test/data"
+REF_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "vectors")  # vendored from reference src/test/data
 
 
 def load(name):
