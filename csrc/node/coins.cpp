@@ -160,7 +160,8 @@ bool CCoinsViewCache::GetCoin(const COutPoint& outpoint, Coin& coin) const {
     auto it = FetchCoin(outpoint);
     if (it == cacheCoins.end()) return false;
     coin = it->second.coin;
-    return !coin.IsSpent();
+    return true; // a spent entry is reported too (callers check IsSpent), so a child cache fetching
+                 // it marks its copy FRESH (reference coins.cpp GetCoin/FetchCoin)
 }
 
 void CCoinsViewCache::AddCoin(const COutPoint& outpoint, Coin&& coin, bool possible_overwrite) {

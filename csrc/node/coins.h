@@ -33,11 +33,11 @@ template <typename S> void SerializeCompressedScript(S& s, const CScript& script
     s.write((const char*)script.data(), script.size());
 }
 template <typename S> void UnserializeCompressedScript(S& s, CScript& script) {
-    unsigned nSize = (unsigned)ReadVarInt(s);
+    uint64_t nSize = ReadVarInt(s);
     if (nSize < nSpecialScripts) {
-        std::vector<unsigned char> v(GetSpecialScriptSize(nSize));
+        std::vector<unsigned char> v(GetSpecialScriptSize((unsigned)nSize));
         s.read((char*)v.data(), v.size());
-        DecompressScript(script, nSize, v);
+        DecompressScript(script, (unsigned)nSize, v);
         return;
     }
     nSize -= nSpecialScripts;
@@ -45,8 +45,12 @@ template <typename S> void UnserializeCompressedScript(S& s, CScript& script) {
         // overly long script: replace with a short unspendable one, skip the payload
         script.clear();
         script << OP_RETURN;
-        std::vector<char> skip(nSize);
-        s.read(skip.data(), nSize);
+        char skip[4096]; // in chunks: a bogus multi-GB size hits the end of the stream, not the allocator
+        for (uint64_t left = nSize; left > 0;) {
+            const size_t k = (size_t)std::min<uint64_t>(left, sizeof(skip));
+            s.read(skip, k);
+            left -= k;
+        }
     } else {
         script.resize(nSize);
         s.read((char*)script.data(), nSize);
@@ -71,6 +75,7 @@ public:
     Coin(CTxOut o, int h, bool cb) : out(std::move(o)), fCoinBase(cb), nHeight((uint32_t)h) {}
     void Clear() {
         out.SetNull();
+        CScript().swap(out.scriptPubKey); // release the script's buffer: a spent entry costs no usage
         fCoinBase = false;
         nHeight = 0;
     }

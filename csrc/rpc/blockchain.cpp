@@ -333,7 +333,7 @@ static UniValue gettxout(const JSONRPCRequest& req) {
         CCoinsViewMemPool view(&cs.CoinsTip(), *n.mempool);
         if (!view.GetCoin(out, coin) || n.mempool->isSpent(out)) return UniValue::NullUniValue;
     } else {
-        if (!cs.CoinsTip().GetCoin(out, coin)) return UniValue::NullUniValue;
+        if (!cs.CoinsTip().GetCoin(out, coin) || coin.IsSpent()) return UniValue::NullUniValue;
     }
     UniValue ret(UniValue::VOBJ);
     ret.pushKV("bestblock", cs.Tip()->GetBlockHash().GetHex());

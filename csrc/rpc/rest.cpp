@@ -151,7 +151,8 @@ static bool rest_getutxos(const HTTPRequest& req, HTTPReply& rep, const std::str
         CCoinsView& view = fCheckMemPool ? static_cast<CCoinsView&>(viewMempool) : static_cast<CCoinsView&>(cs.CoinsTip());
         for (size_t i = 0; i < vOutPoints.size(); i++) {
             Coin coin;
-            const bool hit = view.GetCoin(vOutPoints[i], coin) && !(fCheckMemPool && n->mempool->isSpent(vOutPoints[i]));
+            const bool hit = view.GetCoin(vOutPoints[i], coin) && !coin.IsSpent() &&
+                             !(fCheckMemPool && n->mempool->isSpent(vOutPoints[i]));
             if (hit) {
                 outs.push_back(coin);
                 bitmap[i / 8] |= 1 << (i % 8);

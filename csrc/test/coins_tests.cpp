@@ -1,0 +1,420 @@
+// UTXO cache suites.
+// Parity: reference src/test/coins_tests.cpp:
+//   * coins_cache_simulation: random adds / spends / accesses / flushes / uncaches through a stack
+//     of CCoinsViewCache layers over an in-memory backing view, checked against a plain map model
+//     after every operation (every layer agrees with the model);
+//   * updatecoins_simulation: random transactions (incl. coinbases) applied with AddCoins /
+//     SpendCoin + undo, then undone, restoring the exact previous UTXO set;
+//   * coin_serialization: the reference's compressed-coin byte vectors, and truncated /
+//     oversized scripts throwing at the end of the stream (no huge allocation);
+//   * coin_access / coin_spend / coin_add / coin_write: the DIRTY / FRESH flag transitions of a
+//     cache entry for every (parent value, child value, flags) combination. The expected state
+//     comes from the rules the reference tables encode (written out in Expect* below), so every
+//     combination is covered rather than a copied table.
+#include "test/unittest.h"
+
+#include "node/coins.h"
+#include "primitives/serialize.h"
+#include "script/standard.h"
+#include "util/strencodings.h"
+
+#include <map>
+#include <random>
+
+using namespace bcp;
+using namespace bcp::test;
+
+namespace {
+
+// Backing view with a plain map (reference CCoinsViewTest): stores unspent coins only.
+class MapView : public CCoinsView {
+public:
+    std::map<COutPoint, Coin> coins;
+    uint256 best;
+    bool GetCoin(const COutPoint& o, Coin& c) const override {
+        auto it = coins.find(o);
+        if (it == coins.end()) return false;
+        c = it->second;
+        return !c.IsSpent();
+    }
+    uint256 GetBestBlock() const override { return best; }
+    bool BatchWrite(CCoinsMap& m, const uint256& h) override {
+        for (auto it = m.begin(); it != m.end(); it = m.erase(it)) {
+            if (!(it->second.flags & CCoinsCacheEntry::DIRTY)) continue;
+            if (it->second.coin.IsSpent()) coins.erase(it->first);
+            else coins[it->first] = it->second.coin;
+        }
+        if (!h.IsNull()) best = h;
+        return true;
+    }
+};
+
+// Exposes a cache's entry map (reference CCoinsViewCacheTest).
+class TestCache : public CCoinsViewCache {
+public:
+    explicit TestCache(CCoinsView* base) : CCoinsViewCache(base) {}
+    CCoinsMap& Map() const { return cacheCoins; }
+    size_t& Usage() const { return cachedCoinsUsage; }
+};
+
+COutPoint RandOutpoint(std::mt19937_64& r, int universe) {
+    uint256 h;
+    const uint64_t k = r() % universe;
+    memcpy(h.begin(), &k, 8);
+    return COutPoint(h, (uint32_t)(k % 3));
+}
+Coin RandCoin(std::mt19937_64& r) {
+    CScript s;
+    const int len = (int)(r() % 40) + 1;
+    for (int i = 0; i < len; i++) s.push_back((unsigned char)(r() & 0x7f)); // no OP_RETURN (0x6a) first byte:
+    if (s[0] == OP_RETURN) s[0] = OP_TRUE;                                    // unspendable coins are not added
+    return Coin(CTxOut((Amount)(r() % 100000000) + 1, s), (int)(r() % 1000), (r() & 1) != 0);
+}
+bool SameCoin(const Coin& a, const Coin& b) {
+    return a.IsSpent() == b.IsSpent() &&
+           (a.IsSpent() || (a.out == b.out && a.nHeight == b.nHeight && a.fCoinBase == b.fCoinBase));
+}
+
+} // namespace
+
+TEST_CASE(coins_tests, cache_simulation) {
+    BasicTestingSetup setup;
+    std::mt19937_64 r(2017);
+    MapView base;
+    std::map<COutPoint, Coin> model;
+    std::vector<std::unique_ptr<TestCache>> stack;
+    stack.emplace_back(new TestCache(&base));
+    const int UNIVERSE = 400;
+    size_t adds = 0, spends = 0, flushes = 0, pushes = 0, pops = 0;
+    for (int op = 0; op < 40000; op++) {
+        TestCache& top = *stack.back();
+        const COutPoint o = RandOutpoint(r, UNIVERSE);
+        const unsigned pick = (unsigned)(r() % 100);
+        if (pick < 40) { // add (possible_overwrite when a coin exists there, like coinbases)
+            Coin c = RandCoin(r);
+            const bool exists = model.count(o) && !model[o].IsSpent();
+            top.AddCoin(o, Coin(c), exists ? true : (r() & 1) != 0 ? false : true);
+            model[o] = c;
+            adds++;
+        } else if (pick < 70) { // spend
+            Coin undo;
+            const bool had = model.count(o) && !model[o].IsSpent();
+            const bool ok = top.SpendCoin(o, &undo);
+            CHECK(ok == had || !had); // spending an absent coin may report false
+            if (had) CHECK(SameCoin(undo, model[o]));
+            model.erase(o);
+            spends++;
+        } else if (pick < 85) { // access
+            const Coin& c = top.AccessCoin(o);
+            auto it = model.find(o);
+            CHECK(SameCoin(c, it == model.end() ? Coin() : it->second));
+            CHECK(top.HaveCoin(o) == (it != model.end() && !it->second.IsSpent()));
+        } else if (pick < 88) { // uncache from the top layer (only clean entries go)
+            top.Uncache(o);
+        } else if (pick < 93 && stack.size() > 1) { // flush the top into its parent
+            CHECK(top.Flush());
+            flushes++;
+        } else if (pick < 96 && stack.size() < 5) {
+            stack.emplace_back(new TestCache(stack.back().get()));
+            pushes++;
+        } else if (pick < 100 && stack.size() > 1) {
+            CHECK(stack.back()->Flush());
+            stack.pop_back();
+            pops++;
+        }
+        if (op % 2000 == 0) { // the top layer's view of a sample agrees with the model (lower layers
+            for (int k = 0; k < 64; k++) { // lag until flushed); every layer's usage is consistent
+                const COutPoint q = RandOutpoint(r, UNIVERSE);
+                auto it = model.find(q);
+                CHECK(SameCoin(stack.back()->AccessCoin(q), it == model.end() ? Coin() : it->second));
+            }
+            for (auto& layer : stack) {
+                size_t use = 0;
+                for (auto& kv : layer->Map()) use += kv.second.coin.DynamicMemoryUsage();
+                CHECK_EQ(layer->Usage(), use);
+            }
+        }
+    }
+    while (!stack.empty()) {
+        CHECK(stack.back()->Flush());
+        stack.pop_back();
+    }
+    // the backing store now holds exactly the model's unspent coins
+    size_t live = 0;
+    for (const auto& kv : model)
+        if (!kv.second.IsSpent()) {
+            live++;
+            auto it = base.coins.find(kv.first);
+            CHECK(it != base.coins.end() && SameCoin(it->second, kv.second));
+        }
+    CHECK_EQ(base.coins.size(), live);
+    CHECK(adds > 10000 && spends > 8000 && flushes > 100 && pushes > 50 && pops > 50);
+}
+
+TEST_CASE(coins_tests, updatecoins_simulation) {
+    BasicTestingSetup setup;
+    std::mt19937_64 r(7);
+    MapView base;
+    CCoinsViewCache cache(&base);
+    struct Applied {
+        CTransaction tx;
+        std::vector<Coin> undo;
+        int height;
+    };
+    std::vector<Applied> history;
+    std::vector<COutPoint> utxos;
+    for (int height = 1; height <= 600; height++) {
+        CMutableTransaction mtx;
+        mtx.nVersion = 1;
+        const bool coinbase = utxos.size() < 4 || r() % 4 == 0;
+        if (coinbase) {
+            mtx.vin.resize(1);
+            mtx.vin[0].prevout.SetNull();
+            mtx.vin[0].scriptSig = CScript() << height << OP_0;
+        } else {
+            const int nin = 1 + (int)(r() % std::min<size_t>(3, utxos.size()));
+            for (int i = 0; i < nin; i++) {
+                const size_t k = r() % utxos.size();
+                mtx.vin.emplace_back(utxos[k]);
+                utxos.erase(utxos.begin() + k);
+            }
+        }
+        const int nout = 1 + (int)(r() % 3);
+        for (int i = 0; i < nout; i++) mtx.vout.emplace_back((Amount)(1000 + r() % 1000), CScript() << OP_TRUE << (int)i);
+        const CTransaction tx(mtx);
+        Applied a{tx, {}, height};
+        if (!coinbase)
+            for (const CTxIn& in : tx.vin) {
+                a.undo.emplace_back();
+                CHECK(cache.SpendCoin(in.prevout, &a.undo.back()));
+            }
+        AddCoins(cache, tx, height);
+        for (size_t i = 0; i < tx.vout.size(); i++) utxos.emplace_back(tx.GetHash(), (uint32_t)i);
+        history.push_back(std::move(a));
+        if (height % 97 == 0) CHECK(cache.Flush());
+    }
+    std::set<COutPoint> before(utxos.begin(), utxos.end());
+    for (const COutPoint& o : before) CHECK(cache.HaveCoin(o));
+    // undo the last 200 transactions in reverse: their outputs vanish, their inputs come back
+    std::set<COutPoint> restored = before;
+    for (int k = 0; k < 200; k++) {
+        Applied a = std::move(history.back());
+        history.pop_back();
+        for (size_t i = 0; i < a.tx.vout.size(); i++) {
+            const COutPoint o(a.tx.GetHash(), (uint32_t)i);
+            if (restored.count(o)) {
+                CHECK(cache.SpendCoin(o));
+                restored.erase(o);
+            }
+        }
+        for (size_t i = 0; i < a.undo.size(); i++) {
+            const COutPoint& o = a.tx.vin[i].prevout;
+            CHECK(!cache.HaveCoin(o));
+            cache.AddCoin(o, Coin(a.undo[i]), false);
+            restored.insert(o);
+            CHECK(cache.AccessCoin(o).nHeight == a.undo[i].nHeight);
+        }
+    }
+    CHECK(cache.Flush());
+    for (const COutPoint& o : restored) CHECK(base.coins.count(o) == 1);
+    CHECK_EQ(base.coins.size(), restored.size());
+}
+
+TEST_CASE(coins_tests, coin_serialization) {
+    BasicTestingSetup setup;
+    auto decode = [](const std::string& hex) {
+        std::vector<unsigned char> v = ParseHex(hex);
+        SpanReader s(v.data(), v.size(), SER_DISK, PROTOCOL_VERSION);
+        Coin c;
+        s >> c;
+        return c;
+    };
+    Coin c1 = decode("97f23c835800816115944e077fe7c803cfa57f29b36bf87c1d35");
+    CHECK(!c1.IsCoinBase());
+    CHECK_EQ(c1.GetHeight(), 203998u);
+    CHECK_EQ(c1.GetTxOut().nValue, (Amount)60000000000LL);
+    CHECK(c1.GetTxOut().scriptPubKey ==
+          GetScriptForDestination(CKeyID(uint160(ParseHex("816115944e077fe7c803cfa57f29b36bf87c1d35")))));
+    Coin c2 = decode("8ddf77bbd123008c988f1a4a4de2161e0f50aac7f17e7f9555caa4");
+    CHECK(c2.IsCoinBase());
+    CHECK_EQ(c2.GetHeight(), 120891u);
+    CHECK_EQ(c2.GetTxOut().nValue, (Amount)110397);
+    CHECK(c2.GetTxOut().scriptPubKey ==
+          GetScriptForDestination(CKeyID(uint160(ParseHex("8c988f1a4a4de2161e0f50aac7f17e7f9555caa4")))));
+    Coin c3 = decode("000006"); // smallest coin: height 0, value 0, empty script
+    CHECK(!c3.IsCoinBase() && c3.GetHeight() == 0 && c3.GetTxOut().nValue == 0 &&
+          c3.GetTxOut().scriptPubKey.empty());
+    CHECK_THROWS(decode("000007")); // script ends past the stream
+    std::vector<unsigned char> v;
+    VectorWriter w(v);
+    WriteVarInt(w, 3000000000ULL);
+    CHECK_EQ(HexStr(v.begin(), v.end()), std::string("8a95c0bb00"));
+    CHECK_THROWS(decode("00008a95c0bb00")); // 3e9-byte script past the end: throws, no allocation
+    // round trips
+    std::mt19937_64 r(5);
+    for (int i = 0; i < 200; i++) {
+        Coin c = RandCoin(r);
+        std::vector<unsigned char> buf;
+        VectorWriter ww(buf, SER_DISK);
+        ww << c;
+        SpanReader rr(buf.data(), buf.size(), SER_DISK, PROTOCOL_VERSION);
+        Coin d;
+        rr >> d;
+        CHECK(SameCoin(c, d));
+    }
+}
+
+// ------------------------------------------------------------------ flag transitions
+namespace {
+const Amount SPENT = -1, ABSENT = -2, FAIL = -3, V1 = 100, V2 = 200, V3 = 300;
+const int NO_ENTRY = -1;
+const int DIRTY = CCoinsCacheEntry::DIRTY, FRESH = CCoinsCacheEntry::FRESH;
+const int ALL_FLAGS[] = {0, FRESH, DIRTY, DIRTY | FRESH};
+const COutPoint OP(uint256S("0101010101010101010101010101010101010101010101010101010101010101"), 3);
+
+Coin CoinOf(Amount v) {
+    Coin c;
+    if (v >= 0) c = Coin(CTxOut(v, CScript() << OP_TRUE), 1, false);
+    return c; // SPENT: an entry holding a spent (null) coin
+}
+void Put(CCoinsMap& m, Amount v, int flags) {
+    if (v == ABSENT) return;
+    CCoinsCacheEntry& e = m[OP];
+    e.coin = CoinOf(v);
+    e.flags = (unsigned char)flags;
+}
+std::pair<Amount, int> Get(const CCoinsMap& m) {
+    auto it = m.find(OP);
+    if (it == m.end()) return {ABSENT, NO_ENTRY};
+    return {it->second.coin.IsSpent() ? SPENT : it->second.coin.out.nValue, it->second.flags};
+}
+// parent cache over an empty root, child cache over the parent
+struct Layers {
+    MapView root;
+    TestCache parent{&root};
+    TestCache child{&parent};
+    Layers(Amount pv, int pf, Amount cv, int cf) {
+        Put(parent.Map(), pv, pf);
+        Put(child.Map(), cv, cf);
+        for (auto* c : {&parent, &child})
+            for (auto& kv : c->Map()) c->Usage() += kv.second.coin.DynamicMemoryUsage();
+    }
+};
+
+// Reading through a cache: an entry is used as is; otherwise the parent's coin is copied in, a
+// spent one marked FRESH (the child's copy need never be written back).
+std::pair<Amount, int> ExpectAccess(Amount parent, Amount child, int cflags) {
+    if (child != ABSENT) return {child, cflags};
+    if (parent == ABSENT) return {ABSENT, NO_ENTRY};
+    return {parent, parent == SPENT ? FRESH : 0};
+}
+// Spending: fetch as above; a FRESH entry is dropped, any other becomes spent and DIRTY.
+std::pair<Amount, int> ExpectSpend(Amount parent, Amount child, int cflags) {
+    auto e = ExpectAccess(parent, child, cflags);
+    if (e.first == ABSENT) return e;
+    if (e.second & FRESH) return {ABSENT, NO_ENTRY};
+    return {SPENT, e.second | DIRTY};
+}
+// Adding: over an unspent entry only with possible_overwrite (else it throws); the entry becomes
+// DIRTY, and FRESH when it could not have been written to the parent yet (not overwriting, and
+// the old entry was not DIRTY); existing FRESH is kept.
+std::pair<Amount, int> ExpectAdd(Amount child, int cflags, bool overwrite) {
+    if (child >= 0 && !overwrite) return {FAIL, NO_ENTRY};
+    const int old = child == ABSENT ? 0 : cflags;
+    const bool fresh = !overwrite && !(old & DIRTY);
+    return {V3, old | DIRTY | (fresh ? FRESH : 0)};
+}
+// Writing a child entry into the parent (BatchWrite): clean child entries are ignored; a new
+// entry is created DIRTY (+FRESH if the child's was) unless it is FRESH and spent; a FRESH child
+// over an unspent parent coin is a logic error; a spent child over a FRESH parent erases the
+// parent's entry; otherwise the parent takes the coin and becomes DIRTY.
+std::pair<Amount, int> ExpectWrite(Amount parent, int pflags, Amount child, int cflags) {
+    if (child == ABSENT || !(cflags & DIRTY)) return {parent, parent == ABSENT ? NO_ENTRY : pflags};
+    if (parent == ABSENT) {
+        if ((cflags & FRESH) && child == SPENT) return {ABSENT, NO_ENTRY};
+        return {child, DIRTY | (cflags & FRESH)};
+    }
+    if ((cflags & FRESH) && parent >= 0) return {FAIL, NO_ENTRY};
+    if ((pflags & FRESH) && child == SPENT) return {ABSENT, NO_ENTRY};
+    return {child, pflags | DIRTY};
+}
+} // namespace
+
+TEST_CASE(coins_tests, coin_access) {
+    BasicTestingSetup setup;
+    int n = 0;
+    for (Amount pv : {ABSENT, SPENT, V1})
+        for (Amount cv : {ABSENT, SPENT, V2})
+            for (int cf : ALL_FLAGS) {
+                if (cv == ABSENT && cf) continue;
+                // a spent parent entry in a non-FRESH/non-DIRTY state is only reachable for the
+                // table's purposes; every parent flag combination behaves the same for reads
+                Layers L(pv, pv == ABSENT ? 0 : DIRTY, cv, cf);
+                L.child.AccessCoin(OP);
+                const auto want = ExpectAccess(pv, cv, cv == ABSENT ? NO_ENTRY : cf);
+                CHECK(Get(L.child.Map()) == want);
+                n++;
+            }
+    CHECK_EQ(n, 27); // 3 parent states x (no entry + 2 values x 4 flag sets)
+}
+
+TEST_CASE(coins_tests, coin_spend) {
+    BasicTestingSetup setup;
+    for (Amount pv : {ABSENT, SPENT, V1})
+        for (Amount cv : {ABSENT, SPENT, V2})
+            for (int cf : ALL_FLAGS) {
+                if (cv == ABSENT && cf) continue;
+                Layers L(pv, pv == ABSENT ? 0 : DIRTY, cv, cf);
+                L.child.SpendCoin(OP);
+                CHECK(Get(L.child.Map()) == ExpectSpend(pv, cv, cv == ABSENT ? NO_ENTRY : cf));
+                // usage bookkeeping stays consistent
+                size_t use = 0;
+                for (auto& kv : L.child.Map()) use += kv.second.coin.DynamicMemoryUsage();
+                CHECK_EQ(L.child.Usage(), use);
+            }
+}
+
+TEST_CASE(coins_tests, coin_add) {
+    BasicTestingSetup setup;
+    for (Amount cv : {ABSENT, SPENT, V2})
+        for (int cf : ALL_FLAGS)
+            for (bool overwrite : {false, true}) {
+                if (cv == ABSENT && cf) continue;
+                Layers L(ABSENT, 0, cv, cf);
+                std::pair<Amount, int> got;
+                try {
+                    L.child.AddCoin(OP, CoinOf(V3), overwrite);
+                    got = Get(L.child.Map());
+                } catch (const std::logic_error&) {
+                    got = {FAIL, NO_ENTRY};
+                }
+                CHECK(got == ExpectAdd(cv, cf, overwrite));
+            }
+}
+
+TEST_CASE(coins_tests, coin_write) {
+    BasicTestingSetup setup;
+    int n = 0;
+    for (Amount pv : {ABSENT, SPENT, V1})
+        for (int pf : ALL_FLAGS)
+            for (Amount cv : {ABSENT, SPENT, V2})
+                for (int cf : ALL_FLAGS) {
+                    if ((pv == ABSENT && pf) || (cv == ABSENT && cf)) continue;
+                    Layers L(pv, pf, cv, cf);
+                    std::pair<Amount, int> got;
+                    try {
+                        L.child.Flush();
+                        got = Get(L.parent.Map());
+                    } catch (const std::logic_error&) {
+                        got = {FAIL, NO_ENTRY};
+                    }
+                    const auto want = ExpectWrite(pv, pf, cv, cf);
+                    CHECK(got == want);
+                    if (!(got == want))
+                        std::fprintf(stderr, "    write parent=%lld/%d child=%lld/%d -> %lld/%d (want %lld/%d)\n",
+                                     (long long)pv, pf, (long long)cv, cf, (long long)got.first, got.second,
+                                     (long long)want.first, want.second);
+                    n++;
+                }
+    CHECK_EQ(n, 81); // 9 parent x 9 child entry states
+}
