@@ -103,14 +103,12 @@ BIP9Stats AbstractThresholdConditionChecker::GetStateStatisticsFor(const CBlockI
     stats.period = Period(params);
     stats.threshold = Threshold(params);
     if (pindex == nullptr) return stats;
-    const CBlockIndex* pindexEndOfPrevPeriod = pindex->GetAncestor(pindex->nHeight - ((pindex->nHeight + 1) % stats.period));
-    stats.elapsed = pindex->nHeight - pindexEndOfPrevPeriod->nHeight;
+    // first block of pindex's period; in the very first period there is no previous-period end block
+    const int periodStart = pindex->nHeight - ((pindex->nHeight + 1) % stats.period) + 1;
+    stats.elapsed = pindex->nHeight - periodStart + 1;
     int count = 0;
-    const CBlockIndex* currentIndex = pindex;
-    while (pindexEndOfPrevPeriod->nHeight != currentIndex->nHeight) {
-        if (Condition(currentIndex, params)) count++;
-        currentIndex = currentIndex->pprev;
-    }
+    for (const CBlockIndex* cur = pindex; cur != nullptr && cur->nHeight >= periodStart; cur = cur->pprev)
+        if (Condition(cur, params)) count++;
     stats.count = count;
     stats.possible = (stats.period - stats.threshold) >= (stats.elapsed - count);
     return stats;

@@ -89,9 +89,6 @@
 #ifndef BCP_EH_GEN_WPE // minimum waves per SIMD the generation kernel's registers must allow
 #define BCP_EH_GEN_WPE 1
 #endif
-#ifndef BCP_EH_CHAIN // 1 (merged layout): collisions found through per-key chains built at commit time
-#define BCP_EH_CHAIN 1 //    (LDS atomic exchange) instead of a counting sort + two block scans
-#endif
 
 namespace bcpk {
 
@@ -543,21 +540,14 @@ __device__ __forceinline__ bool sig_hit(uint32_t si, uint32_t sj) {
 // offp[CAP] u16} during the collision search, the slot -> pair table spair[AREA] u32 after it.
 template <class C> constexpr int un_walk_bend(int cap) { return (cap * 2 + 3) / 4 * 4; }
 template <class C> constexpr int un_walk_offp(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
-// Chain layout (BCP_EH_CHAIN): head[NRESTS] u32 then nxt[cap] u16 during the collision search.
-// Each wave appends its kept pairs to a private region of WCAP entries (no shared counter): 25%
-// above an even share of the MP*NT pair budget, in whole 64-lane rows.
-template <class C> constexpr int chain_wcap() {
-    return ((C::AREA + C::NT - 1) / C::NT * C::NT / C::NW * 5 / 4 + 63) / 64 * 64;
-}
 template <class C> constexpr int round_un(int cap) {
-    const int walk = BCP_EH_CHAIN ? C::NRESTS * 4 + cap * 2 : un_walk_offp<C>(cap) + cap * 2;
+    const int walk = un_walk_offp<C>(cap) + cap * 2;
     return walk > C::AREA * 4 ? walk : C::AREA * 4;
 }
 template <class C> constexpr int round_lds(int stage, bool prune) {
     const int WI = C::words(stage - 1);
     const int cap = C::cap(stage);
-    // pair marks (u16) of the scan enumeration, or the chain walk's pair list (u32)
-    const int marks = stage == C::K ? 0 : BCP_EH_CHAIN ? chain_wcap<C>() * C::NW * 4 : (C::AREA + C::NT - 1) / C::NT * C::NT * 2;
+    const int marks = stage == C::K ? 0 : (C::AREA + C::NT - 1) / C::NT * C::NT * 2;
     return (cap * WI + 3) / 4 * 16 + (prune ? cap * 6 : 0) + marks + round_un<C>(cap) + 3 * C::NB * 4 + 512;
 }
 // Depth-1 duplicate pruning wherever its signatures fit next to the full rows.
@@ -610,13 +600,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
     __shared__ uint32_t psig[PRUNE ? CAP : 1];                // merged: the parent's (j << 16) | i
     __shared__ uint16_t pdw[PRUNE ? CAP : 1];                 // producing bucket of each row
-    constexpr bool CHAIN = BCP_EH_CHAIN;
-    static_assert(!CHAIN || MG, "chain collisions need the merged slot layout");
-    __shared__ uint16_t pmark[FINAL || CHAIN ? 1 : MP * NT];  // pair index -> first sorted position
-    constexpr int WCAP = chain_wcap<C>();                      // chain walk: pairs per wave region
-    constexpr int MPW = WCAP / 64;                             //   (per lane)
-    __shared__ uint32_t plist[FINAL || !CHAIN ? 1 : WCAP * C::NW]; // chain walk: kept pairs (j << 16) | i
-    __shared__ uint32_t wcnt[C::NW];
+    __shared__ uint16_t pmark[FINAL ? 1 : MP * NT];           // pair index -> first sorted position
     __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(CAP)];
     __shared__ uint32_t hist[C::NB], cur[C::NB], base[C::NB];
     __shared__ uint32_t wsum[C::NW + 1];
@@ -624,13 +608,6 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     uint32_t* bend = reinterpret_cast<uint32_t*>(un + un_walk_bend<C>(CAP));
     uint16_t* offp = reinterpret_cast<uint16_t*>(un + un_walk_offp<C>(CAP));
     uint32_t* spair = reinterpret_cast<uint32_t*>(un);
-    // Chain search: head[key] = (tag | last row inserted with that key), nxt[row] = the row inserted
-    // before it (NILS: none). Tags carry bit 31 and the bucket iteration, so entries of earlier
-    // buckets - and the spair table that overlays head during claim/emit, whose words keep bit 31
-    // clear (j < 8192) - never read as current: head needs no per-bucket reset.
-    uint32_t* head = reinterpret_cast<uint32_t*>(un);
-    uint16_t* nxt = reinterpret_cast<uint16_t*>(un + C::NRESTS * 4);
-    constexpr uint32_t NILS = 0xffffu;
     const int tid = threadIdx.x;
     const int G = gridDim.x;
     int it = 0;
@@ -711,26 +688,17 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     }
     const int bk1 = xcd_bucket<C::NB>(blockIdx.x, 1, G, nbk);
     uint32_t fill_next = bk1 >= 0 ? CTRin[bk1] : 0u;
-    if constexpr (CHAIN) { // stale-tag initial heads (bit 31 clear)
-        for (int k = tid; k < C::NRESTS; k += NT) head[k] = 0;
-        __syncthreads();
-    }
 
     for (;;) {
         const int nonce = bk / C::NB, d = bk % C::NB;
         EH_STAMP(0);
         // A. commit the prefetched bucket (lane-flat 16-byte LDS stores: conflict-free)
-        const uint32_t tag = 0x80000000u | (((uint32_t)it & 0x7fffu) << 16);
         if constexpr (MG) {
             const uint32_t ot = opaque_tid();
 #pragma unroll
             for (int u = 0; u < RPL; ++u) {
                 const uint32_t r = ot + u * NT;
                 if (r < n) {
-                    if constexpr (CHAIN) { // link the row into its key's chain
-                        const uint32_t old = atomicExch(&head[nr[u][0] >> (32 - C::RB)], tag | r);
-                        nxt[r] = (uint16_t)((old & 0xffff0000u) == tag ? (old & 0xffffu) : NILS);
-                    }
                     uint32_t lbits = 0;
                     if constexpr (C::cp(STAGE - 1)) { // d's top bits out of the row's padding
                         lbits = nr[u][WI - 1];
@@ -775,9 +743,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             }
         }
         for (int b = tid; b < C::NB; b += NT) hist[b] = 0;
-        if constexpr (!CHAIN) {
-            for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
-        }
+        for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
         EH_STAMP(1);
         const int bn = xcd_bucket<C::NB>(blockIdx.x, it + 1, G, nbk);
         const bool more = bn >= 0; // uniform
@@ -792,36 +758,16 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
 
         // D1. counting sort of the rows by their RB key: sidx = row ids grouped by key,
         //     bend[key] = end of the key's group
-        //     (chain mode: the chains built at commit replace the sort)
         auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WI] >> (32 - C::RB); };
-        if constexpr (!CHAIN) {
-            for (uint32_t i = tid; i < n; i += NT) atomicAdd(&bend[key_of(i)], 1u);
-            __syncthreads();
-            block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
-            for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
-            issue(SLI, 2 * SLI);
-            __syncthreads();
-        }
+        for (uint32_t i = tid; i < n; i += NT) atomicAdd(&bend[key_of(i)], 1u);
+        __syncthreads();
+        block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
+        for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
+        issue(SLI, 2 * SLI);
+        __syncthreads();
         EH_STAMP(3);
 
-        if constexpr (FINAL && CHAIN) {
-            // D2 (final round, chains): every row walks the rows inserted before it under its key;
-            // candidates are pairs equal on ALL remaining bits (no pair list, no cap).
-            static_assert(WI == 1, "final-round rows are one word");
-            for (uint32_t i = tid; i < n; i += NT) {
-                const uint32_t ri = rows[i];
-                for (uint32_t j = nxt[i]; j != NILS; j = nxt[j]) {
-                    if (rows[j] != ri) continue;
-                    if constexpr (PRUNE) {
-                        if (sig_hit(psig[i], psig[j]) && pdw[i] == pdw[j]) continue;
-                    }
-                    const uint32_t c = atomicAdd(&ncand[nonce], 1u);
-                    if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
-                }
-            }
-            issue(SLI, 2 * SLI);
-            issue(2 * SLI, NI);
-        } else if constexpr (FINAL) {
+        if constexpr (FINAL) {
             // D2 (final round). Candidates are pairs equal on ALL remaining bits: each sorted
             // position scans the rest of its key group (a few rows). No pair list, so a bucket's
             // pair count is not capped (a capped list here silently lost solutions).
@@ -847,85 +793,13 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             //     in registers (MP per lane: up to MP*NT per bucket, above the row capacity:
             //     capped pair lists lost ~9% of the solutions); identical subtrees and pairs that
             //     share a parent are dropped.
-            // Chain mode: each row walks the rows inserted before it under its key (a key group
-            // of g rows yields its g(g-1)/2 pairs, no cap per group); kept pairs are appended to
-            // an LDS list with one atomic per wave and step (ballot + mbcnt compaction), no scans.
             // c_p is capped at 14 so every prefix fits the u16 offsets (a key group of 16+ rows is
             // ~1e-8 likely; it only loses a few pairs)
-            uint32_t Pc = 0;
-            // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the pairs, so the
-            // remaining words are read only when it matches
-            auto keep_pair = [&](uint32_t i, uint32_t j, uint32_t x0) -> bool {
-                bool keep = x0 != 0;
-                if (!keep) {
-#pragma unroll
-                    for (int w = 1; w < WI; ++w) keep |= rows[i * WI + w] != rows[j * WI + w];
-                }
-                if constexpr (PRUNE) {
-                    // signature hit (a shared parent, or ~1e-4 by chance): parents are
-                    // shared only if both rows were made by the same bucket
-                    if (keep && sig_hit(psig[i], psig[j]) && pdw[i] == pdw[j]) keep = false;
-                }
-                return keep;
-            };
-            uint32_t wpre = 0, wmine = 0; // chain mode: pairs of the waves before this one / of this wave
-            if constexpr (CHAIN) {
-                // all MPR rows of the lane walk their chains together (independent LDS load chains
-                // overlap); every step compacts the kept pairs of the wave into its own region
-                const uint32_t lane = tid & 63;
-                const uint32_t wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-                uint32_t* wl = plist + wid * WCAP;
-                uint32_t wb = 0; // wave-uniform fill of the region
-                uint32_t ii[MPR], jj[MPR], r0[MPR];
-#pragma unroll
-                for (int q = 0; q < MPR; ++q) {
-                    ii[q] = tid + q * NT;
-                    const bool in = ii[q] < n;
-                    jj[q] = in ? nxt[ii[q]] : NILS;
-                    r0[q] = in ? rows[ii[q] * WI] : 0u;
-                }
-                for (;;) {
-                    bool any = false;
-#pragma unroll
-                    for (int q = 0; q < MPR; ++q) any |= jj[q] != NILS;
-                    if (!__ballot(any)) break;
-#pragma unroll
-                    for (int q = 0; q < MPR; ++q) {
-                        const uint32_t j = jj[q];
-                        bool keep = false;
-                        if (j != NILS) keep = keep_pair(ii[q], j, r0[q] ^ rows[j * WI]);
-                        const uint64_t m = __ballot(keep);
-                        if (m) { // wave-uniform
-                            const uint32_t off = __builtin_amdgcn_mbcnt_hi(
-                                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                            if (keep && wb + off < (uint32_t)WCAP) wl[wb + off] = (j << 16) | ii[q];
-                            wb += (uint32_t)__popcll(m);
-                        }
-                        if (j != NILS) jj[q] = nxt[j];
-                    }
-                }
-                if (lane == 0) wcnt[wid] = wb;
-                issue(SLI, 2 * SLI);
-                __syncthreads();
-                uint32_t P = 0, over = 0;
-#pragma unroll
-                for (int w = 0; w < C::NW; ++w) {
-                    const uint32_t c = wcnt[w];
-                    over += c > (uint32_t)WCAP ? c - WCAP : 0u;
-                    const uint32_t cc = min(c, (uint32_t)WCAP);
-                    if ((uint32_t)w < wid) wpre += cc;
-                    if ((uint32_t)w == wid) wmine = cc;
-                    P += cc;
-                }
-                Pc = min(P, (uint32_t)(MP * NT));
-                over += P - Pc;
-                if (tid == 0 && over) atomicAdd(&pdrop[STAGE], over); // rare
-            } else {
             for (uint32_t p = tid; p < n; p += NT) offp[p] = (uint16_t)min(bend[key_of(sidx[p])] - p - 1, 14u);
             for (uint32_t k = tid; k < (uint32_t)(MP * NT); k += NT) pmark[k] = 0;
             __syncthreads();
             const uint32_t P = block_exscan<NT, MPR>(offp, (int)n, wsum);
-            Pc = min(P, (uint32_t)(MP * NT));
+            const uint32_t Pc = min(P, (uint32_t)(MP * NT));
             if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT); // rare
             for (uint32_t p = tid; p < n; p += NT) {
                 const uint32_t o = offp[p], e = (p + 1 < n) ? offp[p + 1] : P;
@@ -933,25 +807,29 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             }
             __syncthreads();
             block_maxscan<NT, MP>(pmark, (int)Pc, wsum);
-            }
-            constexpr int PVN = CHAIN ? MPW : MP; // pairs held per lane
-            uint32_t pv[PVN], pd[PVN];
+            uint32_t pv[MP], pd[MP];
 #pragma unroll
-            for (int u = 0; u < PVN; ++u) {
-                const uint32_t k = CHAIN ? (tid & 63) + u * 64 : tid + u * NT;
+            for (int u = 0; u < MP; ++u) {
+                const uint32_t k = tid + u * NT;
                 pv[u] = NIL;
                 pd[u] = 0;
-                if (CHAIN && k < wmine && wpre + k < Pc) { // this wave's kept pairs: destination histogram
-                    const uint32_t pr = plist[(tid >> 6) * WCAP + k], i = pr & 0xffffu, j = pr >> 16;
-                    const uint32_t x0 = rows[i * WI] ^ rows[j * WI];
-                    pv[u] = pr;
-                    pd[u] = (x0 >> (32 - C::DB)) & (C::NB - 1);
-                    atomicAdd(&hist[pd[u]], 1u);
-                } else if (!CHAIN && k < Pc) {
+                if (k < Pc) {
                     const uint32_t p = pmark[k], q = p + 1 + (k - offp[p]);
                     const uint32_t i = sidx[p], j = sidx[q];
                     const uint32_t x0 = rows[i * WI] ^ rows[j * WI];
-                    if (keep_pair(i, j, x0)) {
+                    // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the
+                    // pairs, so the remaining words are read only when it matches
+                    bool keep = x0 != 0;
+                    if (!keep) {
+#pragma unroll
+                        for (int w = 1; w < WI; ++w) keep |= rows[i * WI + w] != rows[j * WI + w];
+                    }
+                    if constexpr (PRUNE) {
+                        // signature hit (a shared parent, or ~1e-4 by chance): parents are
+                        // shared only if both rows were made by the same bucket
+                        if (keep && sig_hit(psig[i], psig[j]) && pdw[i] == pdw[j]) keep = false;
+                    }
+                    if (keep) {
                         pv[u] = (j << 16) | i;
                         pd[u] = (x0 >> (32 - C::DB)) & (C::NB - 1); // destination bucket
                         atomicAdd(&hist[pd[u]], 1u);
@@ -969,7 +847,7 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             uint32_t start = 0; // thread b < NB: first LDS slot of destination b (NB <= NT: one entry each)
             const uint32_t np = block_exscan<NT>(hist, cur, C::NB, wsum, &start);
 #pragma unroll
-            for (int u = 0; u < PVN; ++u)
+            for (int u = 0; u < MP; ++u)
                 if (pv[u] != NIL) spair[atomicAdd(&cur[pd[u]], 1u)] = pv[u];
             if (tid < C::NB) base[tid] = myb - start; // LDS slot t of destination b -> run position base[b] + t
             __syncthreads();

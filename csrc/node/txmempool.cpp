@@ -8,6 +8,7 @@
 #include "util/memusage.h"
 
 #include <algorithm>
+#include <queue>
 #include <cmath>
 #include <cstring>
 #include <deque>
@@ -56,13 +57,20 @@ CTxMemPool::CTxMemPool(CBlockPolicyEstimator* est) : minerPolicyEstimator(est) {
 const CTxMemPool::setEntries& CTxMemPool::GetMemPoolParents(txiter it) const { return mapLinks.at(it).parents; }
 const CTxMemPool::setEntries& CTxMemPool::GetMemPoolChildren(txiter it) const { return mapLinks.at(it).children; }
 
+// Link sets are accounted incrementally (cachedLinkUsage) so DynamicMemoryUsage stays O(1).
 void CTxMemPool::UpdateParent(txiter entry, txiter parent, bool add) {
-    if (add) mapLinks[entry].parents.insert(parent);
-    else mapLinks[entry].parents.erase(parent);
+    setEntries& s = mapLinks[entry].parents;
+    if (add ? s.insert(parent).second : s.erase(parent) != 0) {
+        if (add) cachedLinkUsage += memusage::IncrementalDynamicUsage(s);
+        else cachedLinkUsage -= memusage::IncrementalDynamicUsage(s);
+    }
 }
 void CTxMemPool::UpdateChild(txiter entry, txiter child, bool add) {
-    if (add) mapLinks[entry].children.insert(child);
-    else mapLinks[entry].children.erase(child);
+    setEntries& s = mapLinks[entry].children;
+    if (add ? s.insert(child).second : s.erase(child) != 0) {
+        if (add) cachedLinkUsage += memusage::IncrementalDynamicUsage(s);
+        else cachedLinkUsage -= memusage::IncrementalDynamicUsage(s);
+    }
 }
 
 bool CTxMemPool::CalculateMemPoolAncestors(const CTxMemPoolEntry& entry, setEntries& setAncestors,
@@ -236,7 +244,13 @@ void CTxMemPool::removeUnchecked(txiter it, MemPoolRemovalReason reason) {
     for (const CTxIn& in : ptx->vin) mapNextTx.erase(in.prevout);
     totalTxSize -= it->second->GetTxSize();
     cachedInnerUsage -= it->second->DynamicMemoryUsage();
-    mapLinks.erase(it);
+    {
+        auto li = mapLinks.find(it);
+        if (li != mapLinks.end()) {
+            cachedLinkUsage -= memusage::DynamicUsage(li->second.parents) + memusage::DynamicUsage(li->second.children);
+            mapLinks.erase(li);
+        }
+    }
     const uint256 h = it->first;
     mapTx.erase(it);
     nTransactionsUpdated++;
@@ -339,6 +353,7 @@ void CTxMemPool::clear() {
     mapNextTx.clear();
     totalTxSize = 0;
     cachedInnerUsage = 0;
+    cachedLinkUsage = 0;
     lastRollingFeeUpdate = GetTime();
     blockSinceLastRollingFeeBump = false;
     rollingMinimumFeeRate = 0;
@@ -392,17 +407,30 @@ void CTxMemPool::TrimToSize(size_t sizelimit, std::vector<COutPoint>* pvNoSpends
     std::lock_guard<CCriticalSection> l(cs);
     unsigned nTxnRemoved = 0;
     CFeeRate maxFeeRateRemoved(0);
-    while (!mapTx.empty() && DynamicMemoryUsage() > sizelimit) {
-        txiter worst = mapTx.end();
-        double worstScore = 0;
-        for (auto it = mapTx.begin(); it != mapTx.end(); ++it) {
-            const double s = DescendantScore(*it->second);
-            if (worst == mapTx.end() || s < worstScore ||
-                (s == worstScore && it->second->GetTime() > worst->second->GetTime())) {
-                worst = it;
-                worstScore = s;
-            }
-        }
+    if (DynamicMemoryUsage() <= sizelimit) return;
+    // Eviction order = lowest descendant score first, newest first on ties, then lowest txid
+    // (reference: the descendant_score index of mapTx). A lazy min-heap replaces the ordered
+    // index: when a package goes, the ancestors it leaves behind are re-queued with their new
+    // score, and a popped candidate whose score no longer matches is stale and skipped.
+    struct Cand {
+        double score;
+        int64_t time;
+        uint256 hash;
+    };
+    auto lowerPriority = [](const Cand& a, const Cand& b) {
+        if (a.score != b.score) return a.score > b.score;
+        if (a.time != b.time) return a.time < b.time;
+        return b.hash < a.hash;
+    };
+    std::vector<Cand> init;
+    init.reserve(mapTx.size());
+    for (const auto& kv : mapTx) init.push_back({DescendantScore(*kv.second), kv.second->GetTime(), kv.first});
+    std::priority_queue<Cand, std::vector<Cand>, decltype(lowerPriority)> heap(lowerPriority, std::move(init));
+    while (!heap.empty() && DynamicMemoryUsage() > sizelimit) {
+        const Cand c = heap.top();
+        heap.pop();
+        txiter worst = mapTx.find(c.hash);
+        if (worst == mapTx.end() || DescendantScore(*worst->second) != c.score) continue;
         CFeeRate removed(worst->second->GetModFeesWithDescendants(), worst->second->GetSizeWithDescendants());
         removed += incrementalRelayFee;
         trackPackageRemoved(removed);
@@ -410,10 +438,25 @@ void CTxMemPool::TrimToSize(size_t sizelimit, std::vector<COutPoint>* pvNoSpends
         setEntries stage;
         CalculateDescendants(worst, stage);
         nTxnRemoved += stage.size();
+        // ancestors outside the package lose descendants: their scores change
+        std::set<uint256> touched;
+        {
+            std::vector<txiter> todo(stage.begin(), stage.end());
+            while (!todo.empty()) {
+                txiter t = todo.back();
+                todo.pop_back();
+                for (txiter p : GetMemPoolParents(t))
+                    if (!stage.count(p) && touched.insert(p->first).second) todo.push_back(p);
+            }
+        }
         std::vector<CTransactionRef> txn;
         if (pvNoSpendsRemaining)
             for (txiter it : stage) txn.push_back(it->second->GetSharedTx());
         RemoveStaged(stage, false, MemPoolRemovalReason::SIZELIMIT);
+        for (const uint256& h : touched) {
+            auto it = mapTx.find(h);
+            if (it != mapTx.end()) heap.push({DescendantScore(*it->second), it->second->GetTime(), h});
+        }
         if (pvNoSpendsRemaining) {
             for (const auto& tx : txn)
                 for (const CTxIn& in : tx->vin) {
@@ -651,11 +694,9 @@ uint64_t CTxMemPool::GetTotalTxSize() const {
 size_t CTxMemPool::DynamicMemoryUsage() const {
     std::lock_guard<CCriticalSection> l(cs);
     // index nodes + entries + link sets (reference CTxMemPool::DynamicMemoryUsage)
-    size_t links = 0;
-    for (const auto& l : mapLinks) links += memusage::DynamicUsage(l.second.parents) + memusage::DynamicUsage(l.second.children);
     return memusage::DynamicUsage(mapTx) + mapTx.size() * memusage::MallocUsage(sizeof(CTxMemPoolEntry)) +
            memusage::MallocUsage(sizeof(memusage::stl_tree_node) + 2 * sizeof(void*)) * mapNextTx.size() +
-           memusage::DynamicUsage(mapLinks) + links + memusage::DynamicUsage(mapDeltas) + cachedInnerUsage;
+           memusage::DynamicUsage(mapLinks) + cachedLinkUsage + memusage::DynamicUsage(mapDeltas) + cachedInnerUsage;
 }
 unsigned CTxMemPool::GetTransactionsUpdated() const {
     std::lock_guard<CCriticalSection> l(cs);
@@ -703,6 +744,9 @@ void CTxMemPool::check(const CCoinsViewCache* pcoins, int spendHeight) const {
     }
     (void)spendHeight;
     if (checkTotal != totalTxSize) throw std::logic_error("mempool: total size mismatch");
+    size_t links = 0;
+    for (const auto& lk : mapLinks) links += memusage::DynamicUsage(lk.second.parents) + memusage::DynamicUsage(lk.second.children);
+    if (links != cachedLinkUsage) throw std::logic_error("mempool: link usage accounting mismatch");
 }
 
 // ------------------------------------------------------------------ coins view

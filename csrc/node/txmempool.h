@@ -231,6 +231,7 @@ private:
     std::map<uint256, std::pair<double, Amount>> mapDeltas;
     uint64_t totalTxSize = 0;
     uint64_t cachedInnerUsage = 0;
+    uint64_t cachedLinkUsage = 0; // parents/children set nodes
     unsigned nTransactionsUpdated = 0;
     uint32_t nCheckFrequency = 0;
     mutable int64_t lastRollingFeeUpdate = 0;

@@ -34,6 +34,7 @@ void RecordFailure(const std::string& what, const char* file, int line) {
     std::fprintf(stderr, "  FAIL %s.%s: %s (%s:%d)\n", g_current ? g_current->suite.c_str() : "?",
                  g_current ? g_current->name.c_str() : "?", what.c_str(), file, line);
 }
+bool HasFailures() { return g_failures != 0; }
 void FatalFailure(const std::string& what, const char* file, int line) {
     RecordFailure(what, file, line);
     throw Failure(what);

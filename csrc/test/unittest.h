@@ -38,6 +38,8 @@ struct Failure : std::runtime_error {
 // Non-fatal check: records a failure (the case keeps running).
 void RecordFailure(const std::string& what, const char* file, int line);
 [[noreturn]] void FatalFailure(const std::string& what, const char* file, int line);
+// True once the running case has recorded a failure.
+bool HasFailures();
 
 template <typename A, typename B> std::string Describe(const A& a, const B& b) {
     std::ostringstream os;
@@ -83,8 +85,9 @@ struct TestChain100Setup : TestingSetup {
     } while (0)
 #define CHECK_EQ(a, b)                                                                                  \
     do {                                                                                                \
-        const auto& _va = (a);                                                                          \
-        const auto& _vb = (b);                                                                          \
+        /* copies: a reference could dangle (e.g. std::max over temporaries) */                         \
+        const auto _va = (a);                                                                           \
+        const auto _vb = (b);                                                                           \
         if (!(_va == _vb))                                                                              \
             ::bcp::test::RecordFailure("CHECK_EQ(" #a ", " #b ")" + ::bcp::test::Describe(_va, _vb), __FILE__, \
                                        __LINE__);                                                       \

@@ -23,7 +23,10 @@ SUITES = _suites()
 
 def test_suite_inventory():
     # the suites ported from reference src/test/ (each must exist and hold cases)
-    for s in ["script_antireplay_tests", "sigopcount_tests"]:
+    for s in [
+        "script_antireplay_tests", "sigopcount_tests", "bloom_tests", "pmt_tests", "blockencodings_tests",
+        "coins_tests", "versionbits_tests", "mempool_tests",
+    ]:
         assert s in SUITES, s
 
 
