@@ -3,8 +3,11 @@
 Each op runs on the MI355X and raises if no HIP device is visible — there is no
 silent CPU fallback.  Ops that have a CPU implementation in the native core take
 an explicit ``use_gpu=False``.  Tensor inputs (``torch.uint8``) are accepted
-where batches are naturally dense; they are staged through pinned host memory by
-the native layer.
+where batches are naturally dense.  They are flattened to host bytes here
+(``.cpu()`` — a pageable copy); the native layer then packs them into per-device
+pinned staging buffers that it keeps across calls (``HostBuf`` in
+csrc/kernels/hip_util.h), so each H2D/D2H transfer is a single DMA from pinned
+memory on the op's own non-blocking stream.
 
 Kernel map (reference hot loops):
   sha256d64          K6  SHA-256d of 64-byte nodes (merkle levels)  sha256.hip

@@ -16,4 +16,9 @@ timeout -k 10 300 python -u bench.py > "$OUT/bench.log" 2>&1
 tail -1 "$OUT/bench.log"
 timeout -k 10 300 python -u tools/eh_recall.py --nonces 32 --threads 16 --json "$OUT/recall.json" > "$OUT/recall.log" 2>&1
 tail -4 "$OUT/recall.log"
+if [ "${2:-}" = "prof" ]; then
+  cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$OUT/prof" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 2 > "$GRAFT_REPO_ROOT/$OUT/prof.log" 2>&1
+  cd "$GRAFT_REPO_ROOT"
+  tail -1 "$OUT/prof.log"
+fi
 echo DONE
