@@ -1,20 +1,39 @@
 // Embedded ordered key-value store (replaces the reference's LevelDB wrapper,
 // src/dbwrapper.{h,cpp}: CDBWrapper Read/Write/Erase/Exists/WriteBatch/NewIterator,
-// CDBBatch, EstimateSize, IsEmpty; used by src/txdb.cpp for the block index and UTXO set).
+// CDBBatch, EstimateSize, IsEmpty; used by src/txdb.cpp for the block index and UTXO set,
+// and by the wallet).
 //
-// Design: a single append-only log of CRC-protected batches plus an in-memory ordered
-// index (key -> offset/length of the latest value in the log). Values are read back
-// with pread, so memory holds keys only. A batch is durable once its record is written
-// (optionally fsync'ed); a torn tail record is detected by the CRC on open and
-// truncated, which gives the atomic-batch semantics the chainstate flush relies on.
-// When dead bytes dominate the log it is rewritten (compaction) via write-new + rename.
+// Design: a log-structured merge store whose memory is bounded by its options, not by the
+// number of keys.
+//  * Writes append one CRC-protected record per batch to the write-ahead log (kv-<n>.log) and
+//    apply the batch to an in-memory ordered table (the memtable). A batch is atomic: on open,
+//    a torn or corrupt tail record is dropped and the log truncated there.
+//  * When the memtable passes `memtableBytes` (or its log passes twice that) it becomes
+//    immutable, a new log starts, and a background thread writes it out as a sorted segment
+//    (seg-<n>.sst: CRC'd data blocks, a sparse block index and a Bloom filter). Writers only
+//    wait if a second memtable fills before the first is on disk.
+//  * Segments are immutable. The background thread merges runs of adjacent segments when there
+//    are more than `maxSegments` (tombstones are dropped when the run reaches the oldest
+//    segment); readers and iterators keep the segment set they started with (shared
+//    ownership), so a merge never blocks them and never pulls a file out from under them.
+//  * MANIFEST (written to a temporary file, fsync'ed, renamed) names the live segments and the
+//    first log still needed; files it does not name are deleted on open.
+//  * Memory: the memtable(s), per segment a sparse index (one key per ~blockSize bytes) and a
+//    Bloom filter (bloomBitsPerKey bits per key), and an LRU cache of decoded blocks
+//    (blockCacheBytes). Point reads cost at most one block read per segment whose filter
+//    matches.
+// A pre-segment store (a single kv.log of batch records) is read as a log and migrated on open.
 #pragma once
 #include "primitives/serialize.h"
 
+#include <atomic>
+#include <condition_variable>
+#include <cstdint>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 namespace bcp {
@@ -31,8 +50,14 @@ public:
         ops.push_back({false, Ser(key), std::string()});
         bytes += ops.back().key.size();
     }
-    void WriteRaw(std::string key, std::string value) { ops.push_back({true, std::move(key), std::move(value)}); }
-    void EraseRaw(std::string key) { ops.push_back({false, std::move(key), std::string()}); }
+    void WriteRaw(std::string key, std::string value) {
+        bytes += key.size() + value.size();
+        ops.push_back({true, std::move(key), std::move(value)});
+    }
+    void EraseRaw(std::string key) {
+        bytes += key.size();
+        ops.push_back({false, std::move(key), std::string()});
+    }
     size_t SizeEstimate() const { return bytes; }
     void Clear() {
         ops.clear();
@@ -57,16 +82,23 @@ private:
     size_t bytes = 0;
 };
 
+// Ordered iteration over a consistent set of segments plus the live memtable (writes made
+// while iterating may or may not be seen, as with the reference's LevelDB iterators).
 class KVIterator {
 public:
     explicit KVIterator(const KVStore* db);
+    ~KVIterator();
     void Seek(const std::string& rawKey);
     template <typename K> void Seek(const K& key) { Seek(KVBatch::Ser(key)); }
     void SeekToFirst();
     bool Valid() const { return valid; }
     void Next();
     const std::string& RawKey() const { return curKey; }
-    bool RawValue(std::string& out) const;
+    bool RawValue(std::string& out) const {
+        if (!valid) return false;
+        out = curValue;
+        return true;
+    }
     template <typename K> bool GetKey(K& key) const {
         try {
             SpanReader r((const unsigned char*)curKey.data(), curKey.size(), SER_DISK, PROTOCOL_VERSION);
@@ -77,10 +109,9 @@ public:
         }
     }
     template <typename V> bool GetValue(V& value) const {
-        std::string raw;
-        if (!RawValue(raw)) return false;
+        if (!valid) return false;
         try {
-            SpanReader r((const unsigned char*)raw.data(), raw.size(), SER_DISK, PROTOCOL_VERSION);
+            SpanReader r((const unsigned char*)curValue.data(), curValue.size(), SER_DISK, PROTOCOL_VERSION);
             r >> value;
             return true;
         } catch (const std::exception&) {
@@ -88,16 +119,37 @@ public:
         }
     }
 
+    struct State;
+
 private:
+    void Settle(); // move to the first live entry at or after the sources' positions
     const KVStore* db;
-    std::string curKey;
+    std::unique_ptr<State> st;
+    std::string curKey, curValue;
     bool valid = false;
+};
+
+struct KVOptions {
+    size_t memtableBytes = 64u << 20;   // memtable size that triggers a segment flush
+    size_t blockCacheBytes = 32u << 20; // decoded-block LRU cache
+    size_t blockBytes = 4u << 10;       // target data block size
+    int bloomBitsPerKey = 10;           // ~1% false positives
+    int maxSegments = 8;                // more segments than this start a background merge
+    int mergeWidth = 4;                 // segments merged at once
+};
+
+struct KVStats {
+    size_t segments = 0;
+    uint64_t segmentBytes = 0, logBytes = 0;
+    size_t memtableBytes = 0, immutableBytes = 0;
+    size_t indexBytes = 0, bloomBytes = 0, cacheBytes = 0;
+    uint64_t flushes = 0, merges = 0, stalls = 0, bloomSkips = 0, blockReads = 0;
 };
 
 class KVStore {
 public:
     // path: directory; memory_only: no file backing (tests, -regtest in-memory dbs).
-    KVStore(const std::string& path, bool memory_only = false, bool wipe = false);
+    KVStore(const std::string& path, bool memory_only = false, bool wipe = false, const KVOptions& opts = KVOptions());
     ~KVStore();
     KVStore(const KVStore&) = delete;
 
@@ -127,36 +179,26 @@ public:
     bool ReadRaw(const std::string& key, std::string& value) const;
     bool ExistsRaw(const std::string& key) const;
     bool IsEmpty() const;
-    size_t Count() const;
+    size_t Count() const; // live keys (a full scan)
     size_t EstimateSize(const std::string& begin, const std::string& end) const;
     std::unique_ptr<KVIterator> NewIterator() const { return std::unique_ptr<KVIterator>(new KVIterator(this)); }
-    void Compact(); // rewrite the log with live records only
-    uint64_t LogBytes() const { return logSize; }
-    // Salvage (reference CDBEnv::Salvage / CWalletDB::Recover): scan a store's log without
-    // trusting its structure — every batch whose header and CRC check out is replayed, damaged
-    // stretches are skipped by searching for the next batch header (instead of truncating the
-    // rest of the log as Replay does). Returns the latest value of every live key; `skipped`
-    // counts the damaged bytes.
+    // Flush the memtable and merge every segment into one (tombstones dropped); synchronous.
+    void Compact();
+    // Write the memtable out as a segment now and wait for it (tests, shutdown paths).
+    void Flush();
+    uint64_t LogBytes() const; // bytes on disk (logs + segments)
+    KVStats Stats() const;
+    // Salvage (reference CDBEnv::Salvage / CWalletDB::Recover): read a store's files without
+    // trusting its manifest — every segment block and log batch whose CRC checks out is kept,
+    // damaged stretches are skipped (log batches by searching for the next record header).
+    // Returns the latest value of every live key; `skipped` counts the damaged bytes.
     static std::map<std::string, std::string> Salvage(const std::string& dir, uint64_t* skipped = nullptr);
+
+    struct Impl;
 
 private:
     friend class KVIterator;
-    struct Loc {
-        uint64_t off; // offset of the value bytes in the log (memory mode: index into mem)
-        uint32_t len;
-    };
-    bool Replay();
-    void MaybeCompact();
-    void DoCompact();
-    bool NextKey(const std::string& after, bool inclusive, std::string& out) const;
-
-    std::string dir, logPath;
-    bool memOnly;
-    int fd = -1;
-    uint64_t logSize = 0, liveBytes = 0;
-    std::map<std::string, Loc> index;
-    std::vector<std::string> mem; // memory-only value storage
-    mutable std::mutex cs;
+    std::unique_ptr<Impl> d;
 };
 
 } // namespace bcp

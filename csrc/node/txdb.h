@@ -62,7 +62,8 @@ struct CDiskTxPos : public CDiskBlockPos {
 
 class CCoinsViewDB : public CCoinsView {
 public:
-    CCoinsViewDB(const std::string& dir, bool fMemory, bool fWipe);
+    // nCacheSize: the store's memory budget (memtable + block cache), reference txdb.cpp:68
+    CCoinsViewDB(const std::string& dir, bool fMemory, bool fWipe, size_t nCacheSize = 8u << 20);
     bool GetCoin(const COutPoint& outpoint, Coin& coin) const override;
     bool HaveCoin(const COutPoint& outpoint) const override;
     uint256 GetBestBlock() const override;
@@ -78,7 +79,7 @@ private:
 
 class CBlockTreeDB {
 public:
-    CBlockTreeDB(const std::string& dir, bool fMemory, bool fWipe);
+    CBlockTreeDB(const std::string& dir, bool fMemory, bool fWipe, size_t nCacheSize = 2u << 20);
     bool WriteBatchSync(const std::vector<std::pair<int, const CBlockFileInfo*>>& fileInfo, int nLastFile,
                         const std::vector<const CBlockIndex*>& blockinfo);
     bool ReadBlockFileInfo(int nFile, CBlockFileInfo& info);

@@ -123,8 +123,14 @@ Chainstate::Chainstate(const CChainParams& p, const ChainstateOptions& o) : para
         TryCreateDirectories(base + "/blocks");
         SetBlocksDir(base + "/blocks");
     }
-    pblocktree.reset(new CBlockTreeDB(base + "/blocks/index", opts.memoryOnly, opts.wipe));
-    pcoinsdbview.reset(new CCoinsViewDB(base + "/chainstate", opts.memoryOnly, opts.wipe));
+    // -dbcache split like the reference (init.cpp:1505-1520): a small block-index store cache, the
+    // coins store's memtable + block cache, and the rest for the in-memory UTXO cache
+    const size_t total = opts.coinsCacheBytes;
+    const size_t blockTreeCache = std::min(total / 8, (size_t)2 << 20);
+    const size_t coinDBCache = std::min(total / 2, total / 4 + ((size_t)1 << 23));
+    opts.coinsCacheBytes = total - blockTreeCache - coinDBCache;
+    pblocktree.reset(new CBlockTreeDB(base + "/blocks/index", opts.memoryOnly, opts.wipe, blockTreeCache));
+    pcoinsdbview.reset(new CCoinsViewDB(base + "/chainstate", opts.memoryOnly, opts.wipe, coinDBCache));
     pcoinsTip.reset(new CCoinsViewCache(pcoinsdbview.get()));
     int threads = opts.scriptThreads <= 0 ? GetNumCores() : opts.scriptThreads;
     threads = std::max(1, std::min(threads, MAX_SCRIPTCHECK_THREADS));

@@ -13,7 +13,7 @@ from bitcoincashplus_amd.node.process import BcpdProcess
 
 pytestmark = pytest.mark.functional
 
-BATCH_MAGIC = struct.pack("<I", 0xB7C0DB01)
+BATCH_MAGIC = struct.pack("<I", 0xB7C0DB02)  # write-ahead log record header (csrc/node/kvstore.cpp)
 
 
 def test_salvagewallet_recovers_keys(tmp_path):
@@ -31,7 +31,8 @@ def test_salvagewallet_recovers_keys(tmp_path):
         port = n.rpcport
     finally:
         n.stop()
-    logs = [p for p in glob.glob(os.path.join(d, "**", "kv.log"), recursive=True) if "wallet.dat" in p]
+    logs = [p for p in glob.glob(os.path.join(d, "**", "kv-*.log"), recursive=True)
+            if "wallet.dat" in p and os.path.getsize(p) > 0]
     assert len(logs) == 1
     data = bytearray(open(logs[0], "rb").read())
     # damage the payload of a batch in the middle of the log (CRC now fails for it)
