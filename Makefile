@@ -100,6 +100,35 @@ bin/bcp-fuzz-asan: $(ASAN_OBJS) $(HIP_OBJS)
 	@mkdir -p bin
 	$(CXX) $(ASAN_FLAGS) -o $@ $^ $(LDLIBS)
 
+# Host sanitizer builds of the node and the unit suites (reference --enable-tsan/--enable-asan,
+# configure.ac:195-275): every CPU source rebuilt instrumented, the gfx950 kernel objects linked as
+# they are.  `make tsan` -> bin/tsan/{bcpd,test_bcp}; `make asan-node` -> bin/asan/{bcpd,test_bcp}.
+# tools/sanitize.sh runs the unit suites and the P2P/ConnectBlock functional tests under both.
+TSAN_FLAGS := -fsanitize=thread -fno-omit-frame-pointer -O1 -g
+SAN_SRCS   := $(CORE_SRCS) $(GPU_HOST)
+TSAN_CORE  := $(patsubst csrc/%.cpp,build/tsan/%.o,$(SAN_SRCS))
+TSAN_TEST  := $(patsubst csrc/%.cpp,build/tsan/%.o,$(TEST_SRCS))
+ASAN_CORE  := $(patsubst csrc/%.cpp,build/asan/%.o,$(SAN_SRCS))
+ASAN_TEST  := $(patsubst csrc/%.cpp,build/asan/%.o,$(TEST_SRCS))
+.PHONY: tsan asan-node
+tsan: bin/tsan/bcpd bin/tsan/test_bcp
+asan-node: bin/asan/bcpd bin/asan/test_bcp
+build/tsan/%.o: csrc/%.cpp
+	@mkdir -p $(dir $@)
+	$(CXX) $(filter-out -O2,$(CXXFLAGS)) $(TSAN_FLAGS) -MMD -MP -c $< -o $@
+bin/tsan/bcpd: build/tsan/tools/bcpd.o $(TSAN_CORE) $(HIP_OBJS)
+	@mkdir -p bin/tsan
+	$(CXX) $(TSAN_FLAGS) -rdynamic -o $@ $^ $(LDLIBS)
+bin/tsan/test_bcp: $(TSAN_TEST) $(TSAN_CORE) $(HIP_OBJS)
+	@mkdir -p bin/tsan
+	$(CXX) $(TSAN_FLAGS) -rdynamic -o $@ $^ $(LDLIBS)
+bin/asan/bcpd: build/asan/tools/bcpd.o $(ASAN_CORE) $(HIP_OBJS)
+	@mkdir -p bin/asan
+	$(CXX) $(ASAN_FLAGS) -rdynamic -o $@ $^ $(LDLIBS)
+bin/asan/test_bcp: $(ASAN_TEST) $(ASAN_CORE) $(HIP_OBJS)
+	@mkdir -p bin/asan
+	$(CXX) $(ASAN_FLAGS) -rdynamic -o $@ $^ $(LDLIBS)
+
 clean:
 	rm -rf build bin lib bitcoincashplus_amd/_bcpnative*.so
 

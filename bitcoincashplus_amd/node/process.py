@@ -78,7 +78,8 @@ class BcpdProcess:
         self.rpcport = port or free_port()
         self.p2p_port = p2p_port or free_port()
         self.user, self.password = rpcuser, rpcpassword
-        self.binary = binary or os.path.join(BIN_DIR, "bcpd")
+        # BCP_BCPD: run another build of the node (e.g. bin/tsan/bcpd, tools/sanitize.sh)
+        self.binary = binary or os.environ.get("BCP_BCPD") or os.path.join(BIN_DIR, "bcpd")
         self.extra_args = list(extra_args)
         self.proc = None
         self.rpc = RPCProxy(self.rpcport, rpcuser, rpcpassword)

@@ -628,6 +628,7 @@ struct KVStore::Impl {
     int logFd = -1, lockFd = -1;
     uint64_t logNum = 0, logBytes = 0, firstLog = 0, nextFile = 1, seq = 0;
     bool stop = false, bgError = false, merging = false;
+    std::atomic<bool> stopping{false}; // `stop` for loops that do not hold mu
 
     std::mutex mergeMu; // one merge at a time (background merger or Compact())
     std::thread flusher, merger;
@@ -801,6 +802,7 @@ struct KVStore::Impl {
         {
             std::lock_guard<std::mutex> l(mu);
             stop = true;
+            stopping = true;
         }
         cv.notify_all();
         if (flusher.joinable()) flusher.join();
@@ -824,7 +826,9 @@ struct KVStore::Impl {
 
     // Seal the memtable: a fresh log takes the next writes; the flusher writes `imm` out.
     bool SealLocked(std::unique_lock<std::mutex>& l) {
-        while (imm && !bgError) {
+        // back-pressure: a second full memtable, or merges far behind (reads would check too
+        // many segments), waits for the background threads
+        while ((imm || (int)segs->size() > 3 * opt.maxSegments) && !bgError && !stop) {
             ctr.stalls++;
             cv.wait(l);
         }
@@ -958,13 +962,11 @@ struct KVStore::Impl {
                 if (win < 0 || CompareBytes(cs[i].e.k, cs[i].e.klen, cs[win].e.k, cs[win].e.klen) < 0) win = (int)i;
             }
             if (win < 0) break;
-            {
+            if (stopping.load(std::memory_order_relaxed)) { // (no lock per entry: writers hold mu for whole batches)
+                w.Abort();
                 std::lock_guard<std::mutex> l(mu);
-                if (stop) {
-                    w.Abort();
-                    merging = false;
-                    return false;
-                }
+                merging = false;
+                return false;
             }
             const EntryView e = cs[win].e; // newest copy (lowest index) wins ties
             last.assign(e.k, e.klen);
