@@ -104,7 +104,7 @@ bin/bcp-fuzz-asan: $(ASAN_OBJS) $(HIP_OBJS)
 # configure.ac:195-275): every CPU source rebuilt instrumented, the gfx950 kernel objects linked as
 # they are.  `make tsan` -> bin/tsan/{bcpd,test_bcp}; `make asan-node` -> bin/asan/{bcpd,test_bcp}.
 # tools/sanitize.sh runs the unit suites and the P2P/ConnectBlock functional tests under both.
-TSAN_FLAGS := -fsanitize=thread -fno-omit-frame-pointer -O1 -g
+TSAN_FLAGS := -fsanitize=thread -fno-omit-frame-pointer -O1 -g -include csrc/util/tsan_compat.h
 SAN_SRCS   := $(CORE_SRCS) $(GPU_HOST)
 TSAN_CORE  := $(patsubst csrc/%.cpp,build/tsan/%.o,$(SAN_SRCS))
 TSAN_TEST  := $(patsubst csrc/%.cpp,build/tsan/%.o,$(TEST_SRCS))
@@ -128,6 +128,19 @@ bin/asan/bcpd: build/asan/tools/bcpd.o $(ASAN_CORE) $(HIP_OBJS)
 bin/asan/test_bcp: $(ASAN_TEST) $(ASAN_CORE) $(HIP_OBJS)
 	@mkdir -p bin/asan
 	$(CXX) $(ASAN_FLAGS) -rdynamic -o $@ $^ $(LDLIBS)
+
+# Clang thread-safety analysis over every CPU source (reference src/threadsafety.h, built with
+# -Wthread-safety under clang): GUARDED_BY / EXCLUSIVE_LOCKS_REQUIRED / LOCKS_EXCLUDED on the
+# chainstate, mempool and connection manager; any warning fails the target.
+TSA_CXX    ?= $(ROCM)/lib/llvm/bin/clang++
+TSA_STAMPS := $(patsubst csrc/%.cpp,build/tsa/%.ok,$(SAN_SRCS))
+.PHONY: thread-safety
+thread-safety: $(TSA_STAMPS)
+build/tsa/%.ok: csrc/%.cpp
+	@mkdir -p $(dir $@)
+	$(TSA_CXX) -std=c++17 -fsyntax-only -Icsrc -Wthread-safety -Werror=thread-safety -Wno-unknown-warning-option \
+	    -MMD -MP -MF $(@:.ok=.d) -MT $@ $<
+	@touch $@
 
 clean:
 	rm -rf build bin lib bitcoincashplus_amd/_bcpnative*.so

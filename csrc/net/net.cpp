@@ -330,14 +330,20 @@ bool CConnman::Start(Scheduler* scheduler, const Options& o, std::string& err) {
     events = o.events;
     nSendBufferMaxSize = o.nSendBufferMaxSize;
     nReceiveFloodSize = o.nReceiveFloodSize;
-    nMaxOutboundLimit = o.nMaxOutboundLimit;
-    nMaxOutboundTimeframe = o.nMaxOutboundTimeframe;
+    {
+        std::lock_guard<Mutex> l(cs_totalBytesSent);
+        nMaxOutboundLimit = o.nMaxOutboundLimit;
+        nMaxOutboundTimeframe = o.nMaxOutboundTimeframe;
+    }
     vWhitelistedRange = o.vWhitelistedRange;
     vConnect = o.vConnect;
     fConnectOnly = o.fConnectOnly;
     fDNSSeed = o.fDNSSeed;
     datadir = o.datadir;
-    for (const std::string& s : o.vSeedNodes) vOneShots.push_back(s);
+    {
+        std::lock_guard<Mutex> l(cs_vOneShots);
+        for (const std::string& s : o.vSeedNodes) vOneShots.push_back(s);
+    }
 
     if (!datadir.empty()) {
         if (addrman.Read(datadir + "/peers.dat", Params().NetMagic()))
@@ -676,7 +682,7 @@ void CConnman::AcceptConnection(const ListenSocket& ls) {
 
 void CConnman::RecordBytesSent(uint64_t n) {
     nTotalBytesSent += n;
-    std::lock_guard<std::mutex> l(cs_totalBytesSent);
+    std::lock_guard<Mutex> l(cs_totalBytesSent);
     const uint64_t now = GetTime();
     if (nMaxOutboundCycleStartTime + nMaxOutboundTimeframe < now) {
         nMaxOutboundCycleStartTime = now;
@@ -686,7 +692,7 @@ void CConnman::RecordBytesSent(uint64_t n) {
 }
 
 bool CConnman::OutboundTargetReached(bool historicalBlockServingLimit) {
-    std::lock_guard<std::mutex> l(cs_totalBytesSent);
+    std::lock_guard<Mutex> l(cs_totalBytesSent);
     if (nMaxOutboundLimit == 0) return false;
     if (historicalBlockServingLimit) {
         const uint64_t timeLeft = nMaxOutboundCycleStartTime + nMaxOutboundTimeframe - (uint64_t)GetTime();
@@ -699,14 +705,14 @@ bool CConnman::OutboundTargetReached(bool historicalBlockServingLimit) {
 }
 
 uint64_t CConnman::GetOutboundTargetBytesLeft() {
-    std::lock_guard<std::mutex> l(cs_totalBytesSent);
+    std::lock_guard<Mutex> l(cs_totalBytesSent);
     if (nMaxOutboundLimit == 0) return 0;
     return nMaxOutboundTotalBytesSentInCycle >= nMaxOutboundLimit ? 0
                                                                    : nMaxOutboundLimit - nMaxOutboundTotalBytesSentInCycle;
 }
 
 uint64_t CConnman::GetMaxOutboundTimeLeftInCycle() {
-    std::lock_guard<std::mutex> l(cs_totalBytesSent);
+    std::lock_guard<Mutex> l(cs_totalBytesSent);
     if (nMaxOutboundLimit == 0) return 0;
     if (nMaxOutboundCycleStartTime == 0) return nMaxOutboundTimeframe;
     const uint64_t end = nMaxOutboundCycleStartTime + nMaxOutboundTimeframe;
@@ -968,14 +974,14 @@ bool CConnman::InterruptibleSleep(int64_t millis) {
 void CConnman::ProcessOneShot() {
     std::string dest;
     {
-        std::lock_guard<std::mutex> l(cs_vOneShots);
+        std::lock_guard<Mutex> l(cs_vOneShots);
         if (vOneShots.empty()) return;
         dest = vOneShots.front();
         vOneShots.pop_front();
     }
     CAddress addr;
     if (!OpenNetworkConnection(addr, false, dest.c_str(), true)) {
-        std::lock_guard<std::mutex> l(cs_vOneShots);
+        std::lock_guard<Mutex> l(cs_vOneShots);
         vOneShots.push_back(dest);
     }
 }
@@ -1050,7 +1056,7 @@ std::vector<AddedNodeInfo> CConnman::GetAddedNodeInfo() {
     std::vector<AddedNodeInfo> ret;
     std::vector<std::string> added;
     {
-        std::lock_guard<std::mutex> l(cs_vAddedNodes);
+        std::lock_guard<Mutex> l(cs_vAddedNodes);
         added = vAddedNodes;
     }
     std::map<CService, bool> mapConnected;
@@ -1087,7 +1093,7 @@ std::vector<AddedNodeInfo> CConnman::GetAddedNodeInfo() {
 
 void CConnman::ThreadOpenAddedConnections() {
     {
-        std::lock_guard<std::mutex> l(cs_vAddedNodes);
+        std::lock_guard<Mutex> l(cs_vAddedNodes);
         for (const std::string& s : gArgs.GetArgs("-addnode")) vAddedNodes.push_back(s);
     }
     while (!interruptNet) {
@@ -1175,7 +1181,7 @@ void CConnman::ClearBanned() {
 }
 
 bool CConnman::AddNode(const std::string& node) {
-    std::lock_guard<std::mutex> l(cs_vAddedNodes);
+    std::lock_guard<Mutex> l(cs_vAddedNodes);
     for (const std::string& s : vAddedNodes)
         if (s == node) return false;
     vAddedNodes.push_back(node);
@@ -1183,7 +1189,7 @@ bool CConnman::AddNode(const std::string& node) {
 }
 
 bool CConnman::RemoveAddedNode(const std::string& node) {
-    std::lock_guard<std::mutex> l(cs_vAddedNodes);
+    std::lock_guard<Mutex> l(cs_vAddedNodes);
     for (auto it = vAddedNodes.begin(); it != vAddedNodes.end(); ++it)
         if (*it == node) {
             vAddedNodes.erase(it);

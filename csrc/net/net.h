@@ -325,9 +325,18 @@ public:
 
     uint64_t GetTotalBytesRecv() const { return nTotalBytesRecv; }
     uint64_t GetTotalBytesSent() const { return nTotalBytesSent; }
-    void SetMaxOutboundTarget(uint64_t limit) { nMaxOutboundLimit = limit; }
-    uint64_t GetMaxOutboundTarget() const { return nMaxOutboundLimit; }
-    uint64_t GetMaxOutboundTimeframe() const { return nMaxOutboundTimeframe; }
+    void SetMaxOutboundTarget(uint64_t limit) {
+        std::lock_guard<Mutex> l(cs_totalBytesSent);
+        nMaxOutboundLimit = limit;
+    }
+    uint64_t GetMaxOutboundTarget() const {
+        std::lock_guard<Mutex> l(cs_totalBytesSent);
+        return nMaxOutboundLimit;
+    }
+    uint64_t GetMaxOutboundTimeframe() const {
+        std::lock_guard<Mutex> l(cs_totalBytesSent);
+        return nMaxOutboundTimeframe;
+    }
     bool OutboundTargetReached(bool historicalBlockServingLimit);
     uint64_t GetOutboundTargetBytesLeft();
     uint64_t GetMaxOutboundTimeLeftInCycle();
@@ -377,22 +386,24 @@ private:
     std::atomic<bool> fNetworkActive{true};
     CAddrMan addrman;
     BanMan banman;
-    std::mutex cs_vOneShots;
-    std::deque<std::string> vOneShots;
-    std::mutex cs_vAddedNodes;
-    std::vector<std::string> vAddedNodes;
+    Mutex cs_vOneShots;
+    std::deque<std::string> vOneShots GUARDED_BY(cs_vOneShots);
+    Mutex cs_vAddedNodes;
+    std::vector<std::string> vAddedNodes GUARDED_BY(cs_vAddedNodes);
     std::vector<std::string> vConnect;
     bool fConnectOnly = false;
     bool fDNSSeed = true;
     std::vector<CSubNet> vWhitelistedRange;
     mutable CCriticalSection cs_vNodes{"cs_vNodes"};
-    std::vector<CNode*> vNodes;
+    std::vector<CNode*> vNodes GUARDED_BY(cs_vNodes);
     std::list<CNode*> vNodesDisconnected;
     std::atomic<NodeId> nLastNodeId{0};
     std::atomic<uint64_t> nTotalBytesRecv{0}, nTotalBytesSent{0};
-    std::mutex cs_totalBytesSent;
-    uint64_t nMaxOutboundTotalBytesSentInCycle = 0, nMaxOutboundCycleStartTime = 0;
-    uint64_t nMaxOutboundLimit = 0, nMaxOutboundTimeframe = 0;
+    mutable Mutex cs_totalBytesSent;
+    uint64_t nMaxOutboundTotalBytesSentInCycle GUARDED_BY(cs_totalBytesSent) = 0;
+    uint64_t nMaxOutboundCycleStartTime GUARDED_BY(cs_totalBytesSent) = 0;
+    uint64_t nMaxOutboundLimit GUARDED_BY(cs_totalBytesSent) = 0;
+    uint64_t nMaxOutboundTimeframe GUARDED_BY(cs_totalBytesSent) = 0;
     const uint64_t nSeed0, nSeed1;
     int64_t nNextInvSendInbound = 0;
 

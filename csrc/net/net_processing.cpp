@@ -111,7 +111,7 @@ struct PeerLogicValidation::Impl {
     int64_t nTimeBestReceived = 0;
     FastRandomContext rng;
 
-    CCriticalSection& csMain() { return cs->cs(); }
+    CCriticalSection& csMain() RETURN_CAPABILITY(cs->cs()) { return cs->cs(); }
     CNodeState* State(NodeId id) {
         auto it = mapNodeState.find(id);
         return it == mapNodeState.end() ? nullptr : &it->second;
@@ -213,7 +213,7 @@ struct PeerLogicValidation::Impl {
         }
     }
 
-    bool CanDirectFetch() {
+    bool CanDirectFetch() EXCLUSIVE_LOCKS_REQUIRED(csMain()) {
         return cs->Tip()->GetBlockTime() > GetAdjustedTime() - cs->Params().GetConsensus().nPowTargetSpacing * 20;
     }
 
@@ -223,7 +223,8 @@ struct PeerLogicValidation::Impl {
         return false;
     }
 
-    void FindNextBlocksToDownload(NodeId id, unsigned count, std::vector<const CBlockIndex*>& vBlocks, NodeId& nodeStaller) {
+    void FindNextBlocksToDownload(NodeId id, unsigned count, std::vector<const CBlockIndex*>& vBlocks, NodeId& nodeStaller)
+        EXCLUSIVE_LOCKS_REQUIRED(csMain()) {
         if (count == 0) return;
         vBlocks.reserve(vBlocks.size() + count);
         CNodeState* st = State(id);
@@ -333,7 +334,7 @@ struct PeerLogicValidation::Impl {
         vExtraTxnForCompactIt = (vExtraTxnForCompactIt + 1) % max;
     }
 
-    bool AlreadyHave(const CInv& inv) {
+    bool AlreadyHave(const CInv& inv) EXCLUSIVE_LOCKS_REQUIRED(csMain()) {
         switch (inv.type) {
         case MSG_TX: {
             if (cs->Tip()->GetBlockHash() != hashRecentRejectsChainTip) {
@@ -1718,6 +1719,7 @@ bool PeerLogicValidation::SendMessages(CNode* pto, std::atomic<bool>& interrupt)
 
     std::unique_lock<CCriticalSection> lockMain(I.csMain(), std::try_to_lock);
     if (!lockMain) return true; // busy validating: try again next round
+    AssertLockHeld(I.csMain());   // (unique_lock is invisible to the thread-safety analysis)
     if (I.SendRejectsAndCheckIfBanned(pto)) return true;
     CNodeState* st = I.State(pto->GetId());
     if (!st) return true;

@@ -130,7 +130,7 @@ bool StartNetwork(NodeContext& node, std::string& err) {
     if (gArgs.GetArg("-prune", (int64_t)0) > 0) o.nLocalServices &= ~(uint64_t)NODE_NETWORK;
     o.nRelevantServices = NODE_NETWORK;
     o.nMaxOutboundLimit = (uint64_t)gArgs.GetArg("-maxuploadtarget", (int64_t)0) * 1024 * 1024;
-    o.nBestHeight = node.chainstate->Height();
+    o.nBestHeight = node.chainstate->HeightNow();
     o.datadir = node.datadir;
     const int port = (int)gArgs.GetArg("-port", (int64_t)params.GetDefaultPort());
     for (const std::string& b : gArgs.GetArgs("-bind")) {

@@ -19,6 +19,7 @@
 #include <unistd.h>
 
 #include <fstream>
+#include <mutex>
 #include <sstream>
 
 namespace bcp {
@@ -70,22 +71,34 @@ public:
     }
     void Stop() {
         stop = true;
-        if (fd >= 0) shutdown(fd, SHUT_RDWR);
+        {
+            // fdMu: the control thread may be closing the socket right now (TSan-found race)
+            std::lock_guard<std::mutex> l(fdMu);
+            if (fd >= 0) shutdown(fd, SHUT_RDWR);
+        }
         if (th.joinable()) th.join();
     }
 
 private:
+    void CloseFd() {
+        std::lock_guard<std::mutex> l(fdMu);
+        if (fd >= 0) close(fd);
+        fd = -1;
+    }
     bool Connect() {
         CService svc;
         if (!Lookup(target, svc, 9051, true)) return false;
         struct sockaddr_storage ss;
         socklen_t len = sizeof(ss);
         svc.GetSockAddr((struct sockaddr*)&ss, &len);
-        fd = socket(((struct sockaddr*)&ss)->sa_family, SOCK_STREAM, IPPROTO_TCP);
-        if (fd < 0) return false;
-        if (connect(fd, (struct sockaddr*)&ss, len) != 0) {
-            close(fd);
-            fd = -1;
+        const int s = socket(((struct sockaddr*)&ss)->sa_family, SOCK_STREAM, IPPROTO_TCP);
+        if (s < 0) return false;
+        {
+            std::lock_guard<std::mutex> l(fdMu);
+            fd = s;
+        }
+        if (stop || connect(s, (struct sockaddr*)&ss, len) != 0) {
+            CloseFd();
             return false;
         }
         return true;
@@ -223,8 +236,7 @@ private:
                     LogPrintf("tor: authentication or ADD_ONION failed on %s\n", target.c_str());
                 }
                 if (onion.IsValid()) RemoveLocal(onion);
-                close(fd);
-                fd = -1;
+                CloseFd();
             } else {
                 LogPrint(BCLog::TOR, "tor: Error connecting to Tor control socket %s\n", target.c_str());
             }
@@ -237,6 +249,7 @@ private:
     int localPort;
     std::atomic<bool> stop{false};
     std::thread th;
+    std::mutex fdMu; // fd is closed by the control thread and shut down by Stop()
     int fd = -1;
     std::string buf;
     CService onion;

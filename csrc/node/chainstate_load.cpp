@@ -16,7 +16,11 @@
 namespace bcp {
 
 bool Chainstate::LoadBlockIndexDB(std::string& err) {
-    if (!pblocktree->LoadBlockIndexGuts([this](const uint256& h) { return InsertBlockIndex(h); }, params.GetConsensus())) {
+    auto insert = [this](const uint256& h) {
+        AssertLockHeld(cs_main); // called back synchronously from LoadBlockIndexGuts
+        return InsertBlockIndex(h);
+    };
+    if (!pblocktree->LoadBlockIndexGuts(insert, params.GetConsensus())) {
         err = "Error loading block index (corrupt entry)";
         return false;
     }
@@ -146,6 +150,7 @@ bool Chainstate::InitBlockIndex(std::string& err) {
 // An interrupted UTXO flush leaves a head-blocks marker [new, old]: roll the coins from
 // `old` forward to `new` by disconnecting back to the fork point and reconnecting.
 bool Chainstate::ReplayBlocks(std::string& err) {
+    std::lock_guard<CCriticalSection> l(cs_main); // startup, but DisconnectBlock expects the lock
     std::vector<uint256> heads = pcoinsdbview->GetHeadBlocks();
     if (heads.empty()) return true;
     if (heads.size() != 2) {

@@ -166,9 +166,12 @@ bool Chainstate::AcceptToMemoryPoolWorker(CValidationState& state, const CTransa
     const size_t nLimitDescendantSize =
         (size_t)gArgs.GetArg("-limitdescendantsize", (int64_t)DEFAULT_DESCENDANT_SIZE_LIMIT) * 1000;
     std::string errString;
-    if (!mempool->CalculateMemPoolAncestors(entry, setAncestors, nLimitAncestors, nLimitAncestorSize, nLimitDescendants,
-                                            nLimitDescendantSize, errString))
-        return state.DoS(0, false, REJECT_NONSTANDARD, "too-long-mempool-chain", false, errString);
+    {
+        std::lock_guard<CCriticalSection> lpool(mempool->cs); // the walk reads mapTx / mapLinks
+        if (!mempool->CalculateMemPoolAncestors(entry, setAncestors, nLimitAncestors, nLimitAncestorSize,
+                                                nLimitDescendants, nLimitDescendantSize, errString))
+            return state.DoS(0, false, REJECT_NONSTANDARD, "too-long-mempool-chain", false, errString);
+    }
     uint32_t scriptVerifyFlags = STANDARD_SCRIPT_VERIFY_FLAGS;
     if (!params.RequireStandard())
         scriptVerifyFlags = (uint32_t)gArgs.GetArg("-promiscuousmempoolflags", (int64_t)scriptVerifyFlags);

@@ -175,8 +175,10 @@ std::unique_ptr<CBlockTemplate> BlockAssembler::CreateNewBlock(const CScript& sc
     pblocktemplate->vTxFees.push_back(-1);
     pblocktemplate->vTxSigOpsCount.push_back(-1);
     std::lock_guard<CCriticalSection> l(chainstate.cs());
-    std::unique_ptr<std::lock_guard<CCriticalSection>> lmp;
-    if (mempool) lmp.reset(new std::lock_guard<CCriticalSection>(mempool->cs));
+    // cs_main then the mempool lock for the whole template, like the reference's LOCK2; without a
+    // mempool (tests) a private lock stands in so the scope stays unconditional
+    static CCriticalSection noMempool{"miner.nomempool"};
+    std::lock_guard<CCriticalSection> lmp(mempool ? mempool->cs : noMempool);
     const CChainParams& chainparams = chainstate.Params();
     const Consensus::Params& cp = chainparams.GetConsensus();
     CBlockIndex* pindexPrev = chainstate.Tip();

@@ -77,13 +77,12 @@ bool CTxMemPool::CalculateMemPoolAncestors(const CTxMemPoolEntry& entry, setEntr
                                            uint64_t limitAncestorCount, uint64_t limitAncestorSize,
                                            uint64_t limitDescendantCount, uint64_t limitDescendantSize,
                                            std::string& errString, bool fSearchForParents) const {
-    CTxMemPool* self = const_cast<CTxMemPool*>(this);
     setEntries parentHashes;
     const CTransaction& tx = entry.GetTx();
     if (fSearchForParents) {
         for (const CTxIn& in : tx.vin) {
-            auto piter = self->mapTx.find(in.prevout.hash);
-            if (piter != self->mapTx.end()) {
+            auto piter = TxMap().find(in.prevout.hash);
+            if (piter != TxMap().end()) {
                 parentHashes.insert(piter);
                 if (parentHashes.size() + 1 > limitAncestorCount) {
                     errString = strprintf("too many unconfirmed parents [limit: %u]", (unsigned)limitAncestorCount);
@@ -92,7 +91,7 @@ bool CTxMemPool::CalculateMemPoolAncestors(const CTxMemPoolEntry& entry, setEntr
             }
         }
     } else {
-        auto it = self->mapTx.find(tx.GetHash());
+        auto it = TxMap().find(tx.GetHash());
         parentHashes = GetMemPoolParents(it);
     }
     size_t totalSizeWithAncestors = entry.GetTxSize();
@@ -633,11 +632,10 @@ std::vector<const CTxMemPoolEntry*> CTxMemPool::GetAncestors(const uint256& hash
 std::vector<const CTxMemPoolEntry*> CTxMemPool::GetDescendants(const uint256& hash) const {
     std::lock_guard<CCriticalSection> l(cs);
     std::vector<const CTxMemPoolEntry*> r;
-    CTxMemPool* self = const_cast<CTxMemPool*>(this);
-    auto it = self->mapTx.find(hash);
-    if (it == self->mapTx.end()) return r;
+    auto it = TxMap().find(hash);
+    if (it == TxMap().end()) return r;
     setEntries d;
-    self->CalculateDescendants(it, d);
+    const_cast<CTxMemPool*>(this)->CalculateDescendants(it, d);
     d.erase(it);
     for (txiter x : d) r.push_back(x->second.get());
     return r;

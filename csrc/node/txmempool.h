@@ -159,8 +159,8 @@ public:
     bool CalculateMemPoolAncestors(const CTxMemPoolEntry& entry, setEntries& setAncestors, uint64_t limitAncestorCount,
                                    uint64_t limitAncestorSize, uint64_t limitDescendantCount,
                                    uint64_t limitDescendantSize, std::string& errString,
-                                   bool fSearchForParents = true) const;
-    void CalculateDescendants(txiter it, setEntries& setDescendants);
+                                   bool fSearchForParents = true) const EXCLUSIVE_LOCKS_REQUIRED(cs);
+    void CalculateDescendants(txiter it, setEntries& setDescendants) EXCLUSIVE_LOCKS_REQUIRED(cs);
 
     void removeRecursive(const CTransaction& tx, MemPoolRemovalReason reason = MemPoolRemovalReason::UNKNOWN);
     void removeForReorg(const CCoinsViewCache* pcoins, unsigned nMemPoolHeight, int flags,
@@ -195,11 +195,11 @@ public:
     std::vector<txiter> SortedByAncestorScore();
     std::vector<const CTxMemPoolEntry*> SortedByDepthAndScore() const;
     std::vector<CTransactionRef> AllTransactions() const;
-    void CompactParents(txiter it, setEntries& out) const;
-    const setEntries& GetMemPoolParents(txiter it) const;
-    const setEntries& GetMemPoolChildren(txiter it) const;
-    txiter MapTxEnd() { return mapTx.end(); }
-    txiter Find(const uint256& h) { return mapTx.find(h); }
+    void CompactParents(txiter it, setEntries& out) const EXCLUSIVE_LOCKS_REQUIRED(cs);
+    const setEntries& GetMemPoolParents(txiter it) const EXCLUSIVE_LOCKS_REQUIRED(cs);
+    const setEntries& GetMemPoolChildren(txiter it) const EXCLUSIVE_LOCKS_REQUIRED(cs);
+    txiter MapTxEnd() EXCLUSIVE_LOCKS_REQUIRED(cs) { return mapTx.end(); }
+    txiter Find(const uint256& h) EXCLUSIVE_LOCKS_REQUIRED(cs) { return mapTx.find(h); }
 
     unsigned long size() const;
     uint64_t GetTotalTxSize() const;
@@ -210,33 +210,37 @@ public:
     void setSanityCheck(double dFrequency) { nCheckFrequency = (uint32_t)(dFrequency * 4294967295.0); }
     CBlockPolicyEstimator* Estimator() { return minerPolicyEstimator; }
 
-    indirectmap<COutPoint, const CTransaction*> mapNextTx; // keys point into the spending txs
+    indirectmap<COutPoint, const CTransaction*> mapNextTx GUARDED_BY(cs); // keys point into the spending txs
 
 private:
+    // mapTx for const members that hand out (mutable) iterators
+    std::map<uint256, std::unique_ptr<CTxMemPoolEntry>>& TxMap() const EXCLUSIVE_LOCKS_REQUIRED(cs) {
+        return const_cast<CTxMemPool*>(this)->mapTx;
+    }
     struct Links {
         setEntries parents, children;
     };
-    void UpdateParent(txiter entry, txiter parent, bool add);
-    void UpdateChild(txiter entry, txiter child, bool add);
-    void UpdateAncestorsOf(bool add, txiter it, setEntries& setAncestors);
-    void UpdateEntryForAncestors(txiter it, const setEntries& setAncestors);
-    void UpdateForRemoveFromMempool(const setEntries& entriesToRemove, bool updateDescendants);
+    void UpdateParent(txiter entry, txiter parent, bool add) EXCLUSIVE_LOCKS_REQUIRED(cs);
+    void UpdateChild(txiter entry, txiter child, bool add) EXCLUSIVE_LOCKS_REQUIRED(cs);
+    void UpdateAncestorsOf(bool add, txiter it, setEntries& setAncestors) EXCLUSIVE_LOCKS_REQUIRED(cs);
+    void UpdateEntryForAncestors(txiter it, const setEntries& setAncestors) EXCLUSIVE_LOCKS_REQUIRED(cs);
+    void UpdateForRemoveFromMempool(const setEntries& entriesToRemove, bool updateDescendants) EXCLUSIVE_LOCKS_REQUIRED(cs);
     void UpdateForDescendants(txiter updateIt, std::map<txiter, setEntries, IterCmp>& cachedDescendants,
-                              const std::set<uint256>& setExclude);
-    void removeUnchecked(txiter entry, MemPoolRemovalReason reason);
-    void trackPackageRemoved(const CFeeRate& rate);
+                              const std::set<uint256>& setExclude) EXCLUSIVE_LOCKS_REQUIRED(cs);
+    void removeUnchecked(txiter entry, MemPoolRemovalReason reason) EXCLUSIVE_LOCKS_REQUIRED(cs);
+    void trackPackageRemoved(const CFeeRate& rate) EXCLUSIVE_LOCKS_REQUIRED(cs);
 
-    std::map<uint256, std::unique_ptr<CTxMemPoolEntry>> mapTx;
-    std::map<txiter, Links, IterCmp> mapLinks;
-    std::map<uint256, std::pair<double, Amount>> mapDeltas;
-    uint64_t totalTxSize = 0;
-    uint64_t cachedInnerUsage = 0;
-    uint64_t cachedLinkUsage = 0; // parents/children set nodes
-    unsigned nTransactionsUpdated = 0;
+    std::map<uint256, std::unique_ptr<CTxMemPoolEntry>> mapTx GUARDED_BY(cs);
+    std::map<txiter, Links, IterCmp> mapLinks GUARDED_BY(cs);
+    std::map<uint256, std::pair<double, Amount>> mapDeltas GUARDED_BY(cs);
+    uint64_t totalTxSize GUARDED_BY(cs) = 0;
+    uint64_t cachedInnerUsage GUARDED_BY(cs) = 0;
+    uint64_t cachedLinkUsage GUARDED_BY(cs) = 0; // parents/children set nodes
+    unsigned nTransactionsUpdated GUARDED_BY(cs) = 0;
     uint32_t nCheckFrequency = 0;
-    mutable int64_t lastRollingFeeUpdate = 0;
-    mutable bool blockSinceLastRollingFeeBump = false;
-    mutable double rollingMinimumFeeRate = 0;
+    mutable int64_t lastRollingFeeUpdate GUARDED_BY(cs) = 0;
+    mutable bool blockSinceLastRollingFeeBump GUARDED_BY(cs) = false;
+    mutable double rollingMinimumFeeRate GUARDED_BY(cs) = 0;
     CBlockPolicyEstimator* minerPolicyEstimator;
     static const int ROLLING_FEE_HALFLIFE = 60 * 60 * 12;
 };

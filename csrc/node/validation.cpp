@@ -150,6 +150,7 @@ void Chainstate::Shutdown() {
 }
 
 CBlockIndex* Chainstate::LookupBlockIndex(const uint256& hash) const {
+    std::lock_guard<CCriticalSection> l(cs_main); // callers outside cs_main too (RPC, net)
     auto it = mapBlockIndex.find(hash);
     return it == mapBlockIndex.end() ? nullptr : it->second;
 }
@@ -1233,15 +1234,7 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
         }
     }
     if (fBlocksDisconnected && mempool) {
-        const int nMemHeight = chainActive.Tip()->nHeight + 1;
-        mempool->removeForReorg(
-            pcoinsTip.get(), (unsigned)nMemHeight, STANDARD_LOCKTIME_VERIFY_FLAGS,
-            [&](const CTransaction& tx, LockPoints& lp, bool validLP) {
-                CValidationState st;
-                if (!ContextualCheckTransactionForCurrentBlock(tx, st, STANDARD_LOCKTIME_VERIFY_FLAGS)) return false;
-                return CheckSequenceLocks(tx, STANDARD_LOCKTIME_VERIFY_FLAGS, &lp, validLP);
-            },
-            [&](const LockPoints* lp) { return TestLockPointValidity(lp); });
+        RemoveForReorgAtTip();
         LimitMempoolSize(gArgs.GetArg("-maxmempool", (int64_t)DEFAULT_MAX_MEMPOOL_SIZE) * 1000000,
                          gArgs.GetArg("-mempoolexpiry", (int64_t)DEFAULT_MEMPOOL_EXPIRY) * 60 * 60);
     }
@@ -1283,7 +1276,7 @@ bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<cons
             uiInterface.NotifyBlockTip(fInitialDownload, pindexNewTip);
         }
     } while (pindexNewTip != pindexMostWork);
-    CheckBlockIndex();
+    CheckBlockIndex(); // (takes cs_main)
     if (!FlushStateToDisk(state, FLUSH_STATE_PERIODIC)) return false;
     return true;
 }
@@ -1316,15 +1309,7 @@ bool Chainstate::InvalidateBlock(CValidationState& state, CBlockIndex* pindex) {
         setDirtyBlockIndex.insert(pindexWalk);
         setBlockIndexCandidates.erase(pindexWalk);
         if (!DisconnectTip(state)) {
-            if (mempool)
-                mempool->removeForReorg(
-                    pcoinsTip.get(), (unsigned)chainActive.Tip()->nHeight + 1, STANDARD_LOCKTIME_VERIFY_FLAGS,
-                    [&](const CTransaction& tx, LockPoints& lp, bool validLP) {
-                        CValidationState st;
-                        if (!ContextualCheckTransactionForCurrentBlock(tx, st, STANDARD_LOCKTIME_VERIFY_FLAGS)) return false;
-                        return CheckSequenceLocks(tx, STANDARD_LOCKTIME_VERIFY_FLAGS, &lp, validLP);
-                    },
-                    [&](const LockPoints* lp) { return TestLockPointValidity(lp); });
+            if (mempool) RemoveForReorgAtTip();
             return false;
         }
     }
@@ -1337,16 +1322,25 @@ bool Chainstate::InvalidateBlock(CValidationState& state, CBlockIndex* pindex) {
             setBlockIndexCandidates.insert(p);
     }
     InvalidChainFound(pindex);
-    if (mempool)
-        mempool->removeForReorg(
-            pcoinsTip.get(), (unsigned)chainActive.Tip()->nHeight + 1, STANDARD_LOCKTIME_VERIFY_FLAGS,
-            [&](const CTransaction& tx, LockPoints& lp, bool validLP) {
-                CValidationState st;
-                if (!ContextualCheckTransactionForCurrentBlock(tx, st, STANDARD_LOCKTIME_VERIFY_FLAGS)) return false;
-                return CheckSequenceLocks(tx, STANDARD_LOCKTIME_VERIFY_FLAGS, &lp, validLP);
-            },
-            [&](const LockPoints* lp) { return TestLockPointValidity(lp); });
+    if (mempool) RemoveForReorgAtTip();
     return true;
+}
+
+// Drop mempool entries whose lock times or sequence locks no longer hold at the (new) tip. The
+// callbacks run inside removeForReorg, still under the caller's cs_main.
+void Chainstate::RemoveForReorgAtTip() {
+    mempool->removeForReorg(
+        pcoinsTip.get(), (unsigned)chainActive.Tip()->nHeight + 1, STANDARD_LOCKTIME_VERIFY_FLAGS,
+        [&](const CTransaction& tx, LockPoints& lp, bool validLP) {
+            AssertLockHeld(cs_main);
+            CValidationState st;
+            if (!ContextualCheckTransactionForCurrentBlock(tx, st, STANDARD_LOCKTIME_VERIFY_FLAGS)) return false;
+            return CheckSequenceLocks(tx, STANDARD_LOCKTIME_VERIFY_FLAGS, &lp, validLP);
+        },
+        [&](const LockPoints* lp) {
+            AssertLockHeld(cs_main);
+            return TestLockPointValidity(lp);
+        });
 }
 
 bool Chainstate::ResetBlockFailureFlags(CBlockIndex* pindex) {
@@ -1387,6 +1381,7 @@ bool Chainstate::IsInitialBlockDownload() const {
 }
 
 CBlockIndex* Chainstate::FindForkInGlobalIndex(const CBlockLocator& locator) const {
+    std::lock_guard<CCriticalSection> l(cs_main);
     for (const uint256& hash : locator.vHave) {
         CBlockIndex* pindex = LookupBlockIndex(hash);
         if (pindex) {
@@ -1433,7 +1428,11 @@ int32_t Chainstate::ComputeBlockVersion(const CBlockIndex* pindexPrev) {
 
 void Chainstate::WaitForBlockChange(int64_t timeoutMillis, const uint256& from) {
     std::unique_lock<CCriticalSection> l(cs_main);
-    auto pred = [&] { return chainActive.Tip() && chainActive.Tip()->GetBlockHash() != from; };
+    AssertLockHeld(cs_main); // (unique_lock is invisible to the thread-safety analysis)
+    auto pred = [&] {
+        AssertLockHeld(cs_main); // evaluated by the wait with `l` held
+        return chainActive.Tip() && chainActive.Tip()->GetBlockHash() != from;
+    };
     if (timeoutMillis <= 0) cvBlockChange.wait(l, pred);
     else cvBlockChange.wait_for(l, std::chrono::milliseconds(timeoutMillis), pred);
 }

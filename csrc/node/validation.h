@@ -132,7 +132,7 @@ public:
     bool ContextualCheckTransaction(const CTransaction& tx, CValidationState& state, int nHeight,
                                     int64_t nLockTimeCutoff) const;
     bool ContextualCheckTransactionForCurrentBlock(const CTransaction& tx, CValidationState& state,
-                                                   int flags = -1) const;
+                                                   int flags = -1) const EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ContextualCheckBlock(const CBlock& block, CValidationState& state, const CBlockIndex* pindexPrev) const;
     uint32_t GetBlockScriptFlags(const CBlockIndex* pindex) const;
     bool IsBCPEnabled(int nHeight) const { return nHeight >= params.GetConsensus().BCPHeight; }
@@ -147,22 +147,32 @@ public:
                             bool* pfMissingInputs, bool fOverrideMempoolLimit = false, Amount nAbsurdFee = 0,
                             int64_t nAcceptTime = 0, Amount* feeOut = nullptr);
     bool CheckSequenceLocks(const CTransaction& tx, int flags, LockPoints* lp = nullptr,
-                            bool useExistingLockPoints = false);
-    bool TestLockPointValidity(const LockPoints* lp) const;
+                            bool useExistingLockPoints = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    bool TestLockPointValidity(const LockPoints* lp) const EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool LoadMempool(const std::string& path);
     bool DumpMempool(const std::string& path);
     void LimitMempoolSize(size_t limit, unsigned long age);
 
     // ---- queries
-    CCriticalSection& cs() const { return cs_main; }
+    CCriticalSection& cs() const RETURN_CAPABILITY(cs_main) { return cs_main; }
     const CChainParams& Params() const { return params; }
-    CChain& ActiveChain() { return chainActive; }
-    const CChain& ActiveChain() const { return chainActive; }
-    CBlockIndex* Tip() const { return chainActive.Tip(); }
-    int Height() const { return chainActive.Height(); }
-    CBlockIndex* BestHeader() const { return pindexBestHeader; }
+    CChain& ActiveChain() EXCLUSIVE_LOCKS_REQUIRED(cs_main) { return chainActive; }
+    const CChain& ActiveChain() const EXCLUSIVE_LOCKS_REQUIRED(cs_main) { return chainActive; }
+    CBlockIndex* Tip() const EXCLUSIVE_LOCKS_REQUIRED(cs_main) { return chainActive.Tip(); }
+    int Height() const EXCLUSIVE_LOCKS_REQUIRED(cs_main) { return chainActive.Height(); }
+    // Tip height for code that does not hold cs_main (takes it; not while holding a mempool lock,
+    // cs_main is always taken first)
+    int HeightNow() const {
+        std::lock_guard<CCriticalSection> l(cs_main);
+        return chainActive.Height();
+    }
+    CBlockIndex* TipNow() const {
+        std::lock_guard<CCriticalSection> l(cs_main);
+        return chainActive.Tip();
+    }
+    CBlockIndex* BestHeader() const EXCLUSIVE_LOCKS_REQUIRED(cs_main) { return pindexBestHeader; }
     CBlockIndex* LookupBlockIndex(const uint256& hash) const;
-    const BlockMap& BlockIndex() const { return mapBlockIndex; }
+    const BlockMap& BlockIndex() const EXCLUSIVE_LOCKS_REQUIRED(cs_main) { return mapBlockIndex; }
     CCoinsViewCache& CoinsTip() { return *pcoinsTip; }
     CCoinsViewDB& CoinsDB() { return *pcoinsdbview; }
     CBlockTreeDB& BlockTree() { return *pblocktree; }
@@ -198,66 +208,68 @@ private:
         std::vector<std::pair<CBlockIndex*, std::shared_ptr<const CBlock>>> blocksConnected;
     };
 
-    CBlockIndex* InsertBlockIndex(const uint256& hash);
-    CBlockIndex* AddToBlockIndex(const CBlockHeader& block);
+    CBlockIndex* InsertBlockIndex(const uint256& hash) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    CBlockIndex* AddToBlockIndex(const CBlockHeader& block) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool AcceptBlockHeader(const CBlockHeader& block, CValidationState& state, CBlockIndex** ppindex,
-                           bool skipPow = false);
+                           bool skipPow = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool AcceptBlock(const std::shared_ptr<const CBlock>& pblock, CValidationState& state, CBlockIndex** ppindex,
-                     bool fRequested, const CDiskBlockPos* dbp, bool* fNewBlock);
+                     bool fRequested, const CDiskBlockPos* dbp, bool* fNewBlock) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ReceivedBlockTransactions(const CBlock& block, CValidationState& state, CBlockIndex* pindexNew,
-                                   const CDiskBlockPos& pos);
+                                   const CDiskBlockPos& pos) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool FindBlockPos(CValidationState& state, CDiskBlockPos& pos, unsigned nAddSize, unsigned nHeight,
-                      uint64_t nTime, bool fKnown = false);
-    bool FindUndoPos(CValidationState& state, int nFile, CDiskBlockPos& pos, unsigned nAddSize);
+                      uint64_t nTime, bool fKnown = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    bool FindUndoPos(CValidationState& state, int nFile, CDiskBlockPos& pos, unsigned nAddSize) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     void FlushBlockFile(bool fFinalize = false);
     bool ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
-                      bool fJustCheck = false);
-    DisconnectResult DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view);
-    bool DisconnectTip(CValidationState& state, bool fBare = false);
+                      bool fJustCheck = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    DisconnectResult DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    bool DisconnectTip(CValidationState& state, bool fBare = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ConnectTip(CValidationState& state, CBlockIndex* pindexNew, const std::shared_ptr<const CBlock>& pblock,
-                    ConnectTrace& trace);
-    CBlockIndex* FindMostWorkChain();
-    void PruneBlockIndexCandidates();
+                    ConnectTrace& trace) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    CBlockIndex* FindMostWorkChain() EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void PruneBlockIndexCandidates() EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ActivateBestChainStep(CValidationState& state, CBlockIndex* pindexMostWork,
-                               const std::shared_ptr<const CBlock>& pblock, bool& fInvalidFound, ConnectTrace& trace);
-    void UpdateTip(CBlockIndex* pindexNew);
-    void InvalidChainFound(CBlockIndex* pindexNew);
-    void InvalidBlockFound(CBlockIndex* pindex, const CValidationState& state);
-    void CheckBlockIndex();
-    bool LoadBlockIndexDB(std::string& err);
-    bool LoadChainTip();
+                               const std::shared_ptr<const CBlock>& pblock, bool& fInvalidFound, ConnectTrace& trace) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void UpdateTip(CBlockIndex* pindexNew) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void InvalidChainFound(CBlockIndex* pindexNew) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void InvalidBlockFound(CBlockIndex* pindex, const CValidationState& state) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void CheckBlockIndex(); // takes cs_main itself
+    bool LoadBlockIndexDB(std::string& err) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    bool LoadChainTip() EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     void NotifyHeaderTip();
     bool CheckIndexAgainstCheckpoint(const CBlockIndex* pindexPrev, CValidationState& state) const;
-    void FindFilesToPrune(std::set<int>& setFilesToPrune, uint64_t nPruneAfterHeight);
-    void FindFilesToPruneManual(std::set<int>& setFilesToPrune, int nManualPruneHeight);
-    void PruneOneBlockFile(int fileNumber);
+    void FindFilesToPrune(std::set<int>& setFilesToPrune, uint64_t nPruneAfterHeight) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void FindFilesToPruneManual(std::set<int>& setFilesToPrune, int nManualPruneHeight) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void PruneOneBlockFile(int fileNumber) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     void UnlinkPrunedFiles(const std::set<int>& setFilesToPrune);
     bool CheckInputs(const CTransaction& tx, CValidationState& state, const CCoinsViewCache& inputs,
-                     bool fScriptChecks, uint32_t flags, bool cacheStore, const PrecomputedTransactionData& txdata);
+                     bool fScriptChecks, uint32_t flags, bool cacheStore, const PrecomputedTransactionData& txdata)
+        EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool AcceptToMemoryPoolWorker(CValidationState& state, const CTransactionRef& ptx, bool fLimitFree,
                                   bool* pfMissingInputs, int64_t nAcceptTime, bool fOverrideMempoolLimit,
-                                  Amount nAbsurdFee, std::vector<COutPoint>& coins_to_uncache, Amount* feeOut);
-    void UpdateMempoolForReorg(const std::vector<CTransactionRef>& disconnected, bool fAddToMempool);
+                                  Amount nAbsurdFee, std::vector<COutPoint>& coins_to_uncache, Amount* feeOut) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void UpdateMempoolForReorg(const std::vector<CTransactionRef>& disconnected, bool fAddToMempool) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
 
     const CChainParams& params;
     ChainstateOptions opts;
     mutable CCriticalSection cs_main{"cs_main"};
     std::condition_variable_any cvBlockChange;
 
-    BlockMap mapBlockIndex;
+    BlockMap mapBlockIndex GUARDED_BY(cs_main);
     std::vector<std::unique_ptr<CBlockIndex>> blockIndexStorage;
     std::vector<std::unique_ptr<uint256>> hashStorage;
-    CChain chainActive;
-    CBlockIndex* pindexBestHeader = nullptr;
+    CChain chainActive GUARDED_BY(cs_main);
+    CBlockIndex* pindexBestHeader GUARDED_BY(cs_main) = nullptr;
     CBlockIndex* pindexBestInvalid = nullptr;
-    void CheckForkWarningConditions();
-    void CheckForkWarningConditionsOnNewFork(CBlockIndex* pindexNewForkTip);
+    void CheckForkWarningConditions() EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void CheckForkWarningConditionsOnNewFork(CBlockIndex* pindexNewForkTip) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void RemoveForReorgAtTip() EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     CBlockIndex* pindexBestForkTip = nullptr;
     CBlockIndex* pindexBestForkBase = nullptr;
-    std::set<CBlockIndex*, WorkComparator> setBlockIndexCandidates;
-    std::multimap<CBlockIndex*, CBlockIndex*> mapBlocksUnlinked;
-    std::set<CBlockIndex*> setDirtyBlockIndex;
-    std::set<int> setDirtyFileInfo;
+    std::set<CBlockIndex*, WorkComparator> setBlockIndexCandidates GUARDED_BY(cs_main);
+    std::multimap<CBlockIndex*, CBlockIndex*> mapBlocksUnlinked GUARDED_BY(cs_main);
+    std::set<CBlockIndex*> setDirtyBlockIndex GUARDED_BY(cs_main);
+    std::set<int> setDirtyFileInfo GUARDED_BY(cs_main);
     std::vector<CBlockFileInfo> vinfoBlockFile;
     int nLastBlockFile = 0;
     int32_t nBlockSequenceId = 1;

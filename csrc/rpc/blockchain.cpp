@@ -26,6 +26,7 @@ double GetDifficulty(const CBlockIndex* blockindex) {
 
 UniValue blockheaderToJSON(const CBlockIndex* blockindex) {
     Chainstate& cs = *Node().chainstate;
+    std::lock_guard<CCriticalSection> l(cs.cs()); // confirmations / next block read the active chain
     UniValue result(UniValue::VOBJ);
     result.pushKV("hash", blockindex->GetBlockHash().GetHex());
     int confirmations = -1;
@@ -50,6 +51,7 @@ UniValue blockheaderToJSON(const CBlockIndex* blockindex) {
 
 UniValue blockToJSON(const CBlock& block, const CBlockIndex* blockindex, bool txDetails) {
     Chainstate& cs = *Node().chainstate;
+    std::lock_guard<CCriticalSection> l(cs.cs());
     const CChainParams& params = cs.Params();
     UniValue result(UniValue::VOBJ);
     result.pushKV("hash", blockindex->GetBlockHash().GetHex());
@@ -172,7 +174,7 @@ static UniValue getchaintips(const JSONRPCRequest& req) {
     return res;
 }
 
-static UniValue BIP9SoftForkDesc(Chainstate& cs, Consensus::DeploymentPos id) {
+static UniValue BIP9SoftForkDesc(Chainstate& cs, Consensus::DeploymentPos id) EXCLUSIVE_LOCKS_REQUIRED(cs.cs()) {
     UniValue rv(UniValue::VOBJ);
     const ThresholdState st = cs.DeploymentState(cs.Tip(), id);
     rv.pushKV("status", ThresholdStateName(st));
@@ -259,10 +261,11 @@ UniValue mempoolToJSON(bool fVerbose) {
     NodeContext& n = Node();
     CTxMemPool& pool = *n.mempool;
     if (fVerbose) {
+        const int height = n.chainstate->HeightNow(); // before the mempool lock: cs_main comes first
         std::lock_guard<CCriticalSection> l(pool.cs);
         UniValue o(UniValue::VOBJ);
         for (const CTxMemPoolEntry* e : pool.SortedByDepthAndScore())
-            o.pushKV(e->GetTx().GetHash().ToString(), entryToJSON(*e, pool, n.chainstate->Height()));
+            o.pushKV(e->GetTx().GetHash().ToString(), entryToJSON(*e, pool, height));
         return o;
     }
     std::vector<uint256> vtxid;
@@ -290,7 +293,8 @@ static UniValue mempoolRelatives(const JSONRPCRequest& req, bool ancestors) {
         return o;
     }
     UniValue o(UniValue::VOBJ);
-    for (const auto* e : rel) o.pushKV(e->GetTx().GetHash().ToString(), entryToJSON(*e, *n.mempool, n.chainstate->Height()));
+    const int height = n.chainstate->HeightNow();
+    for (const auto* e : rel) o.pushKV(e->GetTx().GetHash().ToString(), entryToJSON(*e, *n.mempool, height));
     return o;
 }
 static UniValue getmempoolancestors(const JSONRPCRequest& req) { return mempoolRelatives(req, true); }
@@ -299,10 +303,11 @@ static UniValue getmempooldescendants(const JSONRPCRequest& req) { return mempoo
 static UniValue getmempoolentry(const JSONRPCRequest& req) {
     NodeContext& n = Node();
     const uint256 hash = ParseHashV(req.params[0], "parameter 1");
+    const int height = n.chainstate->HeightNow();
     std::lock_guard<CCriticalSection> l(n.mempool->cs);
     const CTxMemPoolEntry* e = n.mempool->GetEntry(hash);
     if (!e) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Transaction not in mempool");
-    return entryToJSON(*e, *n.mempool, n.chainstate->Height());
+    return entryToJSON(*e, *n.mempool, height);
 }
 
 UniValue mempoolInfoToJSON() {
@@ -478,8 +483,10 @@ static UniValue waitforblockimpl(const JSONRPCRequest& req, const uint256* targe
     if (req.params.size() > idx && !req.params[idx].isNull()) timeout = req.params[idx].get_int();
     const int64_t deadline = GetTimeMillis() + timeout;
     std::unique_lock<CCriticalSection> l(cs.cs());
+    AssertLockHeld(cs.cs()); // (unique_lock is invisible to the thread-safety analysis)
     const uint256 start = cs.Tip()->GetBlockHash();
     auto done = [&] {
+        AssertLockHeld(cs.cs()); // evaluated with `l` held
         if (ShutdownRequested()) return true;
         if (target) return cs.Tip()->GetBlockHash() == *target;
         if (targetHeight >= 0) return cs.Height() >= targetHeight;

@@ -27,6 +27,7 @@ double GetDifficulty(const CBlockIndex* blockindex);
 
 static UniValue GetNetworkHashPS(int lookup, int height) {
     Chainstate& cs = *Node().chainstate;
+    std::lock_guard<CCriticalSection> l(cs.cs());
     CBlockIndex* pb = cs.Tip();
     if (height >= 0 && height < cs.Height()) pb = cs.ActiveChain()[height];
     if (pb == nullptr || !pb->nHeight) return 0;
@@ -182,11 +183,12 @@ static UniValue getblocktemplate(const JSONRPCRequest& req) {
             hashWatchedChain.SetHex(lpstr.substr(0, 64));
             nTransactionsUpdatedLastLP = (unsigned)atoi64(lpstr.substr(64));
         } else {
-            hashWatchedChain = cs.Tip()->GetBlockHash();
+            hashWatchedChain = cs.TipNow()->GetBlockHash();
             nTransactionsUpdatedLastLP = nTransactionsUpdatedLast;
         }
         int64_t checktxtime = GetTimeMillis() + 60000;
         std::unique_lock<CCriticalSection> l(cs.cs());
+        AssertLockHeld(cs.cs()); // (unique_lock is invisible to the thread-safety analysis)
         while (cs.Tip()->GetBlockHash() == hashWatchedChain && !ShutdownRequested()) {
             cs.BlockChangeCV().wait_for(l, std::chrono::milliseconds(1000));
             if (GetTimeMillis() > checktxtime) {

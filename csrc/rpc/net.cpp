@@ -42,7 +42,7 @@ static UniValue getpeerinfo(const JSONRPCRequest& req) {
         obj.pushKV("id", (int64_t)s.nodeid);
         obj.pushKV("addr", s.addrName);
         if (!s.addrLocal.empty()) obj.pushKV("addrlocal", s.addrLocal);
-        obj.pushKV("services", strprintf("%016x", (unsigned long long)s.nServices));
+        obj.pushKV("services", strprintf("%016llx", (unsigned long long)s.nServices));
         obj.pushKV("relaytxes", s.fRelayTxes);
         obj.pushKV("lastsend", s.nLastSend);
         obj.pushKV("lastrecv", s.nLastRecv);
@@ -162,7 +162,7 @@ static UniValue getnetworkinfo(const JSONRPCRequest& req) {
     obj.pushKV("version", CLIENT_VERSION);
     obj.pushKV("subversion", UserAgent(maxBlock));
     obj.pushKV("protocolversion", PROTOCOL_VERSION);
-    if (c) obj.pushKV("localservices", strprintf("%016x", (unsigned long long)c->GetLocalServices()));
+    if (c) obj.pushKV("localservices", strprintf("%016llx", (unsigned long long)c->GetLocalServices()));
     obj.pushKV("localrelay", !gArgs.GetBoolArg("-blocksonly", false));
     obj.pushKV("timeoffset", GetTimeOffset());
     if (c) {

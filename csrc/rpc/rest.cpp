@@ -144,8 +144,12 @@ static bool rest_getutxos(const HTTPRequest& req, HTTPReply& rep, const std::str
     std::vector<unsigned char> bitmap((vOutPoints.size() + 7) / 8);
     std::vector<Coin> outs;
     std::string bitmapStringRepresentation;
+    int chainHeight; // the tip the lookups were made against (same cs_main scope)
+    uint256 tipHash;
     {
         std::lock_guard<CCriticalSection> l(cs.cs());
+        chainHeight = cs.Height();
+        tipHash = cs.Tip()->GetBlockHash();
         std::lock_guard<CCriticalSection> lm(n->mempool->cs);
         CCoinsViewMemPool viewMempool(&cs.CoinsTip(), *n->mempool);
         CCoinsView& view = fCheckMemPool ? static_cast<CCoinsView&>(viewMempool) : static_cast<CCoinsView&>(cs.CoinsTip());
@@ -163,13 +167,13 @@ static bool rest_getutxos(const HTTPRequest& req, HTTPReply& rep, const std::str
     std::vector<unsigned char> bin;
     {
         VectorWriter w(bin);
-        w << (int32_t)cs.Height() << cs.Tip()->GetBlockHash() << bitmap;
+        w << (int32_t)chainHeight << tipHash << bitmap;
         WriteCompactSize(w, outs.size());
         for (const Coin& c : outs) w << (uint32_t)c.nHeight << c.out;
     }
     UniValue objGetUTXOResponse(UniValue::VOBJ);
-    objGetUTXOResponse.pushKV("chainHeight", cs.Height());
-    objGetUTXOResponse.pushKV("chaintipHash", cs.Tip()->GetBlockHash().GetHex());
+    objGetUTXOResponse.pushKV("chainHeight", chainHeight);
+    objGetUTXOResponse.pushKV("chaintipHash", tipHash.GetHex());
     objGetUTXOResponse.pushKV("bitmap", bitmapStringRepresentation);
     UniValue utxos(UniValue::VARR);
     for (const Coin& c : outs) {

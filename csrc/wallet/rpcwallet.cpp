@@ -390,7 +390,7 @@ static Amount ReceivedByDests(CWallet& w, const std::set<CScript>& scripts, int 
     WalletLock l(w);
     for (const auto& kv : w.mapWallet) {
         const CWalletTx& wtx = kv.second;
-        if (wtx.IsCoinBase() || !IsFinalTx(*wtx.tx, GetNode()->chainstate->Height() + 1, GetAdjustedTime())) continue;
+        if (wtx.IsCoinBase() || !IsFinalTx(*wtx.tx, GetNode()->chainstate->HeightNow() + 1, GetAdjustedTime())) continue;
         for (const CTxOut& o : wtx.tx->vout)
             if (scripts.count(o.scriptPubKey) && wtx.GetDepthInMainChain() >= nMinDepth) n += o.nValue;
     }
@@ -436,7 +436,7 @@ static UniValue ListReceived(CWallet& w, const UniValue& params, bool fByAccount
     std::map<CTxDestination, Tally> mapTally;
     for (const auto& kv : w.mapWallet) {
         const CWalletTx& wtx = kv.second;
-        if (wtx.IsCoinBase() || !IsFinalTx(*wtx.tx, GetNode()->chainstate->Height() + 1, GetAdjustedTime())) continue;
+        if (wtx.IsCoinBase() || !IsFinalTx(*wtx.tx, GetNode()->chainstate->HeightNow() + 1, GetAdjustedTime())) continue;
         const int nDepth = wtx.GetDepthInMainChain();
         if (nDepth < nMinDepth) continue;
         for (const CTxOut& o : wtx.tx->vout) {

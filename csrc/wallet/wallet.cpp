@@ -122,7 +122,7 @@ int CWalletTx::GetBlocksToMaturity() const {
 bool CWalletTx::InMempool() const { return pwallet && pwallet->mempool && pwallet->mempool->exists(GetHash()); }
 
 bool CWalletTx::IsTrusted() const {
-    if (!IsFinalTx(*tx, pwallet && pwallet->chainstate ? pwallet->chainstate->Height() + 1 : 0, GetAdjustedTime()))
+    if (!IsFinalTx(*tx, pwallet && pwallet->chainstate ? pwallet->chainstate->HeightNow() + 1 : 0, GetAdjustedTime()))
         return false;
     const int depth = GetDepthInMainChain();
     if (depth >= 1) return true;
@@ -1033,7 +1033,7 @@ Amount CWallet::GetAccountBalance(const std::string& strAccount, int nMinDepth, 
     Amount nBalance = 0;
     for (const auto& kv : mapWallet) {
         const CWalletTx& wtx = kv.second;
-        if (!IsFinalTx(*wtx.tx, chainstate ? chainstate->Height() + 1 : 0, GetAdjustedTime()) ||
+        if (!IsFinalTx(*wtx.tx, chainstate ? chainstate->HeightNow() + 1 : 0, GetAdjustedTime()) ||
             wtx.GetBlocksToMaturity() > 0 || wtx.GetDepthInMainChain() < 0)
             continue;
         std::list<COutputEntry> received, sent;
@@ -1151,7 +1151,7 @@ void CWallet::AvailableCoins(std::vector<COutput>& vCoins, bool fOnlyConfirmed, 
                              bool fIncludeZeroValue) const {
     vCoins.clear();
     WalletLock l(*this);
-    const int height = chainstate ? chainstate->Height() : 0;
+    const int height = chainstate ? chainstate->HeightNow() : 0; // (WalletLock holds cs_main already)
     for (const auto& kv : mapWallet) {
         const CWalletTx& wtx = kv.second;
         if (!IsFinalTx(*wtx.tx, height + 1, GetAdjustedTime())) continue;

@@ -142,8 +142,8 @@ static bool LoadOneWallet(NodeContext& node, const std::string& name, std::strin
     }
     GetMainSignals().Register(w.get());
     uiInterface.LoadWallet(w.get());
-    if (start && start != cs.Tip()) {
-        LogPrintf("Rescanning last %i blocks (from block %i)...\n", cs.Height() - start->nHeight, start->nHeight);
+    if (start && start != cs.TipNow()) {
+        LogPrintf("Rescanning last %i blocks (from block %i)...\n", cs.HeightNow() - start->nHeight, start->nHeight);
         w->ScanForWalletTransactions(start, true);
         std::lock_guard<CCriticalSection> l(cs.cs());
         w->SetBestChain(cs.ActiveChain().GetLocator());
