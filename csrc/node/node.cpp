@@ -29,6 +29,7 @@ std::unique_ptr<NodeContext> BuildNode(const std::string& chain, const std::stri
     o.coinsCacheBytes = (size_t)gArgs.GetArg("-dbcache", (int64_t)450) << 20;
     o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)0);
     o.maxTipAge = gArgs.GetArg("-maxtipage", DEFAULT_MAX_TIP_AGE);
+    o.connectPipeline = (int)gArgs.GetArg("-connectpipeline", (int64_t)o.connectPipeline);
     const int64_t prune = gArgs.GetArg("-prune", (int64_t)0);
     if (prune > 1) o.pruneTarget = (uint64_t)prune * 1024 * 1024;
     if (gArgs.IsArgSet("-assumevalid")) o.assumeValid = uint256S(gArgs.GetArg("-assumevalid", ""));

@@ -48,6 +48,9 @@ void ResetGpuSigFailures() {
     g_gpuDisabled = false;
 }
 bool GpuSigPathDisabled() { return g_gpuDisabled.load(); }
+bool GpuBatchesExpected(bool useGpu) {
+    return useGpu && !g_gpuDisabled.load() && (GpuFaultInjection() || gpu::GpuAvailable());
+}
 
 static std::mutex g_statsMutex;
 static SigVerifyStats g_stats;
@@ -111,7 +114,20 @@ std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*
 
 bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* pool, bool useGpu, bool cacheStore,
                            bool cacheErase) {
-    if (checks.empty()) return true;
+    static const std::vector<DeferredMultisig> none;
+    return BatchVerifySignatures(checks, none, pool, useGpu, cacheStore, cacheErase);
+}
+
+bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, const std::vector<DeferredMultisig>& groups,
+                           WorkerPool* pool, bool useGpu, bool cacheStore, bool cacheErase) {
+    if (checks.empty()) return groups.empty();
+    // speculative pairs of deferred multisig groups: their individual results are kept, and a false
+    // one does not fail the batch
+    std::vector<uint8_t> spec(checks.size(), 0), res(checks.size(), 0);
+    for (const DeferredMultisig& g : groups) {
+        if ((size_t)g.first + g.Pairs() > checks.size()) return false; // malformed group: never valid
+        std::fill(spec.begin() + g.first, spec.begin() + g.first + g.Pairs(), 1);
+    }
     SignatureCache& cache = GetSignatureCache();
     std::vector<uint256> entries(checks.size());
     std::vector<uint8_t> hit(checks.size());
@@ -128,8 +144,12 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
     else
         for (size_t i = 0; i < checks.size(); i++) probe(i);
     for (size_t i = 0; i < checks.size(); i++) {
-        if (hit[i]) hits++;
-        else todo.push_back(i);
+        if (hit[i]) {
+            hits++;
+            res[i] = 1;
+        } else {
+            todo.push_back(i);
+        }
     }
     bool ok = true;
     const size_t n = todo.size();
@@ -140,9 +160,9 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
         if (gpu) {
             std::vector<const DeferredSigCheck*> ptrs(n);
             for (size_t j = 0; j < n; j++) ptrs[j] = &checks[todo[j]];
-            std::vector<uint8_t> res;
+            std::vector<uint8_t> r;
             try {
-                res = GpuVerifyDeferred(ptrs, pool);
+                r = GpuVerifyDeferred(ptrs, pool);
                 g_gpuFailures = 0;
             } catch (const std::exception& e) {
                 const int fails = ++g_gpuFailures;
@@ -156,8 +176,12 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
             }
             if (gpu) {
                 for (size_t j = 0; j < n; j++) {
-                    if (!res[j]) ok = false;
-                    else if (cacheStore) cache.Set(entries[todo[j]]);
+                    res[todo[j]] = r[j];
+                    if (!r[j]) {
+                        if (!spec[todo[j]]) ok = false;
+                    } else if (cacheStore) {
+                        cache.Set(entries[todo[j]]);
+                    }
                 }
                 std::lock_guard<std::mutex> l(g_statsMutex);
                 g_stats.gpu_batches++;
@@ -169,12 +193,15 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
             std::atomic<bool> allOk{true};
             auto work = [&](size_t j) {
                 if (!allOk.load(std::memory_order_relaxed)) return;
-                const DeferredSigCheck& c = checks[todo[j]];
-                if (!secp::VerifySignature(c.pubkey.data(), c.pubkey.size(), c.sig.data(), c.sig.size(),
-                                           c.sighash.begin()))
-                    allOk = false;
-                else if (cacheStore)
-                    cache.Set(entries[todo[j]]);
+                const size_t i = todo[j];
+                const DeferredSigCheck& c = checks[i];
+                res[i] = secp::VerifySignature(c.pubkey.data(), c.pubkey.size(), c.sig.data(), c.sig.size(),
+                                               c.sighash.begin());
+                if (!res[i]) {
+                    if (!spec[i]) allOk = false;
+                } else if (cacheStore) {
+                    cache.Set(entries[i]);
+                }
             };
             if (pool) pool->ParallelFor(n, work, 8);
             else for (size_t j = 0; j < n; j++) work(j);
@@ -184,8 +211,15 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
             g_stats.cpu_ms += (GetTimeMicros() - t0) / 1000.0;
         }
     }
+    if (ok)
+        for (const DeferredMultisig& g : groups)
+            if (!EvalDeferredMultisig(g, &res[g.first])) {
+                ok = false;
+                break;
+            }
     std::lock_guard<std::mutex> l(g_statsMutex);
     g_stats.cache_hits += hits;
+    g_stats.multisig_groups += groups.size();
     return ok;
 }
 

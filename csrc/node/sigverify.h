@@ -44,6 +44,7 @@ size_t InitSignatureCache(int64_t mib);
 
 struct SigVerifyStats {
     uint64_t gpu_batches = 0, gpu_sigs = 0, cpu_sigs = 0, cache_hits = 0, gpu_failures = 0;
+    uint64_t multisig_groups = 0; // CHECKMULTISIGs verified through the batch (speculative pairs)
     double gpu_ms = 0, cpu_ms = 0;
 };
 
@@ -58,12 +59,19 @@ static const int MAX_GPU_SIG_FAILURES = 3;
 // successes (mempool acceptance); block validation erases consumed entries.
 bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* pool, bool useGpu, bool cacheStore,
                            bool cacheErase);
+// Same, with deferred CHECKMULTISIG groups: their pair checks are speculative (a false pair is
+// legal), and each group must pass its replayed greedy match instead.
+bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, const std::vector<DeferredMultisig>& groups,
+                           WorkerPool* pool, bool useGpu, bool cacheStore, bool cacheErase);
 // Device verification of the given checks (no cache); result[i] = 1 iff valid.
 std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool);
 void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path
 size_t GetGpuSigThreshold();
 void ResetGpuSigFailures();
 bool GpuSigPathDisabled();
+// Whether large batches would go to the GPU: CHECKMULTISIG is deferred speculatively (more pairs
+// than the eager match checks) only then; a CPU-only node keeps the eager match on its workers.
+bool GpuBatchesExpected(bool useGpu);
 SigVerifyStats GetSigVerifyStats();
 
 // TransactionSignatureChecker that consults/updates the signature cache.

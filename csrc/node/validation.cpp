@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <thread>
 #include <deque>
+#include <future>
 #include <unistd.h>
 #include <cassert>
 #include <cmath>
@@ -81,8 +82,8 @@ namespace {
 class BlockSigChecker : public DeferringSignatureChecker {
 public:
     BlockSigChecker(const CTransaction* tx, unsigned nIn, Amount amount, const PrecomputedTransactionData* txdata,
-                    std::vector<DeferredSigCheck>* sink)
-        : DeferringSignatureChecker(tx, nIn, amount, txdata, sink) {}
+                    std::vector<DeferredSigCheck>* sink, std::vector<DeferredMultisig>* groups)
+        : DeferringSignatureChecker(tx, nIn, amount, txdata, sink, groups) {}
 
 protected:
     bool VerifySignature(const std::vector<unsigned char>& sig, const std::vector<unsigned char>& pubkey,
@@ -670,9 +671,33 @@ bool Chainstate::CheckInputs(const CTransaction& tx, CValidationState& state, co
     return true;
 }
 
+struct Chainstate::PendingConnect {
+    CBlockIndex* pindex = nullptr;
+    bool genesis = false, postfork = false;
+    size_t nJobs = 0;               // script jobs run for this block
+    bool sigsOk = true;             // verdict when the batch ran synchronously (or scripts failed)
+    std::future<bool> sigs;         // verdict of an asynchronous batch
+    CBlockUndo blockundo;
+    std::vector<std::pair<uint256, CDiskTxPos>> vPos;
+    int64_t nTimeStart = 0, nTime2 = 0;
+    int nInputs = 0;
+};
+
 bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
                               bool fJustCheck) {
+    PendingConnect p;
+    return ConnectBlockPrepare(block, state, pindex, view, fJustCheck, false, p) && ConnectBlockFinish(p, state, fJustCheck);
+}
+
+// Phase 1 of connecting a block: every consensus check that needs the UTXO view, the script
+// runs (ECDSA deferred), and the block's signature batch started - synchronously, or (`async`)
+// on a helper thread so the caller can go on with the next block. The view is fully updated
+// (best block included) when this returns; the block is valid only once Finish agrees.
+bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& state, CBlockIndex* pindex,
+                                     CCoinsViewCache& view, bool fJustCheck, bool async, PendingConnect& p) {
     const int64_t nTimeStart = GetTimeMicros();
+    p.pindex = pindex;
+    p.nTimeStart = nTimeStart;
     const Consensus::Params& cp = params.GetConsensus();
     if (!CheckBlock(block, state, !fJustCheck, !fJustCheck))
         return error("%s: Consensus::CheckBlock: %s", __func__, FormatStateMessage(state).c_str());
@@ -680,6 +705,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     if (hashPrevBlock != view.GetBestBlock()) return state.Error("ConnectBlock: view best block mismatch");
     if (block.GetHash(cp) == cp.hashGenesisBlock) {
         if (!fJustCheck) view.SetBestBlock(pindex->GetBlockHash());
+        p.genesis = true;
         return true;
     }
     bool fScriptChecks = true;
@@ -714,7 +740,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     const uint32_t flags = GetBlockScriptFlags(pindex);
     const bool postfork = IsBCPEnabled(pindex->nHeight);
 
-    CBlockUndo blockundo;
+    CBlockUndo& blockundo = p.blockundo;
     std::vector<int> prevheights;
     Amount nFees = 0;
     int nInputs = 0;
@@ -722,7 +748,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     const uint64_t currentBlockSize = GetSerializeSize(block, PROTOCOL_VERSION);
     const uint64_t nMaxSigOpsCount = GetMaxBlockSigOpsCount(currentBlockSize);
     CDiskTxPos pos(pindex->GetBlockPos(), GetSizeOfCompactSize(block.vtx.size()));
-    std::vector<std::pair<uint256, CDiskTxPos>> vPos;
+    std::vector<std::pair<uint256, CDiskTxPos>>& vPos = p.vPos;
     vPos.reserve(block.vtx.size());
     blockundo.vtxundo.reserve(block.vtx.size() - 1);
     const size_t ntx = block.vtx.size();
@@ -753,6 +779,8 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     // for the batch verifier. Nothing in the UTXO loop may wait on the queue's threads.
     std::vector<ScriptJob> jobs(maxJobs);
     std::vector<std::vector<DeferredSigCheck>> sinks(maxJobs);
+    std::vector<std::vector<DeferredMultisig>> groupSinks(maxJobs); // deferred CHECKMULTISIGs per job
+    const bool deferMultisig = GpuBatchesExpected(opts.useGpu);
     std::atomic<bool> anyFail{false};
     size_t nProduced = 0;
     const bool queued = fScriptChecks && maxJobs > 0;
@@ -760,7 +788,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
         scriptQueue->Begin([&](size_t k) {
             if (anyFail.load(std::memory_order_relaxed)) return;
             const ScriptJob& J = jobs[k];
-            BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k]);
+            BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k], deferMultisig ? &groupSinks[k] : nullptr);
             ScriptError err;
             if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, J.scriptPubKey, flags, checker, &err)) anyFail = true;
         });
@@ -832,24 +860,58 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     // ---- remaining scripts, then one ECDSA batch (GPU when large enough)
     scriptQueue->Complete();
     const size_t nJobs = nProduced;
+    p.nJobs = nJobs;
+    p.postfork = postfork;
+    p.nInputs = nInputs;
+    p.nTime2 = nTime2;
     if (nJobs > 0) {
         bool ok = !anyFail.load();
         if (ok) {
             size_t total = 0;
             for (size_t k = 0; k < nJobs; k++) total += sinks[k].size();
             std::vector<DeferredSigCheck> all;
+            std::vector<DeferredMultisig> groups;
             all.reserve(total);
-            for (size_t k = 0; k < nJobs; k++)
+            for (size_t k = 0; k < nJobs; k++) {
+                for (DeferredMultisig g : groupSinks[k]) { // rebase onto the concatenated batch
+                    g.first += (uint32_t)all.size();
+                    groups.push_back(g);
+                }
                 for (auto& c : sinks[k]) all.push_back(std::move(c));
-            ok = BatchVerifySignatures(all, pool.get(), opts.useGpu, false, !fJustCheck);
+            }
+            if (async) {
+                // the batch owns its checks; the pool is shared (ParallelFor calls serialise)
+                WorkerPool* wp = pool.get();
+                const bool useGpu = opts.useGpu, erase = !fJustCheck;
+                p.sigs = std::async(std::launch::async,
+                                    [wp, useGpu, erase, all = std::move(all), groups = std::move(groups)]() mutable {
+                                        return BatchVerifySignatures(all, groups, wp, useGpu, false, erase);
+                                    });
+            } else {
+                ok = BatchVerifySignatures(all, groups, pool.get(), opts.useGpu, false, !fJustCheck);
+            }
         }
-        // Before the fork script failures do not invalidate blocks (reference validation.cpp:2121-2126).
-        if (!ok && postfork)
-            return state.DoS(100, false, REJECT_INVALID, "blk-bad-inputs", false, "parallel script check failed");
+        p.sigsOk = ok;
     }
+    // the next block of a pipeline layers its view on this one
+    if (!fJustCheck) view.SetBestBlock(pindex->GetBlockHash());
+    return true;
+}
+
+// Phase 2: wait for the signature verdict, then record the block as script-valid (undo data,
+// index status, tx index). On failure nothing of the block has been committed.
+bool Chainstate::ConnectBlockFinish(PendingConnect& p, CValidationState& state, bool fJustCheck) {
+    if (p.genesis) return true;
+    CBlockIndex* pindex = p.pindex;
+    const CBlockUndo& blockundo = p.blockundo;
+    bool ok = p.sigsOk;
+    if (p.sigs.valid()) ok = p.sigs.get() && ok;
+    // Before the fork script failures do not invalidate blocks (reference validation.cpp:2121-2126).
+    if (p.nJobs > 0 && !ok && p.postfork)
+        return state.DoS(100, false, REJECT_INVALID, "blk-bad-inputs", false, "parallel script check failed");
     const int64_t nTime4 = GetTimeMicros();
-    LogPrint(BCLog::BENCH, "    - Connect %u txs (%d inputs, %zu script jobs): %.2fms, verify %.2fms\n",
-             (unsigned)block.vtx.size(), nInputs, nJobs, 0.001 * (nTime2 - nTimeStart), 0.001 * (nTime4 - nTime2));
+    LogPrint(BCLog::BENCH, "    - Connect %d inputs (%zu script jobs): %.2fms, verify %.2fms\n", p.nInputs, p.nJobs,
+             0.001 * (p.nTime2 - p.nTimeStart), 0.001 * (nTime4 - p.nTime2));
     if (fJustCheck) return true;
 
     if (pindex->GetUndoPos().IsNull() || !pindex->IsValid(BLOCK_VALID_SCRIPTS)) {
@@ -865,9 +927,8 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
         pindex->RaiseValidity(BLOCK_VALID_SCRIPTS);
         setDirtyBlockIndex.insert(pindex);
     }
-    if (opts.txindex && !pblocktree->WriteTxIndex(vPos)) return state.Error("Failed to write transaction index");
-    view.SetBestBlock(pindex->GetBlockHash());
-    nLastConnectMicros = GetTimeMicros() - nTimeStart;
+    if (opts.txindex && !pblocktree->WriteTxIndex(p.vPos)) return state.Error("Failed to write transaction index");
+    nLastConnectMicros = GetTimeMicros() - p.nTimeStart;
     return true;
 }
 
@@ -1087,6 +1148,90 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
     return true;
 }
 
+// Cross-block pipeline (SURVEY §2.3 PP; the reference connects strictly one block at a time,
+// src/validation.cpp:2698-2746): block N+1's UTXO pass and script runs (CPU) overlap block N's
+// ECDSA batch (GPU). Each block gets a view layered on the previous block's; a block is
+// committed - view flushed into the coins tip, undo written, tip advanced - only after its own
+// verdict, in order. A failed verdict discards that block's view and every later one, exactly
+// as if the blocks had been connected one by one and the failing one had been rejected.
+bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector<CBlockIndex*>& chain,
+                                      const std::shared_ptr<const CBlock>& pblock, ConnectTrace& trace) {
+    struct Stage {
+        CBlockIndex* pindex;
+        std::shared_ptr<const CBlock> block;
+        std::unique_ptr<CCoinsViewCache> view;
+        std::unique_ptr<PendingConnect> p;
+    };
+    std::deque<Stage> inflight;
+    const size_t depth = (size_t)std::max(2, opts.connectPipeline);
+    LogPrint(BCLog::BENCH, "ConnectTipsPipelined: %u blocks, up to %u in flight\n", (unsigned)chain.size(), (unsigned)depth);
+    // the oldest in-flight block: verdict, then commit (or discard it and everything after it)
+    auto commitFront = [&]() -> bool {
+        AssertLockHeld(cs_main); // runs inside this function's cs_main scope
+        Stage& s = inflight.front();
+        const bool rv = ConnectBlockFinish(*s.p, state, false);
+        GetMainSignals().BlockChecked(*s.block, state);
+        if (!rv) {
+            if (state.IsInvalid()) InvalidBlockFound(s.pindex, state);
+            for (size_t k = 0; k < inflight.size(); k++) trace.blocksConnected.pop_back();
+            // later stages' batches may still run: their results are dropped with them
+            inflight.clear();
+            return error("ConnectTipsPipelined(): block %s failed (%s)", s.pindex->GetBlockHash().ToString().c_str(),
+                         FormatStateMessage(state).c_str());
+        }
+        s.view->Flush(); // into the coins tip: everything older is committed already
+        if (inflight.size() > 1) inflight[1].view->SetBackend(*pcoinsTip);
+        if (mempool) mempool->removeForBlock(s.block->vtx, s.pindex->nHeight);
+        UpdateTip(s.pindex);
+        inflight.pop_front();
+        CValidationState fs;
+        if (!FlushStateToDisk(fs, FLUSH_STATE_IF_NEEDED)) {
+            state = fs;
+            for (size_t k = 0; k < inflight.size(); k++) trace.blocksConnected.pop_back();
+            inflight.clear();
+            return false;
+        }
+        return true;
+    };
+    for (CBlockIndex* pindex : chain) {
+        Stage st;
+        st.pindex = pindex;
+        if (pblock && pblock->GetHash(params.GetConsensus()) == pindex->GetBlockHash()) {
+            st.block = pblock;
+        } else {
+            auto b = std::make_shared<CBlock>();
+            if (!ReadBlockFromDisk(*b, pindex, params)) {
+                while (!inflight.empty())
+                    if (!commitFront()) return false;
+                return state.Error("Failed to read block");
+            }
+            st.block = b;
+        }
+        CCoinsView* base = inflight.empty() ? static_cast<CCoinsView*>(pcoinsTip.get()) : inflight.back().view.get();
+        st.view.reset(new CCoinsViewCache(base));
+        st.p.reset(new PendingConnect());
+        trace.blocksConnected.emplace_back(pindex, st.block);
+        if (!ConnectBlockPrepare(*st.block, state, pindex, *st.view, false, true, *st.p)) {
+            // the blocks before it may still be valid: settle them first (in order)
+            CValidationState failed = state;
+            state = CValidationState();
+            trace.blocksConnected.pop_back();
+            while (!inflight.empty())
+                if (!commitFront()) return false;
+            state = failed;
+            GetMainSignals().BlockChecked(*st.block, state);
+            if (state.IsInvalid()) InvalidBlockFound(pindex, state);
+            return error("ConnectTipsPipelined(): ConnectBlock %s failed (%s)", pindex->GetBlockHash().ToString().c_str(),
+                         FormatStateMessage(state).c_str());
+        }
+        inflight.push_back(std::move(st));
+        if (inflight.size() >= depth && !commitFront()) return false;
+    }
+    while (!inflight.empty())
+        if (!commitFront()) return false;
+    return true;
+}
+
 CBlockIndex* Chainstate::FindMostWorkChain() {
     while (true) {
         if (setBlockIndexCandidates.empty()) return nullptr;
@@ -1211,6 +1356,23 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
             pindexIter = pindexIter->pprev;
         }
         nHeight = nTargetHeight;
+        if (opts.connectPipeline > 1 && vpindexToConnect.size() > 1) {
+            // several blocks in a row: connect them through the pipeline, then let the caller
+            // publish the new tip (one step per batch instead of one per block)
+            const std::vector<CBlockIndex*> chain(vpindexToConnect.rbegin(), vpindexToConnect.rend());
+            if (!ConnectTipsPipelined(state, chain, pblock, trace)) {
+                if (state.IsInvalid()) {
+                    if (!state.CorruptionPossible()) InvalidChainFound(vpindexToConnect.front());
+                    CheckForkWarningConditionsOnNewFork(vpindexToConnect.back());
+                    state = CValidationState();
+                    fInvalidFound = true;
+                    break;
+                }
+                return false;
+            }
+            PruneBlockIndexCandidates();
+            break;
+        }
         for (auto it = vpindexToConnect.rbegin(); it != vpindexToConnect.rend(); ++it) {
             CBlockIndex* pindexConnect = *it;
             if (!ConnectTip(state, pindexConnect, pindexConnect == pindexMostWork ? pblock : std::shared_ptr<const CBlock>(),

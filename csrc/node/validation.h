@@ -78,6 +78,10 @@ struct ChainstateOptions {
     uint64_t pruneTarget = 0;       // bytes; 0 = no pruning
     uint256 assumeValid;
     int64_t maxTipAge = DEFAULT_MAX_TIP_AGE;
+    // -connectpipeline: when several blocks connect in a row (IBD, reorgs), block N+1's UTXO pass
+    // runs while block N's signature batch is on the GPU (at most this many blocks in flight;
+    // <= 1 connects one block at a time like the reference)
+    int connectPipeline = 2;
 };
 
 // Mempool acceptance outcome.
@@ -220,6 +224,14 @@ private:
                       uint64_t nTime, bool fKnown = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool FindUndoPos(CValidationState& state, int nFile, CDiskBlockPos& pos, unsigned nAddSize) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     void FlushBlockFile(bool fFinalize = false);
+    struct PendingConnect; // a block between its UTXO pass and its signature verdict
+    bool ConnectBlockPrepare(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
+                             bool fJustCheck, bool async, PendingConnect& p) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    bool ConnectBlockFinish(PendingConnect& p, CValidationState& state, bool fJustCheck)
+        EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    bool ConnectTipsPipelined(CValidationState& state, const std::vector<CBlockIndex*>& chain,
+                              const std::shared_ptr<const CBlock>& pblock, ConnectTrace& trace)
+        EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
                       bool fJustCheck = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     DisconnectResult DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view) EXCLUSIVE_LOCKS_REQUIRED(cs_main);

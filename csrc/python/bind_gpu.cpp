@@ -325,6 +325,7 @@ void bind_gpu(pyb::module_& m) {
         d["gpu_sigs"] = s.gpu_sigs;
         d["cpu_sigs"] = s.cpu_sigs;
         d["cache_hits"] = s.cache_hits;
+        d["multisig_groups"] = s.multisig_groups;
         d["gpu_failures"] = s.gpu_failures;
         return d;
     });

@@ -112,6 +112,7 @@ static UniValue getgpuinfo(const JSONRPCRequest& req) {
     sv.pushKV("gpu_sigs", (uint64_t)s.gpu_sigs);
     sv.pushKV("cpu_sigs", (uint64_t)s.cpu_sigs);
     sv.pushKV("cache_hits", (uint64_t)s.cache_hits);
+    sv.pushKV("multisig_groups", (uint64_t)s.multisig_groups);
     sv.pushKV("gpu_ms", s.gpu_ms);
     sv.pushKV("cpu_ms", s.cpu_ms);
     sv.pushKV("gpu_threshold", (uint64_t)GetGpuSigThreshold());

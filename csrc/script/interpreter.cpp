@@ -613,7 +613,31 @@ bool EvalScript(std::vector<valtype>& stack, const CScript& script, uint32_t fla
                     for (int k = 0; k < nSigsCount; k++) CleanupScriptCode(scriptCode, stacktop(stack, -isig - k), flags);
 
                     bool fSuccess = true;
-                    while (fSuccess && nSigsCount > 0) {
+                    // Speculative deferral (NULLFAIL, every signature non-empty and well encoded): a
+                    // failed match would fail the script, so a batching checker may take the match
+                    // over. Otherwise the greedy loop below runs eagerly, as in the reference.
+                    bool deferred = false;
+                    if (nullfail && nSigsCount > 0) {
+                        std::vector<const valtype*> sigs, keys;
+                        bool defer = true;
+                        for (int k = 0; k < nSigsCount && defer; k++) {
+                            const valtype& vs = stacktop(stack, -isig - k);
+                            ScriptError e;
+                            defer = !vs.empty() && CheckSignatureEncoding(vs, flags, &e);
+                            sigs.push_back(&vs);
+                        }
+                        if (defer) {
+                            uint32_t keyOk = 0;
+                            for (int k = 0; k < nKeysCount; k++) {
+                                const valtype& vk = stacktop(stack, -ikey - k);
+                                ScriptError e;
+                                if (CheckPubKeyEncoding(vk, flags, &e)) keyOk |= 1u << k;
+                                keys.push_back(&vk);
+                            }
+                            deferred = checker.DeferMultisig(sigs, keys, keyOk, scriptCode, flags);
+                        }
+                    }
+                    while (!deferred && fSuccess && nSigsCount > 0) {
                         valtype& vchSig = stacktop(stack, -isig);
                         valtype& vchPubKey = stacktop(stack, -ikey);
                         if (!CheckSignatureEncoding(vchSig, flags, serror) ||
@@ -822,6 +846,58 @@ bool DeferringSignatureChecker::CheckSig(const valtype& sigIn, const valtype& pu
     c.sig.assign(sigIn.data(), sigIn.size() - 1);
     c.pubkey.assign(pubkey);
     return true;
+}
+
+bool DeferringSignatureChecker::DeferMultisig(const std::vector<const valtype*>& sigs,
+                                              const std::vector<const valtype*>& keys, uint32_t keyOk,
+                                              const CScript& scriptCode, uint32_t flags) const {
+    if (!sink || !groups) return false;
+    const size_t m = sigs.size(), n = keys.size();
+    if (m == 0 || m > n || n > MAX_PUBKEYS_PER_MULTISIG) return false;
+    for (const valtype* k : keys)
+        if (k->size() > decltype(DeferredSigCheck::pubkey)::capacity) return false;
+    std::vector<uint256> digests(m);
+    for (size_t i = 0; i < m; i++) {
+        if (sigs[i]->empty() || sigs[i]->size() - 1 > decltype(DeferredSigCheck::sig)::capacity) return false;
+        if (!SigDigest(*sigs[i], scriptCode, flags, digests[i])) return false;
+    }
+    DeferredMultisig g;
+    g.first = (uint32_t)sink->size();
+    g.m = (uint8_t)m;
+    g.n = (uint8_t)n;
+    g.keyOk = keyOk;
+    sink->reserve(sink->size() + g.Pairs());
+    for (size_t i = 0; i < m; i++) {
+        for (size_t j = i; j <= i + (n - m); j++) {
+            sink->emplace_back();
+            DeferredSigCheck& c = sink->back();
+            c.sighash = digests[i];
+            c.sig.assign(sigs[i]->data(), sigs[i]->size() - 1);
+            const valtype& k = *keys[j];
+            // a key that would fail parsing verifies as false, as the eager check would
+            if (!k.empty() && CPubKey::GetLen(k[0]) == k.size()) c.pubkey.assign(k);
+        }
+    }
+    groups->push_back(g);
+    return true;
+}
+
+bool EvalDeferredMultisig(const DeferredMultisig& g, const uint8_t* pairResults) {
+    const int m = g.m, n = g.n, width = n - m + 1;
+    int isig = 0, ikey = 0, nSigs = m, nKeys = n;
+    bool fSuccess = true;
+    while (fSuccess && nSigs > 0) {
+        if (!((g.keyOk >> ikey) & 1)) return false; // a visited key that fails encoding: script error
+        // (while matching, 0 <= ikey - isig <= n - m: the pair is one of the recorded ones)
+        if (pairResults[isig * width + (ikey - isig)]) {
+            isig++;
+            nSigs--;
+        }
+        ikey++;
+        nKeys--;
+        if (nSigs > nKeys) fSuccess = false;
+    }
+    return fSuccess;
 }
 
 bool TransactionSignatureChecker::CheckLockTime(const CScriptNum& nLockTime) const {

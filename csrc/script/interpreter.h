@@ -11,8 +11,10 @@
 // checks instead of executing them. This is sound exactly when NULLFAIL is active
 // and the signature is non-empty: a failing CHECKSIG then fails the whole script,
 // so "assume true now, verify later in a GPU batch, AND the results" yields the same
-// accept/reject decision. CHECKMULTISIG (where a failed pair is legal) and non-NULLFAIL
-// contexts are always evaluated eagerly.
+// accept/reject decision. CHECKMULTISIG, where a failed (signature, key) pair is legal, is
+// deferred speculatively under the same NULLFAIL condition: every pair the greedy match could
+// try goes into the batch, and the match itself is replayed over the batch results
+// (DeferredMultisig / EvalDeferredMultisig). Non-NULLFAIL contexts are evaluated eagerly.
 #pragma once
 #include "primitives/transaction.h"
 #include "script/script.h"
@@ -128,6 +130,14 @@ public:
                           const CScript& scriptCode, uint32_t flags, bool deferrable = false) const {
         return false;
     }
+    // CHECKMULTISIG under NULLFAIL with only non-empty, well-encoded signatures (a failed match
+    // then fails the script): a batching checker may record the match for later and return
+    // true. keyOk bit j: key j passes the key-encoding rules (a visited bad key fails the script).
+    virtual bool DeferMultisig(const std::vector<const std::vector<unsigned char>*>& sigs,
+                               const std::vector<const std::vector<unsigned char>*>& keys, uint32_t keyOk,
+                               const CScript& scriptCode, uint32_t flags) const {
+        return false;
+    }
     virtual bool CheckLockTime(const CScriptNum& nLockTime) const { return false; }
     virtual bool CheckSequence(const CScriptNum& nSequence) const { return false; }
 };
@@ -193,16 +203,33 @@ struct DeferredSigCheck {
     uint256 sighash;
 };
 
+// A deferred CHECKMULTISIG: the m x (n - m + 1) pairs its greedy match can reach are consecutive
+// checks of the batch starting at `first`, row-major by signature (signature i with keys
+// i .. i + n - m). Their individual results are speculative: only the replayed match counts.
+struct DeferredMultisig {
+    uint32_t first = 0; // index of the first pair check (rebased when job sinks are concatenated)
+    uint8_t m = 0, n = 0;
+    uint32_t keyOk = 0; // bit j: key j passes the key-encoding rules
+    uint32_t Pairs() const { return (uint32_t)m * (uint32_t)(n - m + 1); }
+};
+// Replays the reference's greedy CHECKMULTISIG loop (interpreter.cpp:1054) over the pair results.
+bool EvalDeferredMultisig(const DeferredMultisig& g, const uint8_t* pairResults);
+
 class DeferringSignatureChecker : public TransactionSignatureChecker {
 public:
     DeferringSignatureChecker(const CTransaction* txTo, unsigned int nIn, Amount amount,
-                              const PrecomputedTransactionData* txdata, std::vector<DeferredSigCheck>* sink)
-        : TransactionSignatureChecker(txTo, nIn, amount, txdata), sink(sink) {}
+                              const PrecomputedTransactionData* txdata, std::vector<DeferredSigCheck>* sink,
+                              std::vector<DeferredMultisig>* groups = nullptr)
+        : TransactionSignatureChecker(txTo, nIn, amount, txdata), sink(sink), groups(groups) {}
     bool CheckSig(const std::vector<unsigned char>& sig, const std::vector<unsigned char>& pubkey,
                   const CScript& scriptCode, uint32_t flags, bool deferrable = false) const override;
+    bool DeferMultisig(const std::vector<const std::vector<unsigned char>*>& sigs,
+                       const std::vector<const std::vector<unsigned char>*>& keys, uint32_t keyOk,
+                       const CScript& scriptCode, uint32_t flags) const override;
 
 private:
     std::vector<DeferredSigCheck>* sink;
+    std::vector<DeferredMultisig>* groups; // CHECKMULTISIG deferral (null: multisig runs eagerly)
 };
 
 class MutableTransactionSignatureChecker : public TransactionSignatureChecker {

@@ -526,12 +526,15 @@ CBlock MakeBlock(Chainstate& cs, CTxMemPool& pool, const CScript& spk, const std
     return b;
 }
 
-BigBlockFixture& BigBlock(bool worstCase) {
-    static BigBlockFixture fx[2];
-    static bool built[2] = {false, false};
-    BigBlockFixture& f = fx[worstCase];
-    if (built[worstCase]) return f;
-    built[worstCase] = true;
+// kind 0: P2PKH spends; 1: the 160k-sigop worst case; 2: P2SH 2-of-3 multisig spends (every
+// CHECKMULTISIG deferred speculatively into the batch: 4 (signature, key) pairs per input)
+BigBlockFixture& BigBlock(int kind) {
+    static BigBlockFixture fx[3];
+    static bool built[3] = {false, false, false};
+    const bool worstCase = kind == 1, multisig = kind == 2;
+    BigBlockFixture& f = fx[kind];
+    if (built[kind]) return f;
+    built[kind] = true;
     SelectParams("regtest");
     ChainstateOptions o;
     o.memoryOnly = true;
@@ -557,8 +560,20 @@ BigBlockFixture& BigBlock(bool worstCase) {
     for (int i = 0; i < 100; i++) redeem << OP_2DUP << OP_CHECKSIGVERIFY;
     redeem << OP_CHECKSIG;
     const CScript spkSH = GetScriptForDestination(CScriptID(redeem));
-    const int NFAN = 24, NOUT = 1750;              // 42,000 P2PKH outputs to spend
-    const int NTX = worstCase ? 19500 : 21000;     // 2-in/2-out P2PKH spends in the big block
+    // 2-of-3 multisig behind P2SH (bare multisig outputs would count 20 sigops each)
+    CKey k2, k3;
+    k2.MakeNewKey(true);
+    k3.MakeNewKey(false);
+    ks.AddKey(k2);
+    ks.AddKey(k3);
+    CScript redeemMS;
+    redeemMS << 2 << std::vector<unsigned char>(pub.begin(), pub.end()) << k2.GetPubKey().Raw() << k3.GetPubKey().Raw()
+             << 3 << OP_CHECKMULTISIG;
+    ks.AddCScript(redeemMS);
+    const CScript spkMS = GetScriptForDestination(CScriptID(redeemMS));
+    const CScript& fanOut = multisig ? spkMS : spk;
+    const int NFAN = 24, NOUT = 1750;              // 42,000 outputs to spend
+    const int NTX = worstCase ? 19500 : multisig ? 10700 : 21000; // 2-in/2-out spends in the big block
     const int NSHTX = worstCase ? 8 : 0, NSHIN = 198; // P2SH spends: 198 x 101 sigops < 20,000 per tx
     const CScript& bigOut = worstCase ? spkSH : spk;
     std::vector<CTransactionRef> coinbases;
@@ -587,7 +602,7 @@ BigBlockFixture& BigBlock(bool worstCase) {
         m.vin.resize(1);
         m.vin[0].prevout = COutPoint(cb.GetHash(), 0);
         const Amount each = (cb.vout[0].nValue - 100000) / NOUT;
-        for (int k = 0; k < NOUT; k++) m.vout.push_back(CTxOut(each, spk));
+        for (int k = 0; k < NOUT; k++) m.vout.push_back(CTxOut(each, fanOut));
         if (!SignSignature(ks, cb.vout[0].scriptPubKey, m, 0, cb.vout[0].nValue, hashType))
             throw std::runtime_error("bench: fan-out signing failed");
         fan.push_back(MakeTransactionRef(std::move(m)));
@@ -661,7 +676,7 @@ BigBlockFixture& BigBlock(bool worstCase) {
     for (auto& m : txs) refs.push_back(MakeTransactionRef(std::move(m)));
     for (auto& m : shTxs) refs.push_back(MakeTransactionRef(std::move(m)));
     f.block = MakeBlock(*f.cs, f.pool, spk, refs);
-    f.nSigs = 2 * (size_t)NTX + (size_t)NSHTX * NSHIN * 101;
+    f.nSigs = (multisig ? 4 : 2) * (size_t)NTX + (size_t)NSHTX * NSHIN * 101;
     f.nBytes = GetSerializeSize(f.block, PROTOCOL_VERSION);
     {
         const CCoinsViewCache& view = f.cs->CoinsTip();
@@ -670,13 +685,13 @@ BigBlockFixture& BigBlock(bool worstCase) {
     }
     f.ok = true;
     fprintf(stderr, "# big block%s: %zu txs, %zu signature checks, %zu sigops (limit %llu), %zu bytes, on height %d\n",
-            worstCase ? " (160k sigops)" : "", f.block.vtx.size(), f.nSigs, f.nSigOps,
+            worstCase ? " (160k sigops)" : multisig ? " (2-of-3 P2SH multisig)" : "", f.block.vtx.size(), f.nSigs, f.nSigOps,
             (unsigned long long)GetMaxBlockSigOpsCount(f.nBytes), f.nBytes, f.cs->Height());
     return f;
 }
 
-void ConnectBigBlock(State& st, bool useGpu, bool worstCase) {
-    BigBlockFixture& f = BigBlock(worstCase);
+void ConnectBigBlock(State& st, bool useGpu, int kind) {
+    BigBlockFixture& f = BigBlock(kind);
     const size_t thr = GetGpuSigThreshold();
     SetGpuSigThreshold(useGpu ? DEFAULT_GPU_SIG_THRESHOLD : SIZE_MAX);
     const SigVerifyStats s0 = GetSigVerifyStats();
@@ -691,23 +706,30 @@ void ConnectBigBlock(State& st, bool useGpu, bool worstCase) {
     }
     const SigVerifyStats s1 = GetSigVerifyStats();
     // where the time goes: signature batches (GPU incl. host DER parse/upload, or CPU pool)
-    fprintf(stderr, "# %s: per block %.1f sigs on the GPU (%.2f ms), %.1f on the CPU (%.2f ms), %llu GPU failures\n",
+    fprintf(stderr, "# %s: per block %.1f sigs on the GPU (%.2f ms), %.1f on the CPU (%.2f ms), %llu GPU failures, "
+                    "%.1f deferred multisig groups\n",
             useGpu ? "GPU" : "CPU", (double)(s1.gpu_sigs - s0.gpu_sigs) / iters, (s1.gpu_ms - s0.gpu_ms) / iters,
             (double)(s1.cpu_sigs - s0.cpu_sigs) / iters, (s1.cpu_ms - s0.cpu_ms) / iters,
-            (unsigned long long)(s1.gpu_failures - s0.gpu_failures));
+            (unsigned long long)(s1.gpu_failures - s0.gpu_failures),
+            (double)(s1.multisig_groups - s0.multisig_groups) / iters);
     SetGpuSigThreshold(thr);
 }
 } // namespace
 
-static void ConnectBlock8MB_CPU(State& st) { ConnectBigBlock(st, false, false); }
+static void ConnectBlock8MB_CPU(State& st) { ConnectBigBlock(st, false, 0); }
 static void ConnectBlock8MB_GPU(State& st) {
     if (!gpu::GpuAvailable()) return;
-    ConnectBigBlock(st, true, false);
+    ConnectBigBlock(st, true, 0);
 }
-static void ConnectBlock8MB_160kSigops_CPU(State& st) { ConnectBigBlock(st, false, true); }
+static void ConnectBlock8MB_160kSigops_CPU(State& st) { ConnectBigBlock(st, false, 1); }
 static void ConnectBlock8MB_160kSigops_GPU(State& st) {
     if (!gpu::GpuAvailable()) return;
-    ConnectBigBlock(st, true, true);
+    ConnectBigBlock(st, true, 1);
+}
+static void ConnectBlock8MB_Multisig_CPU(State& st) { ConnectBigBlock(st, false, 2); }
+static void ConnectBlock8MB_Multisig_GPU(State& st) {
+    if (!gpu::GpuAvailable()) return;
+    ConnectBigBlock(st, true, 2);
 }
 // Script evaluation of one worst-case P2SH input (<pk> (2DUP CHECKSIGVERIFY) x100 CHECKSIG, the
 // 160k-sigop block's redeem script) with every CHECKSIG deferred into a batch sink: the per-input
@@ -754,6 +776,8 @@ BENCHMARK(ConnectBlock8MB_CPU);
 BENCHMARK(ConnectBlock8MB_GPU);
 BENCHMARK(ConnectBlock8MB_160kSigops_CPU);
 BENCHMARK(ConnectBlock8MB_160kSigops_GPU);
+BENCHMARK(ConnectBlock8MB_Multisig_CPU);
+BENCHMARK(ConnectBlock8MB_Multisig_GPU);
 
 int main(int argc, char* argv[]) {
     gArgs.ParseParameters(argc, argv);
