@@ -779,6 +779,171 @@ BENCHMARK(ConnectBlock8MB_160kSigops_GPU);
 BENCHMARK(ConnectBlock8MB_Multisig_CPU);
 BENCHMARK(ConnectBlock8MB_Multisig_GPU);
 
+// ------------------------------------------------------------------ IBD pipeline
+// IbdPipeline_{Seq,Pipe}_{CPU,GPU}: a fresh node connects -ibdblocks consecutive big blocks
+// (default 50; each ~7.3 MB: 20,000 2-in/2-out P2PKH spends of the previous block's outputs,
+// 40,000 signatures). The blocks arrive last-to-first, so nothing connects until the first one
+// lands and then the whole run connects in ActivateBestChain steps - one block at a time
+// (-connectpipeline=1, "Seq") or with block N+1's UTXO pass overlapping block N's signature
+// batch ("Pipe"). Reported: ms per block (one iteration = the whole run).
+namespace {
+struct IbdFixture {
+    std::vector<std::shared_ptr<const CBlock>> setup, run; // setup: to the fork + fan-out; run: timed
+    bool built = false;
+};
+IbdFixture& Ibd() {
+    static IbdFixture f;
+    if (f.built) return f;
+    f.built = true;
+    const int nBlocks = (int)gArgs.GetArg("-ibdblocks", (int64_t)50);
+    SelectParams("regtest");
+    ChainstateOptions o;
+    o.memoryOnly = true;
+    char tmpl[] = "/tmp/bench_bcp_ibd_XXXXXX";
+    if (!mkdtemp(tmpl)) throw std::runtime_error("bench: mkdtemp failed");
+    o.datadir = tmpl;
+    o.useGpu = false; // the builder only assembles; validation speed is measured on fresh nodes
+    o.scriptThreads = std::min(16, std::max(2, GetNumCores()));
+    Chainstate cs(Params(), o);
+    CTxMemPool pool;
+    std::string err;
+    if (!cs.InitBlockIndex(err)) throw std::runtime_error("bench: " + err);
+    cs.SetMempool(&pool);
+    CBasicKeyStore ks;
+    CKey key;
+    key.MakeNewKey(true);
+    ks.AddKey(key);
+    const CScript spk = GetScriptForDestination(key.GetPubKey().GetID());
+    const uint32_t hashType = SIGHASH_ALL | SIGHASH_FORKID;
+    auto connect = [&](const CBlock& b, std::vector<std::shared_ptr<const CBlock>>& into) {
+        auto pb = std::make_shared<const CBlock>(b);
+        bool fNew = false;
+        CValidationState st;
+        if (!cs.ProcessNewBlock(pb, true, &fNew, &st)) throw std::runtime_error("bench: " + FormatStateMessage(st));
+        into.push_back(pb);
+    };
+    std::vector<CTransactionRef> coinbases;
+    const int forkHeight = Params().GetConsensus().BCPHeight;
+    while (cs.HeightNow() < forkHeight + 1) {
+        CBlock b = MakeBlock(cs, pool, spk, {});
+        coinbases.push_back(b.vtx[0]);
+        connect(b, f.setup);
+    }
+    const int NFAN = 20, NOUT = 2000, NTX = 20000; // 40,000 outputs carried from block to block
+    std::vector<COutPoint> outs;
+    std::vector<Amount> vals;
+    for (int c0 = 0; c0 < NFAN; c0 += 8) {
+        std::vector<CTransactionRef> v;
+        for (int c = c0; c < std::min(NFAN, c0 + 8); c++) {
+            const CTransaction& cb = *coinbases[c];
+            CMutableTransaction m;
+            m.vin.resize(1);
+            m.vin[0].prevout = COutPoint(cb.GetHash(), 0);
+            const Amount each = (cb.vout[0].nValue - 100000) / NOUT;
+            for (int k = 0; k < NOUT; k++) m.vout.push_back(CTxOut(each, spk));
+            if (!SignSignature(ks, cb.vout[0].scriptPubKey, m, 0, cb.vout[0].nValue, hashType))
+                throw std::runtime_error("bench: fan-out signing failed");
+            const CTransactionRef t = MakeTransactionRef(std::move(m));
+            for (int k = 0; k < NOUT; k++) {
+                outs.push_back(COutPoint(t->GetHash(), (uint32_t)k));
+                vals.push_back(t->vout[k].nValue);
+            }
+            v.push_back(t);
+        }
+        connect(MakeBlock(cs, pool, spk, v), f.setup);
+    }
+    WorkerPool wp(std::min(16, std::max(2, GetNumCores())));
+    for (int b = 0; b < nBlocks; b++) {
+        std::vector<CMutableTransaction> txs(NTX);
+        std::atomic<bool> fail{false};
+        wp.ParallelFor(NTX, [&](size_t t) {
+            CMutableTransaction& m = txs[t];
+            const Amount in = vals[2 * t] + vals[2 * t + 1];
+            for (int k = 0; k < 2; k++) m.vin.emplace_back(CTxIn(outs[2 * t + k]));
+            m.vout.push_back(CTxOut(in / 2 - 300, spk));
+            m.vout.push_back(CTxOut(in / 2 - 300, spk));
+            for (int k = 0; k < 2; k++)
+                if (!SignSignature(ks, spk, m, k, vals[2 * t + k], hashType)) fail = true;
+        }, 32);
+        if (fail) throw std::runtime_error("bench: IBD signing failed");
+        std::vector<CTransactionRef> refs;
+        refs.reserve(NTX);
+        for (int t = 0; t < NTX; t++) {
+            refs.push_back(MakeTransactionRef(std::move(txs[t])));
+            for (int k = 0; k < 2; k++) {
+                outs[2 * t + k] = COutPoint(refs.back()->GetHash(), (uint32_t)k);
+                vals[2 * t + k] = refs.back()->vout[k].nValue;
+            }
+        }
+        connect(MakeBlock(cs, pool, spk, refs), f.run);
+        if (b % 10 == 9) fprintf(stderr, "# ibd fixture: %d/%d blocks built\n", b + 1, nBlocks);
+    }
+    fprintf(stderr, "# ibd fixture: %zu setup blocks, %zu big blocks of %zu bytes\n", f.setup.size(), f.run.size(),
+            GetSerializeSize(*f.run[0], PROTOCOL_VERSION));
+    return f;
+}
+
+void IbdRun(State& st, bool useGpu, int pipeline) {
+    IbdFixture& f = Ibd();
+    const size_t thr = GetGpuSigThreshold();
+    SetGpuSigThreshold(useGpu ? DEFAULT_GPU_SIG_THRESHOLD : SIZE_MAX);
+    double totalMs = 0;
+    int iters = 0;
+    while (st.KeepRunning()) {
+        ChainstateOptions o;
+        o.memoryOnly = true;
+        char tmpl[] = "/tmp/bench_bcp_ibdrun_XXXXXX";
+        if (!mkdtemp(tmpl)) throw std::runtime_error("bench: mkdtemp failed");
+        o.datadir = tmpl;
+        o.useGpu = useGpu;
+        o.connectPipeline = pipeline;
+        o.scriptThreads = std::min(16, std::max(2, GetNumCores()));
+        Chainstate cs(Params(), o);
+        std::string err;
+        if (!cs.InitBlockIndex(err)) throw std::runtime_error("bench: " + err);
+        auto feed = [&](const std::shared_ptr<const CBlock>& b) {
+            bool fNew = false;
+            CValidationState vs;
+            if (!cs.ProcessNewBlock(b, true, &fNew, &vs)) throw std::runtime_error("bench: " + FormatStateMessage(vs));
+        };
+        for (const auto& b : f.setup) feed(b);
+        // headers first, then the blocks last-to-first: the run connects once the first arrives
+        std::vector<CBlockHeader> hdrs;
+        for (const auto& b : f.run) hdrs.push_back(b->GetBlockHeader());
+        CValidationState hs;
+        if (!cs.ProcessNewBlockHeaders(hdrs, hs)) throw std::runtime_error("bench: headers " + FormatStateMessage(hs));
+        for (size_t i = f.run.size(); i-- > 1;) feed(f.run[i]);
+        const int64_t t0 = GetTimeMicros();
+        feed(f.run[0]);
+        const int64_t t1 = GetTimeMicros();
+        if (cs.HeightNow() != f.run.size() + f.setup.size()) {
+            fprintf(stderr, "IBD run ended at height %d\n", cs.HeightNow());
+            exit(1);
+        }
+        totalMs += (t1 - t0) / 1000.0;
+        iters++;
+        const std::string cmd = std::string("rm -rf '") + tmpl + "'";
+        if (system(cmd.c_str()) != 0) {}
+    }
+    printf("{\"bench\": \"IbdPipeline\", \"gpu\": %s, \"pipeline\": %d, \"blocks\": %zu, \"ms_per_block\": %.2f}\n",
+           useGpu ? "true" : "false", pipeline, f.run.size(), totalMs / iters / f.run.size());
+    fflush(stdout);
+    SetGpuSigThreshold(thr);
+}
+} // namespace
+static void IbdPipeline_Seq_CPU(State& st) { IbdRun(st, false, 1); }
+static void IbdPipeline_Pipe_CPU(State& st) { IbdRun(st, false, 2); }
+static void IbdPipeline_Seq_GPU(State& st) {
+    if (gpu::GpuAvailable()) IbdRun(st, true, 1);
+}
+static void IbdPipeline_Pipe_GPU(State& st) {
+    if (gpu::GpuAvailable()) IbdRun(st, true, 2);
+}
+BENCHMARK(IbdPipeline_Seq_CPU);
+BENCHMARK(IbdPipeline_Pipe_CPU);
+BENCHMARK(IbdPipeline_Seq_GPU);
+BENCHMARK(IbdPipeline_Pipe_GPU);
+
 int main(int argc, char* argv[]) {
     gArgs.ParseParameters(argc, argv);
     if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help")) {
