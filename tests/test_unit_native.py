@@ -25,7 +25,8 @@ def test_suite_inventory():
     # the suites ported from reference src/test/ (each must exist and hold cases)
     for s in [
         "script_antireplay_tests", "sigopcount_tests", "bloom_tests", "pmt_tests", "blockencodings_tests",
-        "coins_tests", "versionbits_tests", "mempool_tests",
+        "coins_tests", "versionbits_tests", "mempool_tests", "kvstore_tests", "sigbatch_tests", "miner_tests",
+        "policyestimator_tests", "txvalidationcache_tests",
     ]:
         assert s in SUITES, s
 
