@@ -226,9 +226,12 @@ std::vector<uint8_t> EquihashVerifyBatch(unsigned n, unsigned k, const std::vect
 }
 
 bool GpuAvailable() {
-    int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess) return false;
-    return count > 0;
+    // asked per block (and per batch): probe the runtime once, devices do not come and go
+    static const bool available = [] {
+        int count = 0;
+        return hipGetDeviceCount(&count) == hipSuccess && count > 0;
+    }();
+    return available;
 }
 
 int DeviceCount() {

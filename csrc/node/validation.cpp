@@ -98,7 +98,7 @@ protected:
 struct ScriptJob {
     const CTransaction* tx;
     unsigned nIn;
-    CScript scriptPubKey;
+    const CScript* scriptPubKey; // the spent coin, kept in the block's undo record
     Amount amount;
     const PrecomputedTransactionData* txdata;
 };
@@ -782,7 +782,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     std::vector<std::vector<DeferredMultisig>> groupSinks(maxJobs); // deferred CHECKMULTISIGs per job
     const bool deferMultisig = GpuBatchesExpected(opts.useGpu);
     std::atomic<bool> anyFail{false};
-    size_t nProduced = 0;
+    size_t nProduced = 0, nPublished = 0;
     const bool queued = fScriptChecks && maxJobs > 0;
     if (queued)
         scriptQueue->Begin([&](size_t k) {
@@ -790,7 +790,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             const ScriptJob& J = jobs[k];
             BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k], deferMultisig ? &groupSinks[k] : nullptr);
             ScriptError err;
-            if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, J.scriptPubKey, flags, checker, &err)) anyFail = true;
+            if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, *J.scriptPubKey, flags, checker, &err)) anyFail = true;
         });
     // every return below drains and closes the session first (jobs/sinks outlive it)
     struct CompleteOnExit {
@@ -821,18 +821,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             if (!Consensus::CheckTxInputs(tx, state, view, pindex->nHeight))
                 return error("ConnectBlock(): CheckTxInputs on %s failed with %s", tx.GetHash().ToString().c_str(),
                              FormatStateMessage(state).c_str());
-            if (fScriptChecks) {
-                // transactions fully validated under these flags in the mempool skip re-execution
-                if (!sc.Has(scKeys[i], !fJustCheck)) {
-                    for (size_t j = 0; j < tx.vin.size(); j++) {
-                        const Coin& coin = view.AccessCoin(tx.vin[j].prevout);
-                        jobs[nProduced + j] = ScriptJob{&tx, (unsigned)j, coin.GetTxOut().scriptPubKey,
-                                                        coin.GetTxOut().nValue, txdatas[i].get()};
-                    }
-                    nProduced += tx.vin.size();
-                    scriptQueue->Publish(nProduced);
-                }
-            }
         }
         CTxUndo undoDummy;
         if (i > 0) blockundo.vtxundo.push_back(CTxUndo());
@@ -842,6 +830,21 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             for (const CTxIn& in : tx.vin) {
                 undo.vprevout.emplace_back();
                 if (!view.SpendCoin(in.prevout, &undo.vprevout.back())) return state.Error("ConnectBlock: spend failed");
+            }
+            // transactions fully validated under these flags in the mempool skip re-execution; the
+            // jobs read the spent coins from the undo record (reserved up front: the addresses are
+            // stable for the whole block) instead of copying each script
+            if (fScriptChecks && !sc.Has(scKeys[i], !fJustCheck)) {
+                for (size_t j = 0; j < tx.vin.size(); j++) {
+                    const CTxOut& out = undo.vprevout[j].GetTxOut();
+                    jobs[nProduced + j] = ScriptJob{&tx, (unsigned)j, &out.scriptPubKey, out.nValue, txdatas[i].get()};
+                }
+                nProduced += tx.vin.size();
+                // publish in groups: each publish takes the queue lock and may wake a worker
+                if (nProduced - nPublished >= 16) {
+                    scriptQueue->Publish(nProduced);
+                    nPublished = nProduced;
+                }
             }
         }
         AddCoins(view, tx, pindex->nHeight);
@@ -858,6 +861,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                          REJECT_INVALID, "bad-cb-amount");
 
     // ---- remaining scripts, then one ECDSA batch (GPU when large enough)
+    scriptQueue->Publish(nProduced);
     scriptQueue->Complete();
     const size_t nJobs = nProduced;
     p.nJobs = nJobs;

@@ -7,6 +7,8 @@ namespace bcp {
 // Largest batch one claim takes (reference checkqueue.h: nBatchSize 128 per script check; jobs
 // here are script evaluations with deferred signatures, a few microseconds each).
 static const size_t MAX_CLAIM = 16;
+// Jobs per woken worker (a worker that finds more than it claimed wakes the next one).
+static const size_t MIN_WAKE_JOBS = 4;
 
 CheckQueue::CheckQueue(int nWorkers) : sessionLock(sessionMutex, std::defer_lock) {
     for (int i = 0; i < nWorkers; i++) threads.emplace_back([this] { Loop(); });
@@ -37,19 +39,34 @@ bool CheckQueue::ClaimLocked(size_t& b, size_t& e) {
     return true;
 }
 
+// Wakes as many sleeping workers as the unclaimed jobs can keep busy (called with m held). A
+// notify_all per published transaction would wake every worker for two jobs: on a 21,000-tx
+// block that is hundreds of thousands of futile wake-ups contending for m.
+void CheckQueue::WakeLocked() {
+    if (!active || next >= avail || sleeping == 0) return;
+    const size_t want = std::min<size_t>(sleeping, (avail - next + MIN_WAKE_JOBS - 1) / MIN_WAKE_JOBS);
+    for (size_t i = 0; i < want; i++) cvWork.notify_one();
+}
+
 void CheckQueue::Loop() {
     std::unique_lock<std::mutex> l(m);
     for (;;) {
         size_t b = 0, e = 0;
+        ++sleeping;
         cvWork.wait(l, [&] { return stop || ClaimLocked(b, e); });
+        --sleeping;
         if (stop) return;
-        const std::function<void(size_t)>* f = &fn;
-        l.unlock();
-        for (size_t k = b; k < e; k++) (*f)(k);
-        l.lock();
-        done += e - b;
-        workerJobs += e - b;
-        if (done == avail) cvDone.notify_all();
+        for (;;) {
+            WakeLocked(); // more left than this claim: pass the work on (cascade)
+            const std::function<void(size_t)>* f = &fn;
+            l.unlock();
+            for (size_t k = b; k < e; k++) (*f)(k);
+            l.lock();
+            done += e - b;
+            workerJobs += e - b;
+            if (done == avail) cvDone.notify_all();
+            if (!ClaimLocked(b, e)) break; // keep going while there is work, without sleeping
+        }
     }
 }
 
@@ -62,12 +79,10 @@ void CheckQueue::Begin(std::function<void(size_t)> f) {
 }
 
 void CheckQueue::Publish(size_t total) {
-    {
-        std::lock_guard<std::mutex> l(m);
-        if (!active || total <= avail) return;
-        avail = total;
-    }
-    cvWork.notify_all();
+    std::lock_guard<std::mutex> l(m);
+    if (!active || total <= avail) return;
+    avail = total;
+    WakeLocked();
 }
 
 void CheckQueue::Complete() {

@@ -43,6 +43,7 @@ public:
 private:
     void Loop();
     bool ClaimLocked(size_t& b, size_t& e);
+    void WakeLocked();
     std::vector<std::thread> threads;
     mutable std::mutex m;
     std::condition_variable cvWork, cvDone;
@@ -51,6 +52,7 @@ private:
     std::function<void(size_t)> fn;
     size_t avail = 0, next = 0, done = 0;
     size_t workerJobs = 0;
+    size_t sleeping = 0; // workers waiting on cvWork
     bool active = false, stop = false;
 };
 
