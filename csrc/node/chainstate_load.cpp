@@ -444,7 +444,7 @@ void Chainstate::FindFilesToPrune(std::set<int>& setFilesToPrune, uint64_t nPrun
     if ((uint64_t)chainActive.Tip()->nHeight <= nPruneAfterHeight) return;
     const unsigned nLastBlockWeCanPrune = chainActive.Tip()->nHeight - MIN_BLOCKS_TO_KEEP;
     uint64_t nCurrentUsage = CalculateCurrentUsage();
-    const uint64_t nBuffer = BLOCKFILE_CHUNK_SIZE + UNDOFILE_CHUNK_SIZE;
+    const uint64_t nBuffer = FileSizes().blockChunk + FileSizes().undoChunk;
     if (nCurrentUsage + nBuffer < opts.pruneTarget) return;
     for (int f = 0; f < nLastBlockFile; f++) {
         const uint64_t nBytesToPrune = vinfoBlockFile[f].nSize + vinfoBlockFile[f].nUndoSize;

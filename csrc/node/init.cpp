@@ -100,6 +100,7 @@ std::string HelpMessage() {
         {"-logips", "Include IP addresses in debug output (default: 0)"},
         {"-shrinkdebugfile", "Shrink debug.log file on client startup (default: 1)"},
         {"-checkblockindex", "Do a full consistency check of the block index (regtest default)"},
+        {"-fastprune", "Use 64 KiB block files (regtest only; for pruning tests)"},
         {"-connectpipeline=<n>", "Blocks in flight when connecting several in a row: block N+1's UTXO pass overlaps "
                                  "block N's signature batch (default: 2; 1 = one block at a time)"},
         {"-checkmempool=<n>", "Run checks every <n> transactions"},

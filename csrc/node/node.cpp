@@ -1,6 +1,8 @@
 #include "node/node.h"
 #include "node/policy.h"
 
+#include <limits>
+
 namespace bcp {
 
 static NodeContext* g_node = nullptr;
@@ -30,8 +32,11 @@ std::unique_ptr<NodeContext> BuildNode(const std::string& chain, const std::stri
     o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)0);
     o.maxTipAge = gArgs.GetArg("-maxtipage", DEFAULT_MAX_TIP_AGE);
     o.connectPipeline = (int)gArgs.GetArg("-connectpipeline", (int64_t)o.connectPipeline);
+    SetFastPrune(gArgs.GetBoolArg("-fastprune", false) && node->params->NetworkIDString() == "regtest");
     const int64_t prune = gArgs.GetArg("-prune", (int64_t)0);
-    if (prune > 1) o.pruneTarget = (uint64_t)prune * 1024 * 1024;
+    // -prune=1: manual pruning only (pruneblockchain RPC), never automatic (reference init.cpp)
+    if (prune == 1) o.pruneTarget = std::numeric_limits<uint64_t>::max();
+    else if (prune > 1) o.pruneTarget = (uint64_t)prune * 1024 * 1024;
     if (gArgs.IsArgSet("-assumevalid")) o.assumeValid = uint256S(gArgs.GetArg("-assumevalid", ""));
     else o.assumeValid = node->params->GetConsensus().defaultAssumeValid;
     node->chainstate.reset(new Chainstate(*node->params, o));

@@ -11,6 +11,17 @@
 
 namespace bcp {
 
+static BlockFileSizes g_fileSizes;
+const BlockFileSizes& FileSizes() { return g_fileSizes; }
+void SetFastPrune(bool on) {
+    g_fileSizes = BlockFileSizes();
+    if (on) {
+        g_fileSizes.maxFile = 0x10000;
+        g_fileSizes.blockChunk = 0x1000;
+        g_fileSizes.undoChunk = 0x1000;
+    }
+}
+
 namespace {
 const char DB_COIN = 'C';
 const char DB_BLOCK_FILES = 'f';

@@ -102,6 +102,13 @@ private:
 static const unsigned int MAX_BLOCKFILE_SIZE = 0x8000000; // 128 MiB
 static const unsigned int BLOCKFILE_CHUNK_SIZE = 0x1000000; // 16 MiB
 static const unsigned int UNDOFILE_CHUNK_SIZE = 0x100000;  // 1 MiB
+// -fastprune (regtest): 64 KiB block files and 4 KiB preallocation chunks, so tests can fill,
+// prune and reload many files with a short chain (later reference releases' option of that name)
+struct BlockFileSizes {
+    unsigned maxFile = MAX_BLOCKFILE_SIZE, blockChunk = BLOCKFILE_CHUNK_SIZE, undoChunk = UNDOFILE_CHUNK_SIZE;
+};
+const BlockFileSizes& FileSizes();
+void SetFastPrune(bool on);
 
 void SetBlocksDir(const std::string& dir);
 const std::string& GetBlocksDir();
