@@ -11,7 +11,8 @@
 //   SipHash      <- reference src/hash.{h,cpp}:181-300 (CSipHasher, SipHashUint256[Extra])
 //   ChaCha20     <- reference src/crypto/chacha20.{h,cpp}
 //
-// The CPU implementations are portable scalar code; the throughput paths
+// The CPU implementations are portable scalar code (SHA-256 on the x86 SHA extensions when the
+// host has them, crypto/sha256_x86.cpp); the throughput paths
 // (SHA-256d batches, BLAKE2b for Equihash) live in csrc/kernels/*.hip.
 #pragma once
 #include <cstddef>
@@ -178,5 +179,9 @@ void Sha256(const unsigned char* data, size_t len, unsigned char out[32]);
 void Sha256d(const unsigned char* data, size_t len, unsigned char out[32]);
 void Sha256d64(unsigned char* out, const unsigned char* in, size_t blocks); // N x (64 B -> 32 B)
 void Hash160(const unsigned char* data, size_t len, unsigned char out[20]);
+// The SHA-256 compression engine in use: "shani" (x86 SHA extensions, chosen when the CPU has
+// them) or "scalar". Setting is for tests and benchmarks; it is not thread-safe against hashing.
+std::string Sha256Implementation();
+bool Sha256SetImplementation(const std::string& name);
 
 } // namespace bcp

@@ -3,6 +3,7 @@
 #include "crypto/hashes.h"
 #include "crypto/common.h"
 
+#include <atomic>
 #include <cstring>
 
 namespace bcp {
@@ -25,7 +26,45 @@ const uint32_t H256[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                           0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
 } // namespace
 
+namespace sha256_x86 {
+bool Available();
+void Transform(uint32_t* s, const unsigned char* chunk, size_t blocks);
+} // namespace sha256_x86
+
+namespace {
+void TransformScalar(uint32_t* st, const unsigned char* chunk, size_t blocks);
+void TransformResolve(uint32_t* st, const unsigned char* chunk, size_t blocks);
+using TransformFn = void (*)(uint32_t*, const unsigned char*, size_t);
+// constant-initialised, so hashing during other translation units' static initialisation works;
+// the first call picks the engine
+std::atomic<TransformFn> g_transform{TransformResolve};
+
+void TransformResolve(uint32_t* st, const unsigned char* chunk, size_t blocks) {
+    const TransformFn f = sha256_x86::Available() ? sha256_x86::Transform : TransformScalar;
+    g_transform.store(f, std::memory_order_relaxed);
+    f(st, chunk, blocks);
+}
+} // namespace
+
 void CSHA256::Transform(uint32_t* st, const unsigned char* chunk, size_t blocks) {
+    g_transform.load(std::memory_order_relaxed)(st, chunk, blocks);
+}
+
+std::string Sha256Implementation() {
+    TransformFn f = g_transform.load();
+    if (f == TransformResolve) f = sha256_x86::Available() ? sha256_x86::Transform : TransformScalar;
+    return f == TransformScalar ? "scalar" : "shani";
+}
+
+bool Sha256SetImplementation(const std::string& name) {
+    if (name == "scalar") g_transform = TransformScalar;
+    else if (name == "shani" && sha256_x86::Available()) g_transform = sha256_x86::Transform;
+    else return false;
+    return true;
+}
+
+namespace {
+void TransformScalar(uint32_t* st, const unsigned char* chunk, size_t blocks) {
     while (blocks--) {
         uint32_t w[64];
         for (int i = 0; i < 16; ++i) w[i] = ReadBE32(chunk + 4 * i);
@@ -48,6 +87,7 @@ void CSHA256::Transform(uint32_t* st, const unsigned char* chunk, size_t blocks)
         chunk += 64;
     }
 }
+} // namespace
 
 CSHA256::CSHA256() : bytes(0) { memcpy(s, H256, sizeof(s)); }
 

@@ -212,9 +212,47 @@ const Coin& CCoinsViewCache::AccessCoin(const COutPoint& outpoint) const {
     return it->second.coin;
 }
 
+void CCoinsViewCache::SpendFetched(const COutPoint& outpoint, Coin&& coin, Coin* moveto) {
+    assert(!coin.IsSpent());
+    auto ins = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
+    assert(ins.second);
+    ins.first->second.flags = CCoinsCacheEntry::DIRTY; // not FRESH: the base holds the coin
+    if (moveto) *moveto = std::move(coin);
+}
+
 bool CCoinsViewCache::HaveCoin(const COutPoint& outpoint) const {
     auto it = FetchCoin(outpoint);
     return it != cacheCoins.end() && !it->second.coin.IsSpent();
+}
+
+bool CCoinsViewCache::PeekCoin(const COutPoint& outpoint, Coin& coin) const {
+    auto it = cacheCoins.find(outpoint);
+    if (it == cacheCoins.end()) return base->PeekCoin(outpoint, coin);
+    coin = it->second.coin; // a spent entry here hides the parent's coin
+    return true;
+}
+
+void CCoinsViewCache::PeekCoins(const COutPoint* outpoints, size_t n, Coin* coins, uint8_t* found) const {
+    std::vector<COutPoint> miss;
+    std::vector<size_t> where;
+    for (size_t i = 0; i < n; i++) {
+        auto it = cacheCoins.find(outpoints[i]);
+        if (it != cacheCoins.end()) {
+            coins[i] = it->second.coin;
+            found[i] = 1;
+        } else {
+            miss.push_back(outpoints[i]);
+            where.push_back(i);
+        }
+    }
+    if (miss.empty()) return;
+    std::vector<Coin> got(miss.size());
+    std::unique_ptr<uint8_t[]> ok(new uint8_t[miss.size()]);
+    base->PeekCoins(miss.data(), miss.size(), got.data(), ok.get());
+    for (size_t k = 0; k < miss.size(); k++) {
+        found[where[k]] = ok[k];
+        if (ok[k]) coins[where[k]] = std::move(got[k]);
+    }
 }
 
 bool CCoinsViewCache::HaveCoinInCache(const COutPoint& outpoint) const {

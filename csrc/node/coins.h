@@ -180,6 +180,13 @@ public:
     virtual bool BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlock) { return false; }
     virtual std::unique_ptr<CCoinsViewCursor> Cursor() const { return nullptr; }
     virtual size_t EstimateSize() const { return 0; }
+    // GetCoin without filling any cache on the way, so several threads may peek at once while
+    // nobody writes (the database view's reads are thread-safe; caches override this).
+    virtual bool PeekCoin(const COutPoint& outpoint, Coin& coin) const { return GetCoin(outpoint, coin); }
+    // PeekCoin of n outpoints at once (the database answers a batch under one lock).
+    virtual void PeekCoins(const COutPoint* outpoints, size_t n, Coin* coins, uint8_t* found) const {
+        for (size_t i = 0; i < n; i++) found[i] = PeekCoin(outpoints[i], coins[i]);
+    }
 };
 
 class CCoinsViewBacked : public CCoinsView {
@@ -211,13 +218,26 @@ public:
         throw std::logic_error("CCoinsViewCache cursor iteration not supported");
     }
 
+    bool PeekCoin(const COutPoint& outpoint, Coin& coin) const override;
+    void PeekCoins(const COutPoint* outpoints, size_t n, Coin* coins, uint8_t* found) const override;
     bool HaveCoinInCache(const COutPoint& outpoint) const;
     const Coin& AccessCoin(const COutPoint& output) const;
+    // This cache's own entry for an outpoint (spent or not), without asking the base.
+    const Coin* FindInCache(const COutPoint& outpoint) const {
+        auto it = cacheCoins.find(outpoint);
+        return it == cacheCoins.end() ? nullptr : &it->second.coin;
+    }
+    // SpendCoin of an unspent coin this cache does not hold yet, given the base's copy of it
+    // (read through PeekCoin while the stack below was as it is now): the same entry FetchCoin
+    // followed by SpendCoin would leave, without the round trip through the base.
+    void SpendFetched(const COutPoint& outpoint, Coin&& coin, Coin* moveto);
     void AddCoin(const COutPoint& outpoint, Coin&& coin, bool possible_overwrite);
     bool SpendCoin(const COutPoint& outpoint, Coin* moveto = nullptr);
     bool Flush();
     void Uncache(const COutPoint& outpoint);
     unsigned int GetCacheSize() const { return (unsigned)cacheCoins.size(); }
+    // Sizes the entry table for n entries up front (a block connect knows how many it adds).
+    void Reserve(size_t n) { cacheCoins.reserve(n); }
     size_t DynamicMemoryUsage() const;
     Amount GetValueIn(const CTransaction& tx) const;
     bool HaveInputs(const CTransaction& tx) const;

@@ -10,6 +10,7 @@
 #include <fcntl.h>
 #include <list>
 #include <stdexcept>
+#include <shared_mutex>
 #include <sys/file.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -619,8 +620,8 @@ struct KVStore::Impl {
     std::string dir;
     bool memOnly = false;
 
-    mutable std::mutex mu; // memtables, segment set, log, manifest
-    std::condition_variable cv;
+    mutable std::shared_mutex mu; // memtables, segment set, log, manifest (point reads share it)
+    std::condition_variable_any cv;
     std::shared_ptr<Memtable> mem;
     std::shared_ptr<const Memtable> imm; // sealed, being written out
     uint64_t immSealLog = 0, immMaxSeq = 0;
@@ -784,14 +785,14 @@ struct KVStore::Impl {
         }
         if (!ok) throw std::runtime_error("KVStore: cannot open the log in " + dir);
         if (!migrate) { // a migration's first manifest is the flush's: until then kv.log stays authoritative
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             if (!WriteManifestLocked()) throw std::runtime_error("KVStore: cannot write the manifest in " + dir);
         }
         flusher = std::thread([this] { FlusherLoop(); });
         merger = std::thread([this] { MergerLoop(); });
         if (migrate) {
             FlushAndWait();
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             if (bgError || segs->empty()) throw std::runtime_error("KVStore: migrating " + legacy + " failed");
             ::unlink(legacy.c_str());
             SyncDir(dir);
@@ -800,7 +801,7 @@ struct KVStore::Impl {
 
     void Close() {
         {
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             stop = true;
             stopping = true;
         }
@@ -825,7 +826,7 @@ struct KVStore::Impl {
     }
 
     // Seal the memtable: a fresh log takes the next writes; the flusher writes `imm` out.
-    bool SealLocked(std::unique_lock<std::mutex>& l) {
+    bool SealLocked(std::unique_lock<std::shared_mutex>& l) {
         // back-pressure: a second full memtable, or merges far behind (reads would check too
         // many segments), waits for the background threads
         while ((imm || (int)segs->size() > 3 * opt.maxSegments) && !bgError && !stop) {
@@ -849,7 +850,7 @@ struct KVStore::Impl {
     std::shared_ptr<Segment> WriteSegment(const Memtable& m, uint64_t maxSeq) {
         uint64_t id;
         {
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             id = nextFile++;
         }
         const std::string path = Numbered(dir, "seg", id, "sst");
@@ -863,7 +864,7 @@ struct KVStore::Impl {
     }
 
     void FlusherLoop() {
-        std::unique_lock<std::mutex> l(mu);
+        std::unique_lock<std::shared_mutex> l(mu);
         for (;;) {
             cv.wait(l, [&] { return stop || imm; });
             if (!imm) return; // stop, nothing pending
@@ -894,7 +895,7 @@ struct KVStore::Impl {
     bool NeedMergeLocked() const { return !merging && (int)segs->size() > opt.maxSegments; }
 
     void MergerLoop() {
-        std::unique_lock<std::mutex> l(mu);
+        std::unique_lock<std::shared_mutex> l(mu);
         for (;;) {
             cv.wait(l, [&] { return stop || NeedMergeLocked(); });
             if (stop) return;
@@ -909,7 +910,7 @@ struct KVStore::Impl {
         std::lock_guard<std::mutex> mg(mergeMu);
         std::shared_ptr<const SegList> cur;
         {
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             cur = segs;
             if (cur->empty() || (!full && (int)cur->size() <= opt.maxSegments)) return true;
             merging = true;
@@ -940,12 +941,12 @@ struct KVStore::Impl {
         }
         uint64_t id;
         {
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             id = nextFile++;
         }
         const std::string path = Numbered(dir, "seg", id, "sst");
         auto done = [&](bool ok) {
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             merging = false;
             if (!ok) bgError = true;
             cv.notify_all();
@@ -964,7 +965,7 @@ struct KVStore::Impl {
             if (win < 0) break;
             if (stopping.load(std::memory_order_relaxed)) { // (no lock per entry: writers hold mu for whole batches)
                 w.Abort();
-                std::lock_guard<std::mutex> l(mu);
+                std::lock_guard<std::shared_mutex> l(mu);
                 merging = false;
                 return false;
             }
@@ -984,7 +985,7 @@ struct KVStore::Impl {
             ::unlink(path.c_str());
         }
         {
-            std::lock_guard<std::mutex> l(mu);
+            std::lock_guard<std::shared_mutex> l(mu);
             // flushes only add at the front: the window is still contiguous, shifted
             auto next = std::make_shared<SegList>(*segs);
             auto it = std::find(next->begin(), next->end(), (*cur)[lo]);
@@ -1007,7 +1008,7 @@ struct KVStore::Impl {
     }
 
     void FlushAndWait() {
-        std::unique_lock<std::mutex> l(mu);
+        std::unique_lock<std::shared_mutex> l(mu);
         if (memOnly) return;
         if (!mem->m.empty() && !SealLocked(l)) return;
         cv.wait(l, [&] { return !imm || bgError; }); // also a memtable sealed by an earlier write
@@ -1024,7 +1025,7 @@ KVStore::~KVStore() {}
 
 bool KVStore::WriteBatch(KVBatch& batch, bool fSync) {
     if (batch.ops.empty()) return true;
-    std::unique_lock<std::mutex> l(d->mu);
+    std::unique_lock<std::shared_mutex> l(d->mu);
     if (d->bgError) return false;
     const uint64_t seq = ++d->seq;
     std::vector<RecOp> ops;
@@ -1066,7 +1067,7 @@ bool KVStore::WriteBatch(KVBatch& batch, bool fSync) {
 bool KVStore::ReadRaw(const std::string& key, std::string& value) const {
     std::shared_ptr<const SegList> s;
     {
-        std::lock_guard<std::mutex> l(d->mu);
+        std::shared_lock<std::shared_mutex> l(d->mu);
         auto it = d->mem->m.find(key);
         if (it != d->mem->m.end()) {
             if (it->second.del) return false;
@@ -1093,6 +1094,46 @@ bool KVStore::ReadRaw(const std::string& key, std::string& value) const {
     return false;
 }
 
+void KVStore::ReadRawMany(const std::string* keys, size_t n, std::string* values, uint8_t* found) const {
+    std::shared_ptr<const SegList> s;
+    std::vector<size_t> rest; // not decided by the memtables
+    {
+        std::shared_lock<std::shared_mutex> l(d->mu);
+        for (size_t i = 0; i < n; i++) {
+            found[i] = 0;
+            auto it = d->mem->m.find(keys[i]);
+            if (it != d->mem->m.end()) {
+                if (!it->second.del) {
+                    values[i] = it->second.value;
+                    found[i] = 1;
+                }
+                continue;
+            }
+            if (d->imm) {
+                auto jt = d->imm->m.find(keys[i]);
+                if (jt != d->imm->m.end()) {
+                    if (!jt->second.del) {
+                        values[i] = jt->second.value;
+                        found[i] = 1;
+                    }
+                    continue;
+                }
+            }
+            rest.push_back(i);
+        }
+        s = d->segs;
+    }
+    if (s->empty()) return;
+    for (size_t i : rest) {
+        const uint64_t h = Hash64(keys[i].data(), keys[i].size());
+        for (const auto& seg : *s) {
+            const int r = seg->Get(keys[i], h, &values[i]);
+            if (r == 1) found[i] = 1;
+            if (r != 0) break; // found, tombstone, or an unreadable block
+        }
+    }
+}
+
 bool KVStore::ExistsRaw(const std::string& key) const {
     std::string v;
     return ReadRaw(key, v);
@@ -1115,7 +1156,7 @@ size_t KVStore::EstimateSize(const std::string& begin, const std::string& end) c
     std::shared_ptr<const SegList> s;
     size_t n = 0;
     {
-        std::lock_guard<std::mutex> l(d->mu);
+        std::lock_guard<std::shared_mutex> l(d->mu);
         for (auto* m : {d->mem.get(), const_cast<Memtable*>(d->imm.get())}) {
             if (!m) continue;
             for (auto it = m->m.lower_bound(begin); it != m->m.end() && it->first < end; ++it)
@@ -1140,7 +1181,7 @@ void KVStore::Compact() {
 }
 
 uint64_t KVStore::LogBytes() const {
-    std::lock_guard<std::mutex> l(d->mu);
+    std::lock_guard<std::shared_mutex> l(d->mu);
     uint64_t n = d->logBytes;
     for (const auto& s : *d->segs) n += s->fileBytes;
     return n;
@@ -1148,7 +1189,7 @@ uint64_t KVStore::LogBytes() const {
 
 KVStats KVStore::Stats() const {
     KVStats st;
-    std::lock_guard<std::mutex> l(d->mu);
+    std::lock_guard<std::shared_mutex> l(d->mu);
     st.segments = d->segs->size();
     for (const auto& s : *d->segs) {
         st.segmentBytes += s->fileBytes;
@@ -1277,7 +1318,7 @@ KVIterator::~KVIterator() {}
 void KVIterator::Seek(const std::string& k) {
     KVStore::Impl& I = *db->d;
     {
-        std::lock_guard<std::mutex> l(I.mu);
+        std::lock_guard<std::shared_mutex> l(I.mu);
         st->imm = I.imm;
         st->segs = I.segs;
         auto it = I.mem->m.lower_bound(k);
@@ -1341,7 +1382,7 @@ void KVIterator::Settle() {
         }
         // advance every source past `key`
         {
-            std::lock_guard<std::mutex> l(I.mu);
+            std::lock_guard<std::shared_mutex> l(I.mu);
             auto it = I.mem->m.upper_bound(key);
             s.memValid = it != I.mem->m.end();
             if (s.memValid) {

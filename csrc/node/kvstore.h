@@ -177,6 +177,9 @@ public:
     }
     bool WriteBatch(KVBatch& batch, bool fSync = false);
     bool ReadRaw(const std::string& key, std::string& value) const;
+    // ReadRaw of n keys under one acquisition of the store lock (batched lookups from many
+    // threads would otherwise contend on it per key): found[i] says whether values[i] is set.
+    void ReadRawMany(const std::string* keys, size_t n, std::string* values, uint8_t* found) const;
     bool ExistsRaw(const std::string& key) const;
     bool IsEmpty() const;
     size_t Count() const; // live keys (a full scan)

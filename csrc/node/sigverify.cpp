@@ -120,6 +120,14 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
 
 bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, const std::vector<DeferredMultisig>& groups,
                            WorkerPool* pool, bool useGpu, bool cacheStore, bool cacheErase) {
+    std::vector<const DeferredSigCheck*> ptrs(checks.size());
+    for (size_t i = 0; i < checks.size(); i++) ptrs[i] = &checks[i];
+    return BatchVerifySignatures(ptrs, groups, pool, useGpu, cacheStore, cacheErase);
+}
+
+bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
+                           const std::vector<DeferredMultisig>& groups, WorkerPool* pool, bool useGpu,
+                           bool cacheStore, bool cacheErase) {
     if (checks.empty()) return groups.empty();
     // speculative pairs of deferred multisig groups: their individual results are kept, and a false
     // one does not fail the batch
@@ -136,7 +144,7 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, const std::vec
     uint64_t hits = 0;
     // cache keys are one SHA-256 each: on the pool (the cache takes concurrent lookups)
     auto probe = [&](size_t i) {
-        const DeferredSigCheck& c = checks[i];
+        const DeferredSigCheck& c = *checks[i];
         entries[i] = cache.Entry(c.sighash, c.sig.data(), c.sig.size(), c.pubkey.data(), c.pubkey.size());
         hit[i] = cache.Get(entries[i], cacheErase);
     };
@@ -159,7 +167,7 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, const std::vec
         const int64_t t0 = GetTimeMicros();
         if (gpu) {
             std::vector<const DeferredSigCheck*> ptrs(n);
-            for (size_t j = 0; j < n; j++) ptrs[j] = &checks[todo[j]];
+            for (size_t j = 0; j < n; j++) ptrs[j] = checks[todo[j]];
             std::vector<uint8_t> r;
             try {
                 r = GpuVerifyDeferred(ptrs, pool);
@@ -194,7 +202,7 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, const std::vec
             auto work = [&](size_t j) {
                 if (!allOk.load(std::memory_order_relaxed)) return;
                 const size_t i = todo[j];
-                const DeferredSigCheck& c = checks[i];
+                const DeferredSigCheck& c = *checks[i];
                 res[i] = secp::VerifySignature(c.pubkey.data(), c.pubkey.size(), c.sig.data(), c.sig.size(),
                                                c.sighash.begin());
                 if (!res[i]) {

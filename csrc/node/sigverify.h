@@ -63,6 +63,11 @@ bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, WorkerPool* po
 // legal), and each group must pass its replayed greedy match instead.
 bool BatchVerifySignatures(std::vector<DeferredSigCheck>& checks, const std::vector<DeferredMultisig>& groups,
                            WorkerPool* pool, bool useGpu, bool cacheStore, bool cacheErase);
+// Same, over checks that stay where they were produced (the block path's per-job sinks): no copy
+// into one array first.
+bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
+                           const std::vector<DeferredMultisig>& groups, WorkerPool* pool, bool useGpu,
+                           bool cacheStore, bool cacheErase);
 // Device verification of the given checks (no cache); result[i] = 1 iff valid.
 std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool);
 void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path

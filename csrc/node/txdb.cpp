@@ -71,6 +71,21 @@ CCoinsViewDB::CCoinsViewDB(const std::string& dir, bool fMemory, bool fWipe, siz
 bool CCoinsViewDB::GetCoin(const COutPoint& outpoint, Coin& coin) const { return db.Read(CoinKey(&outpoint), coin); }
 bool CCoinsViewDB::HaveCoin(const COutPoint& outpoint) const { return db.Exists(CoinKey(&outpoint)); }
 
+void CCoinsViewDB::PeekCoins(const COutPoint* outpoints, size_t n, Coin* coins, uint8_t* found) const {
+    std::vector<std::string> keys(n), values(n);
+    for (size_t i = 0; i < n; i++) keys[i] = KVBatch::Ser(CoinKey(&outpoints[i]));
+    db.ReadRawMany(keys.data(), n, values.data(), found);
+    for (size_t i = 0; i < n; i++) {
+        if (!found[i]) continue;
+        try {
+            SpanReader r((const unsigned char*)values[i].data(), values[i].size(), SER_DISK, PROTOCOL_VERSION);
+            r >> coins[i];
+        } catch (const std::exception&) {
+            found[i] = 0; // as Read() treats an undecodable value
+        }
+    }
+}
+
 uint256 CCoinsViewDB::GetBestBlock() const {
     uint256 h;
     if (!db.Read(DB_BEST_BLOCK, h)) return uint256();

@@ -66,6 +66,7 @@ public:
     CCoinsViewDB(const std::string& dir, bool fMemory, bool fWipe, size_t nCacheSize = 8u << 20);
     bool GetCoin(const COutPoint& outpoint, Coin& coin) const override;
     bool HaveCoin(const COutPoint& outpoint) const override;
+    void PeekCoins(const COutPoint* outpoints, size_t n, Coin* coins, uint8_t* found) const override;
     uint256 GetBestBlock() const override;
     std::vector<uint256> GetHeadBlocks() const;
     bool BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlock) override;

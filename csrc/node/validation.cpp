@@ -449,7 +449,7 @@ bool Chainstate::FindBlockPos(CValidationState& state, CDiskBlockPos& pos, unsig
     unsigned nFile = fKnown ? pos.nFile : nLastBlockFile;
     if (vinfoBlockFile.size() <= nFile) vinfoBlockFile.resize(nFile + 1);
     if (!fKnown) {
-        while (vinfoBlockFile[nFile].nSize + nAddSize >= MAX_BLOCKFILE_SIZE) {
+        while (vinfoBlockFile[nFile].nSize + nAddSize >= FileSizes().maxFile) {
             nFile++;
             if (vinfoBlockFile.size() <= nFile) vinfoBlockFile.resize(nFile + 1);
         }
@@ -465,13 +465,14 @@ bool Chainstate::FindBlockPos(CValidationState& state, CDiskBlockPos& pos, unsig
     if (fKnown) vinfoBlockFile[nFile].nSize = std::max(pos.nPos + nAddSize, vinfoBlockFile[nFile].nSize);
     else vinfoBlockFile[nFile].nSize += nAddSize;
     if (!fKnown) {
-        const unsigned nOldChunks = (pos.nPos + BLOCKFILE_CHUNK_SIZE - 1) / BLOCKFILE_CHUNK_SIZE;
-        const unsigned nNewChunks = (vinfoBlockFile[nFile].nSize + BLOCKFILE_CHUNK_SIZE - 1) / BLOCKFILE_CHUNK_SIZE;
+        const unsigned chunk = FileSizes().blockChunk;
+        const unsigned nOldChunks = (pos.nPos + chunk - 1) / chunk;
+        const unsigned nNewChunks = (vinfoBlockFile[nFile].nSize + chunk - 1) / chunk;
         if (nNewChunks > nOldChunks) {
             if (PruneMode()) fCheckForPruning = true;
             FILE* file = OpenBlockFile(pos);
             if (file) {
-                AllocateFileRange(file, pos.nPos, nNewChunks * BLOCKFILE_CHUNK_SIZE - pos.nPos);
+                AllocateFileRange(file, pos.nPos, nNewChunks * chunk - pos.nPos);
                 fclose(file);
             } else {
                 return state.Error("out of disk space");
@@ -487,13 +488,14 @@ bool Chainstate::FindUndoPos(CValidationState& state, int nFile, CDiskBlockPos& 
     const unsigned nNewSize = vinfoBlockFile[nFile].nUndoSize += nAddSize;
     pos.nPos = nNewSize - nAddSize;
     setDirtyFileInfo.insert(nFile);
-    const unsigned nOldChunks = (pos.nPos + UNDOFILE_CHUNK_SIZE - 1) / UNDOFILE_CHUNK_SIZE;
-    const unsigned nNewChunks = (nNewSize + UNDOFILE_CHUNK_SIZE - 1) / UNDOFILE_CHUNK_SIZE;
+    const unsigned chunk = FileSizes().undoChunk;
+    const unsigned nOldChunks = (pos.nPos + chunk - 1) / chunk;
+    const unsigned nNewChunks = (nNewSize + chunk - 1) / chunk;
     if (nNewChunks > nOldChunks) {
         if (PruneMode()) fCheckForPruning = true;
         FILE* file = OpenUndoFile(pos);
         if (!file) return state.Error("out of disk space");
-        AllocateFileRange(file, pos.nPos, nNewChunks * UNDOFILE_CHUNK_SIZE - pos.nPos);
+        AllocateFileRange(file, pos.nPos, nNewChunks * chunk - pos.nPos);
         fclose(file);
     }
     return true;
@@ -701,6 +703,14 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     const Consensus::Params& cp = params.GetConsensus();
     if (!CheckBlock(block, state, !fJustCheck, !fJustCheck))
         return error("%s: Consensus::CheckBlock: %s", __func__, FormatStateMessage(state).c_str());
+    int64_t tPhase = nTimeStart;
+    auto phase = [&](ConnectPhase ph) {
+        const int64_t t = GetTimeMicros();
+        phaseMicros[ph].fetch_add(t - tPhase, std::memory_order_relaxed);
+        tPhase = t;
+    };
+    phase(PH_CHECK);
+    phaseMicros[PH_BLOCKS].fetch_add(1, std::memory_order_relaxed);
     const uint256 hashPrevBlock = pindex->pprev == nullptr ? uint256() : pindex->pprev->GetBlockHash();
     if (hashPrevBlock != view.GetBestBlock()) return state.Error("ConnectBlock: view best block mismatch");
     if (block.GetHash(cp) == cp.hashGenesisBlock) {
@@ -727,13 +737,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
            pindex->GetBlockHash() == uint256S("0x00000000000743f190a18c5577a3c2d2a1f610ae9601ac046a38084ccb7cd721")));
     const CBlockIndex* pindexBIP34height = pindex->pprev->GetAncestor(cp.BIP34Height);
     fEnforceBIP30 = fEnforceBIP30 && (!pindexBIP34height || !(pindexBIP34height->GetBlockHash() == cp.BIP34Hash));
-    if (fEnforceBIP30) {
-        for (const auto& tx : block.vtx)
-            for (size_t o = 0; o < tx->vout.size(); o++)
-                if (view.HaveCoin(COutPoint(tx->GetHash(), (uint32_t)o)))
-                    return state.DoS(100, error("ConnectBlock(): tried to overwrite transaction"), REJECT_INVALID,
-                                     "bad-txns-BIP30");
-    }
     int nLockTimeFlags = 0;
     if (VersionBitsState(pindex->pprev, cp, Consensus::DEPLOYMENT_CSV, versionbitscache) == THRESHOLD_ACTIVE)
         nLockTimeFlags |= LOCKTIME_VERIFY_SEQUENCE;
@@ -754,23 +757,70 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     const size_t ntx = block.vtx.size();
     ScriptCache& sc = GetScriptCache();
 
-    // Per-transaction work that needs no coins runs on the pool first: the BIP143-style sighash
-    // midstates (PrecomputedTransactionData), the script-cache key and the serialized size.
+    // One parallel, read-only pass over the block before anything writes the view stack:
+    //  * BIP30: no output of the block may already exist unspent;
+    //  * every input's coin is fetched (PeekCoin: through the caches to the database without
+    //    filling them), so the serial pass below inserts it into the view instead of walking the
+    //    view stack itself - a coin created or spent earlier in this block is found in the view
+    //    first, so the prefetched copy of an outpoint is only used while it is still current;
+    //  * the per-transaction work that needs no coins: the BIP143-style sighash midstates
+    //    (PrecomputedTransactionData), the script-cache key, the serialized size and the legacy
+    //    sigop count.
     std::vector<std::unique_ptr<PrecomputedTransactionData>> txdatas(ntx);
     std::vector<uint256> scKeys(ntx);
-    std::vector<uint32_t> txSizes(ntx);
-    size_t maxJobs = 0;
-    for (size_t i = 1; i < ntx; i++) maxJobs += block.vtx[i]->vin.size();
+    std::vector<uint32_t> txSizes(ntx), legacySigOps(ntx);
+    std::vector<size_t> firstInput(ntx + 1, 0); // tx i's inputs are [firstInput[i], firstInput[i+1])
+    size_t nOutputs = 0;
+    for (size_t i = 0; i < ntx; i++) {
+        firstInput[i + 1] = firstInput[i] + (i > 0 ? block.vtx[i]->vin.size() : 0);
+        nOutputs += block.vtx[i]->vout.size();
+    }
+    const size_t maxJobs = firstInput[ntx];
+    std::vector<Coin> prefetched(maxJobs);
+    std::unique_ptr<uint8_t[]> prefetchedFound(new uint8_t[maxJobs + 1]);
+    std::atomic<bool> bip30Clash{false};
+    // chunks of transactions, each chunk's coin lookups sent down the view stack as one batch
+    const size_t CHUNK = 48;
     pool->ParallelFor(
-        ntx,
-        [&](size_t i) {
-            const CTransaction& tx = *block.vtx[i];
-            txSizes[i] = (uint32_t)GetSerializeSize(tx, PROTOCOL_VERSION);
-            if (i == 0 || !fScriptChecks) return;
-            scKeys[i] = sc.Key(tx, flags);
-            txdatas[i].reset(new PrecomputedTransactionData(tx));
+        (ntx + CHUNK - 1) / CHUNK,
+        [&](size_t chunk) {
+            const size_t lo = chunk * CHUNK, hi = std::min(ntx, lo + CHUNK);
+            std::vector<COutPoint> keys;
+            for (size_t i = lo; i < hi; i++) {
+                const CTransaction& tx = *block.vtx[i];
+                if (fEnforceBIP30)
+                    for (size_t o = 0; o < tx.vout.size(); o++) keys.emplace_back(tx.GetHash(), (uint32_t)o);
+                if (i > 0)
+                    for (const CTxIn& in : tx.vin) keys.push_back(in.prevout);
+            }
+            std::vector<Coin> got(keys.size());
+            std::unique_ptr<uint8_t[]> found(new uint8_t[keys.size() + 1]);
+            view.PeekCoins(keys.data(), keys.size(), got.data(), found.get());
+            size_t q = 0;
+            for (size_t i = lo; i < hi; i++) {
+                const CTransaction& tx = *block.vtx[i];
+                if (fEnforceBIP30)
+                    for (size_t o = 0; o < tx.vout.size(); o++, q++)
+                        if (found[q] && !got[q].IsSpent()) bip30Clash = true;
+                if (i > 0)
+                    for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++, q++) {
+                        prefetchedFound[k] = found[q];
+                        if (found[q]) prefetched[k] = std::move(got[q]);
+                    }
+                txSizes[i] = (uint32_t)GetSerializeSize(tx, PROTOCOL_VERSION);
+                legacySigOps[i] = (uint32_t)GetSigOpCountWithoutP2SH(tx);
+                if (i > 0 && fScriptChecks) {
+                    scKeys[i] = sc.Key(tx, flags);
+                    txdatas[i].reset(new PrecomputedTransactionData(tx));
+                }
+            }
         },
-        64);
+        1);
+    if (bip30Clash)
+        return state.DoS(100, error("ConnectBlock(): tried to overwrite transaction"), REJECT_INVALID, "bad-txns-BIP30");
+    // the view gains about one entry per input and output: size its table once
+    view.Reserve(view.GetCacheSize() + maxJobs + nOutputs);
+    phase(PH_PRECOMPUTE);
 
     // Script checks overlap the UTXO pass (reference CCheckQueue: the master keeps connecting
     // while workers run the queued CScriptChecks, src/validation.cpp:2011-2127). The loop below
@@ -798,38 +848,77 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         ~CompleteOnExit() { q.Complete(); }
     } completeOnExit{*scriptQueue};
 
+    // The serial UTXO pass. Each input's coin is taken from the view (or the prefetch) once; the
+    // checks below used to go back to the view for it six times (HaveInputs, the height list,
+    // the P2SH sigop count, GetValueIn, CheckTxInputs, SpendCoin). The references stay valid
+    // while the view grows.
+    std::vector<const Coin*> coins;
+    std::vector<uint8_t> fromPrefetch;
     for (size_t i = 0; i < ntx; i++) {
         const CTransaction& tx = *block.vtx[i];
         nInputs += (int)tx.vin.size();
         if (!tx.IsCoinBase()) {
-            if (!view.HaveInputs(tx))
-                return state.DoS(100, error("ConnectBlock(): inputs missing/spent"), REJECT_INVALID,
-                                 "bad-txns-inputs-missingorspent");
+            coins.resize(tx.vin.size());
+            fromPrefetch.resize(tx.vin.size());
+            for (size_t j = 0; j < tx.vin.size(); j++) {
+                // the view's own entry (a coin created or spent earlier in the block) wins
+                const size_t k = firstInput[i] + j;
+                const Coin* c = view.FindInCache(tx.vin[j].prevout);
+                fromPrefetch[j] = c == nullptr;
+                if (!c && prefetchedFound[k]) c = &prefetched[k];
+                if (!c || c->IsSpent())
+                    return state.DoS(100, error("ConnectBlock(): inputs missing/spent"), REJECT_INVALID,
+                                     "bad-txns-inputs-missingorspent");
+                coins[j] = c;
+            }
             prevheights.resize(tx.vin.size());
-            for (size_t j = 0; j < tx.vin.size(); j++) prevheights[j] = view.AccessCoin(tx.vin[j].prevout).GetHeight();
+            for (size_t j = 0; j < tx.vin.size(); j++) prevheights[j] = coins[j]->GetHeight();
             if (!SequenceLocks(tx, nLockTimeFlags, &prevheights, *pindex))
                 return state.DoS(100, error("%s: contains a non-BIP68-final transaction", __func__), REJECT_INVALID,
                                  "bad-txns-nonfinal");
         }
-        const uint64_t txSigOps = GetTransactionSigOpCount(tx, view, flags);
+        // GetTransactionSigOpCount over the looked-up coins
+        uint64_t txSigOps = legacySigOps[i];
+        if (!tx.IsCoinBase() && (flags & SCRIPT_VERIFY_P2SH))
+            for (size_t j = 0; j < tx.vin.size(); j++) {
+                const CScript& spk = coins[j]->GetTxOut().scriptPubKey;
+                if (spk.IsPayToScriptHash()) txSigOps += spk.GetSigOpCount(tx.vin[j].scriptSig);
+            }
         if (txSigOps > MAX_TX_SIGOPS_COUNT) return state.DoS(100, false, REJECT_INVALID, "bad-txn-sigops");
         nSigOpsCount += txSigOps;
         if (nSigOpsCount > nMaxSigOpsCount)
             return state.DoS(100, error("ConnectBlock(): too many sigops"), REJECT_INVALID, "bad-blk-sigops");
         if (!tx.IsCoinBase()) {
-            nFees += view.GetValueIn(tx) - tx.GetValueOut();
-            if (!Consensus::CheckTxInputs(tx, state, view, pindex->nHeight))
-                return error("ConnectBlock(): CheckTxInputs on %s failed with %s", tx.GetHash().ToString().c_str(),
-                             FormatStateMessage(state).c_str());
+            // Consensus::CheckTxInputs over the looked-up coins; on any failure the original runs
+            // for the exact reject reason
+            Amount in = 0;
+            bool ok = true;
+            for (size_t j = 0; j < tx.vin.size() && ok; j++) {
+                const Coin& c = *coins[j];
+                if (c.IsCoinBase() && pindex->nHeight - (int)c.GetHeight() < COINBASE_MATURITY) ok = false;
+                in += c.GetTxOut().nValue;
+                if (!MoneyRange(c.GetTxOut().nValue) || !MoneyRange(in)) ok = false;
+            }
+            const Amount out = tx.GetValueOut();
+            if (!ok || in < out || !MoneyRange(in - out)) {
+                if (!Consensus::CheckTxInputs(tx, state, view, pindex->nHeight))
+                    return error("ConnectBlock(): CheckTxInputs on %s failed with %s", tx.GetHash().ToString().c_str(),
+                                 FormatStateMessage(state).c_str());
+                return state.Error("ConnectBlock: input checks disagree");
+            }
+            nFees += in - out;
         }
         CTxUndo undoDummy;
         if (i > 0) blockundo.vtxundo.push_back(CTxUndo());
         CTxUndo& undo = i == 0 ? undoDummy : blockundo.vtxundo.back();
         if (!tx.IsCoinBase()) {
             undo.vprevout.reserve(tx.vin.size());
-            for (const CTxIn& in : tx.vin) {
+            for (size_t j = 0; j < tx.vin.size(); j++) {
                 undo.vprevout.emplace_back();
-                if (!view.SpendCoin(in.prevout, &undo.vprevout.back())) return state.Error("ConnectBlock: spend failed");
+                if (fromPrefetch[j])
+                    view.SpendFetched(tx.vin[j].prevout, std::move(prefetched[firstInput[i] + j]), &undo.vprevout.back());
+                else if (!view.SpendCoin(tx.vin[j].prevout, &undo.vprevout.back()))
+                    return state.Error("ConnectBlock: spend failed");
             }
             // transactions fully validated under these flags in the mempool skip re-execution; the
             // jobs read the spent coins from the undo record (reserved up front: the addresses are
@@ -841,7 +930,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 }
                 nProduced += tx.vin.size();
                 // publish in groups: each publish takes the queue lock and may wake a worker
-                if (nProduced - nPublished >= 16) {
+                if (nProduced - nPublished >= 512) {
                     scriptQueue->Publish(nProduced);
                     nPublished = nProduced;
                 }
@@ -852,6 +941,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         pos.nTxOffset += txSizes[i];
     }
     const int64_t nTime2 = GetTimeMicros();
+    phase(PH_UTXO);
 
     const Amount blockReward = nFees + GetBlockSubsidy(pindex->nHeight, cp);
     if (block.vtx[0]->GetValueOut() > blockReward)
@@ -863,6 +953,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // ---- remaining scripts, then one ECDSA batch (GPU when large enough)
     scriptQueue->Publish(nProduced);
     scriptQueue->Complete();
+    phase(PH_SCRIPTS);
     const size_t nJobs = nProduced;
     p.nJobs = nJobs;
     p.postfork = postfork;
@@ -871,28 +962,35 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     if (nJobs > 0) {
         bool ok = !anyFail.load();
         if (ok) {
-            size_t total = 0;
-            for (size_t k = 0; k < nJobs; k++) total += sinks[k].size();
-            std::vector<DeferredSigCheck> all;
+            // the batch reads the checks where the jobs left them: a pointer per check
+            std::vector<size_t> off(nJobs + 1, 0);
+            for (size_t k = 0; k < nJobs; k++) off[k + 1] = off[k] + sinks[k].size();
+            std::vector<const DeferredSigCheck*> all(off[nJobs]);
             std::vector<DeferredMultisig> groups;
-            all.reserve(total);
-            for (size_t k = 0; k < nJobs; k++) {
-                for (DeferredMultisig g : groupSinks[k]) { // rebase onto the concatenated batch
-                    g.first += (uint32_t)all.size();
+            for (size_t k = 0; k < nJobs; k++)
+                for (DeferredMultisig g : groupSinks[k]) { // rebase onto the flat numbering
+                    g.first += (uint32_t)off[k];
                     groups.push_back(g);
                 }
-                for (auto& c : sinks[k]) all.push_back(std::move(c));
-            }
+            pool->ParallelFor(
+                nJobs,
+                [&](size_t k) {
+                    for (size_t j = 0; j < sinks[k].size(); j++) all[off[k] + j] = &sinks[k][j];
+                },
+                512);
+            phase(PH_COLLECT);
             if (async) {
-                // the batch owns its checks; the pool is shared (ParallelFor calls serialise)
+                // the batch owns the sinks (moving the outer vector keeps every check in place);
+                // the pool is shared (ParallelFor calls serialise)
                 WorkerPool* wp = pool.get();
                 const bool useGpu = opts.useGpu, erase = !fJustCheck;
-                p.sigs = std::async(std::launch::async,
-                                    [wp, useGpu, erase, all = std::move(all), groups = std::move(groups)]() mutable {
-                                        return BatchVerifySignatures(all, groups, wp, useGpu, false, erase);
-                                    });
+                p.sigs = std::async(std::launch::async, [wp, useGpu, erase, sinks = std::move(sinks), all = std::move(all),
+                                                         groups = std::move(groups)]() mutable {
+                    return BatchVerifySignatures(all, groups, wp, useGpu, false, erase);
+                });
             } else {
                 ok = BatchVerifySignatures(all, groups, pool.get(), opts.useGpu, false, !fJustCheck);
+                phase(PH_BATCH);
             }
         }
         p.sigsOk = ok;

@@ -203,6 +203,12 @@ public:
     void WaitForBlockChange(int64_t timeoutMillis, const uint256& from);
     std::condition_variable_any& BlockChangeCV() { return cvBlockChange; }
     int64_t LastBlockConnectMicros() const { return nLastConnectMicros; }
+    // Cumulative wall time (microseconds) of ConnectBlockPrepare's phases, for -debug=bench and
+    // the connect benchmarks: CheckBlock, the parallel read-only pass (BIP30, input prefetch,
+    // per-tx precompute), the serial UTXO pass, the wait for
+    // the script jobs after it, gathering the deferred checks, and the synchronous batch verify.
+    enum ConnectPhase { PH_CHECK, PH_PRECOMPUTE, PH_UTXO, PH_SCRIPTS, PH_COLLECT, PH_BATCH, PH_BLOCKS, PH_COUNT };
+    int64_t ConnectPhaseMicros(ConnectPhase ph) const { return phaseMicros[ph].load(std::memory_order_relaxed); }
 
 private:
     struct WorkComparator {
@@ -293,6 +299,7 @@ private:
     mutable std::atomic<bool> latchToFalse{false};
     int64_t nLastWrite = 0, nLastFlush = 0, nLastSetChain = 0;
     std::atomic<int64_t> nLastConnectMicros{0};
+    std::atomic<int64_t> phaseMicros[PH_COUNT] = {};
 
     std::unique_ptr<CBlockTreeDB> pblocktree;
     std::unique_ptr<CCoinsViewDB> pcoinsdbview;

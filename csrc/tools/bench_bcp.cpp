@@ -542,7 +542,7 @@ BigBlockFixture& BigBlock(int kind) {
     if (!mkdtemp(tmpl)) throw std::runtime_error("bench: mkdtemp failed");
     o.datadir = tmpl;
     o.useGpu = gpu::GpuAvailable();
-    o.scriptThreads = std::min(16, std::max(2, GetNumCores()));
+    o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
     f.cs.reset(new Chainstate(Params(), o));
     std::string err;
     if (!f.cs->InitBlockIndex(err)) throw std::runtime_error("bench: " + err);
@@ -695,6 +695,8 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
     const size_t thr = GetGpuSigThreshold();
     SetGpuSigThreshold(useGpu ? DEFAULT_GPU_SIG_THRESHOLD : SIZE_MAX);
     const SigVerifyStats s0 = GetSigVerifyStats();
+    int64_t ph0[Chainstate::PH_COUNT];
+    for (int k = 0; k < Chainstate::PH_COUNT; k++) ph0[k] = f.cs->ConnectPhaseMicros((Chainstate::ConnectPhase)k);
     int iters = 0;
     while (st.KeepRunning()) {
         CValidationState state;
@@ -712,6 +714,11 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
             (double)(s1.cpu_sigs - s0.cpu_sigs) / iters, (s1.cpu_ms - s0.cpu_ms) / iters,
             (unsigned long long)(s1.gpu_failures - s0.gpu_failures),
             (double)(s1.multisig_groups - s0.multisig_groups) / iters);
+    auto ms = [&](Chainstate::ConnectPhase k) { return 0.001 * (f.cs->ConnectPhaseMicros(k) - ph0[k]) / iters; };
+    fprintf(stderr, "# %s: connect phases (ms/block): checkblock %.2f, prefetch+precompute %.2f, utxo pass %.2f, "
+                    "script wait %.2f, collect %.2f, batch %.2f\n",
+            useGpu ? "GPU" : "CPU", ms(Chainstate::PH_CHECK), ms(Chainstate::PH_PRECOMPUTE), ms(Chainstate::PH_UTXO),
+            ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_COLLECT), ms(Chainstate::PH_BATCH));
     SetGpuSigThreshold(thr);
 }
 } // namespace
@@ -803,7 +810,7 @@ IbdFixture& Ibd() {
     if (!mkdtemp(tmpl)) throw std::runtime_error("bench: mkdtemp failed");
     o.datadir = tmpl;
     o.useGpu = false; // the builder only assembles; validation speed is measured on fresh nodes
-    o.scriptThreads = std::min(16, std::max(2, GetNumCores()));
+    o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
     Chainstate cs(Params(), o);
     CTxMemPool pool;
     std::string err;
@@ -897,7 +904,7 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         o.datadir = tmpl;
         o.useGpu = useGpu;
         o.connectPipeline = pipeline;
-        o.scriptThreads = std::min(16, std::max(2, GetNumCores()));
+        o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
         Chainstate cs(Params(), o);
         std::string err;
         if (!cs.InitBlockIndex(err)) throw std::runtime_error("bench: " + err);
