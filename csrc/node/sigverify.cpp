@@ -142,15 +142,20 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
     std::vector<size_t> todo;
     todo.reserve(checks.size());
     uint64_t hits = 0;
-    // cache keys are one SHA-256 each: on the pool (the cache takes concurrent lookups)
-    auto probe = [&](size_t i) {
-        const DeferredSigCheck& c = *checks[i];
-        entries[i] = cache.Entry(c.sighash, c.sig.data(), c.sig.size(), c.pubkey.data(), c.pubkey.size());
-        hit[i] = cache.Get(entries[i], cacheErase);
+    // cache keys are one SHA-256 each: on the pool, in chunks whose lookups share one lock
+    const size_t PROBE_CHUNK = 256;
+    auto probe = [&](size_t chunk) {
+        const size_t lo = chunk * PROBE_CHUNK, hi = std::min(checks.size(), lo + PROBE_CHUNK);
+        for (size_t i = lo; i < hi; i++) {
+            const DeferredSigCheck& c = *checks[i];
+            entries[i] = cache.Entry(c.sighash, c.sig.data(), c.sig.size(), c.pubkey.data(), c.pubkey.size());
+        }
+        cache.GetMany(&entries[lo], hi - lo, cacheErase, &hit[lo]);
     };
-    if (pool && checks.size() >= 1024) pool->ParallelFor(checks.size(), probe, 256);
+    const size_t nChunks = (checks.size() + PROBE_CHUNK - 1) / PROBE_CHUNK;
+    if (pool && nChunks > 1) pool->ParallelFor(nChunks, probe, 1);
     else
-        for (size_t i = 0; i < checks.size(); i++) probe(i);
+        for (size_t k = 0; k < nChunks; k++) probe(k);
     for (size_t i = 0; i < checks.size(); i++) {
         if (hit[i]) {
             hits++;

@@ -24,6 +24,9 @@ public:
     SignatureCache();
     bool Get(const uint256& entry, bool erase) const { return set.contains(entry, erase); }
     void Set(const uint256& entry) { set.insert(entry); }
+    void GetMany(const uint256* entries, size_t n, bool erase, uint8_t* hit) const {
+        set.contains_many(entries, n, erase, hit);
+    }
     uint256 Entry(const uint256& sighash, const unsigned char* sig, size_t sigLen, const unsigned char* pubkey,
                   size_t pubLen) const;
     uint256 Entry(const uint256& sighash, const std::vector<unsigned char>& sig,

@@ -184,6 +184,12 @@ public:
         std::unique_lock<std::shared_mutex> l(m);
         set.insert(k);
     }
+    // contains() of n keys under one shared acquisition: many threads probing a block's worth
+    // of entries one lock round trip each would serialise on the lock's cache line.
+    void contains_many(const uint256* k, size_t n, bool erase, uint8_t* out) const {
+        std::shared_lock<std::shared_mutex> l(m);
+        for (size_t i = 0; i < n; i++) out[i] = set.contains(k[i], erase);
+    }
     size_t capacity() const {
         std::shared_lock<std::shared_mutex> l(m);
         return set.capacity();
