@@ -470,6 +470,10 @@ void PeerLogicValidation::Misbehaving(NodeId id, int howmuch, const std::string&
     impl->MisbehavingLocked(id, howmuch, reason);
 }
 
+bool PeerLogicValidation::AddOrphanTx(const CTransactionRef& tx, NodeId peer) { return impl->AddOrphanTx(tx, peer); }
+void PeerLogicValidation::EraseOrphansFor(NodeId peer) { impl->EraseOrphansFor(peer); }
+unsigned PeerLogicValidation::LimitOrphanTxSize(unsigned nMaxOrphans) { return impl->LimitOrphanTxSize(nMaxOrphans); }
+
 size_t PeerLogicValidation::OrphanCount() {
     std::lock_guard<std::mutex> l(impl->cs_orphans);
     return impl->mapOrphanTransactions.size();

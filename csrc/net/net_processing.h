@@ -48,6 +48,12 @@ public:
     bool GetNodeStateStats(NodeId id, CNodeStateStats& stats);
     void Misbehaving(NodeId id, int howmuch, const std::string& reason = "");
     size_t OrphanCount();
+    // The orphan pool (reference net_processing.cpp AddOrphanTx / EraseOrphansFor /
+    // LimitOrphanTxSize, also exercised directly by DoS_tests): returns whether the tx was kept,
+    // and how many orphans the limit evicted.
+    bool AddOrphanTx(const CTransactionRef& tx, NodeId peer);
+    void EraseOrphansFor(NodeId peer);
+    unsigned LimitOrphanTxSize(unsigned nMaxOrphans);
     // relay a locally-submitted transaction (sendrawtransaction / wallet)
     void RelayTransaction(const CTransaction& tx);
 
