@@ -905,12 +905,16 @@ void CConnman::ThreadSocketHandler() {
         }
         // ---- inactivity checks
         const int64_t now = GetSystemTimeInSeconds();
-        const int64_t timeout = gArgs.GetArg("-peertimeout", (int64_t)TIMEOUT_INTERVAL);
+        // -peertimeout: the window a new connection has to exchange its first messages and
+        // finish the version handshake (60 s as in the reference); after that, the 20-minute
+        // send/receive/ping timeouts apply
+        const int64_t connectWindow = std::max<int64_t>(1, gArgs.GetArg("-peertimeout", (int64_t)60));
+        const int64_t timeout = TIMEOUT_INTERVAL;
         for (CNode* p : pollNodes) {
-            if (now - p->nTimeConnected > 60) {
+            if (now - p->nTimeConnected > connectWindow) {
                 if (p->nLastRecv == 0 || p->nLastSend == 0) {
-                    LogPrint(BCLog::NET, "socket no message in first 60 seconds, %d %d from %d\n", p->nLastRecv != 0,
-                             p->nLastSend != 0, (int)p->GetId());
+                    LogPrint(BCLog::NET, "socket no message in first %d seconds, %d %d from %d\n", (int)connectWindow,
+                             p->nLastRecv != 0, p->nLastSend != 0, (int)p->GetId());
                     p->fDisconnect = true;
                 } else if (now - p->nLastSend > timeout) {
                     LogPrintf("socket sending timeout: %ds\n", (int)(now - p->nLastSend));

@@ -41,6 +41,7 @@ std::string NetHelp() {
         {"-port=<port>", "Listen for connections on <port> (default: 8337, testnet: 18337, regtest: 18444)"},
         {"-seednode=<ip>", "Connect to a node to retrieve peer addresses, and disconnect"},
         {"-timeout=<n>", "Specify connection timeout in milliseconds (default: 5000)"},
+        {"-peertimeout=<n>", "Seconds a new connection has to send its first messages and complete the version handshake (default: 60)"},
         {"-whitebind=<addr>", "Bind to given address and whitelist peers connecting to it"},
         {"-whitelist=<IP/netmask>", "Whitelist peers connecting from the given IP address or CIDR netmask"},
         {"-blocksonly", "Whether to operate in a blocks only mode (default: 0)"},
