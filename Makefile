@@ -20,6 +20,9 @@ CXXFLAGS   := -std=c++17 $(OPT) -g1 -fPIC -Wall -Wno-unused-function -Wno-sign-c
 HIPFLAGS   := -std=c++17 $(OPT) -fPIC --offload-arch=$(GPU_ARCH) -Icsrc -munsafe-fp-atomics \
               -Wno-unused-result -Wno-unused-variable -Wno-pass-failed
 LDLIBS     := -L$(ROCM)/lib -lamdhip64 -lcrypto -pthread -ldl -Wl,-rpath,$(ROCM)/lib
+# hardening of every linked binary and library (contrib/devtools/security-check.py: PIE, NX,
+# full RELRO, stack canary; executables get PIE and the canary from the toolchain defaults)
+HARDEN_LD  := -Wl,-z,relro,-z,now,-z,noexecstack
 
 CORE_SRCS  := $(wildcard csrc/crypto/*.cpp csrc/primitives/*.cpp csrc/consensus/*.cpp \
                 csrc/script/*.cpp csrc/secp256k1/*.cpp csrc/util/*.cpp csrc/node/*.cpp \
@@ -67,11 +70,11 @@ $(CORELIB): $(CORE_OBJS) $(HIP_OBJS)
 	rm -f $@ && ar rcs $@ $^
 
 $(PYEXT): $(PY_OBJS) $(CORELIB)
-	$(CXX) -shared -o $@ $(PY_OBJS) -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS)
+	$(CXX) -shared -o $@ $(PY_OBJS) -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS) $(HARDEN_LD)
 
 bin/%: build/obj/tools/%.o $(CORELIB)
 	@mkdir -p bin
-	$(CXX) -rdynamic -o $@ $< -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS)
+	$(CXX) -rdynamic -o $@ $< -Wl,--whole-archive $(CORELIB) -Wl,--no-whole-archive $(LDLIBS) $(HARDEN_LD)
 
 # native unit suites (reference src/test/ -> test_bitcoin); run by tests/test_unit_native.py
 $(UNITTEST): $(TEST_OBJS) $(CORELIB)
@@ -84,7 +87,7 @@ build/obj/tools/%.o: csrc/tools/%.cpp
 
 $(CONSLIB): build/obj/consensuslib/bitcoinconsensus.o $(CORELIB)
 	@mkdir -p lib
-	$(CXX) -shared -o $@ $< $(CORELIB) $(LDLIBS)
+	$(CXX) -shared -o $@ $< $(CORELIB) $(LDLIBS) $(HARDEN_LD)
 
 # Host-side sanitizer build of the fuzz harness (reference --enable-asan/--enable-ubsan):
 # every CPU source rebuilt with ASan+UBSan, the gfx950 kernel objects linked as they are

@@ -1,4 +1,5 @@
 // Per-network parameters (values from reference src/chainparams.cpp:95-432; the code is new).
+#include "consensus/chainparamsseeds.h"
 #include "consensus/merkle.h"
 #include "consensus/params.h"
 #include "util/strencodings.h"
@@ -82,6 +83,7 @@ public:
         vSeeds = {{"bcpfork.org", "seed.bcpfork.org", true},
                   {"bcpseeds.net", "seed.bcpseeds.net", true},
                   {"bitcoincashplus.org", "seed.bitcoincashplus.org", true}};
+        vFixedSeeds = FixedSeedsMain();
         base58Prefixes[PUBKEY_ADDRESS] = {28};
         base58Prefixes[SCRIPT_ADDRESS] = {23};
         base58Prefixes[SECRET_KEY] = {128};
@@ -153,6 +155,7 @@ public:
         vSeeds = {{"bcpfork.org", "test-seed.bcpfork.org", true},
                   {"bcpseeds.net", "test-seed.bcpseeds.net", true},
                   {"bitcoincashplus.org", "test-seed.bitcoincashplus.org", true}};
+        vFixedSeeds = FixedSeedsTest();
         base58Prefixes[PUBKEY_ADDRESS] = {111};
         base58Prefixes[SCRIPT_ADDRESS] = {196};
         base58Prefixes[SECRET_KEY] = {239};

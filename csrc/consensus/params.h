@@ -56,6 +56,13 @@ struct CDNSSeedData {
     bool supportsServiceBitsFiltering;
 };
 
+// A fixed seed node: 16-byte IPv6-form address (IPv4 v4-mapped, onion in the OnionCat prefix)
+// and port (reference chainparamsseeds.h / SeedSpec6).
+struct SeedSpec6 {
+    uint8_t addr[16];
+    uint16_t port;
+};
+
 struct CCheckpointData {
     std::map<int, uint256> mapCheckpoints;
 };
@@ -87,6 +94,7 @@ public:
     const std::string& NetworkIDString() const { return strNetworkID; }
     const std::string& DataDirSuffix() const { return strDataDir; }
     const std::vector<CDNSSeedData>& DNSSeeds() const { return vSeeds; }
+    const std::vector<SeedSpec6>& FixedSeeds() const { return vFixedSeeds; }
     const std::vector<unsigned char>& Base58Prefix(Base58Type t) const { return base58Prefixes[t]; }
     const std::string& CashAddrPrefix() const { return cashaddrPrefix; }
     const CCheckpointData& Checkpoints() const { return checkpointData; }
@@ -106,6 +114,7 @@ protected:
     uint64_t nPruneAfterHeight = 0;
     unsigned int nEquihashN = 0, nEquihashK = 0;
     std::vector<CDNSSeedData> vSeeds;
+    std::vector<SeedSpec6> vFixedSeeds;
     std::vector<unsigned char> base58Prefixes[MAX_BASE58_TYPES];
     std::string cashaddrPrefix;
     std::string strNetworkID, strDataDir;

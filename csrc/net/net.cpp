@@ -1010,8 +1010,20 @@ void CConnman::ThreadOpenConnections() {
         ProcessOneShot();
         if (!InterruptibleSleep(500)) return;
         if (!fNetworkActive) continue;
-        // fixed seeds are not shipped for BCP; regtest never auto-connects
+        // regtest never auto-connects
         if (Params().MineBlocksOnDemand()) continue;
+        // no addresses a minute after start (DNS seeds unreachable or disabled): fall back to the
+        // compiled-in fixed seeds once (reference net.cpp ThreadOpenConnections)
+        if (addrman.size() == 0 && GetTime() - nStart > 60 && !fFixedSeedsAdded) {
+            fFixedSeedsAdded = true;
+            const std::vector<CAddress> seeds = ConvertSeed6(Params().FixedSeeds());
+            if (!seeds.empty()) {
+                LogPrintf("Adding %u fixed seed nodes as DNS doesn't seem to be available.\n", (unsigned)seeds.size());
+                CNetAddr local;
+                local.SetIPv4(0x7f000001);
+                addrman.Add(seeds, CAddress(CService(local, 0), NODE_NONE));
+            }
+        }
         int nOutbound = 0;
         std::set<std::vector<unsigned char>> setConnected;
         {
@@ -1114,6 +1126,22 @@ void CConnman::ThreadOpenAddedConnections() {
         }
         if (!InterruptibleSleep(tried ? 60000 : 2000)) return;
     }
+}
+
+std::vector<CAddress> ConvertSeed6(const std::vector<SeedSpec6>& seeds) {
+    // fixed seeds look a week or two old, so addrman prefers any fresher address it learns
+    static const int64_t nOneWeek = 7 * 24 * 60 * 60;
+    std::vector<CAddress> out;
+    out.reserve(seeds.size());
+    FastRandomContext rng;
+    for (const SeedSpec6& s : seeds) {
+        CNetAddr ip;
+        ip.SetRaw(s.addr);
+        CAddress a(CService(ip, s.port), NODE_NETWORK);
+        a.nTime = (uint32_t)(GetTime() - (int64_t)rng.randrange(nOneWeek) - nOneWeek);
+        out.push_back(a);
+    }
+    return out;
 }
 
 void CConnman::ThreadDNSAddressSeed() {

@@ -10,6 +10,7 @@
 // that round-robins peers, both event-driven by a condition variable.
 #pragma once
 #include "util/limitedmap.h"
+#include "consensus/params.h"
 #include "consensus/merkleblock.h"
 #include "crypto/hashes.h"
 #include "keys/key.h"
@@ -251,6 +252,9 @@ std::map<CNetAddr, std::pair<int, int>> GetLocalAddresses(); // addr -> (port, s
 extern std::atomic<bool> fListen;
 extern std::atomic<bool> fDiscover;
 
+// The chain's compiled-in fixed seeds as addrman entries (reference net.cpp convertSeed6).
+std::vector<CAddress> ConvertSeed6(const std::vector<SeedSpec6>& seeds);
+
 class CConnman {
 public:
     struct Options {
@@ -384,6 +388,7 @@ private:
 
     std::vector<ListenSocket> vhListenSocket;
     std::atomic<bool> fNetworkActive{true};
+    bool fFixedSeedsAdded = false; // ThreadOpenConnections only
     CAddrMan addrman;
     BanMan banman;
     Mutex cs_vOneShots;

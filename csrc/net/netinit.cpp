@@ -42,6 +42,12 @@ std::string NetHelp() {
         {"-seednode=<ip>", "Connect to a node to retrieve peer addresses, and disconnect"},
         {"-timeout=<n>", "Specify connection timeout in milliseconds (default: 5000)"},
         {"-peertimeout=<n>", "Seconds a new connection has to send its first messages and complete the version handshake (default: 60)"},
+        {"-blockreconstructionextratxn=<n>", "Extra transactions to keep in memory for compact block reconstructions (default: 100)"},
+        {"-feefilter", "Tell peers the minimum fee rate of transactions to relay to us (default: 1)"},
+        {"-uacomment=<cmt>", "Append comment to the user agent string"},
+        {"-upnpdiscover=<ip:port>", "SSDP multicast target for UPnP gateway discovery (default: 239.255.255.250:1900)"},
+        {"-whitelistrelay", "Accept relayed transactions received from whitelisted peers even when not relaying transactions (default: 1)"},
+        {"-whitelistforcerelay", "Force relay of transactions from whitelisted peers even if they violate local relay policy (default: 1)"},
         {"-whitebind=<addr>", "Bind to given address and whitelist peers connecting to it"},
         {"-whitelist=<IP/netmask>", "Whitelist peers connecting from the given IP address or CIDR netmask"},
         {"-blocksonly", "Whether to operate in a blocks only mode (default: 0)"},

@@ -104,6 +104,21 @@ std::string HelpMessage() {
         {"-connectpipeline=<n>", "Blocks in flight when connecting several in a row: block N+1's UTXO pass overlaps "
                                  "block N's signature batch (default: 2; 1 = one block at a time)"},
         {"-checkmempool=<n>", "Run checks every <n> transactions"},
+        {"-acceptnonstdtxn", "Relay and mine \"non-standard\" transactions (default: 0 on main, 1 on the test chains)"},
+        {"-assumevalid=<hex>", "If this block is in the chain assume that it and its ancestors are valid and potentially skip their script verification (0 to verify all)"},
+        {"-bytespersigop=<n>", "Equivalent bytes per sigop in transactions for relay and mining (default: 20)"},
+        {"-checkpoints", "Disable expensive verification for known chain history (default: 1)"},
+        {"-debugexclude=<category>", "Exclude debugging information for a category; takes priority over -debug"},
+        {"-debuglockorder", "Check lock-order consistency of the node's mutexes (default: 0)"},
+        {"-debuglockorderabort", "Abort on a detected lock-order inversion (with -debuglockorder; default: 1)"},
+        {"-limitancestorcount=<n>", "Do not accept transactions if the number of in-mempool ancestors is <n> or more (default: 25)"},
+        {"-limitancestorsize=<n>", "Do not accept transactions whose size with all in-mempool ancestors exceeds <n> kilobytes (default: 101)"},
+        {"-limitdescendantcount=<n>", "Do not accept transactions if any ancestor would have <n> or more in-mempool descendants (default: 25)"},
+        {"-limitdescendantsize=<n>", "Do not accept transactions if any ancestor would have more than <n> kilobytes of in-mempool descendants (default: 101)"},
+        {"-maxtimeadjustment=<n>", "Maximum allowed median peer time offset adjustment, in seconds (default: 4200)"},
+        {"-maxtipage=<n>", "Maximum tip age in seconds to consider the node in initial block download (default: 86400)"},
+        {"-maxtxfee=<amt>", "Maximum total fees (in BCP) to use in a single wallet transaction or raw transaction (default: 0.1)"},
+        {"-promiscuousmempoolflags=<n>", "Script verification flags for mempool acceptance (testing only)"},
         {"-blockversion=<n>", "Override block version to test forking scenarios (regtest)"},
     };
     for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);

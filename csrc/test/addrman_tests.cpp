@@ -5,7 +5,9 @@
 // of buckets per (source) group) and the ban-list half of DoS_tests.cpp (ban, expiry, unban).
 #include "test/unittest.h"
 
+#include "consensus/params.h"
 #include "net/addrman.h"
+#include "net/net.h"
 #include "util/strencodings.h"
 #include "util/util.h"
 
@@ -205,5 +207,31 @@ TEST_CASE(addrman_tests, banlist) {
     CHECK(!back.Unban(one));
     const std::string cmd = std::string("rm -rf '") + tmpl + "'";
     if (system(cmd.c_str()) != 0) {}
+    SetMockTime(0);
+}
+
+TEST_CASE(addrman_tests, fixed_seeds) {
+    // contrib/seeds/generate-seeds.py entries: an IPv4 (v4-mapped) and an IPv6 seed
+    const int64_t now = 1600000000;
+    SetMockTime(now);
+    std::vector<SeedSpec6> seeds(2);
+    const unsigned char v4[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff, 1, 2, 3, 4};
+    const unsigned char v6[16] = {0x20, 0x01, 0x0d, 0xb8, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1};
+    memcpy(seeds[0].addr, v4, 16);
+    seeds[0].port = 8337;
+    memcpy(seeds[1].addr, v6, 16);
+    seeds[1].port = 18337;
+    const std::vector<CAddress> a = ConvertSeed6(seeds);
+    REQUIRE(a.size() == 2u);
+    CHECK_EQ(a[0].ToStringIPPort(), std::string("1.2.3.4:8337"));
+    CHECK(a[0].IsIPv4());
+    CHECK_EQ(a[1].ToStringIPPort(), std::string("[2001:db8::1]:18337"));
+    for (const CAddress& x : a) {
+        CHECK(x.nServices & NODE_NETWORK);
+        CHECK((int64_t)x.nTime <= now - 7 * 24 * 3600 && (int64_t)x.nTime > now - 14 * 24 * 3600);
+    }
+    // the shipped lists (reference: empty) load into the chain parameters
+    SelectParams("main");
+    CHECK(Params().FixedSeeds().size() < 1000u);
     SetMockTime(0);
 }

@@ -377,7 +377,7 @@ int main(int argc, char* argv[]) {
     if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help") || !gArgs.IsArgSet("-host")) {
         printf("Usage: bcp-seeder -host=<host> -ns=<ns> [-mbox=<mail>] [-port=<dns port>] [-threads=<n>]\n"
                "                  [-seed=<ip:port>]... [-testnet|-regtest] [-dumpfile=<file>] [-allowlocal]\n"
-               "                  [-minheight=<n>] [-retry=<seconds>]\n");
+               "                  [-minheight=<n>] [-retry=<seconds>] [-dumpinterval=<seconds>]\n");
         return gArgs.IsArgSet("-host") ? 0 : 1;
     }
     SelectParams(gArgs.GetChainName());

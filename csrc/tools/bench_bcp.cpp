@@ -954,7 +954,9 @@ BENCHMARK(IbdPipeline_Pipe_GPU);
 int main(int argc, char* argv[]) {
     gArgs.ParseParameters(argc, argv);
     if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help")) {
-        printf("Usage: bench_bcp [-filter=<regex>] [-time=<seconds per bench>] [-list] [-datadir=bench/data]\n");
+        printf("Usage: bench_bcp [-filter=<regex>] [-time=<seconds per bench>] [-list] [-datadir=bench/data]\n"
+               "                 [-par=<script threads>] [-ibdblocks=<n>] [-kvcoins=<n>] [-kvdbcache=<MiB>]\n"
+               "                 [-debug=<category>]\n");
         return 0;
     }
     { // default: <dir of the binary>/../bench/data, so the working directory does not matter
