@@ -8,8 +8,10 @@
 namespace bcp {
 
 // Blocks with at least this many transactions hash their merkle tree on the GPU when one is
-// visible: 0.18 ms vs 11 ms on one CPU core at 21k leaves (profiles/block_connect_r2.md).
-static std::atomic<size_t> g_gpu_merkle_threshold{2048};
+// visible. With SHA-256 on the SHA extensions the CPU matches the GPU at 21k leaves (0.21 vs
+// 0.19 ms on MI355X) and is 5x slower at 1M (10.2 vs 1.9 ms), profiles/connect_r3.md: the GPU
+// path is kept for blocks of 32k+ transactions (it was 2048 with the scalar CPU hash).
+static std::atomic<size_t> g_gpu_merkle_threshold{32768};
 void SetGpuMerkleThreshold(size_t n) { g_gpu_merkle_threshold = n; }
 
 // One level: pairs (2i, 2i+1), odd tail duplicated. The tail pair is "impure" if its right

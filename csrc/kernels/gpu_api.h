@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <memory>
 #include <string>
+#include <functional>
 #include <vector>
 
 namespace bcp {
@@ -121,6 +122,11 @@ public:
     // Same contract as EcdsaVerifyBatch: n packed jobs, result[i] = 1 iff valid.
     void Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33, size_t n,
                uint8_t* result);
+    // Same, with the inputs written by `fill` straight into the lane's pinned staging buffer
+    // (msg32: n x 32 B, sig64: n x 64 B, pub33: n x 33 B) instead of being copied there.
+    void EcdsaFill(size_t n, const std::function<void(unsigned char* msg32, unsigned char* sig64,
+                                                        unsigned char* pub33)>& fill,
+                   uint8_t* result);
     // Same contract as EquihashVerifyBatch for n (state, solution) pairs; a solution of the
     // wrong length is rejected.
     void Equihash(unsigned N, unsigned K, const EhBaseState* states, const std::vector<unsigned char>* const* sols,

@@ -1093,6 +1093,18 @@ void InitTable(Table& tb) {
 // the Jobs and does all scalar arithmetic; one D2H copy of the verdicts.
 void VerifyLane::Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33, size_t n,
                        uint8_t* result) {
+    EcdsaFill(
+        n,
+        [&](unsigned char* m, unsigned char* s, unsigned char* p) {
+            memcpy(m, msg32, n * 32);
+            memcpy(s, sig64, n * 64);
+            memcpy(p, pub33, n * 33);
+        },
+        result);
+}
+
+void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, unsigned char*, unsigned char*)>& fill,
+                           uint8_t* result) {
     if (n == 0) return;
     LaneState& L = *impl;
     BCP_HIP_CHECK(hipSetDevice(L.device));
@@ -1101,9 +1113,7 @@ void VerifyLane::Ecdsa(const unsigned char* msg32, const unsigned char* sig64, c
     std::call_once(tb.once, [&] { InitTable(tb); });
     unsigned char* h_in = L.Host(0, n * 129);
     uint8_t* h_out = L.Host(1, n);
-    memcpy(h_in, msg32, n * 32);
-    memcpy(h_in + n * 32, sig64, n * 64);
-    memcpy(h_in + n * 96, pub33, n * 33);
+    fill(h_in, h_in + n * 32, h_in + n * 96);
     unsigned char* d_in = L.Dev(0, n * 129);
     Job* d_jobs = reinterpret_cast<Job*>(L.Dev(1, n * sizeof(Job)));
     uint8_t* d_out = L.Dev(2, n);

@@ -182,6 +182,24 @@ std::vector<uint8_t> GpuVerifyService::Ecdsa(const unsigned char* msg32, const u
     return out;
 }
 
+std::vector<uint8_t> GpuVerifyService::EcdsaFill(
+    size_t n,
+    const std::function<void(size_t, size_t, unsigned char*, unsigned char*, unsigned char*)>& fill) {
+    std::vector<uint8_t> out(n, 0);
+    if (n == 0) return out;
+    size_t minShard;
+    {
+        std::lock_guard<std::mutex> l(m);
+        minShard = minShardEcdsa;
+    }
+    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi) {
+        lane.EcdsaFill(
+            hi - lo, [&](unsigned char* msg, unsigned char* sig, unsigned char* pub) { fill(lo, hi, msg, sig, pub); },
+            out.data() + lo);
+    });
+    return out;
+}
+
 std::vector<uint8_t> GpuVerifyService::Equihash(unsigned N, unsigned K, const std::vector<gpu::EhBaseState>& states,
                                                 const std::vector<const std::vector<unsigned char>*>& sols) {
     if (states.size() != sols.size()) throw std::invalid_argument("GpuVerifyService::Equihash: sizes");

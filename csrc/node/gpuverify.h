@@ -47,6 +47,10 @@ public:
     // result[i] = 1 iff job i is valid (gpu::EcdsaVerifyBatch contract, packed arrays).
     std::vector<uint8_t> Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33,
                                size_t n);
+    // The same batch with its inputs produced in place: fill(lo, hi, msg32, sig64, pub33) writes
+    // jobs [lo, hi) into a lane's pinned staging arrays (indexed from 0 = job lo).
+    std::vector<uint8_t> EcdsaFill(size_t n, const std::function<void(size_t lo, size_t hi, unsigned char* msg32,
+                                                                      unsigned char* sig64, unsigned char* pub33)>& fill);
     // result[i] = 1 iff solution i is valid for state i.
     std::vector<uint8_t> Equihash(unsigned N, unsigned K, const std::vector<gpu::EhBaseState>& states,
                                   const std::vector<const std::vector<unsigned char>*>& sols);

@@ -71,43 +71,50 @@ bool CachingTransactionSignatureChecker::VerifySignature(const std::vector<unsig
 }
 
 std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool) {
-    // host: DER parse + low-S normalisation + key form; device: decompression + ecmult
+    // host: DER parse + low-S normalisation + key form, written by the pool straight into the
+    // verify lane's pinned staging buffer; device: decompression + ecmult
     const size_t n = checks.size();
-    std::vector<unsigned char> msg(n * 32), sig(n * 64), pub(n * 33);
     std::vector<uint8_t> hostOk(n, 1);
-    auto prep = [&](size_t j) {
-        const DeferredSigCheck& c = *checks[j];
-        secp::Signature s;
-        if (!secp::sig_parse_der_lax(s, c.sig.data(), c.sig.size())) {
-            hostOk[j] = 0;
-            return;
-        }
-        secp::sig_normalize(s);
-        secp::sig_serialize_compact(&sig[j * 64], s);
-        if (secp::sc_is_zero(s.r) || secp::sc_is_zero(s.s)) hostOk[j] = 0;
-        memcpy(&msg[j * 32], c.sighash.begin(), 32);
-        const auto& pk = c.pubkey;
-        if (pk.size() == 33 && (pk[0] == 2 || pk[0] == 3)) {
-            memcpy(&pub[j * 33], pk.data(), 33);
-        } else {
-            secp::Ge q;
-            if (!secp::pubkey_parse(q, pk.data(), pk.size())) {
-                hostOk[j] = 0;
-                pub[j * 33] = 2;
-                return;
-            }
-            std::vector<unsigned char> comp = secp::pubkey_serialize(q, true);
-            memcpy(&pub[j * 33], comp.data(), 33);
-        }
-    };
-    if (pool) pool->ParallelFor(n, prep, 64);
-    else
-        for (size_t j = 0; j < n; j++) prep(j);
-    for (size_t j = 0; j < n; j++)
-        if (!hostOk[j]) pub[j * 33] = 2; // keep device input well-formed; result masked below
     if (GpuFaultInjection()) throw std::runtime_error("injected GPU signature-verify fault");
+    auto fill = [&](size_t lo, size_t hi, unsigned char* msg, unsigned char* sig, unsigned char* pub) {
+        auto prep = [&](size_t k) {
+            const size_t j = lo + k;
+            const DeferredSigCheck& c = *checks[j];
+            memcpy(&msg[k * 32], c.sighash.begin(), 32);
+            secp::Signature s;
+            bool ok = secp::sig_parse_der_lax(s, c.sig.data(), c.sig.size());
+            if (ok) {
+                secp::sig_normalize(s);
+                secp::sig_serialize_compact(&sig[k * 64], s);
+                if (secp::sc_is_zero(s.r) || secp::sc_is_zero(s.s)) ok = false;
+            } else {
+                memset(&sig[k * 64], 0, 64);
+            }
+            const auto& pk = c.pubkey;
+            if (pk.size() == 33 && (pk[0] == 2 || pk[0] == 3)) {
+                memcpy(&pub[k * 33], pk.data(), 33);
+            } else {
+                secp::Ge q;
+                if (secp::pubkey_parse(q, pk.data(), pk.size())) {
+                    std::vector<unsigned char> comp = secp::pubkey_serialize(q, true);
+                    memcpy(&pub[k * 33], comp.data(), 33);
+                } else {
+                    ok = false;
+                }
+            }
+            // a rejected job keeps the device input well-formed; its result is masked below
+            if (!ok) {
+                hostOk[j] = 0;
+                memset(&pub[k * 33], 0, 33);
+                pub[k * 33] = 2;
+            }
+        };
+        if (pool) pool->ParallelFor(hi - lo, prep, 64);
+        else
+            for (size_t k = 0; k < hi - lo; k++) prep(k);
+    };
     // sharded across the validation GPUs by the verify service (one high-priority lane each)
-    std::vector<uint8_t> res = GpuVerifyService::Instance().Ecdsa(msg.data(), sig.data(), pub.data(), n);
+    std::vector<uint8_t> res = GpuVerifyService::Instance().EcdsaFill(n, fill);
     for (size_t j = 0; j < n; j++) res[j] &= hostOk[j];
     return res;
 }
