@@ -3,6 +3,7 @@
 #include "crypto/hashes.h"
 #include "crypto/common.h"
 
+#include <algorithm>
 #include <cstring>
 #include <mutex>
 
@@ -149,16 +150,70 @@ static void fe_pow(Fe& r, const Fe& a, const uint64_t* e) {
     }
     r = acc;
 }
+// a^(2^223 - 1) and the shorter runs of ones the exponents p - 2 and (p + 1)/4 are made of:
+// xk = a^(2^k - 1). 222 squarings and 11 multiplications instead of a plain square-and-multiply
+// over 256 mostly-one bits (~500 operations).
+struct FeRuns {
+    Fe x2, x3, x22, x223;
+};
+static void fe_sqr_n(Fe& r, const Fe& a, int n) {
+    r = a;
+    for (int i = 0; i < n; ++i) fe_sqr(r, r);
+}
+static void fe_runs(FeRuns& R, const Fe& a) {
+    Fe x6, x9, x11, x44, x88, x176, x220, t;
+    fe_sqr(t, a);
+    fe_mul(R.x2, t, a);
+    fe_sqr(t, R.x2);
+    fe_mul(R.x3, t, a);
+    fe_sqr_n(t, R.x3, 3);
+    fe_mul(x6, t, R.x3);
+    fe_sqr_n(t, x6, 3);
+    fe_mul(x9, t, R.x3);
+    fe_sqr_n(t, x9, 2);
+    fe_mul(x11, t, R.x2);
+    fe_sqr_n(t, x11, 11);
+    fe_mul(R.x22, t, x11);
+    fe_sqr_n(t, R.x22, 22);
+    fe_mul(x44, t, R.x22);
+    fe_sqr_n(t, x44, 44);
+    fe_mul(x88, t, x44);
+    fe_sqr_n(t, x88, 88);
+    fe_mul(x176, t, x88);
+    fe_sqr_n(t, x176, 44);
+    fe_mul(x220, t, x44);
+    fe_sqr_n(t, x220, 3);
+    fe_mul(R.x223, t, R.x3);
+}
 void fe_inv(Fe& r, const Fe& a) {
+    // p - 2 = [223 ones] 0 [22 ones] 0000 1 0 11 0 1
+    FeRuns R;
+    fe_runs(R, a);
+    Fe t;
+    fe_sqr_n(t, R.x223, 23);
+    fe_mul(t, t, R.x22);
+    fe_sqr_n(t, t, 5);
+    fe_mul(t, t, a);
+    fe_sqr_n(t, t, 3);
+    fe_mul(t, t, R.x2);
+    fe_sqr_n(t, t, 2);
+    fe_mul(r, t, a);
+}
+void fe_inv_slow(Fe& r, const Fe& a) {
     static const uint64_t PM2[4] = {0xFFFFFFFEFFFFFC2DULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL,
                                     0xFFFFFFFFFFFFFFFFULL};
     fe_pow(r, a, PM2);
 }
 bool fe_sqrt(Fe& r, const Fe& a) {
-    static const uint64_t E[4] = {0xFFFFFFFFBFFFFF0CULL, 0xFFFFFFFFFFFFFFFFULL, 0xFFFFFFFFFFFFFFFFULL,
-                                  0x3FFFFFFFFFFFFFFFULL}; // (p+1)/4
+    // (p + 1)/4 = [223 ones] 0 [22 ones] 0000 11 00
+    FeRuns R;
+    fe_runs(R, a);
     Fe s, chk;
-    fe_pow(s, a, E);
+    fe_sqr_n(s, R.x223, 23);
+    fe_mul(s, s, R.x22);
+    fe_sqr_n(s, s, 6);
+    fe_mul(s, s, R.x2);
+    fe_sqr_n(s, s, 2);
     fe_sqr(chk, s);
     r = s;
     return fe_equal(chk, a);
@@ -244,12 +299,19 @@ void sc_mul(Scalar& r, const Scalar& a, const Scalar& b) {
     sc_reduce(r.n, t);
 }
 void sc_inv(Scalar& r, const Scalar& a) {
+    // a^(n-2) with a fixed 4-bit window: 256 squarings and 64 multiplications (plus 14 for the
+    // table) instead of ~200 multiplications of plain square-and-multiply
     static const uint64_t NM2[4] = {0xBFD25E8CD036413FULL, 0xBAAEDCE6AF48A03BULL, 0xFFFFFFFFFFFFFFFEULL,
                                     0xFFFFFFFFFFFFFFFFULL};
+    Scalar tab[16];
+    tab[0] = {{1, 0, 0, 0}};
+    tab[1] = a;
+    for (int i = 2; i < 16; ++i) sc_mul(tab[i], tab[i - 1], a);
     Scalar acc = {{1, 0, 0, 0}};
-    for (int i = 255; i >= 0; --i) {
-        sc_mul(acc, acc, acc);
-        if ((NM2[i / 64] >> (i % 64)) & 1) sc_mul(acc, acc, a);
+    for (int i = 63; i >= 0; --i) {
+        for (int k = 0; k < 4; ++k) sc_mul(acc, acc, acc);
+        const unsigned w = (unsigned)(NM2[i / 16] >> ((i % 16) * 4)) & 15;
+        if (w) sc_mul(acc, acc, tab[w]);
     }
     r = acc;
 }
@@ -543,7 +605,171 @@ static int wnaf(int* digits, const Scalar& s, int w) {
     return len;
 }
 
+// ---- GLV endomorphism: lambda * (x, y) = (beta * x, y), so na = k1 + k2 * lambda (mod n) with
+// |k1|, |k2| < 2^129 halves the doublings of na * A. The lattice constants are the GPU verify
+// kernel's (csrc/kernels/secp256k1.hip GLV_*, range-checked there), as 32-bit little-endian limbs:
+// c1 = round(k * g1 / 2^384), c2 = round(k * g2 / 2^384), k2 = c1 * (-b1) - c2 * b2,
+// k1 = k - c1 * a1 - c2 * a2.
+namespace {
+const uint32_t GLV_G1[8] = {0x45DBB031, 0xE893209A, 0x71E8CA7F, 0x3DAA8A14,
+                            0x9284EB15, 0xE86C90E4, 0xA7D46BCD, 0x3086D221};
+const uint32_t GLV_G2[8] = {0x8AC47F71, 0x1571B4AE, 0x9DF506C6, 0x221208AC,
+                            0x0ABFE4C4, 0x6F547FA9, 0x010E8828, 0xE4437ED6};
+const uint32_t GLV_A1[4] = {0x9284EB15, 0xE86C90E4, 0xA7D46BCD, 0x3086D221};
+const uint32_t GLV_B1N[4] = {0x0ABFE4C3, 0x6F547FA9, 0x010E8828, 0xE4437ED6}; // -b1
+const uint32_t GLV_A2[5] = {0x9D44CFD8, 0x57C1108D, 0xA8E2F3F6, 0x14CA50F7, 0x00000001};
+const uint32_t GLV_B2[4] = {0x9284EB15, 0xE86C90E4, 0xA7D46BCD, 0x3086D221};
+// beta, big-endian bytes: a cube root of unity mod p
+const unsigned char GLV_BETA_BE[32] = {0x7A, 0xE9, 0x6A, 0x2B, 0x65, 0x7C, 0x07, 0x10, 0x6E, 0x64, 0x47,
+                                       0x9E, 0xAC, 0x34, 0x34, 0xE9, 0x9C, 0xF0, 0x49, 0x75, 0x12, 0xF5,
+                                       0x89, 0x95, 0xC1, 0x39, 0x6C, 0x28, 0x71, 0x95, 0x01, 0xEE};
+
+template <int NA, int NB> void mul_wide32(uint32_t* r, const uint32_t* a, const uint32_t* b) {
+    for (int i = 0; i < NA + NB; i++) r[i] = 0;
+    for (int i = 0; i < NA; i++) {
+        uint64_t c = 0;
+        for (int j = 0; j < NB; j++) {
+            c += (uint64_t)r[i + j] + (uint64_t)a[i] * b[j];
+            r[i + j] = (uint32_t)c;
+            c >>= 32;
+        }
+        r[i + NB] = (uint32_t)c;
+    }
+}
+
+// |v| of a 10-limb two's-complement value into a Scalar-shaped magnitude (< 2^130); true if v < 0
+bool abs10(Scalar& m, const uint32_t* v) {
+    uint32_t t[10];
+    const bool neg = v[9] >> 31;
+    if (neg) {
+        uint64_t c = 1;
+        for (int i = 0; i < 10; i++) {
+            c += (uint64_t)(uint32_t)~v[i];
+            t[i] = (uint32_t)c;
+            c >>= 32;
+        }
+    } else {
+        for (int i = 0; i < 10; i++) t[i] = v[i];
+    }
+    for (int i = 0; i < 4; i++) m.n[i] = (uint64_t)t[2 * i] | ((uint64_t)t[2 * i + 1] << 32);
+    return neg;
+}
+
+void glv_split(const Scalar& k, Scalar& m1, bool& neg1, Scalar& m2, bool& neg2) {
+    uint32_t kv[8];
+    for (int i = 0; i < 4; i++) {
+        kv[2 * i] = (uint32_t)k.n[i];
+        kv[2 * i + 1] = (uint32_t)(k.n[i] >> 32);
+    }
+    auto mul_shift384 = [&](uint32_t (&c)[4], const uint32_t* g) {
+        uint32_t t[16];
+        mul_wide32<8, 8>(t, kv, g);
+        uint64_t carry = t[11] >> 31; // rounding bit 383
+        for (int i = 0; i < 4; i++) {
+            carry += t[12 + i];
+            c[i] = (uint32_t)carry;
+            carry >>= 32;
+        }
+    };
+    uint32_t c1[4], c2[4];
+    mul_shift384(c1, GLV_G1);
+    mul_shift384(c2, GLV_G2);
+    uint32_t p1[8], p2[8], p3[8], p4[9], k1[10], k2[10];
+    mul_wide32<4, 4>(p1, c1, GLV_B1N);
+    mul_wide32<4, 4>(p2, c2, GLV_B2);
+    mul_wide32<4, 4>(p3, c1, GLV_A1);
+    mul_wide32<4, 5>(p4, c2, GLV_A2);
+    uint64_t br = 0;
+    for (int i = 0; i < 10; i++) { // k2 = c1*(-b1) - c2*b2
+        const uint64_t d = (uint64_t)(i < 8 ? p1[i] : 0u) - (i < 8 ? p2[i] : 0u) - br;
+        k2[i] = (uint32_t)d;
+        br = (d >> 63) & 1;
+    }
+    int64_t sb = 0;
+    for (int i = 0; i < 10; i++) { // k1 = k - c1*a1 - c2*a2 (the borrow reaches 2)
+        const int64_t v = (int64_t)(i < 8 ? kv[i] : 0u) - (int64_t)(i < 8 ? p3[i] : 0u) -
+                          (int64_t)(i < 9 ? p4[i] : 0u) - sb;
+        k1[i] = (uint32_t)v;
+        sb = -(v >> 32);
+    }
+    neg1 = abs10(m1, k1);
+    neg2 = abs10(m2, k2);
+}
+} // namespace
+
+bool glv_check(const Scalar& k) {
+    // k1 + k2 * lambda == k (mod n), for tests
+    Scalar m1, m2;
+    bool n1, n2;
+    glv_split(k, m1, n1, m2, n2);
+    static const unsigned char LAMBDA_BE[32] = {0x53, 0x63, 0xAD, 0x4C, 0xC0, 0x5C, 0x30, 0xE0, 0xA5, 0x26, 0x1C,
+                                                0x02, 0x88, 0x12, 0x64, 0x5A, 0x12, 0x2E, 0x22, 0xEA, 0x20, 0x81,
+                                                0x66, 0x78, 0xDF, 0x02, 0x96, 0x7C, 0x1B, 0x23, 0xBD, 0x72};
+    if (m1.n[3] || (m1.n[2] >> 2) || m2.n[3] || (m2.n[2] >> 2)) return false; // |k1|,|k2| < 2^130
+    Scalar lambda, t, r;
+    sc_set_b32(lambda, LAMBDA_BE);
+    if (n1) sc_neg(m1, m1);
+    if (n2) sc_neg(m2, m2);
+    sc_mul(t, m2, lambda);
+    sc_add(r, m1, t);
+    return memcmp(r.n, k.n, sizeof(r.n)) == 0;
+}
+
+void ecmult_plain(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng);
+
 void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng) {
+    Gej acc;
+    acc.inf = true;
+    if (!a.inf && !sc_is_zero(na)) {
+        // na * A = k1 * A + k2 * (lambda A): odd multiples A .. 15A, and lambda's with X * beta
+        Gej pre_j[8], a2;
+        pre_j[0] = a;
+        gej_double(a2, a);
+        for (int i = 1; i < 8; ++i) gej_add(pre_j[i], pre_j[i - 1], a2);
+        Ge pre[2][8];
+        batch_to_affine(pre[0], pre_j, 8);
+        static const Fe beta = [] {
+            Fe b;
+            fe_set_b32(b, GLV_BETA_BE);
+            return b;
+        }();
+        Scalar m[2];
+        bool neg[2];
+        glv_split(na, m[0], neg[0], m[1], neg[1]);
+        for (int i = 0; i < 8; ++i) {
+            pre[1][i] = pre[0][i];
+            fe_mul(pre[1][i].x, pre[0][i].x, beta);
+        }
+        for (int h = 0; h < 2; ++h)
+            if (neg[h])
+                for (int i = 0; i < 8; ++i) fe_neg(pre[h][i].y, pre[h][i].y);
+        int digits[2][140];
+        int len[2];
+        for (int h = 0; h < 2; ++h) len[h] = wnaf(digits[h], m[h], 5);
+        for (int i = std::max(len[0], len[1]) - 1; i >= 0; --i) {
+            gej_double(acc, acc);
+            for (int h = 0; h < 2; ++h) {
+                const int d = i < len[h] ? digits[h][i] : 0;
+                if (d > 0) {
+                    gej_add_ge(acc, acc, pre[h][(d - 1) / 2]);
+                } else if (d < 0) {
+                    Ge neg_p = pre[h][(-d - 1) / 2];
+                    fe_neg(neg_p.y, neg_p.y);
+                    gej_add_ge(acc, acc, neg_p);
+                }
+            }
+        }
+    }
+    if (!sc_is_zero(ng)) {
+        Gej g;
+        ecmult_gen(g, ng);
+        gej_add(acc, acc, g);
+    }
+    r = acc;
+}
+
+// The straightforward double-and-add over all 256 bits (kept as the differential reference).
+void ecmult_plain(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng) {
     Gej acc;
     acc.inf = true;
     if (!a.inf && !sc_is_zero(na)) {
@@ -803,13 +1029,27 @@ bool ecdsa_verify(const Signature& sig, const unsigned char* msg32, const Ge& pu
     gej_set_ge(pj, pub);
     ecmult(R, pj, u2, u1);
     if (R.inf) return false;
-    Ge Ra;
-    ge_set_gej(Ra, R);
-    unsigned char xb[32];
-    fe_get_b32(xb, Ra.x);
-    Scalar xr;
-    sc_set_b32(xr, xb);
-    return memcmp(xr.n, sig.r.n, 32) == 0;
+    // x(R) mod n == r without leaving Jacobian coordinates: X == r * Z^2 (mod p), or, when
+    // r + n < p, X == (r + n) * Z^2 (the affine x may exceed n)
+    unsigned char rb[32];
+    sc_get_b32(rb, sig.r);
+    Fe rx, z2, t;
+    fe_set_b32(rx, rb);
+    fe_sqr(z2, R.z);
+    fe_mul(t, rx, z2);
+    if (fe_equal(t, R.x)) return true;
+    static const uint64_t PMN[4] = {0x402DA1722FC9BAEEULL, 0x4551231950B75FC4ULL, 1, 0}; // p - n
+    if (!geq4(rx.n, PMN)) { // r < p - n
+        Fe nfe, rn;
+        nfe.n[0] = N[0];
+        nfe.n[1] = N[1];
+        nfe.n[2] = N[2];
+        nfe.n[3] = N[3];
+        fe_add(rn, rx, nfe);
+        fe_mul(t, rn, z2);
+        if (fe_equal(t, R.x)) return true;
+    }
+    return false;
 }
 
 void rfc6979_nonce(unsigned char* out32, const unsigned char* msg32, const unsigned char* key32,

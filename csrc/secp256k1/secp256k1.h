@@ -49,7 +49,8 @@ void fe_sub(Fe& r, const Fe& a, const Fe& b);
 void fe_neg(Fe& r, const Fe& a);
 void fe_mul(Fe& r, const Fe& a, const Fe& b);
 void fe_sqr(Fe& r, const Fe& a);
-void fe_inv(Fe& r, const Fe& a);
+void fe_inv(Fe& r, const Fe& a);      // addition chain
+void fe_inv_slow(Fe& r, const Fe& a); // plain square-and-multiply (tests)
 bool fe_sqrt(Fe& r, const Fe& a); // false if a is not a square
 
 // ---- scalar
@@ -73,7 +74,9 @@ bool ge_is_valid(const Ge& a);
 void ecmult_gen(Gej& r, const Scalar& k);
 // Affine comb table, entry [i*256 + j] = j * 256^i * G (j = 0 is the point at infinity).
 const std::vector<Ge>& generator_table();                                  // k*G
-void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng);     // na*A + ng*G
+void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng);     // na*A + ng*G (GLV)
+void ecmult_plain(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng); // same, no endomorphism
+bool glv_check(const Scalar& k); // the GLV split of k recombines to k with halves < 2^130 (tests)
 
 // ---- keys / serialization
 bool pubkey_parse(Ge& r, const unsigned char* in, size_t len);

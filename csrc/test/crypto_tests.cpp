@@ -1,11 +1,13 @@
 // crypto_tests: the hash primitives against published vectors, and the SHA-NI SHA-256 engine
-// against the portable one.
+// against the portable one; the secp256k1 GLV endomorphism multiplication against plain
+// double-and-add.
 // Parity: reference src/test/crypto_tests.cpp (sha256_testvectors: NIST / well-known vectors,
 // the million-'a' message, streaming in arbitrary splits) - here additionally the two engines
 // must agree on every length and split, since the faster one is picked at run time.
 #include "test/unittest.h"
 
 #include "crypto/hashes.h"
+#include "secp256k1/secp256k1.h"
 #include "util/strencodings.h"
 #include "util/util.h"
 
@@ -101,4 +103,101 @@ TEST_CASE(crypto_tests, other_hash_vectors) {
     unsigned char mac[32];
     CHMAC_SHA256((const unsigned char*)"Jefe", 4).Write((const unsigned char*)"what do ya want for nothing?", 28).Finalize(mac);
     CHECK_EQ(hex(mac, 32), std::string("5bdcc146bf60754e6a042426089575c75a003f089d2739839dec58b964ec3843"));
+}
+
+TEST_CASE(crypto_tests, secp256k1_glv_ecmult) {
+    // the endomorphism path (ecmult) against plain double-and-add (ecmult_plain) and the GLV
+    // split's recombination, on random and edge scalars
+    FastRandomContext rng(true);
+    auto rnd_scalar = [&](secp::Scalar& s) {
+        unsigned char b[32];
+        for (auto& x : b) x = (unsigned char)rng.randbits(8);
+        secp::sc_set_b32(s, b);
+    };
+    std::vector<secp::Scalar> edge;
+    for (const char* hex : {"00", "01", "02", "fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0364140",
+                            "0000000000000000000000000000000100000000000000000000000000000000",
+                            "5363ad4cc05c30e0a5261c028812645a122e22ea20816678df02967c1b23bd72",
+                            "a2a8918ca85bafe22016d0b997e4df60c21f5ab2e3b61db4ae2ef2bd9a62a6a8",
+                            "7fffffffffffffffffffffffffffffff5d576e7357a4501ddfe92f46681b20a0"}) {
+        const std::vector<unsigned char> v = ParseHex(hex);
+        unsigned char b[32] = {0};
+        memcpy(b + 32 - v.size(), v.data(), v.size());
+        secp::Scalar s;
+        secp::sc_set_b32(s, b);
+        edge.push_back(s);
+    }
+    int checked = 0;
+    for (int t = 0; t < 400; t++) {
+        secp::Scalar na, ng, ka;
+        if (t < (int)edge.size()) na = edge[t];
+        else rnd_scalar(na);
+        rnd_scalar(ng);
+        rnd_scalar(ka);
+        if (!secp::glv_check(na)) {
+            test::RecordFailure(strprintf("GLV split of scalar %d does not recombine", t), __FILE__, __LINE__);
+            return;
+        }
+        secp::Gej A;
+        secp::ecmult_gen(A, ka);
+        secp::Gej r1, r2;
+        secp::ecmult(r1, A, na, t % 3 == 0 ? edge[0] : ng);
+        secp::ecmult_plain(r2, A, na, t % 3 == 0 ? edge[0] : ng);
+        secp::Ge g1, g2;
+        secp::ge_set_gej(g1, r1);
+        secp::ge_set_gej(g2, r2);
+        if (g1.inf != g2.inf || (!g1.inf && (!secp::fe_equal(g1.x, g2.x) || !secp::fe_equal(g1.y, g2.y)))) {
+            test::RecordFailure(strprintf("ecmult mismatch at %d", t), __FILE__, __LINE__);
+            return;
+        }
+        checked++;
+    }
+    CHECK_EQ(checked, 400);
+}
+
+TEST_CASE(crypto_tests, secp256k1_field_chains_and_verify) {
+    // addition-chain inverse / square root against square-and-multiply, and the windowed scalar
+    // inverse; then ECDSA verification, including the r + n < p branch of the x check
+    FastRandomContext rng(true);
+    for (int t = 0; t < 300; t++) {
+        unsigned char b[32];
+        for (auto& x : b) x = (unsigned char)rng.randbits(8);
+        secp::Fe a, i1, i2, one, prod;
+        secp::fe_set_b32(a, b);
+        if (secp::fe_is_zero(a)) continue;
+        secp::fe_inv(i1, a);
+        secp::fe_inv_slow(i2, a);
+        CHECK(secp::fe_equal(i1, i2));
+        secp::fe_mul(prod, a, i1);
+        secp::fe_set_int(one, 1);
+        CHECK(secp::fe_equal(prod, one));
+        secp::Fe sq, root, back;
+        secp::fe_sqr(sq, a);
+        CHECK(secp::fe_sqrt(root, sq));
+        secp::fe_sqr(back, root);
+        CHECK(secp::fe_equal(back, sq));
+        secp::Scalar s, si, sp;
+        secp::sc_set_b32(s, b);
+        if (secp::sc_is_zero(s)) continue;
+        secp::sc_inv(si, s);
+        secp::sc_mul(sp, s, si);
+        CHECK(sp.n[0] == 1 && sp.n[1] == 0 && sp.n[2] == 0 && sp.n[3] == 0);
+    }
+    // sign/verify round trips and tampering
+    int good = 0;
+    for (int t = 0; t < 200; t++) {
+        unsigned char key[32], msg[32];
+        for (auto& x : key) x = (unsigned char)rng.randbits(8);
+        for (auto& x : msg) x = (unsigned char)rng.randbits(8);
+        if (!secp::seckey_verify(key)) continue;
+        secp::Ge pub;
+        REQUIRE(secp::pubkey_create(pub, key));
+        secp::Signature sig;
+        REQUIRE(secp::ecdsa_sign(sig, nullptr, msg, key));
+        CHECK(secp::ecdsa_verify(sig, msg, pub));
+        msg[t % 32] ^= 1;
+        CHECK(!secp::ecdsa_verify(sig, msg, pub));
+        good++;
+    }
+    CHECK(good > 150);
 }

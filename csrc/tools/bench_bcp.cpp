@@ -20,6 +20,7 @@
 #include "script/sign.h"
 #include "script/standard.h"
 #include "node/sigverify.h"
+#include "secp256k1/secp256k1.h"
 #include "node/txmempool.h"
 #include "node/validation.h"
 #include "primitives/block.h"
@@ -163,6 +164,39 @@ static void SipHash_32b(State& st) {
         for (int i = 0; i < 1000000; i++) *((uint64_t*)x.begin()) = SipHashUint256(0, ++k1, x.begin());
 }
 BENCHMARK(SipHash_32b);
+
+// One CPU ECDSA verification (CPubKey::Verify path: DER parse, key parse, GLV ecmult) per
+// iteration, and the double-scalar multiplication alone with and without the endomorphism.
+static void ECDSAVerify_CPU(State& st) {
+    CKey key;
+    key.MakeNewKey(true);
+    uint256 h;
+    Sha256d((const unsigned char*)"bench", 5, h.begin());
+    std::vector<unsigned char> sig;
+    key.Sign(h, sig);
+    const std::vector<unsigned char> pub = key.GetPubKey().Raw();
+    while (st.KeepRunning())
+        if (!secp::VerifySignature(pub.data(), pub.size(), sig.data(), sig.size(), h.begin())) abort();
+}
+BENCHMARK(ECDSAVerify_CPU);
+static void EcmultVariant(State& st, bool glv) {
+    secp::Scalar na, ng, ka;
+    unsigned char b[32];
+    for (int i = 0; i < 32; i++) b[i] = (unsigned char)(i * 37 + 1);
+    secp::sc_set_b32(na, b);
+    for (int i = 0; i < 32; i++) b[i] = (unsigned char)(i * 11 + 5);
+    secp::sc_set_b32(ng, b);
+    for (int i = 0; i < 32; i++) b[i] = (unsigned char)(i * 7 + 3);
+    secp::sc_set_b32(ka, b);
+    secp::Gej A, r;
+    secp::ecmult_gen(A, ka);
+    while (st.KeepRunning()) {
+        if (glv) secp::ecmult(r, A, na, ng);
+        else secp::ecmult_plain(r, A, na, ng);
+    }
+}
+static bench::Reg reg_EcmultGLV("Ecmult_CPU_GLV", [](State& st) { EcmultVariant(st, true); });
+static bench::Reg reg_EcmultPlain("Ecmult_CPU_Plain", [](State& st) { EcmultVariant(st, false); });
 
 static void FastRandom_32bit(State& st) {
     FastRandomContext rng(true);
