@@ -393,29 +393,22 @@ WorkerPool::~WorkerPool() {
 void WorkerPool::Loop() {
     RenameThread("bcp-worker");
     uint64_t seen = 0;
+    std::unique_lock<std::mutex> l(m);
     while (true) {
-        const std::function<void(size_t)>* fn;
-        size_t n, g;
-        {
-            std::unique_lock<std::mutex> l(m);
-            cv.wait(l, [&] { return stop || generation != seen; });
-            if (stop) return;
-            seen = generation;
-            fn = job;
-            n = jobN;
-            g = grainSz;
-            active++;
-        }
+        cv.wait(l, [&] { return stop || (cur != nullptr && generation != seen); });
+        if (stop) return;
+        seen = generation;
+        Job* j = cur;
+        j->active++;
+        l.unlock();
         while (true) {
-            const size_t start = next.fetch_add(g);
-            if (start >= n) break;
-            const size_t end = std::min(n, start + g);
-            for (size_t i = start; i < end; i++) (*fn)(i);
+            const size_t start = j->next.fetch_add(j->grain);
+            if (start >= j->n) break;
+            const size_t end = std::min(j->n, start + j->grain);
+            for (size_t i = start; i < end; i++) (*j->fn)(i);
         }
-        {
-            std::lock_guard<std::mutex> l(m);
-            if (--active == 0) cvDone.notify_all();
-        }
+        l.lock();
+        if (--j->active == 0) cvDone.notify_all();
     }
 }
 void WorkerPool::ParallelFor(size_t n, const std::function<void(size_t)>& fn, size_t grain) {
@@ -424,27 +417,30 @@ void WorkerPool::ParallelFor(size_t n, const std::function<void(size_t)>& fn, si
         for (size_t i = 0; i < n; i++) fn(i);
         return;
     }
-    // one job at a time per pool (a nested ParallelFor on the same pool from inside fn would
+    // one call at a time per pool (a nested ParallelFor on the same pool from inside fn would
     // deadlock; fn may use another pool)
     std::lock_guard<std::mutex> one(serialize);
+    Job job;
+    job.fn = &fn;
+    job.n = n;
+    job.grain = std::max<size_t>(1, grain);
     {
         std::lock_guard<std::mutex> l(m);
-        job = &fn;
-        jobN = n;
-        grainSz = std::max<size_t>(1, grain);
-        next = 0;
+        cur = &job;
         generation++;
     }
     cv.notify_all();
     while (true) {
-        const size_t start = next.fetch_add(grainSz);
+        const size_t start = job.next.fetch_add(job.grain);
         if (start >= n) break;
-        const size_t end = std::min(n, start + grainSz);
+        const size_t end = std::min(n, start + job.grain);
         for (size_t i = start; i < end; i++) fn(i);
     }
+    // every index is claimed; wait for the workers still inside, then close the call so a
+    // worker waking late does not join it
     std::unique_lock<std::mutex> l(m);
-    cvDone.wait(l, [&] { return active == 0 && next.load() >= n; });
-    job = nullptr;
+    cvDone.wait(l, [&] { return job.active == 0; });
+    cur = nullptr;
 }
 
 // ---------------------------------------------------------------- Scheduler

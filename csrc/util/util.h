@@ -126,14 +126,19 @@ public:
     void ParallelFor(size_t n, const std::function<void(size_t)>& fn, size_t grain = 1);
 
 private:
+    // One ParallelFor call: lives on the caller's stack until every worker that joined it
+    // (active) has left, so a worker never touches a finished call's state.
+    struct Job {
+        const std::function<void(size_t)>* fn;
+        size_t n, grain;
+        std::atomic<size_t> next{0};
+        int active = 0; // workers inside this job (guarded by m)
+    };
     void Loop();
     std::vector<std::thread> threads;
     std::mutex m, serialize;
     std::condition_variable cv, cvDone;
-    const std::function<void(size_t)>* job = nullptr;
-    size_t jobN = 0, grainSz = 1;
-    std::atomic<size_t> next{0};
-    int active = 0;
+    Job* cur = nullptr; // the open call, if any (guarded by m)
     uint64_t generation = 0;
     bool stop = false;
 };

@@ -26,7 +26,7 @@ def test_suite_inventory():
     for s in [
         "script_antireplay_tests", "sigopcount_tests", "bloom_tests", "pmt_tests", "blockencodings_tests",
         "coins_tests", "versionbits_tests", "mempool_tests", "kvstore_tests", "sigbatch_tests", "miner_tests",
-        "policyestimator_tests", "txvalidationcache_tests", "addrman_tests", "crypto_tests", "dos_tests",
+        "policyestimator_tests", "txvalidationcache_tests", "addrman_tests", "crypto_tests", "dos_tests", "checkqueue_tests",
     ]:
         assert s in SUITES, s
 
