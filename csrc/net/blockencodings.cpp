@@ -3,6 +3,10 @@
 #include "crypto/hashes.h"
 #include "node/txmempool.h"
 #include "util/util.h"
+#include "kernels/gpu_api.h"
+
+#include <atomic>
+#include <cstring>
 
 #include <unordered_map>
 
@@ -28,6 +32,27 @@ void CBlockHeaderAndShortTxIDs::FillShortTxIDSelector() const {
 uint64_t CBlockHeaderAndShortTxIDs::GetShortID(const uint256& txhash) const {
     if (!keyed) FillShortTxIDSelector();
     return SipHashUint256(k0, k1, txhash.begin()) & 0xffffffffffffULL;
+}
+
+static std::atomic<size_t> g_gpuShortIdThreshold{16384};
+void SetGpuShortIdThreshold(size_t n) { g_gpuShortIdThreshold = n; }
+size_t GetGpuShortIdThreshold() { return g_gpuShortIdThreshold.load(); }
+
+std::vector<uint64_t> ShortTxIds(const CBlockHeaderAndShortTxIDs& cmpct, const std::vector<CTransactionRef>& txs) {
+    std::vector<uint64_t> ids(txs.size());
+    if (txs.size() >= g_gpuShortIdThreshold.load() && gpu::GpuAvailable()) {
+        std::vector<unsigned char> flat(txs.size() * 32);
+        for (size_t i = 0; i < txs.size(); i++) memcpy(&flat[32 * i], txs[i]->GetHash().begin(), 32);
+        try {
+            ids = gpu::ShortTxIdBatch(cmpct.Key0(), cmpct.Key1(), flat.data(), txs.size());
+            return ids;
+        } catch (const std::exception& e) {
+            // a device error must not lose the reconstruction: hash on the CPU
+            LogPrint(BCLog::CMPCTBLOCK, "GPU short ids failed (%s); computing them on the CPU\n", e.what());
+        }
+    }
+    for (size_t i = 0; i < txs.size(); i++) ids[i] = cmpct.GetShortID(txs[i]->GetHash());
+    return ids;
 }
 
 ReadStatus PartiallyDownloadedBlock::InitData(const CBlockHeaderAndShortTxIDs& cmpct,
@@ -57,8 +82,8 @@ ReadStatus PartiallyDownloadedBlock::InitData(const CBlockHeaderAndShortTxIDs& c
     }
     // bucket-size sanity (reference: fail if the table degenerates)
     std::vector<bool> haveDup(txn_available.size(), false);
-    auto offer = [&](const uint256& h, const CTransactionRef& tx, size_t& counter) {
-        auto it = idmap.find(cmpct.GetShortID(h));
+    auto offer = [&](const uint256& h, uint64_t shortid, const CTransactionRef& tx, size_t& counter) {
+        auto it = idmap.find(shortid);
         if (it == idmap.end()) return;
         const uint16_t idx = it->second;
         if (!haveDup[idx]) {
@@ -74,11 +99,13 @@ ReadStatus PartiallyDownloadedBlock::InitData(const CBlockHeaderAndShortTxIDs& c
         }
     };
     if (pool) {
-        for (const CTransactionRef& tx : pool->AllTransactions()) offer(tx->GetHash(), tx, mempool_count);
+        const std::vector<CTransactionRef> all = pool->AllTransactions();
+        const std::vector<uint64_t> ids = ShortTxIds(cmpct, all);
+        for (size_t i = 0; i < all.size(); i++) offer(all[i]->GetHash(), ids[i], all[i], mempool_count);
     }
     for (const auto& e : extra_txn) {
         if (!e.second) continue;
-        offer(e.first, e.second, extra_count);
+        offer(e.first, cmpct.GetShortID(e.first), e.second, extra_count);
     }
     LogPrint(BCLog::CMPCTBLOCK, "Initialized PartiallyDownloadedBlock for block %s using a cmpctblock of size %zu\n",
              cmpct.header.GetHash().ToString().c_str(), GetSerializeSize(cmpct));

@@ -83,11 +83,21 @@ public:
         if (BlockTxCount() > 0xFFFF) throw ser_error("indexes overflowed 16 bits");
     }
 
+    // SipHash key (k0, k1) of the short ids (keyed on first use)
+    uint64_t Key0() const { if (!keyed) FillShortTxIDSelector(); return k0; }
+    uint64_t Key1() const { if (!keyed) FillShortTxIDSelector(); return k1; }
+
 private:
     void FillShortTxIDSelector() const;
     mutable uint64_t k0 = 0, k1 = 0;
     mutable bool keyed = false;
 };
+
+// Short ids of many transactions under one compact block's key: on the GPU (K9, relay.hip) for
+// at least -gpushortidthreshold transactions when a device is visible, else on the CPU.
+std::vector<uint64_t> ShortTxIds(const CBlockHeaderAndShortTxIDs& cmpct, const std::vector<CTransactionRef>& txs);
+void SetGpuShortIdThreshold(size_t n);
+size_t GetGpuShortIdThreshold();
 
 class BlockTransactionsRequest {
 public:

@@ -72,7 +72,15 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
                            const std::vector<DeferredMultisig>& groups, WorkerPool* pool, bool useGpu,
                            bool cacheStore, bool cacheErase);
 // Device verification of the given checks (no cache); result[i] = 1 iff valid.
-std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool);
+// Checks carrying sighash recipes go through the fused digest -> verify lane path; digests
+// (optional) receives every check's digest.
+std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool,
+                                       std::vector<uint256>* digests = nullptr);
+// Device sighash recipes in block validation (-gpusighash): 0 off, 1 during initial block
+// download (the signature cache is cold there, and recipe checks skip its pre-batch probe),
+// 2 always.
+void SetGpuSighashMode(int mode);
+int GetGpuSighashMode();
 void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path
 size_t GetGpuSigThreshold();
 void ResetGpuSigFailures();

@@ -193,6 +193,15 @@ void bind_gpu(pyb::module_& m) {
         },
         pyb::arg("leaves"), pyb::arg("device") = -1);
     m.def(
+        "short_txid_batch_gpu",
+        [](uint64_t k0, uint64_t k1, const pyb::bytes& txids, int device) {
+            auto v = to_vec(txids);
+            if (v.size() % 32) throw std::invalid_argument("txids must be 32-byte hashes");
+            pyb::gil_scoped_release rel;
+            return gpu::ShortTxIdBatch(k0, k1, v.data(), v.size() / 32, device);
+        },
+        pyb::arg("k0"), pyb::arg("k1"), pyb::arg("txids"), pyb::arg("device") = -1);
+    m.def(
         "sha256d_scan_nonces_gpu",
         [](const pyb::bytes& header80, const pyb::bytes& target_le, uint32_t start, uint64_t count, int device) {
             auto h = to_vec(header80), t = to_vec(target_le);
