@@ -1228,8 +1228,36 @@ bool Chainstate::DisconnectTip(CValidationState& state, bool fBare) {
     return true;
 }
 
+// -debug=bench accumulators of ConnectTip (reference src/validation.cpp:1690-1700 nTimeCheck,
+// nTimeForks, nTimeConnect, nTimeVerify, nTimeIndex, nTimeCallbacks, nTimeTotal and
+// :2200-2290 ConnectTip's per-step lines): each line shows this block's time and the running
+// total since startup. The connect split is the MI355X pipeline's own phases.
+namespace {
+struct BenchTotals {
+    std::atomic<int64_t> read{0}, connect{0}, flush{0}, chainstate{0}, post{0}, total{0};
+    std::atomic<int64_t> phase[Chainstate::PH_COUNT] = {};
+    std::atomic<int64_t> blocks{0};
+};
+BenchTotals& Bench() {
+    static BenchTotals t;
+    return t;
+}
+const char* const kPhaseNames[Chainstate::PH_COUNT] = {"Sanity checks", "Prefetch + precompute", "UTXO pass",
+                                                      "Script jobs wait", "Collect checks", "Signature batch",
+                                                      "Pipelined blocks"};
+void BenchLine(const char* indent, const char* what, int64_t micros, std::atomic<int64_t>& acc) {
+    const int64_t tot = (acc += micros);
+    LogPrint(BCLog::BENCH, "%s- %s: %.2fms [%.2fs]\n", indent, what, 0.001 * micros, 1e-6 * tot);
+}
+} // namespace
+
 bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, const std::shared_ptr<const CBlock>& pblock,
                             ConnectTrace& trace) {
+    const bool bench = LogAcceptCategory(BCLog::BENCH);
+    const int64_t nTime1 = GetTimeMicros();
+    int64_t ph0[PH_COUNT];
+    if (bench)
+        for (int k = 0; k < PH_COUNT; k++) ph0[k] = ConnectPhaseMicros((ConnectPhase)k);
     std::shared_ptr<const CBlock> pthisBlock;
     if (!pblock) {
         auto pblockNew = std::make_shared<CBlock>();
@@ -1240,6 +1268,8 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
     }
     trace.blocksConnected.emplace_back(pindexNew, pthisBlock);
     const CBlock& blockConnecting = *pthisBlock;
+    const int64_t nTime2 = GetTimeMicros();
+    int64_t nTime3, nTime4;
     {
         CCoinsViewCache view(pcoinsTip.get());
         const bool rv = ConnectBlock(blockConnecting, state, pindexNew, view);
@@ -1249,11 +1279,29 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
             return error("ConnectTip(): ConnectBlock %s failed (%s)", pindexNew->GetBlockHash().ToString().c_str(),
                          FormatStateMessage(state).c_str());
         }
+        nTime3 = GetTimeMicros();
         view.Flush();
+        nTime4 = GetTimeMicros();
     }
     if (!FlushStateToDisk(state, FLUSH_STATE_IF_NEEDED)) return false;
+    const int64_t nTime5 = GetTimeMicros();
     if (mempool) mempool->removeForBlock(blockConnecting.vtx, pindexNew->nHeight);
     UpdateTip(pindexNew);
+    if (bench) {
+        const int64_t nTime6 = GetTimeMicros();
+        BenchTotals& B = Bench();
+        B.blocks++;
+        BenchLine("  ", "Load block from disk", nTime2 - nTime1, B.read);
+        for (int k = 0; k < PH_COUNT; k++) {
+            const int64_t d = ConnectPhaseMicros((ConnectPhase)k) - ph0[k];
+            if (d > 0 || k != PH_BLOCKS) BenchLine("      ", kPhaseNames[k], d, B.phase[k]);
+        }
+        BenchLine("    ", "Connect total", nTime3 - nTime2, B.connect);
+        BenchLine("  ", "Flush", nTime4 - nTime3, B.flush);
+        BenchLine("  ", "Writing chainstate", nTime5 - nTime4, B.chainstate);
+        BenchLine("  ", "Connect postprocess", nTime6 - nTime5, B.post);
+        BenchLine("", "Connect block", nTime6 - nTime1, B.total);
+    }
     return true;
 }
 
