@@ -35,7 +35,7 @@ size_t InitSignatureCache(int64_t mib) {
 }
 
 static std::atomic<size_t> g_gpuThreshold{DEFAULT_GPU_SIG_THRESHOLD};
-static std::atomic<int> g_gpuSighashMode{1};
+static std::atomic<int> g_gpuSighashMode{0}; // measured slower end to end, profiles/sighash_shortid_r3.md
 void SetGpuSighashMode(int mode) { g_gpuSighashMode = mode; }
 int GetGpuSighashMode() { return g_gpuSighashMode.load(); }
 void SetGpuSigThreshold(size_t n) { g_gpuThreshold = n; }
