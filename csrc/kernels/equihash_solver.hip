@@ -4,33 +4,34 @@
 //
 // Design: a bucket-sorted Wagner solver with parent pointers and contiguous buckets.
 //
-//  * Rows are bucketed on the top BB bits of the current digit (NB = 2^BB buckets,
-//    ~INIT/NB rows each; (200,9): 512 buckets x 4096 rows). Every stage keeps each bucket
-//    CONTIGUOUS in its own area of AREA row slots.
+//  * Rows are bucketed on the top BB bits of the current digit (NB = 2^BB buckets, ~INIT/NB rows
+//    each). (200,9) runs BB = 9: 512 buckets of ~4096 rows, one 1024-thread round workgroup per
+//    CU (145 KiB of LDS). BCP_EH_BB=10 builds 1024 buckets of ~2048 rows with two 512-thread
+//    workgroups (<= 80 KiB each) per CU; it measured slower (the phases are latency-bound per
+//    lane, and the producer runs are 4x shorter), profiles/equihash_r4.md.
+//    Every stage keeps each bucket CONTIGUOUS in its own area of AREA row slots.
 //  * Every kernel works "one workgroup per bucket". A producer workgroup counting-sorts its
 //    output rows by destination bucket in LDS, then claims one run per destination with ONE
-//    device-scope atomicAdd on that bucket's fill counter (a 512-lane, 2 KB contiguous wave
-//    instruction set per workgroup, issued as soon as the histogram is known so its latency
-//    hides behind the scan and scatter), and writes its rows into the claimed runs. The
-//    consumer round then reads its bucket as one contiguous block (16-byte loads, lane-flat,
-//    straight into LDS): no run tables, slot maps or per-row gather maps.
+//    device-scope atomicAdd on that bucket's fill counter (issued as soon as the histogram is
+//    known so its latency hides behind the scan and scatter), and writes its rows into the
+//    claimed runs. The consumer round then reads its bucket as one contiguous block (16-byte
+//    loads, straight into LDS): no run tables, slot maps or per-row gather maps.
 //  * Collisions on the remaining RB = DB-BB bits of the digit are found by a counting sort of
 //    the bucket on those bits and an atomic-free pair enumeration (scan + max-scan); each output
-//    row keeps a 64-bit parent triple (producing bucket, LDS row i, LDS row j), so nothing ever
-//    carries index lists: the parents of a stage-s row are the stage-(s-1) slots
-//    bucket*AREA + i and bucket*AREA + j.
-//  * Depth-1 duplicate pruning: pairs whose rows share a parent are dropped.
+//    row keeps a parent triple (producing bucket, LDS row i, LDS row j), so nothing ever carries
+//    index lists: the parents of a stage-s row are the stage-(s-1) slots bucket*AREA + i and
+//    bucket*AREA + j.
+//  * Depth-1 duplicate pruning (pairs whose rows share a parent are dropped) wherever the parent
+//    words fit in the round's LDS budget.
 //  * Final round: pairs equal on all remaining bits are candidates; eh_expand walks the K levels
 //    of parent triples, canonicalises subtree order (reference IsValidSolution ordering rule)
 //    and rejects repeated indices (LDS bitonic sort).
 //  * Block scans use DPP row shifts/broadcasts inside a wave and one LDS word per wave
 //    across waves: two barriers per scan, no ds_bpermute traffic.
 //
-// Memory layout (BCP_EH_MERGED, default): every stage has its own slot array and a stage-s
-// slot holds the row followed by its parent triple, so the emit writes one contiguous slot per
-// output row (one store stream instead of a row stream plus a parent stream: the separate 8-byte
-// parent stores cost 40-50% of the emit phase, profiles/equihash_r2_gen.md) and a pruning round
-// gets the parents with the rows. Keeping all K stage arrays costs 51 words per slot per nonce
+// Memory layout: every stage has its own slot array and a stage-s slot holds the row followed by
+// its parent word(s), so the emit writes one contiguous slot per output row and a pruning round
+// gets the parents with the rows. Keeping all K stage arrays costs ~50 words per slot per nonce
 // (≈17 GB per 32-nonce solver, against 288 GB of HBM); the parents must outlive the rows anyway
 // for the final expansion. Per row per round: one contiguous slot read, one slot write into a
 // claimed run.
@@ -46,29 +47,13 @@
 #include <stdexcept>
 #include <utility>
 
-// Generation kernel choice: BCP_EH_GEN_NTG > 0 selects eh_gen_reg with that many threads per
-// workgroup and BCP_EH_GEN_HPT hashes per thread, where the geometry allows ((200,9)); 0 selects
-// the LDS-sorted eh_gen everywhere (A/B builds, tools/build_variant.sh). 512 x 2 measured best
-// (profiles/equihash_r2_gen.md): 2.06 -> 1.75 ms per 32 nonces.
-#ifndef BCP_EH_GEN_NTG
-#define BCP_EH_GEN_NTG 512
+#ifndef BCP_EH_BB // bucket bits of the (200,9) solver: 9 (one 1024-thread round workgroup per CU) or
+#define BCP_EH_BB 9 //  10 (two 512-thread workgroups per CU; measured slower, profiles/equihash_r4.md)
 #endif
-#ifndef BCP_EH_GEN_HPT
-#define BCP_EH_GEN_HPT 2
-#endif
-#ifndef BCP_EH_MERGED // 1: each stage-s slot holds the row AND its parent triple (one store stream)
-#define BCP_EH_MERGED 1
-#endif
-#ifndef BCP_EH_LEAF_SLOT // 1 (merged layout): a stage-0 slot holds the row and its leaf index
-#define BCP_EH_LEAF_SLOT 0 // measured neutral (round 1 reads 7-word slots), profiles/equihash_r2_gen.md
-#endif
-#ifndef BCP_EH_SLOT_ALIGN // merged layout: slot widths rounded up to a multiple of this many words
-#define BCP_EH_SLOT_ALIGN 1 // 2 and 4 measured slower (more bytes, no alignment gain)
-#endif
-#ifndef BCP_EH_ROWONLY_LOAD // merged layout: non-pruning rounds skip the parent words of a slot
+#ifndef BCP_EH_ROWONLY_LOAD // non-pruning rounds skip the parent words of a slot
 #define BCP_EH_ROWONLY_LOAD 1
 #endif
-#ifndef BCP_EH_COMPACT_PARENT // 1 (merged layout): one parent word where the row has 3 spare bits
+#ifndef BCP_EH_COMPACT_PARENT // 1: one parent word where the row has spare padding bits
 #define BCP_EH_COMPACT_PARENT 1
 #endif
 #ifndef BCP_EH_ST_CPOL // cache-policy bits of the slot stores (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
@@ -80,20 +65,42 @@
 #ifndef BCP_EH_XCD_MAP // 1: every kernel of a nonce runs on one XCD (nonce % 8), so the run writes
 #define BCP_EH_XCD_MAP 1  //    of a nonce meet in one L2 (batches that are a multiple of 8 nonces)
 #endif
-#ifndef BCP_EH_PF_SLICES // merged layout: the next bucket's rows are prefetched in this many slices
+#ifndef BCP_EH_PF_SLICES // the next bucket's rows are prefetched in this many slices
 #define BCP_EH_PF_SLICES 3
-#endif
-#ifndef BCP_EH_EXP_NOPARENT // timing experiment only: emit stores no parent triples (no solutions)
-#define BCP_EH_EXP_NOPARENT 0
 #endif
 #ifndef BCP_EH_GEN_WPE // minimum waves per SIMD the generation kernel's registers must allow
 #define BCP_EH_GEN_WPE 1
 #endif
+#ifndef BCP_EH_GEN_HPT // (200,9) register generation: hashes per thread
+#define BCP_EH_GEN_HPT 2
+#endif
+#ifndef BCP_EH_GEN_PERSIST // > 0: register generation runs this many persistent workgroups per CU
+#define BCP_EH_GEN_PERSIST 0 //  (each loops over work items) instead of one workgroup per item
+#endif
+#ifndef BCP_EH_EXP_STORE // timing experiments only (tools/build_variant.sh): 1 = drop the emit stores,
+#define BCP_EH_EXP_STORE 0 // 2 = store each bucket's output rows contiguously (no scatter; wrong results)
+#endif
+#ifndef BCP_EH_PAIRS // pair enumeration: 1 = per-wave compaction into an LDS pair list (one barrier),
+#define BCP_EH_PAIRS 1 //  0 = block scan + max-scan over pair indices (four barriers)
+#endif
+#ifndef BCP_EH_EXP_LOAD // timing experiment only: 1 = every round bucket loads one of its nonce's first 8
+#define BCP_EH_EXP_LOAD 0 //  areas (L2-resident) instead of its own (wrong results)
+#endif
+#ifndef BCP_EH_ISSUE_LATE // 1: a round issues its next-bucket loads after the key sort, not at the commit
+#define BCP_EH_ISSUE_LATE 0
+#endif
+#ifndef BCP_EH_GEN_LDS // 1: force the LDS-sorted generation kernel everywhere (A/B builds)
+#define BCP_EH_GEN_LDS 0
+#endif
 
 namespace bcpk {
 
+// N, K: Equihash parameters. BB: bucket bits. CAP/CAP4/CAP3: LDS row capacity of rounds reading
+// rows of >= 5, 4, <= 3 words. NT: threads per round workgroup; WGCU: round workgroups per CU
+// the LDS budget must allow. GENWG/NTG: LDS-sorted generation geometry; GNT x GHPT: register
+// generation (threads x hashes per thread; 0 = use the LDS-sorted kernel).
 template <int N_, int K_, int BB_, int CAP_, int NT_, int GENWG_, int NTG_, int MAXCAND_, int CAP4_ = CAP_,
-          int CAP3_ = CAP_>
+          int CAP3_ = CAP_, int WGCU_ = 1, int GNT_ = 512, int GHPT_ = 2>
 struct EhCfg {
     static constexpr int N = N_, K = K_;
     static constexpr int DB = N / (K + 1);           // digit bits
@@ -110,9 +117,12 @@ struct EhCfg {
     static constexpr int AREA = CAP_ > CAP4_ ? (CAP_ > CAP3_ ? CAP_ : CAP3_) : (CAP4_ > CAP3_ ? CAP4_ : CAP3_);
     static constexpr int NT = NT_;                   // threads per round workgroup
     static constexpr int NW = NT_ / 64;
+    static constexpr int WGCU = WGCU_;
+    static constexpr int LDS_BUDGET = 160 * 1024 / WGCU_;
     static constexpr int INIT = 1 << (DB + 1);
-    static constexpr int GENWG = GENWG_;             // generation workgroups per nonce
-    static constexpr int NTG = NTG_;                 // threads per generation workgroup
+    static constexpr int GENWG = GENWG_;             // LDS-sorted generation: workgroups per nonce
+    static constexpr int NTG = NTG_;                 // LDS-sorted generation: threads per workgroup
+    static constexpr int GNT = GNT_, GHPT = GHPT_;   // register generation geometry
     static constexpr int RPW = INIT / GENWG_;        // rows per generation workgroup
     static constexpr int IPH = 512 / N;
     static constexpr int NBYTES = N / 8;
@@ -121,30 +131,39 @@ struct EhCfg {
     static constexpr int bits(int stage) { return N - stage * DB - BB_; }
     static constexpr int words(int stage) { return (bits(stage) + 31) / 32; }
     static constexpr int WMAX = words(0);
-    // words per slot of stage s: the row, plus (s >= 1, merged layout) its parent triple
-    static constexpr bool LEAFSLOT = BCP_EH_MERGED && BCP_EH_LEAF_SLOT;
-    // Compact parents: the triple (d, i, j) as ONE word (i, j: 13 bits each, 6 bits of d) plus the
-    // top 3 bits of d in the low (padding) bits of the row's last word, where the row has them.
+    // Compact parents: the triple (d, i, j) as ONE word. i and j take IB bits each in the two
+    // halves of the word, the 16 - IB spare bits of each half carry DX bits of d, and the DR
+    // remaining bits of d ride in the low (padding) bits of the row's last word.
+    static constexpr int IB = AREA <= 4096 ? 12 : 13;
+    static constexpr int DH = 16 - IB;
+    static constexpr uint32_t DHM = (1u << DH) - 1;
+    static constexpr int DX = 2 * DH;
+    static constexpr int DR = BB_ > DX ? BB_ - DX : 0;
+    static constexpr uint32_t RMASK = (1u << DR) - 1;
+    static constexpr uint32_t IMASK = ((1u << IB) - 1) * 0x10001u;
     static constexpr bool cp(int stage) {
-        return BCP_EH_MERGED && BCP_EH_COMPACT_PARENT && stage >= 1 && stage < K &&
-               32 * words(stage) - bits(stage) >= 3 && NB <= 512;
+        return BCP_EH_COMPACT_PARENT && stage >= 1 && stage < K && 32 * words(stage) - bits(stage) >= DR;
     }
-    static constexpr int sw(int stage) {
-        return !BCP_EH_MERGED ? words(stage)
-                              : ((stage == 0 ? words(0) + (LEAFSLOT ? 1 : 0) : words(stage) + (cp(stage) ? 1 : 2)) +
-                                 BCP_EH_SLOT_ALIGN - 1) /
-                                    BCP_EH_SLOT_ALIGN * BCP_EH_SLOT_ALIGN;
-    }
+    static constexpr uint32_t rmask(int stage) { return cp(stage) ? RMASK : 0u; } // parent bits in a row's padding
+    // words per slot of stage s: the row, plus (s >= 1) its parent word(s)
+    static constexpr int sw(int stage) { return stage == 0 ? words(0) : words(stage) + (cp(stage) ? 1 : 2); }
     static constexpr size_t ROWS = (size_t)NB * AREA; // slots per stage per nonce
+    // 16-bit LDS histograms (two counters per word) where 32-bit ones would not fit two per CU
+    static constexpr bool H16 = NB > 512;
+    static constexpr int HW = H16 ? NB / 2 : NB;      // words per histogram
     static_assert(RPW * GENWG_ == INIT && RPW < 65535, "generation split");
     static_assert(RB > 0 && DB < 32, "digit geometry");
-    static_assert(AREA < 8192, "13-bit LDS row indices in parent triples and signatures");
-    static_assert(NT_ % 64 == 0 && NT_ <= 1024 && NB <= NT_ && NB <= NTG_ && NT_ / 64 <= 64, "workgroup shape");
+    static_assert(AREA < (1 << IB), "LDS row indices in parent words and signatures");
+    static_assert(NT_ % 64 == 0 && NT_ <= 1024 && (NB <= NT_ || NB % NT_ == 0) && NB <= NTG_ && NT_ / 64 <= 64,
+                  "workgroup shape");
     static_assert(words(K - 1) == 1, "final round keeps whole rows in one LDS word");
 };
 
-// Mainnet/testnet (200,9); (96,5); regtest (48,5).
-using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120>;
+// Mainnet/testnet (200,9): 512 buckets x ~4096 rows, one 1024-thread round workgroup per CU
+// (BCP_EH_BB=10: 1024 buckets x ~2048 rows, two 512-thread workgroups per CU); (96,5); regtest (48,5).
+using Cfg200_9_bb10 = EhCfg<200, 9, 10, 2304, 512, 512, 1024, 256, 2560, 2688, 2, 1024, 2>;
+using Cfg200_9_bb9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, 512, BCP_EH_GEN_HPT>;
+using Cfg200_9 = std::conditional_t<BCP_EH_BB == 10, Cfg200_9_bb10, Cfg200_9_bb9>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
 using Cfg48_5 = EhCfg<48, 5, 3, 512, 64, 8, 64, 256>; // 512-slot areas: 8 pairs per lane (a 256-pair list overflowed on duplicate-heavy nonces)
 
@@ -388,18 +407,17 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
     __syncthreads();
     constexpr int SW0 = C::sw(0);
     const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * SW0, (uint32_t)(C::ROWS * SW0 * 4));
-    uint32_t* leaf = C::LEAFSLOT ? nullptr : LEAF + (size_t)nonce * C::ROWS;
+    uint32_t* leaf = LEAF + (size_t)nonce * C::ROWS;
     for (int t = tid; t < C::RPW; t += NTG) {
         const uint32_t li = perm[t], d = dst[li];
         const uint32_t pos = base[d] + (uint32_t)t;
         if (pos < OCAP) {
-            uint32_t o[SW0 > W0 ? SW0 : W0 + 1] = {};
+            uint32_t o[W0];
 #pragma unroll
             for (int w = 0; w < W0; ++w) o[w] = rows[li * W0 + w];
-            o[W0] = r0 + li;
             const uint32_t slot = d * C::AREA + pos;
             row_store<SW0>(rs, slot * (SW0 * 4), o);
-            if constexpr (!C::LEAFSLOT) leaf[slot] = r0 + li;
+            leaf[slot] = r0 + li;
         }
     }
 }
@@ -407,33 +425,37 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
 // Register-resident generation for configs whose rows split evenly over hashes (IPH | RPW):
 // every thread keeps the HPT*IPH rows it hashed in VGPRs, takes its rank inside this
 // workgroup's run of each row's bucket with an LDS atomicAdd (returning), and after the
-// run claims writes the rows straight from registers. LDS holds only the two 512-entry
+// run claims writes the rows straight from registers. LDS holds only the two NB-entry
 // tables, so several workgroups share a CU and one's hashing (VALU) overlaps another's
 // claim and scatter (memory) — the LDS-sorted eh_gen above holds a whole CU with its 118 KB
 // row buffer and runs those phases back to back.
 template <class C, int NTG, int HPT> struct GenReg {
     static constexpr int RPT = HPT * C::IPH;            // rows per thread
     static constexpr int RPW = NTG > 0 ? NTG * RPT : 1; // rows per workgroup
-    static constexpr bool OK = NTG > 0 && C::INIT % RPW == 0;
+    static constexpr bool OK = !BCP_EH_GEN_LDS && NTG > 0 && C::INIT % RPW == 0;
     static constexpr int GWG = OK ? C::INIT / RPW : 1;  // workgroups per nonce
 };
 template <class C, bool HDR, int NTG, int HPT>
 __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_WPE))) void eh_gen_reg(const EhBaseState* __restrict__ states, uint32_t* __restrict__ R,
-                                                  uint32_t* __restrict__ LEAF, uint32_t* __restrict__ CTR0) {
+                                                  uint32_t* __restrict__ LEAF, uint32_t* __restrict__ CTR0, int items) {
     using G = GenReg<C, NTG, HPT>;
     static_assert(G::OK, "register generation geometry");
     constexpr int W0 = C::words(0);
     constexpr int SW = (C::N + 31) / 32 + 1;
     constexpr uint32_t OCAP = C::cap(1);
     __shared__ uint32_t hist[C::NB], base[C::NB];
-    int gw = blockIdx.x % G::GWG;
-    int nonce = blockIdx.x / G::GWG;
-    if (BCP_EH_XCD_MAP && (gridDim.x / G::GWG) % NXCD == 0) { // nonce n's workgroups on XCD n % 8
-        const int x = blockIdx.x % NXCD, j = blockIdx.x / NXCD;
+    const int tid = threadIdx.x;
+    // work item b = (nonce, gw); a persistent grid (gridDim.x < items, a multiple of 8) keeps every
+    // item of a workgroup on that workgroup's XCD
+    for (int b = blockIdx.x; b < items; b += gridDim.x) {
+    int gw = b % G::GWG;
+    int nonce = b / G::GWG;
+    if (BCP_EH_XCD_MAP && (items / G::GWG) % NXCD == 0 && gridDim.x % NXCD == 0) { // nonce n's workgroups on XCD n % 8
+        const int x = b % NXCD, j = b / NXCD;
         gw = j % G::GWG;
         nonce = x + NXCD * (j / G::GWG);
     }
-    const int tid = threadIdx.x;
+    if (b != (int)blockIdx.x) __syncthreads(); // the previous item's scatter has read base[]
     const EhBaseState& bs = states[nonce];
     for (int i = tid; i < C::NB; i += NTG) hist[i] = 0;
     __syncthreads();
@@ -476,7 +498,7 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     __syncthreads();
     constexpr int SW0 = C::sw(0);
     const auto rs = buf_rsrc(R + (size_t)nonce * C::ROWS * SW0, (uint32_t)(C::ROWS * SW0 * 4));
-    const auto rl = buf_rsrc(C::LEAFSLOT ? R : LEAF + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 4));
+    const auto rl = buf_rsrc(LEAF + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 4));
 #pragma unroll
     for (int q = 0; q < G::RPT; ++q) {
         const uint32_t d = rk[q] & 0xffff;
@@ -485,16 +507,9 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
         const bool ok = pos < OCAP;
         const uint32_t g = g0 + (q / C::IPH) * NTG + tid;
         const uint32_t li = g * C::IPH + (q % C::IPH); // leaf index
-        if constexpr (C::LEAFSLOT) {
-            uint32_t o[SW0 > W0 ? SW0 : W0 + 1] = {};
-#pragma unroll
-            for (int w = 0; w < W0; ++w) o[w] = rw[q][w];
-            o[W0] = li;
-            row_store<SW0>(rs, ok ? slot * (SW0 * 4) : OOB, o);
-        } else {
-            row_store<W0>(rs, ok ? slot * (SW0 * 4) : OOB, rw[q]);
-            __builtin_amdgcn_raw_buffer_store_b32(li, rl, ok ? slot * 4 : OOB, 0, 0);
-        }
+        row_store<W0>(rs, ok ? slot * (SW0 * 4) : OOB, rw[q]);
+        __builtin_amdgcn_raw_buffer_store_b32(li, rl, ok ? slot * 4 : OOB, 0, 0);
+    }
     }
 }
 
@@ -504,27 +519,13 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
 __device__ __forceinline__ uint64_t pack_tri(uint32_t d, uint32_t i, uint32_t j) {
     return ((uint64_t)d << 32) | (j << 16) | i;
 }
-// Compact parent word: i | j << 16 with bits 13-15 / 29-31 holding d's bits 0-2 / 3-5; d's bits
-// 6-8 ride in the low 3 bits of the row's last word (EhCfg::cp).
-__device__ __forceinline__ uint32_t cpack(uint32_t d, uint32_t i, uint32_t j) {
-    return i | (j << 16) | ((d & 7) << 13) | (((d >> 3) & 7) << 29);
+// Compact parent word (EhCfg::cp): i | j << 16, the spare high bits of each half holding d's bits
+// 0..DH-1 and DH..DX-1; d's bits DX.. ride in the low bits of the row's last word.
+template <class C> __host__ __device__ __forceinline__ uint32_t cpack(uint32_t d, uint32_t i, uint32_t j) {
+    return i | (j << 16) | ((d & C::DHM) << C::IB) | (((d >> C::DH) & C::DHM) << (16 + C::IB));
 }
-__host__ __device__ __forceinline__ uint32_t cunpack_d(uint32_t pw, uint32_t lastword) {
-    return ((pw >> 13) & 7) | (((pw >> 29) & 7) << 3) | ((lastword & 7) << 6);
-}
-inline uint32_t cunpack_d_host(uint32_t pw, uint32_t lastword) { return cunpack_d(pw, lastword); }
-// 2 x 16-bit signature of a row's parents for depth-1 duplicate pruning: each half is the
-// parent's LDS row (13 bits) plus 3 bits of the producing bucket. A half shared by two rows is
-// confirmed exactly by comparing the full producing buckets: a signature-only prune would drop
-// ~1e-4 of all pairs, ~6% of the solutions (511 pairs each).
-__device__ __forceinline__ uint32_t parent_sig(uint64_t tri) {
-    const uint32_t d = (uint32_t)(tri >> 32), f = (uint32_t)tri;
-    const uint32_t i = f & 0x1fff, j = (f >> 16) & 0x1fff;
-    return ((i | ((d & 7) << 13)) << 16) | (j | ((d & 7) << 13));
-}
-__device__ __forceinline__ bool sig_hit(uint32_t si, uint32_t sj) {
-    return (si >> 16) == (sj >> 16) || (si >> 16) == (sj & 0xffff) || (si & 0xffff) == (sj >> 16) ||
-           (si & 0xffff) == (sj & 0xffff);
+template <class C> __host__ __device__ __forceinline__ uint32_t cunpack_d(uint32_t pw, uint32_t lastword) {
+    return ((pw >> C::IB) & C::DHM) | (((pw >> (16 + C::IB)) & C::DHM) << C::DH) | ((lastword & C::RMASK) << C::DX);
 }
 
 // Diagnostic builds (STAMP) record s_memtime at each phase boundary (thread 0, after the
@@ -536,83 +537,118 @@ __device__ __forceinline__ bool sig_hit(uint32_t si, uint32_t sj) {
         }                                                                                            \
     } while (0)
 
-// LDS bytes of a round. Phase-D union `un` (bytes): {sidx[CAP] u16, bend[NRESTS] u32,
-// offp[CAP] u16} during the collision search, the slot -> pair table spair[AREA] u32 after it.
+// LDS bytes of a round. Phase-D union `un` (bytes): {sidx[CAP] u16, bend[NRESTS] u32, then
+// offp[CAP] u16 or plist[MP*NT] u32} during the collision search, the slot -> pair table
+// spair[MP*NT] u32 after it.
 template <class C> constexpr int un_walk_bend(int cap) { return (cap * 2 + 3) / 4 * 4; }
 template <class C> constexpr int un_walk_offp(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
-template <class C> constexpr int round_un(int cap) {
-    const int walk = un_walk_offp<C>(cap) + cap * 2;
-    return walk > C::AREA * 4 ? walk : C::AREA * 4;
+template <class C> constexpr int round_mp(int stage) { return stage == C::K ? 1 : (C::AREA + C::NT - 1) / C::NT; }
+template <class C> constexpr int round_un(int stage) {
+    const int cap = C::cap(stage);
+    if (stage == C::K) return un_walk_offp<C>(cap); // final round: sidx and bend only
+    // offp[CAP] u16 (scan enumeration) or the pair list plist[MP*NT] u32 (wave compaction)
+    const int walk = un_walk_offp<C>(cap) + (BCP_EH_PAIRS && stage < C::K ? round_mp<C>(stage) * C::NT * 4 : cap * 2);
+    const int pairs = round_mp<C>(stage) * C::NT * 4; // spair: every pair a lane may hold
+    return walk > pairs ? walk : pairs;
 }
 template <class C> constexpr int round_lds(int stage, bool prune) {
     const int WI = C::words(stage - 1);
     const int cap = C::cap(stage);
-    const int marks = stage == C::K ? 0 : (C::AREA + C::NT - 1) / C::NT * C::NT * 2;
-    return (cap * WI + 3) / 4 * 16 + (prune ? cap * 6 : 0) + marks + round_un<C>(cap) + 3 * C::NB * 4 + 512;
+    const int marks = stage == C::K || BCP_EH_PAIRS ? 4 : (round_mp<C>(stage) * C::NT * 2 + 3) / 4 * 4;
+    const int pruneb = prune ? cap * 4 + (C::cp(stage - 1) ? 0 : (cap * 2 + 3) / 4 * 4) : 0;
+    const int hists = stage == C::K ? 12 : 2 * C::HW * 4 + (C::NB * (C::H16 ? 2 : 4) + 3) / 4 * 4;
+    return (cap * WI + 3) / 4 * 16 + pruneb + marks + round_un<C>(stage) + hists + (C::NW + 1) * 4;
 }
-// Depth-1 duplicate pruning wherever its signatures fit next to the full rows.
+// Depth-1 duplicate pruning wherever its parent words fit next to the full rows.
 template <class C> constexpr bool round_prunes(int stage) {
-    return stage >= 2 && round_lds<C>(stage, true) <= 160 * 1024;
+    return stage >= 2 && round_lds<C>(stage, true) <= C::LDS_BUDGET;
 }
 
 // STAGE < K: collision round producing stage-STAGE rows. STAGE == K: final round.
 // Bucket bk = nonce*NB + d holds the stage STAGE-1 rows whose top digit bits are d (area d of
 // that stage, CTRin[bk] rows).
 //
-// The kernel is PERSISTENT and software-pipelined: one workgroup per CU walks buckets
-// blockIdx.x, +gridDim.x, ... While it collides bucket b out of LDS, the rows of its next
-// bucket are in flight into VGPRs (16-byte lane-flat loads of the contiguous area, issued in
-// slices across the phases; plain loads are not drained by a bare barrier). Per bucket:
-//   A. commit: prefetched words (VGPRs) -> LDS rows (+ parent signatures when pruning);
+// The kernel is PERSISTENT and software-pipelined: WGCU workgroups per CU walk buckets
+// blockIdx.x, +gridDim.x, ... While one collides bucket b out of LDS, the rows of its next
+// bucket are in flight into VGPRs (lane-flat row loads of the contiguous area, issued in slices
+// across the phases; plain loads are not drained by a bare barrier). Per bucket:
+//   A. commit: prefetched rows (VGPRs) -> LDS rows (+ parent words when pruning);
 //      issue the first slice of the next bucket's loads;
 //   D1. counting sort of the rows by their RB bits;
 //   D2. atomic-free pair enumeration (scan + max-scan, one lane per pair; depth-1 pruning);
 //   D3. destination histogram -> one atomicAdd per destination bucket claims this bucket's
 //       runs there; counting sort of the pairs by destination;
 //   D4. one-lane-per-row emit (XOR, shift one digit, 16-byte stores) into the claimed runs,
-//       plus the parent triples.
+//       plus the parent word(s).
+// Input rows whose slots carry compact parents keep the parent-bucket bits in their padding in
+// LDS (the prune check reads them); every comparison and the emit XOR mask them out (RMI).
 template <class C, int STAGE, bool STAMP>
-__global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ Rin, const uint64_t* __restrict__ Pin,
-                                                  const uint32_t* __restrict__ CTRin, uint32_t* __restrict__ Rout,
-                                                  uint64_t* __restrict__ Pout, uint32_t* __restrict__ CTRout,
-                                                  uint32_t* __restrict__ ncand, uint64_t* __restrict__ cand,
-                                                  uint64_t* __restrict__ stamps, uint32_t* __restrict__ pdrop,
-                                                  int nbk) {
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::WGCU * C::NT / 256)))
+void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTRin, uint32_t* __restrict__ Rout,
+              uint32_t* __restrict__ CTRout, uint32_t* __restrict__ ncand, uint64_t* __restrict__ cand,
+              uint64_t* __restrict__ stamps, uint32_t* __restrict__ pdrop, int nbk) {
     constexpr int WI = C::words(STAGE - 1);
     constexpr int WO = (STAGE < C::K) ? C::words(STAGE) : 1;
     constexpr int CAP = C::cap(STAGE);                        // LDS rows / pair-list entries
     constexpr bool FINAL = STAGE == C::K;
     constexpr bool PRUNE = round_prunes<C>(STAGE);
-    static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024, "round LDS budget");
+    static_assert(round_lds<C>(STAGE, PRUNE) <= C::LDS_BUDGET, "round LDS budget");
     constexpr int NT = C::NT;
-    constexpr int NV = (CAP * WI + 4 * NT - 1) / (4 * NT); // 16-byte prefetch vectors per lane
-    constexpr int RPL = (CAP + NT - 1) / NT;                // prefetched parent triples per lane
-    constexpr int SL = (NV + 2) / 3;                        // prefetch slice (vectors per phase)
-    constexpr int MP = FINAL ? 1 : (C::AREA + NT - 1) / NT; // pairs per lane (registers)
+    constexpr int RPL = (CAP + NT - 1) / NT;                // prefetched rows per lane
+    constexpr int MP = round_mp<C>(STAGE);                  // pairs per lane (registers)
     constexpr int MPR = (CAP + NT - 1) / NT;                 // LDS rows per lane (scans)
-    // Merged layout: a stage-s slot is its row followed by its parent triple (2 words); rows are
-    // prefetched one per lane (RPL per lane) and the parent words go straight to psig/pdw.
-    constexpr bool MG = BCP_EH_MERGED;
     constexpr int SWI = C::sw(STAGE - 1);                  // words per input slot
     constexpr int SWO = STAGE < C::K ? C::sw(STAGE) : 1;   // words per output slot
-    constexpr int NI = MG ? RPL : NV;                      // prefetch units per lane
-    constexpr int SLI = MG ? (RPL + BCP_EH_PF_SLICES - 1) / BCP_EH_PF_SLICES : SL; // prefetch slice (units per phase)
+    constexpr bool CPI = C::cp(STAGE - 1);                 // input slots carry one compact parent word
+    constexpr uint32_t RMI = C::rmask(STAGE - 1);          // parent bits in the input rows' padding
+    constexpr int SLI = (RPL + BCP_EH_PF_SLICES - 1) / BCP_EH_PF_SLICES; // prefetch slice (rows per phase)
+    constexpr int BPT = (C::NB + NT - 1) / NT;             // destination buckets per thread (claims)
+    using HT = std::conditional_t<C::H16, uint16_t, uint32_t>;
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
-    __shared__ uint32_t psig[PRUNE ? CAP : 1];                // merged: the parent's (j << 16) | i
-    __shared__ uint16_t pdw[PRUNE ? CAP : 1];                 // producing bucket of each row
-    __shared__ uint16_t pmark[FINAL ? 1 : MP * NT];           // pair index -> first sorted position
-    __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(CAP)];
-    __shared__ uint32_t hist[C::NB], cur[C::NB], base[C::NB];
+    __shared__ uint32_t psig[PRUNE ? CAP : 1];                // the input rows' parent word (j << 16 | i, + d bits)
+    __shared__ uint16_t pdw[PRUNE && !CPI ? CAP : 1];         // two-word parents: the producing bucket
+    __shared__ uint16_t pmark[FINAL || BCP_EH_PAIRS ? 2 : MP * NT]; // pair index -> first sorted position
+    __shared__ uint32_t npairs;                                // wave-compaction pair list fill
+    __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(STAGE)];
+    __shared__ uint32_t hist_[FINAL ? 1 : C::HW], cur_[FINAL ? 1 : C::HW]; // H16: two 16-bit counters per word
+    __shared__ HT base[FINAL ? 1 : C::NB];
     __shared__ uint32_t wsum[C::NW + 1];
     uint16_t* sidx = reinterpret_cast<uint16_t*>(un);
     uint32_t* bend = reinterpret_cast<uint32_t*>(un + un_walk_bend<C>(CAP));
     uint16_t* offp = reinterpret_cast<uint16_t*>(un + un_walk_offp<C>(CAP));
+    uint32_t* plist = reinterpret_cast<uint32_t*>(un + un_walk_offp<C>(CAP));
     uint32_t* spair = reinterpret_cast<uint32_t*>(un);
     const int tid = threadIdx.x;
     const int G = gridDim.x;
     int it = 0;
     int bk = xcd_bucket<C::NB>(blockIdx.x, 0, G, nbk);
     if (bk < 0) return; // uniform per workgroup
+
+    // histogram entry b (count or running position) and its returning increment
+    auto hget = [&](const uint32_t* h, int b) -> uint32_t {
+        if constexpr (C::H16) return reinterpret_cast<const uint16_t*>(h)[b];
+        else return h[b];
+    };
+    auto hinc = [&](uint32_t* h, uint32_t b) -> uint32_t {
+        if constexpr (C::H16) {
+            const uint32_t sh = (b & 1) * 16;
+            return (atomicAdd(&h[b >> 1], 1u << sh) >> sh) & 0xffffu;
+        } else {
+            return atomicAdd(&h[b], 1u);
+        }
+    };
+    // rows i and j share a parent (depth-1 duplicate): equal producing bucket and a common LDS row
+    auto shares_parent = [&](uint32_t i, uint32_t j) -> bool {
+        const uint32_t a = psig[i], b = psig[j];
+        const uint32_t ai = a & C::IMASK, bi = b & C::IMASK;
+        const bool hit = (ai & 0xffff) == (bi & 0xffff) || (ai & 0xffff) == (bi >> 16) ||
+                         (ai >> 16) == (bi & 0xffff) || (ai >> 16) == (bi >> 16);
+        if (!hit) return false;
+        if constexpr (CPI)
+            return ((a ^ b) & ~C::IMASK) == 0 && ((rows[i * WI + WI - 1] ^ rows[j * WI + WI - 1]) & RMI) == 0;
+        else
+            return pdw[i] == pdw[j];
+    };
 
     // A thread id the compiler cannot see through: keeps the per-lane index math of the
     // prefetch/commit loops from being hoisted out of the persistent loop (live invariants
@@ -622,69 +658,40 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         asm volatile("v_mov_b32 %0, %1" : "=v"(t) : "v"(tid));
         return t;
     };
-    u4v nx[MG ? 1 : NV];
-    uint64_t nf[PRUNE && !MG ? RPL : 1];
     // (a round that does not prune loads only the row words of each slot)
-    constexpr int LWI = MG ? (PRUNE ? SWI : (BCP_EH_ROWONLY_LOAD ? WI : SWI)) : 1;
-    uint32_t nr[MG ? RPL : 1][LWI];
+    constexpr int LWI = PRUNE ? (CPI ? WI + 1 : WI + 2) : (BCP_EH_ROWONLY_LOAD ? WI : SWI);
+    uint32_t nr[RPL][LWI];
     int pf_bk = bk;
     uint32_t pf_n = 0;
-    // Issue prefetch vectors [u0, u1) of bucket pf_bk (and its parent triples with the first slice).
-    // Every vector-memory instruction of the loop body is issued unconditionally (lanes with nothing
-    // to move use an out-of-range buffer offset, which the descriptor's range check drops), so the
-    // compiler can count the outstanding operations and wait for the prefetched words with a
-    // precise vmcnt(N) instead of vmcnt(0): a vmcnt(0) at the commit would wait for the acks of the
-    // previous bucket's emit stores as well.
+    // Issue prefetch rows [u0, u1) of bucket pf_bk. Every vector-memory instruction of the loop
+    // body is issued unconditionally (lanes with nothing to move use an out-of-range buffer offset,
+    // which the descriptor's range check drops), so the compiler can count the outstanding
+    // operations and wait for the prefetched words with a precise vmcnt(N) instead of vmcnt(0): a
+    // vmcnt(0) at the commit would wait for the acks of the previous bucket's emit stores as well.
     auto issue = [&](int u0, int u1) {
-        const int nonce = pf_bk / C::NB, d = pf_bk % C::NB;
-        if constexpr (MG) {
-            const auto rs = buf_rsrc(Rin + ((size_t)nonce * C::ROWS + (size_t)d * C::AREA) * SWI, CAP * SWI * 4);
-            const uint32_t ot = opaque_tid();
-#pragma unroll
-            for (int u = 0; u < RPL; ++u) {
-                if (u < u0 || u >= u1) continue;
-                const uint32_t r = ot + u * NT;
-                row_load<LWI>(rs, r < pf_n ? r * (SWI * 4) : OOB, nr[u]);
-            }
-        } else {
-        const auto rs = buf_rsrc(Rin + (size_t)nonce * C::ROWS * C::WMAX + (size_t)d * C::AREA * WI, CAP * WI * 4);
+        const int nonce = pf_bk / C::NB, d = BCP_EH_EXP_LOAD ? pf_bk % 8 : pf_bk % C::NB;
+        const auto rs = buf_rsrc(Rin + ((size_t)nonce * C::ROWS + (size_t)d * C::AREA) * SWI, CAP * SWI * 4);
         const uint32_t ot = opaque_tid();
-        const uint32_t lim = pf_n * WI;
 #pragma unroll
-        for (int u = 0; u < NV; ++u) {
+        for (int u = 0; u < RPL; ++u) {
             if (u < u0 || u >= u1) continue;
-            const uint32_t k = 4 * (ot + u * NT);
-            nx[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, k < lim ? k * 4 : OOB, 0, 0);
-        }
-        if constexpr (PRUNE) {
-            if (u0 == 0) {
-                const auto rp = buf_rsrc(Pin + (size_t)nonce * C::ROWS + (size_t)d * C::AREA, CAP * 8);
-#pragma unroll
-                for (int u = 0; u < RPL; ++u) {
-                    const uint32_t r = ot + u * NT;
-                    const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rp, r < pf_n ? r * 8 : OOB, 0, 0);
-                    nf[u] = ((uint64_t)x.y << 32) | x.x;
-                }
-            }
-        }
+            const uint32_t r = ot + u * NT;
+            row_load<LWI>(rs, r < pf_n ? r * (SWI * 4) : OOB, nr[u]);
         }
     };
 
     // prologue: first bucket in flight, fill of the second known
     uint32_t n = min(CTRin[bk], (uint32_t)CAP);
     pf_n = n;
-    issue(0, NI);
+    issue(0, RPL);
     if constexpr (!FINAL) {
         // As many (dropped) stores as one emit issues: the compiler's wait counts at the loop head
         // take the minimum over the entry and back edges; with these, both edges see the prefetch
         // loads followed by MP emit store groups, so the commit waits for its loads only.
-        const auto rs_out = buf_rsrc(Rout, 0), rs_par = buf_rsrc(Pout, 0);
+        const auto rs_out = buf_rsrc(Rout, 0);
         const uint32_t z[SWO] = {};
 #pragma unroll
-        for (int u = 0; u < MP; ++u) { // distinct offsets: identical stores would be merged
-            row_store<SWO>(rs_out, OOB + 256 * u, z);
-            if constexpr (!MG) __builtin_amdgcn_raw_buffer_store_b64(u2v{0u, 0u}, rs_par, OOB + 256 * u, 0, 0);
-        }
+        for (int u = 0; u < MP; ++u) row_store<SWO>(rs_out, OOB + 256 * u, z); // distinct offsets: identical stores would be merged
     }
     const int bk1 = xcd_bucket<C::NB>(blockIdx.x, 1, G, nbk);
     uint32_t fill_next = bk1 >= 0 ? CTRin[bk1] : 0u;
@@ -692,18 +699,13 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
     for (;;) {
         const int nonce = bk / C::NB, d = bk % C::NB;
         EH_STAMP(0);
-        // A. commit the prefetched bucket (lane-flat 16-byte LDS stores: conflict-free)
-        if constexpr (MG) {
+        // A. commit the prefetched bucket (one row per lane per unit)
+        {
             const uint32_t ot = opaque_tid();
 #pragma unroll
             for (int u = 0; u < RPL; ++u) {
                 const uint32_t r = ot + u * NT;
                 if (r < n) {
-                    uint32_t lbits = 0;
-                    if constexpr (C::cp(STAGE - 1)) { // d's top bits out of the row's padding
-                        lbits = nr[u][WI - 1];
-                        nr[u][WI - 1] &= ~7u;
-                    }
                     if constexpr (WI % 2 == 0) {
 #pragma unroll
                         for (int w = 0; w < WI; w += 2)
@@ -713,46 +715,27 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                         for (int w = 0; w < WI; ++w) rows[r * WI + w] = nr[u][w];
                     }
                     if constexpr (PRUNE) {
-                        if constexpr (C::cp(STAGE - 1)) {
-                            psig[r] = nr[u][WI] & 0x1fff1fffu;
-                            pdw[r] = (uint16_t)cunpack_d(nr[u][WI], lbits);
-                        } else {
-                            psig[r] = nr[u][WI];
-                            pdw[r] = (uint16_t)nr[u][WI + 1];
-                        }
-                    }
-                }
-            }
-        } else {
-            const uint32_t ot = opaque_tid();
-            const uint32_t lim = n * WI;
-#pragma unroll
-            for (int u = 0; u < NV; ++u) {
-                const uint32_t k = 4 * (ot + u * NT);
-                if (k < lim) *reinterpret_cast<u4v*>(&rows[k]) = nx[u];
-            }
-            if constexpr (PRUNE) {
-#pragma unroll
-                for (int u = 0; u < RPL; ++u) {
-                    const uint32_t r = ot + u * NT;
-                    if (r < n) {
-                        psig[r] = parent_sig(nf[u]);
-                        pdw[r] = (uint16_t)(nf[u] >> 32);
+                        psig[r] = nr[u][WI];
+                        if constexpr (!CPI) pdw[r] = (uint16_t)nr[u][WI + 1];
                     }
                 }
             }
         }
-        for (int b = tid; b < C::NB; b += NT) hist[b] = 0;
+        if constexpr (!FINAL)
+            for (int b = tid; b < C::HW; b += NT) hist_[b] = 0;
         for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
+        if (tid == 0) npairs = 0;
         EH_STAMP(1);
         const int bn = xcd_bucket<C::NB>(blockIdx.x, it + 1, G, nbk);
         const bool more = bn >= 0; // uniform
         const uint32_t nn = more ? min(fill_next, (uint32_t)CAP) : 0u;
         pf_bk = more ? bn : bk;
         pf_n = nn;
-        issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
         const int bn2 = xcd_bucket<C::NB>(blockIdx.x, it + 2, G, nbk);
+#if !BCP_EH_ISSUE_LATE
+        issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
         fill_next = bn2 >= 0 ? CTRin[bn2] : 0u;
+#endif
         __syncthreads();
         EH_STAMP(2);
 
@@ -763,7 +746,14 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
         __syncthreads();
         block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
         for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
+#if BCP_EH_ISSUE_LATE
+        // the first vector-memory instructions after the previous bucket's emit: issued once the
+        // key sort (LDS only) has given that emit's stores time to drain, so they do not stall
+        fill_next = bn2 >= 0 ? CTRin[bn2] : 0u;
+        issue(0, 2 * SLI);
+#else
         issue(SLI, 2 * SLI);
+#endif
         __syncthreads();
         EH_STAMP(3);
 
@@ -776,16 +766,58 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                 const uint32_t i = sidx[p], ri = rows[i], e = bend[ri >> (32 - C::RB)];
                 for (uint32_t q = p + 1; q < e; ++q) {
                     const uint32_t j = sidx[q];
-                    if (rows[j] != ri) continue;
+                    if ((rows[j] ^ ri) & ~RMI) continue;
                     if constexpr (PRUNE) {
-                        if (sig_hit(psig[i], psig[j]) && pdw[i] == pdw[j]) continue;
+                        if (shares_parent(i, j)) continue;
                     }
                     const uint32_t c = atomicAdd(&ncand[nonce], 1u);
                     if (c < (uint32_t)C::MAXCAND) cand[(size_t)nonce * C::MAXCAND + c] = pack_tri(d, i, j);
                 }
             }
-            issue(2 * SLI, NI);
+            issue(2 * SLI, RPL);
         } else {
+#if BCP_EH_PAIRS
+            // D2. pair list by per-wave compaction. Sorted position p pairs with every later
+            //     position of its key group: c_p = bend[key] - p - 1 pairs (capped at 14; a group
+            //     of 16+ rows is ~1e-8 likely). Each lane counts the pairs of its positions, a DPP
+            //     wave scan gives the lane's offset inside its wave, ONE LDS atomic per wave claims
+            //     the wave's block of the list, and the lane writes its (j << 16 | i) pairs there:
+            //     one barrier. The list holds MP*NT pairs (above the row capacity: capped pair
+            //     lists lost ~9% of the solutions); identical subtrees and pairs that share a
+            //     parent are dropped when the pairs are read back.
+            uint32_t cpl[MPR];
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int u = 0; u < MPR; ++u) {
+                const uint32_t p = tid + u * NT;
+                cpl[u] = p < n ? min(bend[key_of(sidx[p])] - p - 1, 14u) : 0u;
+                cnt += cpl[u];
+            }
+            const uint32_t incl = wave_incl<false>(cnt);
+            uint32_t wb = 0;
+            if ((tid & 63) == 63) wb = atomicAdd(&npairs, incl);
+            uint32_t o = __builtin_amdgcn_readlane(wb, 63) + incl - cnt;
+#pragma unroll
+            for (int u = 0; u < MPR; ++u) {
+                if (!cpl[u]) continue;
+                const uint32_t p = tid + u * NT, i = sidx[p];
+                for (uint32_t q = p + 1; q <= p + cpl[u]; ++q, ++o)
+                    if (o < (uint32_t)(MP * NT)) plist[o] = ((uint32_t)sidx[q] << 16) | i;
+            }
+            __syncthreads();
+            const uint32_t P = npairs;
+            const uint32_t Pc = min(P, (uint32_t)(MP * NT));
+            if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT); // rare
+            uint32_t pv[MP], pd[MP];
+#pragma unroll
+            for (int u = 0; u < MP; ++u) {
+                const uint32_t k = tid + u * NT;
+                pv[u] = NIL;
+                pd[u] = 0;
+                if (k < Pc) {
+                    const uint32_t pr = plist[k];
+                    const uint32_t i = pr & 0xffff, j = pr >> 16;
+#else
             // D2. atomic-free pair enumeration. Sorted position p pairs with every later position
             //     of its group: c_p = bend[key] - p - 1 pairs, first pair index offp[p] (exclusive
             //     scan). A mark p at each group's first pair index, spread by an inclusive
@@ -816,23 +848,27 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
                 if (k < Pc) {
                     const uint32_t p = pmark[k], q = p + 1 + (k - offp[p]);
                     const uint32_t i = sidx[p], j = sidx[q];
-                    const uint32_t x0 = rows[i * WI] ^ rows[j * WI];
+#endif
+                    uint32_t x0 = rows[i * WI] ^ rows[j * WI];
+                    if constexpr (WI == 1) x0 &= ~RMI;
                     // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the
                     // pairs, so the remaining words are read only when it matches
                     bool keep = x0 != 0;
                     if (!keep) {
 #pragma unroll
-                        for (int w = 1; w < WI; ++w) keep |= rows[i * WI + w] != rows[j * WI + w];
+                        for (int w = 1; w < WI; ++w) {
+                            uint32_t y = rows[i * WI + w] ^ rows[j * WI + w];
+                            if (w == WI - 1) y &= ~RMI;
+                            keep |= y != 0;
+                        }
                     }
                     if constexpr (PRUNE) {
-                        // signature hit (a shared parent, or ~1e-4 by chance): parents are
-                        // shared only if both rows were made by the same bucket
-                        if (keep && sig_hit(psig[i], psig[j]) && pdw[i] == pdw[j]) keep = false;
+                        if (keep && shares_parent(i, j)) keep = false;
                     }
                     if (keep) {
                         pv[u] = (j << 16) | i;
                         pd[u] = (x0 >> (32 - C::DB)) & (C::NB - 1); // destination bucket
-                        atomicAdd(&hist[pd[u]], 1u);
+                        hinc(hist_, pd[u]);
                     }
                 }
             }
@@ -840,58 +876,81 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
             EH_STAMP(4);
             // D3. claim this bucket's runs in the destination areas (device-scope atomics whose
             //     latency hides behind the scan and the scatter), then sort the pairs by
-            //     destination: each pair takes the next LDS slot of its destination's run
-            uint32_t myb = 0;
-            if (tid < C::NB) myb = atomicAdd(&CTRout[(size_t)nonce * C::NB + tid], hist[tid]); // wave-uniform branch
-            issue(2 * SLI, NI); // after the claim: waiting for its return then skips these loads
-            uint32_t start = 0; // thread b < NB: first LDS slot of destination b (NB <= NT: one entry each)
-            const uint32_t np = block_exscan<NT>(hist, cur, C::NB, wsum, &start);
+            //     destination: each pair takes the next LDS slot of its destination's run.
+            //     Thread t owns destinations [t*BPT, t*BPT + BPT) (the scan's entry split).
+            uint32_t myb[BPT];
+#pragma unroll
+            for (int k = 0; k < BPT; ++k) {
+                const int b = tid * BPT + k;
+                myb[k] = 0;
+                if (b < C::NB) myb[k] = atomicAdd(&CTRout[(size_t)nonce * C::NB + b], hget(hist_, b)); // wave-uniform branch
+            }
+            issue(2 * SLI, RPL); // after the claim: waiting for its return then skips these loads
+            uint32_t start = 0; // first LDS slot of the thread's first destination
+            uint32_t np;
+            if constexpr (C::H16)
+                np = block_exscan<NT, BPT, uint16_t, uint16_t>(reinterpret_cast<const uint16_t*>(hist_),
+                                                               reinterpret_cast<uint16_t*>(cur_), C::NB, wsum, &start);
+            else
+                np = block_exscan<NT, BPT>(hist_, cur_, C::NB, wsum, &start);
 #pragma unroll
             for (int u = 0; u < MP; ++u)
-                if (pv[u] != NIL) spair[atomicAdd(&cur[pd[u]], 1u)] = pv[u];
-            if (tid < C::NB) base[tid] = myb - start; // LDS slot t of destination b -> run position base[b] + t
+                if (pv[u] != NIL) spair[hinc(cur_, pd[u])] = pv[u];
+#pragma unroll
+            for (int k = 0; k < BPT; ++k) { // LDS slot t of destination b -> run position base[b] + t
+                const int b = tid * BPT + k;
+                if (b < C::NB) {
+                    base[b] = (HT)(myb[k] - start);
+                    start += hget(hist_, b);
+                }
+            }
             __syncthreads();
             EH_STAMP(5);
             // D4. emit, one lane per output row in destination order: XOR, shift one digit,
             //     store into the claimed run (rows past the next round's capacity are dropped)
             constexpr uint32_t OCAP = C::cap(STAGE + 1 <= C::K ? STAGE + 1 : C::K);
-            const auto rs_out = MG ? buf_rsrc(Rout + (size_t)nonce * C::ROWS * SWO, (uint32_t)(C::ROWS * SWO * 4))
-                                   : buf_rsrc(Rout + (size_t)nonce * C::ROWS * C::WMAX, (uint32_t)(C::ROWS * WO * 4));
-            const auto rs_par = buf_rsrc(Pout + (size_t)nonce * C::ROWS, (uint32_t)(C::ROWS * 8));
+            constexpr uint32_t RMO = C::rmask(STAGE);
+            const auto rs_out = buf_rsrc(Rout + (size_t)nonce * C::ROWS * SWO, (uint32_t)(C::ROWS * SWO * 4));
 #pragma unroll
             for (int u = 0; u < MP; ++u) { // fixed trip count, unconditional stores (see issue())
+#if BCP_EH_EXP_STORE == 5 // experiment: the lanes of a wave take output rows MP*NT/64 apart (scattered stores)
+                const uint32_t t0 = tid + u * NT, t = (t0 % (MP * NT / 64)) * 64 + t0 / (MP * NT / 64);
+#else
                 const uint32_t t = tid + u * NT;
+#endif
                 const uint32_t pr = t < np ? spair[t] : 0u;
                 const uint32_t i = pr & 0xffff, j = pr >> 16;
                 uint32_t x[WI + 1], o[WO];
                 lds_row_xor<WI>(rows, i, j, x);
+                x[WI - 1] &= ~RMI;
                 x[WI] = 0;
                 const uint32_t b = (x[0] >> (32 - C::DB)) & (C::NB - 1);
-                const uint32_t pos = base[b] + t;
+                const uint32_t pos = (HT)(base[b] + t);
                 const bool ok = t < np && pos < OCAP;
                 const uint32_t slot = b * C::AREA + pos;
 #pragma unroll
                 for (int w = 0; w < WO; ++w) o[w] = (x[w] << C::DB) | (x[w + 1] >> (32 - C::DB));
-                const uint64_t tri = pack_tri(d, i, j);
-                if constexpr (MG) {
-                    uint32_t ov[SWO] = {};
+                uint32_t ov[SWO] = {};
 #pragma unroll
-                    for (int w = 0; w < WO; ++w) ov[w] = o[w];
-                    if constexpr (C::cp(STAGE)) {
-                        ov[WO - 1] |= (d >> 6) & 7;
-                        ov[WO] = cpack(d, i, j);
-                    } else {
-                        ov[WO] = (uint32_t)tri;
-                        ov[WO + 1] = (uint32_t)(tri >> 32);
-                    }
-                    row_store<SWO>(rs_out, ok ? slot * (SWO * 4) : OOB, ov);
+                for (int w = 0; w < WO; ++w) ov[w] = o[w];
+                if constexpr (C::cp(STAGE)) {
+                    ov[WO - 1] |= (d >> C::DX) & RMO;
+                    ov[WO] = cpack<C>(d, i, j);
                 } else {
-                    row_store<WO>(rs_out, ok ? slot * (WO * 4) : OOB, o);
-                    const u2v tv = {(uint32_t)tri, (uint32_t)(tri >> 32)};
-#if !BCP_EH_EXP_NOPARENT
-                    __builtin_amdgcn_raw_buffer_store_b64(tv, rs_par, ok ? slot * 8 : OOB, 0, 0);
-#endif
+                    ov[WO] = (j << 16) | i;
+                    ov[WO + 1] = d;
                 }
+#if BCP_EH_EXP_STORE == 1 // timing experiment: no emit stores
+                row_store<SWO>(rs_out, OOB, ov);
+#elif BCP_EH_EXP_STORE == 2 // timing experiment: emit rows in LDS order to the producer's own area
+                row_store<SWO>(rs_out, t < OCAP ? (d * C::AREA + t) * (SWO * 4) : OOB, ov);
+#elif BCP_EH_EXP_STORE == 4 // timing experiment: same bytes as dword stores, lane-contiguous
+#pragma unroll
+                for (int w = 0; w < SWO; ++w)
+                    __builtin_amdgcn_raw_buffer_store_b32(ov[w], rs_out, t < OCAP ? ((d * C::AREA + u * NT) * SWO + w * NT + tid) * 4 : OOB, 0, 0);
+#else
+                row_store<SWO>(rs_out, ok ? slot * (SWO * 4) : OOB, ov);
+#endif
             }
         }
         __syncthreads();
@@ -905,16 +964,15 @@ __global__ __launch_bounds__(C::NT) void eh_round(const uint32_t* __restrict__ R
 
 
 // ------------------------------------------------------------------ tree expansion
-// Merged layout: the stage arrays (stage s slot = row, parent triple) passed by value.
+// The stage arrays (stage-s slot = row, parent word(s)) passed by value; LEAF: stage-0 leaf
+// index per slot.
 struct EhStages {
     const uint32_t* r[16];
 };
-// LEAF: stage-0 leaf index per slot; P: K-1 arrays of stage-1..K-1 parent triples.
 template <class C>
-__global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_t* __restrict__ LEAF,
-                                                                  const uint64_t* __restrict__ P, EhStages st,
+__global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_t* __restrict__ LEAF, EhStages st,
                                                                   const uint32_t* __restrict__ ncand,
-                                                                  const uint64_t* __restrict__ cand, int batch,
+                                                                  const uint64_t* __restrict__ cand,
                                                                   uint32_t* __restrict__ out_idx,
                                                                   uint32_t* __restrict__ out_valid,
                                                                   uint32_t* __restrict__ nout,
@@ -933,7 +991,9 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
         dup = 0;
     }
     int cur = 0;
-    // level s: 2^(K-s) triples of round s -> 2^(K-s+1) stage-(s-1) slots -> their triples
+    // level s: 2^(K-s) triples of round s -> 2^(K-s+1) stage-(s-1) slots -> their triples. A
+    // parent outside the slot arrays (never produced by a correct round) is clamped to slot 0
+    // and the candidate is rejected, so no corrupt word can address past the stage arrays.
     for (int s = C::K; s >= 1; --s) {
         __syncthreads();
         const uint32_t cnt = 1u << (C::K - s);
@@ -941,28 +1001,21 @@ __global__ __launch_bounds__(C::L < 64 ? 64 : C::L) void eh_expand(const uint32_
             const uint64_t tr = tri[t >> 1];
             const uint32_t dd = (uint32_t)(tr >> 32);
             const uint32_t r = (t & 1) ? (((uint32_t)tr >> 16) & 0xffff) : ((uint32_t)tr & 0xffff);
-            buf[cur][t] = dd * C::AREA + r;
+            const bool in = dd < (uint32_t)C::NB && r < (uint32_t)C::AREA;
+            if (!in) dup = 1;
+            buf[cur][t] = in ? dd * C::AREA + r : 0u;
         }
         __syncthreads();
-        if (s > 1 && t < 2 * cnt) {
-            if constexpr (BCP_EH_MERGED) { // stage s-1 slot: row words, then the parent triple
-                const uint32_t* q = st.r[s - 1] + ((size_t)nonce * C::ROWS + buf[cur][t]) * C::sw(s - 1) + C::words(s - 1);
-                if (C::cp(s - 1))
-                    tri[t] = ((uint64_t)cunpack_d(q[0], q[-1]) << 32) | (q[0] & 0x1fff1fffu);
-                else
-                    tri[t] = ((uint64_t)q[1] << 32) | q[0];
-            } else {
-                tri[t] = P[(size_t)(s - 2) * batch * C::ROWS + (size_t)nonce * C::ROWS + buf[cur][t]];
-            }
+        if (s > 1 && t < 2 * cnt) { // stage s-1 slot: row words, then the parent word(s)
+            const uint32_t* q = st.r[s - 1] + ((size_t)nonce * C::ROWS + buf[cur][t]) * C::sw(s - 1) + C::words(s - 1);
+            if (C::cp(s - 1))
+                tri[t] = ((uint64_t)cunpack_d<C>(q[0], q[-1]) << 32) | (q[0] & C::IMASK);
+            else
+                tri[t] = ((uint64_t)q[1] << 32) | q[0];
         }
     }
     __syncthreads();
-    if (t < (uint32_t)L) {
-        if constexpr (C::LEAFSLOT)
-            buf[cur][t] = st.r[0][((size_t)nonce * C::ROWS + buf[cur][t]) * C::sw(0) + C::words(0)];
-        else
-            buf[cur][t] = LEAF[(size_t)nonce * C::ROWS + buf[cur][t]];
-    }
+    if (t < (uint32_t)L) buf[cur][t] = LEAF[(size_t)nonce * C::ROWS + buf[cur][t]];
     // Canonical order: at each level the subtree with the smaller first index goes left.
     for (int l = 0; l < C::K; ++l) {
         __syncthreads();
@@ -1051,8 +1104,8 @@ struct EquihashGpuSolver::Impl {
     hipStream_t stream = nullptr;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     DevBuf<bcpk::EhBaseState> d_states;
-    DevBuf<uint32_t> d_rows[2], d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
-    DevBuf<uint64_t> d_par, d_cand;
+    DevBuf<uint32_t> d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
+    DevBuf<uint64_t> d_cand;
     DevBuf<uint32_t> d_rst[16]; // merged layout: stage-s slot arrays (s = 0..K-1)
     HostBuf<bcpk::EhBaseState> h_states;
     HostBuf<uint32_t> h_ncand, h_idx, h_ctr0, h_pdrop, h_nout, h_out;
@@ -1060,7 +1113,7 @@ struct EquihashGpuSolver::Impl {
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
     std::vector<size_t> slot_words, row_words; // per stage
-    size_t leaf_slot_words = 0;
+    uint32_t cp_ib = 0, cp_dh = 0, cp_dhm = 0, cp_dx = 0, cp_rmask = 0, cp_imask = 0; // compact parent layout
     std::vector<bool> compact;                  // per stage: compact parent word                 // > 0: stage-0 slots carry the leaf index last
     int inflight = 0;
     int ncu = 1;
@@ -1088,15 +1141,10 @@ struct EquihashGpuSolver::Impl {
         d_states.alloc(batch);
         h_states.alloc(batch);
         static_assert(C::K <= 16, "stage arrays");
-        if (BCP_EH_MERGED) {
-            for (int s = 0; s < C::K; ++s) d_rst[s].alloc((size_t)batch * C::ROWS * C::sw(s));
-        } else {
-            for (int p = 0; p < 2; ++p) d_rows[p].alloc((size_t)batch * C::ROWS * C::WMAX);
-        }
+        for (int s = 0; s < C::K; ++s) d_rst[s].alloc((size_t)batch * C::ROWS * C::sw(s));
         d_ctr.alloc((size_t)C::K * batch * C::NB);
-        if (!C::LEAFSLOT) d_leaf.alloc((size_t)batch * C::ROWS);
-        leaf_slot_words = C::LEAFSLOT ? C::sw(0) : 0;
-        if (!BCP_EH_MERGED) d_par.alloc((size_t)(C::K - 1) * batch * C::ROWS);
+        d_leaf.alloc((size_t)batch * C::ROWS);
+        cp_ib = C::IB, cp_dh = C::DH, cp_dhm = C::DHM, cp_dx = C::DX, cp_rmask = C::RMASK, cp_imask = C::IMASK;
         d_ncand.alloc(batch);
         d_pdrop.alloc(C::K + 1);
         h_pdrop.alloc(C::K + 1);
@@ -1112,7 +1160,7 @@ struct EquihashGpuSolver::Impl {
         h_idx.alloc((size_t)C::MAXCAND * C::L);
         h_ctr0.alloc((size_t)C::K * C::NB);
         d_stamps.alloc((size_t)C::K * batch * C::NB * 16);
-        bytes = 2 * d_rows[0].n * 4 + d_par.n * 8 + d_leaf.n * 4 + d_ctr.n * 4 + d_idx.n * 4;
+        bytes = d_leaf.n * 4 + d_ctr.n * 4 + d_idx.n * 4;
         for (int s = 0; s < C::K; ++s) bytes += d_rst[s].n * 4;
     }
 
@@ -1127,21 +1175,18 @@ struct EquihashGpuSolver::Impl {
         return std::min(nbk, ncu * per_cu);
     }
     template <class C, int S> void launch_round(int nstates) {
-        const uint32_t* rin = BCP_EH_MERGED ? d_rst[S - 1].p : d_rows[(S - 1) & 1].p;
-        uint32_t* rout = BCP_EH_MERGED ? (S < C::K ? d_rst[S].p : nullptr) : d_rows[S & 1].p;
-        const uint64_t* pin = !BCP_EH_MERGED && S >= 2 ? d_par.p + (size_t)(S - 2) * batch * C::ROWS : nullptr;
-        uint64_t* pout = !BCP_EH_MERGED && S < C::K ? d_par.p + (size_t)(S - 1) * batch * C::ROWS : nullptr;
+        const uint32_t* rin = d_rst[S - 1].p;
+        uint32_t* rout = S < C::K ? d_rst[S].p : nullptr;
         const uint32_t* cin = d_ctr.p + (size_t)(S - 1) * batch * C::NB;
         uint32_t* cout = S < C::K ? d_ctr.p + (size_t)S * batch * C::NB : nullptr;
         const int nbk = C::NB * nstates;
         if (stamp_mode) {
             uint64_t* st = d_stamps.p + (size_t)(S - 1) * batch * C::NB * 16;
             hipLaunchKernelGGL((bcpk::eh_round<C, S, true>), dim3(round_grid<C, S, true>(nbk)), dim3(C::NT), 0,
-                               stream, rin, pin, cin, rout, pout, cout, d_ncand.p, d_cand.p, st, d_pdrop.p, nbk);
+                               stream, rin, cin, rout, cout, d_ncand.p, d_cand.p, st, d_pdrop.p, nbk);
         } else {
             hipLaunchKernelGGL((bcpk::eh_round<C, S, false>), dim3(round_grid<C, S, false>(nbk)), dim3(C::NT), 0,
-                               stream, rin, pin, cin, rout, pout, cout, d_ncand.p, d_cand.p, nullptr, d_pdrop.p,
-                               nbk);
+                               stream, rin, cin, rout, cout, d_ncand.p, d_cand.p, nullptr, d_pdrop.p, nbk);
         }
     }
     template <class C, int... S> void launch_rounds(int nstates, std::integer_sequence<int, S...>) {
@@ -1157,7 +1202,6 @@ struct EquihashGpuSolver::Impl {
         BCP_HIP_CHECK(hipMemsetAsync(d_ctr.p, 0, d_ctr.n * sizeof(uint32_t), stream));
         if (debug) {
             if (d_leaf.n) BCP_HIP_CHECK(hipMemsetAsync(d_leaf.p, 0xff, d_leaf.n * sizeof(uint32_t), stream));
-            if (d_par.n) BCP_HIP_CHECK(hipMemsetAsync(d_par.p, 0xff, d_par.n * sizeof(uint64_t), stream));
             for (int s = 0; s < C::K; ++s)
                 if (d_rst[s].n) BCP_HIP_CHECK(hipMemsetAsync(d_rst[s].p, 0xff, d_rst[s].n * sizeof(uint32_t), stream));
         }
@@ -1170,18 +1214,18 @@ struct EquihashGpuSolver::Impl {
             hdr &= st.g_byte == 12;
             for (int w = 2; w < 16; ++w) hdr &= st.m[w] == 0;
         }
-        uint32_t* r0 = BCP_EH_MERGED ? d_rst[0].p : d_rows[0].p;
-        constexpr bool reg = BCP_EH_GEN_NTG > 0 && bcpk::GenReg<C, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>::OK;
+        uint32_t* r0 = d_rst[0].p;
+        constexpr bool reg = bcpk::GenReg<C, C::GNT, C::GHPT>::OK;
         if constexpr (reg) {
-            using GR = bcpk::GenReg<C, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>;
+            using GR = bcpk::GenReg<C, C::GNT, C::GHPT>;
+            const int items = GR::GWG * (int)nstates;
+            const int grid = BCP_EH_GEN_PERSIST > 0 ? std::min(items, ncu * BCP_EH_GEN_PERSIST) : items;
             if (hdr)
-                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, true, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>),
-                                   dim3(GR::GWG * nstates), dim3(BCP_EH_GEN_NTG), 0, stream, d_states.p,
-                                   r0, d_leaf.p, d_ctr.p);
+                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, true, C::GNT, C::GHPT>), dim3(grid), dim3(C::GNT), 0, stream,
+                                   d_states.p, r0, d_leaf.p, d_ctr.p, items);
             else
-                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, false, BCP_EH_GEN_NTG, BCP_EH_GEN_HPT>),
-                                   dim3(GR::GWG * nstates), dim3(BCP_EH_GEN_NTG), 0, stream, d_states.p,
-                                   r0, d_leaf.p, d_ctr.p);
+                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, false, C::GNT, C::GHPT>), dim3(grid), dim3(C::GNT), 0, stream,
+                                   d_states.p, r0, d_leaf.p, d_ctr.p, items);
         } else if (hdr)
             hipLaunchKernelGGL((bcpk::eh_gen<C, true>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
                                d_states.p, r0, d_leaf.p, d_ctr.p);
@@ -1192,9 +1236,8 @@ struct EquihashGpuSolver::Impl {
         constexpr int EB = C::L < 64 ? 64 : C::L;
         bcpk::EhStages stages{};
         for (int s = 0; s < C::K; ++s) stages.r[s] = d_rst[s].p;
-        if (!BCP_EH_EXP_NOPARENT) // timing experiment builds store no parents: nothing to expand
-        hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND * nstates), dim3(EB), 0, stream, d_leaf.p,
-                           d_par.p, stages, d_ncand.p, d_cand.p, batch, d_idx.p, d_valid.p, d_nout.p, d_out.p);
+        hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND * nstates), dim3(EB), 0, stream, d_leaf.p, stages,
+                           d_ncand.p, d_cand.p, d_idx.p, d_valid.p, d_nout.p, d_out.p);
         BCP_HIP_CHECK(hipGetLastError());
         BCP_HIP_CHECK(hipEventRecord(ev1, stream));
         BCP_HIP_CHECK(
@@ -1285,35 +1328,30 @@ void EquihashGpuSolver::ResetStats() { impl->stats = EhGpuStats(); }
 std::vector<uint64_t> EquihashGpuSolver::DebugDump() {
     BCP_HIP_CHECK(hipSetDevice(impl->device));
     BCP_HIP_CHECK(hipStreamSynchronize(impl->stream));
-    const size_t R = impl->rows, K = impl->kstages, B = impl->batch;
+    const Impl& m = *impl;
+    const size_t R = m.rows, K = m.kstages;
     std::vector<uint64_t> out(K * R);
     std::vector<uint32_t> leaf(R);
-    if (impl->leaf_slot_words) {
-        const size_t sw = impl->leaf_slot_words;
-        std::vector<uint32_t> buf(R * sw);
-        BCP_HIP_CHECK(hipMemcpy(buf.data(), impl->d_rst[0].p, R * sw * 4, hipMemcpyDeviceToHost));
-        for (size_t i = 0; i < R; ++i) leaf[i] = buf[i * sw + impl->row_words[0]];
-    } else {
-        BCP_HIP_CHECK(hipMemcpy(leaf.data(), impl->d_leaf.p, R * 4, hipMemcpyDeviceToHost));
-    }
+    BCP_HIP_CHECK(hipMemcpy(leaf.data(), m.d_leaf.p, R * 4, hipMemcpyDeviceToHost));
     for (size_t i = 0; i < R; ++i) out[i] = leaf[i];
-    for (size_t s = 1; s < K; ++s)
-        if (impl->d_par.n) {
-            BCP_HIP_CHECK(hipMemcpy(out.data() + s * R, impl->d_par.p + (s - 1) * B * R, R * 8, hipMemcpyDeviceToHost));
-        } else { // merged layout: the triple follows the row in every stage-s slot of nonce 0
-            const size_t sw = impl->slot_words[s], w = impl->row_words[s];
-            std::vector<uint32_t> buf(R * sw);
-            BCP_HIP_CHECK(hipMemcpy(buf.data(), impl->d_rst[s].p, R * sw * 4, hipMemcpyDeviceToHost));
-            for (size_t i = 0; i < R; ++i) {
-                const uint32_t* q = &buf[i * sw + w];
-                if (impl->compact[s] && q[0] == 0xffffffffu) // never written (SetDebug fill): no row index is 0x1fff
-                    out[s * R + i] = ~0ull;
-                else
-                    out[s * R + i] = impl->compact[s]
-                                         ? ((uint64_t)bcpk::cunpack_d_host(q[0], q[-1]) << 32) | (q[0] & 0x1fff1fffu)
-                                         : ((uint64_t)q[1] << 32) | q[0];
-            }
+    // the parent word(s) follow the row in every stage-s slot of nonce 0 (bcpk::cpack layout)
+    auto cunpack_d = [&](uint32_t pw, uint32_t last) {
+        return ((pw >> m.cp_ib) & m.cp_dhm) | (((pw >> (16 + m.cp_ib)) & m.cp_dhm) << m.cp_dh) |
+               ((last & m.cp_rmask) << m.cp_dx);
+    };
+    for (size_t s = 1; s < K; ++s) {
+        const size_t sw = m.slot_words[s], w = m.row_words[s];
+        std::vector<uint32_t> buf(R * sw);
+        BCP_HIP_CHECK(hipMemcpy(buf.data(), m.d_rst[s].p, R * sw * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < R; ++i) {
+            const uint32_t* q = &buf[i * sw + w];
+            if (m.compact[s] && q[0] == 0xffffffffu) // never written (SetDebug fill): no LDS row index is all-ones
+                out[s * R + i] = ~0ull;
+            else
+                out[s * R + i] = m.compact[s] ? ((uint64_t)cunpack_d(q[0], q[-1]) << 32) | (q[0] & m.cp_imask)
+                                              : ((uint64_t)q[1] << 32) | q[0];
         }
+    }
     return out;
 }
 size_t EquihashGpuSolver::DeviceBytes() const { return impl->bytes; }

@@ -602,7 +602,7 @@ CTxDestination DecodeCashAddr(const std::string& str, const CChainParams& params
     }
 }
 
-static std::atomic<bool> g_use_cashaddr{true};
+static std::atomic<bool> g_use_cashaddr{false}; // reference src/config.cpp:10 (GlobalConfig: useCashAddr(false))
 void SetUseCashAddr(bool on) { g_use_cashaddr = on; }
 bool UseCashAddr() { return g_use_cashaddr; }
 

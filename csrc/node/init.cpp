@@ -84,7 +84,7 @@ std::string HelpMessage() {
         {"-datacarrier", "Relay and mine data carrier transactions (default: 1)"},
         {"-datacarriersize=<n>", "Maximum size of data in data carrier transactions (default: 83)"},
         {"-permitbaremultisig", "Relay non-P2SH multisig (default: 1)"},
-        {"-usecashaddr", "Use Cash Address for destination encoding (default: 1)"},
+        {"-usecashaddr", "Use Cash Address for destination encoding instead of base58 (activate by default on Jan, 14) (default: 0)"},
         {"-server", "Accept command line and JSON-RPC commands (default: 1 for bcpd)"},
         {"-rest", "Accept public REST requests (default: 0)"},
         {"-webgui", "Serve the browser wallet GUI at http://<rpcbind>:<rpcport>/gui to authenticated RPC users (default: 0)"},
@@ -287,7 +287,7 @@ int AppMain(int argc, char* argv[]) {
     fAcceptDatacarrier = gArgs.GetBoolArg("-datacarrier", DEFAULT_ACCEPT_DATACARRIER);
     nMaxDatacarrierBytes = (unsigned)gArgs.GetArg("-datacarriersize", (int64_t)nMaxDatacarrierBytes);
     nBytesPerSigOp = (unsigned)gArgs.GetArg("-bytespersigop", (int64_t)nBytesPerSigOp);
-    SetUseCashAddr(gArgs.GetBoolArg("-usecashaddr", true));
+    SetUseCashAddr(gArgs.GetBoolArg("-usecashaddr", false)); // reference src/init.cpp:2119-2120
     if (!ParseFeeArg("-minrelaytxfee", minRelayTxFee) || !ParseFeeArg("-dustrelayfee", dustRelayFee) ||
         !ParseFeeArg("-incrementalrelayfee", incrementalRelayFee)) {
         InitError("Invalid fee amount argument");

@@ -67,9 +67,10 @@ def test_uri_rpcs(tmp_path):
     n = BcpdProcess(str(tmp_path / "n"), extra_args=["-gpu=0", "-keypool=5"])
     n.start()
     try:
-        addr = n.rpc.getnewaddress()
+        addr = n.rpc.getnewaddress()  # Base58 by default (reference src/init.cpp:2119-2120)
         uri = n.rpc.formatbitcoinuri(addr, 1.5, "me", "for coffee")
-        assert uri.startswith(addr + "?amount=1.5&label=me&message=for%20coffee")
+        # a Base58 address takes the "bitcoincashplus:" scheme (reference src/qt/guiutil.cpp:168-176,263)
+        assert uri.startswith(f"bitcoincashplus:{addr}?amount=1.5&label=me&message=for%20coffee")
         r = n.rpc.parsebitcoinuri(uri)
         assert r["address"] == addr and r["isvalid"] and float(r["amount"]) == 1.5
         assert r["label"] == "me" and r["message"] == "for coffee"
