@@ -504,6 +504,9 @@ int AppMain(int argc, char* argv[]) {
     StopWallet(*node);
     if (node->scheduler) node->scheduler->Stop();
     node->chainstate->Shutdown();
+    // join the GPU verification lanes and destroy their HIP streams now, while the HIP runtime is
+    // still up (the static singleton's destructor would run after it is torn down)
+    GpuVerifyService::Instance().Shutdown();
     SetChainstate(nullptr);
     SetNode(nullptr);
     RemoveFile(datadir + "/" + gArgs.GetArg("-pid", "bitcoincashplusd.pid"));

@@ -630,6 +630,7 @@ struct KVStore::Impl {
     uint64_t logNum = 0, logBytes = 0, firstLog = 0, nextFile = 1, seq = 0;
     bool stop = false, bgError = false, merging = false;
     std::atomic<bool> stopping{false}; // `stop` for loops that do not hold mu
+    std::atomic<int> faults{0};        // KVStore::InjectFault bits (tests)
 
     std::mutex mergeMu; // one merge at a time (background merger or Compact())
     std::thread flusher, merger;
@@ -642,6 +643,7 @@ struct KVStore::Impl {
     std::string ManifestPath() const { return dir + "/MANIFEST"; }
 
     bool WriteManifestLocked() {
+        if (faults.fetch_and(~KVStore::FAULT_MANIFEST) & KVStore::FAULT_MANIFEST) return false;
         std::string m = "BCPKV 1\n";
         m += "next " + std::to_string(nextFile) + "\n";
         m += "log " + std::to_string(firstLog) + "\n";
@@ -848,6 +850,7 @@ struct KVStore::Impl {
     }
 
     std::shared_ptr<Segment> WriteSegment(const Memtable& m, uint64_t maxSeq) {
+        if (faults.fetch_and(~KVStore::FAULT_SEGMENT) & KVStore::FAULT_SEGMENT) return nullptr;
         uint64_t id;
         {
             std::lock_guard<std::shared_mutex> l(mu);
@@ -874,8 +877,9 @@ struct KVStore::Impl {
             auto seg = WriteSegment(*m, maxSeq);
             l.lock();
             if (!seg) {
+                // the sealed memtable stays readable (its keys are in no segment) and its logs
+                // stay on disk for the replay at the next open; no further writes are taken
                 bgError = true;
-                imm.reset();
                 cv.notify_all();
                 return;
             }
@@ -884,9 +888,16 @@ struct KVStore::Impl {
             segs = next;
             const uint64_t oldFirst = firstLog;
             firstLog = sealLog;
-            if (!WriteManifestLocked()) bgError = true;
             imm.reset();
             ctr.flushes++;
+            if (!WriteManifestLocked()) {
+                // the manifest on disk still names the previous segments and the previous first
+                // log: keep those logs for the replay (the new segment, unnamed there, serves the
+                // keys until then and is discarded at the next open)
+                bgError = true;
+                cv.notify_all();
+                return;
+            }
             for (uint64_t n = oldFirst; n < sealLog; n++) ::unlink(Numbered(dir, "kv", n, "log").c_str());
             cv.notify_all();
         }
@@ -995,11 +1006,21 @@ struct KVStore::Impl {
                 cv.notify_all();
                 return false;
             }
-            for (size_t i = lo; i < hi; i++) (*cur)[i]->obsolete = true;
             it = next->erase(it, it + (hi - lo));
             if (seg) next->insert(it, seg);
+            const auto before = segs;
             segs = next;
-            if (!WriteManifestLocked()) bgError = true;
+            if (!WriteManifestLocked()) {
+                // the manifest on disk still names the inputs: keep serving (and keeping) them,
+                // and drop the merged segment the manifest does not know
+                segs = before;
+                if (seg) seg->obsolete = true;
+                merging = false;
+                bgError = true;
+                cv.notify_all();
+                return false;
+            }
+            for (size_t i = lo; i < hi; i++) (*cur)[i]->obsolete = true; // unlinked when released
             ctr.merges++;
             merging = false;
             cv.notify_all();
@@ -1022,6 +1043,8 @@ KVStore::KVStore(const std::string& path, bool memory_only, bool wipe, const KVO
 }
 
 KVStore::~KVStore() {}
+
+void KVStore::InjectFault(int what) { d->faults.fetch_or(what); }
 
 bool KVStore::WriteBatch(KVBatch& batch, bool fSync) {
     if (batch.ops.empty()) return true;
@@ -1089,7 +1112,8 @@ bool KVStore::ReadRaw(const std::string& key, std::string& value) const {
     for (const auto& seg : *s) {
         const int r = seg->Get(key, h, &value);
         if (r == 1) return true;
-        if (r != 0) return false; // tombstone, or an unreadable block
+        if (r == 2) return false; // tombstone
+        if (r < 0) throw KVCorruption("KVStore: unreadable block in " + seg->path);
     }
     return false;
 }
@@ -1128,8 +1152,9 @@ void KVStore::ReadRawMany(const std::string* keys, size_t n, std::string* values
         const uint64_t h = Hash64(keys[i].data(), keys[i].size());
         for (const auto& seg : *s) {
             const int r = seg->Get(keys[i], h, &values[i]);
+            if (r < 0) throw KVCorruption("KVStore: unreadable block in " + seg->path);
             if (r == 1) found[i] = 1;
-            if (r != 0) break; // found, tombstone, or an unreadable block
+            if (r != 0) break; // found, or a tombstone
         }
     }
 }

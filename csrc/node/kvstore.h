@@ -32,6 +32,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -39,6 +40,11 @@
 namespace bcp {
 
 class KVStore;
+
+// A stored block that fails its CRC or cannot be read (disk damage).
+struct KVCorruption : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
 
 class KVBatch {
 public:
@@ -176,6 +182,9 @@ public:
         return WriteBatch(b, fSync);
     }
     bool WriteBatch(KVBatch& batch, bool fSync = false);
+    // A missing key reads as false; a segment block that fails its CRC or cannot be read throws
+    // KVCorruption (the reference's dbwrapper_error, src/dbwrapper.cpp HandleError): disk damage
+    // must never look like an absent key.
     bool ReadRaw(const std::string& key, std::string& value) const;
     // ReadRaw of n keys under one acquisition of the store lock (batched lookups from many
     // threads would otherwise contend on it per key): found[i] says whether values[i] is set.
@@ -196,6 +205,9 @@ public:
     // damaged stretches are skipped (log batches by searching for the next record header).
     // Returns the latest value of every live key; `skipped` counts the damaged bytes.
     static std::map<std::string, std::string> Salvage(const std::string& dir, uint64_t* skipped = nullptr);
+    // Fault injection (tests): the next manifest write / segment write fails.
+    enum : int { FAULT_MANIFEST = 1, FAULT_SEGMENT = 2 };
+    void InjectFault(int what);
 
     struct Impl;
 

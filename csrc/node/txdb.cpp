@@ -1,4 +1,6 @@
 #include "node/txdb.h"
+#include "node/ui_interface.h"
+#include "util/util.h"
 
 #include "consensus/pow.h"
 #include "util/strencodings.h"
@@ -68,13 +70,38 @@ static KVOptions CacheOptions(size_t nCacheSize) {
 CCoinsViewDB::CCoinsViewDB(const std::string& dir, bool fMemory, bool fWipe, size_t nCacheSize)
     : db(dir, fMemory, fWipe, CacheOptions(nCacheSize)) {}
 
-bool CCoinsViewDB::GetCoin(const COutPoint& outpoint, Coin& coin) const { return db.Read(CoinKey(&outpoint), coin); }
-bool CCoinsViewDB::HaveCoin(const COutPoint& outpoint) const { return db.Exists(CoinKey(&outpoint)); }
+// Disk damage under the coin database (KVCorruption): the reference's CCoinsViewErrorCatcher
+// (src/init.cpp:142-163) reports it and aborts. Returning false instead would read as a spent or
+// missing coin, so ConnectBlock would reject a valid block and mark its chain invalid.
+[[noreturn]] static void CoinsReadFailed(const std::exception& e) {
+    uiInterface.ThreadSafeMessageBox("Error reading from database, shutting down.", "", CClientUIInterface::MSG_ERROR);
+    LogPrintf("Error reading from database: %s\n", e.what());
+    std::abort();
+}
+
+bool CCoinsViewDB::GetCoin(const COutPoint& outpoint, Coin& coin) const {
+    try {
+        return db.Read(CoinKey(&outpoint), coin);
+    } catch (const KVCorruption& e) {
+        CoinsReadFailed(e);
+    }
+}
+bool CCoinsViewDB::HaveCoin(const COutPoint& outpoint) const {
+    try {
+        return db.Exists(CoinKey(&outpoint));
+    } catch (const KVCorruption& e) {
+        CoinsReadFailed(e);
+    }
+}
 
 void CCoinsViewDB::PeekCoins(const COutPoint* outpoints, size_t n, Coin* coins, uint8_t* found) const {
     std::vector<std::string> keys(n), values(n);
     for (size_t i = 0; i < n; i++) keys[i] = KVBatch::Ser(CoinKey(&outpoints[i]));
-    db.ReadRawMany(keys.data(), n, values.data(), found);
+    try {
+        db.ReadRawMany(keys.data(), n, values.data(), found);
+    } catch (const KVCorruption& e) {
+        CoinsReadFailed(e);
+    }
     for (size_t i = 0; i < n; i++) {
         if (!found[i]) continue;
         try {

@@ -616,9 +616,14 @@ bool EvalScript(std::vector<valtype>& stack, const CScript& script, uint32_t fla
                     bool fSuccess = true;
                     // Speculative deferral (NULLFAIL, every signature non-empty and well encoded): a
                     // failed match would fail the script, so a batching checker may take the match
-                    // over. Otherwise the greedy loop below runs eagerly, as in the reference.
+                    // over. It queues every (signature, key) pair the greedy match could try,
+                    // m*(n-m+1) of them, where the eager loop verifies at most n (what sigop
+                    // accounting charges): deferral is taken only while that is within 2n (1-of-n,
+                    // n-of-n, 2-of-3, 3-of-5, ...), so a block of 10-of-20 spends at the sigop limit
+                    // never costs more than twice the reference's worst case, on the GPU or on the CPU
+                    // fallback. Otherwise the greedy loop below runs eagerly, as in the reference.
                     bool deferred = false;
-                    if (nullfail && nSigsCount > 0) {
+                    if (nullfail && nSigsCount > 0 && nSigsCount * (nKeysCount - nSigsCount + 1) <= 2 * nKeysCount) {
                         std::vector<const valtype*> sigs, keys;
                         bool defer = true;
                         for (int k = 0; k < nSigsCount && defer; k++) {

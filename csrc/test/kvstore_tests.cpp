@@ -384,3 +384,118 @@ TEST_CASE(kvstore_tests, salvage_skips_damage) {
     for (const auto& kv : got) CHECK(model.count(kv.first) && model[kv.first] == kv.second);
     RmRf(dir);
 }
+
+// A damaged segment block is an error, never a missing key (reference dbwrapper_error): the
+// chainstate would otherwise read disk damage as a spent coin and reject a valid block.
+TEST_CASE(kvstore_tests, corrupt_block_reads_as_an_error) {
+    const std::string dir = TempDir("db");
+    std::map<std::string, std::string> model;
+    {
+        KVStore db(dir, false, true, Small());
+        for (int i = 0; i < 600; i++) {
+            KVBatch b;
+            b.WriteRaw(K(i), std::string(50, 'a' + i % 26));
+            model[K(i)] = std::string(50, 'a' + i % 26);
+            REQUIRE(db.WriteBatch(b));
+        }
+        db.Flush();
+    }
+    std::string seg;
+    for (int n = 1; n < 400 && seg.empty(); n++) {
+        const std::string p = strprintf("%s/seg-%06d.sst", dir.c_str(), n);
+        struct stat st;
+        if (stat(p.c_str(), &st) == 0 && st.st_size > 2048) seg = p;
+    }
+    REQUIRE(!seg.empty());
+    FILE* f = fopen(seg.c_str(), "r+b");
+    REQUIRE(f != nullptr);
+    fseek(f, 100, SEEK_SET);
+    fputc(0xEE, f);
+    fclose(f);
+    KVStore db(dir, false, false, Small());
+    size_t thrown = 0, ok = 0;
+    for (const auto& kv : model) {
+        std::string v;
+        try {
+            const bool found = db.ReadRaw(kv.first, v);
+            CHECK(found); // never "absent"
+            CHECK(v == kv.second);
+            ++ok;
+        } catch (const KVCorruption&) {
+            ++thrown;
+        }
+    }
+    CHECK(thrown > 0);
+    CHECK(ok > model.size() / 2);
+    // the batched lookup (CCoinsViewDB::PeekCoins) reports the damage the same way
+    std::vector<std::string> keys, vals(model.size());
+    for (const auto& kv : model) keys.push_back(kv.first);
+    std::vector<uint8_t> found(keys.size());
+    bool threw = false;
+    try {
+        db.ReadRawMany(keys.data(), keys.size(), vals.data(), found.data());
+    } catch (const KVCorruption&) {
+        threw = true;
+    }
+    CHECK(threw);
+    RmRf(dir);
+}
+
+// A failed manifest write (flush or merge) keeps every committed key: the logs the old manifest
+// still names are not unlinked, merge inputs are not dropped, and a reopen replays them.
+TEST_CASE(kvstore_tests, failed_manifest_write_loses_nothing) {
+    for (int mode = 0; mode < 2; mode++) { // 0: during a flush, 1: during a merge (Compact)
+        const std::string dir = TempDir("db");
+        std::map<std::string, std::string> model;
+        {
+            KVStore db(dir, false, true, Small());
+            for (int i = 0; i < 400; i++) {
+                KVBatch b;
+                b.WriteRaw(K(i), strprintf("v%d-%d", i, mode));
+                REQUIRE(db.WriteBatch(b));
+                model[K(i)] = strprintf("v%d-%d", i, mode);
+            }
+            db.Flush();
+            db.InjectFault(KVStore::FAULT_MANIFEST);
+            if (mode == 0) {
+                for (int i = 400; i < 2000; i++) { // until the background flush fails
+                    KVBatch b;
+                    b.WriteRaw(K(i), std::string(40, 'x'));
+                    if (!db.WriteBatch(b)) break;
+                    model[K(i)] = std::string(40, 'x');
+                }
+            } else {
+                db.Compact();
+            }
+            CHECK(SameAsModel(db, model, mode ? "after failed merge" : "after failed flush"));
+        }
+        KVStore db(dir, false, false, Small());
+        CHECK(SameAsModel(db, model, mode ? "reopened after failed merge" : "reopened after failed flush"));
+        RmRf(dir);
+    }
+}
+
+// A failed segment write keeps the sealed memtable readable and its logs for the replay.
+TEST_CASE(kvstore_tests, failed_segment_write_loses_nothing) {
+    const std::string dir = TempDir("db");
+    std::map<std::string, std::string> model;
+    bool refused = false;
+    {
+        KVStore db(dir, false, true, Small());
+        db.InjectFault(KVStore::FAULT_SEGMENT);
+        for (int i = 0; i < 3000; i++) {
+            KVBatch b;
+            b.WriteRaw(K(i), std::string(40, 'a' + i % 26));
+            if (!db.WriteBatch(b)) {
+                refused = true;
+                break;
+            }
+            model[K(i)] = std::string(40, 'a' + i % 26);
+        }
+        CHECK(SameAsModel(db, model, "after failed segment write"));
+    }
+    CHECK(refused); // the store stops taking writes once a flush failed
+    KVStore db(dir, false, false, Small());
+    CHECK(SameAsModel(db, model, "reopened after failed segment write"));
+    RmRf(dir);
+}

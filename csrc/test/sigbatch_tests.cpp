@@ -181,3 +181,32 @@ TEST_CASE(sigbatch_tests, checksig_deferral_matches_eager) {
     }
     CHECK(deferred > 300);
 }
+
+// Deferral is bounded: a CHECKMULTISIG whose candidate pairs m*(n-m+1) exceed 2n (10-of-20: 110
+// pairs against the 20 the reference's greedy loop can verify) runs eagerly, so a block at the
+// sigop limit made of such spends costs no more than twice the reference's worst case. Typical
+// shapes (2-of-3, 3-of-5, n-of-n) still defer. Verdicts match the eager run either way.
+TEST_CASE(sigbatch_tests, multisig_deferral_is_bounded) {
+    test::BasicTestingSetup setup("main");
+    std::vector<CKey> keys(20);
+    for (size_t i = 0; i < keys.size(); i++) keys[i].MakeNewKey(true);
+    struct Shape { int m, n; bool defers; };
+    for (const Shape sh : {Shape{10, 20, false}, Shape{5, 10, false}, Shape{2, 3, true}, Shape{3, 5, true},
+                           Shape{20, 20, true}, Shape{1, 20, true}}) {
+        CScript spk;
+        spk << sh.m;
+        for (int j = 0; j < sh.n; j++) spk << keys[j].GetPubKey().Raw();
+        spk << sh.n << OP_CHECKMULTISIG;
+        const CMutableTransaction tx = SpendOf(spk);
+        CScript sigs;
+        sigs << OP_0;
+        for (int j = 0; j < sh.m; j++) sigs << SignFor(keys[2 * j * sh.n / (2 * sh.m)], spk, tx, SIGHASH_ALL | SIGHASH_FORKID);
+        CMutableTransaction mtx = tx;
+        mtx.vin[0].scriptSig = sigs;
+        const Outcome o = RunBoth(sigs, spk, mtx);
+        CHECK(o.eager && o.deferred);
+        CHECK_EQ(o.groups, sh.defers ? 1u : 0u);
+        // pairs queued for the batch: at most 2n
+        CHECK(o.checks <= (size_t)(2 * sh.n));
+    }
+}

@@ -10,7 +10,7 @@ static const size_t MAX_CLAIM = 16;
 // Jobs per woken worker (a worker that finds more than it claimed wakes the next one).
 static const size_t MIN_WAKE_JOBS = 4;
 
-CheckQueue::CheckQueue(int nWorkers) : sessionLock(sessionMutex, std::defer_lock) {
+CheckQueue::CheckQueue(int nWorkers) {
     for (int i = 0; i < nWorkers; i++) threads.emplace_back([this] { Loop(); });
 }
 
@@ -71,11 +71,12 @@ void CheckQueue::Loop() {
 }
 
 void CheckQueue::Begin(std::function<void(size_t)> f) {
-    sessionLock.lock();
+    sessionMutex.lock(); // a second caller blocks here until the open session completes
     std::lock_guard<std::mutex> l(m);
     fn = std::move(f);
     avail = next = done = 0;
     active = true;
+    sessionOwner = std::this_thread::get_id();
 }
 
 void CheckQueue::Publish(size_t total) {
@@ -86,8 +87,8 @@ void CheckQueue::Publish(size_t total) {
 }
 
 void CheckQueue::Complete() {
-    if (!sessionLock.owns_lock()) return;
     std::unique_lock<std::mutex> l(m);
+    if (!active || sessionOwner != std::this_thread::get_id()) return; // no session of this thread
     size_t b = 0, e = 0;
     while (ClaimLocked(b, e)) { // the caller helps drain the queue
         l.unlock();
@@ -97,10 +98,11 @@ void CheckQueue::Complete() {
     }
     cvDone.wait(l, [&] { return done == avail; });
     active = false;
+    sessionOwner = std::thread::id();
     fn = nullptr;
     avail = next = done = 0;
     l.unlock();
-    sessionLock.unlock();
+    sessionMutex.unlock();
 }
 
 } // namespace bcp

@@ -47,8 +47,8 @@ private:
     std::vector<std::thread> threads;
     mutable std::mutex m;
     std::condition_variable cvWork, cvDone;
-    std::mutex sessionMutex; // one open session per queue
-    std::unique_lock<std::mutex> sessionLock;
+    std::mutex sessionMutex;      // one open session per queue: held from Begin to Complete
+    std::thread::id sessionOwner; // the thread that opened the session (guarded by m)
     std::function<void(size_t)> fn;
     size_t avail = 0, next = 0, done = 0;
     size_t workerJobs = 0;
