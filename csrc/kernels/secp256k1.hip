@@ -46,6 +46,12 @@ __device__ __forceinline__ void fe_set(fe& r, const fe& a) {
     for (int i = 0; i < 8; i++) r.v[i] = a.v[i];
 }
 
+// Field elements are kept LAZILY reduced: any value in [0, 2^256) stands for itself mod p.
+// Additions, subtractions and products fold the excess over 2^256 back in as
+// 2^256 = 2^32 + 977 (mod p) instead of comparing against p, and only fe_normalize (used by
+// every comparison and parity test) brings a value below p — a value below 2^256 < 2p needs at
+// most one subtraction of p.
+
 // r = a - p if a >= p (a < 2p)
 __device__ __forceinline__ void fe_cond_sub_p(fe& a, uint32_t carry_in) {
     uint32_t t[8];
@@ -61,116 +67,141 @@ __device__ __forceinline__ void fe_cond_sub_p(fe& a, uint32_t carry_in) {
 #pragma unroll
     for (int i = 0; i < 8; i++) a.v[i] = take ? t[i] : a.v[i];
 }
+__device__ __forceinline__ void fe_normalize(fe& a) { fe_cond_sub_p(a, 0); }
+
+// 32-bit add / subtract with carry (v_add_co / v_addc, v_sub_co / v_subb chains)
+__device__ __forceinline__ uint32_t addc(uint32_t a, uint32_t b, uint32_t ci, uint32_t* co) {
+    return __builtin_addc(a, b, ci, co);
+}
+__device__ __forceinline__ uint32_t subb(uint32_t a, uint32_t b, uint32_t bi, uint32_t* bo) {
+    return __builtin_subc(a, b, bi, bo);
+}
+
+// r += c * 2^256 (mod p) for c < 2^40, as r += c * (2^32 + 977); repeats while the sum carries
+// out of 2^256 again (only for r within (2^32 + 977) c of 2^256).
+__device__ __forceinline__ void fe_fold(fe& r, uint64_t c) {
+    while (c) {
+        uint32_t co;
+        const uint64_t lo = c * 977u;                          // < 2^50
+        const uint64_t mid = (lo >> 32) + (uint32_t)c;         // limb 1 (< 2^33)
+        r.v[0] = addc(r.v[0], (uint32_t)lo, 0, &co);
+        r.v[1] = addc(r.v[1], (uint32_t)mid, co, &co);
+        r.v[2] = addc(r.v[2], (uint32_t)(mid >> 32) + (uint32_t)(c >> 32), co, &co);
+#pragma unroll
+        for (int i = 3; i < 8; i++) r.v[i] = addc(r.v[i], 0, co, &co);
+        c = co;
+    }
+}
+// r -= b * 2^256 (mod p), as r -= b * (2^32 + 977), while the difference borrows below 0
+__device__ __forceinline__ void fe_unfold(fe& r, uint32_t b) {
+    while (b) {
+        uint32_t bo;
+        r.v[0] = subb(r.v[0], 977u * b, 0, &bo);
+        r.v[1] = subb(r.v[1], b, bo, &bo);
+#pragma unroll
+        for (int i = 2; i < 8; i++) r.v[i] = subb(r.v[i], 0, bo, &bo);
+        b = bo;
+    }
+}
 
 __device__ __forceinline__ void fe_add(fe& r, const fe& a, const fe& b) {
-    uint64_t c = 0;
+    uint32_t c = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        c += (uint64_t)a.v[i] + b.v[i];
-        r.v[i] = (uint32_t)c;
-        c >>= 32;
-    }
-    fe_cond_sub_p(r, (uint32_t)c);
+    for (int i = 0; i < 8; i++) r.v[i] = addc(a.v[i], b.v[i], c, &c);
+    fe_fold(r, c);
 }
 
 __device__ __forceinline__ void fe_sub(fe& r, const fe& a, const fe& b) {
-    uint64_t borrow = 0;
-    uint32_t t[8];
+    uint32_t bo = 0;
 #pragma unroll
-    for (int i = 0; i < 8; i++) {
-        const uint64_t d = (uint64_t)a.v[i] - b.v[i] - borrow;
-        t[i] = (uint32_t)d;
-        borrow = (d >> 63) & 1;
-    }
-    // if negative, add p back
-    uint64_t c = 0;
-    const uint32_t mask = borrow ? 0xFFFFFFFFu : 0u;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        c += (uint64_t)t[i] + (P_LIMBS[i] & mask);
-        r.v[i] = (uint32_t)c;
-        c >>= 32;
-    }
+    for (int i = 0; i < 8; i++) r.v[i] = subb(a.v[i], b.v[i], bo, &bo);
+    fe_unfold(r, bo); // a - b + 2^256 was computed: take 2^256 = 2^32 + 977 back out
 }
 
 __device__ __forceinline__ void fe_mul_small(fe& r, const fe& a, uint32_t m) {
     // r = a*m mod p for small m (2, 3, 4, 8)
-    uint64_t c = 0;
-    uint32_t t[8];
+    uint32_t hi = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        c += (uint64_t)a.v[i] * m;
-        t[i] = (uint32_t)c;
-        c >>= 32;
+        const uint64_t p = (uint64_t)a.v[i] * m + hi;
+        r.v[i] = (uint32_t)p;
+        hi = (uint32_t)(p >> 32);
     }
-    // fold c * 2^256 = c * (2^32 + 977)
-    uint64_t f = (uint64_t)t[0] + c * 977u;
-    r.v[0] = (uint32_t)f;
-    f = (f >> 32) + (uint64_t)t[1] + c;
-    r.v[1] = (uint32_t)f;
-    f >>= 32;
-#pragma unroll
-    for (int i = 2; i < 8; i++) {
-        f += t[i];
-        r.v[i] = (uint32_t)f;
-        f >>= 32;
-    }
-    fe_cond_sub_p(r, (uint32_t)f);
+    fe_fold(r, hi);
 }
 
-__device__ __forceinline__ void fe_reduce512(fe& r, const uint32_t (&t)[16]);
+// One product-scanning step: {acc} += a*b, c2 += the carry out of the 64-bit accumulator
+// (v_mad_u64_u32 writes its carry to VCC, which v_addc folds into the column's third word; a
+// VALU carry-in read needs two wait states after the VALU write of VCC on gfx950).
+__device__ __forceinline__ void fe_mac(uint64_t& acc, uint32_t& c2, uint32_t a, uint32_t b) {
+    asm("v_mad_u64_u32 %0, vcc, %2, %3, %0\n\ts_nop 1\n\tv_addc_co_u32_e32 %1, vcc, 0, %1, vcc"
+        : "+v"(acc), "+v"(c2)
+        : "v"(a), "v"(b)
+        : "vcc");
+}
 
-// 512-bit product reduced mod p.
-__device__ __forceinline__ void fe_mul_impl(fe& r, const fe& a, const fe& b) {
-    uint32_t t[16];
+// 512-bit value t reduced to r < 2^256 (r = t mod p, lazily): r = lo + hi * (2^32 + 977)
+__device__ __forceinline__ void fe_reduce512(fe& r, const uint32_t (&t)[16]) {
+    uint32_t u[8], c = 0; // u = lo + (hi << 32), u8 its top word (33 bits)
+    u[0] = t[0];
 #pragma unroll
-    for (int i = 0; i < 16; i++) t[i] = 0;
+    for (int i = 1; i < 8; i++) u[i] = addc(t[i], t[7 + i], c, &c);
+    const uint64_t u8 = (uint64_t)t[15] + c;
+    uint32_t cc = 0; // + hi * 977, carried limb by limb (every partial < 2^43)
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-        uint64_t carry = 0;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            const uint64_t p = (uint64_t)a.v[i] * b.v[j] + t[i + j] + carry;
-            t[i + j] = (uint32_t)p;
-            carry = p >> 32;
-        }
-        t[i + 8] = (uint32_t)carry;
+        const uint64_t p = (uint64_t)t[8 + i] * 977u + cc;
+        uint32_t co;
+        r.v[i] = addc(u[i], (uint32_t)p, 0, &co);
+        cc = (uint32_t)(p >> 32) + co;
     }
+    fe_fold(r, u8 + cc); // value = r + (u8 + cc) * 2^256, u8 + cc < 2^34
+}
+
+// Product scanning (Comba): column k of a*b accumulates every a_i*b_j with i + j = k in a
+// 3-word accumulator; 64 v_mad_u64_u32 + 64 v_addc, no zero-extended 64-bit adds.
+__device__ __forceinline__ void fe_mul_impl(fe& r, const fe& a, const fe& b) {
+    uint32_t t[16];
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
+#pragma unroll
+    for (int k = 0; k < 15; k++) {
+#pragma unroll
+        for (int i = (k > 7 ? k - 7 : 0); i <= (k < 7 ? k : 7); i++) fe_mac(acc, c2, a.v[i], b.v[k - i]);
+        t[k] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)c2 << 32);
+        c2 = 0;
+    }
+    t[15] = (uint32_t)acc;
     fe_reduce512(r, t);
 }
 
-// Squaring: the 28 cross products a_i*a_j (i<j) once, doubled with a 1-bit shift, plus the 8
-// diagonal squares — 36 32x32 multiplies instead of the 64 of fe_mul. Point doubling and the
-// inversion/sqrt ladders are mostly squarings.
+// Squaring: the 28 cross products a_i*a_j (i<j) once by product scanning, doubled with a 1-bit
+// shift, plus the 8 diagonal squares — 36 multiplies instead of 64.
 __device__ __forceinline__ void fe_sqr_impl(fe& r, const fe& a) {
     uint32_t t[16];
+    t[0] = 0;
+    uint64_t acc = 0;
+    uint32_t c2 = 0;
 #pragma unroll
-    for (int i = 0; i < 16; i++) t[i] = 0;
+    for (int k = 1; k < 14; k++) {
 #pragma unroll
-    for (int i = 0; i < 7; i++) {
-        uint64_t carry = 0;
-#pragma unroll
-        for (int j = i + 1; j < 8; j++) {
-            const uint64_t p = (uint64_t)a.v[i] * a.v[j] + t[i + j] + carry;
-            t[i + j] = (uint32_t)p;
-            carry = p >> 32;
-        }
-        t[i + 8] = (uint32_t)carry;
+        for (int i = (k > 7 ? k - 7 : 0); 2 * i < k; i++) fe_mac(acc, c2, a.v[i], a.v[k - i]);
+        t[k] = (uint32_t)acc;
+        acc = (acc >> 32) | ((uint64_t)c2 << 32);
+        c2 = 0;
     }
+    t[14] = (uint32_t)acc;
     t[15] = t[14] >> 31;
 #pragma unroll
-    for (int i = 14; i > 0; i--) t[i] = (t[i] << 1) | (t[i - 1] >> 31);
-    t[0] <<= 1;
-    uint64_t c = 0;
+    for (int i = 14; i > 0; i--) t[i] = __builtin_amdgcn_alignbit(t[i], t[i - 1], 31); // (t[i] << 1) | (t[i-1] >> 31)
+    t[0] = 0;
+    uint32_t c = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
         const uint64_t sq = (uint64_t)a.v[i] * a.v[i];
-        c += (uint64_t)t[2 * i] + (uint32_t)sq;
-        t[2 * i] = (uint32_t)c;
-        c >>= 32;
-        c += (uint64_t)t[2 * i + 1] + (sq >> 32);
-        t[2 * i + 1] = (uint32_t)c;
-        c >>= 32;
+        t[2 * i] = addc(t[2 * i], (uint32_t)sq, c, &c);
+        t[2 * i + 1] = addc(t[2 * i + 1], (uint32_t)(sq >> 32), c, &c);
     }
     fe_reduce512(r, t);
 }
@@ -192,74 +223,25 @@ __device__ __noinline__ fe fe_sqr_v(fe a) {
 __device__ __forceinline__ void fe_mul(fe& r, const fe& a, const fe& b) { r = fe_mul_v(a, b); }
 __device__ __forceinline__ void fe_sqr(fe& r, const fe& a) { r = fe_sqr_v(a); }
 
-// 512-bit value t (t < 2^512) reduced mod p.
-__device__ __forceinline__ void fe_reduce512(fe& r, const uint32_t (&t)[16]) {
-    // lo + hi * (2^32 + 977)
-    uint32_t u[9];
-    uint64_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        c += (uint64_t)t[i] + (uint64_t)t[8 + i] * 977u;
-        u[i] = (uint32_t)c;
-        c >>= 32;
-    }
-    u[8] = (uint32_t)c;
-    // add hi << 32
-    c = 0;
-#pragma unroll
-    for (int i = 1; i < 9; i++) {
-        c += (uint64_t)u[i] + t[8 + i - 1];
-        u[i] = (uint32_t)c;
-        c >>= 32;
-    }
-    // u[8] + c*2^32 is the overflow limb(s): value = u[0..7] + (u[8] + c<<32) * 2^256
-    const uint64_t top = (uint64_t)u[8] + (c << 32);
-    // fold top * (2^32 + 977)
-    uint64_t f = (uint64_t)u[0] + (top & 0xFFFFFFFFu) * 977u;
-    const uint64_t topHi977 = (top >> 32) * 977u; // top>>32 is tiny (0 or 1)
-    r.v[0] = (uint32_t)f;
-    f = (f >> 32) + (uint64_t)u[1] + (top & 0xFFFFFFFFu) + topHi977;
-    r.v[1] = (uint32_t)f;
-    f = (f >> 32) + (uint64_t)u[2] + (top >> 32);
-    r.v[2] = (uint32_t)f;
-    f >>= 32;
-#pragma unroll
-    for (int i = 3; i < 8; i++) {
-        f += u[i];
-        r.v[i] = (uint32_t)f;
-        f >>= 32;
-    }
-    // f is 0 or 1 here; a final fold keeps r < 2^256 then reduce below p
-    if (f) {
-        uint64_t g = (uint64_t)r.v[0] + 977u;
-        r.v[0] = (uint32_t)g;
-        g = (g >> 32) + (uint64_t)r.v[1] + 1u;
-        r.v[1] = (uint32_t)g;
-        g >>= 32;
-#pragma unroll
-        for (int i = 2; i < 8; i++) {
-            g += r.v[i];
-            r.v[i] = (uint32_t)g;
-            g >>= 32;
-        }
-    }
-    fe_cond_sub_p(r, 0);
-}
-
-
 __device__ __forceinline__ void fe_sqr_n(fe& r, const fe& a, int n) {
     fe_sqr(r, a);
     for (int i = 1; i < n; i++) fe_sqr(r, r);
 }
 
-__device__ __forceinline__ bool fe_is_zero(const fe& a) {
+// comparisons see canonical values (a lazily reduced p reads as 0)
+__device__ __forceinline__ bool fe_is_zero(const fe& in) {
+    fe a = in;
+    fe_normalize(a);
     uint32_t o = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) o |= a.v[i];
     return o == 0;
 }
 
-__device__ __forceinline__ bool fe_eq(const fe& a, const fe& b) {
+__device__ __forceinline__ bool fe_eq(const fe& ain, const fe& bin) {
+    fe a = ain, b = bin;
+    fe_normalize(a);
+    fe_normalize(b);
     uint32_t o = 0;
 #pragma unroll
     for (int i = 0; i < 8; i++) o |= a.v[i] ^ b.v[i];
@@ -893,6 +875,7 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
     fe_mul(y2, y2, qx);
     fe_add(y2, y2, seven);
     ok = ok && fe_sqrt(qy, y2);
+    fe_normalize(qy); // the parity of the canonical root
     if ((qy.v[0] & 1) != (uint32_t)(J.pub[0] & 1)) {
         fe zero;
 #pragma unroll
