@@ -302,4 +302,16 @@ CMerkleBlock::CMerkleBlock(const CBlock& block, const std::set<uint256>& txids) 
     txn = CPartialMerkleTree(vHashes, vMatch);
 }
 
+bool DecodeTxOutProof(const std::vector<unsigned char>& data, CMerkleBlock& mb) {
+    for (int legacy = 0; legacy < 2; legacy++) {
+        try {
+            SpanReader r(data.data(), data.size(), SER_NETWORK, PROTOCOL_VERSION | (legacy ? SERIALIZE_BLOCK_LEGACY : 0));
+            r >> mb;
+            if (r.empty()) return true;
+        } catch (const std::exception&) {
+        }
+    }
+    return false;
+}
+
 } // namespace bcp

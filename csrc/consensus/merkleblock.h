@@ -126,4 +126,9 @@ public:
     }
 };
 
+// A gettxoutproof proof (a serialized CMerkleBlock). The header inside is the legacy 80-byte form
+// below the fork height and the new form above it, and nothing in the bytes says which: both are
+// tried and the one that consumes the proof exactly wins (verifytxoutproof, importprunedfunds).
+bool DecodeTxOutProof(const std::vector<unsigned char>& data, CMerkleBlock& mb);
+
 } // namespace bcp

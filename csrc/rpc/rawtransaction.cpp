@@ -348,17 +348,7 @@ static UniValue verifytxoutproof(const JSONRPCRequest& req) {
     Chainstate& cs = *n.chainstate;
     std::vector<unsigned char> data = ParseHexV(req.params[0], "proof");
     CMerkleBlock merkleBlock;
-    bool ok = false;
-    // the header format (legacy 80 B vs new) is not self-describing: try both
-    for (int legacy = 0; legacy < 2 && !ok; legacy++) {
-        try {
-            SpanReader r(data.data(), data.size(), SER_NETWORK, PROTOCOL_VERSION | (legacy ? SERIALIZE_BLOCK_LEGACY : 0));
-            r >> merkleBlock;
-            ok = r.empty();
-        } catch (const std::exception&) {
-        }
-    }
-    if (!ok) ThrowRPC(RPC_DESERIALIZATION_ERROR, "Proof decode failed");
+    if (!DecodeTxOutProof(data, merkleBlock)) ThrowRPC(RPC_DESERIALIZATION_ERROR, "Proof decode failed");
     UniValue res(UniValue::VARR);
     std::vector<uint256> vMatch;
     std::vector<unsigned> vIndex;

@@ -644,9 +644,13 @@ static UniValue listsinceblock(const JSONRPCRequest& req) {
     int target_confirms = 1;
     isminefilter filter = ISMINE_SPENDABLE;
     if (!req.params.empty() && !req.params[0].isNull()) {
-        const uint256 h = ParseHashV(req.params[0], "blockhash");
+        // an unknown block lists everything; a block of a branch that is no longer active is
+        // replaced by its fork point with the active chain, so transactions the reorg moved onto
+        // the winning branch are reported (reference src/wallet/rpcwallet.cpp:2069-2082)
+        uint256 h;
+        h.SetHex(req.params[0].get_str());
         pindex = cs.LookupBlockIndex(h);
-        if (!pindex) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Block not found");
+        if (pindex && cs.ActiveChain()[pindex->nHeight] != pindex) pindex = cs.ActiveChain().FindFork(pindex);
     }
     if (req.params.size() > 1 && !req.params[1].isNull()) {
         target_confirms = req.params[1].get_int();
@@ -1241,63 +1245,126 @@ static UniValue importmulti(const JSONRPCRequest& req) {
     for (size_t i = 0; i < requests.size(); i++) {
         const UniValue& d = requests[i];
         UniValue result(UniValue::VOBJ);
+        // the timestamp is checked outside the per-request error capture: a missing or malformed
+        // one fails the whole call (reference GetImportTimestamp, src/wallet/rpcdump.cpp:1065)
+        int64_t ts = 0;
+        if (!d.exists("timestamp")) ThrowRPC(RPC_TYPE_ERROR, "Missing required timestamp field for key");
+        if (d["timestamp"].isNum()) ts = d["timestamp"].get_int64();
+        else if (d["timestamp"].isStr() && d["timestamp"].get_str() == "now") ts = GetTime();
+        else ThrowRPC(RPC_TYPE_ERROR, "Expected number or \"now\" timestamp value for key");
         try {
+            // One request (reference src/wallet/rpcdump.cpp:692-1060 ProcessImport): the same
+            // checks, error codes and messages, in the same order.
             const UniValue& spk = d["scriptPubKey"];
-            const std::string label = d.exists("label") ? d["label"].get_str() : "";
-            const bool watchOnly = d.exists("watchonly") && d["watchonly"].get_bool();
+            if (!(spk.isObject() && spk.exists("address")) && !spk.isStr())
+                ThrowRPC(RPC_INVALID_PARAMETER, "Invalid scriptPubKey");
+            const std::string redeemHex = d.exists("redeemscript") ? d["redeemscript"].get_str() : "";
+            const UniValue pubKeys = d.exists("pubkeys") ? d["pubkeys"].get_array() : UniValue(UniValue::VARR);
+            const UniValue keys = d.exists("keys") ? d["keys"].get_array() : UniValue(UniValue::VARR);
             const bool internal = d.exists("internal") && d["internal"].get_bool();
-            int64_t ts = 0;
-            if (d.exists("timestamp")) {
-                if (d["timestamp"].isNum()) ts = d["timestamp"].get_int64();
-                else if (d["timestamp"].get_str() == "now") ts = GetTime();
-            } else {
-                ThrowRPC(RPC_TYPE_ERROR, "Missing required timestamp field for key");
-            }
+            const bool watchOnly = d.exists("watchonly") && d["watchonly"].get_bool();
+            const std::string label = d.exists("label") && !internal ? d["label"].get_str() : "";
+            const bool isScript = spk.isStr();
+            const bool isP2SH = !redeemHex.empty();
             CScript script;
             CTxDestination dest;
-            if (spk.isObject()) {
+            if (!isScript) {
                 dest = DecodeDestination(spk["address"].get_str(), P());
                 if (!dest.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid address");
                 script = GetScriptForDestination(dest);
             } else {
+                if (!IsHex(spk.get_str())) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid scriptPubKey");
                 const std::vector<unsigned char> data = ParseHex(spk.get_str());
                 script = CScript(data.begin(), data.end());
-                ExtractDestination(script, dest);
             }
-            if (!internal && !dest.IsValid() && !spk.isObject())
-                ThrowRPC(RPC_INVALID_PARAMETER, "Internal must be set for hex scriptPubKey");
+            if (watchOnly && keys.size()) ThrowRPC(RPC_INVALID_PARAMETER, "Incompatibility found between watchonly and keys");
+            if (internal && d.exists("label")) ThrowRPC(RPC_INVALID_PARAMETER, "Incompatibility found between internal and label");
+            if (!internal && isScript) ThrowRPC(RPC_INVALID_PARAMETER, "Internal must be set for hex scriptPubKey");
+            if (!isP2SH && (keys.size() > 1 || pubKeys.size() > 1))
+                ThrowRPC(RPC_INVALID_PARAMETER, "More than private key given for one address");
+            if (isP2SH && !IsHex(redeemHex)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid redeem script");
+            auto alreadyMine = [&](const CScript& s) {
+                if (IsMine(w, s) == ISMINE_SPENDABLE)
+                    ThrowRPC(RPC_WALLET_ERROR, "The wallet already contains the private key for this address or script");
+            };
+            auto watch = [&](const CScript& s) {
+                if (!w.HaveWatchOnly(s) && !w.AddWatchOnly(s, ts)) ThrowRPC(RPC_WALLET_ERROR, "Error adding address to wallet");
+            };
+            auto decodeKey = [&](const UniValue& v) {
+                const CKey key = DecodeSecret(v.get_str(), P());
+                if (!key.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid private key encoding");
+                return key;
+            };
+            // a key or pubkey must belong to the destination being imported
+            auto consistent = [&](const CKeyID& id) {
+                CTxDestination sd;
+                if (!isScript ? !(dest == CTxDestination(id)) : (ExtractDestination(script, sd) && !(sd == CTxDestination(id))))
+                    ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Consistency check failed");
+            };
+            bool success = false;
             WalletLock l(w);
-            if (d.exists("redeemscript")) {
-                const std::vector<unsigned char> rs = ParseHex(d["redeemscript"].get_str());
-                w.AddCScript(CScript(rs.begin(), rs.end()));
-            }
-            bool importedKey = false;
-            if (d.exists("keys")) {
-                const UniValue& keys = d["keys"].get_array();
+            if (isP2SH) {
+                const std::vector<unsigned char> rd = ParseHex(redeemHex);
+                const CScript redeem(rd.begin(), rd.end());
+                if (!script.IsPayToScriptHash()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid P2SH address / script");
+                watch(redeem);
+                if (!w.HaveCScript(CScriptID(redeem)) && !w.AddCScript(redeem))
+                    ThrowRPC(RPC_WALLET_ERROR, "Error adding p2sh redeemScript to wallet");
+                const CScript redeemDest = GetScriptForDestination(CTxDestination(CScriptID(redeem)));
+                alreadyMine(redeemDest);
+                watch(redeemDest);
+                if (dest.IsValid()) w.SetAddressBook(dest, label, "receive");
                 for (size_t k = 0; k < keys.size(); k++) {
-                    EnsureWalletIsUnlocked(w);
-                    const CKey key = DecodeSecret(keys[k].get_str(), P());
-                    if (!key.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid private key encoding");
+                    const CKey key = decodeKey(keys[k]);
                     const CPubKey pub = key.GetPubKey();
-                    if (!w.HaveKey(pub.GetID())) {
-                        w.mapKeyMetadata[pub.GetID()].nCreateTime = ts;
-                        w.AddKeyPubKey(key, pub);
-                    }
-                    importedKey = true;
+                    w.SetAddressBook(pub.GetID(), label, "receive");
+                    if (w.HaveKey(pub.GetID())) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Already have this key");
+                    w.mapKeyMetadata[pub.GetID()].nCreateTime = ts;
+                    if (!w.AddKeyPubKey(key, pub)) ThrowRPC(RPC_WALLET_ERROR, "Error adding key to wallet");
+                    w.UpdateTimeFirstKey(ts);
                 }
-            }
-            if (d.exists("pubkeys")) {
-                const UniValue& pubs = d["pubkeys"].get_array();
-                for (size_t k = 0; k < pubs.size(); k++) {
-                    const std::vector<unsigned char> pd = ParseHex(pubs[k].get_str());
+                success = true;
+            } else {
+                if (pubKeys.size() && keys.size() == 0) {
+                    const std::string hex = pubKeys[0].get_str();
+                    if (!IsHex(hex)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Pubkey must be a hex string");
+                    const std::vector<unsigned char> pd = ParseHex(hex);
                     const CPubKey pub(pd.begin(), pd.end());
                     if (!pub.IsFullyValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Pubkey is not a valid public key");
+                    consistent(pub.GetID());
+                    const CScript pubKeyScript = GetScriptForDestination(CTxDestination(pub.GetID()));
+                    alreadyMine(pubKeyScript);
+                    watch(pubKeyScript);
+                    w.SetAddressBook(pub.GetID(), label, "receive");
+                    const CScript raw = GetScriptForRawPubKey(pub);
+                    alreadyMine(raw);
+                    watch(raw);
+                    success = true;
+                }
+                if (keys.size()) {
+                    const CKey key = decodeKey(keys[0]);
+                    const CPubKey pub = key.GetPubKey();
+                    consistent(pub.GetID());
+                    w.SetAddressBook(pub.GetID(), label, "receive");
+                    if (!w.HaveKey(pub.GetID())) {
+                        w.mapKeyMetadata[pub.GetID()].nCreateTime = ts;
+                        if (!w.AddKeyPubKey(key, pub)) ThrowRPC(RPC_WALLET_ERROR, "Error adding key to wallet");
+                        w.UpdateTimeFirstKey(ts);
+                        success = true;
+                    }
+                }
+                if (pubKeys.size() == 0 && keys.size() == 0) {
+                    alreadyMine(script);
+                    watch(script);
+                    if (!isScript && dest.IsValid()) w.SetAddressBook(dest, label, "receive");
+                    success = true;
                 }
             }
-            if (!importedKey || watchOnly) {
-                if (IsMine(w, script) != ISMINE_SPENDABLE && !w.HaveWatchOnly(script)) w.AddWatchOnly(script, ts);
+            if (!success) { // the key was already in the wallet (reference: "success": false, no error)
+                result.pushKV("success", false);
+                response.push_back(result);
+                continue;
             }
-            if (dest.IsValid() && !internal) w.SetAddressBook(dest, label, "receive");
             nLowestTimestamp = std::min(nLowestTimestamp, ts);
             anySuccess = true;
             result.pushKV("success", true);
@@ -1322,12 +1389,7 @@ static UniValue importprunedfunds(const JSONRPCRequest& req) {
     const CTransactionRef tx = MakeTransactionRef(std::move(mtx));
     const std::vector<unsigned char> proof = ParseHex(req.params[1].get_str());
     CMerkleBlock mb;
-    try {
-        SpanReader r(proof.data(), proof.size(), SER_NETWORK, PROTOCOL_VERSION);
-        r >> mb;
-    } catch (const std::exception&) {
-        ThrowRPC(RPC_DESERIALIZATION_ERROR, "Proof decode failed");
-    }
+    if (!DecodeTxOutProof(proof, mb)) ThrowRPC(RPC_DESERIALIZATION_ERROR, "Proof decode failed");
     std::vector<uint256> vMatch;
     std::vector<unsigned int> vIndex;
     Chainstate& cs = *GetNode()->chainstate;
