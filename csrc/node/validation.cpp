@@ -1176,35 +1176,77 @@ void Chainstate::FlushStateToDisk() {
 }
 
 // ------------------------------------------------------------------ tip management
+namespace {
+// Reference validation.cpp:1770 WarningBitsConditionChecker: a version bit this node does not
+// set itself that a BIP9 window's threshold of blocks signals (begin 0, never times out).
+class WarningBitsConditionChecker : public AbstractThresholdConditionChecker {
+    int bit;
+    VersionBitsCache& vbcache;
+
+public:
+    WarningBitsConditionChecker(int bitIn, VersionBitsCache& c) : bit(bitIn), vbcache(c) {}
+    int64_t BeginTime(const Consensus::Params&) const override { return 0; }
+    int64_t EndTime(const Consensus::Params&) const override { return std::numeric_limits<int64_t>::max(); }
+    int Period(const Consensus::Params& p) const override { return p.nMinerConfirmationWindow; }
+    int Threshold(const Consensus::Params& p) const override { return p.nRuleChangeActivationThreshold; }
+    bool Condition(const CBlockIndex* pindex, const Consensus::Params& p) const override {
+        return (pindex->nVersion & VERSIONBITS_TOP_MASK) == VERSIONBITS_TOP_BITS && ((pindex->nVersion >> bit) & 1) != 0 &&
+               ((bcp::ComputeBlockVersion(pindex->pprev, p, vbcache) >> bit) & 1) == 0;
+    }
+};
+} // namespace
+
+// Reference validation.cpp:2348 UpdateTip: besides moving the tip, warn (and -alertnotify once)
+// about unknown rules: a versionbit that locked in / activated without this node knowing it, or
+// more than half of the last 100 blocks carrying bits this node would not set.
 void Chainstate::UpdateTip(CBlockIndex* pindexNew) {
     chainActive.SetTip(pindexNew);
     if (mempool) mempool->AddTransactionsUpdated(1);
     cvBlockChange.notify_all();
     std::string strWarning;
+    std::vector<std::string> warningMessages;
     if (!IsInitialBlockDownload()) {
-        int nUpgraded = 0;
         const CBlockIndex* pindex = chainActive.Tip();
+        for (int bit = 0; bit < VERSIONBITS_NUM_BITS; bit++) {
+            WarningBitsConditionChecker checker(bit, versionbitscache);
+            const ThresholdState state = checker.GetStateFor(pindex, params.GetConsensus(), warningcache[bit]);
+            if (state == THRESHOLD_ACTIVE) {
+                strWarning = strprintf("Warning: unknown new rules activated (versionbit %i)", bit);
+                if (!fUnknownRulesWarned) {
+                    AlertNotify(strWarning);
+                    fUnknownRulesWarned = true;
+                }
+            } else if (state == THRESHOLD_LOCKED_IN) {
+                warningMessages.push_back(strprintf("unknown new rules are about to activate (versionbit %i)", bit));
+            }
+        }
+        int nUpgraded = 0;
         for (int i = 0; i < 100 && pindex != nullptr; i++) {
             const int32_t nExpectedVersion = bcp::ComputeBlockVersion(pindex->pprev, params.GetConsensus(), versionbitscache);
             if (pindex->nVersion > VERSIONBITS_LAST_OLD_BLOCK_VERSION && (pindex->nVersion & ~nExpectedVersion) != 0)
                 ++nUpgraded;
             pindex = pindex->pprev;
         }
+        if (nUpgraded > 0) warningMessages.push_back(strprintf("%d of last 100 blocks have unexpected version", nUpgraded));
         if (nUpgraded > 100 / 2) {
             strWarning = "Warning: Unknown block versions being mined! It's possible unknown rules are in effect";
-            static bool fWarned = false;
-            if (!fWarned) {
+            if (!fUnknownRulesWarned) {
                 AlertNotify(strWarning);
-                fWarned = true;
+                fUnknownRulesWarned = true;
             }
         }
     }
-    bcp::SetMiscWarning(strWarning);
+    if (!strWarning.empty()) bcp::SetMiscWarning(strWarning);
     LogPrintf("UpdateTip: new best=%s height=%d version=0x%08x log2_work=%.8g tx=%lu date='%lld' cache=%.1fMiB(%utxo)\n",
               chainActive.Tip()->GetBlockHash().ToString().c_str(), chainActive.Height(), chainActive.Tip()->nVersion,
               std::log(chainActive.Tip()->nChainWork.getdouble()) / std::log(2.0),
               (unsigned long)chainActive.Tip()->nChainTx, (long long)chainActive.Tip()->GetBlockTime(),
               pcoinsTip->DynamicMemoryUsage() * (1.0 / (1 << 20)), pcoinsTip->GetCacheSize());
+    if (!warningMessages.empty()) {
+        std::string joined;
+        for (const auto& w : warningMessages) joined += (joined.empty() ? "" : ", ") + w;
+        LogPrintf("UpdateTip: warning='%s'\n", joined.c_str());
+    }
 }
 
 bool Chainstate::ReadBlock(CBlock& block, const CBlockIndex* pindex, bool checkPow) const {

@@ -307,6 +307,8 @@ private:
     std::unique_ptr<WorkerPool> pool;
     std::unique_ptr<CheckQueue> scriptQueue; // ConnectBlock script checks (reference CCheckQueue)
     VersionBitsCache versionbitscache;
+    ThresholdConditionCache warningcache[VERSIONBITS_NUM_BITS]; // unknown-versionbit tracking (cs_main)
+    bool fUnknownRulesWarned = false;
     CTxMemPool* mempool = nullptr;
 };
 

@@ -4,7 +4,8 @@
 python tools/ab_bench.py [--reps 3] [--steps 20] A.so B.so ...
 Each build is loaded through BCP_NATIVE_PATH (bitcoincashplus_amd/_native.py) in its own
 process; runs alternate A, B, A, B, ... so clock/thermal drift hits every build alike.
-Prints one JSON line per run and a median summary per build.
+Prints one JSON line per run and a summary per build: median, min, max and the relative
+spread ((max - min) / median), so a difference smaller than the spread is read as noise.
 """
 import argparse
 import json
@@ -38,7 +39,9 @@ def main():
             res[b].append(v["value"])
             print(json.dumps({"build": b, "rep": r, "value": v["value"], "ms_per_step": v["ms_per_step"],
                               "sol_per_nonce": v["config"]["solutions_per_nonce"]}), flush=True)
-    print(json.dumps({"median": {b: statistics.median(v) for b, v in res.items()}}))
+    summary = {b: {"median": statistics.median(v), "min": min(v), "max": max(v),
+                   "spread": (max(v) - min(v)) / statistics.median(v), "n": len(v)} for b, v in res.items()}
+    print(json.dumps({"median": {b: s["median"] for b, s in summary.items()}, "summary": summary}))
 
 
 if __name__ == "__main__":
