@@ -9,13 +9,18 @@ Scans csrc/ for GetArg / GetBoolArg / IsArgSet / GetArgs / SoftSet*Arg / ForceSe
 Parity: reference contrib/devtools/check-doc.py (same scan of the sources against the help
 strings, with a short allow-list of hidden options). Usage: check-doc.py [REPO_ROOT]; prints
 the undocumented options and exits 1 if there are any.
+
+With --reference it also walks contrib/devtools/reference_options.txt (every option the
+reference node reads or documents) and reports each one this tree neither reads nor
+documents, apart from REFERENCE_NOT_APPLICABLE (the Qt GUI's own switches: this node's GUI is
+the browser wallet, see -webgui).
 """
 import os
 import re
 import subprocess
 import sys
 
-USE = re.compile(r'(?:GetArg|GetBoolArg|IsArgSet|GetArgs|SoftSetArg|SoftSetBoolArg|ForceSetArg|ClearArg)'
+USE = re.compile(r'(?:GetArg|GetBoolArg|IsArgSet|GetArgs|SoftSetArg|SoftSetBoolArg|ForceSetArg|ClearArg|ParseFeeArg)'
                  r'\(\s*(?:std::string\()?\s*"(-[a-zA-Z0-9][a-zA-Z0-9_.-]*)"')
 HELP = re.compile(r"^\s*(-[a-zA-Z0-9][a-zA-Z0-9_.-]*)", re.M)
 USAGE = re.compile(r"(?<![\w-])(-[a-zA-Z][a-zA-Z0-9_.-]*)")  # options inlined in a Usage: line
@@ -25,7 +30,11 @@ UNDOCUMENTED = {
     "-gpufaultinjection", "-dropmessagestest", "-fuzzmessagestest", "-mocktime", "-stopafterblockimport",
     "-checkblockindex", "-checkmempool", "-limitfreerelay", "-relaypriority", "-datadir", "-conf", "-help",
     "-version", "-?", "-h", "-regtest", "-testnet", "-fastprune", "-banscore",
+    # obsolete options, read only to refuse them or warn (reference init.cpp:1336-1358)
+    "-benchmark", "-blockminsize", "-debugnet", "-rpcssl", "-socks", "-tor", "-whitelistalwaysrelay",
 }
+# reference options with no counterpart here: the Qt wallet's startup switches
+REFERENCE_NOT_APPLICABLE = {"-choosedatadir", "-lang", "-min", "-resetguisettings", "-splash", "-uiplatform"}
 
 
 def used_options(root):
@@ -48,7 +57,7 @@ def documented(root):
         exe = os.path.join(root, "bin", prog)
         if not os.path.exists(exe):
             continue
-        r = subprocess.run([exe, "-help"], capture_output=True, text=True, timeout=60)
+        r = subprocess.run([exe, "-help", "-help-debug"], capture_output=True, text=True, timeout=60)
         text = r.stdout + r.stderr
         for m in HELP.finditer(text):
             doc.add(m.group(1).split("=")[0].split("<")[0])
@@ -59,7 +68,18 @@ def documented(root):
     return doc
 
 
+def reference_options(root):
+    out = {}
+    for line in open(os.path.join(root, "contrib", "devtools", "reference_options.txt")):
+        if line.strip() and not line.startswith("#"):
+            name, where = line.split()
+            out[name] = where
+    return out
+
+
 def main(argv):
+    check_ref = "--reference" in argv
+    argv = [a for a in argv if a != "--reference"]
     root = argv[0] if argv else os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     used = used_options(root)
     doc = documented(root)
@@ -67,7 +87,15 @@ def main(argv):
     for o in missing:
         print(f"undocumented option {o} (read in {used[o]})")
     print(f"{len(used)} options read, {len(doc)} documented, {len(missing)} undocumented")
-    return 1 if missing else 0
+    bad = len(missing)
+    if check_ref:
+        ref = reference_options(root)
+        absent = sorted(o for o in ref if o not in used and o not in doc and o not in REFERENCE_NOT_APPLICABLE)
+        for o in absent:
+            print(f"reference option {o} (read in {ref[o]}) is neither read nor documented here")
+        print(f"{len(ref)} reference options, {len(absent)} missing")
+        bad += len(absent)
+    return 1 if bad else 0
 
 
 if __name__ == "__main__":

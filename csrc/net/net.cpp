@@ -339,6 +339,7 @@ bool CConnman::Start(Scheduler* scheduler, const Options& o, std::string& err) {
     vConnect = o.vConnect;
     fConnectOnly = o.fConnectOnly;
     fDNSSeed = o.fDNSSeed;
+    fForceDNSSeed = o.fForceDNSSeed;
     datadir = o.datadir;
     {
         std::lock_guard<Mutex> l(cs_vOneShots);
@@ -532,7 +533,7 @@ CNode* CConnman::ConnectNode(CAddress addrConnect, const char* pszDest) {
     } else {
         if (pszDest) {
             std::vector<CService> resolved;
-            if (Lookup(pszDest, resolved, Params().GetDefaultPort(), true, 256) && !resolved.empty()) {
+            if (Lookup(pszDest, resolved, Params().GetDefaultPort(), fNameLookup, 256) && !resolved.empty()) {
                 addrConnect = CAddress(resolved[GetRand(resolved.size())], NODE_NONE);
                 if (!addrConnect.IsValid()) return nullptr;
                 std::lock_guard<CCriticalSection> l(cs_vNodes);
@@ -1145,9 +1146,10 @@ std::vector<CAddress> ConvertSeed6(const std::vector<SeedSpec6>& seeds) {
 }
 
 void CConnman::ThreadDNSAddressSeed() {
-    // only query DNS seeds when the address book is thin (reference net.cpp:1582)
+    // only query DNS seeds when the address book is thin, unless -forcednsseed (reference
+    // net.cpp:1582-1660)
     if (!InterruptibleSleep(11000)) return;
-    if (addrman.size() > 0) {
+    if (addrman.size() > 0 && !fForceDNSSeed) {
         std::lock_guard<CCriticalSection> l(cs_vNodes);
         int n = 0;
         for (CNode* p : vNodes) n += (p->fSuccessfullyConnected && !p->fOneShot && !p->fFeeler && !p->fInbound);

@@ -278,6 +278,7 @@ public:
         bool fListen = true;
         bool fDefaultBinds = false; // wildcard binds: succeed if any family binds
         bool fDNSSeed = true;
+        bool fForceDNSSeed = false; // -forcednsseed: query the seeds even with a full address book
         std::string datadir;
     };
 
@@ -398,6 +399,7 @@ private:
     std::vector<std::string> vConnect;
     bool fConnectOnly = false;
     bool fDNSSeed = true;
+    bool fForceDNSSeed = false;
     std::vector<CSubNet> vWhitelistedRange;
     mutable CCriticalSection cs_vNodes{"cs_vNodes"};
     std::vector<CNode*> vNodes GUARDED_BY(cs_vNodes);

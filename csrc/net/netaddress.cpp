@@ -300,6 +300,8 @@ void SplitHostPort(const std::string& in, int& portOut, std::string& hostOut) {
     if (hostOut.size() > 0 && hostOut[0] == '[' && hostOut.back() == ']') hostOut = hostOut.substr(1, hostOut.size() - 2);
 }
 
+bool fNameLookup = true;
+
 bool LookupHost(const std::string& name, std::vector<CNetAddr>& out, unsigned maxSolutions, bool fAllowLookup) {
     std::string host = name;
     if (host.empty()) return false;

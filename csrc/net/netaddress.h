@@ -144,6 +144,8 @@ private:
     bool valid = false;
 };
 
+// -dns: allow DNS lookups for -addnode, -seednode and -connect (reference netbase.cpp fNameLookup).
+extern bool fNameLookup;
 // Name resolution (numeric only when fAllowLookup is false).
 bool LookupHost(const std::string& name, std::vector<CNetAddr>& out, unsigned maxSolutions, bool fAllowLookup);
 bool LookupHost(const std::string& name, CNetAddr& out, bool fAllowLookup);

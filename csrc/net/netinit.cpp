@@ -32,7 +32,11 @@ std::string NetHelp() {
         {"-bind=<addr>", "Bind to given address and always listen on it"},
         {"-connect=<ip>", "Connect only to the specified node(s); -connect=0 disables automatic connections"},
         {"-discover", "Discover own IP addresses (default: 1 when listening and no -externalip)"},
-        {"-dnsseed", "Query for peer addresses via DNS lookup if low on addresses (default: 1)"},
+        {"-dns", "Allow DNS lookups for -addnode, -seednode and -connect (default: 1)"},
+        {"-dnsseed", "Query for peer addresses via DNS lookup, if low on addresses (default: 1 unless -connect)"},
+        {"-forcednsseed", "Always query for peer addresses via DNS lookup (default: 0)"},
+        {"-maxreceivebuffer=<n>", "Maximum per-connection receive buffer, <n>*1000 bytes (default: 5000)"},
+        {"-maxsendbuffer=<n>", "Maximum per-connection send buffer, <n>*1000 bytes (default: 1000)"},
         {"-externalip=<ip>", "Specify your own public address"},
         {"-listen", "Accept connections from outside (default: 1 if no -connect)"},
         {"-maxconnections=<n>", "Maintain at most <n> connections to peers (default: 125)"},
@@ -130,7 +134,12 @@ bool StartNetwork(NodeContext& node, std::string& err) {
     o.fListen = fListen;
     fDiscover = gArgs.GetBoolArg("-discover", fListen && !gArgs.IsArgSet("-externalip"));
     o.fDNSSeed = gArgs.GetBoolArg("-dnsseed", !o.fConnectOnly && !gArgs.IsArgSet("-seednode"));
+    o.fForceDNSSeed = gArgs.GetBoolArg("-forcednsseed", false);
     o.vSeedNodes = gArgs.GetArgs("-seednode");
+    fNameLookup = gArgs.GetBoolArg("-dns", true);
+    // per-connection buffers in kB (reference init.cpp:2205-2207)
+    o.nSendBufferMaxSize = 1000 * (size_t)std::max<int64_t>(gArgs.GetArg("-maxsendbuffer", (int64_t)1000), 0);
+    o.nReceiveFloodSize = 1000 * (size_t)std::max<int64_t>(gArgs.GetArg("-maxreceivebuffer", (int64_t)5000), 0);
     o.nMaxConnections = (int)gArgs.GetArg("-maxconnections", (int64_t)DEFAULT_MAX_PEER_CONNECTIONS);
     o.nLocalServices = NODE_NETWORK;
     if (gArgs.GetBoolArg("-peerbloomfilters", true)) o.nLocalServices |= NODE_BLOOM;

@@ -21,8 +21,10 @@
 #include <execinfo.h>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <fcntl.h>
 #include <sys/file.h>
+#include <sys/stat.h>
 #include <unistd.h>
 
 namespace bcp {
@@ -56,7 +58,6 @@ std::string HelpMessage() {
         {"-gpushortidthreshold=<n>", "Smallest mempool whose compact-block short ids are computed on the GPU (default: 16384)"},
         {"-gpudevices=<list>", "Comma-separated GPU indices the built-in Equihash miner runs on, one host thread per device (default: all visible)"},
         {"-gpuvalidationdevices=<list>", "Comma-separated GPU indices that verify block signatures and header solutions, one high-priority stream and service thread each; batches are sharded across them. When set, the built-in miner leaves these devices alone if others are available (default: device 0, shared with the miner)"},
-        {"-gpufaultinjection", "(testing) make every validation GPU batch fail so the CPU fallback runs (default: 0)"},
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
         {"-blocknotify=<cmd>", "Execute command when the best block changes (%s in cmd is replaced by block hash)"},
@@ -79,8 +80,12 @@ std::string HelpMessage() {
         {"-blockprioritypercentage=<n>", "Set maximum percentage of a block reserved to high-priority transactions (default: 5)"},
         {"-blockmintxfee=<amt>", "Set lowest fee rate (BCP/kB) for transactions to be included in block creation"},
         {"-minrelaytxfee=<amt>", "Fees (BCP/kB) smaller than this are considered zero fee for relaying (default: 0.00001)"},
-        {"-limitfreerelay=<n>", "Continuously rate-limit free transactions to <n>*1000 bytes per minute"},
-        {"-relaypriority", "Require high priority for relaying free or low-fee transactions (default: 1)"},
+        {"-dustrelayfee=<amt>", "Fee rate (BCP/kB) used to define dust, the value of an output such that it will cost about 1/3 of its value in fees at this fee rate to spend it (default: 0.00001)"},
+        {"-incrementalrelayfee=<amt>", "Fee rate (BCP/kB) used to define cost of relay, used for mempool limiting and BIP 125 replacement (default: 0.00001)"},
+        {"-zmqpubhashblock=<address>", "Enable publish hash block in <address>"},
+        {"-zmqpubhashtx=<address>", "Enable publish hash transaction in <address>"},
+        {"-zmqpubrawblock=<address>", "Enable publish raw block in <address>"},
+        {"-zmqpubrawtx=<address>", "Enable publish raw transaction in <address>"},
         {"-datacarrier", "Relay and mine data carrier transactions (default: 1)"},
         {"-datacarriersize=<n>", "Maximum size of data in data carrier transactions (default: 83)"},
         {"-permitbaremultisig", "Relay non-P2SH multisig (default: 1)"},
@@ -102,11 +107,9 @@ std::string HelpMessage() {
         {"-logtimemicros", "Add microsecond precision to debug timestamps (default: 0)"},
         {"-logips", "Include IP addresses in debug output (default: 0)"},
         {"-shrinkdebugfile", "Shrink debug.log file on client startup (default: 1)"},
-        {"-checkblockindex", "Do a full consistency check of the block index (regtest default)"},
         {"-fastprune", "Use 64 KiB block files (regtest only; for pruning tests)"},
         {"-connectpipeline=<n>", "Blocks in flight when connecting several in a row: block N+1's UTXO pass overlaps "
                                  "block N's signature batch (default: 2; 1 = one block at a time)"},
-        {"-checkmempool=<n>", "Run checks every <n> transactions"},
         {"-acceptnonstdtxn", "Relay and mine \"non-standard\" transactions (default: 0 on main, 1 on the test chains)"},
         {"-assumevalid=<hex>", "If this block is in the chain assume that it and its ancestors are valid and potentially skip their script verification (0 to verify all)"},
         {"-bytespersigop=<n>", "Equivalent bytes per sigop in transactions for relay and mining (default: 20)"},
@@ -123,8 +126,30 @@ std::string HelpMessage() {
         {"-maxtxfee=<amt>", "Maximum total fees (in BCP) to use in a single wallet transaction or raw transaction (default: 0.1)"},
         {"-promiscuousmempoolflags=<n>", "Script verification flags for mempool acceptance (testing only)"},
         {"-blockversion=<n>", "Override block version to test forking scenarios (regtest)"},
+        {"-sysperms", "Create new files with system default permissions, instead of umask 077 (only effective with disabled wallet functionality)"},
+        {"-rpccookiefile=<loc>", "Location of the auth cookie (default: data dir)"},
+        {"-rpcworkqueue=<n>", "Set the depth of the work queue to service RPC calls (default: 16)"},
+        {"-help-debug", "Show all debugging options (usage: --help -help-debug)"},
+        {"-nodebug", "Turn off debugging messages, same as -debug=0"},
     };
     for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);
+    // debug-only options, shown with -help-debug (reference init.cpp:306 showDebug)
+    if (gArgs.GetBoolArg("-help-debug", false)) {
+        const std::pair<const char*, const char*> dbg[] = {
+            {"-mocktime=<n>", "Replace actual time with <n> seconds since epoch (default: 0)"},
+            {"-stopafterblockimport", "Stop running after importing blocks from disk (default: 0)"},
+            {"-printpriority", "Log transaction priority and fee per kB when mining blocks (default: 0)"},
+            {"-limitfreerelay=<n>", "Continuously rate-limit free transactions to <n>*1000 bytes per minute (default: 0)"},
+            {"-relaypriority", "Require high priority for relaying free or low-fee transactions (default: 1)"},
+            {"-checkblockindex", "Do a full consistency check for mapBlockIndex, setBlockIndexCandidates, chainActive and mapBlocksUnlinked occasionally (default: 1 on regtest)"},
+            {"-checkmempool=<n>", "Run checks every <n> transactions (default: 1 on regtest)"},
+            {"-dropmessagestest=<n>", "Randomly drop 1 of every <n> network messages"},
+            {"-fuzzmessagestest=<n>", "Randomly fuzz 1 of every <n> network messages"},
+            {"-gpufaultinjection", "Make every validation GPU batch fail so the CPU fallback runs (default: 0)"},
+        };
+        s += "\nDebugging/Testing options:\n";
+        for (const auto& o : dbg) s += strprintf("  %-32s %s\n", o.first, o.second);
+    }
     s += NetHelp();
     s += WalletHelp();
     return s;
@@ -190,6 +215,8 @@ int AppMain(int argc, char* argv[]) {
         return 1;
     }
     SelectParams(chain);
+    // new files private unless -sysperms (reference init.cpp:1244); the wallet refuses -sysperms
+    if (!gArgs.GetBoolArg("-sysperms", false)) umask(077);
     // -bip9params=deployment:start:end, regtest only (reference chainparams.cpp:474
     // UpdateRegtestBIP9Parameters + init.cpp parsing)
     for (const std::string& p : gArgs.GetArgs("-bip9params")) {
@@ -248,8 +275,13 @@ int AppMain(int argc, char* argv[]) {
     LogInit(console ? "" : datadir + "/debug.log", console, gArgs.GetBoolArg("-logtimestamps", true));
     LogSetTimeMicros(gArgs.GetBoolArg("-logtimemicros", false));
     fLogIPs = gArgs.GetBoolArg("-logips", false);
-    for (const std::string& c : gArgs.GetArgs("-debug"))
-        if (!LogEnableCategory(c)) LogPrintf("Unsupported logging category -debug=%s.\n", c.c_str());
+    {
+        // -debug=0 / -nodebug turn debugging off (reference init.cpp:1327-1334)
+        const std::vector<std::string> cats = gArgs.GetArgs("-debug");
+        if (!gArgs.GetBoolArg("-nodebug", false) && std::find(cats.begin(), cats.end(), "0") == cats.end())
+            for (const std::string& c : cats)
+                if (!LogEnableCategory(c)) LogPrintf("Unsupported logging category -debug=%s.\n", c.c_str());
+    }
     for (const std::string& c : gArgs.GetArgs("-debugexclude")) LogDisableCategory(c);
     LogPrintf("\n\n\n\n\n");
     LogPrintf("%s version %s (MI355X)\n", CLIENT_NAME, FormatFullVersion().c_str());
@@ -280,6 +312,28 @@ int AppMain(int argc, char* argv[]) {
         sa.sa_flags = SA_ONSTACK;
         for (int sig : {SIGSEGV, SIGABRT, SIGBUS, SIGFPE}) sigaction(sig, &sa, nullptr);
     }
+
+    // obsolete options (reference init.cpp:1336-1358)
+    if (gArgs.GetBoolArg("-debugnet", false)) InitWarning("Unsupported argument -debugnet ignored, use -debug=net.");
+    if (gArgs.IsArgSet("-socks")) {
+        InitError("Unsupported argument -socks found. Setting SOCKS version isn't possible anymore, only SOCKS5 proxies are "
+                  "supported.");
+        return 1;
+    }
+    if (gArgs.GetBoolArg("-tor", false)) {
+        InitError("Unsupported argument -tor found, use -onion.");
+        return 1;
+    }
+    if (gArgs.GetBoolArg("-benchmark", false)) InitWarning("Unsupported argument -benchmark ignored, use -debug=bench.");
+    if (gArgs.GetBoolArg("-whitelistalwaysrelay", false))
+        InitWarning("Unsupported argument -whitelistalwaysrelay ignored, use -whitelistrelay and/or -whitelistforcerelay.");
+    if (gArgs.IsArgSet("-blockminsize")) InitWarning("Unsupported argument -blockminsize ignored.");
+    if (gArgs.GetBoolArg("-rpcssl", false)) {
+        InitError("SSL mode for RPC (-rpcssl) is no longer supported.");
+        return 1;
+    }
+    // regression tests start with a fixed clock (reference init.cpp:1522)
+    SetMockTime(gArgs.GetArg("-mocktime", 0));
 
     // ---- parameter interaction (policy globals)
     const CChainParams& params = Params();
@@ -369,6 +423,8 @@ int AppMain(int argc, char* argv[]) {
         }
         ho.threads = (int)gArgs.GetArg("-rpcthreads", (int64_t)4);
         ho.timeoutSeconds = (int)gArgs.GetArg("-rpcservertimeout", (int64_t)30);
+        ho.workQueueDepth = (int)std::max<int64_t>(gArgs.GetArg("-rpcworkqueue", (int64_t)16), 1);
+        LogPrintf("HTTP: creating work queue of depth %d\n", ho.workQueueDepth);
         http.reset(new HTTPServer(ho));
         std::string err;
         if (!http->Start(err)) {
@@ -453,6 +509,10 @@ int AppMain(int argc, char* argv[]) {
             CValidationState state;
             cs->ActivateBestChain(state);
             LogPrintf("Block import finished\n");
+            if (gArgs.GetBoolArg("-stopafterblockimport", false)) { // reference init.cpp:1039
+                LogPrintf("Stopping after block import\n");
+                RequestShutdown();
+            }
         });
     }
     uiInterface.InitMessage("Loading wallet...");

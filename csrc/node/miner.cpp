@@ -59,6 +59,7 @@ int64_t UpdateTime(CBlockHeader* pblock, const Consensus::Params& params, const 
 BlockAssembler::BlockAssembler(Chainstate& cs, CTxMemPool* mp, const Options& o) : chainstate(cs), mempool(mp), options(o) {
     nMaxGeneratedBlockSize = std::max<uint64_t>(1000, std::min<uint64_t>(chainstate.MaxBlockSize() - 1000,
                                                                           options.nMaxGeneratedBlockSize));
+    fPrintPriority = gArgs.GetBoolArg("-printpriority", false);
 }
 
 void BlockAssembler::resetBlock() {
@@ -77,15 +78,23 @@ bool BlockAssembler::TestTxForBlock(const CTransaction& tx, uint64_t size, int64
     return true;
 }
 
-void BlockAssembler::AddToBlock(const CTransactionRef& tx, Amount fee, int64_t sigops) {
+void BlockAssembler::AddToBlock(const CTxMemPoolEntry& e) {
+    const CTransactionRef& tx = e.GetSharedTx();
     pblock->vtx.push_back(tx);
-    pblocktemplate->vTxFees.push_back(fee);
-    pblocktemplate->vTxSigOpsCount.push_back(sigops);
+    pblocktemplate->vTxFees.push_back(e.GetFee());
+    pblocktemplate->vTxSigOpsCount.push_back(e.GetSigOpCount());
     nBlockSize += tx->GetTotalSize();
     ++nBlockTx;
-    nBlockSigOps += sigops;
-    nFees += fee;
+    nBlockSigOps += e.GetSigOpCount();
+    nFees += e.GetFee();
     inBlock.insert(tx->GetHash());
+    if (fPrintPriority) { // reference miner.cpp:362-371
+        double dPriority = e.GetPriority(nHeight);
+        Amount dummy = 0;
+        mempool->ApplyDeltas(tx->GetHash(), dPriority, dummy);
+        LogPrintf("priority %.1f fee %s txid %s\n", dPriority, CFeeRate(e.GetModifiedFee(), e.GetTxSize()).ToString().c_str(),
+                  tx->GetHash().ToString().c_str());
+    }
 }
 
 void BlockAssembler::addPriorityTxs() {
@@ -116,7 +125,7 @@ void BlockAssembler::addPriorityTxs() {
                 if (mempool->exists(in.prevout.hash) && !inBlock.count(in.prevout.hash)) dependent = true;
             if (dependent) continue;
             if (!TestTxForBlock(e->GetTx(), e->GetTxSize(), e->GetSigOpCount())) continue;
-            AddToBlock(e->GetSharedTx(), e->GetFee(), e->GetSigOpCount());
+            AddToBlock(*e);
             progress = true;
             if (nBlockSize >= nBlockPrioritySize) return;
         }
@@ -161,7 +170,7 @@ void BlockAssembler::addPackageTxs() {
                 return a->GetCountWithAncestors() < b->GetCountWithAncestors();
             return a->GetTx().GetHash() < b->GetTx().GetHash();
         });
-        for (const CTxMemPoolEntry* p : pkg) AddToBlock(p->GetSharedTx(), p->GetFee(), p->GetSigOpCount());
+        for (const CTxMemPoolEntry* p : pkg) AddToBlock(*p);
         nConsecutiveFailed = 0;
     }
 }

@@ -21,6 +21,7 @@
 namespace bcp {
 
 class CTxMemPool;
+class CTxMemPoolEntry;
 
 struct CBlockTemplate {
     CBlock block;
@@ -45,7 +46,7 @@ public:
 
 private:
     void resetBlock();
-    void AddToBlock(const CTransactionRef& tx, Amount fee, int64_t sigops);
+    void AddToBlock(const CTxMemPoolEntry& e);
     bool TestTxForBlock(const CTransaction& tx, uint64_t size, int64_t sigops) const;
     void addPriorityTxs();
     void addPackageTxs();
@@ -61,6 +62,7 @@ private:
     int nHeight = 0;
     int64_t nLockTimeCutoff = 0;
     uint64_t nMaxGeneratedBlockSize = 0;
+    bool fPrintPriority = false; // -printpriority
     static uint64_t nLastBlockTx, nLastBlockSize;
 };
 

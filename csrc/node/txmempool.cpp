@@ -569,6 +569,13 @@ std::map<uint256, std::pair<double, Amount>> CTxMemPool::GetDeltas() const {
     return mapDeltas;
 }
 
+bool CTxMemPool::TransactionWithinChainLimit(const uint256& txid, size_t chainLimit) const {
+    std::lock_guard<CCriticalSection> l(cs);
+    auto it = mapTx.find(txid);
+    return it == mapTx.end() ||
+           (it->second->GetCountWithAncestors() < chainLimit && it->second->GetCountWithDescendants() < chainLimit);
+}
+
 bool CTxMemPool::exists(const uint256& hash) const {
     std::lock_guard<CCriticalSection> l(cs);
     return mapTx.count(hash) > 0;

@@ -181,6 +181,9 @@ public:
     std::map<uint256, std::pair<double, Amount>> GetDeltas() const;
 
     bool exists(const uint256& hash) const;
+    // true unless the transaction is in the pool with chainLimit or more ancestors or
+    // descendants (reference txmempool.cpp TransactionWithinChainLimit)
+    bool TransactionWithinChainLimit(const uint256& txid, size_t chainLimit) const;
     CTransactionRef get(const uint256& hash) const;
     const CTxMemPoolEntry* GetEntry(const uint256& hash) const;
     TxMempoolInfo info(const uint256& hash) const;

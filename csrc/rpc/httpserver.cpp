@@ -250,13 +250,24 @@ void HTTPServer::ServeConnection(int fd, std::string peer) {
         const std::string conn = ToLower(req.Header("connection"));
         keepAlive = req.version == "HTTP/1.1" ? conn != "close" : conn == "keep-alive";
         HTTPReply rep;
-        try {
-            Dispatch(req, rep);
-        } catch (const std::exception& e) {
+        // work queue (reference httpserver.cpp:268-280): -rpcthreads requests run, up to
+        // -rpcworkqueue more may wait; anything beyond is answered 500 at once
+        if (inFlight.fetch_add(1) >= opts.threads + std::max(opts.workQueueDepth, 1)) {
+            LogPrintf("WARNING: request rejected because http work queue depth exceeded, it can be increased with "
+                      "the -rpcworkqueue= setting\n");
             rep.status = 500;
             rep.contentType = "text/plain";
-            rep.body = e.what();
+            rep.body = "Work queue depth exceeded";
+        } else {
+            try {
+                Dispatch(req, rep);
+            } catch (const std::exception& e) {
+                rep.status = 500;
+                rep.contentType = "text/plain";
+                rep.body = e.what();
+            }
         }
+        inFlight.fetch_sub(1);
         std::string out = strprintf("HTTP/1.1 %d %s\r\n", rep.status, StatusText(rep.status));
         out += "Content-Type: " + rep.contentType + "\r\n";
         out += strprintf("Content-Length: %zu\r\n", rep.body.size());

@@ -45,6 +45,7 @@ public:
         int threads = 4;
         int timeoutSeconds = 30;
         int maxConnections = 128;
+        int workQueueDepth = 16; // -rpcworkqueue: requests waiting beyond the -rpcthreads running ones
     };
     explicit HTTPServer(const Options& opts);
     ~HTTPServer();
@@ -58,6 +59,7 @@ private:
     void AcceptLoop(int fd);
     void ServeConnection(int fd, std::string peer);
     bool Allowed(const std::string& peer) const;
+    std::atomic<int> inFlight{0}; // requests being dispatched
     bool Dispatch(const HTTPRequest& req, HTTPReply& rep);
 
     Options opts;

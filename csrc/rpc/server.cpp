@@ -340,12 +340,18 @@ UniValue RPCConvertNamedValues(const std::string& strMethod, const std::vector<s
 static const char* const COOKIEAUTH_USER = "__cookie__";
 static const char* const COOKIEAUTH_FILE = ".cookie";
 
+// -rpccookiefile: an absolute path, or one relative to the data directory (reference
+// src/rpc/protocol.cpp:67 GetAuthCookieFile).
+static std::string AuthCookieFile(const std::string& datadir) {
+    const std::string f = gArgs.GetArg("-rpccookiefile", COOKIEAUTH_FILE);
+    return !f.empty() && f[0] == '/' ? f : datadir + "/" + f;
+}
+
 bool GenerateAuthCookie(const std::string& datadir, std::string* cookie_out) {
     unsigned char rand_pwd[32];
     GetRandBytes(rand_pwd, 32);
     const std::string cookie = std::string(COOKIEAUTH_USER) + ":" + HexStr(rand_pwd, rand_pwd + 32);
-    const std::string path = datadir + "/" + COOKIEAUTH_FILE;
-    std::ofstream file(path.c_str(), std::ios::out | std::ios::trunc);
+    std::ofstream file(AuthCookieFile(datadir).c_str(), std::ios::out | std::ios::trunc);
     if (!file.is_open()) return false;
     file << cookie;
     file.close();
@@ -353,13 +359,13 @@ bool GenerateAuthCookie(const std::string& datadir, std::string* cookie_out) {
     return true;
 }
 bool GetAuthCookie(const std::string& datadir, std::string* cookie_out) {
-    std::ifstream file((datadir + "/" + COOKIEAUTH_FILE).c_str());
+    std::ifstream file(AuthCookieFile(datadir).c_str());
     if (!file.is_open()) return false;
     std::string cookie;
     std::getline(file, cookie);
     if (cookie_out) *cookie_out = cookie;
     return true;
 }
-void DeleteAuthCookie(const std::string& datadir) { RemoveFile(datadir + "/" + COOKIEAUTH_FILE); }
+void DeleteAuthCookie(const std::string& datadir) { RemoveFile(AuthCookieFile(datadir)); }
 
 } // namespace bcp

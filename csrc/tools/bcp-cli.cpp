@@ -56,6 +56,10 @@ int main(int argc, char* argv[]) {
         return 1;
     }
     SelectParams(chain);
+    if (gArgs.GetBoolArg("-rpcssl", false)) { // reference src/bitcoin-cli.cpp:143
+        fprintf(stderr, "Error: SSL mode for RPC (-rpcssl) is no longer supported.\n");
+        return 1;
+    }
 
     std::vector<std::string> args(argv + first, argv + argc);
     if (gArgs.GetBoolArg("-stdin", false)) {

@@ -349,7 +349,7 @@ static void CoinSelection(State& st) {
     while (st.KeepRunning()) {
         std::set<std::pair<const CWalletTx*, unsigned int>> setCoinsRet;
         Amount nValueRet;
-        const bool ok = wallet.SelectCoinsMinConf(1003 * 100000000LL, 1, 6, vCoins, setCoinsRet, nValueRet);
+        const bool ok = wallet.SelectCoinsMinConf(1003 * 100000000LL, 1, 6, 0, vCoins, setCoinsRet, nValueRet);
         if (!ok || nValueRet != 1003 * 100000000LL || setCoinsRet.size() != 2) exit(1);
     }
 }

@@ -851,7 +851,7 @@ static UniValue getwalletinfo(const JSONRPCRequest& req) {
     WalletLock l(w);
     UniValue obj(UniValue::VOBJ);
     obj.pushKV("walletname", w.GetName());
-    obj.pushKV("walletversion", WALLET_FEATURE_LATEST);
+    obj.pushKV("walletversion", w.GetVersion());
     obj.pushKV("balance", ValueFromAmount(w.GetBalance()));
     obj.pushKV("unconfirmed_balance", ValueFromAmount(w.GetUnconfirmedBalance()));
     obj.pushKV("immature_balance", ValueFromAmount(w.GetImmatureBalance()));

@@ -255,8 +255,16 @@ void CReserveKey::ReturnKey() {
 }
 
 // ------------------------------------------------------------------ CWallet
+// -dblogsize: megabytes of wallet writes kept in the store's log before they are written out as
+// a segment (the reference's Berkeley DB log size, wallet/db.cpp:319)
+static KVOptions WalletStoreOptions() {
+    KVOptions o;
+    o.memtableBytes = (size_t)std::max<int64_t>(1, gArgs.GetArg("-dblogsize", (int64_t)100)) << 20;
+    return o;
+}
+
 CWallet::CWallet(const std::string& name, const std::string& path, bool memoryOnly)
-    : strWalletName(name), db(new KVStore(path, memoryOnly)) {
+    : strWalletName(name), db(new KVStore(path, memoryOnly, false, WalletStoreOptions())) {
     std::lock_guard<std::mutex> l(cs_wallets);
     g_wallets.push_back(this);
 }
@@ -267,6 +275,22 @@ CWallet::~CWallet() {
 }
 
 void CWallet::Flush() { db->Write(std::string("orderposnext"), nOrderPosNext, true); }
+
+void CWallet::FlushIfDirty() {
+    WalletLock l(*this);
+    const uint64_t b = db->LogBytes();
+    if (b == nLastFlushBytes) return;
+    Flush();
+    nLastFlushBytes = db->LogBytes();
+}
+
+void CWallet::SetMinVersion(int v) {
+    WalletLock l(*this);
+    if (nWalletVersion >= v) return;
+    nWalletVersion = v;
+    if (v > nWalletMaxVersion) nWalletMaxVersion = v;
+    db->Write(std::string("minversion"), v, true);
+}
 
 bool CWallet::Load(std::string& err, bool& firstRun) {
     WalletLock l(*this);
@@ -364,6 +388,13 @@ bool CWallet::Load(std::string& err, bool& firstRun) {
                 it.GetValue(vchDefaultKey);
             } else if (type == "orderposnext") {
                 it.GetValue(nOrderPosNext);
+            } else if (type == "minversion") {
+                it.GetValue(nWalletVersion);
+                if (nWalletVersion > CLIENT_VERSION) {
+                    err = "Error loading " + strWalletName + ": Wallet requires newer version of Bitcoin Cash Plus";
+                    return false;
+                }
+                nWalletMaxVersion = std::max(nWalletMaxVersion, nWalletVersion);
             } else if (type == "acentry") {
                 std::pair<std::string, uint64_t> k;
                 r >> k;
@@ -378,6 +409,7 @@ bool CWallet::Load(std::string& err, bool& firstRun) {
         }
     }
     for (const auto& kv : pendingCrypted) CCryptoKeyStore::AddCryptedKey(kv.first, kv.second);
+    if (nWalletVersion == 0) nWalletVersion = nWalletMaxVersion = WALLET_FEATURE_BASE;
     // order index and spend map
     for (auto& kv : mapWallet) {
         CWalletTx& wtx = kv.second;
@@ -627,6 +659,7 @@ bool CWallet::EncryptWallet(const std::string& passphrase) {
             b.Erase(K("key", kv.second.first));
         }
         db->WriteBatch(b, true);
+        SetMinVersion(WALLET_FEATURE_WALLETCRYPT);
         Lock();
         Unlock(passphrase);
         // fresh HD seed and key pool: the old ones were written unencrypted
@@ -1208,7 +1241,7 @@ static void ApproximateBestSubset(const std::vector<std::pair<Amount, std::pair<
     }
 }
 
-bool CWallet::SelectCoinsMinConf(Amount nTargetValue, int nConfMine, int nConfTheirs, std::vector<COutput> vCoins,
+bool CWallet::SelectCoinsMinConf(Amount nTargetValue, int nConfMine, int nConfTheirs, uint64_t nMaxAncestors, std::vector<COutput> vCoins,
                                  std::set<std::pair<const CWalletTx*, unsigned int>>& setCoinsRet,
                                  Amount& nValueRet) const {
     setCoinsRet.clear();
@@ -1222,6 +1255,7 @@ bool CWallet::SelectCoinsMinConf(Amount nTargetValue, int nConfMine, int nConfTh
         if (!o.fSpendable) continue;
         const CWalletTx* pcoin = o.tx;
         if (o.nDepth < (pcoin->IsFromMe(ISMINE_ALL) ? nConfMine : nConfTheirs)) continue;
+        if (mempool && !mempool->TransactionWithinChainLimit(pcoin->GetHash(), nMaxAncestors)) continue;
         const Amount n = pcoin->tx->vout[o.i].nValue;
         const ValuedCoin coin{n, {pcoin, (unsigned)o.i}};
         if (n == nTargetValue) {
@@ -1295,11 +1329,22 @@ bool CWallet::SelectCoins(const std::vector<COutput>& vAvailableCoins, Amount nT
         if (setPresetCoins.count({it->tx, (unsigned)it->i})) it = vCoins.erase(it);
         else ++it;
     }
+    // confirmed coins first, then unconfirmed change with ever longer mempool chains; beyond
+    // the mempool's chain limits only without -walletrejectlongchains (reference wallet.cpp:2513-2540)
     const Amount target = nTargetValue - nValueFromPresetInputs;
-    bool res = target <= 0 || SelectCoinsMinConf(target, 1, 6, vCoins, setCoinsRet, nValueRet) ||
-               SelectCoinsMinConf(target, 1, 1, vCoins, setCoinsRet, nValueRet) ||
-               (gArgs.GetBoolArg("-spendzeroconfchange", DEFAULT_SPEND_ZEROCONF_CHANGE) &&
-                SelectCoinsMinConf(target, 0, 1, vCoins, setCoinsRet, nValueRet));
+    const uint64_t nMaxChainLength = (uint64_t)std::min(gArgs.GetArg("-limitancestorcount", (int64_t)DEFAULT_ANCESTOR_LIMIT),
+                                                        gArgs.GetArg("-limitdescendantcount", (int64_t)DEFAULT_DESCENDANT_LIMIT));
+    const bool fRejectLongChains = gArgs.GetBoolArg("-walletrejectlongchains", DEFAULT_WALLET_REJECT_LONG_CHAINS);
+    const bool zc = gArgs.GetBoolArg("-spendzeroconfchange", DEFAULT_SPEND_ZEROCONF_CHANGE);
+    bool res = target <= 0 || SelectCoinsMinConf(target, 1, 6, 0, vCoins, setCoinsRet, nValueRet) ||
+               SelectCoinsMinConf(target, 1, 1, 0, vCoins, setCoinsRet, nValueRet) ||
+               (zc && SelectCoinsMinConf(target, 0, 1, 2, vCoins, setCoinsRet, nValueRet)) ||
+               (zc && SelectCoinsMinConf(target, 0, 1, std::min<uint64_t>(4, nMaxChainLength / 3), vCoins, setCoinsRet,
+                                         nValueRet)) ||
+               (zc && SelectCoinsMinConf(target, 0, 1, nMaxChainLength / 2, vCoins, setCoinsRet, nValueRet)) ||
+               (zc && SelectCoinsMinConf(target, 0, 1, nMaxChainLength, vCoins, setCoinsRet, nValueRet)) ||
+               (zc && !fRejectLongChains &&
+                SelectCoinsMinConf(target, 0, 1, std::numeric_limits<uint64_t>::max(), vCoins, setCoinsRet, nValueRet));
     setCoinsRet.insert(setPresetCoins.begin(), setPresetCoins.end());
     nValueRet += nValueFromPresetInputs;
     return res;
@@ -1460,6 +1505,29 @@ bool CWallet::CreateTransaction(const std::vector<CRecipient>& vecSend, CWalletT
             strFailReason = "Transaction too large";
             return false;
         }
+        // a small, old-coin transaction may go free (-sendfreetransactions; reference wallet.cpp:2889-2899)
+        if (fSendFreeTransactions && nBytes <= MAX_FREE_TRANSACTION_CREATE_SIZE && mempool) {
+            double dPriority = 0;
+            for (const auto& coin : setCoins)
+                dPriority += (double)coin.first->tx->vout[coin.second].nValue * coin.first->GetDepthInMainChain();
+            unsigned nModSize = nBytes;
+            for (const CTxIn& in : txNew.vin) {
+                const unsigned offset = 41U + std::min(110U, (unsigned)in.scriptSig.size());
+                if (nModSize > offset) nModSize -= offset;
+            }
+            dPriority = nModSize ? dPriority / nModSize : 0;
+            int found = 0;
+            // a mempool that is full enough to charge a minimum fee takes nothing free
+            // (reference txmempool.cpp estimateSmartPriority)
+            const size_t maxmempool = (size_t)gArgs.GetArg("-maxmempool", (int64_t)DEFAULT_MAX_MEMPOOL_SIZE) * 1000000;
+            const double dPriorityNeeded = mempool->GetMinFee(maxmempool).GetFeePerK() > 0 || !mempool->Estimator()
+                                               ? 1e16
+                                               : mempool->Estimator()->estimateSmartPriority((int)confTarget, &found);
+            if (dPriority >= dPriorityNeeded && AllowFree(dPriority)) {
+                wtxNew.tx = MakeTransactionRef(std::move(txNew));
+                break;
+            }
+        }
         Amount nFeeNeeded = GetMinimumFee(nBytes, confTarget);
         if (coinControl && coinControl->fOverrideFeeRate) nFeeNeeded = coinControl->nFeeRate.GetFee(nBytes);
         if (nFeeNeeded < minRelayTxFee.GetFee(nBytes)) {
@@ -1472,6 +1540,21 @@ bool CWallet::CreateTransaction(const std::vector<CRecipient>& vecSend, CWalletT
             break;
         }
         nFeeRet = nFeeNeeded;
+    }
+    if (gArgs.GetBoolArg("-walletrejectlongchains", DEFAULT_WALLET_REJECT_LONG_CHAINS) && mempool) {
+        // the transaction must pass the mempool's chain limits (reference wallet.cpp:3000-3025)
+        CTxMemPoolEntry entry(wtxNew.tx, 0, 0, 0.0, 0, 0, false, 0, LockPoints());
+        CTxMemPool::setEntries setAncestors;
+        std::string errString;
+        std::lock_guard<CCriticalSection> lmp(mempool->cs);
+        if (!mempool->CalculateMemPoolAncestors(
+                entry, setAncestors, (uint64_t)gArgs.GetArg("-limitancestorcount", (int64_t)DEFAULT_ANCESTOR_LIMIT),
+                (uint64_t)gArgs.GetArg("-limitancestorsize", (int64_t)DEFAULT_ANCESTOR_SIZE_LIMIT) * 1000,
+                (uint64_t)gArgs.GetArg("-limitdescendantcount", (int64_t)DEFAULT_DESCENDANT_LIMIT),
+                (uint64_t)gArgs.GetArg("-limitdescendantsize", (int64_t)DEFAULT_DESCENDANT_SIZE_LIMIT) * 1000, errString)) {
+            strFailReason = "Transaction has too long of a mempool chain";
+            return false;
+        }
     }
     return true;
 }

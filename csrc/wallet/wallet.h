@@ -42,8 +42,18 @@ static const Amount MIN_CHANGE = 1000000; // CENT
 static const Amount MIN_FINAL_CHANGE = MIN_CHANGE / 2;
 static const unsigned int DEFAULT_TX_CONFIRM_TARGET = 6;
 static const bool DEFAULT_SPEND_ZEROCONF_CHANGE = true;
+static const bool DEFAULT_SEND_FREE_TRANSACTIONS = false;
+static const bool DEFAULT_WALLET_REJECT_LONG_CHAINS = false;
+static const unsigned int MAX_FREE_TRANSACTION_CREATE_SIZE = 1000;
+static const bool DEFAULT_FLUSHWALLET = true;
 static const bool DEFAULT_WALLETBROADCAST = true;
-static const int WALLET_FEATURE_LATEST = 130000;
+// wallet format versions (reference wallet.h WalletFeature): a store records the lowest client
+// version that can open it ("minversion")
+static const int WALLET_FEATURE_BASE = 10500;
+static const int WALLET_FEATURE_WALLETCRYPT = 40000;
+static const int WALLET_FEATURE_COMPRPUBKEY = 60000;
+static const int WALLET_FEATURE_HD = 130000;
+static const int WALLET_FEATURE_LATEST = WALLET_FEATURE_COMPRPUBKEY; // HD is optional
 
 enum isminetype : uint8_t {
     ISMINE_NO = 0,
@@ -369,7 +379,7 @@ public:
     // ---- spending
     void AvailableCoins(std::vector<COutput>& vCoins, bool fOnlyConfirmed = true, const CCoinControl* coinControl = nullptr,
                         bool fIncludeZeroValue = false) const;
-    bool SelectCoinsMinConf(Amount nTargetValue, int nConfMine, int nConfTheirs, std::vector<COutput> vCoins,
+    bool SelectCoinsMinConf(Amount nTargetValue, int nConfMine, int nConfTheirs, uint64_t nMaxAncestors, std::vector<COutput> vCoins,
                             std::set<std::pair<const CWalletTx*, unsigned int>>& setCoinsRet, Amount& nValueRet) const;
     bool SelectCoins(const std::vector<COutput>& vAvailableCoins, Amount nTargetValue,
                      std::set<std::pair<const CWalletTx*, unsigned int>>& setCoinsRet, Amount& nValueRet,
@@ -408,6 +418,11 @@ public:
     CTxMemPool* mempool = nullptr;
     CFeeRate payTxFee{DEFAULT_TRANSACTION_FEE};
     unsigned int nTxConfirmTarget = DEFAULT_TX_CONFIRM_TARGET;
+    bool fSendFreeTransactions = DEFAULT_SEND_FREE_TRANSACTIONS; // -sendfreetransactions
+    int nWalletVersion = 0, nWalletMaxVersion = 0;                 // "minversion" record, -upgradewallet cap
+    void SetMinVersion(int v);
+    void FlushIfDirty(); // -flushwallet: fsync the store if anything was written since the last call
+    int GetVersion() const { return nWalletVersion; }
     bool fBroadcastTransactions = DEFAULT_WALLETBROADCAST;
     CPubKey vchDefaultKey;
     KVStore& DB() { return *db; }
@@ -419,6 +434,7 @@ private:
     CPubKey DeriveNewChildKey(CKeyMetadata& metadata, CKey& secret);
 
     std::string strWalletName;
+    uint64_t nLastFlushBytes = 0;
     std::unique_ptr<KVStore> db;
     std::map<unsigned int, CMasterKey> mapMasterKeys;
     unsigned int nMasterKeyMaxID = 0;

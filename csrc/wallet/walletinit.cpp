@@ -41,8 +41,20 @@ std::string WalletHelp() {
         {"-allowselfsignedrootcertificates", "Accept a self-signed merchant certificate in BIP70 payment requests (default: 0)"},
         {"-walletnotify=<cmd>", "Execute command when a wallet transaction changes (%s in cmd is replaced by TxID)"},
         {"-zapwallettxes", "Delete all wallet transactions and only recover those parts of the blockchain through -rescan on startup"},
+        {"-upgradewallet", "Upgrade wallet to latest format on startup"},
     };
     for (const auto& o : opts) s += strprintf("  %-32s %s\n", o.first, o.second);
+    if (gArgs.GetBoolArg("-help-debug", false)) {
+        const std::pair<const char*, const char*> dbg[] = {
+            {"-sendfreetransactions", "Send transactions as zero-fee transactions if possible (default: 0)"},
+            {"-dblogsize=<n>", "Flush wallet database activity from memory to disk log every <n> megabytes (default: 100)"},
+            {"-flushwallet", "Run a thread to flush wallet periodically (default: 1)"},
+            {"-privdb", "Sets the DB_PRIVATE flag in the wallet db environment (default: 1; the wallet store is always private to this process)"},
+            {"-walletrejectlongchains", "Wallet will not create transactions that violate mempool chain limits (default: 0)"},
+        };
+        s += "\nWallet debugging/testing options:\n";
+        for (const auto& o : dbg) s += strprintf("  %-32s %s\n", o.first, o.second);
+    }
     return s;
 }
 
@@ -111,12 +123,30 @@ static bool LoadOneWallet(NodeContext& node, const std::string& name, std::strin
     }
     w->nTxConfirmTarget = (unsigned)gArgs.GetArg("-txconfirmtarget", (int64_t)DEFAULT_TX_CONFIRM_TARGET);
     w->fBroadcastTransactions = gArgs.GetBoolArg("-walletbroadcast", DEFAULT_WALLETBROADCAST);
+    w->fSendFreeTransactions = gArgs.GetBoolArg("-sendfreetransactions", DEFAULT_SEND_FREE_TRANSACTIONS);
+    // -upgradewallet[=<max version>], implied on first run (reference wallet.cpp:4063-4081)
+    if (gArgs.GetBoolArg("-upgradewallet", firstRun)) {
+        int64_t nMaxVersion = gArgs.GetArg("-upgradewallet", (int64_t)0);
+        if (nMaxVersion == 0 || nMaxVersion == 1) { // no argument (a bare flag reads as 1)
+            LogPrintf("Performing wallet upgrade to %i\n", WALLET_FEATURE_LATEST);
+            nMaxVersion = CLIENT_VERSION;
+            w->SetMinVersion(WALLET_FEATURE_LATEST);
+        } else {
+            LogPrintf("Allowing wallet upgrade up to %i\n", (int)nMaxVersion);
+        }
+        if (nMaxVersion < w->GetVersion()) {
+            err = "Cannot downgrade wallet";
+            return false;
+        }
+        w->nWalletMaxVersion = (int)nMaxVersion;
+    }
     if (firstRun) {
         if (gArgs.GetBoolArg("-usehd", true) && !w->IsHDEnabled()) {
             if (!w->SetHDMasterKey(w->GenerateNewHDMasterKey())) {
                 err = "Storing master key failed";
                 return false;
             }
+            w->SetMinVersion(WALLET_FEATURE_HD); // only HD-aware clients may open it
         }
         w->TopUpKeyPool();
         CPubKey def;
@@ -158,6 +188,16 @@ bool StartWallet(NodeContext& node, std::string& err) {
         LogPrintf("Wallet disabled!\n");
         return true;
     }
+    // wallet parameter interaction (reference wallet.cpp:4268-4368 ParameterInteraction / InitAutoStart)
+    if (gArgs.GetBoolArg("-sysperms", false)) {
+        err = "-sysperms is not allowed in combination with enabled wallet functionality";
+        return false;
+    }
+    if (gArgs.GetBoolArg("-sendfreetransactions", DEFAULT_SEND_FREE_TRANSACTIONS) &&
+        gArgs.GetArg("-limitfreerelay", (int64_t)0) <= 0) {
+        err = "Creation of free transactions with their relay disabled is not supported.";
+        return false;
+    }
     std::vector<std::string> names = gArgs.GetArgs("-wallet");
     if (names.empty()) names.push_back("wallet.dat");
     for (const std::string& n : names) {
@@ -178,7 +218,7 @@ bool StartWallet(NodeContext& node, std::string& err) {
         return GetScriptForDestination(pub.GetID());
     };
     g_walletGetInfo = [w](UniValue& obj) {
-        obj.pushKV("walletversion", WALLET_FEATURE_LATEST);
+        obj.pushKV("walletversion", w->GetVersion());
         obj.pushKV("balance", ValueFromAmount(w->GetBalance()));
         obj.pushKV("keypoololdest", w->GetOldestKeyPoolTime());
         obj.pushKV("keypoolsize", (int64_t)w->KeypoolCountExternalKeys());
@@ -216,6 +256,14 @@ bool StartWallet(NodeContext& node, std::string& err) {
         }
         return true;
     };
+    // -flushwallet: make the wallet stores durable every few seconds (reference walletdb.cpp:750
+    // ThreadFlushWalletDB; the stores here are write-ahead logged, so this is an fsync point)
+    if (node.scheduler && gArgs.GetBoolArg("-flushwallet", DEFAULT_FLUSHWALLET))
+        node.scheduler->ScheduleEvery(
+            [] {
+                for (CWallet* x : GetWallets()) x->FlushIfDirty();
+            },
+            2 * 1000);
     // periodic rebroadcast of unconfirmed wallet transactions
     if (node.scheduler)
         node.scheduler->ScheduleEvery(
