@@ -5,6 +5,8 @@
 #include "node/policy.h"
 #include "node/txmempool.h"
 #include "node/validation.h"
+#include "node/ui_interface.h"
+#include "node/warnings.h"
 #include "util/strencodings.h"
 
 #include <algorithm>
@@ -960,7 +962,10 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
                   fLogIPs ? (", peeraddr=" + pfrom->addr.ToString()).c_str() : "");
         const int64_t nTimeOffset = nTime - GetTime();
         pfrom->nTimeOffset = nTimeOffset;
-        AddTimeData(pfrom->addr.ToStringIP(), nTimeOffset);
+        if (AddTimeData(pfrom->addr.ToStringIP(), nTimeOffset)) {
+            SetMiscWarning(CLOCK_WARNING);
+            uiInterface.ThreadSafeMessageBox(CLOCK_WARNING, "", CClientUIInterface::MSG_WARNING);
+        }
         if (pfrom->fFeeler) pfrom->fDisconnect = true;
         return true;
     }

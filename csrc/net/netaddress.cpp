@@ -143,7 +143,8 @@ std::vector<unsigned char> CNetAddr::GetGroup() const {
     if (IsLocal()) {
         nClass = 255;
         nBits = 0;
-    } else if (!IsRoutable()) {
+    }
+    if (!IsRoutable()) { // local addresses are unroutable too: one group for all of them
         nClass = NET_UNROUTABLE;
         nBits = 0;
     } else if (IsIPv4() || IsRFC6145() || IsRFC6052()) {
@@ -250,6 +251,21 @@ CSubNet::CSubNet(const CNetAddr& addr, int bits) : network(addr), valid(true) {
 
 CSubNet::CSubNet(const CNetAddr& addr) : network(addr), valid(addr.IsValid()) { memset(netmask, 0xFF, 16); }
 
+// Any mask, contiguous or not (reference netaddress.cpp CSubNet(addr, mask)); an IPv4 mask
+// applies to the IPv4 part only.
+CSubNet::CSubNet(const CNetAddr& addr, const CNetAddr& mask) : network(addr), valid(true) {
+    if (addr.IsIPv4() != mask.IsIPv4()) {
+        valid = false;
+        return;
+    }
+    memset(netmask, 0xFF, 16);
+    const int start = addr.IsIPv4() ? 12 : 0;
+    for (int i = start; i < 16; i++) netmask[i] = mask.Raw()[i];
+    unsigned char raw[16];
+    for (int i = 0; i < 16; i++) raw[i] = addr.Raw()[i] & netmask[i];
+    network.SetRaw(raw);
+}
+
 bool CSubNet::Match(const CNetAddr& addr) const {
     if (!valid || !addr.IsValid()) return false;
     for (int i = 0; i < 16; i++)
@@ -272,10 +288,16 @@ std::string CSubNet::ToString() const {
         bits += b;
         if (b < 8 && i + 1 < 16 && netmask[i + 1]) valid_cidr = false;
     }
-    if (!valid_cidr) {
-        std::string s;
-        for (int i = start; i < 16; i++) s += strprintf(i == start ? "%d" : ".%d", netmask[i]);
-        return network.ToString() + "/" + s;
+    if (!valid_cidr) { // the mask itself, printed as an address of the subnet's family
+        CNetAddr m;
+        unsigned char raw[16];
+        memcpy(raw, netmask, 16);
+        if (network.IsIPv4()) {
+            static const unsigned char mapped[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0xff, 0xff};
+            memcpy(raw, mapped, 12);
+        }
+        m.SetRaw(raw);
+        return network.ToString() + "/" + m.ToStringIP();
     }
     return network.ToString() + "/" + std::to_string(bits);
 }
@@ -373,19 +395,10 @@ bool LookupSubNet(const std::string& str, CSubNet& out) {
         out = CSubNet(network, (int)n);
         return out.IsValid();
     }
-    // dotted netmask
+    // a netmask written as an address
     CNetAddr mask;
     if (!LookupHost(rest, mask, false)) return false;
-    int bits = 0;
-    const int start = mask.IsIPv4() ? 12 : 0;
-    for (int i = start; i < 16; i++) {
-        unsigned char m = mask.Raw()[i];
-        while (m & 0x80) {
-            bits++;
-            m <<= 1;
-        }
-    }
-    out = CSubNet(network, bits);
+    out = CSubNet(network, mask);
     return out.IsValid();
 }
 

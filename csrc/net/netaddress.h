@@ -113,6 +113,7 @@ public:
     CSubNet() { memset(netmask, 0, 16); }
     CSubNet(const CNetAddr& addr, int bits);
     explicit CSubNet(const CNetAddr& addr); // single host
+    CSubNet(const CNetAddr& addr, const CNetAddr& mask);
     bool Match(const CNetAddr& addr) const;
     bool IsValid() const { return valid; }
     std::string ToString() const;

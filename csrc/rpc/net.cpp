@@ -99,10 +99,21 @@ static UniValue addnode(const JSONRPCRequest& req) {
     return UniValue::NullUniValue;
 }
 
+// By address, or by node id with an empty/null address (reference net.cpp disconnectnode).
 static UniValue disconnectnode(const JSONRPCRequest& req) {
-    if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "disconnectnode \"address\"");
-    if (!Connman().DisconnectNode(req.params[0].get_str()))
-        ThrowRPC(RPC_CLIENT_NODE_NOT_CONNECTED, "Node not found in connected nodes");
+    if (req.params.size() == 0 || req.params.size() > 2)
+        ThrowRPC(RPC_INVALID_PARAMS, "disconnectnode \"[address]\" [nodeid]");
+    const UniValue& address = req.params[0];
+    const UniValue& id = req.params.size() < 2 ? UniValue::NullUniValue : req.params[1];
+    bool success;
+    if (!address.isNull() && id.isNull()) {
+        success = Connman().DisconnectNode(address.get_str());
+    } else if (!id.isNull() && (address.isNull() || (address.isStr() && address.get_str().empty()))) {
+        success = Connman().DisconnectNode((NodeId)id.get_int64());
+    } else {
+        ThrowRPC(RPC_INVALID_PARAMS, "Only one of address and nodeid should be provided.");
+    }
+    if (!success) ThrowRPC(RPC_CLIENT_NODE_NOT_CONNECTED, "Node not found in connected nodes");
     return UniValue::NullUniValue;
 }
 
@@ -261,7 +272,7 @@ void RegisterNetRPCCommands(CRPCTable& t) {
         {"network", "ping", ping, true, {}, "ping\nRequests that a ping be sent to all other nodes, to measure ping time."},
         {"network", "getpeerinfo", getpeerinfo, true, {}, "getpeerinfo\nReturns data about each connected network node as a json array of objects."},
         {"network", "addnode", addnode, true, {"node", "command"}, "addnode \"node\" \"add|remove|onetry\"\nAttempts to add or remove a node from the addnode list."},
-        {"network", "disconnectnode", disconnectnode, true, {"address"}, "disconnectnode \"address\"\nImmediately disconnects from the specified peer node."},
+        {"network", "disconnectnode", disconnectnode, true, {"address", "nodeid"}, "disconnectnode \"[address]\" [nodeid]\nImmediately disconnects from the specified peer node, by address or (with an empty address) by node id."},
         {"network", "getaddednodeinfo", getaddednodeinfo, true, {"node"}, "getaddednodeinfo ( \"node\" )\nReturns information about the given added node, or all added nodes."},
         {"network", "getnettotals", getnettotals, true, {}, "getnettotals\nReturns information about network traffic."},
         {"network", "getnetworkinfo", getnetworkinfo, true, {}, "getnetworkinfo\nReturns an object containing various state info regarding P2P networking."},

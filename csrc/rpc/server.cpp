@@ -128,6 +128,10 @@ UniValue CRPCTable::execute(const JSONRPCRequest& request) const {
     const CRPCCommand* pcmd = (*this)[request.strMethod];
     if (!pcmd) ThrowRPC(RPC_METHOD_NOT_FOUND, "Method not found");
     if (!pcmd->okSafeMode) bcp::ObserveSafeMode();
+    // more positional arguments than the command takes: its usage, as each reference handler
+    // answers "if (request.fHelp || request.params.size() > N) throw runtime_error(help)"
+    if (request.params.isArray() && request.params.size() > pcmd->argNames.size())
+        ThrowRPC(RPC_MISC_ERROR, pcmd->help.empty() ? request.strMethod : pcmd->help);
     try {
         if (request.params.isObject()) return pcmd->actor(transformNamedArguments(request, pcmd->argNames));
         return pcmd->actor(request);

@@ -1,0 +1,240 @@
+// Wallet coin selection and address-book records.
+// Parity: reference src/wallet/test/wallet_tests.cpp (coin_selection_tests,
+// ApproximateBestSubset) and src/wallet/test/walletdb_tests.cpp (write/erase of name, purpose
+// and destdata, which the reference reads back through a fresh CWalletDB). Coins here are
+// in-memory wallet transactions; "from me" coins really spend one of the wallet's own outputs.
+#include "test/unittest.h"
+#include "wallet/wallet.h"
+
+#include <cmath>
+#include <deque>
+#include <unistd.h>
+
+namespace bcp {
+namespace {
+
+typedef std::set<std::pair<const CWalletTx*, unsigned int>> CoinSet;
+
+struct Pool {
+    CWallet wallet{"test", "", true};
+    std::deque<CWalletTx> txs; // stable addresses for COutput::tx
+    std::vector<COutput> coins;
+    CKey key;
+    uint256 fundingTx; // a wallet-owned output the "from me" coins spend
+    uint32_t lockTime = 0;
+    Pool() {
+        key.MakeNewKey(true);
+        wallet.AddKeyPubKey(key, key.GetPubKey());
+        CMutableTransaction f;
+        f.vin.resize(1);
+        f.vout.push_back(CTxOut(COIN, GetScriptForDestination(key.GetPubKey().GetID())));
+        CWalletTx wtx(&wallet, MakeTransactionRef(std::move(f)));
+        fundingTx = wtx.GetHash();
+        WalletLock l(wallet);
+        wallet.mapWallet[fundingTx] = wtx;
+    }
+    // a coin of value v, `depth` confirmations, optionally spending our own output
+    void Add(Amount v, int depth = 144, bool fromMe = false) {
+        CMutableTransaction t;
+        t.nLockTime = lockTime++; // distinct hashes
+        if (fromMe) t.vin.push_back(CTxIn(COutPoint(fundingTx, 0)));
+        t.vout.push_back(CTxOut(v, CScript() << OP_TRUE));
+        txs.emplace_back(&wallet, MakeTransactionRef(std::move(t)));
+        coins.push_back({&txs.back(), 0, depth, true, true});
+    }
+    void Clear() {
+        coins.clear();
+        txs.clear();
+    }
+    bool Select(Amount target, int confMine, int confTheirs, CoinSet& set, Amount& value) {
+        return wallet.SelectCoinsMinConf(target, confMine, confTheirs, 0, coins, set, value);
+    }
+};
+
+} // namespace
+
+TEST_CASE(wallet_tests, selection_depths_and_origin) {
+    Pool p;
+    CoinSet set;
+    Amount v = 0;
+    CHECK(!p.Select(CENT, 1, 6, set, v)); // nothing at all
+    p.Add(2 * CENT, 3);                   // young coin from someone else
+    CHECK(!p.Select(2 * CENT, 1, 6, set, v));
+    CHECK(p.Select(2 * CENT, 1, 3, set, v));
+    CHECK_EQ(v, 2 * CENT);
+    p.Add(3 * CENT, 2, true); // young change of our own
+    CHECK(p.Select(3 * CENT, 1, 6, set, v)); // our own coins need one confirmation only
+    CHECK_EQ(v, 3 * CENT);
+    CHECK(!p.Select(3 * CENT, 6, 6, set, v));
+    p.Add(40 * CENT); // mature
+    CHECK(p.Select(45 * CENT, 1, 3, set, v));
+    CHECK_EQ(v, 45 * CENT);
+    CHECK(!p.Select(45 * CENT, 1, 6, set, v)); // the 2-cent coin is too young for 6
+    CHECK(p.Select(43 * CENT, 1, 6, set, v));
+    CHECK_EQ(v, 43 * CENT);
+    CHECK(!p.Select(46 * CENT, 1, 1, set, v)); // more than everything
+}
+
+TEST_CASE(wallet_tests, selection_subsets_versus_larger_coin) {
+    for (int rep = 0; rep < 50; rep++) { // the search is randomised: repeat it
+        Pool p;
+        CoinSet set;
+        Amount v = 0;
+        for (int c : {3, 4, 9, 25, 50}) p.Add(c * CENT);
+        // an exact single coin wins
+        CHECK(p.Select(9 * CENT, 1, 1, set, v));
+        CHECK_EQ(v, 9 * CENT);
+        CHECK_EQ(set.size(), (size_t)1);
+        // an exact subset of the small coins: 3 + 4
+        CHECK(p.Select(7 * CENT, 1, 1, set, v));
+        CHECK_EQ(v, 7 * CENT);
+        CHECK_EQ(set.size(), (size_t)2);
+        // 20: the small coins (3+4+9 = 16) cannot reach it, so the smallest larger coin
+        CHECK(p.Select(20 * CENT, 1, 1, set, v));
+        CHECK_EQ(v, 25 * CENT);
+        CHECK_EQ(set.size(), (size_t)1);
+        // 15: 3+4+9 = 16 beats the next larger coin (25)
+        CHECK(p.Select(15 * CENT, 1, 1, set, v));
+        CHECK_EQ(v, 16 * CENT);
+        CHECK_EQ(set.size(), (size_t)3);
+        p.Add(16 * CENT);
+        // now a single 16 ties with 3+4+9: the single larger coin wins a tie
+        CHECK(p.Select(15 * CENT, 1, 1, set, v));
+        CHECK_EQ(v, 16 * CENT);
+        CHECK_EQ(set.size(), (size_t)1);
+        // everything, and not a satoshi more
+        CHECK(p.Select(107 * CENT, 1, 1, set, v));
+        CHECK_EQ(v, 107 * CENT);
+        CHECK(!p.Select(107 * CENT + 1, 1, 1, set, v));
+        // among larger coins the smallest is used
+        for (int c : {2, 3, 5}) p.Add(c * COIN);
+        CHECK(p.Select(180 * CENT, 1, 1, set, v));
+        CHECK_EQ(v, 2 * COIN);
+        CHECK_EQ(set.size(), (size_t)1);
+    }
+}
+
+TEST_CASE(wallet_tests, selection_avoids_small_change) {
+    for (int rep = 0; rep < 50; rep++) {
+        Pool p;
+        CoinSet set;
+        Amount v = 0;
+        // only tiny coins: change below MIN_CHANGE is unavoidable, so the target exactly
+        for (int i = 1; i <= 6; i++) p.Add(i * MIN_CHANGE / 10);
+        CHECK(p.Select(MIN_CHANGE, 1, 1, set, v));
+        CHECK_EQ(v, MIN_CHANGE);
+        // with a big coin around, the exact subset is still preferred over big change
+        p.Add(500 * MIN_CHANGE);
+        CHECK(p.Select(MIN_CHANGE, 1, 1, set, v));
+        CHECK_EQ(v, MIN_CHANGE);
+        p.Clear();
+        // small coins that cannot reach target + MIN_CHANGE and have no exact subset: the big coin
+        for (int i : {5, 6, 7}) p.Add(i * MIN_CHANGE / 10);
+        p.Add(800 * MIN_CHANGE);
+        CHECK(p.Select(MIN_CHANGE, 1, 1, set, v));
+        CHECK_EQ(v, 800 * MIN_CHANGE);
+        CHECK_EQ(set.size(), (size_t)1);
+        p.Clear();
+        // 0.03 + 1 + 100 for 100.01: all three (change 1.02 is fine); for 99.9: 100 + 1
+        p.Add(3 * MIN_CHANGE / 100);
+        p.Add(MIN_CHANGE);
+        p.Add(100 * MIN_CHANGE);
+        CHECK(p.Select(10001 * MIN_CHANGE / 100, 1, 1, set, v));
+        CHECK_EQ(v, 10103 * MIN_CHANGE / 100);
+        CHECK_EQ(set.size(), (size_t)3);
+        CHECK(p.Select(9990 * MIN_CHANGE / 100, 1, 1, set, v));
+        CHECK_EQ(v, 101 * MIN_CHANGE);
+        CHECK_EQ(set.size(), (size_t)2);
+    }
+}
+
+TEST_CASE(wallet_tests, selection_many_equal_coins) {
+    Pool p;
+    CoinSet set, set2;
+    Amount v = 0;
+    // consolidating 30 equal coins into an amount of 12 of them: exactly 12
+    for (int i = 0; i < 30; i++) p.Add(40000 * COIN);
+    CHECK(p.Select(480000 * COIN, 1, 1, set, v));
+    CHECK_EQ(v, 480000 * COIN);
+    CHECK_EQ(set.size(), (size_t)12);
+    // hundreds of small inputs: as few as cover target + MIN_CHANGE, or one if a coin suffices
+    for (Amount a = 2500; a < COIN; a *= 10) {
+        p.Clear();
+        for (int i = 0; i < 600; i++) p.Add(a);
+        CHECK(p.Select(3000, 1, 1, set, v));
+        if (a - 3000 < MIN_CHANGE) {
+            const size_t n = (size_t)std::ceil((3000.0 + MIN_CHANGE) / a);
+            CHECK_EQ(set.size(), n);
+            CHECK_EQ(v, (Amount)n * a);
+        } else {
+            CHECK_EQ(set.size(), (size_t)1);
+            CHECK_EQ(v, a);
+        }
+    }
+    // the choice among identical coins is random
+    p.Clear();
+    for (int i = 0; i < 100; i++) p.Add(COIN);
+    CHECK(p.Select(50 * COIN, 1, 6, set, v));
+    CHECK(p.Select(50 * COIN, 1, 6, set2, v));
+    CHECK(set != set2);
+    int same = 0;
+    for (int i = 0; i < 6; i++) {
+        CHECK(p.Select(COIN, 1, 6, set, v));
+        CHECK(p.Select(COIN, 1, 6, set2, v));
+        same += set == set2;
+    }
+    CHECK(same < 6);
+    // sort order of the subset search: many big coins and one small one
+    p.Clear();
+    for (int i = 0; i < 800; i++) p.Add(1000 * COIN);
+    p.Add(3 * COIN);
+    CHECK(p.Select(1003 * COIN, 1, 6, set, v));
+    CHECK_EQ(v, 1003 * COIN);
+    CHECK_EQ(set.size(), (size_t)2);
+}
+
+TEST_CASE(walletdb_tests, address_book_records_persist) {
+    char tmpl[] = "/tmp/bcp_walletdb_XXXXXX";
+    REQUIRE(mkdtemp(tmpl) != nullptr);
+    const std::string path = std::string(tmpl) + "/wallet.dat";
+    CKey k;
+    k.MakeNewKey(true);
+    const CTxDestination a = k.GetPubKey().GetID();
+    CKey k2;
+    k2.MakeNewKey(true);
+    const CTxDestination b = k2.GetPubKey().GetID();
+    {
+        CWallet w("w", path, false);
+        std::string err;
+        bool first = false;
+        REQUIRE(w.Load(err, first));
+        CHECK(w.SetAddressBook(a, "alice", "receive"));
+        CHECK(w.SetAddressBook(b, "bob", "send"));
+        CHECK(w.AddDestData(a, "rr0", "request-0"));
+        CHECK(w.AddDestData(a, "used", "1"));
+        CHECK(w.AddDestData(b, "rr1", "request-1"));
+        CHECK(!w.AddDestData(CTxDestination(), "x", "y")); // no destination, no record
+        CHECK(w.EraseDestData(a, "used"));
+        CHECK(!w.EraseDestData(a, "never-set"));
+        CHECK(w.DelAddressBook(b)); // takes its destdata with it
+    }
+    {
+        CWallet w("w", path, false);
+        std::string err;
+        bool first = true;
+        REQUIRE(w.Load(err, first));
+        CHECK(!first);
+        REQUIRE(w.mapAddressBook.count(a));
+        CHECK_EQ(w.mapAddressBook[a].name, std::string("alice"));
+        CHECK_EQ(w.mapAddressBook[a].purpose, std::string("receive"));
+        std::string v;
+        CHECK(w.GetDestData(a, "rr0", &v) && v == "request-0");
+        CHECK(!w.GetDestData(a, "used", &v));
+        CHECK(!w.mapAddressBook.count(b));
+        CHECK(!w.GetDestData(b, "rr1", &v));
+    }
+    std::string cmd = std::string("rm -rf '") + tmpl + "'";
+    CHECK(std::system(cmd.c_str()) == 0);
+}
+
+} // namespace bcp

@@ -274,11 +274,24 @@ std::string FormatMoney(int64_t n) {
     return str;
 }
 
+// Reference utilmoneystr.cpp ParseMoney: optional surrounding whitespace, at most ten integer
+// digits, at most eight decimals, no sign or exponent ("" reads as zero).
 bool ParseMoney(const std::string& s, int64_t& n) {
-    int64_t v;
-    if (!ParseFixedPoint(s, 8, &v)) return false;
-    if (v < 0) return false;
-    n = v;
+    size_t i = 0;
+    while (i < s.size() && isspace((unsigned char)s[i])) i++;
+    int64_t whole = 0, units = 0;
+    int wholeDigits = 0;
+    for (; i < s.size() && isdigit((unsigned char)s[i]); i++, wholeDigits++)
+        if (wholeDigits < 11) whole = whole * 10 + (s[i] - '0');
+    if (i < s.size() && s[i] == '.') {
+        i++;
+        int64_t mult = 10000000; // 0.1 BCP in satoshis
+        for (; i < s.size() && isdigit((unsigned char)s[i]) && mult > 0; i++, mult /= 10) units += mult * (s[i] - '0');
+    }
+    for (; i < s.size(); i++)
+        if (!isspace((unsigned char)s[i])) return false;
+    if (wholeDigits > 10) return false; // 63-bit overflow guard
+    n = whole * 100000000 + units;
     return true;
 }
 

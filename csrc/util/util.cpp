@@ -47,21 +47,29 @@ int64_t GetTimeOffset() {
 }
 int64_t GetAdjustedTime() { return GetTime() + GetTimeOffset(); }
 
-// Median of peer clock offsets, recomputed at odd sample counts (reference timedata.cpp:44).
-void AddTimeData(const std::string& peer, int64_t nOffsetSample) {
+// Median of peer clock offsets, recomputed at odd sample counts (reference timedata.cpp:44-110;
+// at 200 samples the count stays even, so the offset freezes, as there).
+bool AddTimeData(const std::string& peer, int64_t nOffsetSample) {
     static std::set<std::string> setKnown;
-    static std::vector<int64_t> samples{0};
+    static MedianFilter<int64_t> offsets(200, 0);
+    static bool fWarned = false;
     std::lock_guard<std::mutex> l(cs_nTimeOffset);
-    if (setKnown.size() == 200 || !setKnown.insert(peer).second) return;
-    if (samples.size() >= 200) samples.erase(samples.begin());
-    samples.push_back(nOffsetSample);
-    if (samples.size() >= 5 && samples.size() % 2 == 1) {
-        std::vector<int64_t> sorted = samples;
-        std::sort(sorted.begin(), sorted.end());
-        const int64_t median = sorted[sorted.size() / 2];
-        if (std::abs(median) <= gArgs.GetArg("-maxtimeadjustment", DEFAULT_MAX_TIME_ADJUSTMENT)) nTimeOffset = median;
-        else nTimeOffset = 0;
+    if (setKnown.size() == 200 || !setKnown.insert(peer).second) return false;
+    offsets.input(nOffsetSample);
+    LogPrint(BCLog::NET, "added time data, samples %d, offset %+lld (%+lld minutes)\n", offsets.size(),
+             (long long)nOffsetSample, (long long)nOffsetSample / 60);
+    if (offsets.size() < 5 || offsets.size() % 2 == 0) return false;
+    const int64_t median = offsets.median();
+    if (std::abs(median) <= std::max<int64_t>(0, gArgs.GetArg("-maxtimeadjustment", DEFAULT_MAX_TIME_ADJUSTMENT))) {
+        nTimeOffset = median;
+        return false;
     }
+    nTimeOffset = 0;
+    if (fWarned) return false;
+    for (int64_t o : offsets.sorted())
+        if (o != 0 && std::abs(o) < 5 * 60) return false; // someone agrees with us
+    fWarned = true;
+    return true;
 }
 
 // ---------------------------------------------------------------- logging
@@ -218,6 +226,8 @@ void ShrinkDebugFile() {
 // ---------------------------------------------------------------- args
 ArgsManager gArgs;
 
+static bool InterpretBool(const std::string& v) { return v.empty() ? true : atoi64(v) != 0; }
+
 void ArgsManager::ParseParameters(int argc, const char* const argv[]) {
     std::lock_guard<CCriticalSection> l(cs_args);
     mapArgs.clear();
@@ -231,10 +241,10 @@ void ArgsManager::ParseParameters(int argc, const char* const argv[]) {
         }
         if (key.empty() || key[0] != '-') break;
         if (key.size() > 1 && key[1] == '-') key = key.substr(1); // --foo == -foo
-        // -nofoo => -foo=0
-        if (key.compare(0, 3, "-no") == 0 && key.size() > 3 && value.empty()) {
+        // -nofoo => -foo=0, -nofoo=0 => -foo=1 (reference util.cpp InterpretNegativeSetting)
+        if (key.compare(0, 3, "-no") == 0 && key.size() > 3) {
             key = "-" + key.substr(3);
-            value = "0";
+            value = InterpretBool(value) ? "0" : "1";
         }
         mapArgs[key] = value;
         mapMultiArgs[key].push_back(value);
@@ -280,7 +290,6 @@ int64_t ArgsManager::GetArg(const std::string& a, int64_t d) const {
     auto it = mapArgs.find(a);
     return it == mapArgs.end() ? d : atoi64(it->second);
 }
-static bool InterpretBool(const std::string& v) { return v.empty() ? true : atoi64(v) != 0; }
 bool ArgsManager::GetBoolArg(const std::string& a, bool d) const {
     std::lock_guard<CCriticalSection> l(cs_args);
     auto it = mapArgs.find(a);

@@ -7,6 +7,7 @@
 // replaced here by ParallelFor), src/scheduler.{h,cpp}.
 #pragma once
 #include "util/sync.h"
+#include <algorithm>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -31,7 +32,41 @@ void MilliSleep(int64_t n);
 
 int64_t GetTimeOffset();
 int64_t GetAdjustedTime();
-void AddTimeData(const std::string& peer, int64_t nOffsetSample);
+// Returns true once, the first time the samples disagree with our clock by more than
+// -maxtimeadjustment and no peer is within 5 minutes of it (the caller raises the "check your
+// computer's date and time" warning, reference timedata.cpp:86-105).
+bool AddTimeData(const std::string& peer, int64_t nOffsetSample);
+static const char* const CLOCK_WARNING =
+    "Please check that your computer's date and time are correct! If your clock is wrong, Bitcoin Cash Plus will "
+    "not work properly.";
+
+// Median of the last N values (reference timedata.h CMedianFilter). The window keeps arrival
+// order for eviction and a sorted copy updated by one binary-search insert/erase per value.
+template <typename T> class MedianFilter {
+public:
+    MedianFilter(unsigned size, T initial) : nSize(size) {
+        window.push_back(initial);
+        ordered.push_back(initial);
+    }
+    void input(T v) {
+        if (window.size() == nSize) {
+            ordered.erase(std::lower_bound(ordered.begin(), ordered.end(), window.front()));
+            window.erase(window.begin());
+        }
+        window.push_back(v);
+        ordered.insert(std::upper_bound(ordered.begin(), ordered.end(), v), v);
+    }
+    T median() const {
+        const size_t n = ordered.size();
+        return (n & 1) ? ordered[n / 2] : (ordered[n / 2 - 1] + ordered[n / 2]) / 2;
+    }
+    int size() const { return (int)window.size(); }
+    const std::vector<T>& sorted() const { return ordered; }
+
+private:
+    unsigned nSize;
+    std::vector<T> window, ordered;
+};
 static const int64_t DEFAULT_MAX_TIME_ADJUSTMENT = 70 * 60;
 
 // ---------------------------------------------------------------- logging

@@ -1657,6 +1657,30 @@ bool CWallet::DelAddressBook(const CTxDestination& address) {
     return db->WriteBatch(b, true);
 }
 
+bool CWallet::AddDestData(const CTxDestination& dest, const std::string& key, const std::string& value) {
+    if (!dest.IsValid()) return false;
+    WalletLock l(*this);
+    mapAddressBook[dest].destdata[key] = value;
+    return db->Write(K("destdata", std::make_pair(DestKey{dest}, key)), value, true);
+}
+
+bool CWallet::EraseDestData(const CTxDestination& dest, const std::string& key) {
+    WalletLock l(*this);
+    auto it = mapAddressBook.find(dest);
+    if (it == mapAddressBook.end() || !it->second.destdata.erase(key)) return false;
+    return db->Erase(K("destdata", std::make_pair(DestKey{dest}, key)), true);
+}
+
+bool CWallet::GetDestData(const CTxDestination& dest, const std::string& key, std::string* value) const {
+    WalletLock l(*this);
+    auto it = mapAddressBook.find(dest);
+    if (it == mapAddressBook.end()) return false;
+    auto d = it->second.destdata.find(key);
+    if (d == it->second.destdata.end()) return false;
+    if (value) *value = d->second;
+    return true;
+}
+
 bool CWallet::GetAccountPubkey(CPubKey& pubKey, const std::string& strAccount, bool bForceNew) {
     WalletLock l(*this);
     CPubKey cur;

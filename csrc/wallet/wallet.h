@@ -403,6 +403,11 @@ public:
     std::map<CTxDestination, CAddressBookData> mapAddressBook;
     bool SetAddressBook(const CTxDestination& address, const std::string& strName, const std::string& purpose);
     bool DelAddressBook(const CTxDestination& address);
+    // Per-destination key/value data (reference wallet.cpp AddDestData/EraseDestData/GetDestData:
+    // e.g. payment requests "rr<id>" and "used" markers), stored with the address book.
+    bool AddDestData(const CTxDestination& dest, const std::string& key, const std::string& value);
+    bool EraseDestData(const CTxDestination& dest, const std::string& key);
+    bool GetDestData(const CTxDestination& dest, const std::string& key, std::string* value) const;
     bool GetAccountPubkey(CPubKey& pubKey, const std::string& strAccount, bool bForceNew = false);
 
     // ---- validation callbacks
