@@ -16,8 +16,7 @@ Kernel map (reference hot loops):
   scan_nonces        K5  legacy SHA-256d header nonce scan           sha256.hip
   equihash_verify    K4  batched IsValidSolution                     equihash_verify.hip
   ecdsa_verify       K8  batched secp256k1 verify                    secp256k1.hip
-  sighash_forkid     K7  FORKID digests from recipes                 relay.hip / sighash_device.h
-  verify_forkid      K7+K8 fused digest -> verify (node deferral)    secp256k1.hip EcdsaSighashFill
+  verify_forkid      K8  block-path deferred checks -> verify batch  secp256k1.hip (GpuVerifyDeferred)
   short_txids        K9  BIP152 SipHash-2-4 short ids                relay.hip
   Equihash solving (K1-K3) is ``models.EquihashModel.gpu_solver``.
 """
@@ -103,18 +102,10 @@ def short_txids(k0: int, k1: int, txids, device: int = -1) -> list:
     return native.short_txid_batch_gpu(k0, k1, raw, device)
 
 
-def sighash_forkid(items: Iterable, use_gpu: bool = True, device: int = -1) -> list:
-    """FORKID signature hashes of (script_code, tx_bytes, n_in, hash_type, amount) items, as
-    (digest, computed_from_a_recipe) pairs. use_gpu=False evaluates the same recipes on the CPU."""
-    if use_gpu:
-        require_gpu("sighash_forkid")
-    return native.sighash_recipes(list(items), use_gpu=use_gpu, device=device)
-
-
-def verify_forkid(items: Iterable, use_gpu: bool = True, recipes: bool = True):
+def verify_forkid(items: Iterable, use_gpu: bool = True):
     """Block-path signature checks (pubkey, sig_with_hashtype, script_code, tx_bytes, n_in,
-    amount) through the node's deferring checker; with recipes the GPU computes the digests in
-    the verify batch. Returns (results, digests, recipe_flags)."""
+    amount) through the node's deferring checker (the digest computed as a script worker does)
+    and the GPU verify batch. Returns (results, digests)."""
     if use_gpu:
         require_gpu("verify_forkid")
-    return native.verify_sig_recipes(list(items), use_gpu=use_gpu, recipes=recipes)
+    return native.verify_sig_deferred(list(items), use_gpu=use_gpu)

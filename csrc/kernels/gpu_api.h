@@ -101,48 +101,6 @@ int64_t Sha256dScanNonces(const unsigned char header80[80], const unsigned char 
 std::vector<uint64_t> ShortTxIdBatch(uint64_t k0, uint64_t k1, const unsigned char* txids32, size_t n,
                                      int device = -1);
 
-// --------------------------------------------------------------- FORKID signature hashes
-// A signature-hash recipe (reference src/script/interpreter.cpp:1354-1404, the SIGHASH_FORKID
-// digest): the device computes
-//   SHA256d(version | hashPrevouts | hashSequence | outpoint | compactsize(L) code[L] |
-//           amount | nSequence | hashOutputs | nLockTime | nHashType)
-// from one SighashTx shared by a transaction's checks and one SighashJob per check. The host has
-// already applied the hash-type rules: the ZERO_* flags blank the shared hashes, and a check
-// whose digest the recipe cannot express (SIGHASH_SINGLE with a matching output, legacy
-// digests) carries SIGHASH_JOB_PRECOMPUTED and its digest is supplied by the host instead.
-struct SighashTx {                 // 104 bytes, serialization byte order
-    unsigned char version[4];
-    unsigned char hashPrevouts[32];
-    unsigned char hashSequence[32];
-    unsigned char hashOutputs[32];
-    unsigned char lockTime[4];
-};
-enum : uint32_t {
-    SIGHASH_JOB_ZERO_PREVOUTS = 1,
-    SIGHASH_JOB_ZERO_SEQUENCE = 2,
-    SIGHASH_JOB_ZERO_OUTPUTS = 4,
-    SIGHASH_JOB_PRECOMPUTED = 8,
-};
-struct SighashJob {                // 80 bytes
-    uint32_t tx;                   // index of the transaction's SighashTx
-    uint32_t flags;                // SIGHASH_JOB_*
-    uint32_t codeOff, codeLen;     // script code bytes in the code arena
-    uint32_t hashType;             // serialized little-endian as the last 4 preimage bytes
-    unsigned char outpoint[36];    // prevout hash || n (LE)
-    unsigned char amount[8];       // LE
-    unsigned char sequence[4];     // LE
-    uint32_t pad[3];
-};
-static_assert(sizeof(SighashTx) == 104 && sizeof(SighashJob) == 80, "recipe layouts are shared with the device");
-// Digests of n recipes (n x 32 bytes, raw SHA256d output = the ECDSA message). Jobs flagged
-// PRECOMPUTED get their digest from `precomputed` (n x 32, may be null if none are flagged).
-std::vector<unsigned char> SighashBatch(const std::vector<SighashTx>& txs, const std::vector<SighashJob>& jobs,
-                                        const std::vector<unsigned char>& code,
-                                        const std::vector<unsigned char>& precomputed, int device = -1);
-// Throws std::invalid_argument if a non-PRECOMPUTED job names a transaction or code range
-// outside the arrays (checked on the host before every recipe launch).
-void CheckSighashRecipes(const SighashTx* txs, size_t ntx, const SighashJob* jobs, size_t n, size_t codeBytes);
-
 // --------------------------------------------------------------- secp256k1
 // ECDSA verification batch: N jobs, msg32 = N*32 (big-endian digest bytes as signed),
 // sig64 = N*64 (r||s big-endian, s low-S-normalised, r,s in [1,n-1] checked on host),
@@ -176,17 +134,6 @@ public:
     void EcdsaFill(size_t n, const std::function<void(unsigned char* msg32, unsigned char* sig64,
                                                         unsigned char* pub33)>& fill,
                    uint8_t* result);
-    // Fused signature hash -> verify: the messages are FORKID digests the device computes from
-    // recipes (ntx SighashTx, n SighashJob, codeBytes of script code) on the lane's stream right
-    // before the ECDSA kernels read them; no digest crosses PCIe on the way in. `fill` writes the
-    // recipes, the signatures and keys (and, for PRECOMPUTED jobs, the digest into msg32) into
-    // the pinned staging. digestsOut (n x 32, optional) receives the digests for the
-    // signature cache.
-    void EcdsaSighashFill(size_t n, size_t ntx, size_t codeBytes,
-                          const std::function<void(SighashTx* txs, SighashJob* jobs, unsigned char* code,
-                                                   unsigned char* msg32, unsigned char* sig64,
-                                                   unsigned char* pub33)>& fill,
-                          uint8_t* result, unsigned char* digestsOut);
     // Same contract as EquihashVerifyBatch for n (state, solution) pairs; a solution of the
     // wrong length is rejected.
     void Equihash(unsigned N, unsigned K, const EhBaseState* states, const std::vector<unsigned char>* const* sols,

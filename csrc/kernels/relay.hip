@@ -2,15 +2,12 @@
 //   K9  BIP152 short transaction ids (SipHash-2-4 of a txid, 48 bits): the mempool side of
 //       compact-block reconstruction, reference src/blockencodings.cpp:37-42 and
 //       PartiallyDownloadedBlock::InitData (:67-178), SipHashUint256 src/hash.cpp:181-300;
-//   K7  FORKID signature hashes from recipes (kernels/sighash_device.h), the stand-alone form
-//       of the digest the fused verify lane (secp256k1.hip EcdsaSighashFill) computes.
 // One lane per item; 64-bit SipHash words stay in VGPR pairs (v_lshl_add_u64 adds,
 // v_alignbit rotates).
 #include <hip/hip_runtime.h>
 
 #include "kernels/gpu_api.h"
 #include "kernels/hip_util.h"
-#include "kernels/sighash_device.h"
 
 #include <algorithm>
 #include <cstring>
@@ -102,51 +99,6 @@ std::vector<uint64_t> ShortTxIdBatch(uint64_t k0, uint64_t k1, const unsigned ch
     BCP_HIP_CHECK(hipMemcpyAsync(h_out, d_out, n * 8, hipMemcpyDeviceToHost, c.s));
     BCP_HIP_CHECK(hipStreamSynchronize(c.s));
     memcpy(out.data(), h_out, n * 8);
-    return out;
-}
-
-// Validates recipe references on the host before any launch: a job naming a transaction or
-// code range outside the arrays would read out of bounds on the device.
-void CheckSighashRecipes(const SighashTx* /*txs*/, size_t ntx, const SighashJob* jobs, size_t n, size_t codeBytes) {
-    for (size_t i = 0; i < n; ++i) {
-        const SighashJob& j = jobs[i];
-        if (j.flags & SIGHASH_JOB_PRECOMPUTED) continue;
-        if (j.tx >= ntx) throw std::invalid_argument("sighash recipe: transaction index out of range");
-        if ((uint64_t)j.codeOff + j.codeLen > codeBytes) throw std::invalid_argument("sighash recipe: code out of range");
-    }
-}
-
-std::vector<unsigned char> SighashBatch(const std::vector<SighashTx>& txs, const std::vector<SighashJob>& jobs,
-                                        const std::vector<unsigned char>& code,
-                                        const std::vector<unsigned char>& precomputed, int device) {
-    const size_t n = jobs.size();
-    std::vector<unsigned char> out(n * 32, 0);
-    if (!n) return out;
-    CheckSighashRecipes(txs.data(), txs.size(), jobs.data(), n, code.size());
-    bool anyPre = false;
-    for (const SighashJob& j : jobs) anyPre |= (j.flags & SIGHASH_JOB_PRECOMPUTED) != 0;
-    if (anyPre && precomputed.size() != n * 32) throw std::invalid_argument("SighashBatch: precomputed digests");
-    device = UseDevice(device);
-    RelayCtx& c = Ctx(device);
-    auto l = Lock(c);
-    const size_t tb = (std::max<size_t>(txs.size(), 1) * sizeof(SighashTx) + 15) & ~(size_t)15, jb = n * sizeof(SighashJob),
-                 cb = (std::max<size_t>(code.size(), 1) + 15) & ~(size_t)15, db = n * 32; // 16-B aligned digests
-    unsigned char* h = c.st.Host(0, tb + jb + cb + db);
-    unsigned char* d = c.st.Dev(0, tb + jb + cb + db);
-    unsigned char* h_out = c.st.Host(1, db);
-    if (!txs.empty()) memcpy(h, txs.data(), txs.size() * sizeof(SighashTx));
-    memcpy(h + tb, jobs.data(), jb);
-    if (!code.empty()) memcpy(h + tb + jb, code.data(), code.size());
-    if (anyPre) memcpy(h + tb + jb + cb, precomputed.data(), db);
-    else memset(h + tb + jb + cb, 0, db);
-    BCP_HIP_CHECK(hipMemcpyAsync(d, h, tb + jb + cb + db, hipMemcpyHostToDevice, c.s));
-    hipLaunchKernelGGL(bcpk::sighash_forkid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, c.s,
-                       (const uint8_t*)d, (const uint8_t*)(d + tb), (const uint8_t*)(d + tb + jb), d + tb + jb + cb,
-                       (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    BCP_HIP_CHECK(hipMemcpyAsync(h_out, d + tb + jb + cb, db, hipMemcpyDeviceToHost, c.s));
-    BCP_HIP_CHECK(hipStreamSynchronize(c.s));
-    memcpy(out.data(), h_out, db);
     return out;
 }
 

@@ -22,7 +22,6 @@
 
 #include "kernels/gpu_api.h"
 #include "kernels/hip_util.h"
-#include "kernels/sighash_device.h"
 #include "secp256k1/secp256k1.h"
 
 #include <cstring>
@@ -1112,54 +1111,6 @@ void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, un
     BCP_HIP_CHECK(hipMemcpyAsync(h_out, d_out, n, hipMemcpyDeviceToHost, L.stream));
     BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
     memcpy(result, h_out, n);
-    L.batches++;
-    L.items += n;
-}
-
-// Fused K7 -> K8: the FORKID digests are computed on the lane's stream from the recipes and land
-// in the message slots the prep kernel reads; the verdicts (and, for the signature cache, the
-// digests) come back in one D2H pair.
-void VerifyLane::EcdsaSighashFill(
-    size_t n, size_t ntx, size_t codeBytes,
-    const std::function<void(SighashTx*, SighashJob*, unsigned char*, unsigned char*, unsigned char*, unsigned char*)>&
-        fill,
-    uint8_t* result, unsigned char* digestsOut) {
-    if (n == 0) return;
-    LaneState& L = *impl;
-    BCP_HIP_CHECK(hipSetDevice(L.device));
-    Table& tb = T(L.device);
-    std::call_once(tb.once, [&] { InitTable(tb); });
-    const size_t txb = (std::max<size_t>(ntx, 1) * sizeof(SighashTx) + 15) & ~(size_t)15;
-    const size_t jb = n * sizeof(SighashJob), cb = std::max<size_t>(codeBytes, 1);
-    unsigned char* h_in = L.Host(0, n * 129);
-    unsigned char* h_rec = L.Host(3, txb + jb + cb);
-    uint8_t* h_out = L.Host(1, n * 33);
-    SighashTx* htx = reinterpret_cast<SighashTx*>(h_rec);
-    SighashJob* hjob = reinterpret_cast<SighashJob*>(h_rec + txb);
-    fill(htx, hjob, h_rec + txb + jb, h_in, h_in + n * 32, h_in + n * 96);
-    CheckSighashRecipes(htx, ntx, hjob, n, codeBytes);
-    unsigned char* d_in = L.Dev(0, n * 129);
-    unsigned char* d_rec = L.Dev(3, txb + jb + cb);
-    Job* d_jobs = reinterpret_cast<Job*>(L.Dev(1, n * sizeof(Job)));
-    uint8_t* d_out = L.Dev(2, n);
-    BCP_HIP_CHECK(hipMemcpyAsync(d_rec, h_rec, txb + jb + codeBytes, hipMemcpyHostToDevice, L.stream));
-    BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, n * 129, hipMemcpyHostToDevice, L.stream));
-    hipLaunchKernelGGL(bcpk::sighash_forkid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, L.stream,
-                       (const uint8_t*)d_rec, (const uint8_t*)(d_rec + txb), (const uint8_t*)(d_rec + txb + jb), d_in,
-                       (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, L.stream, d_jobs,
-                       (const unsigned char*)d_in, (const unsigned char*)(d_in + n * 32),
-                       (const unsigned char*)(d_in + n * 96), (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    const int grid = (int)((n + WG - 1) / WG);
-    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, L.stream, d_jobs, tb.d_gtab, d_out, (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    BCP_HIP_CHECK(hipMemcpyAsync(h_out, d_out, n, hipMemcpyDeviceToHost, L.stream));
-    if (digestsOut) BCP_HIP_CHECK(hipMemcpyAsync(h_out + n, d_in, n * 32, hipMemcpyDeviceToHost, L.stream));
-    BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
-    memcpy(result, h_out, n);
-    if (digestsOut) memcpy(digestsOut, h_out + n, n * 32);
     L.batches++;
     L.items += n;
 }

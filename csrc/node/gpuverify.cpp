@@ -200,28 +200,6 @@ std::vector<uint8_t> GpuVerifyService::EcdsaFill(
     return out;
 }
 
-std::vector<uint8_t> GpuVerifyService::EcdsaSighashFill(
-    size_t n, const std::function<size_t(size_t, size_t)>& codeBytes,
-    const std::function<void(size_t, size_t, gpu::SighashTx*, gpu::SighashJob*, unsigned char*, unsigned char*,
-                             unsigned char*, unsigned char*)>& fill,
-    unsigned char* digests) {
-    std::vector<uint8_t> out(n, 0);
-    if (n == 0) return out;
-    size_t minShard;
-    {
-        std::lock_guard<std::mutex> l(m);
-        minShard = minShardEcdsa;
-    }
-    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi) {
-        lane.EcdsaSighashFill(
-            hi - lo, hi - lo, codeBytes(lo, hi),
-            [&](gpu::SighashTx* t, gpu::SighashJob* j, unsigned char* c, unsigned char* msg, unsigned char* sig,
-                unsigned char* pub) { fill(lo, hi, t, j, c, msg, sig, pub); },
-            out.data() + lo, digests ? digests + lo * 32 : nullptr);
-    });
-    return out;
-}
-
 std::vector<uint8_t> GpuVerifyService::Equihash(unsigned N, unsigned K, const std::vector<gpu::EhBaseState>& states,
                                                 const std::vector<const std::vector<unsigned char>*>& sols) {
     if (states.size() != sols.size()) throw std::invalid_argument("GpuVerifyService::Equihash: sizes");

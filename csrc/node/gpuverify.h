@@ -51,16 +51,6 @@ public:
     // jobs [lo, hi) into a lane's pinned staging arrays (indexed from 0 = job lo).
     std::vector<uint8_t> EcdsaFill(size_t n, const std::function<void(size_t lo, size_t hi, unsigned char* msg32,
                                                                       unsigned char* sig64, unsigned char* pub33)>& fill);
-    // Fused sighash -> verify (K7 + K8): per shard, fill(lo, hi, txs, jobs, code, msg32, sig64, pub33)
-    // writes one SighashTx and one SighashJob per job (job i's recipe names transaction i of the
-    // shard) plus the script code (codeBytes(lo, hi) bytes) into the lane's staging; the device
-    // computes the digests and verifies. digests (n x 32) receives every job's digest.
-    std::vector<uint8_t> EcdsaSighashFill(
-        size_t n, const std::function<size_t(size_t lo, size_t hi)>& codeBytes,
-        const std::function<void(size_t lo, size_t hi, gpu::SighashTx* txs, gpu::SighashJob* jobs,
-                                 unsigned char* code, unsigned char* msg32, unsigned char* sig64,
-                                 unsigned char* pub33)>& fill,
-        unsigned char* digests);
     // result[i] = 1 iff solution i is valid for state i.
     std::vector<uint8_t> Equihash(unsigned N, unsigned K, const std::vector<gpu::EhBaseState>& states,
                                   const std::vector<const std::vector<unsigned char>*>& sols);

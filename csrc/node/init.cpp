@@ -54,7 +54,6 @@ std::string HelpMessage() {
         {"-par=<n>", "Number of script verification threads (0 = auto)"},
         {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
         {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 512)"},
-        {"-gpusighash=<n>", "Compute FORKID signature hashes of block validation on the GPU, fused into the verify batch: 0 never, 1 during initial block download, 2 always (default: 0)"},
         {"-gpushortidthreshold=<n>", "Smallest mempool whose compact-block short ids are computed on the GPU (default: 16384)"},
         {"-gpudevices=<list>", "Comma-separated GPU indices the built-in Equihash miner runs on, one host thread per device (default: all visible)"},
         {"-gpuvalidationdevices=<list>", "Comma-separated GPU indices that verify block signatures and header solutions, one high-priority stream and service thread each; batches are sharded across them. When set, the built-in miner leaves these devices alone if others are available (default: device 0, shared with the miner)"},
@@ -362,7 +361,6 @@ int AppMain(int argc, char* argv[]) {
         }
     }
     SetGpuSigThreshold((size_t)gArgs.GetArg("-gpusigthreshold", (int64_t)GetGpuSigThreshold()));
-    SetGpuSighashMode((int)gArgs.GetArg("-gpusighash", (int64_t)GetGpuSighashMode()));
     SetGpuShortIdThreshold((size_t)gArgs.GetArg("-gpushortidthreshold", (int64_t)GetGpuShortIdThreshold()));
     if (gArgs.IsArgSet("-gpudevices")) {
         std::vector<int> devs;

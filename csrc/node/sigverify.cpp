@@ -35,9 +35,6 @@ size_t InitSignatureCache(int64_t mib) {
 }
 
 static std::atomic<size_t> g_gpuThreshold{DEFAULT_GPU_SIG_THRESHOLD};
-static std::atomic<int> g_gpuSighashMode{0}; // measured slower end to end, profiles/sighash_shortid_r3.md
-void SetGpuSighashMode(int mode) { g_gpuSighashMode = mode; }
-int GetGpuSighashMode() { return g_gpuSighashMode.load(); }
 void SetGpuSigThreshold(size_t n) { g_gpuThreshold = n; }
 size_t GetGpuSigThreshold() { return g_gpuThreshold.load(); }
 
@@ -104,67 +101,24 @@ static bool PrepSigAndKey(const DeferredSigCheck& c, unsigned char* sig64, unsig
     return ok;
 }
 
-std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool,
-                                       std::vector<uint256>* digests) {
+std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool) {
     // host: DER parse + low-S normalisation + key form, written by the pool straight into the
-    // verify lane's pinned staging buffer; device: (recipe checks) the FORKID digest, then
-    // decompression + ecmult
+    // verify lane's pinned staging buffer; device: scalar prep, decompression + ecmult
     const size_t n = checks.size();
     std::vector<uint8_t> hostOk(n, 1);
     if (GpuFaultInjection()) throw std::runtime_error("injected GPU signature-verify fault");
-    bool anyRecipe = false;
-    for (const DeferredSigCheck* c : checks)
-        if (c->recipe) {
-            anyRecipe = true;
-            break;
-        }
-    auto parallel = [&](size_t count, const std::function<void(size_t)>& f) {
-        if (pool) pool->ParallelFor(count, f, 64);
+    auto fill = [&](size_t lo, size_t hi, unsigned char* msg, unsigned char* sig, unsigned char* pub) {
+        auto one = [&](size_t k) {
+            const DeferredSigCheck& c = *checks[lo + k];
+            memcpy(&msg[k * 32], c.sighash.begin(), 32);
+            if (!PrepSigAndKey(c, &sig[k * 64], &pub[k * 33])) hostOk[lo + k] = 0;
+        };
+        if (pool) pool->ParallelFor(hi - lo, one, 64);
         else
-            for (size_t k = 0; k < count; k++) f(k);
+            for (size_t k = 0; k < hi - lo; k++) one(k);
     };
-    std::vector<uint8_t> res;
-    if (!anyRecipe) {
-        auto fill = [&](size_t lo, size_t hi, unsigned char* msg, unsigned char* sig, unsigned char* pub) {
-            parallel(hi - lo, [&](size_t k) {
-                const DeferredSigCheck& c = *checks[lo + k];
-                memcpy(&msg[k * 32], c.sighash.begin(), 32);
-                if (!PrepSigAndKey(c, &sig[k * 64], &pub[k * 33])) hostOk[lo + k] = 0;
-            });
-        };
-        // sharded across the validation GPUs by the verify service (one high-priority lane each)
-        res = GpuVerifyService::Instance().EcdsaFill(n, fill);
-        if (digests) {
-            digests->resize(n);
-            for (size_t j = 0; j < n; j++) (*digests)[j] = checks[j]->sighash;
-        }
-    } else {
-        // fused K7 -> K8: one SighashTx + SighashJob per job (job k of a shard names tx k), the
-        // inline script code at 32-byte stride; other jobs carry their digest (PRECOMPUTED)
-        std::vector<uint256> dg(n);
-        auto fill = [&](size_t lo, size_t hi, gpu::SighashTx* txs, gpu::SighashJob* jobs, unsigned char* code,
-                        unsigned char* msg, unsigned char* sig, unsigned char* pub) {
-            parallel(hi - lo, [&](size_t k) {
-                const DeferredSigCheck& c = *checks[lo + k];
-                if (c.recipe) {
-                    FillSighashTx(c, txs[k]);
-                    jobs[k] = c.job;
-                    jobs[k].tx = (uint32_t)k;
-                    jobs[k].codeOff = (uint32_t)(k * 32);
-                    jobs[k].codeLen = c.sighash.begin()[0];
-                    memcpy(&code[k * 32], c.sighash.begin() + 1, 31);
-                } else {
-                    memset(&jobs[k], 0, sizeof(gpu::SighashJob));
-                    jobs[k].flags = gpu::SIGHASH_JOB_PRECOMPUTED;
-                    memcpy(&msg[k * 32], c.sighash.begin(), 32);
-                }
-                if (!PrepSigAndKey(c, &sig[k * 64], &pub[k * 33])) hostOk[lo + k] = 0;
-            });
-        };
-        res = GpuVerifyService::Instance().EcdsaSighashFill(
-            n, [](size_t lo, size_t hi) { return (hi - lo) * 32; }, fill, dg[0].begin());
-        if (digests) digests->swap(dg);
-    }
+    // sharded across the validation GPUs by the verify service (one high-priority lane each)
+    std::vector<uint8_t> res = GpuVerifyService::Instance().EcdsaFill(n, fill);
     for (size_t j = 0; j < n; j++) res[j] &= hostOk[j];
     return res;
 }
@@ -205,12 +159,9 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
         const size_t lo = chunk * PROBE_CHUNK, hi = std::min(checks.size(), lo + PROBE_CHUNK);
         for (size_t i = lo; i < hi; i++) {
             const DeferredSigCheck& c = *checks[i];
-            // a recipe check's digest is first known on the device: no cache key before the batch
-            if (!c.recipe) entries[i] = cache.Entry(c.sighash, c.sig.data(), c.sig.size(), c.pubkey.data(), c.pubkey.size());
+            entries[i] = cache.Entry(c.sighash, c.sig.data(), c.sig.size(), c.pubkey.data(), c.pubkey.size());
         }
         cache.GetMany(&entries[lo], hi - lo, cacheErase, &hit[lo]);
-        for (size_t i = lo; i < hi; i++)
-            if (checks[i]->recipe) hit[i] = 0;
     };
     const size_t nChunks = (checks.size() + PROBE_CHUNK - 1) / PROBE_CHUNK;
     if (pool && nChunks > 1) pool->ParallelFor(nChunks, probe, 1);
@@ -234,9 +185,8 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
             std::vector<const DeferredSigCheck*> ptrs(n);
             for (size_t j = 0; j < n; j++) ptrs[j] = checks[todo[j]];
             std::vector<uint8_t> r;
-            std::vector<uint256> dg;
             try {
-                r = GpuVerifyDeferred(ptrs, pool, cacheStore ? &dg : nullptr);
+                r = GpuVerifyDeferred(ptrs, pool);
                 g_gpuFailures = 0;
             } catch (const std::exception& e) {
                 const int fails = ++g_gpuFailures;
@@ -254,10 +204,7 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
                     if (!r[j]) {
                         if (!spec[todo[j]]) ok = false;
                     } else if (cacheStore) {
-                        const DeferredSigCheck& c = *checks[todo[j]];
-                        cache.Set(c.recipe ? cache.Entry(dg[j], c.sig.data(), c.sig.size(), c.pubkey.data(),
-                                                         c.pubkey.size())
-                                           : entries[todo[j]]);
+                        cache.Set(entries[todo[j]]);
                     }
                 }
                 std::lock_guard<std::mutex> l(g_statsMutex);
@@ -272,15 +219,12 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
                 if (!allOk.load(std::memory_order_relaxed)) return;
                 const size_t i = todo[j];
                 const DeferredSigCheck& c = *checks[i];
-                const uint256 digest = DeferredDigest(c);
                 res[i] = secp::VerifySignature(c.pubkey.data(), c.pubkey.size(), c.sig.data(), c.sig.size(),
-                                               digest.begin());
+                                               c.sighash.begin());
                 if (!res[i]) {
                     if (!spec[i]) allOk = false;
                 } else if (cacheStore) {
-                    cache.Set(c.recipe ? cache.Entry(digest, c.sig.data(), c.sig.size(), c.pubkey.data(),
-                                                     c.pubkey.size())
-                                       : entries[i]);
+                    cache.Set(entries[i]);
                 }
             };
             if (pool) pool->ParallelFor(n, work, 8);

@@ -72,15 +72,7 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
                            const std::vector<DeferredMultisig>& groups, WorkerPool* pool, bool useGpu,
                            bool cacheStore, bool cacheErase);
 // Device verification of the given checks (no cache); result[i] = 1 iff valid.
-// Checks carrying sighash recipes go through the fused digest -> verify lane path; digests
-// (optional) receives every check's digest.
-std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool,
-                                       std::vector<uint256>* digests = nullptr);
-// Device sighash recipes in block validation (-gpusighash): 0 off (default: measured slower
-// end to end on a 16-thread host, profiles/sighash_shortid_r3.md), 1 during initial block
-// download (the signature cache is cold there; recipe checks skip its pre-batch probe), 2 always.
-void SetGpuSighashMode(int mode);
-int GetGpuSighashMode();
+std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool);
 void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path
 size_t GetGpuSigThreshold();
 void ResetGpuSigFailures();

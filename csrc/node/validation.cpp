@@ -831,10 +831,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     std::vector<std::vector<DeferredSigCheck>> sinks(maxJobs);
     std::vector<std::vector<DeferredMultisig>> groupSinks(maxJobs); // deferred CHECKMULTISIGs per job
     const bool deferMultisig = GpuBatchesExpected(opts.useGpu);
-    // FORKID digests computed on the device, fused into the verify batch (no cache probe for
-    // them, so by default only while the cache is cold: initial block download)
-    const int sighashMode = GetGpuSighashMode();
-    const bool recipes = deferMultisig && (sighashMode >= 2 || (sighashMode == 1 && IsInitialBlockDownload()));
     std::atomic<bool> anyFail{false};
     size_t nProduced = 0, nPublished = 0;
     const bool queued = fScriptChecks && maxJobs > 0;
@@ -843,7 +839,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             if (anyFail.load(std::memory_order_relaxed)) return;
             const ScriptJob& J = jobs[k];
             BlockSigChecker checker(J.tx, J.nIn, J.amount, J.txdata, &sinks[k], deferMultisig ? &groupSinks[k] : nullptr);
-            checker.SetRecipes(recipes);
             ScriptError err;
             if (!VerifyScript(J.tx->vin[J.nIn].scriptSig, *J.scriptPubKey, flags, checker, &err)) anyFail = true;
         });
@@ -989,10 +984,8 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 // the pool is shared (ParallelFor calls serialise)
                 WorkerPool* wp = pool.get();
                 const bool useGpu = opts.useGpu, erase = !fJustCheck;
-                // (recipe checks point into txdatas: the batch owns them too)
                 p.sigs = std::async(std::launch::async, [wp, useGpu, erase, sinks = std::move(sinks), all = std::move(all),
-                                                         groups = std::move(groups),
-                                                         txdatas = std::move(txdatas)]() mutable {
+                                                         groups = std::move(groups)]() mutable {
                     return BatchVerifySignatures(all, groups, wp, useGpu, false, erase);
                 });
             } else {

@@ -8,7 +8,6 @@
 #include "consensus/tx_verify.h"
 #include "kernels/gpu_api.h"
 #include "node/sigverify.h"
-#include "script/sighash_recipe.h"
 #include "secp256k1/secp256k1.h"
 
 #include <cstring>
@@ -145,66 +144,15 @@ void bind_script(pyb::module_& m) {
         pyb::arg("tx"), pyb::arg("n_in"), pyb::arg("script_pubkey"), pyb::arg("amount"), pyb::arg("keys"),
         pyb::arg("redeem_scripts") = std::vector<pyb::bytes>(), pyb::arg("hash_type") = SIGHASH_ALL | SIGHASH_FORKID);
 
-    // FORKID signature-hash recipes (K7): items = [(script_code, tx, n_in, hash_type, amount)].
-    // Returns [(digest, recipe_used)]: the device (use_gpu) or CPU evaluation of each recipe;
-    // checks the recipe cannot express (legacy, SIGHASH_SINGLE with a matching output) carry the
-    // CPU SignatureHash as a PRECOMPUTED job.
+    // Block-validation signature checks through the node's deferral path: items = [(pubkey,
+    // sig_with_hashtype, script_code, tx, n_in, amount)]. Each check's digest is computed by the
+    // deferring checker (as a script worker does); the GPU path is the verify lane batch
+    // (GpuVerifyDeferred), the CPU path verifies each check. Returns (results, digests); a check
+    // the checker refused to defer is (False, b"").
     m.def(
-        "sighash_recipes",
-        [](const std::vector<std::tuple<pyb::bytes, pyb::bytes, unsigned, uint32_t, int64_t>>& items, bool use_gpu,
-           uint32_t flags, int device) {
-            const size_t n = items.size();
-            std::vector<gpu::SighashTx> txs(n);
-            std::vector<gpu::SighashJob> jobs(n);
-            std::vector<unsigned char> code, pre(n * 32, 0);
-            std::vector<bool> used(n);
-            for (size_t i = 0; i < n; i++) {
-                const CScript sc = to_script(std::get<0>(items[i]));
-                const CTransaction tx = tx_from_bytes(std::get<1>(items[i]));
-                const unsigned nIn = std::get<2>(items[i]);
-                const uint32_t ht = std::get<3>(items[i]);
-                const Amount amount = std::get<4>(items[i]);
-                if (nIn >= tx.vin.size()) throw std::invalid_argument("n_in out of range");
-                const PrecomputedTransactionData txdata(tx);
-                FillSighashTx(tx, txdata, txs[i]);
-                used[i] = FillSighashJob(tx, nIn, ht, amount, flags, (uint32_t)i, (uint32_t)code.size(),
-                                         (uint32_t)sc.size(), jobs[i]);
-                if (used[i]) {
-                    code.insert(code.end(), sc.begin(), sc.end());
-                } else {
-                    memset(&jobs[i], 0, sizeof(jobs[i]));
-                    jobs[i].flags = gpu::SIGHASH_JOB_PRECOMPUTED;
-                    const uint256 h = SignatureHash(sc, tx, nIn, ht, amount, &txdata, flags);
-                    memcpy(&pre[32 * i], h.begin(), 32);
-                }
-            }
-            std::vector<unsigned char> out(n * 32);
-            if (use_gpu) {
-                pyb::gil_scoped_release rel;
-                out = gpu::SighashBatch(txs, jobs, code, pre, device);
-            } else {
-                for (size_t i = 0; i < n; i++) {
-                    const uint256 h = used[i] ? SighashFromRecipe(txs[i], jobs[i], code.data()) : uint256();
-                    memcpy(&out[32 * i], used[i] ? h.begin() : &pre[32 * i], 32);
-                }
-            }
-            pyb::list l;
-            for (size_t i = 0; i < n; i++) l.append(pyb::make_tuple(to_bytes(&out[32 * i], 32), (bool)used[i]));
-            return l;
-        },
-        pyb::arg("items"), pyb::arg("use_gpu") = false, pyb::arg("flags") = (uint32_t)SCRIPT_ENABLE_SIGHASH_FORKID,
-        pyb::arg("device") = -1);
-
-    // Block-validation signature checks through the node's deferral path with device sighash
-    // recipes (DeferringSignatureChecker::SetRecipes): items = [(pubkey, sig_with_hashtype,
-    // script_code, tx, n_in, amount)]. The GPU path is the fused digest -> verify lane batch
-    // (GpuVerifyDeferred); the CPU path evaluates each recipe (DeferredDigest) and verifies.
-    // Returns (results, digests, recipe flags); a check the checker refused to defer is (False,
-    // b"", False).
-    m.def(
-        "verify_sig_recipes",
+        "verify_sig_deferred",
         [](const std::vector<std::tuple<pyb::bytes, pyb::bytes, pyb::bytes, pyb::bytes, unsigned, int64_t>>& items,
-           bool use_gpu, bool recipes, uint32_t flags) {
+           bool use_gpu, uint32_t flags) {
             const size_t n = items.size();
             std::vector<std::unique_ptr<CTransaction>> txs;
             std::vector<std::unique_ptr<PrecomputedTransactionData>> txdatas;
@@ -217,7 +165,6 @@ void bind_script(pyb::module_& m) {
                 if (nIn >= txs.back()->vin.size()) throw std::invalid_argument("n_in out of range");
                 DeferringSignatureChecker checker(txs.back().get(), nIn, std::get<5>(items[i]), txdatas.back().get(),
                                                   &sink);
-                checker.SetRecipes(recipes);
                 const size_t before = sink.size();
                 checker.CheckSig(to_vec(std::get<1>(items[i])), to_vec(std::get<0>(items[i])),
                                  to_script(std::get<2>(items[i])), flags, true);
@@ -226,35 +173,31 @@ void bind_script(pyb::module_& m) {
             std::vector<const DeferredSigCheck*> ptrs;
             for (const auto& c : sink) ptrs.push_back(&c);
             std::vector<uint8_t> res(sink.size());
-            std::vector<uint256> dg(sink.size());
             {
                 pyb::gil_scoped_release rel;
                 if (use_gpu && !sink.empty()) {
-                    res = GpuVerifyDeferred(ptrs, nullptr, &dg);
+                    res = GpuVerifyDeferred(ptrs, nullptr);
                 } else {
                     for (size_t j = 0; j < sink.size(); j++) {
                         const DeferredSigCheck& c = sink[j];
-                        dg[j] = DeferredDigest(c);
                         res[j] = secp::VerifySignature(c.pubkey.data(), c.pubkey.size(), c.sig.data(), c.sig.size(),
-                                                       dg[j].begin());
+                                                       c.sighash.begin());
                     }
                 }
             }
-            pyb::list r, d, f;
+            pyb::list r, d;
             for (size_t i = 0; i < n; i++) {
                 if (slot[i] < 0) {
                     r.append(false);
                     d.append(pyb::bytes(""));
-                    f.append(false);
                     continue;
                 }
                 r.append((bool)res[slot[i]]);
-                d.append(to_bytes(dg[slot[i]].begin(), 32));
-                f.append(sink[slot[i]].recipe);
+                d.append(to_bytes(sink[slot[i]].sighash.begin(), 32));
             }
-            return pyb::make_tuple(r, d, f);
+            return pyb::make_tuple(r, d);
         },
-        pyb::arg("items"), pyb::arg("use_gpu") = false, pyb::arg("recipes") = true,
+        pyb::arg("items"), pyb::arg("use_gpu") = false,
         pyb::arg("flags") = (uint32_t)(SCRIPT_ENABLE_SIGHASH_FORKID | SCRIPT_VERIFY_STRICTENC));
 }
 

@@ -1,6 +1,5 @@
 // Script interpreter. See interpreter.h for the parity map.
 #include "script/interpreter.h"
-#include "script/sighash_recipe.h"
 #include "crypto/hashes.h"
 #include "keys/key.h"
 #include "secp256k1/secp256k1.h"
@@ -845,18 +844,6 @@ bool DeferringSignatureChecker::CheckSig(const valtype& sigIn, const valtype& pu
         return TransactionSignatureChecker::CheckSig(sigIn, pubkey, scriptCode, flags, false);
     sink->emplace_back();
     DeferredSigCheck& c = sink->back();
-    if (recipes && scriptCode.size() <= MAX_RECIPE_CODE &&
-        FillSighashJob(*txTo, nIn, sigIn.back(), amount, flags, 0, 0, (uint32_t)scriptCode.size(), c.job)) {
-        c.recipe = true;
-        c.txdata = txdata;
-        c.txVersion = (uint32_t)txTo->nVersion;
-        c.txLockTime = txTo->nLockTime;
-        c.sighash.begin()[0] = (unsigned char)scriptCode.size();
-        if (!scriptCode.empty()) memcpy(c.sighash.begin() + 1, scriptCode.data(), scriptCode.size());
-        c.sig.assign(sigIn.data(), sigIn.size() - 1);
-        c.pubkey.assign(pubkey);
-        return true;
-    }
     if (!SigDigest(sigIn, scriptCode, flags, c.sighash)) {
         sink->pop_back();
         return false;
@@ -864,26 +851,6 @@ bool DeferringSignatureChecker::CheckSig(const valtype& sigIn, const valtype& pu
     c.sig.assign(sigIn.data(), sigIn.size() - 1);
     c.pubkey.assign(pubkey);
     return true;
-}
-
-uint256 DeferredDigest(const DeferredSigCheck& c) {
-    if (!c.recipe) return c.sighash;
-    gpu::SighashTx t;
-    FillSighashTx(c, t);
-    gpu::SighashJob j = c.job;
-    j.codeOff = 0;
-    j.codeLen = c.sighash.begin()[0];
-    return SighashFromRecipe(t, j, c.sighash.begin() + 1);
-}
-
-void FillSighashTx(const DeferredSigCheck& c, gpu::SighashTx& t) {
-    for (int i = 0; i < 4; ++i) {
-        t.version[i] = (unsigned char)(c.txVersion >> (8 * i));
-        t.lockTime[i] = (unsigned char)(c.txLockTime >> (8 * i));
-    }
-    memcpy(t.hashPrevouts, c.txdata->hashPrevouts.begin(), 32);
-    memcpy(t.hashSequence, c.txdata->hashSequence.begin(), 32);
-    memcpy(t.hashOutputs, c.txdata->hashOutputs.begin(), 32);
 }
 
 bool DeferringSignatureChecker::DeferMultisig(const std::vector<const valtype*>& sigs,

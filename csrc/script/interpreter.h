@@ -201,21 +201,8 @@ template <size_t CAP> struct InlineBytes {
 struct DeferredSigCheck {
     InlineBytes<65> pubkey; // serialized (33/65 bytes)
     InlineBytes<72> sig;    // DER (strict DER is at most 72 bytes), hashtype stripped
-    // The digest; for a recipe check, the script code instead (byte 0: length <= 31, then the
-    // code bytes): its FORKID digest is computed on the device from `job` and `txdata`
-    // (kernels/sighash_device.h, fused into the verify batch) or by DeferredDigest on the CPU.
-    uint256 sighash;
-    bool recipe = false;
-    uint32_t txVersion = 0, txLockTime = 0;          // recipe: the SighashTx fields not in txdata
-    const PrecomputedTransactionData* txdata = nullptr; // recipe: outlives the batch
-    gpu::SighashJob job;                             // recipe: tx/codeOff are set when staged
+    uint256 sighash; // the signature hash (computed by the script worker that deferred the check)
 };
-// Largest script code a recipe check carries inline (P2PKH's is 25 bytes).
-static const size_t MAX_RECIPE_CODE = 31;
-// The check's digest: the stored one, or the recipe's evaluated on the CPU.
-uint256 DeferredDigest(const DeferredSigCheck& c);
-// The recipe check's shared transaction fields (version, lock time, txdata's three hashes).
-void FillSighashTx(const DeferredSigCheck& c, gpu::SighashTx& t);
 
 // A deferred CHECKMULTISIG: the m x (n - m + 1) pairs its greedy match can reach are consecutive
 // checks of the batch starting at `first`, row-major by signature (signature i with keys
@@ -240,13 +227,7 @@ public:
     bool DeferMultisig(const std::vector<const std::vector<unsigned char>*>& sigs,
                        const std::vector<const std::vector<unsigned char>*>& keys, uint32_t keyOk,
                        const CScript& scriptCode, uint32_t flags) const override;
-    // Record FORKID checks as device sighash recipes (no CPU digest) where the recipe can
-    // express them; needs txdata. Their digests are unknown before the batch, so a caller that
-    // probes the signature cache first must leave this off.
-    void SetRecipes(bool on) { recipes = on && txdata != nullptr; }
-
 private:
-    bool recipes = false;
     std::vector<DeferredSigCheck>* sink;
     std::vector<DeferredMultisig>* groups; // CHECKMULTISIG deferral (null: multisig runs eagerly)
 };

@@ -17,7 +17,6 @@
 #include "node/coins.h"
 #include "node/kvstore.h"
 #include "node/miner.h"
-#include "script/sighash_recipe.h"
 #include "script/sign.h"
 #include "script/standard.h"
 #include "node/sigverify.h"
@@ -542,34 +541,6 @@ static void ShortIdBench(State& st, bool gpuPath) {
 static bench::Reg reg_CpuShortId("CPU_ShortIds_250k", [](State& st) { ShortIdBench(st, false); });
 static bench::Reg reg_GpuShortId("GPU_ShortIds_250k", [](State& st) { ShortIdBench(st, true); });
 
-// FORKID digests of 160k P2PKH-shaped recipes (K7): CPU SighashFromRecipe loop (one thread) vs
-// the device batch (incl. staging and copies).
-static void SighashBench(State& st, bool gpuPath) {
-    if (gpuPath && !gpu::GpuAvailable()) return;
-    const size_t n = 160000, ntx = n / 2;
-    std::vector<gpu::SighashTx> txs(ntx);
-    std::vector<gpu::SighashJob> jobs(n);
-    std::vector<unsigned char> code(25 * n), pre;
-    for (size_t t = 0; t < ntx; t++) memset(&txs[t], (int)(t & 0xff), sizeof(gpu::SighashTx));
-    for (size_t i = 0; i < n; i++) {
-        memset(&jobs[i], (int)(i * 7 & 0xff), sizeof(gpu::SighashJob));
-        jobs[i].tx = (uint32_t)(i / 2);
-        jobs[i].flags = 0;
-        jobs[i].codeOff = (uint32_t)(25 * i);
-        jobs[i].codeLen = 25;
-        jobs[i].hashType = 0x41;
-    }
-    for (size_t i = 0; i < code.size(); i++) code[i] = (unsigned char)(i * 31);
-    std::vector<unsigned char> out;
-    while (st.KeepRunning()) {
-        if (gpuPath) out = gpu::SighashBatch(txs, jobs, code, pre);
-        else
-            for (size_t i = 0; i < n; i++) SighashFromRecipe(txs[jobs[i].tx], jobs[i], code.data());
-    }
-}
-static bench::Reg reg_CpuSighash("CPU_Sighash_160k", [](State& st) { SighashBench(st, false); });
-static bench::Reg reg_GpuSighash("GPU_Sighash_160k", [](State& st) { SighashBench(st, true); });
-
 // ---- 8 MB block connect (BASELINE.md "block connect time for an 8 MB / 160k-sigop block"): a
 // regtest chain past the BCP fork (Equihash(48,5) headers) in a memory-only chainstate, one big
 // block on top of it, then Chainstate::TestBlockValidity (CheckBlock + contextual checks +
@@ -775,9 +746,6 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
     BigBlockFixture& f = BigBlock(kind);
     const size_t thr = GetGpuSigThreshold();
     SetGpuSigThreshold(useGpu ? DEFAULT_GPU_SIG_THRESHOLD : SIZE_MAX);
-    // -gpusighash=0/1/2: FORKID digests on the CPU workers, or device recipes fused into the batch
-    const int shMode = GetGpuSighashMode();
-    SetGpuSighashMode((int)gArgs.GetArg("-gpusighash", (int64_t)shMode));
     const SigVerifyStats s0 = GetSigVerifyStats();
     int64_t ph0[Chainstate::PH_COUNT];
     for (int k = 0; k < Chainstate::PH_COUNT; k++) ph0[k] = f.cs->ConnectPhaseMicros((Chainstate::ConnectPhase)k);
@@ -804,7 +772,6 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
             useGpu ? "GPU" : "CPU", ms(Chainstate::PH_CHECK), ms(Chainstate::PH_PRECOMPUTE), ms(Chainstate::PH_UTXO),
             ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_COLLECT), ms(Chainstate::PH_BATCH));
     SetGpuSigThreshold(thr);
-    SetGpuSighashMode(shMode);
 }
 } // namespace
 

@@ -27,14 +27,8 @@ def test_short_ids_reject_ragged_input(native):
 
 
 @pytest.mark.gpu
-def test_ops_facade_short_ids_and_sighash(native):
+def test_ops_facade_short_ids(native):
     from bitcoincashplus_amd import ops
     rng = random.Random(9)
     txids = [rng.randbytes(32) for _ in range(64)]
     assert ops.short_txids(5, 6, txids) == [native.siphash_uint256(5, 6, t) & MASK for t in txids]
-    import json, os
-    raw, script, n_in, _, _ = [v for v in json.load(open(os.path.join(os.path.dirname(__file__), "data", "vectors",
-                                                                          "sighash.json"))) if len(v) == 5][3]
-    item = (bytes.fromhex(script), bytes.fromhex(raw), n_in, 0x41, 1234)
-    (d, used), = ops.sighash_forkid([item])
-    assert used and d == native.signature_hash(*item)

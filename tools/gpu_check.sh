@@ -22,8 +22,7 @@
 #   ecdsa-cpu TAG        CPU ECDSA / ecmult micro-benches and the CPU 8 MB connect
 #   connect TAG [BLOCKS] 8 MB block connects CPU vs GPU, the IBD pipeline, and a kernel profile
 #                        of the 160k-sigop GPU connect
-#   relay TAG            device sighash recipes / short-id kernels: tests, micro-benches, connects
-#                        with -gpusighash=0 vs 2
+#   relay TAG            BIP152 short-id kernel: GPU tests and the CPU vs GPU micro-bench
 #   hash TAG             SHA256d64 / merkle micro-benches (CPU SHA-NI vs GPU)
 #   baseline TAG         BASELINE.md secondary metrics (tools/baseline_metrics.py + bench_bcp)
 #   multirank TAG        bench.py as 2 ranks on one GPU over gloo (the multi-rank launcher path)
@@ -32,7 +31,7 @@
 # r3_eh_ab.sh, eh_ab_check.sh, eh_validate.sh, eh_variants.sh -> eh-ab; r3_eh_trace.sh,
 # eh_ktrace.sh, eh_prof_builds.sh -> eh-trace; pmc_eh.sh, pmc_bw.sh, pmc_rounds.sh -> pmc-eh;
 # ecdsa_check.sh, ec_ab.sh -> ecdsa; r3_ecdsa_cpu.sh -> ecdsa-cpu; r3_connect*.sh -> connect;
-# r3s2_relay.sh -> relay; r3_gpu_check.sh -> check + hash; baseline_check.sh -> baseline;
+# r3s2_relay.sh -> relay (short ids; the device sighash path was removed in round 4); r3_gpu_check.sh -> check + hash; baseline_check.sh -> baseline;
 # r3_ab_batch.sh, eh_sweep.sh -> eh-sweep; multirank_rehearsal.sh -> multirank.
 set -e
 cd "$GRAFT_REPO_ROOT"
@@ -147,16 +146,11 @@ connect)
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- "$R/bin/bench_bcp" \
     -filter='ConnectBlock8MB_160kSigops_GPU' -time=2 > "$O/prof.log" 2>&1) ;;
 relay)
-  timeout -k 10 300 python -u -m pytest tests/test_sighash_recipes.py tests/test_shortid_gpu.py -m gpu -x -v \
-    --timeout 120 --timeout-method thread > "$O/pytest.log" 2>&1
+  timeout -k 10 300 python -u -m pytest tests/test_shortid_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread \
+    > "$O/pytest.log" 2>&1
   tail -n 3 "$O/pytest.log"
-  timeout -k 10 120 ./bin/bench_bcp -filter='(CPU|GPU)_(ShortIds|Sighash).*' -time=2 > "$O/micro.log" 2>&1
-  cat "$O/micro.log"
-  for m in 0 2; do
-    timeout -k 10 300 ./bin/bench_bcp -filter='ConnectBlock8MB(_160kSigops)?_GPU' -gpusighash=$m -time=3 \
-      > "$O/connect_sh$m.log" 2> "$O/connect_sh$m.err"
-    echo "== -gpusighash=$m"; cat "$O/connect_sh$m.log"
-  done ;;
+  timeout -k 10 120 ./bin/bench_bcp -filter='(CPU|GPU)_ShortIds.*' -time=2 > "$O/micro.log" 2>&1
+  cat "$O/micro.log" ;;
 hash)
   timeout -k 10 300 ./bin/bench_bcp -filter='MerkleRoot|SHA256d64|^SHA256$' -time=1 > "$O/hash.log" 2>&1
   cat "$O/hash.log" ;;

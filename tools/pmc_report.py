@@ -6,10 +6,14 @@ python tools/pmc_report.py gpurun_out/TAG [> profiles/xxx.md]
 Counters of each kernel are averaged over its dispatches (every pass runs the same dispatch
 sequence); durations come from each pass's kernel trace. Derived columns:
   VALU/wave, LDS/wave, VMEM/wave : instructions issued per wave (SQ_INSTS_* / SQ_WAVES)
-  VALU busy %  : 100 * SQ_ACTIVE_INST_VALU / CUs / GRBM_GUI_ACTIVE (rocprof's VALUBusy)
-  LDS busy %   : 100 * SQ_LDS_IDX_ACTIVE / CUs / GRBM_GUI_ACTIVE
+  VALU busy %  : 100 * 4 * SQ_ACTIVE_INST_VALU / SIMDs / (GRBM_GUI_ACTIVE / 8): the SQ_ACTIVE_*
+                 counters count quad-cycles summed over the chip, GRBM_GUI_ACTIVE is summed over
+                 the 8 XCDs (MI355X_MICROARCH.md, PMC notes); rocprof's gfx94x VALUBusy formula
+  LDS busy %   : the same normalisation of SQ_LDS_IDX_ACTIVE
   bank conf %  : 100 * SQ_LDS_BANK_CONFLICT / SQ_LDS_IDX_ACTIVE
-  waves/CU     : SQ_WAVE_CYCLES / SQ_BUSY_CYCLES-normalised mean resident waves per CU
+  waves/CU     : mean resident waves per CU, 4 * SQ_WAVE_CYCLES (quad-cycles) over SQ_BUSY_CYCLES
+                 per SQ (32 SQs)
+Kernels launched at several sizes (the ECDSA bench sweeps batch sizes) get one row per grid size.
   rd GB, wr GB : FETCH_SIZE x 2 (gfx950 tallies 128-B reads at 64 B, MI355X_MICROARCH.md) and
                  WRITE_SIZE, per dispatch; TB/s over the dispatch's duration
 """
@@ -21,6 +25,7 @@ import statistics
 import sys
 
 CUS = 256
+SIMDS = 4 * CUS
 
 
 def kname(name):
@@ -40,7 +45,10 @@ def main():
     for f in sorted(glob.glob(f"{d}/*/*_counter_collection.csv")):
         rows = collections.defaultdict(dict)
         for r in csv.DictReader(open(f)):
-            key = (r["Dispatch_Id"], kname(r["Kernel_Name"]))
+            k = kname(r["Kernel_Name"])
+            if k.startswith("ecdsa"):
+                k += " n=%d" % (int(r.get("Grid_Size", 0) or 0))
+            key = (r["Dispatch_Id"], k)
             rows[key][r["Counter_Name"]] = float(r["Counter_Value"])
             rows[key]["_ns"] = float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
         for (_, k), cs in rows.items():
@@ -66,10 +74,11 @@ def main():
         rd = 2 * m(k, "FETCH_SIZE") * 1024 / 1e9
         wr = m(k, "WRITE_SIZE") * 1024 / 1e9
         tbs = (rd + wr) / (us * 1e-6) / 1e3 if us == us else float("nan")
-        wpc = m(k, "SQ_WAVE_CYCLES") / max(m(k, "SQ_BUSY_CYCLES"), 1) / (CUS / 32)
+        wpc = 4 * m(k, "SQ_WAVE_CYCLES") / max(m(k, "SQ_BUSY_CYCLES"), 1) / (CUS / 32)
+        busy = lambda c: 100 * 4 * m(k, c) / SIMDS / (gui / 8)
         print(f"| {k} | {us:.0f} | {w:.0f} | {m(k, 'SQ_INSTS_VALU') / w:.0f} | {m(k, 'SQ_INSTS_LDS') / w:.0f} | "
               f"{m(k, 'SQ_INSTS_SALU') / w:.0f} | {m(k, 'SQ_INSTS_VMEM_RD') / w:.1f}/{m(k, 'SQ_INSTS_VMEM_WR') / w:.1f} | "
-              f"{100 * m(k, 'SQ_ACTIVE_INST_VALU') / CUS / gui:.0f} | {100 * m(k, 'SQ_LDS_IDX_ACTIVE') / CUS / gui:.0f} | "
+              f"{busy('SQ_ACTIVE_INST_VALU'):.0f} | {busy('SQ_LDS_IDX_ACTIVE'):.0f} | "
               f"{100 * m(k, 'SQ_LDS_BANK_CONFLICT') / max(m(k, 'SQ_LDS_IDX_ACTIVE'), 1):.0f} | {wpc:.1f} | "
               f"{rd:.2f} | {wr:.2f} | {tbs:.2f} |")
 
