@@ -103,19 +103,45 @@ def main(argv=None):
         run(args, world)
 
 
+def aggregate(nsol, dt, nbad, world, red_dev):
+    """Whole-job totals of the timed region: solutions and rejects summed over ranks, the
+    slowest rank's time (the job takes as long as its slowest rank)."""
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([float(nsol), dt, float(nbad)], dtype=torch.float64, device=red_dev)
+    if world == 1:
+        return float(nsol), dt, float(nbad)
+    tot = t.clone()
+    dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+    mx = t.clone()
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    return float(tot[0]), float(mx[1]), float(tot[2])
+
+
 def dry_run(world):
-    """Exercise the rank launch and the collective path without a GPU."""
+    """CPU rehearsal of the multi-rank path: the launcher, the gloo rendezvous, the barriers
+    around a timed region and the same whole-job aggregation as a real run (each rank reports a
+    synthetic solution count and time)."""
     import torch
     import torch.distributed as dist
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
         dist.init_process_group("gloo")
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))  # ranks finish at different times
+    nsol = 100 + rank
+    dt = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+    total_sols, max_dt, total_bad = aggregate(nsol, dt, 0, world, "cpu")
     t = torch.tensor([1.0, float(rank)], dtype=torch.float64)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
     if rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(t[0]),
-                          "rank_sum": int(t[1])}), flush=True)
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": int(t[0]), "rank_sum": int(t[1]),
+                          "total_solutions": total_sols, "max_rank_seconds": max_dt, "rank0_seconds": dt,
+                          "value": total_sols / max_dt}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -202,15 +228,7 @@ def run(args, world):
         nbad = sum(1 for x in ok if not x)
         verified = nbad == 0
 
-    t = torch.tensor([float(nsol), dt, float(nbad)], dtype=torch.float64, device=red_dev)
-    if world > 1:
-        tot = t.clone()
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        total_sols, max_dt, total_bad = float(tot[0]), float(mx[1]), float(tot[2])
-    else:
-        total_sols, max_dt, total_bad = float(nsol), dt, float(nbad)
+    total_sols, max_dt, total_bad = aggregate(nsol, dt, nbad, world, red_dev)
     if total_bad:
         raise SystemExit(f"bench: GPU verifier rejected {int(total_bad)} solver solution(s)")
     nonces = args.steps * args.batch * world

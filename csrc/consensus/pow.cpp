@@ -1,11 +1,13 @@
 #include "consensus/pow.h"
 #include "consensus/equihash.h"
+#include "crypto/common.h"
 #include "kernels/gpu_api.h"
 #include "node/gpuverify.h"
 #include "util/util.h"
 
 #include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <stdexcept>
 
 namespace bcp {
@@ -105,6 +107,23 @@ uint32_t GetNextCashPlusWorkRequired(const CBlockIndex* pindexPrev, const CBlock
     return nextTarget.GetCompact();
 }
 
+// CEquihashInput || nNonce (140 bytes) without a temporary vector.
+static void WriteEquihashInput(const CBlockHeader& h, uint8_t* out) {
+    auto le32 = [&](uint32_t v) {
+        WriteLE32(out, v);
+        out += 4;
+    };
+    le32((uint32_t)h.nVersion);
+    memcpy(out, h.hashPrevBlock.begin(), 32);
+    memcpy(out + 32, h.hashMerkleRoot.begin(), 32);
+    out += 64;
+    le32(h.nHeight);
+    for (int i = 0; i < 7; ++i) le32(h.nReserved[i]);
+    le32(h.nTime);
+    le32(h.nBits);
+    memcpy(out, h.nNonce.begin(), 32);
+}
+
 static CBlake2b EquihashStateFor(const CBlockHeader* pblock, const EquihashParams& ep) {
     CBlake2b st = EhInitialiseState(ep);
     std::vector<unsigned char> in = pblock->EquihashInput();
@@ -129,15 +148,24 @@ std::vector<bool> CheckEquihashSolutions(const std::vector<const CBlockHeader*>&
         // verify the same batch on the CPU. Three consecutive failures turn the GPU path off.
         try {
             if (GpuFaultInjection()) throw std::runtime_error("injected GPU Equihash-verify fault");
-            std::vector<gpu::EhBaseState> states;
-            std::vector<const std::vector<unsigned char>*> sols;
-            states.reserve(headers.size());
-            for (const CBlockHeader* h : headers) {
-                states.push_back(gpu::MakeEhBaseState(EquihashStateFor(h, ep)));
-                sols.push_back(&h->nSolution);
-            }
-            // sharded across the validation GPUs (node/gpuverify.h)
-            std::vector<uint8_t> r = GpuVerifyService::Instance().Equihash(ep.N, ep.K, states, sols);
+            // raw header bytes straight into each lane's pinned staging (its own fill workers); the
+            // device builds the BLAKE2b base states (no host hashing), sharded across the
+            // validation GPUs (node/gpuverify.h)
+            const size_t solBytes = gpu::EquihashSolutionBytes(ep.N, ep.K);
+            auto fill = [&](size_t lo, size_t hi, uint8_t* in, uint8_t* sols, uint8_t* lenok, WorkerPool& workers) {
+                workers.ParallelFor(
+                    hi - lo,
+                    [&](size_t k) {
+                        const CBlockHeader& h = *headers[lo + k];
+                        WriteEquihashInput(h, in + k * 140);
+                        const bool ok = h.nSolution.size() == solBytes;
+                        lenok[k] = ok;
+                        if (ok) memcpy(sols + k * solBytes, h.nSolution.data(), solBytes);
+                        else memset(sols + k * solBytes, 0, solBytes);
+                    },
+                    32);
+            };
+            std::vector<uint8_t> r = GpuVerifyService::Instance().EquihashHeaders(ep.N, ep.K, headers.size(), fill);
             for (size_t i = 0; i < r.size(); ++i) out[i] = r[i] != 0;
             gpuFailures = 0;
             return out;

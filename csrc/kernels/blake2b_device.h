@@ -115,6 +115,65 @@ __device__ __forceinline__ void blake2b_compress_final(const uint64_t hin[8], co
     out[7] = hin[7] ^ v7 ^ v15;
 }
 
+// One compression of a full, non-final 128-byte block (t0 = bytes hashed so far, this block
+// included): the chaining value h is updated in place.
+__device__ __forceinline__ void blake2b_compress_block(uint64_t h[8], const uint64_t m[16], uint64_t t0) {
+    const uint64_t IV0 = 0x6a09e667f3bcc908ULL, IV1 = 0xbb67ae8584caa73bULL, IV2 = 0x3c6ef372fe94f82bULL,
+                   IV3 = 0xa54ff53a5f1d36f1ULL, IV4 = 0x510e527fade682d1ULL, IV5 = 0x9b05688c2b3e6c1fULL,
+                   IV6 = 0x1f83d9abfb41bd6bULL, IV7 = 0x5be0cd19137e2179ULL;
+    uint64_t v0 = h[0], v1 = h[1], v2 = h[2], v3 = h[3], v4 = h[4], v5 = h[5], v6 = h[6], v7 = h[7];
+    uint64_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3, v12 = IV4 ^ t0, v13 = IV5, v14 = IV6, v15 = IV7;
+    for (int r = 0; r < 12; ++r) { // not unrolled: one compression per header, code size matters more
+        BCPK_B2G(v0, v4, v8, v12, m[kB2Sigma[r][0]], m[kB2Sigma[r][1]]);
+        BCPK_B2G(v1, v5, v9, v13, m[kB2Sigma[r][2]], m[kB2Sigma[r][3]]);
+        BCPK_B2G(v2, v6, v10, v14, m[kB2Sigma[r][4]], m[kB2Sigma[r][5]]);
+        BCPK_B2G(v3, v7, v11, v15, m[kB2Sigma[r][6]], m[kB2Sigma[r][7]]);
+        BCPK_B2G(v0, v5, v10, v15, m[kB2Sigma[r][8]], m[kB2Sigma[r][9]]);
+        BCPK_B2G(v1, v6, v11, v12, m[kB2Sigma[r][10]], m[kB2Sigma[r][11]]);
+        BCPK_B2G(v2, v7, v8, v13, m[kB2Sigma[r][12]], m[kB2Sigma[r][13]]);
+        BCPK_B2G(v3, v4, v9, v14, m[kB2Sigma[r][14]], m[kB2Sigma[r][15]]);
+    }
+    h[0] ^= v0 ^ v8;
+    h[1] ^= v1 ^ v9;
+    h[2] ^= v2 ^ v10;
+    h[3] ^= v3 ^ v11;
+    h[4] ^= v4 ^ v12;
+    h[5] ^= v5 ^ v13;
+    h[6] ^= v6 ^ v14;
+    h[7] ^= v7 ^ v15;
+}
+
+// The base state of a block header's Equihash input, built on the device from the raw 140 bytes
+// (CEquihashInput 108 B || nNonce 32 B): BLAKE2b with digest length (512/N)*N/8 and personal
+// "ZcashPoW" || le32(N) || le32(K) (reference src/crypto/equihash.cpp:26-36 InitialiseState),
+// the first 128 bytes compressed, the last 12 left in the final block ahead of le32(g).
+// The same state the host builds with MakeEhBaseState(EquihashStateFor(header)).
+__device__ __forceinline__ void eh_header_state(const uint8_t* in140, uint32_t N, uint32_t K, EhBaseState& bs) {
+    const uint32_t outlen = (512 / N) * N / 8;
+    uint64_t h[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
+                     0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL, 0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+    h[0] ^= (uint64_t)outlen | (1ULL << 16) | (1ULL << 24); // digest length, key 0, fanout 1, depth 1
+    h[6] ^= 0x576f50687361635aULL;                           // "ZcashPoW" (little-endian)
+    h[7] ^= (uint64_t)N | ((uint64_t)K << 32);
+    uint64_t m[16];
+    for (int i = 0; i < 16; ++i) {
+        uint64_t w = 0;
+        for (int b = 7; b >= 0; --b) w = (w << 8) | in140[8 * i + b];
+        m[i] = w;
+    }
+    blake2b_compress_block(h, m, 128);
+    for (int i = 0; i < 8; ++i) bs.h[i] = h[i];
+    uint64_t w0 = 0, w1 = 0;
+    for (int b = 7; b >= 0; --b) w0 = (w0 << 8) | in140[128 + b];
+    for (int b = 3; b >= 0; --b) w1 = (w1 << 8) | in140[136 + b];
+    bs.m[0] = w0;
+    bs.m[1] = w1;
+    for (int i = 2; i < 16; ++i) bs.m[i] = 0;
+    bs.t0 = 144;
+    bs.g_byte = 12;
+    bs.outlen = outlen;
+}
+
 // H(base || le32(g)) -> 8 chaining words (digest = first outlen bytes, little-endian).
 __device__ __forceinline__ void eh_hash_g(const EhBaseState& bs, uint32_t g, uint64_t out[8]) {
     uint64_t m[16];

@@ -84,8 +84,8 @@
 #define BCP_EH_PAIRS 1 //  0 = block scan + max-scan over pair indices (four barriers)
 #endif
 #ifndef BCP_EH_EXP_LOAD // timing experiment only: 1 = every round bucket loads one of its nonce's first 8
-#define BCP_EH_EXP_LOAD 0 //  areas (L2-resident) instead of its own (wrong results)
-#endif
+#define BCP_EH_EXP_LOAD 0 //  areas (L2-resident) instead of its own (wrong results); 2 = gather the
+#endif                    //  bucket from 512 runs of 8 rows spread over the nonce's areas
 #ifndef BCP_EH_ISSUE_LATE // 1: a round issues its next-bucket loads after the key sort, not at the commit
 #define BCP_EH_ISSUE_LATE 0
 #endif
@@ -669,6 +669,20 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // operations and wait for the prefetched words with a precise vmcnt(N) instead of vmcnt(0): a
     // vmcnt(0) at the commit would wait for the acks of the previous bucket's emit stores as well.
     auto issue = [&](int u0, int u1) {
+#if BCP_EH_EXP_LOAD == 2
+        // timing experiment: gather the bucket from 512 source runs of 8 rows (as a layout that
+        // writes every producer's output contiguously would have to), wrong results
+        const int nonce = pf_bk / C::NB, d = pf_bk % C::NB;
+        const auto rs = buf_rsrc(Rin + (size_t)nonce * C::ROWS * SWI, (uint32_t)(C::ROWS * SWI * 4));
+        const uint32_t ot = opaque_tid();
+#pragma unroll
+        for (int u = 0; u < RPL; ++u) {
+            if (u < u0 || u >= u1) continue;
+            const uint32_t r = ot + u * NT;
+            const uint32_t src = (r >> 3) & (C::NB - 1), pos = ((uint32_t)d * 8 + (r & 7)) % (uint32_t)C::AREA;
+            row_load<LWI>(rs, r < pf_n ? (src * C::AREA + pos) * (SWI * 4) : OOB, nr[u]);
+        }
+#else
         const int nonce = pf_bk / C::NB, d = BCP_EH_EXP_LOAD ? pf_bk % 8 : pf_bk % C::NB;
         const auto rs = buf_rsrc(Rin + ((size_t)nonce * C::ROWS + (size_t)d * C::AREA) * SWI, CAP * SWI * 4);
         const uint32_t ot = opaque_tid();
@@ -678,6 +692,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             const uint32_t r = ot + u * NT;
             row_load<LWI>(rs, r < pf_n ? r * (SWI * 4) : OOB, nr[u]);
         }
+#endif
     };
 
     // prologue: first bucket in flight, fill of the second known

@@ -130,6 +130,17 @@ __global__ __launch_bounds__(C::NTH) void eh_verify(const EhBaseState* __restric
     if (t == 0) ok[item] = bad ? 0 : 1;
 }
 
+// One lane per header: the base state from the raw 140-byte Equihash input (header prep on the
+// device instead of a host BLAKE2b per header).
+__global__ __launch_bounds__(64) void eh_state_kernel(const uint8_t* __restrict__ in140, EhBaseState* __restrict__ out,
+                                                      uint32_t N, uint32_t K, int n) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    EhBaseState bs;
+    eh_header_state(in140 + (size_t)i * 140, N, K, bs);
+    out[i] = bs;
+}
+
 } // namespace bcpk
 
 namespace bcp {
@@ -168,6 +179,46 @@ static void verify_lane(LaneState& L, const EhBaseState* states, const std::vect
     L.batches++;
     L.items += n;
 }
+
+// Raw headers: `fill` writes n x 140 input bytes, n x SOLW solution bytes and n length flags
+// straight into the pinned staging; one H2D copy, the state kernel, the verify kernel, one D2H.
+template <class C>
+static void verify_lane_headers(LaneState& L, size_t n, const std::function<void(uint8_t*, uint8_t*, uint8_t*)>& fill,
+                                uint8_t* result) {
+    if (n == 0) return;
+    BCP_HIP_CHECK(hipSetDevice(L.device));
+    const size_t ib = (n * 140 + 15) & ~(size_t)15, pb = n * C::SOLW;
+    unsigned char* h_in = L.Host(0, ib + pb + n);
+    uint8_t* lenok = h_in + ib + pb;
+    fill(h_in, h_in + ib, lenok);
+    uint8_t* h_ok = L.Host(1, n);
+    unsigned char* d_in = L.Dev(0, ib + pb);
+    bcpk::EhBaseState* d_states = reinterpret_cast<bcpk::EhBaseState*>(L.Dev(2, n * sizeof(bcpk::EhBaseState)));
+    uint8_t* d_ok = L.Dev(1, n);
+    BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, ib + pb, hipMemcpyHostToDevice, L.stream));
+    hipLaunchKernelGGL(bcpk::eh_state_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, L.stream,
+                       (const uint8_t*)d_in, d_states, (uint32_t)C::N, (uint32_t)C::K, (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL((bcpk::eh_verify<C>), dim3(n), dim3(C::NTH), 0, L.stream, (const bcpk::EhBaseState*)d_states,
+                       (const uint8_t*)(d_in + ib), d_ok);
+    BCP_HIP_CHECK(hipGetLastError());
+    BCP_HIP_CHECK(hipMemcpyAsync(h_ok, d_ok, n, hipMemcpyDeviceToHost, L.stream));
+    BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
+    for (size_t i = 0; i < n; ++i) result[i] = lenok[i] ? h_ok[i] : 0;
+    L.batches++;
+    L.items += n;
+}
+
+void VerifyLane::EquihashHeaders(unsigned N, unsigned K, size_t n,
+                                 const std::function<void(uint8_t*, uint8_t*, uint8_t*)>& fill, uint8_t* result) {
+    if (N == 200 && K == 9) return verify_lane_headers<bcpk::EvCfg<200, 9>>(*impl, n, fill, result);
+    if (N == 96 && K == 5) return verify_lane_headers<bcpk::EvCfg<96, 5>>(*impl, n, fill, result);
+    if (N == 48 && K == 5) return verify_lane_headers<bcpk::EvCfg<48, 5>>(*impl, n, fill, result);
+    if (N == 96 && K == 3) return verify_lane_headers<bcpk::EvCfg<96, 3>>(*impl, n, fill, result);
+    throw std::invalid_argument("EquihashVerifyBatch: unsupported (N,K)");
+}
+
+size_t EquihashSolutionBytes(unsigned N, unsigned K) { return ((size_t)1 << K) * (N / (K + 1) + 1) / 8; }
 
 VerifyLane::VerifyLane(int device, bool highPriority) : impl(new Impl) {
     impl->device = UseDevice(device);

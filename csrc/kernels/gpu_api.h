@@ -32,6 +32,8 @@ struct EhBaseState {
 // Build the g-independent state from a BLAKE2b state that already absorbed
 // CEquihashInput || nNonce (the solver/verifier then appends le32(g)).
 EhBaseState MakeEhBaseState(const CBlake2b& st);
+// Bytes of a minimal-encoded (N, K) solution (1344 for (200, 9)).
+size_t EquihashSolutionBytes(unsigned N, unsigned K);
 
 struct EhGpuStats {
     uint64_t nonces = 0;
@@ -134,6 +136,13 @@ public:
     void EcdsaFill(size_t n, const std::function<void(unsigned char* msg32, unsigned char* sig64,
                                                         unsigned char* pub33)>& fill,
                    uint8_t* result);
+    // n block headers: fill(in140, sols, lenok) writes each header's 140-byte Equihash input
+    // (CEquihashInput || nNonce), its solution (EquihashSolutionBytes bytes) and whether the
+    // solution had that length into the lane's pinned staging; the device builds the BLAKE2b
+    // base states and verifies. result[i] = 1 iff header i's solution is valid.
+    void EquihashHeaders(unsigned N, unsigned K, size_t n,
+                         const std::function<void(uint8_t* in140, uint8_t* sols, uint8_t* lenok)>& fill,
+                         uint8_t* result);
     // Same contract as EquihashVerifyBatch for n (state, solution) pairs; a solution of the
     // wrong length is rejected.
     void Equihash(unsigned N, unsigned K, const EhBaseState* states, const std::vector<unsigned char>* const* sols,

@@ -39,11 +39,24 @@ void GpuVerifyService::SetDevices(const std::vector<int>& devs) {
     lanesStale = true;
 }
 
+// Default: every visible device, two lanes each (the built-in miner runs only on demand, and
+// its streams share a device at a lower priority than validation's). Two lanes per device let
+// one shard's host fill overlap the other's kernels: a 199k-signature batch took 10.5 ms on one
+// lane and 8.8 ms on two of the same MI355X (profiles/lanes_headers_r4.md).
+static std::vector<int> AllDevices() {
+    std::vector<int> d;
+    if (!gpu::GpuAvailable()) return d;
+    for (int i = 0; i < gpu::DeviceCount(); i++) {
+        d.push_back(i);
+        d.push_back(i);
+    }
+    return d;
+}
+
 std::vector<int> GpuVerifyService::Devices() const {
     std::lock_guard<std::mutex> l(m);
     if (!devices.empty()) return devices;
-    if (gpu::GpuAvailable()) return {0};
-    return {};
+    return AllDevices();
 }
 
 std::vector<int> GpuVerifyService::ConfiguredDevices() const {
@@ -86,11 +99,16 @@ std::vector<std::shared_ptr<GpuVerifyService::Lane>> GpuVerifyService::AcquireLa
         std::lock_guard<std::mutex> l(m);
         if (lanesStale) {
             std::vector<int> devs = devices;
-            if (devs.empty() && gpu::GpuAvailable()) devs = {0};
+            if (devs.empty()) devs = AllDevices();
             retire.swap(lanes);
+            // host-fill workers: the cores split between the lanes (a caller thread joins each),
+            // at most 16 per lane (a fill is a few hundred microseconds: waking more threads than
+            // that costs more than they save)
+            const int perLane = std::min(16, std::max(1, (GetNumCores() - 1) / std::max<int>(1, (int)devs.size())));
             for (int d : devs) {
                 auto L = std::make_shared<Lane>();
                 L->device = d;
+                L->fill.reset(new WorkerPool(perLane - 1));
                 L->th = std::thread(LaneLoop, L.get());
                 lanes.push_back(L);
             }
@@ -110,7 +128,7 @@ std::vector<std::shared_ptr<GpuVerifyService::Lane>> GpuVerifyService::AcquireLa
 }
 
 void GpuVerifyService::RunSharded(size_t n, size_t minShard,
-                                  const std::function<void(gpu::VerifyLane&, size_t, size_t)>& fn) {
+                                  const std::function<void(gpu::VerifyLane&, size_t, size_t, WorkerPool&)>& fn) {
     std::vector<std::shared_ptr<Lane>> ls = AcquireLanes();
     if (ls.empty()) throw std::runtime_error("GpuVerifyService: no validation GPU");
     const size_t shards = std::max<size_t>(1, std::min(ls.size(), n / minShard));
@@ -135,7 +153,7 @@ void GpuVerifyService::RunSharded(size_t n, size_t minShard,
             try {
                 if (!L->gl) throw std::runtime_error("GPU verify lane on device " + std::to_string(L->device) +
                                                      " unavailable: " + L->initError);
-                fn(*L->gl, lo, hi);
+                fn(*L->gl, lo, hi, *L->fill);
                 L->batches++;
                 L->items += hi - lo;
             } catch (...) {
@@ -176,15 +194,13 @@ std::vector<uint8_t> GpuVerifyService::Ecdsa(const unsigned char* msg32, const u
         std::lock_guard<std::mutex> l(m);
         minShard = minShardEcdsa;
     }
-    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi) {
+    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi, WorkerPool&) {
         lane.Ecdsa(msg32 + lo * 32, sig64 + lo * 64, pub33 + lo * 33, hi - lo, out.data() + lo);
     });
     return out;
 }
 
-std::vector<uint8_t> GpuVerifyService::EcdsaFill(
-    size_t n,
-    const std::function<void(size_t, size_t, unsigned char*, unsigned char*, unsigned char*)>& fill) {
+std::vector<uint8_t> GpuVerifyService::EcdsaFill(size_t n, const EcdsaFillFn& fill) {
     std::vector<uint8_t> out(n, 0);
     if (n == 0) return out;
     size_t minShard;
@@ -192,9 +208,26 @@ std::vector<uint8_t> GpuVerifyService::EcdsaFill(
         std::lock_guard<std::mutex> l(m);
         minShard = minShardEcdsa;
     }
-    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi) {
+    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi, WorkerPool& workers) {
         lane.EcdsaFill(
-            hi - lo, [&](unsigned char* msg, unsigned char* sig, unsigned char* pub) { fill(lo, hi, msg, sig, pub); },
+            hi - lo,
+            [&](unsigned char* msg, unsigned char* sig, unsigned char* pub) { fill(lo, hi, msg, sig, pub, workers); },
+            out.data() + lo);
+    });
+    return out;
+}
+
+std::vector<uint8_t> GpuVerifyService::EquihashHeaders(unsigned N, unsigned K, size_t n, const HeaderFillFn& fill) {
+    std::vector<uint8_t> out(n, 0);
+    if (n == 0) return out;
+    size_t minShard;
+    {
+        std::lock_guard<std::mutex> l(m);
+        minShard = minShardEquihash;
+    }
+    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi, WorkerPool& workers) {
+        lane.EquihashHeaders(
+            N, K, hi - lo, [&](uint8_t* in, uint8_t* sols, uint8_t* lenok) { fill(lo, hi, in, sols, lenok, workers); },
             out.data() + lo);
     });
     return out;
@@ -211,7 +244,7 @@ std::vector<uint8_t> GpuVerifyService::Equihash(unsigned N, unsigned K, const st
         std::lock_guard<std::mutex> l(m);
         minShard = minShardEquihash;
     }
-    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi) {
+    RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi, WorkerPool&) {
         lane.Equihash(N, K, states.data() + lo, sols.data() + lo, hi - lo, out.data() + lo);
     });
     return out;

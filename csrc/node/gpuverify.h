@@ -9,14 +9,19 @@
 //    kernels on a shared device) and its pinned staging buffers (gpu::VerifyLane);
 //  * a batch is split into contiguous shards, one per lane, that run concurrently on their
 //    devices; per-item verdicts are gathered in order (the caller AND-reduces);
-//  * -gpuvalidationdevices selects the devices (default: device 0); the built-in miner leaves
-//    those devices alone whenever other GPUs are available (miner.cpp GetMinerGpuDevices);
+//  * -gpuvalidationdevices selects the devices (default: every visible device, two lanes each); the built-in
+//    miner leaves configured validation devices alone whenever other GPUs are available
+//    (miner.cpp GetMinerGpuDevices);
 //  * a lane failure fails the whole call (the caller re-verifies on the CPU: a device fault
-//    must never decide validity).
+//    must never decide validity);
+//  * each lane has its own host-fill workers (a share of the cores), so the shards' host
+//    preparation (DER parse, key forms, header bytes) runs concurrently instead of queueing on
+//    one pool.
 // A device may be listed twice (two lanes on one GPU, two streams): the test suite uses that
 // to exercise the sharded path on a one-GPU box.
 #pragma once
 #include "kernels/gpu_api.h"
+#include "util/util.h"
 
 #include <atomic>
 #include <condition_variable>
@@ -36,8 +41,8 @@ public:
     static GpuVerifyService& Instance();
     ~GpuVerifyService();
 
-    // Validation devices (duplicates allowed: one lane each). Empty = default ({0} when a GPU
-    // is visible). Takes effect for the next batch; running batches finish on the old lanes.
+    // Validation devices (duplicates allowed: one lane each). Empty = default (every visible
+    // device, twice). Takes effect for the next batch; running batches finish on the old lanes.
     void SetDevices(const std::vector<int>& devices);
     std::vector<int> Devices() const;           // resolved list
     std::vector<int> ConfiguredDevices() const; // as set (empty: default)
@@ -47,10 +52,17 @@ public:
     // result[i] = 1 iff job i is valid (gpu::EcdsaVerifyBatch contract, packed arrays).
     std::vector<uint8_t> Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33,
                                size_t n);
-    // The same batch with its inputs produced in place: fill(lo, hi, msg32, sig64, pub33) writes
-    // jobs [lo, hi) into a lane's pinned staging arrays (indexed from 0 = job lo).
-    std::vector<uint8_t> EcdsaFill(size_t n, const std::function<void(size_t lo, size_t hi, unsigned char* msg32,
-                                                                      unsigned char* sig64, unsigned char* pub33)>& fill);
+    // The same batch with its inputs produced in place: fill(lo, hi, msg32, sig64, pub33, workers)
+    // writes jobs [lo, hi) into a lane's pinned staging arrays (indexed from 0 = job lo), using
+    // that lane's own fill workers.
+    using EcdsaFillFn = std::function<void(size_t lo, size_t hi, unsigned char* msg32, unsigned char* sig64,
+                                           unsigned char* pub33, WorkerPool& workers)>;
+    std::vector<uint8_t> EcdsaFill(size_t n, const EcdsaFillFn& fill);
+    // Block headers [0, n): fill(lo, hi, in140, sols, lenok, workers) writes headers [lo, hi)
+    // (gpu::VerifyLane::EquihashHeaders layout); the device builds the BLAKE2b states.
+    using HeaderFillFn = std::function<void(size_t lo, size_t hi, uint8_t* in140, uint8_t* sols, uint8_t* lenok,
+                                            WorkerPool& workers)>;
+    std::vector<uint8_t> EquihashHeaders(unsigned N, unsigned K, size_t n, const HeaderFillFn& fill);
     // result[i] = 1 iff solution i is valid for state i.
     std::vector<uint8_t> Equihash(unsigned N, unsigned K, const std::vector<gpu::EhBaseState>& states,
                                   const std::vector<const std::vector<unsigned char>*>& sols);
@@ -78,12 +90,13 @@ private:
         std::string initError;
         std::atomic<int> priority{0};
         std::atomic<uint64_t> batches{0}, items{0};
+        std::unique_ptr<WorkerPool> fill; // this lane's host-fill workers
     };
     static void LaneLoop(Lane* L);
     std::vector<std::shared_ptr<Lane>> AcquireLanes();
-    // Runs fn(lane, lo, hi) for the shards of [0, n) and waits; rethrows the first failure.
+    // Runs fn(lane, lo, hi, workers) for the shards of [0, n) and waits; rethrows the first failure.
     void RunSharded(size_t n, size_t minShard,
-                    const std::function<void(gpu::VerifyLane&, size_t, size_t)>& fn);
+                    const std::function<void(gpu::VerifyLane&, size_t, size_t, WorkerPool&)>& fn);
 
     mutable std::mutex m;
     std::vector<int> devices;

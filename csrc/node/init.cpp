@@ -56,7 +56,7 @@ std::string HelpMessage() {
         {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 512)"},
         {"-gpushortidthreshold=<n>", "Smallest mempool whose compact-block short ids are computed on the GPU (default: 16384)"},
         {"-gpudevices=<list>", "Comma-separated GPU indices the built-in Equihash miner runs on, one host thread per device (default: all visible)"},
-        {"-gpuvalidationdevices=<list>", "Comma-separated GPU indices that verify block signatures and header solutions, one high-priority stream and service thread each; batches are sharded across them. When set, the built-in miner leaves these devices alone if others are available (default: device 0, shared with the miner)"},
+        {"-gpuvalidationdevices=<list>", "Comma-separated GPU indices that verify block signatures and header solutions, one high-priority stream, service thread and host-fill worker group each; batches are sharded across them. When set, the built-in miner leaves these devices alone if others are available (default: every visible device, two lanes each)"},
         {"-maxsigcachesize=<n>", "Limit size of signature cache to <n> MiB (default: 32)"},
         {"-maxscriptcachesize=<n>", "Limit size of script cache to <n> MiB (default: 32)"},
         {"-blocknotify=<cmd>", "Execute command when the best block changes (%s in cmd is replaced by block hash)"},

@@ -101,21 +101,23 @@ static bool PrepSigAndKey(const DeferredSigCheck& c, unsigned char* sig64, unsig
     return ok;
 }
 
-std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool) {
+std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks) {
     // host: DER parse + low-S normalisation + key form, written by the pool straight into the
     // verify lane's pinned staging buffer; device: scalar prep, decompression + ecmult
     const size_t n = checks.size();
     std::vector<uint8_t> hostOk(n, 1);
     if (GpuFaultInjection()) throw std::runtime_error("injected GPU signature-verify fault");
-    auto fill = [&](size_t lo, size_t hi, unsigned char* msg, unsigned char* sig, unsigned char* pub) {
-        auto one = [&](size_t k) {
-            const DeferredSigCheck& c = *checks[lo + k];
-            memcpy(&msg[k * 32], c.sighash.begin(), 32);
-            if (!PrepSigAndKey(c, &sig[k * 64], &pub[k * 33])) hostOk[lo + k] = 0;
-        };
-        if (pool) pool->ParallelFor(hi - lo, one, 64);
-        else
-            for (size_t k = 0; k < hi - lo; k++) one(k);
+    // each lane's shard is filled by that lane's own workers, concurrently with the other lanes
+    auto fill = [&](size_t lo, size_t hi, unsigned char* msg, unsigned char* sig, unsigned char* pub,
+                    WorkerPool& workers) {
+        workers.ParallelFor(
+            hi - lo,
+            [&](size_t k) {
+                const DeferredSigCheck& c = *checks[lo + k];
+                memcpy(&msg[k * 32], c.sighash.begin(), 32);
+                if (!PrepSigAndKey(c, &sig[k * 64], &pub[k * 33])) hostOk[lo + k] = 0;
+            },
+            64);
     };
     // sharded across the validation GPUs by the verify service (one high-priority lane each)
     std::vector<uint8_t> res = GpuVerifyService::Instance().EcdsaFill(n, fill);
@@ -186,7 +188,7 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
             for (size_t j = 0; j < n; j++) ptrs[j] = checks[todo[j]];
             std::vector<uint8_t> r;
             try {
-                r = GpuVerifyDeferred(ptrs, pool);
+                r = GpuVerifyDeferred(ptrs);
                 g_gpuFailures = 0;
             } catch (const std::exception& e) {
                 const int fails = ++g_gpuFailures;

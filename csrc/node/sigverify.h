@@ -72,7 +72,7 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
                            const std::vector<DeferredMultisig>& groups, WorkerPool* pool, bool useGpu,
                            bool cacheStore, bool cacheErase);
 // Device verification of the given checks (no cache); result[i] = 1 iff valid.
-std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks, WorkerPool* pool);
+std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks);
 void SetGpuSigThreshold(size_t n);   // minimum batch size for the GPU path
 size_t GetGpuSigThreshold();
 void ResetGpuSigFailures();

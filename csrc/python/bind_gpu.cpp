@@ -233,7 +233,7 @@ void bind_gpu(pyb::module_& m) {
                 if (use_gpu) {
                     std::vector<const DeferredSigCheck*> ptrs;
                     for (auto& c : checks) ptrs.push_back(&c);
-                    res = GpuVerifyDeferred(ptrs, &pool);
+                    res = GpuVerifyDeferred(ptrs);
                 } else {
                     pool.ParallelFor(checks.size(), [&](size_t i) {
                         const DeferredSigCheck& c = checks[i];

@@ -176,7 +176,7 @@ void bind_script(pyb::module_& m) {
             {
                 pyb::gil_scoped_release rel;
                 if (use_gpu && !sink.empty()) {
-                    res = GpuVerifyDeferred(ptrs, nullptr);
+                    res = GpuVerifyDeferred(ptrs);
                 } else {
                     for (size_t j = 0; j < sink.size(); j++) {
                         const DeferredSigCheck& c = sink[j];

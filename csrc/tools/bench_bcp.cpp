@@ -20,6 +20,9 @@
 #include "script/sign.h"
 #include "script/standard.h"
 #include "node/sigverify.h"
+#include "node/gpuverify.h"
+#include "consensus/pow.h"
+#include "consensus/equihash.h"
 #include "secp256k1/secp256k1.h"
 #include "node/txmempool.h"
 #include "node/validation.h"
@@ -65,8 +68,9 @@ public:
         std::sort(s.begin(), s.end());
         double total = 0;
         for (double d : s) total += d;
-        printf("%-34s %10zu %14.9f %14.9f %14.9f %14.9f\n", name.c_str(), s.size(), total, s.front(), s.back(),
-               s[s.size() / 2]);
+        // quartiles for the spread (IQR = p75 - p25)
+        printf("%-34s %10zu %14.9f %14.9f %14.9f %14.9f %14.9f %14.9f\n", name.c_str(), s.size(), total, s.front(),
+               s.back(), s[s.size() / 2], s[s.size() / 4], s[(3 * s.size()) / 4]);
         fflush(stdout);
     }
 
@@ -540,6 +544,110 @@ static void ShortIdBench(State& st, bool gpuPath) {
 }
 static bench::Reg reg_CpuShortId("CPU_ShortIds_250k", [](State& st) { ShortIdBench(st, false); });
 static bench::Reg reg_GpuShortId("GPU_ShortIds_250k", [](State& st) { ShortIdBench(st, true); });
+
+// ---- verify-service sharding overhead on one GPU: the same batch over lanes [0], [0,0] and
+// [0,0,0,0] (one stream and one host-fill worker group each). 199k deferred ECDSA checks
+// (1024 distinct signatures repeated, end to end from DeferredSigCheck records: DER parse, key
+// forms, upload, prep + verify kernels, verdicts) and a 2000-header Equihash(200,9) batch
+// (CheckEquihashSolutions: raw header bytes staged, BLAKE2b states and verification on the
+// device; random solutions cost the kernel the same as valid ones).
+static void LanesEcdsa(State& st, int lanes) {
+    if (!gpu::GpuAvailable()) return;
+    static std::vector<DeferredSigCheck> checks;
+    if (checks.empty()) {
+        std::vector<DeferredSigCheck> uniq(1024);
+        for (size_t i = 0; i < uniq.size(); i++) {
+            CKey key;
+            key.MakeNewKey(true);
+            uint256 h;
+            Sha256d((const unsigned char*)&i, sizeof(i), h.begin());
+            std::vector<unsigned char> sig;
+            key.Sign(h, sig);
+            uniq[i].sighash = h;
+            uniq[i].sig.assign(sig);
+            uniq[i].pubkey.assign(key.GetPubKey().Raw());
+        }
+        checks.resize(199000);
+        for (size_t i = 0; i < checks.size(); i++) checks[i] = uniq[i % uniq.size()];
+    }
+    std::vector<const DeferredSigCheck*> ptrs(checks.size());
+    for (size_t i = 0; i < checks.size(); i++) ptrs[i] = &checks[i];
+    GpuVerifyService& svc = GpuVerifyService::Instance();
+    svc.SetDevices(std::vector<int>(lanes, 0));
+    svc.SetMinShard(1024, 64);
+    std::vector<uint8_t> r = GpuVerifyDeferred(ptrs); // lanes up, buffers grown
+    while (st.KeepRunning()) r = GpuVerifyDeferred(ptrs);
+    if (std::count(r.begin(), r.end(), 1) != (long)r.size()) {
+        fprintf(stderr, "LanesEcdsa: %zu of %zu verdicts false\n", (size_t)std::count(r.begin(), r.end(), 0), r.size());
+        exit(1);
+    }
+    svc.SetMinShard(256, 32);
+    svc.SetDevices({});
+}
+static bench::Reg reg_LanesEcdsa1("Lanes1_Ecdsa199k_GPU", [](State& st) { LanesEcdsa(st, 1); });
+static bench::Reg reg_LanesEcdsa2("Lanes2_Ecdsa199k_GPU", [](State& st) { LanesEcdsa(st, 2); });
+static bench::Reg reg_LanesEcdsa4("Lanes4_Ecdsa199k_GPU", [](State& st) { LanesEcdsa(st, 4); });
+
+static void LanesHeaders(State& st, int lanes) {
+    if (!gpu::GpuAvailable()) return;
+    SelectParams("main");
+    static std::vector<CBlockHeader> headers;
+    if (headers.empty()) {
+        FastRandomContext rng(true);
+        headers.resize(2000);
+        for (CBlockHeader& h : headers) {
+            h.nVersion = 4;
+            h.hashPrevBlock = rng.rand256();
+            h.hashMerkleRoot = rng.rand256();
+            h.nTime = 1500000000 + rng.rand32() % 1000000;
+            h.nBits = 0x1d00ffff;
+            h.nNonce = rng.rand256();
+            h.nSolution.resize(1344);
+            for (auto& b : h.nSolution) b = (unsigned char)rng.rand32();
+        }
+    }
+    std::vector<const CBlockHeader*> ptrs;
+    for (const CBlockHeader& h : headers) ptrs.push_back(&h);
+    GpuVerifyService& svc = GpuVerifyService::Instance();
+    svc.SetDevices(std::vector<int>(lanes, 0));
+    svc.SetMinShard(1024, 64);
+    std::vector<bool> r = CheckEquihashSolutions(ptrs, Params(), true);
+    while (st.KeepRunning()) r = CheckEquihashSolutions(ptrs, Params(), true);
+    svc.SetMinShard(256, 32);
+    svc.SetDevices({});
+}
+static bench::Reg reg_LanesHdr1("Lanes1_Headers2000_GPU", [](State& st) { LanesHeaders(st, 1); });
+static bench::Reg reg_LanesHdr2("Lanes2_Headers2000_GPU", [](State& st) { LanesHeaders(st, 2); });
+static bench::Reg reg_LanesHdr4("Lanes4_Headers2000_GPU", [](State& st) { LanesHeaders(st, 4); });
+// the same 2000 headers with host-built states (the round-3 path), for the prep split
+static void HeadersHostStates(State& st) {
+    if (!gpu::GpuAvailable()) return;
+    SelectParams("main");
+    const EquihashParams ep(200, 9);
+    FastRandomContext rng(true);
+    std::vector<CBlockHeader> headers(2000);
+    for (CBlockHeader& h : headers) {
+        h.nVersion = 4;
+        h.hashPrevBlock = rng.rand256();
+        h.nNonce = rng.rand256();
+        h.nSolution.resize(1344);
+        for (auto& b : h.nSolution) b = (unsigned char)rng.rand32();
+    }
+    while (st.KeepRunning()) {
+        std::vector<gpu::EhBaseState> states;
+        std::vector<const std::vector<unsigned char>*> sols;
+        for (const CBlockHeader& h : headers) {
+            CBlake2b b = EhInitialiseState(ep);
+            std::vector<unsigned char> in = h.EquihashInput();
+            b.Write(in.data(), in.size());
+            b.Write(h.nNonce.begin(), 32);
+            states.push_back(gpu::MakeEhBaseState(b));
+            sols.push_back(&h.nSolution);
+        }
+        GpuVerifyService::Instance().Equihash(200, 9, states, sols);
+    }
+}
+BENCHMARK(HeadersHostStates);
 
 // ---- 8 MB block connect (BASELINE.md "block connect time for an 8 MB / 160k-sigop block"): a
 // regtest chain past the BCP fork (Equihash(48,5) headers) in a memory-only chainstate, one big
@@ -1031,7 +1139,8 @@ int main(int argc, char* argv[]) {
         for (const auto& b : bench::Registry()) printf("%s\n", b.first.c_str());
         return 0;
     }
-    printf("# %-32s %10s %14s %14s %14s %14s\n", "Benchmark", "iterations", "total", "min", "max", "median");
+    printf("# %-32s %10s %14s %14s %14s %14s %14s %14s\n", "Benchmark", "iterations", "total", "min", "max", "median",
+           "p25", "p75");
     for (const auto& b : bench::Registry()) {
         if (!std::regex_match(b.first, filter)) continue;
         State st(b.first, minTime);

@@ -27,6 +27,22 @@ def test_launcher_spawns_n_ranks():
     assert out["n_gpus"] == 3 and out["ranks_seen"] == 3 and out["rank_sum"] == 0 + 1 + 2
 
 
+def test_eight_rank_rehearsal():
+    """The N=8 shape the driver runs on an 8-GPU node, rehearsed on the CPU over gloo: eight ranks
+    rendezvous, time a region between barriers, and rank 0 alone reports the whole-job value
+    from the summed solutions and the slowest rank's time."""
+    p = subprocess.run([sys.executable, BENCH, "--gpus", "8", "--dry-run"], capture_output=True, text=True,
+                       env=_env(), timeout=480)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = lines[0]
+    assert out["n_gpus"] == 8 and out["ranks_seen"] == 8 and out["rank_sum"] == sum(range(8))
+    assert out["total_solutions"] == sum(100 + r for r in range(8))
+    assert out["max_rank_seconds"] >= 0.08 > out["rank0_seconds"]  # the slowest rank (7) sets the time
+    assert abs(out["value"] - out["total_solutions"] / out["max_rank_seconds"]) < 1e-6
+
+
 def test_refuses_more_gpus_than_visible():
     # this container has no GPU: asking for 2 real ranks must fail before anything starts
     p = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1"], capture_output=True, text=True,

@@ -88,6 +88,51 @@ def test_sharded_equihash_headers_match_cpu(native, two_lanes):
     assert all(l["items"] > 0 for l in native.gpu_verify_stats()["lanes"])
 
 
+@pytest.mark.gpu
+def test_raw_header_batches_match_cpu(native, two_lanes):
+    """Header batches through CheckEquihashSolutions' GPU path: the device builds each header's
+    BLAKE2b base state from the raw 140 bytes (eh_state_kernel), the lanes fill their shards on
+    their own workers. Valid regtest (48,5) and mainnet (200,9) headers, plus corrupted ones
+    (a header field, the nonce, a solution byte, a short solution), against the CPU verdicts."""
+    from test_equihash import header_input
+
+    def compact(n):
+        return bytes([n]) if n < 253 else b"\xfd" + struct.pack("<H", n)
+
+    for n, k, chain, nonces in [(48, 5, "regtest", 40), (200, 9, "main", 6)]:
+        solver = native.EquihashGpuSolver(n, k, nonces)
+        datas, states = [], []
+        for i in range(nonces):
+            data = header_input(i, b"rawhdr%d" % n)
+            st = native.EquihashState(n, k)
+            st.update(data)
+            datas.append(data)
+            states.append(st)
+        batch = []
+        for data, ss in zip(datas, solver.solve(states)):
+            for s in ss[:2]:
+                batch.append(data + compact(len(s)) + s)
+        assert len(batch) >= 8
+        rng = random.Random(n)
+        for h in list(batch[:6]):
+            b = bytearray(h)
+            which = rng.randrange(4)
+            if which == 0:
+                b[rng.randrange(4, 108)] ^= 1 << rng.randrange(8)   # a header field
+            elif which == 1:
+                b[rng.randrange(108, 140)] ^= 1 << rng.randrange(8)  # the nonce
+            elif which == 2:
+                b[-1 - rng.randrange(20)] ^= 1 << rng.randrange(8)   # the solution
+            else:
+                ln = len(h) - 140 - len(compact(len(h)))
+                b = bytearray(h[:140] + compact(ln - 1) + h[-(ln - 1):])  # one byte short
+            batch.append(bytes(b))
+        cpu = native.check_equihash_headers(batch, chain, False)
+        gpu = native.check_equihash_headers(batch, chain, True)
+        assert gpu == cpu and any(cpu) and not all(cpu)
+    assert all(l["items"] > 0 for l in native.gpu_verify_stats()["lanes"])
+
+
 # ------------------------------------------------------------------ randomized differential
 
 def _mutate_sig(rng, pub, sig, msg):

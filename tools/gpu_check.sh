@@ -23,6 +23,9 @@
 #   connect TAG [BLOCKS] 8 MB block connects CPU vs GPU, the IBD pipeline, and a kernel profile
 #                        of the 160k-sigop GPU connect
 #   relay TAG            BIP152 short-id kernel: GPU tests and the CPU vs GPU micro-bench
+#   lanes TAG            verify-service tests, then a 199k-signature and a 2000-header batch over
+#                        lanes [0], [0,0], [0,0,0,0] (sharding overhead) and the host-built-state
+#                        header path, with a kernel trace of the 2000-header runs
 #   hash TAG             SHA256d64 / merkle micro-benches (CPU SHA-NI vs GPU)
 #   baseline TAG         BASELINE.md secondary metrics (tools/baseline_metrics.py + bench_bcp)
 #   multirank TAG        bench.py as 2 ranks on one GPU over gloo (the multi-rank launcher path)
@@ -151,6 +154,14 @@ relay)
   tail -n 3 "$O/pytest.log"
   timeout -k 10 120 ./bin/bench_bcp -filter='(CPU|GPU)_ShortIds.*' -time=2 > "$O/micro.log" 2>&1
   cat "$O/micro.log" ;;
+lanes)
+  timeout -k 10 400 python -u -m pytest tests/test_gpu_verify_service.py -m gpu -x -v --timeout 300 --timeout-method thread \
+    > "$O/pytest.log" 2>&1 || { tail -n 30 "$O/pytest.log"; exit 1; }
+  tail -n 2 "$O/pytest.log"
+  timeout -k 10 300 ./bin/bench_bcp -filter='Lanes.*|HeadersHostStates' -time=3 > "$O/lanes.log" 2>&1
+  cat "$O/lanes.log"
+  (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --stats -d "$O/prof" -o hdr -- "$R/bin/bench_bcp" \
+    -filter='Lanes1_Headers2000_GPU|Lanes1_Ecdsa199k_GPU' -time=2 > "$O/prof.log" 2>&1) ;;
 hash)
   timeout -k 10 300 ./bin/bench_bcp -filter='MerkleRoot|SHA256d64|^SHA256$' -time=1 > "$O/hash.log" 2>&1
   cat "$O/hash.log" ;;
