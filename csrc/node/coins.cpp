@@ -220,6 +220,12 @@ void CCoinsViewCache::SpendFetched(const COutPoint& outpoint, Coin&& coin, Coin*
     if (moveto) *moveto = std::move(coin);
 }
 
+void CCoinsViewCache::SpendFetchedMoved(const COutPoint& outpoint) {
+    auto ins = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
+    assert(ins.second);
+    ins.first->second.flags = CCoinsCacheEntry::DIRTY; // not FRESH: the base holds the coin
+}
+
 bool CCoinsViewCache::HaveCoin(const COutPoint& outpoint) const {
     auto it = FetchCoin(outpoint);
     return it != cacheCoins.end() && !it->second.coin.IsSpent();

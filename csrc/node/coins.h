@@ -231,6 +231,9 @@ public:
     // (read through PeekCoin while the stack below was as it is now): the same entry FetchCoin
     // followed by SpendCoin would leave, without the round trip through the base.
     void SpendFetched(const COutPoint& outpoint, Coin&& coin, Coin* moveto);
+    // The same entry when the caller already moved the base's copy of the coin elsewhere (into
+    // an undo record): a spent, DIRTY, not FRESH entry.
+    void SpendFetchedMoved(const COutPoint& outpoint);
     void AddCoin(const COutPoint& outpoint, Coin&& coin, bool possible_overwrite);
     bool SpendCoin(const COutPoint& outpoint, Coin* moveto = nullptr);
     bool Flush();
@@ -238,6 +241,7 @@ public:
     unsigned int GetCacheSize() const { return (unsigned)cacheCoins.size(); }
     // Sizes the entry table for n entries up front (a block connect knows how many it adds).
     void Reserve(size_t n) { cacheCoins.reserve(n); }
+    size_t BucketCount() const { return cacheCoins.bucket_count(); }
     size_t DynamicMemoryUsage() const;
     Amount GetValueIn(const CTransaction& tx) const;
     bool HaveInputs(const CTransaction& tx) const;

@@ -4,6 +4,7 @@
 #include "node/ui_interface.h"
 #include "node/warnings.h"
 #include "consensus/merkle.h"
+#include "crypto/common.h"
 #include "consensus/pow.h"
 #include "node/policy.h"
 #include "node/signals.h"
@@ -101,6 +102,35 @@ struct ScriptJob {
     const CScript* scriptPubKey; // the spent coin, kept in the block's undo record
     Amount amount;
     const PrecomputedTransactionData* txdata;
+};
+
+// One piece of work on a thread of its own; an exception it throws is reported by Join. The
+// destructor joins, so an early return cannot leave it running over freed state.
+class BackgroundTask {
+public:
+    template <typename F> void Start(F&& f) {
+        thread = std::thread([this, f = std::forward<F>(f)]() mutable {
+            try {
+                f();
+            } catch (const std::exception& e) {
+                error = e.what();
+                failed = true;
+            }
+        });
+    }
+    bool Join(std::string* what) {
+        if (thread.joinable()) thread.join();
+        if (failed && what) *what = error;
+        return !failed;
+    }
+    ~BackgroundTask() {
+        if (thread.joinable()) thread.join();
+    }
+
+private:
+    std::thread thread;
+    std::string error;
+    bool failed = false;
 };
 } // namespace
 
@@ -848,97 +878,319 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         ~CompleteOnExit() { q.Complete(); }
     } completeOnExit{*scriptQueue};
 
-    // The serial UTXO pass. Each input's coin is taken from the view (or the prefetch) once; the
-    // checks below used to go back to the view for it six times (HaveInputs, the height list,
-    // the P2SH sigop count, GetValueIn, CheckTxInputs, SpendCoin). The references stay valid
-    // while the view grows.
-    std::vector<const Coin*> coins;
-    std::vector<uint8_t> fromPrefetch;
-    for (size_t i = 0; i < ntx; i++) {
-        const CTransaction& tx = *block.vtx[i];
-        nInputs += (int)tx.vin.size();
-        if (!tx.IsCoinBase()) {
-            coins.resize(tx.vin.size());
-            fromPrefetch.resize(tx.vin.size());
-            for (size_t j = 0; j < tx.vin.size(); j++) {
-                // the view's own entry (a coin created or spent earlier in the block) wins
-                const size_t k = firstInput[i] + j;
-                const Coin* c = view.FindInCache(tx.vin[j].prevout);
-                fromPrefetch[j] = c == nullptr;
-                if (!c && prefetchedFound[k]) c = &prefetched[k];
-                if (!c || c->IsSpent())
-                    return state.DoS(100, error("ConnectBlock(): inputs missing/spent"), REJECT_INVALID,
-                                     "bad-txns-inputs-missingorspent");
-                coins[j] = c;
-            }
-            prevheights.resize(tx.vin.size());
-            for (size_t j = 0; j < tx.vin.size(); j++) prevheights[j] = coins[j]->GetHeight();
-            if (!SequenceLocks(tx, nLockTimeFlags, &prevheights, *pindex))
-                return state.DoS(100, error("%s: contains a non-BIP68-final transaction", __func__), REJECT_INVALID,
-                                 "bad-txns-nonfinal");
+    // The UTXO pass, in parallel for a valid block (round 4). Every input's coin is resolved
+    // without touching the view: the view's own entry, else an output of an earlier transaction
+    // of this block (block-local txid index), else the prefetched coin. All per-transaction checks
+    // (missing or doubly spent inputs, BIP68, sigop limits, amounts, coinbase maturity) run on the
+    // pool; the block sigop total is a prefix sum. Only a block that passes everything takes the
+    // fast path: undo records and script jobs are built in parallel, the scripts start, and the
+    // view is then updated serially while they run - spends of fetched coins, spends of the view's
+    // own coins, and the outputs that no later transaction of the block spends (an output created
+    // and spent inside the block leaves no entry, as AddCoin + SpendCoin of a FRESH entry would).
+    // Any failure, or an unusual overlap of the view with the block's own outputs, runs the
+    // serial pass below instead, which yields the reference's exact reject reason.
+    bool fastDone = false;
+    BackgroundTask viewApply; // joined before the prepare phase returns
+    if (fEnforceBIP30 && opts.parallelUtxoMinTx > 0 && ntx >= opts.parallelUtxoMinTx && maxJobs > 0) {
+        size_t tcap = 16;
+        while (tcap < 2 * ntx) tcap <<= 1;
+        std::vector<int32_t> tslot(tcap, -1); // block-local txid -> index (CheckBlock refused duplicates)
+        for (size_t i = 0; i < ntx; i++) {
+            size_t h = ReadLE64(block.vtx[i]->GetHash().begin()) & (tcap - 1);
+            while (tslot[h] >= 0) h = (h + 1) & (tcap - 1);
+            tslot[h] = (int32_t)i;
         }
-        // GetTransactionSigOpCount over the looked-up coins
-        uint64_t txSigOps = legacySigOps[i];
-        if (!tx.IsCoinBase() && (flags & SCRIPT_VERIFY_P2SH))
-            for (size_t j = 0; j < tx.vin.size(); j++) {
-                const CScript& spk = coins[j]->GetTxOut().scriptPubKey;
-                if (spk.IsPayToScriptHash()) txSigOps += spk.GetSigOpCount(tx.vin[j].scriptSig);
+        auto findTx = [&](const uint256& txid) -> int {
+            size_t h = ReadLE64(txid.begin()) & (tcap - 1);
+            while (tslot[h] >= 0) {
+                if (block.vtx[tslot[h]]->GetHash() == txid) return tslot[h];
+                h = (h + 1) & (tcap - 1);
             }
-        if (txSigOps > MAX_TX_SIGOPS_COUNT) return state.DoS(100, false, REJECT_INVALID, "bad-txn-sigops");
-        nSigOpsCount += txSigOps;
-        if (nSigOpsCount > nMaxSigOpsCount)
-            return state.DoS(100, error("ConnectBlock(): too many sigops"), REJECT_INVALID, "bad-blk-sigops");
-        if (!tx.IsCoinBase()) {
-            // Consensus::CheckTxInputs over the looked-up coins; on any failure the original runs
-            // for the exact reject reason
-            Amount in = 0;
-            bool ok = true;
-            for (size_t j = 0; j < tx.vin.size() && ok; j++) {
-                const Coin& c = *coins[j];
-                if (c.IsCoinBase() && pindex->nHeight - (int)c.GetHeight() < COINBASE_MATURITY) ok = false;
-                in += c.GetTxOut().nValue;
-                if (!MoneyRange(c.GetTxOut().nValue) || !MoneyRange(in)) ok = false;
+            return -1;
+        };
+        std::vector<size_t> firstOutput(ntx + 1, 0);
+        for (size_t i = 0; i < ntx; i++) firstOutput[i + 1] = firstOutput[i] + block.vtx[i]->vout.size();
+        std::unique_ptr<std::atomic<uint8_t>[]> outSpent(new std::atomic<uint8_t>[nOutputs + 1]);
+        for (size_t o = 0; o <= nOutputs; o++) outSpent[o].store(0, std::memory_order_relaxed);
+        // concurrent set of spent outpoints (input index + 1 per slot): a second spend of one
+        // outpoint within the block is found by whichever insert comes second
+        size_t scap = 16;
+        while (scap < 2 * maxJobs) scap <<= 1;
+        std::unique_ptr<std::atomic<uint32_t>[]> spentSet(new std::atomic<uint32_t>[scap]);
+        for (size_t q = 0; q < scap; q++) spentSet[q].store(0, std::memory_order_relaxed);
+        std::vector<size_t> inputTx(maxJobs);
+        for (size_t i = 1; i < ntx; i++)
+            for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++) inputTx[k] = i;
+        auto prevoutOf = [&](size_t k) -> const COutPoint& {
+            return block.vtx[inputTx[k]]->vin[k - firstInput[inputTx[k]]].prevout;
+        };
+        auto insertSpent = [&](const COutPoint& op, size_t k) -> bool {
+            size_t h = (ReadLE64(op.hash.begin()) ^ ((uint64_t)op.n * 0x9E3779B97F4A7C15ULL)) & (scap - 1);
+            for (;;) {
+                uint32_t cur = spentSet[h].load(std::memory_order_acquire);
+                if (cur == 0) {
+                    if (spentSet[h].compare_exchange_strong(cur, (uint32_t)(k + 1), std::memory_order_acq_rel)) return true;
+                }
+                if (cur != 0 && prevoutOf(cur - 1) == op) return false; // spent twice in this block
+                if (cur != 0) h = (h + 1) & (scap - 1);
             }
-            const Amount out = tx.GetValueOut();
-            if (!ok || in < out || !MoneyRange(in - out)) {
-                if (!Consensus::CheckTxInputs(tx, state, view, pindex->nHeight))
-                    return error("ConnectBlock(): CheckTxInputs on %s failed with %s", tx.GetHash().ToString().c_str(),
-                                 FormatStateMessage(state).c_str());
-                return state.Error("ConnectBlock: input checks disagree");
-            }
-            nFees += in - out;
+        };
+        enum : uint8_t { SRC_PREFETCH = 0, SRC_VIEW = 1, SRC_BLOCK = 2 };
+        std::vector<const Coin*> coinOf(maxJobs, nullptr);
+        std::vector<Coin> made(maxJobs); // coins of in-block outputs spent within the block
+        std::vector<uint8_t> src(maxJobs, SRC_PREFETCH);
+        std::vector<uint64_t> txSigOps(ntx, 0);
+        std::vector<Amount> txFee(ntx, 0);
+        std::atomic<bool> bad{false};
+        txSigOps[0] = legacySigOps[0];
+        const size_t TCHUNK = 32;
+        pool->ParallelFor(
+            (ntx + TCHUNK - 1) / TCHUNK,
+            [&](size_t chunk) {
+                std::vector<int> heights;
+                for (size_t i = std::max<size_t>(1, chunk * TCHUNK); i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
+                    if (bad.load(std::memory_order_relaxed)) return;
+                    const CTransaction& tx = *block.vtx[i];
+                    bool ok = true;
+                    for (size_t j = 0; j < tx.vin.size() && ok; j++) {
+                        const size_t k = firstInput[i] + j;
+                        const COutPoint& op = tx.vin[j].prevout;
+                        const Coin* c = view.FindInCache(op);
+                        const int t = findTx(op.hash);
+                        if (c) {
+                            if (t >= 0) ok = false; // the view already holds an output of this block: serial pass
+                            src[k] = SRC_VIEW;
+                        } else if (t >= 0) {
+                            const CTransaction& ptx = *block.vtx[t];
+                            if (t >= (int)i || op.n >= ptx.vout.size() || ptx.vout[op.n].scriptPubKey.IsUnspendable()) {
+                                ok = false;
+                            } else {
+                                made[k] = Coin(ptx.vout[op.n], pindex->nHeight, t == 0);
+                                c = &made[k];
+                                src[k] = SRC_BLOCK;
+                                outSpent[firstOutput[t] + op.n].store(1, std::memory_order_relaxed);
+                            }
+                        } else if (prefetchedFound[k]) {
+                            c = &prefetched[k];
+                        }
+                        if (!ok || !c || c->IsSpent() || !insertSpent(op, k)) {
+                            ok = false;
+                            break;
+                        }
+                        coinOf[k] = c;
+                    }
+                    if (ok) {
+                        heights.resize(tx.vin.size());
+                        for (size_t j = 0; j < tx.vin.size(); j++) heights[j] = coinOf[firstInput[i] + j]->GetHeight();
+                        ok = SequenceLocks(tx, nLockTimeFlags, &heights, *pindex);
+                    }
+                    if (ok) {
+                        uint64_t so = legacySigOps[i];
+                        if (flags & SCRIPT_VERIFY_P2SH)
+                            for (size_t j = 0; j < tx.vin.size(); j++) {
+                                const CScript& spk = coinOf[firstInput[i] + j]->GetTxOut().scriptPubKey;
+                                if (spk.IsPayToScriptHash()) so += spk.GetSigOpCount(tx.vin[j].scriptSig);
+                            }
+                        txSigOps[i] = so;
+                        ok = so <= MAX_TX_SIGOPS_COUNT;
+                    }
+                    if (ok) {
+                        Amount in = 0;
+                        for (size_t j = 0; j < tx.vin.size() && ok; j++) {
+                            const Coin& c = *coinOf[firstInput[i] + j];
+                            if (c.IsCoinBase() && pindex->nHeight - (int)c.GetHeight() < COINBASE_MATURITY) ok = false;
+                            in += c.GetTxOut().nValue;
+                            if (!MoneyRange(c.GetTxOut().nValue) || !MoneyRange(in)) ok = false;
+                        }
+                        const Amount out = tx.GetValueOut();
+                        if (!ok || in < out || !MoneyRange(in - out)) ok = false;
+                        else txFee[i] = in - out;
+                    }
+                    if (!ok) bad.store(true, std::memory_order_relaxed);
+                }
+            },
+            1);
+        uint64_t sigTotal = 0;
+        for (size_t i = 0; i < ntx && !bad.load(); i++) {
+            if (txSigOps[i] > MAX_TX_SIGOPS_COUNT) bad = true; // the coinbase's legacy count
+            sigTotal += txSigOps[i];
+            if (sigTotal > nMaxSigOpsCount) bad = true;
         }
-        CTxUndo undoDummy;
-        if (i > 0) blockundo.vtxundo.push_back(CTxUndo());
-        CTxUndo& undo = i == 0 ? undoDummy : blockundo.vtxundo.back();
-        if (!tx.IsCoinBase()) {
-            undo.vprevout.reserve(tx.vin.size());
-            for (size_t j = 0; j < tx.vin.size(); j++) {
-                undo.vprevout.emplace_back();
-                if (fromPrefetch[j])
-                    view.SpendFetched(tx.vin[j].prevout, std::move(prefetched[firstInput[i] + j]), &undo.vprevout.back());
-                else if (!view.SpendCoin(tx.vin[j].prevout, &undo.vprevout.back()))
-                    return state.Error("ConnectBlock: spend failed");
+        if (!bad.load()) {
+            fastDone = true;
+            phaseMicros[PH_FASTUTXO].fetch_add(1, std::memory_order_relaxed);
+            // undo records (the spent coins, moved into place) and script-cache probes
+            blockundo.vtxundo.resize(ntx - 1);
+            std::vector<uint8_t> needScripts(ntx, 0);
+            std::vector<Coin> newCoins(nOutputs); // the block's outputs that stay unspent, built here
+            pool->ParallelFor(
+                (ntx + TCHUNK - 1) / TCHUNK,
+                [&](size_t chunk) {
+                    for (size_t i = std::max<size_t>(1, chunk * TCHUNK); i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
+                        const CTransaction& tx = *block.vtx[i];
+                        CTxUndo& undo = blockundo.vtxundo[i - 1];
+                        undo.vprevout.resize(tx.vin.size());
+                        for (size_t j = 0; j < tx.vin.size(); j++) {
+                            const size_t k = firstInput[i] + j;
+                            if (src[k] == SRC_PREFETCH) undo.vprevout[j] = std::move(prefetched[k]);
+                            else if (src[k] == SRC_BLOCK) undo.vprevout[j] = std::move(made[k]);
+                            else undo.vprevout[j] = *coinOf[k];
+                        }
+                        needScripts[i] = fScriptChecks && !sc.Has(scKeys[i], !fJustCheck);
+                    }
+                    for (size_t i = chunk * TCHUNK; i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
+                        const CTransaction& tx = *block.vtx[i];
+                        for (size_t o = 0; o < tx.vout.size(); o++)
+                            if (!outSpent[firstOutput[i] + o].load(std::memory_order_relaxed) &&
+                                !tx.vout[o].scriptPubKey.IsUnspendable())
+                                newCoins[firstOutput[i] + o] = Coin(tx.vout[o], pindex->nHeight, i == 0);
+                    }
+                },
+                1);
+            // script jobs (the spent coins are read from the undo records, whose addresses are
+            // fixed from here on), then the scripts start while the view is updated
+            std::vector<size_t> jobOff(ntx + 1, 0);
+            for (size_t i = 0; i < ntx; i++) jobOff[i + 1] = jobOff[i] + (needScripts[i] ? block.vtx[i]->vin.size() : 0);
+            pool->ParallelFor(
+                ntx,
+                [&](size_t i) {
+                    if (!needScripts[i]) return;
+                    const CTransaction& tx = *block.vtx[i];
+                    const CTxUndo& undo = blockundo.vtxundo[i - 1];
+                    for (size_t j = 0; j < tx.vin.size(); j++) {
+                        const CTxOut& out = undo.vprevout[j].GetTxOut();
+                        jobs[jobOff[i] + j] = ScriptJob{&tx, (unsigned)j, &out.scriptPubKey, out.nValue, txdatas[i].get()};
+                    }
+                },
+                64);
+            nProduced = jobOff[ntx];
+            if (queued && nProduced > 0) {
+                scriptQueue->Publish(nProduced);
+                nPublished = nProduced;
             }
-            // transactions fully validated under these flags in the mempool skip re-execution; the
-            // jobs read the spent coins from the undo record (reserved up front: the addresses are
-            // stable for the whole block) instead of copying each script
-            if (fScriptChecks && !sc.Has(scKeys[i], !fJustCheck)) {
+            for (size_t i = 0; i < ntx; i++) {
+                nInputs += (int)block.vtx[i]->vin.size();
+                nFees += txFee[i];
+                vPos.push_back(std::make_pair(block.vtx[i]->GetHash(), pos));
+                pos.nTxOffset += txSizes[i];
+            }
+            nSigOpsCount = sigTotal;
+            // The view updates (about 180 ns each, one per input and per output) run on their own
+            // thread while this one waits for the scripts and runs the signature batch: nothing
+            // from here to the end of the prepare phase reads the view.
+            viewApply.Start([&, newCoins = std::move(newCoins), src = std::move(src), firstOutput = std::move(firstOutput)]() mutable {
+                for (size_t i = 1; i < ntx; i++) {
+                    const CTransaction& tx = *block.vtx[i];
+                    for (size_t j = 0; j < tx.vin.size(); j++) {
+                        const size_t k = firstInput[i] + j;
+                        if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(tx.vin[j].prevout);
+                        else if (src[k] == SRC_VIEW && !view.SpendCoin(tx.vin[j].prevout))
+                            throw std::runtime_error("view spend failed");
+                    }
+                }
+                for (size_t i = 0; i < ntx; i++) {
+                    const CTransaction& tx = *block.vtx[i];
+                    const bool cb = tx.IsCoinBase();
+                    for (size_t o = 0; o < tx.vout.size(); o++)
+                        if (!newCoins[firstOutput[i] + o].IsSpent())
+                            view.AddCoin(COutPoint(tx.GetHash(), (uint32_t)o), std::move(newCoins[firstOutput[i] + o]), cb);
+                }
+            });
+        }
+    }
+    if (!fastDone) {
+        // The serial UTXO pass. Each input's coin is taken from the view (or the prefetch) once; the
+        // checks below used to go back to the view for it six times (HaveInputs, the height list,
+        // the P2SH sigop count, GetValueIn, CheckTxInputs, SpendCoin). The references stay valid
+        // while the view grows.
+        std::vector<const Coin*> coins;
+        std::vector<uint8_t> fromPrefetch;
+        for (size_t i = 0; i < ntx; i++) {
+            const CTransaction& tx = *block.vtx[i];
+            nInputs += (int)tx.vin.size();
+            if (!tx.IsCoinBase()) {
+                coins.resize(tx.vin.size());
+                fromPrefetch.resize(tx.vin.size());
                 for (size_t j = 0; j < tx.vin.size(); j++) {
-                    const CTxOut& out = undo.vprevout[j].GetTxOut();
-                    jobs[nProduced + j] = ScriptJob{&tx, (unsigned)j, &out.scriptPubKey, out.nValue, txdatas[i].get()};
+                    // the view's own entry (a coin created or spent earlier in the block) wins
+                    const size_t k = firstInput[i] + j;
+                    const Coin* c = view.FindInCache(tx.vin[j].prevout);
+                    fromPrefetch[j] = c == nullptr;
+                    if (!c && prefetchedFound[k]) c = &prefetched[k];
+                    if (!c || c->IsSpent())
+                        return state.DoS(100, error("ConnectBlock(): inputs missing/spent"), REJECT_INVALID,
+                                         "bad-txns-inputs-missingorspent");
+                    coins[j] = c;
                 }
-                nProduced += tx.vin.size();
-                // publish in groups: each publish takes the queue lock and may wake a worker
-                if (nProduced - nPublished >= 512) {
-                    scriptQueue->Publish(nProduced);
-                    nPublished = nProduced;
+                prevheights.resize(tx.vin.size());
+                for (size_t j = 0; j < tx.vin.size(); j++) prevheights[j] = coins[j]->GetHeight();
+                if (!SequenceLocks(tx, nLockTimeFlags, &prevheights, *pindex))
+                    return state.DoS(100, error("%s: contains a non-BIP68-final transaction", __func__), REJECT_INVALID,
+                                     "bad-txns-nonfinal");
+            }
+            // GetTransactionSigOpCount over the looked-up coins
+            uint64_t txSigOps = legacySigOps[i];
+            if (!tx.IsCoinBase() && (flags & SCRIPT_VERIFY_P2SH))
+                for (size_t j = 0; j < tx.vin.size(); j++) {
+                    const CScript& spk = coins[j]->GetTxOut().scriptPubKey;
+                    if (spk.IsPayToScriptHash()) txSigOps += spk.GetSigOpCount(tx.vin[j].scriptSig);
+                }
+            if (txSigOps > MAX_TX_SIGOPS_COUNT) return state.DoS(100, false, REJECT_INVALID, "bad-txn-sigops");
+            nSigOpsCount += txSigOps;
+            if (nSigOpsCount > nMaxSigOpsCount)
+                return state.DoS(100, error("ConnectBlock(): too many sigops"), REJECT_INVALID, "bad-blk-sigops");
+            if (!tx.IsCoinBase()) {
+                // Consensus::CheckTxInputs over the looked-up coins; on any failure the original runs
+                // for the exact reject reason
+                Amount in = 0;
+                bool ok = true;
+                for (size_t j = 0; j < tx.vin.size() && ok; j++) {
+                    const Coin& c = *coins[j];
+                    if (c.IsCoinBase() && pindex->nHeight - (int)c.GetHeight() < COINBASE_MATURITY) ok = false;
+                    in += c.GetTxOut().nValue;
+                    if (!MoneyRange(c.GetTxOut().nValue) || !MoneyRange(in)) ok = false;
+                }
+                const Amount out = tx.GetValueOut();
+                if (!ok || in < out || !MoneyRange(in - out)) {
+                    if (!Consensus::CheckTxInputs(tx, state, view, pindex->nHeight))
+                        return error("ConnectBlock(): CheckTxInputs on %s failed with %s", tx.GetHash().ToString().c_str(),
+                                     FormatStateMessage(state).c_str());
+                    return state.Error("ConnectBlock: input checks disagree");
+                }
+                nFees += in - out;
+            }
+            CTxUndo undoDummy;
+            if (i > 0) blockundo.vtxundo.push_back(CTxUndo());
+            CTxUndo& undo = i == 0 ? undoDummy : blockundo.vtxundo.back();
+            if (!tx.IsCoinBase()) {
+                undo.vprevout.reserve(tx.vin.size());
+                for (size_t j = 0; j < tx.vin.size(); j++) {
+                    undo.vprevout.emplace_back();
+                    if (fromPrefetch[j])
+                        view.SpendFetched(tx.vin[j].prevout, std::move(prefetched[firstInput[i] + j]), &undo.vprevout.back());
+                    else if (!view.SpendCoin(tx.vin[j].prevout, &undo.vprevout.back()))
+                        return state.Error("ConnectBlock: spend failed");
+                }
+                // transactions fully validated under these flags in the mempool skip re-execution; the
+                // jobs read the spent coins from the undo record (reserved up front: the addresses are
+                // stable for the whole block) instead of copying each script
+                if (fScriptChecks && !sc.Has(scKeys[i], !fJustCheck)) {
+                    for (size_t j = 0; j < tx.vin.size(); j++) {
+                        const CTxOut& out = undo.vprevout[j].GetTxOut();
+                        jobs[nProduced + j] = ScriptJob{&tx, (unsigned)j, &out.scriptPubKey, out.nValue, txdatas[i].get()};
+                    }
+                    nProduced += tx.vin.size();
+                    // publish in groups: each publish takes the queue lock and may wake a worker
+                    if (nProduced - nPublished >= 512) {
+                        scriptQueue->Publish(nProduced);
+                        nPublished = nProduced;
+                    }
                 }
             }
+            AddCoins(view, tx, pindex->nHeight);
+            vPos.push_back(std::make_pair(tx.GetHash(), pos));
+            pos.nTxOffset += txSizes[i];
         }
-        AddCoins(view, tx, pindex->nHeight);
-        vPos.push_back(std::make_pair(tx.GetHash(), pos));
-        pos.nTxOffset += txSizes[i];
     }
     const int64_t nTime2 = GetTimeMicros();
     phase(PH_UTXO);
@@ -995,6 +1247,8 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         }
         p.sigsOk = ok;
     }
+    std::string applyError;
+    if (!viewApply.Join(&applyError)) return state.Error("ConnectBlock: " + applyError);
     // the next block of a pipeline layers its view on this one
     if (!fJustCheck) view.SetBestBlock(pindex->GetBlockHash());
     return true;

@@ -82,6 +82,8 @@ struct ChainstateOptions {
     // runs while block N's signature batch is on the GPU (at most this many blocks in flight;
     // <= 1 connects one block at a time like the reference)
     int connectPipeline = 2;
+    // the UTXO pass of a block with at least this many transactions runs in parallel (0: never)
+    size_t parallelUtxoMinTx = 64;
 };
 
 // Mempool acceptance outcome.
@@ -198,6 +200,7 @@ public:
     WorkerPool& Pool() { return *pool; }
     bool UseGpu() const { return opts.useGpu; }
     void SetUseGpu(bool v) { opts.useGpu = v; }
+    void SetParallelUtxoMinTx(size_t n) { opts.parallelUtxoMinTx = n; }
     std::string Warnings() const; // bcp::GetWarnings("statusbar")
     // block-change notification for RPC long-poll / waitfornewblock
     void WaitForBlockChange(int64_t timeoutMillis, const uint256& from);
@@ -207,7 +210,8 @@ public:
     // the connect benchmarks: CheckBlock, the parallel read-only pass (BIP30, input prefetch,
     // per-tx precompute), the serial UTXO pass, the wait for
     // the script jobs after it, gathering the deferred checks, and the synchronous batch verify.
-    enum ConnectPhase { PH_CHECK, PH_PRECOMPUTE, PH_UTXO, PH_SCRIPTS, PH_COLLECT, PH_BATCH, PH_BLOCKS, PH_COUNT };
+    // PH_BLOCKS counts connected blocks, PH_FASTUTXO those whose UTXO pass took the parallel path
+    enum ConnectPhase { PH_CHECK, PH_PRECOMPUTE, PH_UTXO, PH_SCRIPTS, PH_COLLECT, PH_BATCH, PH_BLOCKS, PH_FASTUTXO, PH_COUNT };
     int64_t ConnectPhaseMicros(ConnectPhase ph) const { return phaseMicros[ph].load(std::memory_order_relaxed); }
 
 private:

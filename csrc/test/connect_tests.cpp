@@ -1,0 +1,210 @@
+// ConnectBlock's parallel UTXO pass against the serial one.
+// Parity: the UTXO rules of reference src/validation.cpp ConnectBlock (:2011-2127: missing or
+// spent inputs, BIP68, sigop limits, input values, coinbase maturity, AddCoins/SpendCoin, undo
+// records) and CheckTxInputs (src/consensus/tx_verify.cpp). The reference has one serial pass;
+// these cases pin that the parallel pass (taken for blocks of -parallelutxo transactions or more)
+// leaves the same coins and undo data, and that a block it refuses gets the serial pass's exact
+// reject reason.
+#include "test/unittest.h"
+
+#include "node/miner.h"
+#include "node/validation.h"
+#include "script/sign.h"
+#include "util/strencodings.h"
+#include "util/util.h"
+
+#include <cstdio>
+#include <map>
+
+using namespace bcp;
+
+namespace {
+
+CScript P2PK(const CKey& k) { return CScript() << k.GetPubKey().Raw() << OP_CHECKSIG; }
+
+struct Prev {
+    CTransaction tx;
+    uint32_t n;
+};
+
+// spend `ins` (all P2PK to `key`) into `outs`
+CMutableTransaction Make(const std::vector<Prev>& ins, const std::vector<CTxOut>& outs, const CKey& key) {
+    CMutableTransaction m;
+    for (const Prev& p : ins) m.vin.push_back(CTxIn(COutPoint(p.tx.GetHash(), p.n), CScript()));
+    m.vout = outs;
+    CBasicKeyStore ks;
+    ks.AddKey(key);
+    for (size_t i = 0; i < ins.size(); i++) {
+        const CTxOut& o = ins[i].tx.vout[ins[i].n];
+        if (o.scriptPubKey.IsUnspendable()) continue; // refused before its script runs
+        if (!SignSignature(ks, o.scriptPubKey, m, (unsigned)i, o.nValue, SIGHASH_ALL | SIGHASH_FORKID))
+            throw std::runtime_error("test: signing failed");
+    }
+    return m;
+}
+
+// every coin the block touches, as the tip's view now has it ("" = none)
+std::map<std::string, std::string> Snapshot(Chainstate& cs, const std::vector<CMutableTransaction>& txs,
+                                            const std::vector<COutPoint>& extra) {
+    std::map<std::string, std::string> out;
+    auto add = [&](const COutPoint& op) {
+        Coin c;
+        std::string v;
+        if (cs.CoinsTip().GetCoin(op, c) && !c.IsSpent())
+            v = strprintf("%lld/%u/%d/%s", (long long)c.out.nValue, c.nHeight, (int)c.fCoinBase,
+                          HexStr(c.out.scriptPubKey).c_str());
+        out[op.ToString()] = v;
+    };
+    for (const CMutableTransaction& m : txs) {
+        const CTransaction t(m);
+        for (const CTxIn& in : t.vin) add(in.prevout);
+        for (size_t o = 0; o < t.vout.size(); o++) add(COutPoint(t.GetHash(), (uint32_t)o));
+    }
+    for (const COutPoint& op : extra) add(op);
+    return out;
+}
+
+CBlock Assemble(Chainstate& cs, const std::vector<CMutableTransaction>& txs, const CScript& spk) {
+    BlockAssembler ba(cs, nullptr);
+    std::unique_ptr<CBlockTemplate> t = ba.CreateNewBlock(spk);
+    CBlock b = t->block;
+    b.vtx.resize(1);
+    for (const CMutableTransaction& m : txs) b.vtx.push_back(MakeTransactionRef(m));
+    unsigned extra = 0;
+    IncrementExtraNonce(&b, cs.TipNow(), extra, cs.MaxBlockSize());
+    return b;
+}
+
+// TestBlockValidity's reject reason with the parallel pass forced on (1) and off (0)
+std::pair<std::string, std::string> Verdicts(Chainstate& cs, const CBlock& b) {
+    std::string r[2];
+    for (int par = 0; par < 2; par++) {
+        cs.SetParallelUtxoMinTx(par ? 1 : 0);
+        CValidationState st;
+        r[par] = cs.TestBlockValidity(st, b, cs.TipNow(), false, true) ? "valid" : st.GetRejectReason();
+    }
+    cs.SetParallelUtxoMinTx(64);
+    return {r[0], r[1]};
+}
+
+bool Same(const std::map<std::string, std::string>& a, const std::map<std::string, std::string>& b) {
+    for (const auto& kv : a)
+        if (!b.count(kv.first) || b.at(kv.first) != kv.second)
+            std::printf("  %s: '%s' vs '%s'\n", kv.first.c_str(), kv.second.c_str(),
+                        b.count(kv.first) ? b.at(kv.first).c_str() : "(absent)");
+    return a == b;
+}
+
+} // namespace
+
+TEST_CASE(connectblock_tests, parallel_pass_matches_serial) {
+    test::TestChain100Setup setup;
+    Chainstate& cs = *setup.node->chainstate;
+    const CKey& key = setup.coinbaseKey;
+    const CScript spk = P2PK(key);
+    for (int i = 0; i < 10; i++) setup.CreateAndProcessBlock({}, spk);
+    // a fan-out, 70 children of it (two outputs each, every fifth with an OP_RETURN too), 35
+    // grandchildren spending a child's first output, and 6 spends of mature coinbases
+    std::vector<CMutableTransaction> txs;
+    const Amount fanEach = (setup.coinbaseTxns[0].vout[0].nValue - 100000) / 70;
+    txs.push_back(Make({{setup.coinbaseTxns[0], 0}}, std::vector<CTxOut>(70, CTxOut(fanEach, spk)), key));
+    const CTransaction fan(txs[0]);
+    std::vector<CTransaction> children;
+    for (uint32_t i = 0; i < 70; i++) {
+        std::vector<CTxOut> outs{CTxOut(fanEach / 2 - 1000, spk), CTxOut(fanEach / 2 - 1000, spk)};
+        if (i % 5 == 0) outs.push_back(CTxOut(0, CScript() << OP_RETURN << std::vector<unsigned char>(4, (unsigned char)i)));
+        txs.push_back(Make({{fan, i}}, outs, key));
+        children.emplace_back(txs.back());
+    }
+    for (uint32_t i = 0; i < 35; i++)
+        txs.push_back(Make({{children[2 * i], 0}}, {CTxOut(fanEach / 2 - 5000, spk)}, key));
+    for (int c = 1; c <= 6; c++)
+        txs.push_back(Make({{setup.coinbaseTxns[c], 0}}, {CTxOut(setup.coinbaseTxns[c].vout[0].nValue - 2000, spk)}, key));
+    REQUIRE(txs.size() >= 64);
+    const std::vector<COutPoint> none;
+    const auto before = Snapshot(cs, txs, none);
+
+    // both passes accept it
+    const CBlock probe = Assemble(cs, txs, spk);
+    const auto v = Verdicts(cs, probe);
+    CHECK_EQ(v.first, std::string("valid"));
+    CHECK_EQ(v.second, std::string("valid"));
+
+    // connect it with the parallel pass (the default threshold; the block has 112 transactions)
+    const int64_t fastBefore = cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO);
+    const CBlock blk = setup.CreateAndProcessBlock(txs, spk);
+    CHECK_EQ(cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO), fastBefore + 1);
+    const COutPoint cbOut(blk.vtx[0]->GetHash(), 0);
+    const auto parallel = Snapshot(cs, txs, {cbOut});
+    // what it must hold: every input spent; outputs spent inside the block and OP_RETURNs absent;
+    // the rest at the block's height, the coinbase flagged
+    const int h = cs.HeightNow();
+    for (const CMutableTransaction& m : txs)
+        for (const CTxIn& in : m.vin) CHECK_EQ(parallel.at(in.prevout.ToString()), std::string());
+    for (uint32_t i = 0; i < 70; i++) {
+        const std::string first = parallel.at(COutPoint(children[i].GetHash(), 0).ToString());
+        CHECK_EQ(first.empty(), i % 2 == 0);
+        CHECK(!parallel.at(COutPoint(children[i].GetHash(), 1).ToString()).empty());
+        if (i % 5 == 0) CHECK(parallel.at(COutPoint(children[i].GetHash(), 2).ToString()).empty());
+    }
+    const std::string cb = parallel.at(cbOut.ToString());
+    CHECK(cb.find(strprintf("/%d/1/", h)) != std::string::npos);
+    const std::string last = parallel.at(COutPoint(CTransaction(txs.back()).GetHash(), 0).ToString());
+    CHECK(last.find(strprintf("/%d/0/", h)) != std::string::npos);
+
+    // disconnecting with the parallel pass's undo data restores every spent coin exactly
+    CBlockIndex* pindex = cs.LookupBlockIndex(blk.GetHash());
+    REQUIRE(pindex != nullptr);
+    CValidationState st;
+    REQUIRE(cs.InvalidateBlock(st, pindex));
+    CHECK(Same(before, Snapshot(cs, txs, none)));
+
+    // and the serial pass, reconnecting the same block, leaves the same coins
+    cs.SetParallelUtxoMinTx(0);
+    REQUIRE(cs.ResetBlockFailureFlags(pindex));
+    REQUIRE(cs.ActivateBestChain(st));
+    REQUIRE(cs.TipNow() == pindex);
+    CHECK(Same(parallel, Snapshot(cs, txs, {cbOut})));
+    cs.SetParallelUtxoMinTx(64);
+}
+
+TEST_CASE(connectblock_tests, parallel_pass_reject_reasons) {
+    test::TestChain100Setup setup;
+    Chainstate& cs = *setup.node->chainstate;
+    const CKey& key = setup.coinbaseKey;
+    const CScript spk = P2PK(key);
+    for (int i = 0; i < 5; i++) setup.CreateAndProcessBlock({}, spk);
+    const Amount v0 = setup.coinbaseTxns[0].vout[0].nValue;
+    const CMutableTransaction fan = Make({{setup.coinbaseTxns[0], 0}},
+                                         {CTxOut(v0 / 4, spk), CTxOut(v0 / 4, spk),
+                                          CTxOut(0, CScript() << OP_RETURN), CTxOut(v0 / 4, spk)},
+                                         key);
+    const CTransaction f(fan);
+    auto spend = [&](const CTransaction& p, uint32_t n, Amount v) { return Make({{p, n}}, {CTxOut(v, spk)}, key); };
+    const Amount small = v0 / 8;
+    struct Case {
+        const char* what;
+        std::vector<CMutableTransaction> txs;
+    };
+    const CTransaction cbImmature = setup.coinbaseTxns.back();
+    CMutableTransaction beyond = spend(f, 0, small);
+    beyond.vin[0].prevout.n = 9; // no such output (signature no longer matters: the input is missing)
+    std::vector<Case> cases{
+        {"in-block output spent twice", {fan, spend(f, 0, small), spend(f, 0, small / 2)}},
+        {"tip coin spent twice", {spend(setup.coinbaseTxns[1], 0, small), spend(setup.coinbaseTxns[1], 0, small / 2)}},
+        {"child before its parent", {spend(f, 1, small), fan}},
+        {"missing output of an in-block tx", {fan, beyond}},
+        {"in-block OP_RETURN output spent", {fan, spend(f, 2, 0)}},
+        {"outputs above inputs", {fan, spend(f, 3, v0)}},
+        {"immature coinbase", {spend(cbImmature, 0, small)}},
+        {"valid chain", {fan, spend(f, 0, small), spend(f, 1, small), spend(f, 3, small)}},
+    };
+    for (const Case& c : cases) {
+        const CBlock b = Assemble(cs, c.txs, spk);
+        const auto v = Verdicts(cs, b);
+        if (v.second != v.first) std::printf("  %s: serial %s, parallel %s\n", c.what, v.first.c_str(), v.second.c_str());
+        CHECK_EQ(v.second, v.first);
+        if (std::string(c.what) == "valid chain") CHECK_EQ(v.first, std::string("valid"));
+        else CHECK(v.first != "valid");
+    }
+}

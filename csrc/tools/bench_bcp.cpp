@@ -333,6 +333,29 @@ static void CCoinsCaching(State& st) {
 }
 BENCHMARK(CCoinsCaching);
 
+// The view updates of one 8 MB block's UTXO pass, alone: 42k spends of fetched coins and 42k
+// new P2PKH outputs into a fresh per-block cache sized up front (the serial tail of the parallel
+// pass in ConnectBlockPrepare)
+static void CoinsApply84k(State& st) {
+    CCoinsView base;
+    const size_t N = 42000;
+    std::vector<COutPoint> spent(N), made(N);
+    FastRandomContext rng(true);
+    for (size_t i = 0; i < N; i++) {
+        spent[i] = COutPoint(rng.rand256(), (uint32_t)(i & 1));
+        made[i] = COutPoint(rng.rand256(), (uint32_t)(i & 1));
+    }
+    const CScript spk = CScript() << OP_DUP << OP_HASH160 << std::vector<unsigned char>(20, 7) << OP_EQUALVERIFY
+                                  << OP_CHECKSIG;
+    while (st.KeepRunning()) {
+        CCoinsViewCache view(&base);
+        view.Reserve(2 * N);
+        for (size_t i = 0; i < N; i++) view.SpendFetchedMoved(spent[i]);
+        for (size_t i = 0; i < N; i++) view.AddCoin(made[i], Coin(CTxOut(1000, spk), 100, false), false);
+    }
+}
+BENCHMARK(CoinsApply84k);
+
 static void CoinSelection(State& st) {
     SelectParams("regtest");
     CWallet wallet("bench", "", true);
@@ -703,6 +726,7 @@ BigBlockFixture& BigBlock(int kind) {
     o.datadir = tmpl;
     o.useGpu = gpu::GpuAvailable();
     o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
+    o.parallelUtxoMinTx = (size_t)gArgs.GetArg("-parallelutxo", (int64_t)o.parallelUtxoMinTx);
     f.cs.reset(new Chainstate(Params(), o));
     std::string err;
     if (!f.cs->InitBlockIndex(err)) throw std::runtime_error("bench: " + err);
@@ -876,9 +900,10 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
             (double)(s1.multisig_groups - s0.multisig_groups) / iters);
     auto ms = [&](Chainstate::ConnectPhase k) { return 0.001 * (f.cs->ConnectPhaseMicros(k) - ph0[k]) / iters; };
     fprintf(stderr, "# %s: connect phases (ms/block): checkblock %.2f, prefetch+precompute %.2f, utxo pass %.2f, "
-                    "script wait %.2f, collect %.2f, batch %.2f\n",
+                    "script wait %.2f, collect %.2f, batch %.2f; parallel UTXO pass in %lld of %d blocks\n",
             useGpu ? "GPU" : "CPU", ms(Chainstate::PH_CHECK), ms(Chainstate::PH_PRECOMPUTE), ms(Chainstate::PH_UTXO),
-            ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_COLLECT), ms(Chainstate::PH_BATCH));
+            ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_COLLECT), ms(Chainstate::PH_BATCH),
+            (long long)(f.cs->ConnectPhaseMicros(Chainstate::PH_FASTUTXO) - ph0[Chainstate::PH_FASTUTXO]), iters);
     SetGpuSigThreshold(thr);
 }
 } // namespace
@@ -971,6 +996,7 @@ IbdFixture& Ibd() {
     o.datadir = tmpl;
     o.useGpu = false; // the builder only assembles; validation speed is measured on fresh nodes
     o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
+    o.parallelUtxoMinTx = (size_t)gArgs.GetArg("-parallelutxo", (int64_t)o.parallelUtxoMinTx);
     Chainstate cs(Params(), o);
     CTxMemPool pool;
     std::string err;
@@ -1065,6 +1091,7 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         o.useGpu = useGpu;
         o.connectPipeline = pipeline;
         o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
+        o.parallelUtxoMinTx = (size_t)gArgs.GetArg("-parallelutxo", (int64_t)o.parallelUtxoMinTx);
         Chainstate cs(Params(), o);
         std::string err;
         if (!cs.InitBlockIndex(err)) throw std::runtime_error("bench: " + err);
