@@ -7,6 +7,7 @@
 #pragma once
 #include "crypto/hashes.h"
 #include "primitives/transaction.h"
+#include "util/poolalloc.h"
 
 #include <functional>
 #include <memory>
@@ -153,7 +154,10 @@ struct CCoinsCacheEntry {
     CCoinsCacheEntry() {}
     explicit CCoinsCacheEntry(Coin&& c) : coin(std::move(c)) {}
 };
-typedef std::unordered_map<COutPoint, CCoinsCacheEntry, SaltedOutpointHasher> CCoinsMap;
+// nodes come from a per-map arena (util/poolalloc.h)
+typedef std::unordered_map<COutPoint, CCoinsCacheEntry, SaltedOutpointHasher, std::equal_to<COutPoint>,
+                           NodePoolAllocator<std::pair<const COutPoint, CCoinsCacheEntry>>>
+    CCoinsMap;
 
 class CCoinsViewCursor {
 public:

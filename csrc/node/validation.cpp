@@ -12,6 +12,7 @@
 #include "node/txmempool.h"
 #include "script/interpreter.h"
 #include "util/strencodings.h"
+#include "util/reaper.h"
 
 #include <algorithm>
 #include <thread>
@@ -657,7 +658,12 @@ bool Chainstate::TestBlockValidity(CValidationState& state, const CBlock& block,
                                    bool fCheckMerkleRoot) {
     std::lock_guard<CCriticalSection> l(cs_main);
     if (!(pindexPrev && pindexPrev == chainActive.Tip())) return state.Error("TestBlockValidity: not on tip");
-    CCoinsViewCache viewNew(pcoinsTip.get());
+    // the block's coins view is freed on the reaper thread (util/reaper.h)
+    std::unique_ptr<CCoinsViewCache> viewNew(new CCoinsViewCache(pcoinsTip.get()));
+    struct DropView {
+        std::unique_ptr<CCoinsViewCache>& v;
+        ~DropView() { Reaper::Get().Drop(std::move(v)); }
+    } dropView{viewNew};
     CBlockIndex indexDummy(block);
     indexDummy.pprev = pindexPrev;
     indexDummy.nHeight = pindexPrev->nHeight + 1;
@@ -667,7 +673,7 @@ bool Chainstate::TestBlockValidity(CValidationState& state, const CBlock& block,
         return error("%s: Consensus::CheckBlock: %s", __func__, FormatStateMessage(state).c_str());
     if (!ContextualCheckBlock(block, state, pindexPrev))
         return error("%s: Consensus::ContextualCheckBlock: %s", __func__, FormatStateMessage(state).c_str());
-    if (!ConnectBlock(block, state, &indexDummy, viewNew, true)) return false;
+    if (!ConnectBlock(block, state, &indexDummy, *viewNew, true)) return false;
     return true;
 }
 
@@ -718,7 +724,9 @@ struct Chainstate::PendingConnect {
 bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
                               bool fJustCheck) {
     PendingConnect p;
-    return ConnectBlockPrepare(block, state, pindex, view, fJustCheck, false, p) && ConnectBlockFinish(p, state, fJustCheck);
+    const bool ok = ConnectBlockPrepare(block, state, pindex, view, fJustCheck, false, p) && ConnectBlockFinish(p, state, fJustCheck);
+    Reaper::Get().Drop(std::move(p.blockundo)); // 21k+ undo vectors for a big block
+    return ok;
 }
 
 // Phase 1 of connecting a block: every consensus check that needs the UTXO view, the script
@@ -1251,6 +1259,13 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     if (!viewApply.Join(&applyError)) return state.Error("ConnectBlock: " + applyError);
     // the next block of a pipeline layers its view on this one
     if (!fJustCheck) view.SetBestBlock(pindex->GetBlockHash());
+    // a big block leaves ~100k heap objects in these: freed on the reaper thread
+    if (ntx >= 1024) {
+        Reaper::Get().Drop(std::move(sinks));
+        Reaper::Get().Drop(std::move(groupSinks));
+        Reaper::Get().Drop(std::move(txdatas));
+        Reaper::Get().Drop(std::move(prefetched));
+    }
     return true;
 }
 

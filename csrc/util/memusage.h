@@ -56,8 +56,8 @@ template <typename X, typename Y, typename Z> inline size_t DynamicUsage(const s
 template <typename X, typename Y, typename Z> inline size_t DynamicUsage(const std::unordered_set<X, Y, Z>& s) {
     return MallocUsage(sizeof(stl_hash_node) + sizeof(X)) * s.size() + MallocUsage(sizeof(void*) * s.bucket_count());
 }
-template <typename X, typename Y, typename Z, typename W>
-inline size_t DynamicUsage(const std::unordered_map<X, Y, Z, W>& m) {
+template <typename X, typename Y, typename Z, typename W, typename A>
+inline size_t DynamicUsage(const std::unordered_map<X, Y, Z, W, A>& m) {
     return MallocUsage(sizeof(stl_hash_node) + sizeof(std::pair<const X, Y>)) * m.size() +
            MallocUsage(sizeof(void*) * m.bucket_count());
 }

@@ -20,7 +20,7 @@
 #   ecdsa TAG [N]        ECDSA GPU tests, per-build kernel times of ab/*/ at N signatures,
 #                        the CPU-pool vs GPU crossover sweep
 #   ecdsa-cpu TAG        CPU ECDSA / ecmult micro-benches and the CPU 8 MB connect
-#   connect TAG [BLOCKS] 8 MB block connects CPU vs GPU, the IBD pipeline, and a kernel profile
+#   connect TAG [BLOCKS] 8 MB block connects on the GPU path, parallel vs serial UTXO pass, the IBD pipeline, a kernel profile
 #                        of the 160k-sigop GPU connect
 #   relay TAG            BIP152 short-id kernel: GPU tests and the CPU vs GPU micro-bench
 #   lanes TAG            verify-service tests, then a 199k-signature and a 2000-header batch over
@@ -142,8 +142,12 @@ ecdsa-cpu)
   timeout -k 10 300 ./bin/bench_bcp -filter='ConnectBlock8MB_CPU' -time=3 > "$O/connect_cpu.log" 2> "$O/connect_cpu.err"
   cat "$O/connect_cpu.log" ;;
 connect)
-  timeout -k 10 420 ./bin/bench_bcp -filter='ConnectBlock8MB.*' -time=4 > "$O/connect.log" 2> "$O/connect.err"
+  # GPU path, parallel UTXO pass (default) then the serial pass (-parallelutxo=0), >= 20 iterations each
+  timeout -k 10 300 ./bin/bench_bcp -filter='ConnectBlock8MB.*_GPU' -time=4 > "$O/connect.log" 2> "$O/connect.err"
   cat "$O/connect.log"; grep '^#' "$O/connect.err" | tail -n 12
+  timeout -k 10 300 ./bin/bench_bcp -filter='ConnectBlock8MB.*_GPU' -time=4 -parallelutxo=0 > "$O/connect_serial.log" \
+    2> "$O/connect_serial.err"
+  cat "$O/connect_serial.log"; grep '^#' "$O/connect_serial.err" | tail -n 12
   timeout -k 10 600 ./bin/bench_bcp -filter='IbdPipeline_(Seq|Pipe)_GPU' -ibdblocks="${3:-50}" -time=0 > "$O/ibd.log" 2> "$O/ibd.err"
   cat "$O/ibd.log"
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- "$R/bin/bench_bcp" \
