@@ -5,6 +5,7 @@
 
 #include <cassert>
 #include <cstring>
+#include <mutex>
 
 namespace bcp {
 
@@ -137,7 +138,9 @@ CCoinsViewCache::CCoinsViewCache(CCoinsView* b) : CCoinsViewBacked(b) {}
 
 size_t CCoinsViewCache::DynamicMemoryUsage() const {
     // hash-table nodes and buckets plus the scripts' heap buffers (reference coins.cpp)
-    return memusage::DynamicUsage(cacheCoins) + cachedCoinsUsage;
+    size_t n = CachedCoinsUsage();
+    for (unsigned s = 0; s < CCoinsMap::SHARDS; s++) n += memusage::DynamicUsage(cacheCoins.shard(s));
+    return n;
 }
 
 CCoinsMap::iterator CCoinsViewCache::FetchCoin(const COutPoint& outpoint) const {
@@ -145,15 +148,16 @@ CCoinsMap::iterator CCoinsViewCache::FetchCoin(const COutPoint& outpoint) const 
     if (it != cacheCoins.end()) return it;
     Coin tmp;
     if (!base->GetCoin(outpoint, tmp)) return cacheCoins.end();
-    auto ret = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint),
-                                  std::forward_as_tuple(std::move(tmp)))
+    const unsigned s = CCoinsMap::ShardOf(outpoint);
+    auto ret = cacheCoins.shard(s)
+                   .emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::forward_as_tuple(std::move(tmp)))
                    .first;
     if (ret->second.coin.IsSpent()) {
         // a spent coin in the parent is FRESH from our point of view
         ret->second.flags = CCoinsCacheEntry::FRESH;
     }
-    cachedCoinsUsage += ret->second.coin.DynamicMemoryUsage();
-    return ret;
+    usage[s].bytes += ret->second.coin.DynamicMemoryUsage();
+    return CCoinsMap::iterator(&cacheCoins, s, ret);
 }
 
 bool CCoinsViewCache::GetCoin(const COutPoint& outpoint, Coin& coin) const {
@@ -167,17 +171,18 @@ bool CCoinsViewCache::GetCoin(const COutPoint& outpoint, Coin& coin) const {
 void CCoinsViewCache::AddCoin(const COutPoint& outpoint, Coin&& coin, bool possible_overwrite) {
     assert(!coin.IsSpent());
     if (coin.out.scriptPubKey.IsUnspendable()) return;
-    auto ins = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
+    const unsigned s = CCoinsMap::ShardOf(outpoint);
+    auto ins = cacheCoins.shard(s).emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
     auto it = ins.first;
     bool fresh = false;
-    if (!ins.second) cachedCoinsUsage -= it->second.coin.DynamicMemoryUsage();
+    if (!ins.second) usage[s].bytes -= it->second.coin.DynamicMemoryUsage();
     if (!possible_overwrite) {
         if (!it->second.coin.IsSpent()) throw std::logic_error("Adding new coin that replaces non-pruned entry");
         fresh = !(it->second.flags & CCoinsCacheEntry::DIRTY);
     }
     it->second.coin = std::move(coin);
     it->second.flags |= CCoinsCacheEntry::DIRTY | (fresh ? CCoinsCacheEntry::FRESH : 0);
-    cachedCoinsUsage += it->second.coin.DynamicMemoryUsage();
+    usage[s].bytes += it->second.coin.DynamicMemoryUsage();
 }
 
 void AddCoins(CCoinsViewCache& cache, const CTransaction& tx, int nHeight, bool check) {
@@ -193,7 +198,8 @@ void AddCoins(CCoinsViewCache& cache, const CTransaction& tx, int nHeight, bool 
 bool CCoinsViewCache::SpendCoin(const COutPoint& outpoint, Coin* moveout) {
     auto it = FetchCoin(outpoint);
     if (it == cacheCoins.end()) return false;
-    cachedCoinsUsage -= it->second.coin.DynamicMemoryUsage();
+    const unsigned s = CCoinsMap::ShardOf(outpoint);
+    usage[s].bytes -= it->second.coin.DynamicMemoryUsage();
     if (moveout) *moveout = std::move(it->second.coin);
     if (it->second.flags & CCoinsCacheEntry::FRESH) {
         cacheCoins.erase(it);
@@ -214,14 +220,16 @@ const Coin& CCoinsViewCache::AccessCoin(const COutPoint& outpoint) const {
 
 void CCoinsViewCache::SpendFetched(const COutPoint& outpoint, Coin&& coin, Coin* moveto) {
     assert(!coin.IsSpent());
-    auto ins = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
+    auto ins = cacheCoins.shard(CCoinsMap::ShardOf(outpoint))
+                   .emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
     assert(ins.second);
     ins.first->second.flags = CCoinsCacheEntry::DIRTY; // not FRESH: the base holds the coin
     if (moveto) *moveto = std::move(coin);
 }
 
 void CCoinsViewCache::SpendFetchedMoved(const COutPoint& outpoint) {
-    auto ins = cacheCoins.emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
+    auto ins = cacheCoins.shard(CCoinsMap::ShardOf(outpoint))
+                   .emplace(std::piecewise_construct, std::forward_as_tuple(outpoint), std::tuple<>());
     assert(ins.second);
     ins.first->second.flags = CCoinsCacheEntry::DIRTY; // not FRESH: the base holds the coin
 }
@@ -273,16 +281,25 @@ uint256 CCoinsViewCache::GetBestBlock() const {
 
 void CCoinsViewCache::SetBestBlock(const uint256& h) { hashBlock = h; }
 
-bool CCoinsViewCache::BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlockIn) {
-    for (auto it = mapCoins.begin(); it != mapCoins.end(); it = mapCoins.erase(it)) {
+void CCoinsViewCache::ForEachShard(const std::function<void(unsigned)>& fn, WorkerPool* with) const {
+    if (with) with->ParallelFor(CCoinsMap::SHARDS, [&](size_t s) { fn((unsigned)s); }, 1);
+    else
+        for (unsigned s = 0; s < CCoinsMap::SHARDS; s++) fn(s);
+}
+
+// a child's shard s into ours (the same s: the shard function is shared by every cache)
+void CCoinsViewCache::MergeShard(CCoinsMap::Shard& from, unsigned s) {
+    CCoinsMap::Shard& ours = cacheCoins.shard(s);
+    size_t& used = usage[s].bytes;
+    for (auto it = from.begin(); it != from.end(); it = from.erase(it)) {
         if (!(it->second.flags & CCoinsCacheEntry::DIRTY)) continue; // non-dirty: nothing to merge
-        auto itUs = cacheCoins.find(it->first);
-        if (itUs == cacheCoins.end()) {
+        auto itUs = ours.find(it->first);
+        if (itUs == ours.end()) {
             // child has a modified entry the parent lacks; a FRESH spent one can be dropped
             if (!(it->second.flags & CCoinsCacheEntry::FRESH && it->second.coin.IsSpent())) {
-                CCoinsCacheEntry& entry = cacheCoins[it->first];
+                CCoinsCacheEntry& entry = ours[it->first];
                 entry.coin = std::move(it->second.coin);
-                cachedCoinsUsage += entry.coin.DynamicMemoryUsage();
+                used += entry.coin.DynamicMemoryUsage();
                 entry.flags = CCoinsCacheEntry::DIRTY;
                 if (it->second.flags & CCoinsCacheEntry::FRESH) entry.flags |= CCoinsCacheEntry::FRESH;
             }
@@ -291,16 +308,34 @@ bool CCoinsViewCache::BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlockIn
                 throw std::logic_error("FRESH flag misapplied to cache entry for base transaction with spendable outputs");
             if ((itUs->second.flags & CCoinsCacheEntry::FRESH) && it->second.coin.IsSpent()) {
                 // parent entry is FRESH and now spent: forget it entirely
-                cachedCoinsUsage -= itUs->second.coin.DynamicMemoryUsage();
-                cacheCoins.erase(itUs);
+                used -= itUs->second.coin.DynamicMemoryUsage();
+                ours.erase(itUs);
             } else {
-                cachedCoinsUsage -= itUs->second.coin.DynamicMemoryUsage();
+                used -= itUs->second.coin.DynamicMemoryUsage();
                 itUs->second.coin = std::move(it->second.coin);
-                cachedCoinsUsage += itUs->second.coin.DynamicMemoryUsage();
+                used += itUs->second.coin.DynamicMemoryUsage();
                 itUs->second.flags |= CCoinsCacheEntry::DIRTY;
             }
         }
     }
+}
+
+bool CCoinsViewCache::BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlockIn) {
+    // a block's worth of entries merges one shard per task; a misapplied FRESH flag in any
+    // shard is reported after every task has finished
+    std::string err;
+    std::mutex errMu;
+    ForEachShard(
+        [&](unsigned s) {
+            try {
+                MergeShard(mapCoins.shard(s), s);
+            } catch (const std::logic_error& e) {
+                std::lock_guard<std::mutex> l(errMu);
+                err = e.what();
+            }
+        },
+        mapCoins.size() >= 4096 ? pool : nullptr);
+    if (!err.empty()) throw std::logic_error(err);
     hashBlock = hashBlockIn;
     return true;
 }
@@ -308,14 +343,14 @@ bool CCoinsViewCache::BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlockIn
 bool CCoinsViewCache::Flush() {
     const bool ok = base->BatchWrite(cacheCoins, hashBlock);
     cacheCoins.clear();
-    cachedCoinsUsage = 0;
+    for (ShardUsage& u : usage) u.bytes = 0;
     return ok;
 }
 
 void CCoinsViewCache::Uncache(const COutPoint& outpoint) {
     auto it = cacheCoins.find(outpoint);
     if (it != cacheCoins.end() && it->second.flags == 0) {
-        cachedCoinsUsage -= it->second.coin.DynamicMemoryUsage();
+        usage[CCoinsMap::ShardOf(outpoint)].bytes -= it->second.coin.DynamicMemoryUsage();
         cacheCoins.erase(it);
     }
 }

@@ -8,9 +8,11 @@
 #include "crypto/hashes.h"
 #include "primitives/transaction.h"
 #include "util/poolalloc.h"
+#include "util/util.h"
 
 #include <functional>
 #include <memory>
+#include <type_traits>
 #include <unordered_map>
 
 namespace bcp {
@@ -154,10 +156,104 @@ struct CCoinsCacheEntry {
     CCoinsCacheEntry() {}
     explicit CCoinsCacheEntry(Coin&& c) : coin(std::move(c)) {}
 };
-// nodes come from a per-map arena (util/poolalloc.h)
-typedef std::unordered_map<COutPoint, CCoinsCacheEntry, SaltedOutpointHasher, std::equal_to<COutPoint>,
-                           NodePoolAllocator<std::pair<const COutPoint, CCoinsCacheEntry>>>
-    CCoinsMap;
+// A coins cache's entries, split over SHARDS hash maps by a fixed function of the outpoint (the
+// reference's single CCoinsMap, src/coins.h:183). Because the split is the same in every cache,
+// a child's shard i only ever merges into its parent's shard i, and the entries of one shard
+// never touch another's: a block's view updates and the flush of a block's view into the tip
+// run one shard per thread. Each shard is salted-SipHash keyed (collision flooding stays as hard
+// as in the reference) and takes its nodes from its own arena (util/poolalloc.h).
+class CCoinsMap {
+public:
+    static constexpr unsigned SHARDS = 16;
+    typedef std::unordered_map<COutPoint, CCoinsCacheEntry, SaltedOutpointHasher, std::equal_to<COutPoint>,
+                               NodePoolAllocator<std::pair<const COutPoint, CCoinsCacheEntry>>>
+        Shard;
+    typedef Shard::value_type value_type;
+
+    // txids are already uniform hashes: the top bits of a cheap mix choose the shard
+    static unsigned ShardOf(const COutPoint& o) {
+        return (unsigned)((o.hash.GetCheapHash() + (uint64_t)o.n * 0x9E3779B97F4A7C15ULL) >> 60);
+    }
+
+    template <bool Const> class Iter {
+    public:
+        typedef std::conditional_t<Const, const CCoinsMap, CCoinsMap> Map;
+        typedef std::conditional_t<Const, Shard::const_iterator, Shard::iterator> Inner;
+        typedef std::conditional_t<Const, const Shard::value_type, Shard::value_type> Value;
+        typedef std::forward_iterator_tag iterator_category;
+        typedef std::ptrdiff_t difference_type;
+        typedef Value value_type;
+        typedef Value* pointer;
+        typedef Value& reference;
+
+        Iter() = default;
+        Iter(Map* m, unsigned s, Inner i) : map(m), shard(s), it(i) { Settle(); }
+        template <bool C, typename = std::enable_if_t<Const && !C>>
+        Iter(const Iter<C>& o) : map(o.map), shard(o.shard), it(o.it) {}
+        Value& operator*() const { return *it; }
+        Value* operator->() const { return &*it; }
+        Iter& operator++() {
+            ++it;
+            Settle();
+            return *this;
+        }
+        bool operator==(const Iter& o) const { return shard == o.shard && it == o.it; }
+        bool operator!=(const Iter& o) const { return !(*this == o); }
+
+    private:
+        template <bool> friend class Iter;
+        friend class CCoinsMap;
+        // past the end of a shard: move to the next non-empty one (the last shard's end is end())
+        void Settle() {
+            while (it == map->shards[shard].end() && shard + 1 < SHARDS) it = map->shards[++shard].begin();
+        }
+        Map* map = nullptr;
+        unsigned shard = 0;
+        Inner it;
+    };
+    typedef Iter<false> iterator;
+    typedef Iter<true> const_iterator;
+
+    iterator begin() { return iterator(this, 0, shards[0].begin()); }
+    iterator end() { return iterator(this, SHARDS - 1, shards[SHARDS - 1].end()); }
+    const_iterator begin() const { return const_iterator(this, 0, shards[0].begin()); }
+    const_iterator end() const { return const_iterator(this, SHARDS - 1, shards[SHARDS - 1].end()); }
+    iterator find(const COutPoint& k) {
+        const unsigned s = ShardOf(k);
+        auto it = shards[s].find(k);
+        return it == shards[s].end() ? end() : iterator(this, s, it);
+    }
+    const_iterator find(const COutPoint& k) const {
+        const unsigned s = ShardOf(k);
+        auto it = shards[s].find(k);
+        return it == shards[s].end() ? end() : const_iterator(this, s, it);
+    }
+    iterator erase(iterator pos) { return iterator(this, pos.shard, shards[pos.shard].erase(pos.it)); }
+    CCoinsCacheEntry& operator[](const COutPoint& k) { return shards[ShardOf(k)][k]; }
+    size_t size() const {
+        size_t n = 0;
+        for (const Shard& s : shards) n += s.size();
+        return n;
+    }
+    bool empty() const { return size() == 0; }
+    void clear() {
+        for (Shard& s : shards) s.clear();
+    }
+    // room for n entries spread over the shards (with slack for an uneven split)
+    void reserve(size_t n) {
+        for (Shard& s : shards) s.reserve(n / SHARDS + n / (4 * SHARDS) + 16);
+    }
+    size_t bucket_count() const {
+        size_t n = 0;
+        for (const Shard& s : shards) n += s.bucket_count();
+        return n;
+    }
+    Shard& shard(unsigned i) { return shards[i]; }
+    const Shard& shard(unsigned i) const { return shards[i]; }
+
+private:
+    Shard shards[SHARDS];
+};
 
 class CCoinsViewCursor {
 public:
@@ -250,12 +346,30 @@ public:
     Amount GetValueIn(const CTransaction& tx) const;
     bool HaveInputs(const CTransaction& tx) const;
     const CTxOut& GetOutputFor(const CTxIn& input) const;
+    // A pool for shard-parallel work: a large BatchWrite into this cache merges one shard per
+    // task. The cache is still single-writer: the pool only splits that one call.
+    void SetPool(WorkerPool* p) { pool = p; }
+    // Calls fn(shard) for every shard, on the pool when one is set; fn may only touch entries of
+    // its own shard (AddCoin / SpendCoin / SpendFetchedMoved of outpoints in it, and SpendCoin
+    // only of entries this cache already holds).
+    void ForEachShard(const std::function<void(unsigned)>& fn, WorkerPool* with) const;
 
 protected:
     CCoinsMap::iterator FetchCoin(const COutPoint& outpoint) const;
+    // bytes of the coins' own heap buffers, per shard (one cache line each)
+    struct alignas(64) ShardUsage {
+        size_t bytes = 0;
+    };
+    size_t CachedCoinsUsage() const {
+        size_t n = 0;
+        for (const ShardUsage& u : usage) n += u.bytes;
+        return n;
+    }
+    void MergeShard(CCoinsMap::Shard& from, unsigned s);
     mutable uint256 hashBlock;
     mutable CCoinsMap cacheCoins;
-    mutable size_t cachedCoinsUsage = 0;
+    mutable ShardUsage usage[CCoinsMap::SHARDS];
+    WorkerPool* pool = nullptr;
 };
 
 // Add all outputs of a tx. check=true handles the BIP30 overwrite case.

@@ -6,6 +6,7 @@
 #include "util/strencodings.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -360,14 +361,83 @@ bool WriteBlockToDisk(const CBlock& block, CDiskBlockPos& pos, const unsigned ch
     return true;
 }
 
-bool ReadBlockFromDisk(CBlock& block, const CDiskBlockPos& pos, const CChainParams& params, bool checkPow) {
+namespace {
+// moves the reader past one serialized transaction (the layout CMutableTransaction::Unserialize
+// reads, with the same compact-size range checks)
+void SkipTransaction(SpanReader& r) {
+    r.ignore(4); // nVersion
+    const uint64_t nIn = ReadCompactSize(r);
+    for (uint64_t i = 0; i < nIn; i++) {
+        r.ignore(36); // prevout
+        r.ignore(ReadCompactSize(r)); // scriptSig
+        r.ignore(4); // nSequence
+    }
+    const uint64_t nOut = ReadCompactSize(r);
+    for (uint64_t i = 0; i < nOut; i++) {
+        r.ignore(8); // nValue
+        r.ignore(ReadCompactSize(r)); // scriptPubKey
+    }
+    r.ignore(4); // nLockTime
+}
+} // namespace
+
+bool DecodeBlock(const unsigned char* data, size_t len, CBlock& block, WorkerPool* pool) {
     block.SetNull();
-    FileStream in(OpenBlockFile(pos, true), SER_DISK, PROTOCOL_VERSION);
-    if (!in.Get()) return false;
     try {
-        in >> block;
+        SpanReader r(data, len, SER_DISK, PROTOCOL_VERSION);
+        static_cast<CBlockHeader&>(block).Unserialize(r);
+        const uint64_t ntx = ReadCompactSize(r);
+        if (ntx > len / 10) return false; // not even 10 bytes per transaction: truncated or corrupt
+        if (!pool || ntx < 256) {
+            block.vtx.reserve(ntx);
+            for (uint64_t i = 0; i < ntx; i++) block.vtx.push_back(std::make_shared<const CTransaction>(deserialize, r));
+            return true;
+        }
+        // one pass finds every transaction's bytes, then they are decoded (and their txids
+        // hashed) in parallel
+        std::vector<size_t> start(ntx + 1);
+        for (uint64_t i = 0; i < ntx; i++) {
+            start[i] = r.tell();
+            SkipTransaction(r);
+        }
+        start[ntx] = r.tell();
+        block.vtx.resize(ntx);
+        std::atomic<bool> bad{false};
+        pool->ParallelFor(
+            ntx,
+            [&](size_t i) {
+                try {
+                    SpanReader tr(data + start[i], start[i + 1] - start[i], SER_DISK, PROTOCOL_VERSION);
+                    block.vtx[i] = std::make_shared<const CTransaction>(deserialize, tr);
+                    if (!tr.empty()) bad = true;
+                } catch (const std::exception&) {
+                    bad = true;
+                }
+            },
+            32);
+        if (bad) block.SetNull();
+        return !bad;
     } catch (const std::exception&) {
+        block.SetNull();
         return false;
+    }
+}
+
+bool ReadBlockFromDisk(CBlock& block, const CDiskBlockPos& pos, const CChainParams& params, bool checkPow,
+                       WorkerPool* pool) {
+    block.SetNull();
+    std::vector<unsigned char> raw;
+    if (pool && ReadRawBlockFromDisk(raw, pos)) {
+        // the whole record in one read, decoded in memory (the stream path below reads field by field)
+        if (!DecodeBlock(raw.data(), raw.size(), block, pool)) return false;
+    } else {
+        FileStream in(OpenBlockFile(pos, true), SER_DISK, PROTOCOL_VERSION);
+        if (!in.Get()) return false;
+        try {
+            in >> block;
+        } catch (const std::exception&) {
+            return false;
+        }
     }
     if (!checkPow) return true;
     const bool postfork = (int)block.nHeight >= params.GetConsensus().BCPHeight;
@@ -375,8 +445,9 @@ bool ReadBlockFromDisk(CBlock& block, const CDiskBlockPos& pos, const CChainPara
     return CheckProofOfWork(block.GetHash(params.GetConsensus()), block.nBits, postfork, params.GetConsensus());
 }
 
-bool ReadBlockFromDisk(CBlock& block, const CBlockIndex* pindex, const CChainParams& params, bool checkPow) {
-    if (!ReadBlockFromDisk(block, pindex->GetBlockPos(), params, checkPow)) return false;
+bool ReadBlockFromDisk(CBlock& block, const CBlockIndex* pindex, const CChainParams& params, bool checkPow,
+                       WorkerPool* pool) {
+    if (!ReadBlockFromDisk(block, pindex->GetBlockPos(), params, checkPow, pool)) return false;
     return block.GetHash(params.GetConsensus()) == pindex->GetBlockHash();
 }
 

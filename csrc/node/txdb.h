@@ -14,6 +14,7 @@
 #include <string>
 
 namespace bcp {
+class WorkerPool;
 
 struct CBlockFileInfo {
     unsigned nBlocks = 0, nSize = 0, nUndoSize = 0, nHeightFirst = 0, nHeightLast = 0;
@@ -121,8 +122,16 @@ void AllocateFileRange(FILE* file, unsigned offset, unsigned length);
 
 bool WriteBlockToDisk(const CBlock& block, CDiskBlockPos& pos, const unsigned char diskMagic[4]);
 // Reads the raw block; `checkPow` re-validates Equihash/PoW like the reference.
-bool ReadBlockFromDisk(CBlock& block, const CDiskBlockPos& pos, const CChainParams& params, bool checkPow = true);
-bool ReadBlockFromDisk(CBlock& block, const CBlockIndex* pindex, const CChainParams& params, bool checkPow = true);
+// With a pool, the record is read in one piece and its transactions decoded in parallel
+// (DecodeBlock); without one, field by field from the file.
+bool ReadBlockFromDisk(CBlock& block, const CDiskBlockPos& pos, const CChainParams& params, bool checkPow = true,
+                       WorkerPool* pool = nullptr);
+bool ReadBlockFromDisk(CBlock& block, const CBlockIndex* pindex, const CChainParams& params, bool checkPow = true,
+                       WorkerPool* pool = nullptr);
+// Decodes a serialized block (disk format). With a pool and 256+ transactions, one pass finds
+// the transactions' boundaries and they are decoded - txids hashed - in parallel. Any decode
+// error (truncation, trailing bytes inside a transaction's span) fails the whole block.
+bool DecodeBlock(const unsigned char* data, size_t len, CBlock& block, WorkerPool* pool);
 bool ReadRawBlockFromDisk(std::vector<unsigned char>& out, const CDiskBlockPos& pos);
 bool UndoWriteToDisk(const CBlockUndo& undo, CDiskBlockPos& pos, const uint256& hashBlock,
                      const unsigned char diskMagic[4]);

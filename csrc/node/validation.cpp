@@ -105,34 +105,6 @@ struct ScriptJob {
     const PrecomputedTransactionData* txdata;
 };
 
-// One piece of work on a thread of its own; an exception it throws is reported by Join. The
-// destructor joins, so an early return cannot leave it running over freed state.
-class BackgroundTask {
-public:
-    template <typename F> void Start(F&& f) {
-        thread = std::thread([this, f = std::forward<F>(f)]() mutable {
-            try {
-                f();
-            } catch (const std::exception& e) {
-                error = e.what();
-                failed = true;
-            }
-        });
-    }
-    bool Join(std::string* what) {
-        if (thread.joinable()) thread.join();
-        if (failed && what) *what = error;
-        return !failed;
-    }
-    ~BackgroundTask() {
-        if (thread.joinable()) thread.join();
-    }
-
-private:
-    std::thread thread;
-    std::string error;
-    bool failed = false;
-};
 } // namespace
 
 // ------------------------------------------------------------------ construction
@@ -167,6 +139,7 @@ Chainstate::Chainstate(const CChainParams& p, const ChainstateOptions& o) : para
     int threads = opts.scriptThreads <= 0 ? GetNumCores() : opts.scriptThreads;
     threads = std::max(1, std::min(threads, MAX_SCRIPTCHECK_THREADS));
     pool.reset(new WorkerPool(threads));
+    pcoinsTip->SetPool(pool.get()); // a block's view merges into the tip one shard per task
     scriptQueue.reset(new CheckQueue(threads - 1)); // the connecting thread is the last worker
     fReindex = opts.wipe;
 }
@@ -898,7 +871,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // Any failure, or an unusual overlap of the view with the block's own outputs, runs the
     // serial pass below instead, which yields the reference's exact reject reason.
     bool fastDone = false;
-    BackgroundTask viewApply; // joined before the prepare phase returns
     if (fEnforceBIP30 && opts.parallelUtxoMinTx > 0 && ntx >= opts.parallelUtxoMinTx && maxJobs > 0) {
         size_t tcap = 16;
         while (tcap < 2 * ntx) tcap <<= 1;
@@ -1031,6 +1003,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             blockundo.vtxundo.resize(ntx - 1);
             std::vector<uint8_t> needScripts(ntx, 0);
             std::vector<Coin> newCoins(nOutputs); // the block's outputs that stay unspent, built here
+            std::vector<uint8_t> inShard(maxJobs), outShard(nOutputs); // CCoinsMap::ShardOf of each
             pool->ParallelFor(
                 (ntx + TCHUNK - 1) / TCHUNK,
                 [&](size_t chunk) {
@@ -1048,6 +1021,10 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                     }
                     for (size_t i = chunk * TCHUNK; i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
                         const CTransaction& tx = *block.vtx[i];
+                        for (size_t j = 0; i > 0 && j < tx.vin.size(); j++)
+                            inShard[firstInput[i] + j] = (uint8_t)CCoinsMap::ShardOf(tx.vin[j].prevout);
+                        for (size_t o = 0; o < tx.vout.size(); o++)
+                            outShard[firstOutput[i] + o] = (uint8_t)CCoinsMap::ShardOf(COutPoint(tx.GetHash(), (uint32_t)o));
                         for (size_t o = 0; o < tx.vout.size(); o++)
                             if (!outSpent[firstOutput[i] + o].load(std::memory_order_relaxed) &&
                                 !tx.vout[o].scriptPubKey.IsUnspendable())
@@ -1083,27 +1060,35 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 pos.nTxOffset += txSizes[i];
             }
             nSigOpsCount = sigTotal;
-            // The view updates (about 180 ns each, one per input and per output) run on their own
-            // thread while this one waits for the scripts and runs the signature batch: nothing
-            // from here to the end of the prepare phase reads the view.
-            viewApply.Start([&, newCoins = std::move(newCoins), src = std::move(src), firstOutput = std::move(firstOutput)]() mutable {
-                for (size_t i = 1; i < ntx; i++) {
-                    const CTransaction& tx = *block.vtx[i];
-                    for (size_t j = 0; j < tx.vin.size(); j++) {
-                        const size_t k = firstInput[i] + j;
-                        if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(tx.vin[j].prevout);
-                        else if (src[k] == SRC_VIEW && !view.SpendCoin(tx.vin[j].prevout))
-                            throw std::runtime_error("view spend failed");
+            // The view updates, one coins-map shard per task (CCoinsMap): spends of fetched coins
+            // and of the view's own coins, then the block's outputs that stay unspent. The scripts
+            // published above run meanwhile; nothing they read is in the view.
+            std::string applyError;
+            std::mutex applyMu;
+            view.ForEachShard(
+                [&](unsigned sh) {
+                    try {
+                        for (size_t k = 0; k < maxJobs; k++) {
+                            if (inShard[k] != sh) continue;
+                            const COutPoint& op = prevoutOf(k);
+                            if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(op);
+                            else if (src[k] == SRC_VIEW && !view.SpendCoin(op)) throw std::runtime_error("view spend failed");
+                        }
+                        for (size_t i = 0; i < ntx; i++) {
+                            const CTransaction& tx = *block.vtx[i];
+                            for (size_t o = 0; o < tx.vout.size(); o++) {
+                                const size_t q = firstOutput[i] + o;
+                                if (outShard[q] == sh && !newCoins[q].IsSpent())
+                                    view.AddCoin(COutPoint(tx.GetHash(), (uint32_t)o), std::move(newCoins[q]), i == 0);
+                            }
+                        }
+                    } catch (const std::exception& e) {
+                        std::lock_guard<std::mutex> l(applyMu);
+                        applyError = e.what();
                     }
-                }
-                for (size_t i = 0; i < ntx; i++) {
-                    const CTransaction& tx = *block.vtx[i];
-                    const bool cb = tx.IsCoinBase();
-                    for (size_t o = 0; o < tx.vout.size(); o++)
-                        if (!newCoins[firstOutput[i] + o].IsSpent())
-                            view.AddCoin(COutPoint(tx.GetHash(), (uint32_t)o), std::move(newCoins[firstOutput[i] + o]), cb);
-                }
-            });
+                },
+                pool.get());
+            if (!applyError.empty()) return state.Error("ConnectBlock: " + applyError);
         }
     }
     if (!fastDone) {
@@ -1255,8 +1240,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         }
         p.sigsOk = ok;
     }
-    std::string applyError;
-    if (!viewApply.Join(&applyError)) return state.Error("ConnectBlock: " + applyError);
     // the next block of a pipeline layers its view on this one
     if (!fJustCheck) view.SetBestBlock(pindex->GetBlockHash());
     // a big block leaves ~100k heap objects in these: freed on the reaper thread
@@ -1546,9 +1529,9 @@ BenchTotals& Bench() {
     static BenchTotals t;
     return t;
 }
-const char* const kPhaseNames[Chainstate::PH_COUNT] = {"Sanity checks", "Prefetch + precompute", "UTXO pass",
-                                                      "Script jobs wait", "Collect checks", "Signature batch",
-                                                      "Pipelined blocks"};
+// the timed phases (PH_BLOCKS and PH_FASTUTXO are counters)
+const char* const kPhaseNames[Chainstate::PH_BLOCKS] = {"Sanity checks", "Prefetch + precompute", "UTXO pass",
+                                                       "Script jobs wait", "Collect checks", "Signature batch"};
 void BenchLine(const char* indent, const char* what, int64_t micros, std::atomic<int64_t>& acc) {
     const int64_t tot = (acc += micros);
     LogPrint(BCLog::BENCH, "%s- %s: %.2fms [%.2fs]\n", indent, what, 0.001 * micros, 1e-6 * tot);
@@ -1565,7 +1548,7 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
     std::shared_ptr<const CBlock> pthisBlock;
     if (!pblock) {
         auto pblockNew = std::make_shared<CBlock>();
-        if (!ReadBlockFromDisk(*pblockNew, pindexNew, params)) return state.Error("Failed to read block");
+        if (!ReadBlockFromDisk(*pblockNew, pindexNew, params, true, pool.get())) return state.Error("Failed to read block");
         pthisBlock = pblockNew;
     } else {
         pthisBlock = pblock;
@@ -1596,10 +1579,9 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
         BenchTotals& B = Bench();
         B.blocks++;
         BenchLine("  ", "Load block from disk", nTime2 - nTime1, B.read);
-        for (int k = 0; k < PH_COUNT; k++) {
-            const int64_t d = ConnectPhaseMicros((ConnectPhase)k) - ph0[k];
-            if (d > 0 || k != PH_BLOCKS) BenchLine("      ", kPhaseNames[k], d, B.phase[k]);
-        }
+        for (int k = 0; k < PH_BLOCKS; k++)
+            BenchLine("      ", kPhaseNames[k], ConnectPhaseMicros((ConnectPhase)k) - ph0[k], B.phase[k]);
+        if (ConnectPhaseMicros(PH_FASTUTXO) > ph0[PH_FASTUTXO]) LogPrint(BCLog::BENCH, "      - (parallel UTXO pass)\n");
         BenchLine("    ", "Connect total", nTime3 - nTime2, B.connect);
         BenchLine("  ", "Flush", nTime4 - nTime3, B.flush);
         BenchLine("  ", "Writing chainstate", nTime5 - nTime4, B.chainstate);
@@ -1661,7 +1643,7 @@ bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector
             st.block = pblock;
         } else {
             auto b = std::make_shared<CBlock>();
-            if (!ReadBlockFromDisk(*b, pindex, params)) {
+            if (!ReadBlockFromDisk(*b, pindex, params, true, pool.get())) {
                 while (!inflight.empty())
                     if (!commitFront()) return false;
                 return state.Error("Failed to read block");

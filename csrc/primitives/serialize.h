@@ -339,6 +339,10 @@ public:
         memcpy(dst, p + pos, k);
         pos += k;
     }
+    void ignore(size_t k) {
+        if (k > n - pos) throw ser_error("SpanReader::ignore(): end of data");
+        pos += k;
+    }
     size_t size() const { return n - pos; }
     bool empty() const { return pos == n; }
     size_t tell() const { return pos; }

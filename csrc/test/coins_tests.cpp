@@ -54,7 +54,8 @@ class TestCache : public CCoinsViewCache {
 public:
     explicit TestCache(CCoinsView* base) : CCoinsViewCache(base) {}
     CCoinsMap& Map() const { return cacheCoins; }
-    size_t& Usage() const { return cachedCoinsUsage; }
+    size_t Usage() const { return CachedCoinsUsage(); }
+    void AddUsage(size_t n) { usage[0].bytes += n; } // entries put straight into the map
 };
 
 COutPoint RandOutpoint(std::mt19937_64& r, int universe) {
@@ -297,7 +298,7 @@ struct Layers {
         Put(parent.Map(), pv, pf);
         Put(child.Map(), cv, cf);
         for (auto* c : {&parent, &child})
-            for (auto& kv : c->Map()) c->Usage() += kv.second.coin.DynamicMemoryUsage();
+            for (auto& kv : c->Map()) c->AddUsage(kv.second.coin.DynamicMemoryUsage());
     }
 };
 
