@@ -8,13 +8,16 @@
 #include "test/unittest.h"
 
 #include "node/miner.h"
+#include "node/txdb.h"
 #include "node/validation.h"
 #include "script/sign.h"
 #include "util/strencodings.h"
 #include "util/util.h"
 
 #include <cstdio>
+#include <cstring>
 #include <map>
+#include <random>
 
 using namespace bcp;
 
@@ -207,4 +210,70 @@ TEST_CASE(connectblock_tests, parallel_pass_reject_reasons) {
         if (std::string(c.what) == "valid chain") CHECK_EQ(v.first, std::string("valid"));
         else CHECK(v.first != "valid");
     }
+}
+
+// DecodeBlock (the parallel decode of blocks read for connecting) against the stream decode.
+TEST_CASE(blockdecode_tests, parallel_decode_matches_stream) {
+    std::mt19937_64 rng(7);
+    CBlock b;
+    b.nVersion = 4;
+    b.nHeight = 5000;
+    b.nBits = 0x207fffff;
+    for (int i = 0; i < 700; i++) {
+        CMutableTransaction m;
+        m.nVersion = 1 + (int)(rng() % 2);
+        m.nLockTime = (uint32_t)rng();
+        const int nin = 1 + (int)(rng() % 4), nout = 1 + (int)(rng() % 5);
+        for (int k = 0; k < nin; k++) {
+            uint256 h;
+            for (int w = 0; w < 4; w++) {
+                const uint64_t x = rng();
+                memcpy(h.begin() + 8 * w, &x, 8);
+            }
+            m.vin.push_back(CTxIn(COutPoint(h, (uint32_t)(rng() % 7)),
+                                  CScript(std::vector<unsigned char>(rng() % 300, (unsigned char)k)), (uint32_t)rng()));
+        }
+        for (int k = 0; k < nout; k++)
+            m.vout.push_back(CTxOut((Amount)(rng() % 100000000), CScript(std::vector<unsigned char>(rng() % 60, 0x51))));
+        b.vtx.push_back(MakeTransactionRef(std::move(m)));
+    }
+    DataStream s(SER_DISK, PROTOCOL_VERSION);
+    s << b;
+    const std::vector<unsigned char> raw((const unsigned char*)s.data(), (const unsigned char*)s.data() + s.size());
+    WorkerPool pool(4);
+    for (WorkerPool* p : {(WorkerPool*)nullptr, &pool}) {
+        CBlock got;
+        REQUIRE(DecodeBlock(raw.data(), raw.size(), got, p));
+        CHECK(got.GetBlockHeader().GetHash() == b.GetBlockHeader().GetHash());
+        REQUIRE(got.vtx.size() == b.vtx.size());
+        bool same = true;
+        for (size_t i = 0; i < b.vtx.size(); i++) same &= got.vtx[i]->GetHash() == b.vtx[i]->GetHash();
+        CHECK(same);
+    }
+    // a block cut anywhere fails both ways, like the stream decode
+    for (int t = 0; t < 40; t++) {
+        const size_t cut = 81 + rng() % (raw.size() - 82);
+        CBlock a, c;
+        DataStream ss((const char*)raw.data(), (const char*)raw.data() + cut, SER_DISK, PROTOCOL_VERSION);
+        bool streamOk = true;
+        try {
+            ss >> a;
+        } catch (const std::exception&) {
+            streamOk = false;
+        }
+        CHECK(!streamOk);
+        CHECK(!DecodeBlock(raw.data(), cut, c, &pool));
+        CHECK(c.vtx.empty());
+    }
+    // an absurd transaction count is refused before anything is allocated for it
+    std::vector<unsigned char> bogus(raw.begin(), raw.begin() + 200);
+    SpanReader hr(raw.data(), raw.size(), SER_DISK, PROTOCOL_VERSION);
+    CBlockHeader h;
+    h.Unserialize(hr);
+    const size_t hdrLen = hr.tell();
+    bogus.resize(hdrLen);
+    bogus.push_back(0xfe);
+    for (unsigned char x : {0xff, 0xff, 0xff, 0x01}) bogus.push_back(x);
+    CBlock d;
+    CHECK(!DecodeBlock(bogus.data(), bogus.size(), d, &pool));
 }
