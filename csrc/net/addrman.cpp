@@ -390,6 +390,10 @@ bool CAddrMan::Read(const std::string& path, const unsigned char* magic) {
             if (!in.nRefCount && !in.fInTried) Delete(id);
         }
     } catch (const std::exception& e) {
+        // a file that claims more than it holds leaves no half-loaded table behind
+        // (reference addrdb.cpp CAddrDB::Read -> addr.Clear())
+        std::lock_guard<CCriticalSection> l(cs);
+        Clear();
         return error("%s: deserialize error: %s", __func__, e.what());
     }
     return true;

@@ -77,6 +77,9 @@ public:
     bool Find(const CService& addr, CAddrInfo* out = nullptr) const;
     size_t NumTried() const;
     size_t NumNew() const;
+    // Tests: a fixed (null) bucket key, so placements repeat run to run (the reference's
+    // CAddrManSerializationMock::MakeDeterministic, src/test/net_tests.cpp:23)
+    void MakeDeterministic() { nKey.SetNull(); }
 
     // peers.dat: magic + version + key + entries + SHA256d checksum
     bool Write(const std::string& path, const unsigned char* magic) const;

@@ -93,7 +93,14 @@ std::string UserAgent(uint64_t maxBlockSize) {
     std::vector<std::string> comments{"EB" + GetSubVersionEB(maxBlockSize)};
     for (const std::string& c : gArgs.GetArgs("-uacomment")) comments.push_back(SanitizeString(c));
     std::string ua = FormatSubVersion(CLIENT_NAME, CLIENT_VERSION, comments);
-    if (ua.size() > MAX_SUBVERSION_LENGTH) ua = FormatSubVersion(CLIENT_NAME, CLIENT_VERSION, {comments[0]});
+    if (ua.size() > MAX_SUBVERSION_LENGTH) {
+        // cut to the limit, still closed like a version string (reference net.cpp:3041-3049)
+        LogPrintf("Total length of network version string (%i) exceeds maximum length (%i). Reduce the number or "
+                  "size of uacomments. String has been resized to the max length allowed.\n",
+                  (int)ua.size(), (int)MAX_SUBVERSION_LENGTH);
+        ua.resize(MAX_SUBVERSION_LENGTH - 2);
+        ua += ")/";
+    }
     return ua;
 }
 

@@ -314,12 +314,7 @@ bool Chainstate::LoadExternalBlockFile(FILE* fileIn, CDiskBlockPos* dbp) {
         if (fread(buf.data(), 1, nSize, fileIn) != nSize) break;
         offset += nSize;
         auto pblock = std::make_shared<CBlock>();
-        try {
-            SpanReader r(buf.data(), buf.size(), SER_DISK, PROTOCOL_VERSION);
-            r >> *pblock;
-        } catch (const std::exception&) {
-            continue;
-        }
+        if (!DecodeBlock(buf.data(), buf.size(), *pblock, pool.get())) continue; // transactions decoded in parallel
         const uint256 hash = pblock->GetHash(params.GetConsensus());
         CDiskBlockPos pos;
         if (dbp) {
