@@ -994,6 +994,10 @@ static void RescanFromGenesis(CWallet& w, int64_t nTimeBegin = 0) {
     w.ReacceptWalletTransactions();
 }
 
+// the single-key imports rescan from genesis, which a pruned node cannot (reference
+// rpcdump.cpp:116-118, 234-236, 419-421, 461-463)
+static bool PruneMode() { return GetNode()->chainstate->PruneMode(); }
+
 static UniValue importprivkey(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() < 1 || req.params.size() > 3) ThrowRPC(RPC_INVALID_PARAMS, "importprivkey \"bitcoinprivkey\" ( \"label\" ) ( rescan )");
@@ -1001,6 +1005,7 @@ static UniValue importprivkey(const JSONRPCRequest& req) {
     if (req.params.size() > 1) label = req.params[1].get_str();
     bool fRescan = true;
     if (req.params.size() > 2) fRescan = req.params[2].get_bool();
+    if (fRescan && PruneMode()) ThrowRPC(RPC_WALLET_ERROR, "Rescan is disabled in pruned mode");
     EnsureWalletIsUnlocked(w);
     const CKey key = DecodeSecret(req.params[0].get_str(), P());
     if (!key.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid private key encoding");
@@ -1039,6 +1044,7 @@ static UniValue importaddress(const JSONRPCRequest& req) {
     if (req.params.size() > 1) label = req.params[1].get_str();
     bool fRescan = true;
     if (req.params.size() > 2) fRescan = req.params[2].get_bool();
+    if (fRescan && PruneMode()) ThrowRPC(RPC_WALLET_ERROR, "Rescan is disabled in pruned mode");
     bool fP2SH = false;
     if (req.params.size() > 3) fP2SH = req.params[3].get_bool();
     const std::string s = req.params[0].get_str();
@@ -1066,6 +1072,7 @@ static UniValue importpubkey(const JSONRPCRequest& req) {
     if (req.params.size() > 1) label = req.params[1].get_str();
     bool fRescan = true;
     if (req.params.size() > 2) fRescan = req.params[2].get_bool();
+    if (fRescan && PruneMode()) ThrowRPC(RPC_WALLET_ERROR, "Rescan is disabled in pruned mode");
     if (!IsHex(req.params[0].get_str())) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Pubkey must be a hex string");
     const std::vector<unsigned char> data(ParseHex(req.params[0].get_str()));
     const CPubKey pub(data.begin(), data.end());
@@ -1185,6 +1192,7 @@ static UniValue dumpwallet(const JSONRPCRequest& req) {
 static UniValue importwallet(const JSONRPCRequest& req) {
     CWallet& w = Wallet(req);
     if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "importwallet \"filename\"");
+    if (PruneMode()) ThrowRPC(RPC_WALLET_ERROR, "Importing wallets is disabled in pruned mode");
     EnsureWalletIsUnlocked(w);
     std::ifstream file(req.params[0].get_str());
     if (!file.is_open()) ThrowRPC(RPC_INVALID_PARAMETER, "Cannot open wallet dump file");

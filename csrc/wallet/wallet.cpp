@@ -10,6 +10,7 @@
 #include "util/util.h"
 
 #include <algorithm>
+#include <limits>
 #include <functional>
 #include <random>
 
@@ -721,7 +722,39 @@ const CWalletTx* CWallet::GetWalletTx(const uint256& hash) const {
     return it == mapWallet.end() ? nullptr : &it->second;
 }
 
-void CWallet::AddToSpends(const COutPoint& outpoint, const uint256& wtxid) { mapTxSpends.insert({outpoint, wtxid}); }
+void CWallet::AddToSpends(const COutPoint& outpoint, const uint256& wtxid) {
+    mapTxSpends.insert({outpoint, wtxid});
+    SyncMetaData(outpoint);
+}
+
+// Wallet transactions that spend the same outpoint and differ only in their signatures (a
+// malleated copy, or a clone signed with another hash type) share the oldest one's metadata:
+// comments, order form, smart time, from-me and the account it was sent from (reference
+// wallet.cpp:590-634 SyncMetaData).
+void CWallet::SyncMetaData(const COutPoint& outpoint) {
+    auto range = mapTxSpends.equal_range(outpoint);
+    const CWalletTx* copyFrom = nullptr;
+    int64_t minOrder = std::numeric_limits<int64_t>::max();
+    for (auto it = range.first; it != range.second; ++it) {
+        auto mit = mapWallet.find(it->second);
+        if (mit != mapWallet.end() && mit->second.nOrderPos < minOrder) {
+            minOrder = mit->second.nOrderPos;
+            copyFrom = &mit->second;
+        }
+    }
+    if (!copyFrom) return;
+    for (auto it = range.first; it != range.second; ++it) {
+        auto mit = mapWallet.find(it->second);
+        if (mit == mapWallet.end()) continue;
+        CWalletTx* copyTo = &mit->second;
+        if (copyTo == copyFrom || !copyFrom->IsEquivalentTo(*copyTo)) continue;
+        copyTo->mapValue = copyFrom->mapValue;
+        copyTo->vOrderForm = copyFrom->vOrderForm;
+        copyTo->nTimeSmart = copyFrom->nTimeSmart; // nTimeReceived and nOrderPos stay the copy's own
+        copyTo->fFromMe = copyFrom->fFromMe;
+        copyTo->strFromAccount = copyFrom->strFromAccount;
+    }
+}
 
 void CWallet::AddToSpends(const uint256& wtxid) {
     const CWalletTx& wtx = mapWallet.at(wtxid);

@@ -436,6 +436,7 @@ private:
     bool WriteKeyRecords(const CPubKey& pub, const CKey* key, const std::vector<unsigned char>* crypted);
     void AddToSpends(const uint256& wtxid);
     void AddToSpends(const COutPoint& outpoint, const uint256& wtxid);
+    void SyncMetaData(const COutPoint& outpoint);
     CPubKey DeriveNewChildKey(CKeyMetadata& metadata, CKey& secret);
 
     std::string strWalletName;

@@ -20,6 +20,8 @@ Parity (reference test/functional/):
   the mempool, one that matures a block later is refused (bad-txns-premature-spend-of-coinbase).
 * forknotify.py: more than 50 of the last 100 blocks with a version this node would not mine
   raise "Unknown block versions being mined" through -alertnotify, once.
+* maxblocksinflight.py: invs for 8, 16, 128 and 1024 unknown blocks from one (whitelisted) peer
+  never draw more than 128 block requests in total, and no block is requested twice.
 * p2p-versionbits-warning.py: a period with fewer than threshold blocks signalling an unknown
   versionbit raises nothing; a period at the threshold shows the unknown-version warning in
   getinfo/getmininginfo/getnetworkinfo; after a restart the bit is ACTIVE and the node warns
@@ -438,5 +440,27 @@ def test_versionbits_warning(tmp_path):
         n.stop()
         assert vb_pattern.match(_read(alert))
         n.start()
+    finally:
+        n.stop()
+
+
+def test_max_blocks_in_flight(tmp_path):
+    import random
+    MAX_REQUESTS = 128
+    n = node(tmp_path, "n", "-whitelist=127.0.0.1")
+    try:
+        n.rpc.generate(1)  # leave IBD
+        peer = P2PPeer().connect("127.0.0.1", n.p2p_port)
+        rng = random.Random(5)
+        for count in (8, 16, 128, 1024):
+            peer.send(msg_inv([CInv(MSG_BLOCK, rng.randrange(0, 1 << 256)) for _ in range(count)]))
+            peer.sync_with_ping()
+            time.sleep(2)
+            with peer.lock:
+                asked = [inv.hash for inv in peer.getdata_requests if inv.type == MSG_BLOCK]
+            assert len(asked) == len(set(asked)), "a block was requested more than once"
+            assert len(asked) <= MAX_REQUESTS, len(asked)
+        peer.sync_with_ping()  # still connected
+        peer.close()
     finally:
         n.stop()

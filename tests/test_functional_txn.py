@@ -8,6 +8,8 @@ Parity:
   - the payment is conflicted (negative confirmations, listed in walletconflicts);
   - the double spend is confirmed;
   - the balance counts only the double spend.
+* reference test/functional/txn_clone.py: the same split, but the conflicting spend is a malleated
+  clone of the payment (signed ALL|FORKID|ANYONECANPAY); account balances follow the clone.
 * reference test/functional/smartfees.py: transactions at a spread of fee rates, with blocks too
   small to take all of them, so cheaper ones wait longer. From the estimator's data:
   - estimatefee(n) stays within the range of fee rates that were paid;
@@ -137,3 +139,74 @@ def test_smartfees(tmp_path):
             assert lo / 2 <= D(s["feerate"]) <= hi * 2
     finally:
         n.stop()
+
+
+def test_txn_clone(tmp_path):
+    """reference test/functional/txn_clone.py: a malleated clone of a wallet payment (same input
+    and outputs, signed ALL|FORKID|ANYONECANPAY) is mined on the other side of a split and wins."""
+    a = BcpdProcess(str(tmp_path / "a"), extra_args=["-gpu=0"])
+    b = BcpdProcess(str(tmp_path / "b"), extra_args=["-gpu=0"])
+    a.start()
+    b.start()
+    try:
+        a.rpc.generate(110)
+        connect(a, b)
+        wait_until(lambda: b.rpc.getblockcount() == 110)
+        for p in a.rpc.getpeerinfo():
+            a.rpc.disconnectnode(p["addr"])
+        wait_until(lambda: a.rpc.getconnectioncount() == 0 and b.rpc.getconnectioncount() == 0)
+        starting = D(a.rpc.getbalance())
+        assert starting == 500
+        a.rpc.getnewaddress("")
+        a.rpc.settxfee(0.001)
+        fund_foo_txid = a.rpc.sendfrom("", a.rpc.getnewaddress("foo"), 219)
+        fund_foo = a.rpc.gettransaction(fund_foo_txid)
+        fund_bar_txid = a.rpc.sendfrom("", a.rpc.getnewaddress("bar"), 29)
+        fund_bar = a.rpc.gettransaction(fund_bar_txid)
+        assert D(a.rpc.getbalance("")) == starting - 219 - 29 + D(fund_foo["fee"]) + D(fund_bar["fee"])
+        to_b = b.rpc.getnewaddress("from0")
+        txid1 = a.rpc.sendfrom("foo", to_b, 40, 0)
+        txid2 = a.rpc.sendfrom("bar", to_b, 20, 0)
+        # the clone: tx1's input and outputs, another signature hash type
+        raw1 = a.rpc.getrawtransaction(txid1, 1)
+        assert len(raw1["vin"]) == 1
+        outs = {o["scriptPubKey"]["addresses"][0]: float(o["value"]) for o in raw1["vout"]}
+        clone_raw = a.rpc.createrawtransaction([{"txid": raw1["vin"][0]["txid"], "vout": raw1["vin"][0]["vout"]}],
+                                               outs, raw1["locktime"])
+        clone = a.rpc.signrawtransaction(clone_raw, None, None, "ALL|FORKID|ANYONECANPAY")
+        assert clone["complete"]
+        tx1 = a.rpc.gettransaction(txid1)
+        tx2 = a.rpc.gettransaction(txid2)
+        expected = starting + D(fund_foo["fee"]) + D(fund_bar["fee"])
+        expected += D(tx1["amount"]) + D(tx1["fee"]) + D(tx2["amount"]) + D(tx2["fee"])
+        assert D(a.rpc.getbalance()) == expected
+        assert D(a.rpc.getbalance("foo", 0)) == 219 + D(tx1["amount"]) + D(tx1["fee"])
+        assert D(a.rpc.getbalance("bar", 0)) == 29 + D(tx2["amount"]) + D(tx2["fee"])
+        assert tx1["confirmations"] == 0 and tx2["confirmations"] == 0
+        # the clone (and its parent) are mined on b's side
+        b.rpc.sendrawtransaction(fund_foo["hex"])
+        clone_txid = b.rpc.sendrawtransaction(clone["hex"])
+        assert clone_txid != txid1
+        b.rpc.generate(1)
+        connect(a, b)
+        b.rpc.sendrawtransaction(fund_bar["hex"])
+        b.rpc.sendrawtransaction(tx2["hex"])
+        b.rpc.generate(1)
+        wait_until(lambda: a.rpc.getbestblockhash() == b.rpc.getbestblockhash())
+        tx1 = a.rpc.gettransaction(txid1)
+        tx1_clone = a.rpc.gettransaction(clone_txid)
+        tx2 = a.rpc.gettransaction(txid2)
+        assert tx1["confirmations"] == -2
+        assert tx1_clone["confirmations"] == 2
+        assert tx2["confirmations"] == 1
+        # two more coinbases matured; the clone moved exactly what tx1 would have
+        expected += 100
+        wait_until(lambda: D(a.rpc.getbalance()) == expected)
+        assert D(a.rpc.getbalance("*", 0)) == expected
+        assert D(a.rpc.getbalance("foo")) == 219 + D(tx1["amount"]) + D(tx1["fee"])
+        assert D(a.rpc.getbalance("bar", 0)) == 29 + D(tx2["amount"]) + D(tx2["fee"])
+        assert D(a.rpc.getbalance("", 0)) == starting - 219 + D(fund_foo["fee"]) - 29 + D(fund_bar["fee"]) + 100
+        assert D(b.rpc.getbalance("from0", 0)) == -(D(tx1["amount"]) + D(tx2["amount"]))
+    finally:
+        a.stop()
+        b.stop()
