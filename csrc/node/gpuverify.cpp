@@ -41,8 +41,8 @@ void GpuVerifyService::SetDevices(const std::vector<int>& devs) {
 
 // Default: every visible device, two lanes each (the built-in miner runs only on demand, and
 // its streams share a device at a lower priority than validation's). Two lanes per device let
-// one shard's host fill overlap the other's kernels: a 199k-signature batch took 10.5 ms on one
-// lane and 8.8 ms on two of the same MI355X (profiles/lanes_headers_r4.md).
+// one shard's host fill overlap the other's kernels: a 199k-signature batch took 10.1 ms on one
+// lane and 8.2 ms on two of the same MI355X (profiles/lanes_headers_r4.md).
 static std::vector<int> AllDevices() {
     std::vector<int> d;
     if (!gpu::GpuAvailable()) return d;
