@@ -113,6 +113,24 @@ std::vector<uint64_t> ShortTxIdBatch(uint64_t k0, uint64_t k1, const unsigned ch
 std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
                                       const std::vector<unsigned char>& pub33, int device = -1);
 
+// --------------------------------------------------------------- device-resident entry points
+// The tensor API (bitcoincashplus_amd.ops with torch tensors on the GPU): every pointer is
+// device memory on `device`, the kernels are enqueued on `stream` (a hipStream_t passed as an
+// integer, e.g. torch.cuda.current_stream().cuda_stream) after the work already queued there,
+// and nothing is copied or synchronised. The caller keeps the buffers alive until the stream
+// has run (torch's caching allocator does this for tensors used on their own stream).
+// out32[i] = SHA256d(in64[64*i .. 64*i+64))
+void Sha256d64Device(const void* in64, void* out32, size_t n, int device, uintptr_t stream);
+// out[i] = BIP152 short id of txid i (48 bits in a uint64); txids32 16-byte aligned
+void ShortTxIdsDevice(uint64_t k0, uint64_t k1, const void* txids32, void* out64, size_t n, int device,
+                      uintptr_t stream);
+// Device scratch the ECDSA kernels need per signature (the prep kernel's job records).
+size_t EcdsaJobBytes();
+// result[i] = 1 iff signature i verifies; inputs as EcdsaVerifyBatch (msg32 n x 32, sig64 compact
+// r||s n x 64, pub33 compressed n x 33), jobs = n x EcdsaJobBytes() of scratch.
+void EcdsaVerifyDevice(const void* msg32, const void* sig64, const void* pub33, void* jobs, void* result, size_t n,
+                       int device, uintptr_t stream);
+
 // --------------------------------------------------------------- verification lanes
 // A verification lane is one device plus one HIP stream (created at the device's greatest
 // priority when `highPriority`, so a validation batch is scheduled ahead of the persistent

@@ -29,6 +29,22 @@ inline int UseDevice(int device) {
     return device;
 }
 
+// Makes `device` (-1: the current one) current for a scope and restores the caller's device
+// after: the device-resident entry points run on threads (torch's) whose current device matters.
+struct DeviceScope {
+    int prev = -1;
+    int device = -1;
+    explicit DeviceScope(int d) {
+        BCP_HIP_CHECK(hipGetDevice(&prev));
+        device = UseDevice(d);
+    }
+    ~DeviceScope() {
+        if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+    }
+    DeviceScope(const DeviceScope&) = delete;
+    DeviceScope& operator=(const DeviceScope&) = delete;
+};
+
 // RAII device buffer.
 template <typename T> struct DevBuf {
     T* p = nullptr;

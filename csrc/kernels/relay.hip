@@ -102,5 +102,16 @@ std::vector<uint64_t> ShortTxIdBatch(uint64_t k0, uint64_t k1, const unsigned ch
     return out;
 }
 
+void ShortTxIdsDevice(uint64_t k0, uint64_t k1, const void* txids32, void* out64, size_t n, int device,
+                      uintptr_t stream) {
+    if (!n) return;
+    if (reinterpret_cast<uintptr_t>(txids32) % 16) throw std::invalid_argument("ShortTxIdsDevice: txids not 16-byte aligned");
+    DeviceScope ds(device);
+    hipLaunchKernelGGL(bcpk::shortid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), k0, k1, static_cast<const uint4*>(txids32),
+                       static_cast<uint64_t*>(out64), n);
+    BCP_HIP_CHECK(hipGetLastError());
+}
+
 } // namespace gpu
 } // namespace bcp

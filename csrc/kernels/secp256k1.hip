@@ -1134,6 +1134,26 @@ void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, un
     L.items += n;
 }
 
+size_t EcdsaJobBytes() { return sizeof(Job); }
+
+void EcdsaVerifyDevice(const void* msg32, const void* sig64, const void* pub33, void* jobs, void* result, size_t n,
+                       int device, uintptr_t stream) {
+    if (!n) return;
+    if (reinterpret_cast<uintptr_t>(jobs) % alignof(Job)) throw std::invalid_argument("EcdsaVerifyDevice: job scratch alignment");
+    DeviceScope ds(device);
+    Table& tb = T(ds.device);
+    std::call_once(tb.once, [&] { InitTable(tb); });
+    const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    Job* d_jobs = static_cast<Job*>(jobs);
+    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_jobs,
+                       static_cast<const unsigned char*>(msg32), static_cast<const unsigned char*>(sig64),
+                       static_cast<const unsigned char*>(pub33), (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, d_jobs, tb.d_gtab,
+                       static_cast<uint8_t*>(result), (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+}
+
 std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
                                       const std::vector<unsigned char>& pub33, int device) {
     const size_t n = msg32.size() / 32;

@@ -271,6 +271,14 @@ std::vector<unsigned char> Sha256d64Batch(const std::vector<unsigned char>& data
     return out;
 }
 
+void Sha256d64Device(const void* in64, void* out32, size_t n, int device, uintptr_t stream) {
+    if (!n) return;
+    DeviceScope ds(device);
+    hipLaunchKernelGGL(bcpk::sha256d_64, dim3(grid_for(n)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       static_cast<const uint8_t*>(in64), static_cast<uint8_t*>(out32), n);
+    BCP_HIP_CHECK(hipGetLastError());
+}
+
 std::vector<unsigned char> Sha256dBatch(const std::vector<unsigned char>& data, const std::vector<uint64_t>& offs,
                                         const std::vector<uint32_t>& lens, int device) {
     if (offs.size() != lens.size()) throw std::invalid_argument("Sha256dBatch: offs/lens mismatch");

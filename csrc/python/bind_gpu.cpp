@@ -192,6 +192,33 @@ void bind_gpu(pyb::module_& m) {
             return pyb::make_tuple(to_bytes(root), mutated);
         },
         pyb::arg("leaves"), pyb::arg("device") = -1);
+    // device-resident entry points: device pointers and a stream handle (torch tensors' data_ptr()
+    // and torch.cuda.current_stream().cuda_stream); asynchronous on that stream
+    m.def(
+        "sha256d64_device",
+        [](uintptr_t in, uintptr_t out, size_t n, int device, uintptr_t stream) {
+            gpu::Sha256d64Device(reinterpret_cast<const void*>(in), reinterpret_cast<void*>(out), n, device, stream);
+        },
+        pyb::arg("in_ptr"), pyb::arg("out_ptr"), pyb::arg("n"), pyb::arg("device"), pyb::arg("stream"));
+    m.def(
+        "short_txids_device",
+        [](uint64_t k0, uint64_t k1, uintptr_t in, uintptr_t out, size_t n, int device, uintptr_t stream) {
+            gpu::ShortTxIdsDevice(k0, k1, reinterpret_cast<const void*>(in), reinterpret_cast<void*>(out), n, device,
+                                  stream);
+        },
+        pyb::arg("k0"), pyb::arg("k1"), pyb::arg("in_ptr"), pyb::arg("out_ptr"), pyb::arg("n"), pyb::arg("device"),
+        pyb::arg("stream"));
+    m.def("ecdsa_job_bytes", &gpu::EcdsaJobBytes);
+    m.def(
+        "ecdsa_verify_device",
+        [](uintptr_t msg, uintptr_t sig, uintptr_t pub, uintptr_t jobs, uintptr_t result, size_t n, int device,
+           uintptr_t stream) {
+            gpu::EcdsaVerifyDevice(reinterpret_cast<const void*>(msg), reinterpret_cast<const void*>(sig),
+                                   reinterpret_cast<const void*>(pub), reinterpret_cast<void*>(jobs),
+                                   reinterpret_cast<void*>(result), n, device, stream);
+        },
+        pyb::arg("msg_ptr"), pyb::arg("sig_ptr"), pyb::arg("pub_ptr"), pyb::arg("jobs_ptr"), pyb::arg("result_ptr"),
+        pyb::arg("n"), pyb::arg("device"), pyb::arg("stream"));
     m.def(
         "short_txid_batch_gpu",
         [](uint64_t k0, uint64_t k1, const pyb::bytes& txids, int device) {
