@@ -13,6 +13,8 @@
 // one of these checks (order-of-checks only changes which reason, not the result).
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+
 #include "kernels/blake2b_device.h"
 #include "kernels/gpu_api.h"
 #include "kernels/hip_util.h"
@@ -190,7 +192,9 @@ static void verify_lane_headers(LaneState& L, size_t n, const std::function<void
     const size_t ib = (n * 140 + 15) & ~(size_t)15, pb = n * C::SOLW;
     unsigned char* h_in = L.Host(0, ib + pb + n);
     uint8_t* lenok = h_in + ib + pb;
+    const auto t0 = std::chrono::steady_clock::now();
     fill(h_in, h_in + ib, lenok);
+    const auto t1 = std::chrono::steady_clock::now();
     uint8_t* h_ok = L.Host(1, n);
     unsigned char* d_in = L.Dev(0, ib + pb);
     bcpk::EhBaseState* d_states = reinterpret_cast<bcpk::EhBaseState*>(L.Dev(2, n * sizeof(bcpk::EhBaseState)));
@@ -205,6 +209,9 @@ static void verify_lane_headers(LaneState& L, size_t n, const std::function<void
     BCP_HIP_CHECK(hipMemcpyAsync(h_ok, d_ok, n, hipMemcpyDeviceToHost, L.stream));
     BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
     for (size_t i = 0; i < n; ++i) result[i] = lenok[i] ? h_ok[i] : 0;
+    const auto t2 = std::chrono::steady_clock::now();
+    L.fillMicros += std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+    L.deviceMicros += std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count();
     L.batches++;
     L.items += n;
 }
@@ -238,6 +245,8 @@ int VerifyLane::Device() const { return impl->device; }
 int VerifyLane::Priority() const { return impl->priority; }
 uint64_t VerifyLane::Batches() const { return impl->batches; }
 uint64_t VerifyLane::Items() const { return impl->items; }
+uint64_t VerifyLane::FillMicros() const { return impl->fillMicros; }
+uint64_t VerifyLane::DeviceMicros() const { return impl->deviceMicros; }
 
 void VerifyLane::Equihash(unsigned N, unsigned K, const EhBaseState* states,
                           const std::vector<unsigned char>* const* sols, size_t n, uint8_t* result) {

@@ -168,6 +168,9 @@ public:
     // Batches and items this lane has run (service statistics).
     uint64_t Batches() const;
     uint64_t Items() const;
+    // time spent in the callers' fills (host) and in copies + kernels + the wait (device)
+    uint64_t FillMicros() const;
+    uint64_t DeviceMicros() const;
     struct Impl;
 
 private:

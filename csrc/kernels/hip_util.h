@@ -93,6 +93,9 @@ struct LaneState {
     HostBuf<unsigned char> host[SLOTS];
     DevBuf<unsigned char> dev[SLOTS];
     uint64_t batches = 0, items = 0;
+    // host share (the caller's fill into pinned staging) and device share (copies, kernels and
+    // the wait for them) of the batches, microseconds
+    uint64_t fillMicros = 0, deviceMicros = 0;
     unsigned char* Host(int slot, size_t bytes) {
         if (host[slot].n < bytes) host[slot].alloc(bytes + bytes / 2);
         return host[slot].p;

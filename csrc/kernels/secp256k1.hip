@@ -25,6 +25,7 @@
 #include "kernels/modinv.h"
 #include "secp256k1/secp256k1.h"
 
+#include <chrono>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -1115,7 +1116,9 @@ void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, un
     std::call_once(tb.once, [&] { InitTable(tb); });
     unsigned char* h_in = L.Host(0, n * 129);
     uint8_t* h_out = L.Host(1, n);
+    const auto t0 = std::chrono::steady_clock::now();
     fill(h_in, h_in + n * 32, h_in + n * 96);
+    const auto t1 = std::chrono::steady_clock::now();
     unsigned char* d_in = L.Dev(0, n * 129);
     Job* d_jobs = reinterpret_cast<Job*>(L.Dev(1, n * sizeof(Job)));
     uint8_t* d_out = L.Dev(2, n);
@@ -1130,6 +1133,9 @@ void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, un
     BCP_HIP_CHECK(hipMemcpyAsync(h_out, d_out, n, hipMemcpyDeviceToHost, L.stream));
     BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
     memcpy(result, h_out, n);
+    const auto t2 = std::chrono::steady_clock::now();
+    L.fillMicros += std::chrono::duration_cast<std::chrono::microseconds>(t1 - t0).count();
+    L.deviceMicros += std::chrono::duration_cast<std::chrono::microseconds>(t2 - t1).count();
     L.batches++;
     L.items += n;
 }

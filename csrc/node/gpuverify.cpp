@@ -156,6 +156,8 @@ void GpuVerifyService::RunSharded(size_t n, size_t minShard,
                 fn(*L->gl, lo, hi, *L->fill);
                 L->batches++;
                 L->items += hi - lo;
+                L->fillMicros = L->gl->FillMicros(); // published for Stats() (this is the lane's thread)
+                L->deviceMicros = L->gl->DeviceMicros();
             } catch (...) {
                 e = std::current_exception();
             }
@@ -259,7 +261,8 @@ std::vector<GpuVerifyService::LaneStats> GpuVerifyService::Stats() const {
     std::vector<LaneStats> out;
     std::lock_guard<std::mutex> l(m);
     for (const auto& L : lanes) {
-        out.push_back(LaneStats{L->device, L->priority.load(), L->batches.load(), L->items.load()});
+        out.push_back(LaneStats{L->device, L->priority.load(), L->batches.load(), L->items.load(),
+                                L->fillMicros.load(), L->deviceMicros.load()});
     }
     return out;
 }

@@ -71,6 +71,7 @@ public:
         int device;
         int priority;
         uint64_t batches, items;
+        uint64_t fillMicros, deviceMicros; // host fill vs device share of the lane's batches
     };
     std::vector<LaneStats> Stats() const;
     uint64_t ShardedBatches() const;
@@ -90,6 +91,7 @@ private:
         std::string initError;
         std::atomic<int> priority{0};
         std::atomic<uint64_t> batches{0}, items{0};
+        std::atomic<uint64_t> fillMicros{0}, deviceMicros{0}; // the lane's host fill vs device time
         std::unique_ptr<WorkerPool> fill; // this lane's host-fill workers
     };
     static void LaneLoop(Lane* L);

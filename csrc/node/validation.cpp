@@ -872,6 +872,12 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // serial pass below instead, which yields the reference's exact reject reason.
     bool fastDone = false;
     if (fEnforceBIP30 && opts.parallelUtxoMinTx > 0 && ntx >= opts.parallelUtxoMinTx && maxJobs > 0) {
+        int64_t tSub = GetTimeMicros();
+        auto sub = [&](ConnectPhase ph) {
+            const int64_t t = GetTimeMicros();
+            phaseMicros[ph].fetch_add(t - tSub, std::memory_order_relaxed);
+            tSub = t;
+        };
         size_t tcap = 16;
         while (tcap < 2 * ntx) tcap <<= 1;
         std::vector<int32_t> tslot(tcap, -1); // block-local txid -> index (CheckBlock refused duplicates)
@@ -924,6 +930,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         std::atomic<bool> bad{false};
         txSigOps[0] = legacySigOps[0];
         const size_t TCHUNK = 32;
+        sub(PH_FU_SETUP);
         pool->ParallelFor(
             (ntx + TCHUNK - 1) / TCHUNK,
             [&](size_t chunk) {
@@ -991,6 +998,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             },
             1);
         uint64_t sigTotal = 0;
+        sub(PH_FU_CHECKS);
         for (size_t i = 0; i < ntx && !bad.load(); i++) {
             if (txSigOps[i] > MAX_TX_SIGOPS_COUNT) bad = true; // the coinbase's legacy count
             sigTotal += txSigOps[i];
@@ -1049,6 +1057,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 },
                 64);
             nProduced = jobOff[ntx];
+            sub(PH_FU_UNDO);
             if (queued && nProduced > 0) {
                 scriptQueue->Publish(nProduced);
                 nPublished = nProduced;
@@ -1088,6 +1097,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                     }
                 },
                 pool.get());
+            sub(PH_FU_APPLY);
             if (!applyError.empty()) return state.Error("ConnectBlock: " + applyError);
         }
     }

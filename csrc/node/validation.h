@@ -210,8 +210,12 @@ public:
     // the connect benchmarks: CheckBlock, the parallel read-only pass (BIP30, input prefetch,
     // per-tx precompute), the serial UTXO pass, the wait for
     // the script jobs after it, gathering the deferred checks, and the synchronous batch verify.
-    // PH_BLOCKS counts connected blocks, PH_FASTUTXO those whose UTXO pass took the parallel path
-    enum ConnectPhase { PH_CHECK, PH_PRECOMPUTE, PH_UTXO, PH_SCRIPTS, PH_COLLECT, PH_BATCH, PH_BLOCKS, PH_FASTUTXO, PH_COUNT };
+    // PH_BLOCKS counts connected blocks, PH_FASTUTXO those whose UTXO pass took the parallel path;
+    // PH_FU_* split that parallel pass (setup, checks, undo + jobs, view updates; inside PH_UTXO)
+    enum ConnectPhase {
+        PH_CHECK, PH_PRECOMPUTE, PH_UTXO, PH_SCRIPTS, PH_COLLECT, PH_BATCH, PH_BLOCKS, PH_FASTUTXO,
+        PH_FU_SETUP, PH_FU_CHECKS, PH_FU_UNDO, PH_FU_APPLY, PH_COUNT
+    };
     int64_t ConnectPhaseMicros(ConnectPhase ph) const { return phaseMicros[ph].load(std::memory_order_relaxed); }
 
 private:

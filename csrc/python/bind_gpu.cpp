@@ -313,6 +313,8 @@ void bind_gpu(pyb::module_& m) {
             d["priority"] = L.priority;
             d["batches"] = L.batches;
             d["items"] = L.items;
+            d["fill_us"] = L.fillMicros;
+            d["device_us"] = L.deviceMicros;
             lanes.append(d);
         }
         pyb::dict out;

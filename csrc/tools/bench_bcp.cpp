@@ -881,6 +881,15 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
     const SigVerifyStats s0 = GetSigVerifyStats();
     int64_t ph0[Chainstate::PH_COUNT];
     for (int k = 0; k < Chainstate::PH_COUNT; k++) ph0[k] = f.cs->ConnectPhaseMicros((Chainstate::ConnectPhase)k);
+    auto laneTimes = [] {
+        uint64_t fill = 0, dev = 0;
+        for (const auto& L : GpuVerifyService::Instance().Stats()) {
+            fill += L.fillMicros;
+            dev += L.deviceMicros;
+        }
+        return std::make_pair(fill, dev);
+    };
+    const auto lt0 = laneTimes();
     int iters = 0;
     while (st.KeepRunning()) {
         CValidationState state;
@@ -899,11 +908,19 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
             (unsigned long long)(s1.gpu_failures - s0.gpu_failures),
             (double)(s1.multisig_groups - s0.multisig_groups) / iters);
     auto ms = [&](Chainstate::ConnectPhase k) { return 0.001 * (f.cs->ConnectPhaseMicros(k) - ph0[k]) / iters; };
+    if (useGpu) {
+        const auto lt1 = laneTimes();
+        fprintf(stderr, "# GPU: verify lanes (ms/block, summed over lanes): host fill %.2f, device (copies + kernels) %.2f\n",
+                0.001 * (lt1.first - lt0.first) / iters, 0.001 * (lt1.second - lt0.second) / iters);
+    }
     fprintf(stderr, "# %s: connect phases (ms/block): checkblock %.2f, prefetch+precompute %.2f, utxo pass %.2f, "
                     "script wait %.2f, collect %.2f, batch %.2f; parallel UTXO pass in %lld of %d blocks\n",
             useGpu ? "GPU" : "CPU", ms(Chainstate::PH_CHECK), ms(Chainstate::PH_PRECOMPUTE), ms(Chainstate::PH_UTXO),
             ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_COLLECT), ms(Chainstate::PH_BATCH),
             (long long)(f.cs->ConnectPhaseMicros(Chainstate::PH_FASTUTXO) - ph0[Chainstate::PH_FASTUTXO]), iters);
+    fprintf(stderr, "# %s: parallel UTXO pass (ms/block): setup %.2f, checks %.2f, undo+jobs %.2f, view updates %.2f\n",
+            useGpu ? "GPU" : "CPU", ms(Chainstate::PH_FU_SETUP), ms(Chainstate::PH_FU_CHECKS), ms(Chainstate::PH_FU_UNDO),
+            ms(Chainstate::PH_FU_APPLY));
     SetGpuSigThreshold(thr);
 }
 } // namespace
