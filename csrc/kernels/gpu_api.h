@@ -154,6 +154,14 @@ public:
     void EcdsaFill(size_t n, const std::function<void(unsigned char* msg32, unsigned char* sig64,
                                                         unsigned char* pub33)>& fill,
                    uint8_t* result);
+    // Same with DER signatures parsed on the device: sig73 holds n slots of [length byte][up to
+    // 72 DER bytes] (hash type stripped), parsed with the reference's lax rules
+    // (src/pubkey.cpp ecdsa_signature_parse_der_lax) and low-S normalised by the prep kernel; a
+    // signature that does not parse verifies false. (The host then only copies bytes.)
+    static constexpr size_t DER_SLOT = 73;
+    void EcdsaDerFill(size_t n, const std::function<void(unsigned char* msg32, unsigned char* sig73,
+                                                           unsigned char* pub33)>& fill,
+                      uint8_t* result);
     // n block headers: fill(in140, sols, lenok) writes each header's 140-byte Equihash input
     // (CEquihashInput || nNonce), its solution (EquihashSolutionBytes bytes) and whether the
     // solution had that length into the lane's pinned staging; the device builds the BLAKE2b

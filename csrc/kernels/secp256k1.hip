@@ -741,26 +741,119 @@ __device__ __forceinline__ void store_be32(unsigned char* b, const fe& a) {
     }
 }
 
+// Lax DER parse on the device (the reference's ecdsa_signature_parse_der_lax, src/pubkey.cpp,
+// as secp::sig_parse_der_lax on the host): false if the encoding cannot be walked; otherwise
+// r and s as 32-byte big-endian values, both zero when either does not fit in 32 bytes.
+__device__ bool der_lax_parse(const unsigned char* in, uint32_t len, unsigned char out[64]) {
+    for (int i = 0; i < 64; i++) out[i] = 0;
+    uint32_t pos = 0;
+    if (pos == len || in[pos] != 0x30) return false;
+    pos++;
+    if (pos == len) return false;
+    uint32_t lenbyte = in[pos++];
+    if (lenbyte & 0x80) {
+        lenbyte -= 0x80;
+        if (pos + lenbyte > len) return false;
+        pos += lenbyte;
+    }
+    uint32_t ipos[2], ilen[2];
+    for (int k = 0; k < 2; k++) {
+        if (pos == len || in[pos] != 0x02) return false;
+        pos++;
+        if (pos == len) return false;
+        lenbyte = in[pos++];
+        uint64_t l;
+        if (lenbyte & 0x80) {
+            lenbyte -= 0x80;
+            if (pos + lenbyte > len) return false;
+            while (lenbyte > 0 && in[pos] == 0) {
+                pos++;
+                lenbyte--;
+            }
+            if (lenbyte >= 8) return false;
+            l = 0;
+            while (lenbyte > 0) {
+                l = (l << 8) + in[pos];
+                pos++;
+                lenbyte--;
+            }
+        } else {
+            l = lenbyte;
+        }
+        if (l > (uint64_t)(len - pos)) return false;
+        ipos[k] = pos;
+        ilen[k] = (uint32_t)l;
+        pos += (uint32_t)l;
+    }
+    bool overflow = false;
+    for (int k = 0; k < 2; k++) {
+        while (ilen[k] > 0 && in[ipos[k]] == 0) {
+            ilen[k]--;
+            ipos[k]++;
+        }
+        if (ilen[k] > 32) overflow = true;
+    }
+    if (!overflow)
+        for (int k = 0; k < 2; k++)
+            for (uint32_t b = 0; b < ilen[k]; b++) out[32 * k + 32 - ilen[k] + b] = in[ipos[k] + b];
+    return true;
+}
+
+// s > n/2 ? (the high half of the group order)
+__device__ __forceinline__ bool sc_is_high(const fe& a) {
+    // n/2 = 7FFFFFFF FFFFFFFF FFFFFFFF FFFFFFFF 5D576E73 57A4501D DFE92F46 681B20A0
+    const uint32_t H[8] = {0x681B20A0, 0xDFE92F46, 0x57A4501D, 0x5D576E73, 0xFFFFFFFF, 0xFFFFFFFF, 0xFFFFFFFF, 0x7FFFFFFF};
+    for (int i = 7; i >= 0; i--)
+        if (a.v[i] != H[i]) return a.v[i] > H[i];
+    return false;
+}
+
 // One lane per signature: scalar checks, s^-1, u1, u2, wNAF(u2), r+n.
 // Reads the packed host arrays (msg 32 B, compact sig 64 B, compressed key 33 B per
 // signature: 129 B uploaded instead of a 272 B Job) and builds the Job on the device.
+// DER: sig holds [length][72 DER bytes] slots, parsed and low-S normalised here; otherwise
+// 64-byte compact r||s, already normalised by the host.
+template <bool DER>
 __global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs, const unsigned char* __restrict__ msg,
                                                          const unsigned char* __restrict__ sig,
                                                          const unsigned char* __restrict__ pub, int n) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= n) return;
     Job& J = jobs[idx];
-    const unsigned char* sg = sig + (size_t)idx * 64;
     const unsigned char* pk = pub + (size_t)idx * 33;
-#pragma unroll
-    for (int i = 0; i < 32; i++) J.r[i] = sg[i];
+    unsigned char c64[64];
+    bool parsed = true;
+    if constexpr (DER) {
+        const unsigned char* slot = sig + (size_t)idx * VerifyLane::DER_SLOT;
+        unsigned char der[72];
+        const uint32_t len = slot[0] > 72 ? 72u : slot[0];
+        for (uint32_t i = 0; i < 72; i++) der[i] = i < len ? slot[1 + i] : 0;
+        parsed = der_lax_parse(der, len, c64);
+    } else {
+        const unsigned char* sg = sig + (size_t)idx * 64;
+        for (int i = 0; i < 64; i++) c64[i] = sg[i];
+    }
 #pragma unroll
     for (int i = 0; i < 33; i++) J.pub[i] = pk[i];
     fe r, s, z;
-    load_be32(r, sg);
-    load_be32(s, sg + 32);
+    load_be32(r, c64);
+    load_be32(s, c64 + 32);
     load_be32(z, msg + (size_t)idx * 32);
-    const bool ok = sc_lt_n(r) && sc_lt_n(s) && !fe_is_zero(r) && !fe_is_zero(s);
+    bool ok = parsed && sc_lt_n(r) && sc_lt_n(s);
+    if (DER && ok && sc_is_high(s)) { // low-S normalisation (secp::sig_normalize)
+        uint64_t br = 0;
+        for (int i = 0; i < 8; i++) {
+            const uint64_t d = (uint64_t)N_LIMBS[i] - s.v[i] - br;
+            s.v[i] = (uint32_t)d;
+            br = (d >> 63) & 1;
+        }
+    }
+    ok = ok && !fe_is_zero(r) && !fe_is_zero(s);
+    if (!ok) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) r.v[i] = 0;
+    }
+    store_be32(J.r, r);
     if (!sc_lt_n(z)) sc_sub_n(z); // z < 2^256 < 2n
     fe one;
 #pragma unroll
@@ -1106,26 +1199,30 @@ void VerifyLane::Ecdsa(const unsigned char* msg32, const unsigned char* sig64, c
         result);
 }
 
-void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, unsigned char*, unsigned char*)>& fill,
-                           uint8_t* result) {
+namespace {
+// Shared by EcdsaFill (compact sigs, sigBytes 64) and EcdsaDerFill (DER slots): staging is
+// msg n x 32 | sig n x sigBytes | pub n x 33, one H2D copy, prep + verify, one D2H copy.
+void LaneEcdsa(LaneState& L, size_t n, size_t sigBytes,
+               const std::function<void(unsigned char*, unsigned char*, unsigned char*)>& fill, uint8_t* result) {
     if (n == 0) return;
-    LaneState& L = *impl;
     BCP_HIP_CHECK(hipSetDevice(L.device));
     Table& tb = T(L.device);
     // a throwing init leaves the once_flag unset, so the next call retries it
     std::call_once(tb.once, [&] { InitTable(tb); });
-    unsigned char* h_in = L.Host(0, n * 129);
+    const size_t bytes = n * (32 + sigBytes + 33);
+    unsigned char* h_in = L.Host(0, bytes);
     uint8_t* h_out = L.Host(1, n);
     const auto t0 = std::chrono::steady_clock::now();
-    fill(h_in, h_in + n * 32, h_in + n * 96);
+    fill(h_in, h_in + n * 32, h_in + n * (32 + sigBytes));
     const auto t1 = std::chrono::steady_clock::now();
-    unsigned char* d_in = L.Dev(0, n * 129);
+    unsigned char* d_in = L.Dev(0, bytes);
     Job* d_jobs = reinterpret_cast<Job*>(L.Dev(1, n * sizeof(Job)));
     uint8_t* d_out = L.Dev(2, n);
-    BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, n * 129, hipMemcpyHostToDevice, L.stream));
-    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, L.stream, d_jobs,
-                       (const unsigned char*)d_in, (const unsigned char*)(d_in + n * 32),
-                       (const unsigned char*)(d_in + n * 96), (int)n);
+    BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, bytes, hipMemcpyHostToDevice, L.stream));
+    const dim3 pg((unsigned)((n + 255) / 256));
+    const unsigned char *dm = d_in, *ds = d_in + n * 32, *dp = d_in + n * (32 + sigBytes);
+    if (sigBytes == 64) hipLaunchKernelGGL(ecdsa_prep_kernel<false>, pg, dim3(256), 0, L.stream, d_jobs, dm, ds, dp, (int)n);
+    else hipLaunchKernelGGL(ecdsa_prep_kernel<true>, pg, dim3(256), 0, L.stream, d_jobs, dm, ds, dp, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
     const int grid = (int)((n + WG - 1) / WG);
     hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, L.stream, d_jobs, tb.d_gtab, d_out, (int)n);
@@ -1139,6 +1236,17 @@ void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, un
     L.batches++;
     L.items += n;
 }
+} // namespace
+
+void VerifyLane::EcdsaFill(size_t n, const std::function<void(unsigned char*, unsigned char*, unsigned char*)>& fill,
+                           uint8_t* result) {
+    LaneEcdsa(*impl, n, 64, fill, result);
+}
+
+void VerifyLane::EcdsaDerFill(size_t n, const std::function<void(unsigned char*, unsigned char*, unsigned char*)>& fill,
+                              uint8_t* result) {
+    LaneEcdsa(*impl, n, DER_SLOT, fill, result);
+}
 
 size_t EcdsaJobBytes() { return sizeof(Job); }
 
@@ -1151,7 +1259,7 @@ void EcdsaVerifyDevice(const void* msg32, const void* sig64, const void* pub33, 
     std::call_once(tb.once, [&] { InitTable(tb); });
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     Job* d_jobs = static_cast<Job*>(jobs);
-    hipLaunchKernelGGL(ecdsa_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_jobs,
+    hipLaunchKernelGGL(ecdsa_prep_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_jobs,
                        static_cast<const unsigned char*>(msg32), static_cast<const unsigned char*>(sig64),
                        static_cast<const unsigned char*>(pub33), (int)n);
     BCP_HIP_CHECK(hipGetLastError());

@@ -202,7 +202,7 @@ std::vector<uint8_t> GpuVerifyService::Ecdsa(const unsigned char* msg32, const u
     return out;
 }
 
-std::vector<uint8_t> GpuVerifyService::EcdsaFill(size_t n, const EcdsaFillFn& fill) {
+std::vector<uint8_t> GpuVerifyService::EcdsaFillImpl(size_t n, bool der, const EcdsaFillFn& fill) {
     std::vector<uint8_t> out(n, 0);
     if (n == 0) return out;
     size_t minShard;
@@ -211,13 +211,16 @@ std::vector<uint8_t> GpuVerifyService::EcdsaFill(size_t n, const EcdsaFillFn& fi
         minShard = minShardEcdsa;
     }
     RunSharded(n, minShard, [&](gpu::VerifyLane& lane, size_t lo, size_t hi, WorkerPool& workers) {
-        lane.EcdsaFill(
-            hi - lo,
-            [&](unsigned char* msg, unsigned char* sig, unsigned char* pub) { fill(lo, hi, msg, sig, pub, workers); },
-            out.data() + lo);
+        auto f = [&](unsigned char* msg, unsigned char* sig, unsigned char* pub) { fill(lo, hi, msg, sig, pub, workers); };
+        if (der) lane.EcdsaDerFill(hi - lo, f, out.data() + lo);
+        else lane.EcdsaFill(hi - lo, f, out.data() + lo);
     });
     return out;
 }
+
+std::vector<uint8_t> GpuVerifyService::EcdsaFill(size_t n, const EcdsaFillFn& fill) { return EcdsaFillImpl(n, false, fill); }
+
+std::vector<uint8_t> GpuVerifyService::EcdsaDerFill(size_t n, const EcdsaFillFn& fill) { return EcdsaFillImpl(n, true, fill); }
 
 std::vector<uint8_t> GpuVerifyService::EquihashHeaders(unsigned N, unsigned K, size_t n, const HeaderFillFn& fill) {
     std::vector<uint8_t> out(n, 0);

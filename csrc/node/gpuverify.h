@@ -58,6 +58,10 @@ public:
     using EcdsaFillFn = std::function<void(size_t lo, size_t hi, unsigned char* msg32, unsigned char* sig64,
                                            unsigned char* pub33, WorkerPool& workers)>;
     std::vector<uint8_t> EcdsaFill(size_t n, const EcdsaFillFn& fill);
+    // The same with DER signatures: the fill writes gpu::VerifyLane::DER_SLOT-byte slots
+    // ([length][DER bytes]) where EcdsaFill takes 64-byte compact signatures; the device parses
+    // them (lax rules) and low-S normalises.
+    std::vector<uint8_t> EcdsaDerFill(size_t n, const EcdsaFillFn& fill);
     // Block headers [0, n): fill(lo, hi, in140, sols, lenok, workers) writes headers [lo, hi)
     // (gpu::VerifyLane::EquihashHeaders layout); the device builds the BLAKE2b states.
     using HeaderFillFn = std::function<void(size_t lo, size_t hi, uint8_t* in140, uint8_t* sols, uint8_t* lenok,
@@ -99,6 +103,7 @@ private:
     // Runs fn(lane, lo, hi, workers) for the shards of [0, n) and waits; rethrows the first failure.
     void RunSharded(size_t n, size_t minShard,
                     const std::function<void(gpu::VerifyLane&, size_t, size_t, WorkerPool&)>& fn);
+    std::vector<uint8_t> EcdsaFillImpl(size_t n, bool der, const EcdsaFillFn& fill);
 
     mutable std::mutex m;
     std::vector<int> devices;

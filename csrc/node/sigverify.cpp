@@ -70,40 +70,33 @@ bool CachingTransactionSignatureChecker::VerifySignature(const std::vector<unsig
     return true;
 }
 
-// Host half of one job: DER parse + low-S normalisation into sig64, the key in compressed form
-// into pub33. A rejected job keeps the device input well-formed; false masks its result.
-static bool PrepSigAndKey(const DeferredSigCheck& c, unsigned char* sig64, unsigned char* pub33) {
-    secp::Signature s;
-    bool ok = secp::sig_parse_der_lax(s, c.sig.data(), c.sig.size());
-    if (ok) {
-        secp::sig_normalize(s);
-        secp::sig_serialize_compact(sig64, s);
-        if (secp::sc_is_zero(s.r) || secp::sc_is_zero(s.s)) ok = false;
-    } else {
-        memset(sig64, 0, 64);
-    }
+// Host half of one job on the device-DER path: the raw DER bytes into their slot (the device
+// parses and normalises them) and the key in compressed form. A key that does not parse keeps
+// the device input well-formed; false masks its result.
+static bool PrepDerAndKey(const DeferredSigCheck& c, unsigned char* slot, unsigned char* pub33) {
+    const size_t len = c.sig.size(); // <= 72 (InlineBytes<72>)
+    slot[0] = (unsigned char)len;
+    memcpy(slot + 1, c.sig.data(), len);
     const auto& pk = c.pubkey;
     if (pk.size() == 33 && (pk[0] == 2 || pk[0] == 3)) {
         memcpy(pub33, pk.data(), 33);
-    } else {
-        secp::Ge q;
-        if (secp::pubkey_parse(q, pk.data(), pk.size())) {
-            std::vector<unsigned char> comp = secp::pubkey_serialize(q, true);
-            memcpy(pub33, comp.data(), 33);
-        } else {
-            ok = false;
-        }
+        return true;
     }
-    if (!ok) {
-        memset(pub33, 0, 33);
-        pub33[0] = 2;
+    secp::Ge q;
+    if (secp::pubkey_parse(q, pk.data(), pk.size())) {
+        std::vector<unsigned char> comp = secp::pubkey_serialize(q, true);
+        memcpy(pub33, comp.data(), 33);
+        return true;
     }
-    return ok;
+    memset(pub33, 0, 33);
+    pub33[0] = 2;
+    return false;
 }
 
 std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*>& checks) {
-    // host: DER parse + low-S normalisation + key form, written by the pool straight into the
-    // verify lane's pinned staging buffer; device: scalar prep, decompression + ecmult
+    // host: copy the digest, the DER bytes and the key (converted to compressed form when it is
+    // not) straight into the verify lane's pinned staging buffer; device: DER parse + low-S,
+    // scalar prep, decompression + ecmult
     const size_t n = checks.size();
     std::vector<uint8_t> hostOk(n, 1);
     if (GpuFaultInjection()) throw std::runtime_error("injected GPU signature-verify fault");
@@ -115,12 +108,12 @@ std::vector<uint8_t> GpuVerifyDeferred(const std::vector<const DeferredSigCheck*
             [&](size_t k) {
                 const DeferredSigCheck& c = *checks[lo + k];
                 memcpy(&msg[k * 32], c.sighash.begin(), 32);
-                if (!PrepSigAndKey(c, &sig[k * 64], &pub[k * 33])) hostOk[lo + k] = 0;
+                if (!PrepDerAndKey(c, &sig[k * gpu::VerifyLane::DER_SLOT], &pub[k * 33])) hostOk[lo + k] = 0;
             },
-            64);
+            256);
     };
     // sharded across the validation GPUs by the verify service (one high-priority lane each)
-    std::vector<uint8_t> res = GpuVerifyService::Instance().EcdsaFill(n, fill);
+    std::vector<uint8_t> res = GpuVerifyService::Instance().EcdsaDerFill(n, fill);
     for (size_t j = 0; j < n; j++) res[j] &= hostOk[j];
     return res;
 }
