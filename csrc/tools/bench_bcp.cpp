@@ -356,6 +356,39 @@ static void CoinsApply84k(State& st) {
 }
 BENCHMARK(CoinsApply84k);
 
+// The same updates one coins-map shard per pool task (the parallel UTXO pass's view updates)
+static void CoinsApply84k_Sharded(State& st) {
+    CCoinsView base;
+    const size_t N = 42000;
+    std::vector<COutPoint> spent(N), made(N);
+    FastRandomContext rng(true);
+    for (size_t i = 0; i < N; i++) {
+        spent[i] = COutPoint(rng.rand256(), (uint32_t)(i & 1));
+        made[i] = COutPoint(rng.rand256(), (uint32_t)(i & 1));
+    }
+    std::vector<uint8_t> ss(N), ms(N);
+    for (size_t i = 0; i < N; i++) {
+        ss[i] = (uint8_t)CCoinsMap::ShardOf(spent[i]);
+        ms[i] = (uint8_t)CCoinsMap::ShardOf(made[i]);
+    }
+    const CScript spk = CScript() << OP_DUP << OP_HASH160 << std::vector<unsigned char>(20, 7) << OP_EQUALVERIFY
+                                  << OP_CHECKSIG;
+    WorkerPool pool(std::min(16, std::max(2, GetNumCores())));
+    while (st.KeepRunning()) {
+        CCoinsViewCache view(&base);
+        view.Reserve(2 * N);
+        view.ForEachShard(
+            [&](unsigned sh) {
+                for (size_t i = 0; i < N; i++)
+                    if (ss[i] == sh) view.SpendFetchedMoved(spent[i]);
+                for (size_t i = 0; i < N; i++)
+                    if (ms[i] == sh) view.AddCoin(made[i], Coin(CTxOut(1000, spk), 100, false), false);
+            },
+            &pool);
+    }
+}
+BENCHMARK(CoinsApply84k_Sharded);
+
 static void CoinSelection(State& st) {
     SelectParams("regtest");
     CWallet wallet("bench", "", true);
