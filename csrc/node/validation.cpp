@@ -221,6 +221,14 @@ bool Chainstate::CheckBlockHeader(const CBlockHeader& block, CValidationState& s
     return true;
 }
 
+// GetSerializeSize(block, version) without walking the transactions again: each one's size was
+// taken when its txid was hashed
+uint64_t BlockSerializeSize(const CBlock& block, int version) {
+    uint64_t n = GetSerializeSize(static_cast<const CBlockHeader&>(block), version) + GetSizeOfCompactSize(block.vtx.size());
+    for (const auto& tx : block.vtx) n += tx->GetTotalSize();
+    return n;
+}
+
 bool Chainstate::CheckBlock(const CBlock& block, CValidationState& state, bool fCheckPOW, bool fCheckMerkleRoot) const {
     if (block.fChecked) return true;
     if (!CheckBlockHeader(block, state, fCheckPOW)) return false;
@@ -237,7 +245,7 @@ bool Chainstate::CheckBlock(const CBlock& block, CValidationState& state, bool f
     const uint64_t nMaxBlockSize = opts.maxBlockSize;
     if (block.vtx.size() * MIN_TRANSACTION_SIZE > nMaxBlockSize)
         return state.DoS(100, false, REJECT_INVALID, "bad-blk-length", false, "size limits failed");
-    const uint64_t currentBlockSize = GetSerializeSize(block, PROTOCOL_VERSION | serFlags);
+    const uint64_t currentBlockSize = BlockSerializeSize(block, PROTOCOL_VERSION | serFlags);
     if (currentBlockSize > nMaxBlockSize)
         return state.DoS(100, false, REJECT_INVALID, "bad-blk-length", false, "size limits failed");
     if (!CheckCoinbase(*block.vtx[0], state, false))
@@ -818,7 +826,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                         prefetchedFound[k] = found[q];
                         if (found[q]) prefetched[k] = std::move(got[q]);
                     }
-                txSizes[i] = (uint32_t)GetSerializeSize(tx, PROTOCOL_VERSION);
+                txSizes[i] = tx.GetTotalSize();
                 legacySigOps[i] = (uint32_t)GetSigOpCountWithoutP2SH(tx);
                 if (i > 0 && fScriptChecks) {
                     scKeys[i] = sc.Key(tx, flags);

@@ -93,6 +93,8 @@ struct MempoolAcceptResult {
     Amount fee = 0;
 };
 
+// GetSerializeSize(block, version) from the transactions' cached sizes.
+uint64_t BlockSerializeSize(const CBlock& block, int version);
 // -maxscriptcachesize (MiB): resize the script-execution cache; returns its capacity.
 size_t InitScriptExecutionCache(int64_t mib);
 // UI alert + -alertnotify command.

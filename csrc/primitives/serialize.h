@@ -366,11 +366,16 @@ public:
 class HashWriter {
     CSHA256 ctx;
     int nType, nVersion;
+    size_t nBytes = 0;
 public:
     HashWriter(int type = SER_GETHASH, int version = PROTOCOL_VERSION) : nType(type), nVersion(version) {}
     int GetType() const { return nType; }
     int GetVersion() const { return nVersion; }
-    void write(const char* p, size_t n) { ctx.Write((const unsigned char*)p, n); }
+    void write(const char* p, size_t n) {
+        ctx.Write((const unsigned char*)p, n);
+        nBytes += n;
+    }
+    size_t BytesWritten() const { return nBytes; }
     uint256 GetHash() {
         uint256 r;
         ctx.Finalize(r.begin());

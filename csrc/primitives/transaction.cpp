@@ -28,7 +28,13 @@ CMutableTransaction::CMutableTransaction(const CTransaction& tx)
 
 uint256 CMutableTransaction::GetId() const { return SerializeHash(*this, SER_GETHASH, 0); }
 
-uint256 CTransaction::ComputeHash() const { return SerializeHash(*this, SER_GETHASH, 0); }
+// The txid, and the serialized size as a by-product (the same bytes are hashed)
+uint256 CTransaction::ComputeHash() const {
+    HashWriter hw(SER_GETHASH, 0);
+    hw << *this;
+    nTotalSize = (uint32_t)hw.BytesWritten();
+    return hw.GetHash();
+}
 
 CTransaction::CTransaction() : nVersion(CTransaction::CURRENT_VERSION), vin(), vout(), nLockTime(0), hash() {}
 CTransaction::CTransaction(const CMutableTransaction& tx)
@@ -46,7 +52,10 @@ Amount CTransaction::GetValueOut() const {
     return nValueOut;
 }
 
-unsigned int CTransaction::GetTotalSize() const { return (unsigned int)GetSerializeSize(*this, PROTOCOL_VERSION); }
+unsigned int CTransaction::GetTotalSize() const {
+    // every serialized transaction is at least 10 bytes: 0 means not computed (default-constructed)
+    return nTotalSize ? nTotalSize : (unsigned int)GetSerializeSize(*this, PROTOCOL_VERSION);
+}
 
 unsigned int CTransaction::CalculateModifiedSize(unsigned int nTxSize) const {
     // Discount inputs' scriptSig prefix overhead (reference CTransaction::CalculateModifiedSize).

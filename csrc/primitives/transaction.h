@@ -119,6 +119,7 @@ public:
     std::string ToString() const;
 
 private:
+    mutable uint32_t nTotalSize = 0; // set by ComputeHash; declared before hash, so initialised first
     const uint256 hash;
     uint256 ComputeHash() const;
 };

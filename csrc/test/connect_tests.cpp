@@ -250,6 +250,11 @@ TEST_CASE(blockdecode_tests, parallel_decode_matches_stream) {
         for (size_t i = 0; i < b.vtx.size(); i++) same &= got.vtx[i]->GetHash() == b.vtx[i]->GetHash();
         CHECK(same);
     }
+    // the block size from the transactions' cached sizes matches a full serialization walk, in
+    // both header formats
+    for (int v : {PROTOCOL_VERSION, PROTOCOL_VERSION | SERIALIZE_BLOCK_LEGACY})
+        CHECK_EQ(BlockSerializeSize(b, v), (uint64_t)GetSerializeSize(b, v));
+    CHECK_EQ(b.vtx[5]->GetTotalSize(), (unsigned)GetSerializeSize(*b.vtx[5], PROTOCOL_VERSION));
     // a block cut anywhere fails both ways, like the stream decode
     for (int t = 0; t < 40; t++) {
         const size_t cut = 81 + rng() % (raw.size() - 82);
