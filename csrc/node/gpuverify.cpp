@@ -40,16 +40,18 @@ void GpuVerifyService::SetDevices(const std::vector<int>& devs) {
 }
 
 // Default: every visible device, two lanes each (the built-in miner runs only on demand, and
-// its streams share a device at a lower priority than validation's). Two lanes per device let
-// one shard's host fill overlap the other's kernels: a 199k-signature batch took 10.1 ms on one
-// lane and 8.2 ms on two of the same MI355X (profiles/lanes_headers_r4.md).
+// its streams share a device at a lower priority than validation's), listed device by device
+// round-robin ([0, 1, .., n-1, 0, 1, ..]) so a batch cut into k shards lands on k different
+// devices first. A shard is at least minShardEcdsa signatures: two kernels of one batch on the
+// same device do not overlap (each waits out the ~2.5 ms verify latency), so an 8 MB block's
+// 42k-signature batch took 3.3 ms device time whole and 7.5 ms in two shards; only the 199k
+// worst case gains from a second lane (profiles/connect_r4.md).
 static std::vector<int> AllDevices() {
     std::vector<int> d;
     if (!gpu::GpuAvailable()) return d;
-    for (int i = 0; i < gpu::DeviceCount(); i++) {
-        d.push_back(i);
-        d.push_back(i);
-    }
+    const int n = gpu::DeviceCount();
+    for (int rep = 0; rep < 2; rep++)
+        for (int i = 0; i < n; i++) d.push_back(i);
     return d;
 }
 

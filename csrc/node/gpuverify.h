@@ -109,7 +109,9 @@ private:
     std::vector<int> devices;
     std::vector<std::shared_ptr<Lane>> lanes;
     bool lanesStale = true;
-    size_t minShardEcdsa = 256, minShardEquihash = 32;
+    // smallest shard worth another lane (see AllDevices in gpuverify.cpp): below these a batch
+    // runs whole on one lane
+    size_t minShardEcdsa = 65536, minShardEquihash = 2048;
     uint64_t sharded = 0;
 };
 

@@ -637,7 +637,7 @@ static void LanesEcdsa(State& st, int lanes) {
         fprintf(stderr, "LanesEcdsa: %zu of %zu verdicts false\n", (size_t)std::count(r.begin(), r.end(), 0), r.size());
         exit(1);
     }
-    svc.SetMinShard(256, 32);
+    svc.SetMinShard(65536, 2048); // the service defaults
     svc.SetDevices({});
 }
 static bench::Reg reg_LanesEcdsa1("Lanes1_Ecdsa199k_GPU", [](State& st) { LanesEcdsa(st, 1); });
@@ -669,7 +669,7 @@ static void LanesHeaders(State& st, int lanes) {
     svc.SetMinShard(1024, 64);
     std::vector<bool> r = CheckEquihashSolutions(ptrs, Params(), true);
     while (st.KeepRunning()) r = CheckEquihashSolutions(ptrs, Params(), true);
-    svc.SetMinShard(256, 32);
+    svc.SetMinShard(65536, 2048); // the service defaults
     svc.SetDevices({});
 }
 static bench::Reg reg_LanesHdr1("Lanes1_Headers2000_GPU", [](State& st) { LanesHeaders(st, 1); });
@@ -914,6 +914,9 @@ void ConnectBigBlock(State& st, bool useGpu, int kind) {
     const SigVerifyStats s0 = GetSigVerifyStats();
     int64_t ph0[Chainstate::PH_COUNT];
     for (int k = 0; k < Chainstate::PH_COUNT; k++) ph0[k] = f.cs->ConnectPhaseMicros((Chainstate::ConnectPhase)k);
+    // -ecdsaminshard=N: a batch is split over the verify lanes only in shards of at least N
+    if (gArgs.IsArgSet("-ecdsaminshard"))
+        GpuVerifyService::Instance().SetMinShard((size_t)gArgs.GetArg("-ecdsaminshard", (int64_t)256), 32);
     auto laneTimes = [] {
         uint64_t fill = 0, dev = 0;
         for (const auto& L : GpuVerifyService::Instance().Stats()) {
@@ -1193,7 +1196,7 @@ int main(int argc, char* argv[]) {
     if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help")) {
         printf("Usage: bench_bcp [-filter=<regex>] [-time=<seconds per bench>] [-list] [-datadir=bench/data]\n"
                "                 [-par=<script threads>] [-ibdblocks=<n>] [-kvcoins=<n>] [-kvdbcache=<MiB>]\n"
-               "                 [-debug=<category>]\n");
+               "                 [-parallelutxo=<min txs>] [-ecdsaminshard=<signatures>] [-debug=<category>]\n");
         return 0;
     }
     { // default: <dir of the binary>/../bench/data, so the working directory does not matter

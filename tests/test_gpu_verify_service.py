@@ -40,7 +40,7 @@ def two_lanes(native):
     native.gpu_verify_set_devices([0, 0])
     native.gpu_verify_set_min_shard(64, 8)
     yield
-    native.gpu_verify_set_min_shard(256, 32)
+    native.gpu_verify_set_min_shard(65536, 2048)  # the service defaults
     native.gpu_verify_set_devices([])
 
 
