@@ -6,6 +6,7 @@
 
 #include <atomic>
 #include <cstring>
+#include <future>
 
 namespace bcp {
 
@@ -159,9 +160,79 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
         cache.GetMany(&entries[lo], hi - lo, cacheErase, &hit[lo]);
     };
     const size_t nChunks = (checks.size() + PROBE_CHUNK - 1) / PROBE_CHUNK;
-    if (pool && nChunks > 1) pool->ParallelFor(nChunks, probe, 1);
-    else
+    // A cold cache (initial sync, a block nobody relayed first): when the first chunk's probes
+    // mostly miss, the whole batch goes to the GPU right away and the remaining probes run on the
+    // CPU meanwhile; a hit then only saves the cache insert. A warm cache (a synced node, whose
+    // mempool already verified most of the block) keeps probe-first, so hits never wait for the
+    // GPU. Either way res[i] = hit or verified.
+    bool gpuFailedEarly = false; // the overlapped GPU batch below failed: the rest stays on the CPU
+    const bool gpuEligible = useGpu && !g_gpuDisabled.load() && checks.size() >= g_gpuThreshold.load() &&
+                             (GpuFaultInjection() || gpu::GpuAvailable());
+    if (gpuEligible && nChunks > 1) {
+        probe(0);
+        size_t sampleHits = 0;
+        for (size_t i = 0; i < PROBE_CHUNK; i++) sampleHits += hit[i];
+        if (sampleHits * 2 < PROBE_CHUNK) {
+            auto gpuRun = std::async(std::launch::async, [&checks] { return GpuVerifyDeferred(checks); });
+            const int64_t t0 = GetTimeMicros();
+            if (pool) pool->ParallelFor(nChunks - 1, [&](size_t k) { probe(k + 1); }, 1);
+            else
+                for (size_t k = 1; k < nChunks; k++) probe(k);
+            std::vector<uint8_t> r;
+            bool gpuOk = true;
+            try {
+                r = gpuRun.get();
+                g_gpuFailures = 0;
+            } catch (const std::exception& e) {
+                gpuOk = false;
+                const int fails = ++g_gpuFailures;
+                LogPrintf("GPU signature verification failed (%s); re-verifying on the CPU\n", e.what());
+                if (fails >= MAX_GPU_SIG_FAILURES && !g_gpuDisabled.exchange(true))
+                    LogPrintf("GPU signature verification disabled after %d consecutive failures\n", fails);
+                std::lock_guard<std::mutex> l(g_statsMutex);
+                g_stats.gpu_failures++;
+            }
+            if (gpuOk) {
+                bool ok = true;
+                for (size_t i = 0; i < checks.size(); i++) {
+                    if (hit[i]) {
+                        hits++;
+                        res[i] = 1;
+                    } else {
+                        res[i] = r[i];
+                        if (!r[i]) {
+                            if (!spec[i]) ok = false;
+                        } else if (cacheStore) {
+                            cache.Set(entries[i]);
+                        }
+                    }
+                }
+                if (ok)
+                    for (const DeferredMultisig& g : groups)
+                        if (!EvalDeferredMultisig(g, &res[g.first])) {
+                            ok = false;
+                            break;
+                        }
+                std::lock_guard<std::mutex> l(g_statsMutex);
+                g_stats.gpu_batches++;
+                g_stats.gpu_sigs += checks.size();
+                g_stats.gpu_ms += (GetTimeMicros() - t0) / 1000.0;
+                g_stats.cache_hits += hits;
+                g_stats.multisig_groups += groups.size();
+                return ok;
+            }
+            // the GPU failed: the probes are complete; the CPU path below verifies the misses
+            gpuFailedEarly = true;
+        } else if (pool) {
+            pool->ParallelFor(nChunks - 1, [&](size_t k) { probe(k + 1); }, 1);
+        } else {
+            for (size_t k = 1; k < nChunks; k++) probe(k);
+        }
+    } else if (pool && nChunks > 1) {
+        pool->ParallelFor(nChunks, probe, 1);
+    } else {
         for (size_t k = 0; k < nChunks; k++) probe(k);
+    }
     for (size_t i = 0; i < checks.size(); i++) {
         if (hit[i]) {
             hits++;
@@ -173,7 +244,7 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
     bool ok = true;
     const size_t n = todo.size();
     if (n > 0) {
-        bool gpu = useGpu && !g_gpuDisabled.load() && n >= g_gpuThreshold.load() &&
+        bool gpu = !gpuFailedEarly && useGpu && !g_gpuDisabled.load() && n >= g_gpuThreshold.load() &&
                    (GpuFaultInjection() || gpu::GpuAvailable());
         const int64_t t0 = GetTimeMicros();
         if (gpu) {
