@@ -89,6 +89,9 @@
 #ifndef BCP_EH_ISSUE_LATE // 1: a round issues its next-bucket loads after the key sort, not at the commit
 #define BCP_EH_ISSUE_LATE 0
 #endif
+#ifndef BCP_EH_KEY_COMMIT // 1: a collision round counts its rows' keys while committing them to LDS
+#define BCP_EH_KEY_COMMIT 1 //  (the rank comes back from that atomic): one LDS pass and one barrier less
+#endif
 #ifndef BCP_EH_GEN_LDS // 1: force the LDS-sorted generation kernel everywhere (A/B builds)
 #define BCP_EH_GEN_LDS 0
 #endif
@@ -603,6 +606,10 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     constexpr uint32_t RMI = C::rmask(STAGE - 1);          // parent bits in the input rows' padding
     constexpr int SLI = (RPL + BCP_EH_PF_SLICES - 1) / BCP_EH_PF_SLICES; // prefetch slice (rows per phase)
     constexpr int BPT = (C::NB + NT - 1) / NT;             // destination buckets per thread (claims)
+    // key counting folded into the commit (non-final rounds with the wave-compacted pair list):
+    // bend holds counts after the commit and group starts after the scan; spair then aliases the
+    // pair list, so bend survives the emit and is cleared for the next bucket in D3
+    constexpr bool FOLD = BCP_EH_KEY_COMMIT && BCP_EH_PAIRS && !FINAL;
     using HT = std::conditional_t<C::H16, uint16_t, uint32_t>;
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
     __shared__ uint32_t psig[PRUNE ? CAP : 1];                // the input rows' parent word (j << 16 | i, + d bits)
@@ -617,7 +624,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     uint32_t* bend = reinterpret_cast<uint32_t*>(un + un_walk_bend<C>(CAP));
     uint16_t* offp = reinterpret_cast<uint16_t*>(un + un_walk_offp<C>(CAP));
     uint32_t* plist = reinterpret_cast<uint32_t*>(un + un_walk_offp<C>(CAP));
-    uint32_t* spair = reinterpret_cast<uint32_t*>(un);
+    uint32_t* spair = FOLD ? plist : reinterpret_cast<uint32_t*>(un);
     const int tid = threadIdx.x;
     const int G = gridDim.x;
     int it = 0;
@@ -661,6 +668,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // (a round that does not prune loads only the row words of each slot)
     constexpr int LWI = PRUNE ? (CPI ? WI + 1 : WI + 2) : (BCP_EH_ROWONLY_LOAD ? WI : SWI);
     uint32_t nr[RPL][LWI];
+    uint32_t krank[FOLD ? RPL : 1]; // FOLD: (key << 16) | rank in the key group of each committed row
     int pf_bk = bk;
     uint32_t pf_n = 0;
     // Issue prefetch rows [u0, u1) of bucket pf_bk. Every vector-memory instruction of the loop
@@ -708,6 +716,10 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #pragma unroll
         for (int u = 0; u < MP; ++u) row_store<SWO>(rs_out, OOB + 256 * u, z); // distinct offsets: identical stores would be merged
     }
+    if constexpr (FOLD) {
+        for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
+        __syncthreads();
+    }
     const int bk1 = xcd_bucket<C::NB>(blockIdx.x, 1, G, nbk);
     uint32_t fill_next = bk1 >= 0 ? CTRin[bk1] : 0u;
 
@@ -733,12 +745,17 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                         psig[r] = nr[u][WI];
                         if constexpr (!CPI) pdw[r] = (uint16_t)nr[u][WI + 1];
                     }
+                    if constexpr (FOLD) {
+                        const uint32_t key = nr[u][0] >> (32 - C::RB);
+                        krank[u] = (key << 16) | atomicAdd(&bend[key], 1u);
+                    }
                 }
             }
         }
         if constexpr (!FINAL)
             for (int b = tid; b < C::HW; b += NT) hist_[b] = 0;
-        for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
+        if constexpr (!FOLD)
+            for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
         if (tid == 0) npairs = 0;
         EH_STAMP(1);
         const int bn = xcd_bucket<C::NB>(blockIdx.x, it + 1, G, nbk);
@@ -757,10 +774,26 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         // D1. counting sort of the rows by their RB key: sidx = row ids grouped by key,
         //     bend[key] = end of the key's group
         auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WI] >> (32 - C::RB); };
-        for (uint32_t i = tid; i < n; i += NT) atomicAdd(&bend[key_of(i)], 1u);
-        __syncthreads();
-        block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
-        for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
+        if constexpr (FOLD) {
+            // the commit counted the keys: scan to group starts, place each row by its rank
+            block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
+            const uint32_t ot = opaque_tid();
+#pragma unroll
+            for (int u = 0; u < RPL; ++u) {
+                const uint32_t r = ot + u * NT;
+                if (r < n) sidx[bend[krank[u] >> 16] + (krank[u] & 0xffff)] = (uint16_t)r;
+            }
+        } else {
+            for (uint32_t i = tid; i < n; i += NT) atomicAdd(&bend[key_of(i)], 1u);
+            __syncthreads();
+            block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
+            for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
+        }
+        // end of a key group: bend holds group ends (or, FOLD, group starts)
+        auto gend = [&](uint32_t key) -> uint32_t {
+            if constexpr (FOLD) return key + 1 < (uint32_t)C::NRESTS ? bend[key + 1] : n;
+            else return bend[key];
+        };
 #if BCP_EH_ISSUE_LATE
         // the first vector-memory instructions after the previous bucket's emit: issued once the
         // key sort (LDS only) has given that emit's stores time to drain, so they do not stall
@@ -805,7 +838,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #pragma unroll
             for (int u = 0; u < MPR; ++u) {
                 const uint32_t p = tid + u * NT;
-                cpl[u] = p < n ? min(bend[key_of(sidx[p])] - p - 1, 14u) : 0u;
+                cpl[u] = p < n ? min(gend(key_of(sidx[p])) - p - 1, 14u) : 0u;
                 cnt += cpl[u];
             }
             const uint32_t incl = wave_incl<false>(cnt);
@@ -887,6 +920,8 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     }
                 }
             }
+            if constexpr (FOLD) // bend's last reads were before the barrier above; next commit counts here
+                for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
             __syncthreads();
             EH_STAMP(4);
             // D3. claim this bucket's runs in the destination areas (device-scope atomics whose
