@@ -774,6 +774,9 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         // D1. counting sort of the rows by their RB key: sidx = row ids grouped by key,
         //     bend[key] = end of the key's group
         auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WI] >> (32 - C::RB); };
+        // FOLD: each lane's committed rows: sorted position (krank, reused) and the number of
+        // later positions in the row's key group (its pairs, capped at 14 as below)
+        uint32_t kpairs[FOLD ? RPL : 1];
         if constexpr (FOLD) {
             // the commit counted the keys: scan to group starts, place each row by its rank
             block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
@@ -781,7 +784,15 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #pragma unroll
             for (int u = 0; u < RPL; ++u) {
                 const uint32_t r = ot + u * NT;
-                if (r < n) sidx[bend[krank[u] >> 16] + (krank[u] & 0xffff)] = (uint16_t)r;
+                kpairs[u] = 0;
+                if (r < n) {
+                    const uint32_t key = krank[u] >> 16;
+                    const uint32_t pos = bend[key] + (krank[u] & 0xffff);
+                    const uint32_t e = key + 1 < (uint32_t)C::NRESTS ? bend[key + 1] : n;
+                    sidx[pos] = (uint16_t)r;
+                    krank[u] = pos;
+                    kpairs[u] = min(e - pos - 1, 14u);
+                }
             }
         } else {
             for (uint32_t i = tid; i < n; i += NT) atomicAdd(&bend[key_of(i)], 1u);
@@ -789,11 +800,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
             for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
         }
-        // end of a key group: bend holds group ends (or, FOLD, group starts)
-        auto gend = [&](uint32_t key) -> uint32_t {
-            if constexpr (FOLD) return key + 1 < (uint32_t)C::NRESTS ? bend[key + 1] : n;
-            else return bend[key];
-        };
+
 #if BCP_EH_ISSUE_LATE
         // the first vector-memory instructions after the previous bucket's emit: issued once the
         // key sort (LDS only) has given that emit's stores time to drain, so they do not stall
@@ -833,12 +840,14 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             //     one barrier. The list holds MP*NT pairs (above the row capacity: capped pair
             //     lists lost ~9% of the solutions); identical subtrees and pairs that share a
             //     parent are dropped when the pairs are read back.
+            // (FOLD: a lane takes the pairs of the rows it committed, from registers)
             uint32_t cpl[MPR];
             uint32_t cnt = 0;
 #pragma unroll
             for (int u = 0; u < MPR; ++u) {
                 const uint32_t p = tid + u * NT;
-                cpl[u] = p < n ? min(gend(key_of(sidx[p])) - p - 1, 14u) : 0u;
+                if constexpr (FOLD) cpl[u] = kpairs[u];
+                else cpl[u] = p < n ? min(bend[key_of(sidx[p])] - p - 1, 14u) : 0u;
                 cnt += cpl[u];
             }
             const uint32_t incl = wave_incl<false>(cnt);
@@ -848,7 +857,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #pragma unroll
             for (int u = 0; u < MPR; ++u) {
                 if (!cpl[u]) continue;
-                const uint32_t p = tid + u * NT, i = sidx[p];
+                const uint32_t p = FOLD ? krank[u] : tid + u * NT, i = FOLD ? tid + u * NT : sidx[p];
                 for (uint32_t q = p + 1; q <= p + cpl[u]; ++q, ++o)
                     if (o < (uint32_t)(MP * NT)) plist[o] = ((uint32_t)sidx[q] << 16) | i;
             }
