@@ -95,6 +95,9 @@
 #ifndef BCP_EH_DEST_RANK // 1: a pair keeps its rank in its destination from the histogram atomic and is
 #define BCP_EH_DEST_RANK 0 //  placed by it after the scan (no second atomic per pair); measured 0.3% slower
 #endif
+#ifndef BCP_EH_FILTER_GEN // 1 (with BCP_EH_KEY_COMMIT): pairs are filtered (identical subtrees, shared
+#define BCP_EH_FILTER_GEN 0 //  parents) and counted by destination as they are listed, not on read-back; measured 20% slower
+#endif
 #ifndef BCP_EH_GEN_LDS // 1: force the LDS-sorted generation kernel everywhere (A/B builds)
 #define BCP_EH_GEN_LDS 0
 #endif
@@ -557,13 +560,17 @@ template <class C> constexpr int round_un(int stage) {
     const int pairs = round_mp<C>(stage) * C::NT * 4; // spair: every pair a lane may hold
     return walk > pairs ? walk : pairs;
 }
+template <class C> constexpr bool round_fgen(int stage) {
+    return BCP_EH_FILTER_GEN && BCP_EH_KEY_COMMIT && BCP_EH_PAIRS && stage < C::K;
+}
 template <class C> constexpr int round_lds(int stage, bool prune) {
     const int WI = C::words(stage - 1);
     const int cap = C::cap(stage);
     const int marks = stage == C::K || BCP_EH_PAIRS ? 4 : (round_mp<C>(stage) * C::NT * 2 + 3) / 4 * 4;
     const int pruneb = prune ? cap * 4 + (C::cp(stage - 1) ? 0 : (cap * 2 + 3) / 4 * 4) : 0;
     const int hists = stage == C::K ? 12 : 2 * C::HW * 4 + (C::NB * (C::H16 ? 2 : 4) + 3) / 4 * 4;
-    return (cap * WI + 3) / 4 * 16 + pruneb + marks + round_un<C>(stage) + hists + (C::NW + 1) * 4;
+    const int pdlb = round_fgen<C>(stage) ? (round_mp<C>(stage) * C::NT * 2 + 3) / 4 * 4 : 0;
+    return (cap * WI + 3) / 4 * 16 + pruneb + marks + round_un<C>(stage) + hists + pdlb + (C::NW + 1) * 4;
 }
 // Depth-1 duplicate pruning wherever its parent words fit next to the full rows.
 template <class C> constexpr bool round_prunes(int stage) {
@@ -613,12 +620,14 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // bend holds counts after the commit and group starts after the scan; spair then aliases the
     // pair list, so bend survives the emit and is cleared for the next bucket in D3
     constexpr bool FOLD = BCP_EH_KEY_COMMIT && BCP_EH_PAIRS && !FINAL;
+    constexpr bool FGEN = round_fgen<C>(STAGE); // filter pairs while listing them (implies FOLD)
     using HT = std::conditional_t<C::H16, uint16_t, uint32_t>;
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
     __shared__ uint32_t psig[PRUNE ? CAP : 1];                // the input rows' parent word (j << 16 | i, + d bits)
     __shared__ uint16_t pdw[PRUNE && !CPI ? CAP : 1];         // two-word parents: the producing bucket
     __shared__ uint16_t pmark[FINAL || BCP_EH_PAIRS ? 2 : MP * NT]; // pair index -> first sorted position
     __shared__ uint32_t npairs;                                // wave-compaction pair list fill
+    __shared__ uint16_t pdl[FGEN ? MP * NT : 1];              // FGEN: destination bucket of each listed pair
     __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(STAGE)];
     __shared__ uint32_t hist_[FINAL ? 1 : C::HW], cur_[FINAL ? 1 : C::HW]; // H16: two 16-bit counters per word
     __shared__ HT base[FINAL ? 1 : C::NB];
@@ -658,6 +667,29 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             return ((a ^ b) & ~C::IMASK) == 0 && ((rows[i * WI + WI - 1] ^ rows[j * WI + WI - 1]) & RMI) == 0;
         else
             return pdw[i] == pdw[j];
+    };
+
+    // a collision pair (LDS rows i, j) is kept unless the rows are identical or share a parent;
+    // dest = its destination bucket
+    auto pair_keep = [&](uint32_t i, uint32_t j, uint32_t& dest) -> bool {
+        uint32_t x0 = rows[i * WI] ^ rows[j * WI];
+        if constexpr (WI == 1) x0 &= ~RMI;
+        // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the pairs, so the
+        // remaining words are read only when it matches
+        bool keep = x0 != 0;
+        if (!keep) {
+#pragma unroll
+            for (int w = 1; w < WI; ++w) {
+                uint32_t y = rows[i * WI + w] ^ rows[j * WI + w];
+                if (w == WI - 1) y &= ~RMI;
+                keep |= y != 0;
+            }
+        }
+        if constexpr (PRUNE) {
+            if (keep && shares_parent(i, j)) keep = false;
+        }
+        dest = (x0 >> (32 - C::DB)) & (C::NB - 1);
+        return keep;
     };
 
     // A thread id the compiler cannot see through: keeps the per-lane index math of the
@@ -861,9 +893,26 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             for (int u = 0; u < MPR; ++u) {
                 if (!cpl[u]) continue;
                 const uint32_t p = FOLD ? krank[u] : tid + u * NT, i = FOLD ? tid + u * NT : sidx[p];
-                for (uint32_t q = p + 1; q <= p + cpl[u]; ++q, ++o)
-                    if (o < (uint32_t)(MP * NT)) plist[o] = ((uint32_t)sidx[q] << 16) | i;
+                for (uint32_t q = p + 1; q <= p + cpl[u]; ++q, ++o) {
+                    if (o >= (uint32_t)(MP * NT)) continue;
+                    if constexpr (FGEN) {
+                        // filtered here, on the lane that lists the pair: a dropped pair leaves
+                        // a NIL hole in the list
+                        const uint32_t j = sidx[q];
+                        uint32_t dest;
+                        const bool keep = pair_keep(i, j, dest);
+                        plist[o] = keep ? (j << 16) | i : NIL;
+                        if (keep) {
+                            pdl[o] = (uint16_t)dest;
+                            hinc(hist_, dest);
+                        }
+                    } else {
+                        plist[o] = ((uint32_t)sidx[q] << 16) | i;
+                    }
+                }
             }
+            if constexpr (FGEN) // bend's last reads were before the barrier above
+                for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
             __syncthreads();
             const uint32_t P = npairs;
             const uint32_t Pc = min(P, (uint32_t)(MP * NT));
@@ -874,7 +923,10 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                 const uint32_t k = tid + u * NT;
                 pv[u] = NIL;
                 pd[u] = 0;
-                if (k < Pc) {
+                if (FGEN && k < Pc) { // filtered and counted when listed
+                    pv[u] = plist[k];
+                    if (pv[u] != NIL) pd[u] = pdl[k];
+                } else if (!FGEN && k < Pc) {
                     const uint32_t pr = plist[k];
                     const uint32_t i = pr & 0xffff, j = pr >> 16;
 #else
@@ -909,33 +961,19 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     const uint32_t p = pmark[k], q = p + 1 + (k - offp[p]);
                     const uint32_t i = sidx[p], j = sidx[q];
 #endif
-                    uint32_t x0 = rows[i * WI] ^ rows[j * WI];
-                    if constexpr (WI == 1) x0 &= ~RMI;
-                    // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the
-                    // pairs, so the remaining words are read only when it matches
-                    bool keep = x0 != 0;
-                    if (!keep) {
-#pragma unroll
-                        for (int w = 1; w < WI; ++w) {
-                            uint32_t y = rows[i * WI + w] ^ rows[j * WI + w];
-                            if (w == WI - 1) y &= ~RMI;
-                            keep |= y != 0;
-                        }
-                    }
-                    if constexpr (PRUNE) {
-                        if (keep && shares_parent(i, j)) keep = false;
-                    }
-                    if (keep) {
+                    uint32_t dest;
+                    if (pair_keep(i, j, dest)) {
                         pv[u] = (j << 16) | i;
-                        pd[u] = (x0 >> (32 - C::DB)) & (C::NB - 1); // destination bucket
+                        pd[u] = dest; // destination bucket
                         if constexpr (BCP_EH_DEST_RANK) pd[u] |= hinc(hist_, pd[u]) << 16; // rank in the destination
                         else hinc(hist_, pd[u]);
                     }
                 }
             }
-            if constexpr (FOLD) // bend's last reads were before the barrier above; next commit counts here
+            if constexpr (FOLD && !FGEN) // bend's last reads were before the barrier above; next commit counts here
                 for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
-            __syncthreads();
+            if constexpr (!FGEN) // FGEN: the histogram was complete at the list barrier
+                __syncthreads();
             EH_STAMP(4);
             // D3. claim this bucket's runs in the destination areas (device-scope atomics whose
             //     latency hides behind the scan and the scatter), then sort the pairs by
