@@ -914,6 +914,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             if constexpr (FGEN) // bend's last reads were before the barrier above
                 for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
             __syncthreads();
+            EH_STAMP(7); // pair list complete (splits D2 into listing and filtering)
             const uint32_t P = npairs;
             const uint32_t Pc = min(P, (uint32_t)(MP * NT));
             if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT); // rare
@@ -1410,7 +1411,8 @@ std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
     BCP_HIP_CHECK(hipMemcpy(h.data(), impl->d_stamps.p, h.size() * 8, hipMemcpyDeviceToHost));
     std::vector<std::vector<double>> out;
     for (size_t s = 0; s < impl->kstages; ++s) {
-        std::vector<double> acc(7, 0.0);
+        // phases 1..6, then D2 split at stamp 7: listing (3 -> 7) and filtering (7 -> 4)
+        std::vector<double> acc(9, 0.0);
         size_t cnt = 0;
         for (size_t wg = 0; wg < (size_t)nonces * impl->nb; ++wg) {
             const uint64_t* t = &h[s * per + wg * 16];
@@ -1418,6 +1420,10 @@ std::vector<std::vector<double>> EquihashGpuSolver::PhaseCycles(int nonces) {
             for (int k = 1; k < 7; ++k)
                 if (t[k] >= t[k - 1] && t[k] != 0) acc[k] += (double)(t[k] - t[k - 1]);
             acc[0] += (double)(t[6] - t[0]);
+            if (t[7] >= t[3] && t[4] >= t[7] && t[7] != 0) {
+                acc[7] += (double)(t[7] - t[3]);
+                acc[8] += (double)(t[4] - t[7]);
+            }
             ++cnt;
         }
         for (auto& a : acc) a = cnt ? a / cnt : 0;

@@ -73,7 +73,7 @@ def phases():
         sts.append(st)
     s.solve(sts)
     s.solve(sts)
-    names = ["total", "commit", "issue", "chain", "pairs", "claim_sort", "emit"]
+    names = ["total", "commit", "issue", "chain", "pairs", "claim_sort", "emit", "pairs_list", "pairs_filter"]
     for stage, ph in enumerate(s.phase_cycles(4)):
         print(json.dumps({"round": stage + 1, **{n: round(v) for n, v in zip(names, ph)}}))
 
