@@ -98,6 +98,12 @@
 #ifndef BCP_EH_FILTER_GEN // 1 (with BCP_EH_KEY_COMMIT): pairs are filtered (identical subtrees, shared
 #define BCP_EH_FILTER_GEN 0 //  parents) and counted by destination as they are listed, not on read-back; measured 20% slower
 #endif
+#ifndef BCP_EH_VMEM_FILL // 1: a round reads the next-but-one bucket's fill with a vector (buffer) load.
+#define BCP_EH_VMEM_FILL 1 //  A scalar load shares lgkmcnt with LDS, so the barrier's lgkmcnt(0) waited on it
+#endif
+#ifndef BCP_EH_COMMIT_USE // 1: every prefetched register is used once, unconditionally, after the commit
+#define BCP_EH_COMMIT_USE 0 //  (see the commit): the compiler then knows the loads are done on every path
+#endif
 #ifndef BCP_EH_GEN_LDS // 1: force the LDS-sorted generation kernel everywhere (A/B builds)
 #define BCP_EH_GEN_LDS 0
 #endif
@@ -757,6 +763,16 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     }
     const int bk1 = xcd_bucket<C::NB>(blockIdx.x, 1, G, nbk);
     uint32_t fill_next = bk1 >= 0 ? CTRin[bk1] : 0u;
+    // Fill of bucket b (0 for b < 0). As a buffer load it is counted by vmcnt, which barriers do not
+    // drain; a plain load of this uniform address would be a scalar load, counted with the LDS
+    // operations in lgkmcnt, and the lgkmcnt(0) before the next barrier would wait for its
+    // global-memory round trip. It is read (readfirstlane) one bucket later, after the commit has
+    // waited for the prefetched rows that were issued around it.
+    const auto ctr_rs = buf_rsrc(CTRin, (uint32_t)nbk * 4);
+    auto fill_of = [&](int b) -> uint32_t {
+        if constexpr (BCP_EH_VMEM_FILL) return __builtin_amdgcn_raw_buffer_load_b32(ctr_rs, b >= 0 ? (uint32_t)b * 4 : OOB, 0, 0);
+        else return b >= 0 ? CTRin[b] : 0u;
+    };
 
     for (;;) {
         const int nonce = bk / C::NB, d = bk % C::NB;
@@ -787,6 +803,18 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                 }
             }
         }
+        if constexpr (BCP_EH_COMMIT_USE) {
+            // The commit consumes the prefetched registers under `r < n`, and a wave whose lanes all
+            // skip a unit branches past that unit's vmcnt wait. The compiler's wait counting then
+            // treats those loads as possibly in flight on the join path, and the next write to
+            // one of those registers (the next issue, or a temporary) waits for them with a count
+            // that also drains this wave's older emit stores. One empty use of every register,
+            // outside the branches, settles the loads here instead, where they have landed anyway.
+#pragma unroll
+            for (int u = 0; u < RPL; ++u)
+#pragma unroll
+                for (int w = 0; w < LWI; ++w) asm volatile("" ::"v"(nr[u][w]));
+        }
         if constexpr (!FINAL)
             for (int b = tid; b < C::HW; b += NT) hist_[b] = 0;
         if constexpr (!FOLD)
@@ -795,13 +823,13 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         EH_STAMP(1);
         const int bn = xcd_bucket<C::NB>(blockIdx.x, it + 1, G, nbk);
         const bool more = bn >= 0; // uniform
-        const uint32_t nn = more ? min(fill_next, (uint32_t)CAP) : 0u;
+        const uint32_t nn = more ? min((uint32_t)__builtin_amdgcn_readfirstlane(fill_next), (uint32_t)CAP) : 0u;
         pf_bk = more ? bn : bk;
         pf_n = nn;
         const int bn2 = xcd_bucket<C::NB>(blockIdx.x, it + 2, G, nbk);
 #if !BCP_EH_ISSUE_LATE
         issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
-        fill_next = bn2 >= 0 ? CTRin[bn2] : 0u;
+        fill_next = fill_of(bn2);
 #endif
         __syncthreads();
         EH_STAMP(2);
@@ -839,7 +867,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #if BCP_EH_ISSUE_LATE
         // the first vector-memory instructions after the previous bucket's emit: issued once the
         // key sort (LDS only) has given that emit's stores time to drain, so they do not stall
-        fill_next = bn2 >= 0 ? CTRin[bn2] : 0u;
+        fill_next = fill_of(bn2);
         issue(0, 2 * SLI);
 #else
         issue(SLI, 2 * SLI);
