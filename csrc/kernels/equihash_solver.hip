@@ -102,7 +102,7 @@
 #define BCP_EH_VMEM_FILL 1 //  A scalar load shares lgkmcnt with LDS, so the barrier's lgkmcnt(0) waited on it
 #endif
 #ifndef BCP_EH_COMMIT_USE // 1: every prefetched register is used once, unconditionally, after the commit
-#define BCP_EH_COMMIT_USE 0 //  (see the commit): the compiler then knows the loads are done on every path
+#define BCP_EH_COMMIT_USE 0 //  (see the commit): the compiler then knows the loads are done on every path; no change measured
 #endif
 #ifndef BCP_EH_GEN_LDS // 1: force the LDS-sorted generation kernel everywhere (A/B builds)
 #define BCP_EH_GEN_LDS 0
