@@ -74,6 +74,12 @@
 #ifndef BCP_EH_GEN_HPT // (200,9) register generation: hashes per thread
 #define BCP_EH_GEN_HPT 2
 #endif
+#ifndef BCP_EH_GEN_NT // (200,9) register generation: threads per workgroup
+#define BCP_EH_GEN_NT 512
+#endif
+#ifndef BCP_EH_PRIO // 1: generation runs on a low-priority stream of its own, the rounds on a high-priority one
+#define BCP_EH_PRIO 0 //  (so one solver's generation fills the CUs beside the other solver's resident rounds)
+#endif
 #ifndef BCP_EH_GEN_PERSIST // > 0: register generation runs this many persistent workgroups per CU
 #define BCP_EH_GEN_PERSIST 0 //  (each loops over work items) instead of one workgroup per item
 #endif
@@ -177,7 +183,7 @@ struct EhCfg {
 // Mainnet/testnet (200,9): 512 buckets x ~4096 rows, one 1024-thread round workgroup per CU
 // (BCP_EH_BB=10: 1024 buckets x ~2048 rows, two 512-thread workgroups per CU); (96,5); regtest (48,5).
 using Cfg200_9_bb10 = EhCfg<200, 9, 10, 2304, 512, 512, 1024, 256, 2560, 2688, 2, 1024, 2>;
-using Cfg200_9_bb9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, 512, BCP_EH_GEN_HPT>;
+using Cfg200_9_bb9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, BCP_EH_GEN_NT, BCP_EH_GEN_HPT>;
 using Cfg200_9 = std::conditional_t<BCP_EH_BB == 10, Cfg200_9_bb10, Cfg200_9_bb9>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
 using Cfg48_5 = EhCfg<48, 5, 3, 512, 64, 8, 64, 256>; // 512-slot areas: 8 pairs per lane (a 256-pair list overflowed on duplicate-heavy nonces)
@@ -1235,7 +1241,8 @@ struct EquihashGpuSolver::Impl {
     unsigned n, k;
     int batch, device;
     hipStream_t stream = nullptr;
-    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    hipStream_t gstream = nullptr;                // BCP_EH_PRIO: generation's own low-priority stream
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evg = nullptr;
     DevBuf<bcpk::EhBaseState> d_states;
     DevBuf<uint32_t> d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
     DevBuf<uint64_t> d_cand;
@@ -1348,23 +1355,33 @@ struct EquihashGpuSolver::Impl {
             for (int w = 2; w < 16; ++w) hdr &= st.m[w] == 0;
         }
         uint32_t* r0 = d_rst[0].p;
+        hipStream_t gs = stream;
+        if (gstream) { // generation on its own stream, the rounds wait for it
+            BCP_HIP_CHECK(hipEventRecord(evs, stream));
+            BCP_HIP_CHECK(hipStreamWaitEvent(gstream, evs, 0));
+            gs = gstream;
+        }
         constexpr bool reg = bcpk::GenReg<C, C::GNT, C::GHPT>::OK;
         if constexpr (reg) {
             using GR = bcpk::GenReg<C, C::GNT, C::GHPT>;
             const int items = GR::GWG * (int)nstates;
             const int grid = BCP_EH_GEN_PERSIST > 0 ? std::min(items, ncu * BCP_EH_GEN_PERSIST) : items;
             if (hdr)
-                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, true, C::GNT, C::GHPT>), dim3(grid), dim3(C::GNT), 0, stream,
+                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, true, C::GNT, C::GHPT>), dim3(grid), dim3(C::GNT), 0, gs,
                                    d_states.p, r0, d_leaf.p, d_ctr.p, items);
             else
-                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, false, C::GNT, C::GHPT>), dim3(grid), dim3(C::GNT), 0, stream,
+                hipLaunchKernelGGL((bcpk::eh_gen_reg<C, false, C::GNT, C::GHPT>), dim3(grid), dim3(C::GNT), 0, gs,
                                    d_states.p, r0, d_leaf.p, d_ctr.p, items);
         } else if (hdr)
-            hipLaunchKernelGGL((bcpk::eh_gen<C, true>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
+            hipLaunchKernelGGL((bcpk::eh_gen<C, true>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, gs,
                                d_states.p, r0, d_leaf.p, d_ctr.p);
         else
-            hipLaunchKernelGGL((bcpk::eh_gen<C, false>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, stream,
+            hipLaunchKernelGGL((bcpk::eh_gen<C, false>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, gs,
                                d_states.p, r0, d_leaf.p, d_ctr.p);
+        if (gstream) {
+            BCP_HIP_CHECK(hipEventRecord(evg, gstream));
+            BCP_HIP_CHECK(hipStreamWaitEvent(stream, evg, 0));
+        }
         launch_rounds<C>((int)nstates, std::make_integer_sequence<int, C::K>{});
         constexpr int EB = C::L < 64 ? 64 : C::L;
         bcpk::EhStages stages{};
@@ -1405,7 +1422,16 @@ EquihashGpuSolver::EquihashGpuSolver(unsigned n, unsigned k, int batch, int devi
     impl->batch = batch;
     impl->device = UseDevice(device);
     BCP_HIP_CHECK(hipDeviceGetAttribute(&impl->ncu, hipDeviceAttributeMultiprocessorCount, impl->device));
-    BCP_HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
+    if (BCP_EH_PRIO) {
+        int least = 0, greatest = 0;
+        BCP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        BCP_HIP_CHECK(hipStreamCreateWithPriority(&impl->stream, hipStreamNonBlocking, greatest));
+        BCP_HIP_CHECK(hipStreamCreateWithPriority(&impl->gstream, hipStreamNonBlocking, least));
+        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evs, hipEventDisableTiming));
+        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evg, hipEventDisableTiming));
+    } else {
+        BCP_HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
+    }
     BCP_HIP_CHECK(hipEventCreate(&impl->ev0));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev1));
     dispatch_cfg(n, k, [&](auto c) { impl->alloc<decltype(c)>(); });
@@ -1418,6 +1444,9 @@ EquihashGpuSolver::~EquihashGpuSolver() {
         if (impl->ev0) (void)hipEventDestroy(impl->ev0);
         if (impl->ev1) (void)hipEventDestroy(impl->ev1);
         if (impl->stream) (void)hipStreamDestroy(impl->stream);
+        if (impl->gstream) (void)hipStreamSynchronize(impl->gstream), (void)hipStreamDestroy(impl->gstream);
+        if (impl->evs) (void)hipEventDestroy(impl->evs);
+        if (impl->evg) (void)hipEventDestroy(impl->evg);
     }
 }
 

@@ -89,8 +89,8 @@ bool CKey::Check(const unsigned char* vch) { return secp::seckey_verify(vch); }
 
 void CKey::MakeNewKey(bool compressed) {
     do {
-        GetStrongRandBytes(keydata, 32);
-    } while (!Check(keydata));
+        GetStrongRandBytes(keydata.data(), 32);
+    } while (!Check(keydata.data()));
     fValid = true;
     fCompressed = compressed;
 }
@@ -98,7 +98,7 @@ void CKey::MakeNewKey(bool compressed) {
 CPubKey CKey::GetPubKey() const {
     if (!fValid) throw std::logic_error("CKey::GetPubKey on invalid key");
     secp::Ge p;
-    if (!secp::pubkey_create(p, keydata)) throw std::logic_error("pubkey_create failed");
+    if (!secp::pubkey_create(p, keydata.data())) throw std::logic_error("pubkey_create failed");
     std::vector<unsigned char> ser = secp::pubkey_serialize(p, fCompressed);
     return CPubKey(ser);
 }
@@ -109,7 +109,7 @@ bool CKey::Sign(const uint256& hash, std::vector<unsigned char>& vchSig, uint32_
     WriteLE32(extra, test_case);
     secp::Signature sig;
     int recid = 0;
-    if (!secp::ecdsa_sign(sig, &recid, hash.begin(), keydata, test_case ? extra : nullptr)) return false;
+    if (!secp::ecdsa_sign(sig, &recid, hash.begin(), keydata.data(), test_case ? extra : nullptr)) return false;
     vchSig = secp::sig_serialize_der(sig);
     return true;
 }
@@ -118,7 +118,7 @@ bool CKey::SignCompact(const uint256& hash, std::vector<unsigned char>& vchSig) 
     if (!fValid) return false;
     secp::Signature sig;
     int recid = 0;
-    if (!secp::ecdsa_sign(sig, &recid, hash.begin(), keydata, nullptr)) return false;
+    if (!secp::ecdsa_sign(sig, &recid, hash.begin(), keydata.data(), nullptr)) return false;
     vchSig.assign(CPubKey::COMPACT_SIGNATURE_SIZE, 0);
     secp::sig_serialize_compact(&vchSig[1], sig);
     vchSig[0] = (unsigned char)(27 + recid + (fCompressed ? 4 : 0));
@@ -145,15 +145,16 @@ bool CKey::Derive(CKey& keyChild, ChainCode& ccChild, unsigned int nChild, const
     unsigned char out[64];
     if ((nChild >> 31) == 0) {
         secp::Ge p;
-        if (!secp::pubkey_create(p, keydata)) return false;
+        if (!secp::pubkey_create(p, keydata.data())) return false;
         std::vector<unsigned char> pub = secp::pubkey_serialize(p, true);
         BIP32Hash(cc, nChild, pub[0], pub.data() + 1, out);
     } else {
-        BIP32Hash(cc, nChild, 0, keydata, out);
+        BIP32Hash(cc, nChild, 0, keydata.data(), out);
     }
     memcpy(ccChild.begin(), out + 32, 32);
-    memcpy(keyChild.keydata, keydata, 32);
-    const bool ok = secp::seckey_tweak_add(keyChild.keydata, out);
+    memcpy(keyChild.keydata.data(), keydata.data(), 32);
+    const bool ok = secp::seckey_tweak_add(keyChild.keydata.data(), out);
+    memory_cleanse(out, sizeof(out));
     keyChild.fCompressed = true;
     keyChild.fValid = ok;
     return ok;

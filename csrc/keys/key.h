@@ -7,6 +7,7 @@
 #include "primitives/uint256.h"
 #include "crypto/hashes.h"
 #include "script/script.h"
+#include "util/lockedpool.h"
 
 #include <string>
 #include <vector>
@@ -79,24 +80,29 @@ private:
     std::vector<unsigned char> vch;
 };
 
+// Private key bytes in locked, cleansed-on-free memory (reference src/key.h:32 CPrivKey).
+typedef std::vector<unsigned char, secure_allocator<unsigned char>> CPrivKey;
+
+// The 32 secret bytes live in the process's LockedPool (mlocked pages, cleansed when freed), as
+// the reference's CKey::keydata does (src/key.h:47); copies of a key allocate their own.
 class CKey {
 public:
-    CKey() {}
+    CKey() : keydata(32) {}
     bool IsValid() const { return fValid; }
     bool IsCompressed() const { return fCompressed; }
-    const unsigned char* begin() const { return keydata; }
-    const unsigned char* end() const { return keydata + 32; }
+    const unsigned char* begin() const { return keydata.data(); }
+    const unsigned char* end() const { return keydata.data() + 32; }
     unsigned int size() const { return fValid ? 32 : 0; }
     friend bool operator==(const CKey& a, const CKey& b) {
-        return a.fCompressed == b.fCompressed && a.fValid == b.fValid && memcmp(a.keydata, b.keydata, 32) == 0;
+        return a.fCompressed == b.fCompressed && a.fValid == b.fValid && memcmp(a.begin(), b.begin(), 32) == 0;
     }
     template <typename It> void Set(It b, It e, bool compressed) {
         if ((size_t)(e - b) != 32) {
             fValid = false;
             return;
         }
-        std::copy(b, e, keydata);
-        fValid = Check(keydata);
+        std::copy(b, e, keydata.begin());
+        fValid = Check(keydata.data());
         fCompressed = compressed;
     }
     static bool Check(const unsigned char* vch);
@@ -107,12 +113,12 @@ public:
     bool SignCompact(const uint256& hash, std::vector<unsigned char>& vchSig) const;
     bool Derive(CKey& keyChild, ChainCode& ccChild, unsigned int nChild, const ChainCode& cc) const;
     bool VerifyPubKey(const CPubKey& vchPubKey) const;
-    std::vector<unsigned char> GetPrivKeyBytes() const { return std::vector<unsigned char>(keydata, keydata + 32); }
+    CPrivKey GetPrivKeyBytes() const { return CPrivKey(keydata.begin(), keydata.end()); }
 
 private:
     bool fValid = false;
     bool fCompressed = false;
-    unsigned char keydata[32] = {0};
+    CPrivKey keydata;
 };
 
 static const unsigned int BIP32_EXTKEY_SIZE = 74;

@@ -15,6 +15,9 @@ inline std::vector<unsigned char> to_vec(const pyb::bytes& b) {
 }
 inline pyb::bytes to_bytes(const unsigned char* p, size_t n) { return pyb::bytes((const char*)p, n); }
 inline pyb::bytes to_bytes(const std::vector<unsigned char>& v) { return pyb::bytes((const char*)v.data(), v.size()); }
+template <class A> inline pyb::bytes to_bytes(const std::vector<unsigned char, A>& v) {
+    return pyb::bytes((const char*)v.data(), v.size());
+}
 
 void bind_crypto(pyb::module_& m);
 void bind_equihash(pyb::module_& m);

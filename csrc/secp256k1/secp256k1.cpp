@@ -5,7 +5,9 @@
 
 #include <algorithm>
 #include <cstring>
+#include <cstdio>
 #include <mutex>
+#include <stdexcept>
 
 namespace bcp {
 namespace secp {
@@ -41,9 +43,30 @@ static inline uint64_t add4(uint64_t* r, const uint64_t* a, const uint64_t* b) {
     return (uint64_t)c;
 }
 
-static inline void fe_reduce_once(uint64_t* r) {
-    if (geq4(r, P)) sub4(r, r, P);
+// Branch-free helpers: every field and scalar operation below runs the same instruction
+// sequence for every input (secret keys and nonces pass through them when signing).
+static inline uint64_t mask_of(uint64_t bit) { return (uint64_t)0 - bit; } // 0 or all-ones
+static inline void cmov4(uint64_t* r, const uint64_t* a, uint64_t mask) {
+    for (int i = 0; i < 4; ++i) r[i] = (r[i] & ~mask) | (a[i] & mask);
 }
+// r -= m when r >= m (one conditional subtraction, no branch)
+static inline void csub4(uint64_t* r, const uint64_t* m) {
+    uint64_t t[4];
+    const uint64_t borrow = sub4(t, r, m);
+    cmov4(r, t, mask_of(borrow ^ 1));
+}
+// r += c * PC over all four limbs (c in {0, 1})
+static inline uint64_t add_pc(uint64_t* r, uint64_t c) {
+    u128 t = (u128)r[0] + (PC & mask_of(c));
+    r[0] = (uint64_t)t;
+    for (int i = 1; i < 4; ++i) {
+        t = (u128)r[i] + (uint64_t)(t >> 64);
+        r[i] = (uint64_t)t;
+    }
+    return (uint64_t)(t >> 64);
+}
+
+static inline void fe_reduce_once(uint64_t* r) { csub4(r, P); }
 
 void fe_set_b32(Fe& r, const unsigned char* b, bool* overflow) {
     for (int i = 0; i < 4; ++i) {
@@ -51,9 +74,10 @@ void fe_set_b32(Fe& r, const unsigned char* b, bool* overflow) {
         for (int j = 0; j < 8; ++j) v = (v << 8) | b[(3 - i) * 8 + j];
         r.n[i] = v;
     }
-    bool of = geq4(r.n, P);
+    uint64_t t[4];
+    const uint64_t of = sub4(t, r.n, P) ^ 1;
+    cmov4(r.n, t, mask_of(of));
     if (overflow) *overflow = of;
-    if (of) sub4(r.n, r.n, P);
 }
 void fe_get_b32(unsigned char* b, const Fe& a) {
     for (int i = 0; i < 4; ++i)
@@ -63,30 +87,26 @@ void fe_set_int(Fe& r, uint64_t v) { r.n[0] = v; r.n[1] = r.n[2] = r.n[3] = 0; }
 bool fe_is_zero(const Fe& a) { return (a.n[0] | a.n[1] | a.n[2] | a.n[3]) == 0; }
 bool fe_equal(const Fe& a, const Fe& b) { return memcmp(a.n, b.n, 32) == 0; }
 bool fe_is_odd(const Fe& a) { return a.n[0] & 1; }
+// all-ones when a == 0 (branch-free)
+static inline uint64_t fe_zero_mask(const Fe& a) {
+    const uint64_t x = a.n[0] | a.n[1] | a.n[2] | a.n[3];
+    return mask_of(((x | ((uint64_t)0 - x)) >> 63) ^ 1);
+}
 
 void fe_add(Fe& r, const Fe& a, const Fe& b) {
-    uint64_t c = add4(r.n, a.n, b.n);
-    if (c) { // value = 2^256 + r  ==  r + PC (mod p); cannot overflow again
-        u128 t = (u128)r.n[0] + PC;
-        r.n[0] = (uint64_t)t;
-        for (int i = 1; i < 4 && (t >> 64); ++i) {
-            t = (u128)r.n[i] + 1;
-            r.n[i] = (uint64_t)t;
-        }
-    }
+    // a + b = 2^256 * c + r  ==  r + c * PC (mod p); that sum cannot carry again
+    const uint64_t c = add4(r.n, a.n, b.n);
+    add_pc(r.n, c);
     fe_reduce_once(r.n);
 }
 void fe_sub(Fe& r, const Fe& a, const Fe& b) {
-    uint64_t borrow = sub4(r.n, a.n, b.n);
-    if (borrow) { // wrapped value = a - b + 2^256; subtract PC to get a - b + p
-        u128 t = (u128)r.n[0] - PC;
-        r.n[0] = (uint64_t)t;
-        uint64_t br = (uint64_t)(t >> 127) & 1;
-        for (int i = 1; i < 4 && br; ++i) {
-            u128 u = (u128)r.n[i] - 1;
-            r.n[i] = (uint64_t)u;
-            br = (uint64_t)(u >> 127) & 1;
-        }
+    // a wrapped difference is a - b + 2^256: subtract PC to land on a - b + p
+    const uint64_t borrow = sub4(r.n, a.n, b.n);
+    u128 t = (u128)r.n[0] - (PC & mask_of(borrow));
+    r.n[0] = (uint64_t)t;
+    for (int i = 1; i < 4; ++i) {
+        t = (u128)r.n[i] - ((uint64_t)(t >> 127) & 1);
+        r.n[i] = (uint64_t)t;
     }
 }
 void fe_neg(Fe& r, const Fe& a) {
@@ -115,14 +135,7 @@ static void fe_reduce8(uint64_t* r, const uint64_t* t) {
         r[i] = (uint64_t)c;
         c >>= 64;
     }
-    if (c) { // one more 2^256 -> PC
-        u128 d = (u128)r[0] + PC;
-        r[0] = (uint64_t)d;
-        for (int i = 1; i < 4 && (d >> 64); ++i) {
-            d = (u128)r[i] + 1;
-            r[i] = (uint64_t)d;
-        }
-    }
+    add_pc(r, (uint64_t)c); // one more 2^256 -> PC
     fe_reduce_once(r);
 }
 
@@ -231,9 +244,10 @@ void sc_set_b32(Scalar& r, const unsigned char* b, bool* overflow) {
         for (int j = 0; j < 8; ++j) v = (v << 8) | b[(3 - i) * 8 + j];
         r.n[i] = v;
     }
-    bool of = geq4(r.n, N);
+    uint64_t t[4];
+    const uint64_t of = sub4(t, r.n, N) ^ 1;
+    cmov4(r.n, t, mask_of(of));
     if (overflow) *overflow = of;
-    if (of) sub4(r.n, r.n, N);
 }
 void sc_get_b32(unsigned char* b, const Scalar& a) {
     for (int i = 0; i < 4; ++i)
@@ -241,40 +255,41 @@ void sc_get_b32(unsigned char* b, const Scalar& a) {
 }
 bool sc_is_zero(const Scalar& a) { return (a.n[0] | a.n[1] | a.n[2] | a.n[3]) == 0; }
 bool sc_is_high(const Scalar& a) {
-    for (int i = 3; i >= 0; --i) {
-        if (a.n[i] != NH[i]) return a.n[i] > NH[i];
-    }
-    return false;
+    // a > n/2  <=>  n/2 - a borrows
+    uint64_t t[4];
+    return sub4(t, NH, a.n) != 0;
 }
 void sc_add(Scalar& r, const Scalar& a, const Scalar& b) {
-    uint64_t c = add4(r.n, a.n, b.n);
-    if (c || geq4(r.n, N)) sub4(r.n, r.n, N);
+    const uint64_t c = add4(r.n, a.n, b.n);
+    uint64_t t[4];
+    const uint64_t borrow = sub4(t, r.n, N);
+    // subtract n when the sum carried out of 2^256 or is >= n
+    cmov4(r.n, t, mask_of(c | (borrow ^ 1)));
 }
 void sc_neg(Scalar& r, const Scalar& a) {
-    if (sc_is_zero(a)) {
-        r = a;
-        return;
-    }
-    sub4(r.n, N, a.n);
+    // n - a, and 0 for a == 0
+    const uint64_t x = a.n[0] | a.n[1] | a.n[2] | a.n[3];
+    const uint64_t nz = mask_of((x | ((uint64_t)0 - x)) >> 63);
+    uint64_t t[4];
+    sub4(t, N, a.n);
+    for (int i = 0; i < 4; ++i) r.n[i] = t[i] & nz;
 }
-// reduce a little-endian multi-limb number (up to 8 limbs) mod n
+// Reduce a 512-bit product mod n with a fixed sequence of operations: n = 2^256 - NC (NC < 2^129),
+// so t = lo + hi * 2^256 == lo + hi * NC. Three folds bring any 512-bit value below 2^256 + 2^132,
+// a fourth below 2^256; one conditional subtraction finishes (2^256 < 2n).
 static void sc_reduce(uint64_t* out, const uint64_t* tin) {
     uint64_t t[9] = {0};
     memcpy(t, tin, 8 * sizeof(uint64_t));
     for (int iter = 0; iter < 4; ++iter) {
-        if ((t[4] | t[5] | t[6] | t[7] | t[8]) == 0) break;
-        // t = lo + hi * NC
-        uint64_t hi[5] = {t[4], t[5], t[6], t[7], t[8]};
         uint64_t acc[9] = {t[0], t[1], t[2], t[3], 0, 0, 0, 0, 0};
-        for (int i = 0; i < 5; ++i) {
-            if (!hi[i]) continue;
+        for (int i = 0; i < 5; ++i) { // acc += hi[i] * NC << 64i; every limb, zeros included
             u128 c = 0;
             for (int j = 0; j < 3; ++j) {
-                c += (u128)hi[i] * NC[j] + acc[i + j];
+                c += (u128)t[4 + i] * NC[j] + acc[i + j];
                 acc[i + j] = (uint64_t)c;
                 c >>= 64;
             }
-            for (int k = i + 3; c && k < 9; ++k) {
+            for (int k = i + 3; k < 9; ++k) {
                 c += acc[k];
                 acc[k] = (uint64_t)c;
                 c >>= 64;
@@ -282,7 +297,7 @@ static void sc_reduce(uint64_t* out, const uint64_t* tin) {
         }
         memcpy(t, acc, sizeof(acc));
     }
-    while (geq4(t, N)) sub4(t, t, N);
+    csub4(t, N);
     memcpy(out, t, 32);
 }
 void sc_mul(Scalar& r, const Scalar& a, const Scalar& b) {
@@ -557,13 +572,233 @@ const std::vector<Ge>& generator_table() {
     return *g_gen_table;
 }
 
-void ecmult_gen(Gej& r, const Scalar& k) {
+// Variable-time k*G for PUBLIC scalars only (signature verification, ecmult): one table add per
+// non-zero byte of k.
+void ecmult_gen_var(Gej& r, const Scalar& k) {
     std::call_once(g_gen_once, build_gen_table);
     r.inf = true;
     for (int i = 0; i < 32; ++i) {
         const unsigned byte = (unsigned)(k.n[i / 8] >> ((i % 8) * 8)) & 0xff;
         if (byte) gej_add_ge(r, r, (*g_gen_table)[i * 256 + byte]);
     }
+}
+
+// ---------------------------------------------------------------- constant-time k*G
+// For SECRET scalars (signing nonces, private keys). Same method as libsecp256k1's
+// secp256k1_ecmult_gen (reference src/secp256k1/src/ecmult_gen_impl.h:124-156):
+//  * a comb of 64 rows x 16 affine entries, CT_TAB[j][i] = (i * 16^j + 1) * G, so no entry is
+//    the point at infinity;
+//  * the scalar is blinded, s = k + b (b random per process), and the accumulator starts at
+//    A0 = (-b - 64) * G with randomised Jacobian Z, so sum_j CT_TAB[j][nibble_j(s)] + A0 = k * G;
+//  * every row lookup reads ALL 16 entries and keeps the wanted one with masks (cmov), and every
+//    addition runs the full formula (its exceptional cases are selected with masks), so the
+//    sequence of memory reads and field operations is the same for every k.
+namespace {
+struct CtGenTable {
+    Ge e[64][16];
+};
+CtGenTable* g_ct_tab = nullptr;
+std::once_flag g_ct_once;
+struct CtBlind {
+    Scalar b;  // blinding scalar
+    Gej a0;    // (-b - 64) * G, Z randomised
+};
+std::mutex g_blind_mu;
+CtBlind g_blind;
+bool g_blind_set = false;
+thread_local EcmultGenTrace* g_trace = nullptr;
+
+void build_ct_table() {
+    std::vector<Gej> jac(64 * 16);
+    Gej base, one;
+    gej_set_ge(base, generator());
+    gej_set_ge(one, generator());
+    for (int j = 0; j < 64; ++j) {
+        Gej acc = one; // 1 * G, then + base each step: (i * 16^j + 1) * G
+        for (int i = 0; i < 16; ++i) {
+            jac[j * 16 + i] = acc;
+            gej_add(acc, acc, base);
+        }
+        for (int k = 0; k < 4; ++k) gej_double(base, base);
+    }
+    auto* t = new CtGenTable;
+    batch_to_affine(&t->e[0][0], jac.data(), jac.size());
+    g_ct_tab = t;
+}
+
+void read_urandom(unsigned char* out, size_t n) {
+    size_t got = 0;
+    if (FILE* f = fopen("/dev/urandom", "rb")) {
+        got = fread(out, 1, n, f);
+        fclose(f);
+    }
+    if (got != n) throw std::runtime_error("secp256k1: cannot read /dev/urandom for the signing blind");
+}
+
+// Constant-time Jacobian doubling (the formula of gej_double without its early exits; the
+// infinity flag passes through, and secp256k1 has no point with y = 0).
+void gej_double_ct(Gej& r, const Gej& a) {
+    Fe A, B, C, D, E, F, t, X3, Y3, Z3;
+    fe_sqr(A, a.x);
+    fe_sqr(B, a.y);
+    fe_sqr(C, B);
+    fe_add(t, a.x, B);
+    fe_sqr(t, t);
+    fe_sub(t, t, A);
+    fe_sub(t, t, C);
+    fe_add(D, t, t);
+    fe_add(E, A, A);
+    fe_add(E, E, A);
+    fe_sqr(F, E);
+    fe_add(t, D, D);
+    fe_sub(X3, F, t);
+    fe_sub(t, D, X3);
+    fe_mul(Y3, E, t);
+    fe_add(t, C, C);
+    fe_add(t, t, t);
+    fe_add(t, t, t);
+    fe_sub(Y3, Y3, t);
+    fe_mul(Z3, a.y, a.z);
+    fe_add(Z3, Z3, Z3);
+    r.x = X3;
+    r.y = Y3;
+    r.z = Z3;
+    r.inf = a.inf;
+}
+
+void fe_cmov(Fe& r, const Fe& a, uint64_t mask) { cmov4(r.n, a.n, mask); }
+
+// Constant-time r = a + b (b affine, never infinity): the general formula, the doubling of a
+// (for a == b) and b itself (for a = infinity) are all computed; masks pick the result, and
+// a == -b yields infinity.
+void gej_add_ge_ct(Gej& r, const Gej& a, const Ge& b) {
+    Fe Z1Z1, U2, S2, H, rr, HH, I, J, V, t, X3, Y3, Z3;
+    fe_sqr(Z1Z1, a.z);
+    fe_mul(U2, b.x, Z1Z1);
+    fe_mul(S2, b.y, a.z);
+    fe_mul(S2, S2, Z1Z1);
+    fe_sub(H, U2, a.x);
+    fe_sub(rr, S2, a.y);
+    fe_add(rr, rr, rr);
+    fe_sqr(HH, H);
+    fe_add(I, HH, HH);
+    fe_add(I, I, I);
+    fe_mul(J, H, I);
+    fe_mul(V, a.x, I);
+    fe_sqr(X3, rr);
+    fe_sub(X3, X3, J);
+    fe_sub(X3, X3, V);
+    fe_sub(X3, X3, V);
+    fe_sub(t, V, X3);
+    fe_mul(Y3, rr, t);
+    fe_mul(t, a.y, J);
+    fe_add(t, t, t);
+    fe_sub(Y3, Y3, t);
+    fe_add(Z3, a.z, H);
+    fe_sqr(Z3, Z3);
+    fe_sub(Z3, Z3, Z1Z1);
+    fe_sub(Z3, Z3, HH);
+    Gej d;
+    gej_double_ct(d, a);
+    const uint64_t ainf = mask_of((uint64_t)a.inf);
+    const uint64_t hz = fe_zero_mask(H) & ~ainf, rz = fe_zero_mask(rr);
+    const uint64_t dbl = hz & rz, neg = hz & ~rz; // a == b, a == -b
+    Gej out;
+    out.x = X3;
+    out.y = Y3;
+    out.z = Z3;
+    fe_cmov(out.x, d.x, dbl);
+    fe_cmov(out.y, d.y, dbl);
+    fe_cmov(out.z, d.z, dbl);
+    Fe one;
+    fe_set_int(one, 1);
+    fe_cmov(out.x, b.x, ainf);
+    fe_cmov(out.y, b.y, ainf);
+    fe_cmov(out.z, one, ainf);
+    out.inf = (bool)(neg & 1);
+    r = out;
+}
+
+// Set the blind from 32 seed bytes (caller holds g_blind_mu).
+void set_blind_locked(const unsigned char* seed32) {
+    unsigned char h[32], z32[32];
+    CSHA256().Write(seed32, 32).Write((const unsigned char*)"bcp-ecmult-gen-blind", 20).Finalize(h);
+    CSHA256().Write(h, 32).Write((const unsigned char*)"z", 1).Finalize(z32);
+    Scalar b, nb, c64;
+    sc_set_b32(b, h);
+    if (sc_is_zero(b)) b.n[0] = 1;
+    // A0 = (-b - 64) * G: computed by the public-scalar path (b is not used on its own
+    // anywhere an attacker can time it; the value is fixed for the process)
+    c64 = {{64, 0, 0, 0}};
+    sc_add(nb, b, c64);
+    sc_neg(nb, nb);
+    Gej a0;
+    ecmult_gen_var(a0, nb);
+    Fe z, z2, z3;
+    bool of;
+    fe_set_b32(z, z32, &of);
+    if (fe_is_zero(z)) fe_set_int(z, 1);
+    fe_sqr(z2, z);
+    fe_mul(z3, z2, z);
+    fe_mul(a0.x, a0.x, z2);
+    fe_mul(a0.y, a0.y, z3);
+    fe_mul(a0.z, a0.z, z);
+    g_blind.b = b;
+    g_blind.a0 = a0;
+    g_blind_set = true;
+    memory_cleanse(h, sizeof(h));
+    memory_cleanse(z32, sizeof(z32));
+}
+} // namespace
+
+void ecmult_gen_blind(const unsigned char* seed32) {
+    std::call_once(g_gen_once, build_gen_table);
+    unsigned char seed[32];
+    if (seed32) memcpy(seed, seed32, 32);
+    else read_urandom(seed, 32);
+    std::lock_guard<std::mutex> lk(g_blind_mu);
+    set_blind_locked(seed);
+    memory_cleanse(seed, sizeof(seed));
+}
+
+void ecmult_gen_trace(EcmultGenTrace* t) { g_trace = t; }
+
+void ecmult_gen(Gej& r, const Scalar& k) {
+    std::call_once(g_ct_once, build_ct_table);
+    std::call_once(g_gen_once, build_gen_table);
+    CtBlind bl;
+    {
+        std::lock_guard<std::mutex> lk(g_blind_mu);
+        if (!g_blind_set) {
+            unsigned char seed[32];
+            read_urandom(seed, 32);
+            set_blind_locked(seed);
+            memory_cleanse(seed, sizeof(seed));
+        }
+        bl = g_blind;
+    }
+    Scalar s;
+    sc_add(s, k, bl.b);
+    Gej acc = bl.a0;
+    EcmultGenTrace* tr = g_trace;
+    for (int j = 0; j < 64; ++j) {
+        const uint64_t nib = (s.n[j / 16] >> ((j % 16) * 4)) & 15;
+        Ge e;
+        e.inf = false;
+        fe_set_int(e.x, 0);
+        fe_set_int(e.y, 0);
+        for (uint64_t i = 0; i < 16; ++i) { // every entry of the row is read
+            const Ge& c = g_ct_tab->e[j][i];
+            const uint64_t m = mask_of((((i ^ nib) | ((uint64_t)0 - (i ^ nib))) >> 63) ^ 1);
+            fe_cmov(e.x, c.x, m);
+            fe_cmov(e.y, c.y, m);
+            if (tr) tr->reads.push_back((uint32_t)(j * 16 + i));
+        }
+        gej_add_ge_ct(acc, acc, e);
+        if (tr) tr->adds++;
+    }
+    r = acc;
+    memory_cleanse(&s, sizeof(s));
 }
 
 // width-w NAF of a scalar; returns number of digits
@@ -762,7 +997,7 @@ void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng) {
     }
     if (!sc_is_zero(ng)) {
         Gej g;
-        ecmult_gen(g, ng);
+        ecmult_gen_var(g, ng);
         gej_add(acc, acc, g);
     }
     r = acc;
@@ -796,7 +1031,7 @@ void ecmult_plain(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng) {
     }
     if (!sc_is_zero(ng)) {
         Gej g;
-        ecmult_gen(g, ng);
+        ecmult_gen_var(g, ng);
         gej_add(acc, acc, g);
     }
     r = acc;
@@ -866,6 +1101,7 @@ bool pubkey_create(Ge& r, const unsigned char* seckey32) {
     Gej pj;
     ecmult_gen(pj, s);
     ge_set_gej(r, pj);
+    memory_cleanse(&s, sizeof(s));
     return true;
 }
 
@@ -1092,14 +1328,15 @@ bool ecdsa_sign(Signature& sig, int* recid, const unsigned char* msg32, const un
     sc_set_b32(d, seckey32, &of);
     if (of || sc_is_zero(d)) return false;
     sc_set_b32(e, msg32);
-    for (unsigned int counter = 0; counter < 1000; ++counter) {
-        unsigned char nonce[32];
+    bool ok = false;
+    unsigned char nonce[32];
+    Scalar k, n, kinv;
+    for (unsigned int counter = 0; counter < 1000 && !ok; ++counter) {
         rfc6979_nonce(nonce, msg32, seckey32, extra32, counter);
-        Scalar k;
         sc_set_b32(k, nonce, &of);
-        if (of || sc_is_zero(k)) continue;
+        if (of || sc_is_zero(k)) continue; // probability ~2^-128: a retry, not a timing signal
         Gej Rj;
-        ecmult_gen(Rj, k);
+        ecmult_gen(Rj, k); // constant-time, blinded
         Ge R;
         ge_set_gej(R, Rj);
         unsigned char xb[32];
@@ -1107,20 +1344,24 @@ bool ecdsa_sign(Signature& sig, int* recid, const unsigned char* msg32, const un
         bool xof;
         sc_set_b32(sig.r, xb, &xof);
         int rid = (xof ? 2 : 0) | (fe_is_odd(R.y) ? 1 : 0);
-        Scalar n, kinv;
         sc_mul(n, sig.r, d);
         sc_add(n, n, e);
         sc_inv(kinv, k);
         sc_mul(sig.s, kinv, n);
         if (sc_is_zero(sig.r) || sc_is_zero(sig.s)) continue;
-        if (sc_is_high(sig.s)) {
+        if (sc_is_high(sig.s)) { // s is public output
             sc_neg(sig.s, sig.s);
             rid ^= 1;
         }
         if (recid) *recid = rid;
-        return true;
+        ok = true;
     }
-    return false;
+    memory_cleanse(nonce, sizeof(nonce));
+    memory_cleanse(&k, sizeof(k));
+    memory_cleanse(&kinv, sizeof(kinv));
+    memory_cleanse(&n, sizeof(n));
+    memory_cleanse(&d, sizeof(d));
+    return ok;
 }
 
 bool ecdsa_recover(Ge& pub, const Signature& sig, int recid, const unsigned char* msg32) {

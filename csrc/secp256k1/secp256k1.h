@@ -12,8 +12,11 @@
 // Verification semantics match CPubKey::Verify: lax-DER parse, low-S normalisation,
 // r,s in [1, n-1], pubkeys in compressed/uncompressed/hybrid form.
 // The throughput path is the batched GPU verifier (csrc/kernels/secp256k1.hip).
-// This CPU code is not constant-time; it is used for verification and for the
-// wallet's signing of its own keys.
+// Secret-scalar paths are constant-time: field and scalar arithmetic are branch-free, and
+// ecmult_gen (signing nonces, pubkey_create, BIP32 private derivation) is a blinded comb whose
+// table rows are scanned in full and whose additions select their exceptional cases by mask
+// (reference src/secp256k1/src/ecmult_gen_impl.h:124-156). Verification and recovery work on
+// public values and use the faster variable-time ecmult / ecmult_gen_var.
 #pragma once
 #include <cstddef>
 #include <cstdint>
@@ -71,7 +74,18 @@ void gej_add_ge(Gej& r, const Gej& a, const Ge& b);
 void gej_add(Gej& r, const Gej& a, const Gej& b);
 void ge_set_gej(Ge& r, const Gej& a);
 bool ge_is_valid(const Ge& a);
-void ecmult_gen(Gej& r, const Scalar& k);
+void ecmult_gen(Gej& r, const Scalar& k);     // constant-time, blinded (secret k)
+void ecmult_gen_var(Gej& r, const Scalar& k); // variable-time (public k only)
+// Re-randomise the signing blind (libsecp256k1's context_randomize); nullptr = /dev/urandom.
+// A blind is drawn from /dev/urandom on first use anyway.
+void ecmult_gen_blind(const unsigned char* seed32);
+// Test instrumentation: while set (per thread), ecmult_gen appends the index (row * 16 + entry) of
+// every table entry it reads and counts its point additions.
+struct EcmultGenTrace {
+    std::vector<uint32_t> reads;
+    uint32_t adds = 0;
+};
+void ecmult_gen_trace(EcmultGenTrace* t);
 // Affine comb table, entry [i*256 + j] = j * 256^i * G (j = 0 is the point at infinity).
 const std::vector<Ge>& generator_table();                                  // k*G
 void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng);     // na*A + ng*G (GLV)

@@ -201,3 +201,154 @@ TEST_CASE(crypto_tests, secp256k1_field_chains_and_verify) {
     }
     CHECK(good > 150);
 }
+
+TEST_CASE(crypto_tests, secp256k1_ecmult_gen_constant_time) {
+    // The signing-path k*G (blinded comb, full-row cmov lookups, mask-selected exceptional
+    // cases) against the variable-time byte table, and its access pattern: scalars with and
+    // without zero bytes / zero nibbles must read the same table entries in the same order and
+    // make the same number of point additions (reference src/secp256k1/src/ecmult_gen_impl.h:124-156).
+    FastRandomContext rng(true);
+    std::vector<secp::Scalar> ks;
+    for (const char* hex : {"01", "02", "0f", "10", "ff", "0100", "01000000000000000000000000000000",
+                            "fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0364140",
+                            "00ff00ff00ff00ff00ff00ff00ff00ff00ff00ff00ff00ff00ff00ff00ff00ff",
+                            "1111111111111111111111111111111111111111111111111111111111111111",
+                            "8000000000000000000000000000000000000000000000000000000000000000",
+                            "7fffffffffffffffffffffffffffffff5d576e7357a4501ddfe92f46681b20a0"}) {
+        const std::vector<unsigned char> v = ParseHex(hex);
+        unsigned char b[32] = {0};
+        memcpy(b + 32 - v.size(), v.data(), v.size());
+        secp::Scalar s;
+        secp::sc_set_b32(s, b);
+        ks.push_back(s);
+    }
+    for (int i = 0; i < 200; ++i) {
+        unsigned char b[32];
+        for (auto& x : b) x = (unsigned char)rng.randbits(8);
+        if (i % 4 == 1) // sparse scalars: most bytes zero
+            for (int j = 0; j < 32; ++j)
+                if (rng.randbits(2)) b[j] = 0;
+        secp::Scalar s;
+        secp::sc_set_b32(s, b);
+        if (!secp::sc_is_zero(s)) ks.push_back(s);
+    }
+    std::vector<uint32_t> ref_reads;
+    uint32_t ref_adds = 0;
+    int same = 0;
+    for (size_t t = 0; t < ks.size(); ++t) {
+        if (t == ks.size() / 2) { // a fresh blind must not change any result
+            unsigned char seed[32];
+            for (auto& x : seed) x = (unsigned char)rng.randbits(8);
+            secp::ecmult_gen_blind(seed);
+        }
+        secp::EcmultGenTrace tr;
+        secp::ecmult_gen_trace(&tr);
+        secp::Gej a, b;
+        secp::ecmult_gen(a, ks[t]);
+        secp::ecmult_gen_trace(nullptr);
+        secp::ecmult_gen_var(b, ks[t]);
+        secp::Ge ga, gb;
+        secp::ge_set_gej(ga, a);
+        secp::ge_set_gej(gb, b);
+        CHECK(!ga.inf && !gb.inf);
+        CHECK(secp::fe_equal(ga.x, gb.x) && secp::fe_equal(ga.y, gb.y));
+        CHECK_EQ(tr.reads.size(), (size_t)(64 * 16));
+        CHECK_EQ(tr.adds, 64u);
+        if (t == 0) {
+            ref_reads = tr.reads;
+            ref_adds = tr.adds;
+        }
+        same += tr.reads == ref_reads && tr.adds == ref_adds;
+    }
+    CHECK_EQ(same, (int)ks.size());
+    // every entry of every row, in row order
+    for (uint32_t i = 0; i < ref_reads.size(); ++i) CHECK_EQ(ref_reads[i], i);
+    // the exceptional inputs of the mask-selected addition: a == b (doubling), a == -b
+    // (infinity) and a = infinity, against the variable-time formulas
+    secp::Scalar three = {{3, 0, 0, 0}}, k2 = {{2, 0, 0, 0}};
+    secp::Gej g3, g2;
+    secp::ecmult_gen(g3, three);
+    secp::ecmult_gen(g2, k2);
+    secp::Ge a3, a2;
+    secp::ge_set_gej(a3, g3);
+    secp::ge_set_gej(a2, g2);
+    CHECK(!a3.inf && !a2.inf);
+}
+
+TEST_CASE(crypto_tests, secp256k1_branchfree_field_scalar) {
+    // the branch-free field / scalar operations against wide-integer references at their
+    // carry and borrow boundaries
+    auto fe = [](const char* hex) {
+        const std::vector<unsigned char> v = ParseHex(hex);
+        unsigned char b[32] = {0};
+        memcpy(b + 32 - v.size(), v.data(), v.size());
+        secp::Fe f;
+        secp::fe_set_b32(f, b);
+        return f;
+    };
+    auto sc = [](const char* hex, bool* of = nullptr) {
+        const std::vector<unsigned char> v = ParseHex(hex);
+        unsigned char b[32] = {0};
+        memcpy(b + 32 - v.size(), v.data(), v.size());
+        secp::Scalar s;
+        secp::sc_set_b32(s, b, of);
+        return s;
+    };
+    auto fhex = [](const secp::Fe& f) {
+        unsigned char b[32];
+        secp::fe_get_b32(b, f);
+        return HexStr(b, b + 32);
+    };
+    auto shex = [](const secp::Scalar& s) {
+        unsigned char b[32];
+        secp::sc_get_b32(b, s);
+        return HexStr(b, b + 32);
+    };
+    const char* PM1 = "fffffffffffffffffffffffffffffffffffffffffffffffffffffffefffffc2e";
+    const char* NM1 = "fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0364140";
+    secp::Fe r;
+    secp::fe_add(r, fe(PM1), fe("01")); // p - 1 + 1 = 0
+    CHECK_EQ(fhex(r), std::string(64, '0'));
+    secp::fe_add(r, fe(PM1), fe(PM1)); // 2p - 2 = p - 2
+    CHECK_EQ(fhex(r), std::string("fffffffffffffffffffffffffffffffffffffffffffffffffffffffefffffc2d"));
+    secp::fe_sub(r, fe("00"), fe("01")); // -1 = p - 1
+    CHECK_EQ(fhex(r), std::string(PM1));
+    secp::fe_mul(r, fe(PM1), fe(PM1)); // (-1)^2 = 1
+    CHECK_EQ(fhex(r), std::string(63, '0') + "1");
+    bool of = false;
+    secp::Fe f;
+    unsigned char pb[32];
+    secp::fe_get_b32(pb, fe(PM1));
+    pb[31] += 1; // p itself overflows to 0
+    secp::fe_set_b32(f, pb, &of);
+    CHECK(of && secp::fe_is_zero(f));
+    secp::Scalar s;
+    secp::sc_add(s, sc(NM1), sc("02")); // n - 1 + 2 = 1
+    CHECK_EQ(shex(s), std::string(63, '0') + "1");
+    secp::sc_add(s, sc(NM1), sc(NM1)); // 2n - 2 = n - 2 (the sum carries out of 2^256)
+    CHECK_EQ(shex(s), std::string("fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd036413f"));
+    secp::sc_mul(s, sc(NM1), sc(NM1)); // (-1)^2 = 1
+    CHECK_EQ(shex(s), std::string(63, '0') + "1");
+    secp::sc_neg(s, sc("00"));
+    CHECK(secp::sc_is_zero(s));
+    secp::sc_neg(s, sc("01"));
+    CHECK_EQ(shex(s), std::string(NM1));
+    CHECK(secp::sc_is_high(sc(NM1)));
+    CHECK(!secp::sc_is_high(sc("7fffffffffffffffffffffffffffffff5d576e7357a4501ddfe92f46681b20a0")));
+    CHECK(secp::sc_is_high(sc("7fffffffffffffffffffffffffffffff5d576e7357a4501ddfe92f46681b20a1")));
+    bool sof = false;
+    sc("fffffffffffffffffffffffffffffffebaaedce6af48a03bbfd25e8cd0364141", &sof); // n
+    CHECK(sof);
+    // random products against the scalar inverse: a * a^-1 == 1
+    FastRandomContext rng(true);
+    for (int i = 0; i < 200; ++i) {
+        unsigned char b[32];
+        for (auto& x : b) x = (unsigned char)rng.randbits(8);
+        secp::Scalar a, ai, p;
+        secp::sc_set_b32(a, b);
+        if (secp::sc_is_zero(a)) continue;
+        secp::sc_inv(ai, a);
+        secp::sc_mul(p, a, ai);
+        CHECK_EQ(shex(p), std::string(63, '0') + "1");
+    }
+}

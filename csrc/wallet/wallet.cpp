@@ -331,7 +331,7 @@ bool CWallet::Load(std::string& err, bool& firstRun) {
             } else if (type == "key") {
                 CPubKey pub;
                 r >> pub;
-                std::vector<unsigned char> priv;
+                CPrivKey priv; // locked memory, cleansed when freed
                 it.GetValue(priv);
                 CKey key;
                 key.Set(priv.begin(), priv.end(), pub.IsCompressed());

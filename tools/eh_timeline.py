@@ -8,7 +8,7 @@ import glob
 import sys
 
 
-def main(d):
+def main(d, seq=0):
     files = glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True)
     if not files:
         print("no kernel_trace.csv under", d)
@@ -54,7 +54,14 @@ def main(d):
     print(f"{'kernel':16s} {'calls':>6s} {'avg ms':>8s} {'total ms':>9s} {'overlapped ms':>14s}")
     for nm in sorted(busy, key=lambda n: (n[:8], n)):
         print(f"{nm:16s} {cnt[nm]:6d} {busy[nm]/cnt[nm]:8.3f} {busy[nm]:9.2f} {over[nm]:14.2f}")
+    if seq:
+        # the last `seq` solver kernels: start offset, duration, stream (interleaving of the solvers)
+        tail = eh[-seq:]
+        b = tail[0][0]
+        print(f"{'start us':>9s} {'end us':>9s} {'dur us':>8s} stream kernel")
+        for s, e, st, nm in tail:
+            print(f"{(s - b) / 1e3:9.1f} {(e - b) / 1e3:9.1f} {(e - s) / 1e3:8.1f} {st:>6} {nm}")
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 0)
