@@ -36,6 +36,19 @@
 
 namespace bcp {
 
+// One shard of a batch: items [lo, hi) on lane `lane`.
+struct VerifyShard {
+    size_t lane, lo, hi;
+};
+// The shard plan of an n-item batch over lanes whose devices are laneDevices[i] (a device may
+// own several lanes). Distinct devices are used first: the batch is cut into
+// k = clamp(n / minPerDevice, 1, #devices) device shares (devices in first-listed order), and a
+// device's share is spread over its further lanes only while each keeps >= minPerLane items
+// (two kernels on one device do not overlap, so a second lane there pays only for very large
+// batches). Shards are contiguous, in lane order, and sized evenly. Pure: no GPU needed.
+std::vector<VerifyShard> PlanShards(size_t n, const std::vector<int>& laneDevices, size_t minPerDevice,
+                                    size_t minPerLane);
+
 class GpuVerifyService {
 public:
     static GpuVerifyService& Instance();
@@ -46,8 +59,12 @@ public:
     void SetDevices(const std::vector<int>& devices);
     std::vector<int> Devices() const;           // resolved list
     std::vector<int> ConfiguredDevices() const; // as set (empty: default)
-    // Smallest shard worth a lane of its own (items); below 2x this a batch stays on one lane.
+    // Smallest shard worth a second lane on the SAME device (items).
     void SetMinShard(size_t ecdsa, size_t equihash);
+    // Smallest shard worth a device of its own (items); see PlanShards.
+    void SetMinDeviceShard(size_t ecdsa, size_t equihash);
+    // The plan a batch of n ECDSA (or Equihash) items would get on the current lanes.
+    std::vector<VerifyShard> Plan(size_t n, bool equihash);
 
     // result[i] = 1 iff job i is valid (gpu::EcdsaVerifyBatch contract, packed arrays).
     std::vector<uint8_t> Ecdsa(const unsigned char* msg32, const unsigned char* sig64, const unsigned char* pub33,
@@ -101,7 +118,7 @@ private:
     static void LaneLoop(Lane* L);
     std::vector<std::shared_ptr<Lane>> AcquireLanes();
     // Runs fn(lane, lo, hi, workers) for the shards of [0, n) and waits; rethrows the first failure.
-    void RunSharded(size_t n, size_t minShard,
+    void RunSharded(size_t n, bool equihash,
                     const std::function<void(gpu::VerifyLane&, size_t, size_t, WorkerPool&)>& fn);
     std::vector<uint8_t> EcdsaFillImpl(size_t n, bool der, const EcdsaFillFn& fill);
 
@@ -109,9 +126,12 @@ private:
     std::vector<int> devices;
     std::vector<std::shared_ptr<Lane>> lanes;
     bool lanesStale = true;
-    // smallest shard worth another lane (see AllDevices in gpuverify.cpp): below these a batch
-    // runs whole on one lane
+    // smallest shard worth a second lane on one device (see AllDevices in gpuverify.cpp)
     size_t minShardEcdsa = 65536, minShardEquihash = 2048;
+    // smallest shard worth a device of its own: the ECDSA floor is the batch at which the
+    // verify kernel's fixed latency stops dominating (profiles/ecdsa_r5.md), the header floor a
+    // few hundred headers (one workgroup per header, 0.2 ms per 2000)
+    size_t minDevEcdsa = 4096, minDevEquihash = 256;
     uint64_t sharded = 0;
 };
 

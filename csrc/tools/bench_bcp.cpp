@@ -1196,7 +1196,8 @@ int main(int argc, char* argv[]) {
     if (gArgs.IsArgSet("-?") || gArgs.IsArgSet("-h") || gArgs.IsArgSet("-help")) {
         printf("Usage: bench_bcp [-filter=<regex>] [-time=<seconds per bench>] [-list] [-datadir=bench/data]\n"
                "                 [-par=<script threads>] [-ibdblocks=<n>] [-kvcoins=<n>] [-kvdbcache=<MiB>]\n"
-               "                 [-parallelutxo=<min txs>] [-ecdsaminshard=<signatures>] [-debug=<category>]\n");
+               "                 [-parallelutxo=<min txs>] [-ecdsaminshard=<signatures>] [-debug=<category>]\n"
+               "                 [-shardplan] (print the GPU verify shard plans for 1, 2 and 8 devices)\n");
         return 0;
     }
     { // default: <dir of the binary>/../bench/data, so the working directory does not matter
@@ -1212,6 +1213,26 @@ int main(int argc, char* argv[]) {
     if (gArgs.IsArgSet("-debug")) { // e.g. -debug=bench: ConnectBlock's phase timers on stderr-side console
         LogInit("", true, false);
         LogEnableCategory(gArgs.GetArg("-debug", "bench"));
+    }
+    if (gArgs.IsArgSet("-shardplan")) { // the verify service's shard plans for 1, 2 and 8 devices
+        for (int ndev : {1, 2, 8}) {
+            std::vector<int> lanes; // the default lane list: every device, twice, round-robin
+            for (int rep = 0; rep < 2; rep++)
+                for (int d = 0; d < ndev; d++) lanes.push_back(d);
+            for (size_t n : {(size_t)512, (size_t)42000, (size_t)199000}) {
+                const auto plan = PlanShards(n, lanes, 4096, 65536); // the ECDSA defaults
+                printf("ecdsa devices=%d n=%zu shards=%zu:", ndev, n, plan.size());
+                for (const auto& sh : plan) printf(" [lane %zu dev %d: %zu]", sh.lane, lanes[sh.lane], sh.hi - sh.lo);
+                printf("\n");
+            }
+            for (size_t n : {(size_t)160, (size_t)2000}) {
+                const auto plan = PlanShards(n, lanes, 256, 2048); // the header defaults
+                printf("headers devices=%d n=%zu shards=%zu:", ndev, n, plan.size());
+                for (const auto& sh : plan) printf(" [dev %d: %zu]", lanes[sh.lane], sh.hi - sh.lo);
+                printf("\n");
+            }
+        }
+        return 0;
     }
     const std::regex filter(gArgs.GetArg("-filter", ".*"));
     const double minTime = atof(gArgs.GetArg("-time", "1.0").c_str());
