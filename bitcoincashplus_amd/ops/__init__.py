@@ -147,7 +147,8 @@ def short_txids(k0: int, k1: int, txids, device: int = -1) -> list:
 
 def ecdsa_verify_compact(msg32, sig64, pub33):
     """Batched verify of packed signatures: msg32 [N,32] digests, sig64 [N,64] compact r||s
-    (low S), pub33 [N,33] compressed keys. GPU tensors stay on the device and give a [N] uint8
+    (low S: a high-S signature is reported invalid, as secp256k1_ecdsa_verify does), pub33
+    [N,33] compressed keys. GPU tensors stay on the device and give a [N] uint8
     GPU tensor (1 = valid) on the current stream; bytes give a list of bools through the
     node's verify lanes."""
     require_gpu("ecdsa_verify_compact")

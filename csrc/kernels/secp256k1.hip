@@ -791,6 +791,9 @@ __global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs,
             br = (d >> 63) & 1;
         }
     }
+    // compact inputs must already be low-S, as secp::ecdsa_verify requires (s and n - s both
+    // satisfy the verification equation, so a high-S input is a malleated signature)
+    if (!DER && ok && sc_is_high(s)) ok = false;
     ok = ok && !fe_is_zero(r) && !fe_is_zero(s);
     if (!ok) {
 #pragma unroll

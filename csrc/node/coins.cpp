@@ -1,4 +1,6 @@
 #include "node/coins.h"
+
+#include <algorithm>
 #include "util/memusage.h"
 #include "keys/key.h"
 #include "secp256k1/secp256k1.h"
@@ -137,9 +139,18 @@ SaltedOutpointHasher::SaltedOutpointHasher() {
 CCoinsViewCache::CCoinsViewCache(CCoinsView* b) : CCoinsViewBacked(b) {}
 
 size_t CCoinsViewCache::DynamicMemoryUsage() const {
-    // hash-table nodes and buckets plus the scripts' heap buffers (reference coins.cpp)
+    // hash-table nodes and buckets plus the scripts' heap buffers (reference coins.cpp). The
+    // nodes live in each shard's NodeArena, which keeps its chunks (and the free-list slack in
+    // them) after entries are erased or the cache is flushed: the node share is whichever is
+    // larger, the live nodes' estimate or the chunk bytes the arena holds, so -dbcache sees
+    // the memory the process really keeps.
     size_t n = CachedCoinsUsage();
-    for (unsigned s = 0; s < CCoinsMap::SHARDS; s++) n += memusage::DynamicUsage(cacheCoins.shard(s));
+    for (unsigned s = 0; s < CCoinsMap::SHARDS; s++) {
+        const auto& sh = cacheCoins.shard(s);
+        const size_t buckets = memusage::MallocUsage(sizeof(void*) * sh.bucket_count());
+        const size_t nodes = memusage::DynamicUsage(sh) - buckets;
+        n += buckets + std::max(nodes, sh.get_allocator().ArenaBytes());
+    }
     return n;
 }
 

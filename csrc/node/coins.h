@@ -236,8 +236,14 @@ public:
         return n;
     }
     bool empty() const { return size() == 0; }
+    // Empties every shard and hands its node arena back to the system: the shard is swapped
+    // with a fresh one (the allocators travel with the swap), so the old arena's chunks go
+    // with the temporary instead of staying behind as free-list slack.
     void clear() {
-        for (Shard& s : shards) s.clear();
+        for (Shard& s : shards) {
+            Shard fresh;
+            s.swap(fresh);
+        }
     }
     // room for n entries spread over the shards (with slack for an uneven split)
     void reserve(size_t n) {

@@ -748,14 +748,15 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         }
     }
     // BIP30 (exceptions for the two historic duplicate coinbases; moot after BIP34 block)
-    bool fEnforceBIP30 =
-        (!pindex->phashBlock) ||
-        !((pindex->nHeight == 91842 &&
-           pindex->GetBlockHash() == uint256S("0x00000000000a4d0a398161ffc163c503763b1f4360639393e0e4c8e300e0caec")) ||
-          (pindex->nHeight == 91880 &&
-           pindex->GetBlockHash() == uint256S("0x00000000000743f190a18c5577a3c2d2a1f610ae9601ac046a38084ccb7cd721")));
+    const bool fBIP30Exception =
+        pindex->phashBlock &&
+        ((pindex->nHeight == 91842 &&
+          pindex->GetBlockHash() == uint256S("0x00000000000a4d0a398161ffc163c503763b1f4360639393e0e4c8e300e0caec")) ||
+         (pindex->nHeight == 91880 &&
+          pindex->GetBlockHash() == uint256S("0x00000000000743f190a18c5577a3c2d2a1f610ae9601ac046a38084ccb7cd721")));
     const CBlockIndex* pindexBIP34height = pindex->pprev->GetAncestor(cp.BIP34Height);
-    fEnforceBIP30 = fEnforceBIP30 && (!pindexBIP34height || !(pindexBIP34height->GetBlockHash() == cp.BIP34Hash));
+    const bool fEnforceBIP30 =
+        !fBIP30Exception && (!pindexBIP34height || !(pindexBIP34height->GetBlockHash() == cp.BIP34Hash));
     int nLockTimeFlags = 0;
     if (VersionBitsState(pindex->pprev, cp, Consensus::DEPLOYMENT_CSV, versionbitscache) == THRESHOLD_ACTIVE)
         nLockTimeFlags |= LOCKTIME_VERIFY_SEQUENCE;
@@ -879,7 +880,10 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // Any failure, or an unusual overlap of the view with the block's own outputs, runs the
     // serial pass below instead, which yields the reference's exact reject reason.
     bool fastDone = false;
-    if (fEnforceBIP30 && opts.parallelUtxoMinTx > 0 && ntx >= opts.parallelUtxoMinTx && maxJobs > 0) {
+    // Taken whenever the block is not one of the two historic BIP30 exceptions: with BIP30
+    // enforced the prefetch above has checked every output; after the BIP34 block txids are
+    // unique and, like the serial pass's AddCoins, the output adds assume no overwrite.
+    if (!fBIP30Exception && opts.parallelUtxoMinTx > 0 && ntx >= opts.parallelUtxoMinTx && maxJobs > 0) {
         int64_t tSub = GetTimeMicros();
         auto sub = [&](ConnectPhase ph) {
             const int64_t t = GetTimeMicros();

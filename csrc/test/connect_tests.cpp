@@ -6,6 +6,7 @@
 // leaves the same coins and undo data, and that a block it refuses gets the serial pass's exact
 // reject reason.
 #include "test/unittest.h"
+#include "util/sync.h"
 
 #include "node/miner.h"
 #include "node/txdb.h"
@@ -281,4 +282,46 @@ TEST_CASE(blockdecode_tests, parallel_decode_matches_stream) {
     for (unsigned char x : {0xff, 0xff, 0xff, 0x01}) bogus.push_back(x);
     CBlock d;
     CHECK(!DecodeBlock(bogus.data(), bogus.size(), d, &pool));
+}
+
+TEST_CASE(connectblock_tests, parallel_pass_with_bip34_active) {
+    // Mainnet and testnet stop enforcing BIP30 once the BIP34 block is buried (every mainnet
+    // block above 227931). The parallel UTXO pass must still run there: activate BIP34 on this
+    // regtest chain at height 5 (its hash pinned), connect a 64+ transaction block, and check
+    // that the parallel pass took it and agrees with the serial pass.
+    test::TestChain100Setup setup;
+    Chainstate& cs = *setup.node->chainstate;
+    Consensus::Params& cons = const_cast<CChainParams&>(Params()).MutableConsensus();
+    const int savedHeight = cons.BIP34Height;
+    const uint256 savedHash = cons.BIP34Hash;
+    cons.BIP34Height = 5;
+    {
+        std::lock_guard<CCriticalSection> l(cs.cs());
+        cons.BIP34Hash = cs.ActiveChain()[5]->GetBlockHash();
+    }
+    struct Restore {
+        Consensus::Params& c;
+        int h;
+        uint256 hh;
+        ~Restore() {
+            c.BIP34Height = h;
+            c.BIP34Hash = hh;
+        }
+    } restore{cons, savedHeight, savedHash};
+    const CKey& key = setup.coinbaseKey;
+    const CScript spk = P2PK(key);
+    for (int i = 0; i < 3; i++) setup.CreateAndProcessBlock({}, spk);
+    std::vector<CMutableTransaction> txs;
+    const Amount each = (setup.coinbaseTxns[0].vout[0].nValue - 100000) / 80;
+    txs.push_back(Make({{setup.coinbaseTxns[0], 0}}, std::vector<CTxOut>(80, CTxOut(each, spk)), key));
+    const CTransaction fan(txs[0]);
+    for (uint32_t i = 0; i < 70; i++) txs.push_back(Make({{fan, i}}, {CTxOut(each - 1000, spk)}, key));
+    const auto v = Verdicts(cs, Assemble(cs, txs, spk));
+    CHECK_EQ(v.first, std::string("valid"));
+    CHECK_EQ(v.second, std::string("valid"));
+    const int64_t fastBefore = cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO);
+    const CBlock blk = setup.CreateAndProcessBlock(txs, spk);
+    CHECK_EQ(cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO), fastBefore + 1);
+    std::lock_guard<CCriticalSection> l(cs.cs());
+    CHECK(cs.Tip()->GetBlockHash() == blk.GetHash());
 }

@@ -90,6 +90,9 @@ public:
     // the original)
     NodePoolAllocator select_on_container_copy_construction() const { return NodePoolAllocator(); }
 
+    // bytes the arena holds from the system (chunks, live nodes and free-list slack alike)
+    size_t ArenaBytes() const { return arena->ChunkBytes(); }
+
     template <typename U> bool operator==(const NodePoolAllocator<U>& o) const noexcept { return arena == o.arena; }
     template <typename U> bool operator!=(const NodePoolAllocator<U>& o) const noexcept { return arena != o.arena; }
 

@@ -69,6 +69,9 @@ def test_ecdsa_verify_compact_device(native):
         if s > ref.N // 2:
             s = ref.N - s
         ok = True
+        if i % 11 == 7:  # the malleated twin n - s: rejected, as libsecp256k1's verify does
+            s = ref.N - s
+            ok = False
         if i % 7 == 3:  # wrong message
             msg = bytes([msg[0] ^ 1]) + msg[1:]
             ok = False
