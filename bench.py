@@ -74,6 +74,8 @@ def parse(argv=None):
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
     ap.add_argument("--solvers", type=int, default=int(os.environ.get("BCP_EH_SOLVERS", "2")),
                     help="solvers in flight per GPU (each its own stream and buffers)")
+    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("BCP_EH_PIPELINE", "1")),
+                    help="pipeline each batch behind the previous one (generation beside the rounds)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher: ranks rendezvous over gloo, all-reduce, "
                          "report n_gpus; no GPU work and no metric")
@@ -213,7 +215,10 @@ def run(args, world):
     for s in range(args.steps):
         if len(pending) == nsolv:  # this step's solver still holds an older batch
             collect()
-        solvers[s % nsolv].launch(all_states[s])
+        # pipelined behind the previous step's solver: this batch's generation overlaps that
+        # batch's collision rounds (solver.launch(states, after=prev))
+        prev = solvers[(s - 1) % nsolv] if (args.pipeline and s > 0 and nsolv > 1) else None
+        solvers[s % nsolv].launch(all_states[s], prev)
         pending.append((s, solvers[s % nsolv]))
     while pending:
         collect()

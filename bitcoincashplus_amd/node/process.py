@@ -29,6 +29,14 @@ def free_port() -> int:
     return port
 
 
+def _json_default(o):
+    """Decimal amounts travel as JSON numbers (reference authproxy EncodeDecimal)."""
+    import decimal
+    if isinstance(o, decimal.Decimal):
+        return float(o)
+    raise TypeError(f"{type(o).__name__} is not JSON serializable")
+
+
 class RPCProxy:
     """Minimal JSON-RPC-over-HTTP client (reference authproxy.AuthServiceProxy)."""
 
@@ -51,7 +59,7 @@ class RPCProxy:
     def call(self, method, *params, **named):
         self._id += 1
         req = {"version": "1.1", "method": method, "params": named if named else list(params), "id": self._id}
-        status, text = self._post(json.dumps(req))
+        status, text = self._post(json.dumps(req, default=_json_default))
         if status == 401:
             raise RPCError(-1, "authorization failed")
         reply = json.loads(text)

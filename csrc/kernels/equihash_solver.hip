@@ -1243,6 +1243,8 @@ struct EquihashGpuSolver::Impl {
     hipStream_t stream = nullptr;
     hipStream_t gstream = nullptr;                // BCP_EH_PRIO: generation's own low-priority stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evg = nullptr;
+    hipEvent_t ev_gen = nullptr, ev_rounds = nullptr; // this solver's last generation / rounds done (pipelining)
+    const Impl* after = nullptr;                        // Launch(states, prev): the batch to pipeline behind
     DevBuf<bcpk::EhBaseState> d_states;
     DevBuf<uint32_t> d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
     DevBuf<uint64_t> d_cand;
@@ -1361,6 +1363,7 @@ struct EquihashGpuSolver::Impl {
             BCP_HIP_CHECK(hipStreamWaitEvent(gstream, evs, 0));
             gs = gstream;
         }
+        if (after) BCP_HIP_CHECK(hipStreamWaitEvent(gs, after->ev_gen, 0)); // one generation at a time
         constexpr bool reg = bcpk::GenReg<C, C::GNT, C::GHPT>::OK;
         if constexpr (reg) {
             using GR = bcpk::GenReg<C, C::GNT, C::GHPT>;
@@ -1378,16 +1381,16 @@ struct EquihashGpuSolver::Impl {
         else
             hipLaunchKernelGGL((bcpk::eh_gen<C, false>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, gs,
                                d_states.p, r0, d_leaf.p, d_ctr.p);
-        if (gstream) {
-            BCP_HIP_CHECK(hipEventRecord(evg, gstream));
-            BCP_HIP_CHECK(hipStreamWaitEvent(stream, evg, 0));
-        }
+        BCP_HIP_CHECK(hipEventRecord(ev_gen, gs));
+        if (gstream) BCP_HIP_CHECK(hipStreamWaitEvent(stream, ev_gen, 0));
+        if (after) BCP_HIP_CHECK(hipStreamWaitEvent(stream, after->ev_rounds, 0)); // one round chain at a time
         launch_rounds<C>((int)nstates, std::make_integer_sequence<int, C::K>{});
         constexpr int EB = C::L < 64 ? 64 : C::L;
         bcpk::EhStages stages{};
         for (int s = 0; s < C::K; ++s) stages.r[s] = d_rst[s].p;
         hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND * nstates), dim3(EB), 0, stream, d_leaf.p, stages,
                            d_ncand.p, d_cand.p, d_idx.p, d_valid.p, d_nout.p, d_out.p);
+        BCP_HIP_CHECK(hipEventRecord(ev_rounds, stream));
         BCP_HIP_CHECK(hipGetLastError());
         BCP_HIP_CHECK(hipEventRecord(ev1, stream));
         BCP_HIP_CHECK(
@@ -1432,6 +1435,8 @@ EquihashGpuSolver::EquihashGpuSolver(unsigned n, unsigned k, int batch, int devi
     } else {
         BCP_HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
     }
+    BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_gen, hipEventDisableTiming));
+    BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_rounds, hipEventDisableTiming));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev0));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev1));
     dispatch_cfg(n, k, [&](auto c) { impl->alloc<decltype(c)>(); });
@@ -1446,6 +1451,8 @@ EquihashGpuSolver::~EquihashGpuSolver() {
         if (impl->stream) (void)hipStreamDestroy(impl->stream);
         if (impl->gstream) (void)hipStreamSynchronize(impl->gstream), (void)hipStreamDestroy(impl->gstream);
         if (impl->evs) (void)hipEventDestroy(impl->evs);
+        if (impl->ev_gen) (void)hipEventDestroy(impl->ev_gen);
+        if (impl->ev_rounds) (void)hipEventDestroy(impl->ev_rounds);
         if (impl->evg) (void)hipEventDestroy(impl->evg);
     }
 }
@@ -1530,6 +1537,19 @@ void EquihashGpuSolver::Launch(const std::vector<EhBaseState>& states) {
     memcpy(impl->h_states.p, states.data(), states.size() * sizeof(EhBaseState));
     dispatch_cfg(impl->n, impl->k, [&](auto c) { impl->launch<decltype(c)>(states.size()); });
     impl->inflight = (int)states.size();
+}
+
+void EquihashGpuSolver::Launch(const std::vector<EhBaseState>& states, const EquihashGpuSolver& prev) {
+    if (&prev == this) throw std::invalid_argument("EquihashGpuSolver: cannot pipeline behind itself");
+    if (prev.impl->device != impl->device) throw std::invalid_argument("EquihashGpuSolver: pipelined solvers on different devices");
+    impl->after = prev.impl.get();
+    try {
+        Launch(states);
+    } catch (...) {
+        impl->after = nullptr;
+        throw;
+    }
+    impl->after = nullptr;
 }
 
 std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {

@@ -63,6 +63,12 @@ public:
     // Asynchronous split used by the pipelined miner/bench: Launch enqueues the
     // whole sequence on the solver's stream; Collect waits and decodes.
     void Launch(const std::vector<EhBaseState>& states);
+    // The same, pipelined behind `prev` (another solver on the same device whose batch was
+    // launched just before this one): this batch's generation starts once prev's generation is
+    // done, and its collision rounds once prev's rounds are done. Generation (VALU-bound) then
+    // runs beside the previous batch's rounds (LDS/latency-bound) instead of beside another
+    // generation.
+    void Launch(const std::vector<EhBaseState>& states, const EquihashGpuSolver& prev);
     std::vector<std::vector<std::vector<uint32_t>>> Collect();
     const EhGpuStats& Stats() const;
     void SetDebug(bool on);   // collect per-stage bucket statistics (extra D2H copies)

@@ -47,7 +47,13 @@ void bind_gpu(pyb::module_& m) {
                  }
                  return out;
              })
-        .def("launch", [](gpu::EquihashGpuSolver& s, const std::vector<CBlake2b>& sts) { s.Launch(states_from(sts)); })
+        .def(
+            "launch",
+            [](gpu::EquihashGpuSolver& s, const std::vector<CBlake2b>& sts, const gpu::EquihashGpuSolver* after) {
+                if (after) s.Launch(states_from(sts), *after);
+                else s.Launch(states_from(sts));
+            },
+            pyb::arg("states"), pyb::arg("after") = nullptr)
         .def("collect",
              [](gpu::EquihashGpuSolver& s) {
                  std::vector<std::vector<std::vector<uint32_t>>> r;

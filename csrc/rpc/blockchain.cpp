@@ -284,6 +284,7 @@ static UniValue mempoolRelatives(const JSONRPCRequest& req, bool ancestors) {
     NodeContext& n = Node();
     const uint256 hash = ParseHashV(req.params[0], "parameter 1");
     const bool fVerbose = req.params.size() > 1 && !req.params[1].isNull() && req.params[1].get_bool();
+    const int height = n.chainstate->HeightNow(); // before the mempool lock: cs_main comes first
     std::lock_guard<CCriticalSection> l(n.mempool->cs);
     if (!n.mempool->exists(hash)) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Transaction not in mempool");
     auto rel = ancestors ? n.mempool->GetAncestors(hash) : n.mempool->GetDescendants(hash);
@@ -293,7 +294,6 @@ static UniValue mempoolRelatives(const JSONRPCRequest& req, bool ancestors) {
         return o;
     }
     UniValue o(UniValue::VOBJ);
-    const int height = n.chainstate->HeightNow();
     for (const auto* e : rel) o.pushKV(e->GetTx().GetHash().ToString(), entryToJSON(*e, *n.mempool, height));
     return o;
 }

@@ -226,7 +226,10 @@ static UniValue setban(const JSONRPCRequest& req) {
     }
     if (!subNet.IsValid()) ThrowRPC(RPC_CLIENT_INVALID_IP_OR_SUBNET, "Error: Invalid IP/Subnet");
     if (strCommand == "add") {
-        if (c.IsBanned(subNet)) ThrowRPC(RPC_CLIENT_NODE_ALREADY_ADDED, "Error: IP/Subnet already banned");
+        // a single address counts as banned when any banned subnet covers it (reference
+        // src/rpc/net.cpp setban: IsBanned(netAddr) for an address, IsBanned(subNet) for a subnet)
+        if (isSubnet ? c.IsBanned(subNet) : c.IsBanned(netAddr))
+            ThrowRPC(RPC_CLIENT_NODE_ALREADY_ADDED, "Error: IP/Subnet already banned");
         int64_t banTime = 0;
         if (req.params.size() >= 3 && !req.params[2].isNull()) banTime = req.params[2].get_int64();
         bool absolute = false;

@@ -56,7 +56,7 @@ static std::string AccountFromValue(const UniValue& v) {
 
 static CTxDestination ParseDest(const std::string& s) {
     const CTxDestination d = DecodeDestination(s, P());
-    if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin Cash Plus address");
+    if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin address");
     return d;
 }
 
@@ -273,7 +273,7 @@ static UniValue sendmany(const JSONRPCRequest& req) {
     Amount totalAmount = 0;
     for (const std::string& name : sendTo.getKeys()) {
         const CTxDestination d = DecodeDestination(name, P());
-        if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin Cash Plus address: " + name);
+        if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin address: " + name);
         if (seen.count(d)) ThrowRPC(RPC_INVALID_PARAMETER, "Invalid parameter, duplicated address: " + name);
         seen.insert(d);
         const Amount nAmount = AmountFromValue(sendTo[name]);
@@ -718,7 +718,7 @@ static UniValue listunspent(const JSONRPCRequest& req) {
         const UniValue& a = req.params[2].get_array();
         for (size_t i = 0; i < a.size(); i++) {
             const CTxDestination d = DecodeDestination(a[i].get_str(), P());
-            if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin Cash Plus address: " + a[i].get_str());
+            if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin address: " + a[i].get_str());
             if (!dests.insert(d).second) ThrowRPC(RPC_INVALID_PARAMETER, "Invalid parameter, duplicated address: " + a[i].get_str());
         }
     }
@@ -1058,7 +1058,7 @@ static UniValue importaddress(const JSONRPCRequest& req) {
             const std::vector<unsigned char> data(ParseHex(s));
             ImportScript(w, CScript(data.begin(), data.end()), label, fP2SH);
         } else {
-            ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin Cash Plus address or script");
+            ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin address or script");
         }
     }
     if (fRescan) RescanFromGenesis(w);
@@ -1091,7 +1091,7 @@ static UniValue dumpprivkey(const JSONRPCRequest& req) {
     if (req.params.size() != 1) ThrowRPC(RPC_INVALID_PARAMS, "dumpprivkey \"address\"");
     EnsureWalletIsUnlocked(w);
     const CTxDestination d = DecodeDestination(req.params[0].get_str(), P());
-    if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin Cash Plus address");
+    if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin address");
     if (d.type != DestType::KEYID) ThrowRPC(RPC_TYPE_ERROR, "Address does not refer to a key");
     CKey key;
     if (!w.GetKey(CKeyID(d.hash), key))
@@ -1637,7 +1637,7 @@ static UniValue sendwithcoincontrol(const JSONRPCRequest& req) {
     std::set<CTxDestination> seen;
     for (const std::string& name : sendTo.getKeys()) {
         const CTxDestination d = DecodeDestination(name, P());
-        if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin Cash Plus address: " + name);
+        if (!d.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "Invalid Bitcoin address: " + name);
         if (!seen.insert(d).second) ThrowRPC(RPC_INVALID_PARAMETER, "Invalid parameter, duplicated address: " + name);
         const Amount nAmount = AmountFromValue(sendTo[name]);
         if (nAmount <= 0) ThrowRPC(RPC_TYPE_ERROR, "Invalid amount for send");

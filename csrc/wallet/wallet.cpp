@@ -1,4 +1,6 @@
 #include "wallet/wallet.h"
+
+#include <filesystem>
 #include "node/ui_interface.h"
 #include "consensus/params.h"
 #include "consensus/tx_verify.h"
@@ -265,7 +267,7 @@ static KVOptions WalletStoreOptions() {
 }
 
 CWallet::CWallet(const std::string& name, const std::string& path, bool memoryOnly)
-    : strWalletName(name), db(new KVStore(path, memoryOnly, false, WalletStoreOptions())) {
+    : strWalletName(name), strWalletPath(path), db(new KVStore(path, memoryOnly, false, WalletStoreOptions())) {
     std::lock_guard<std::mutex> l(cs_wallets);
     g_wallets.push_back(this);
 }
@@ -424,17 +426,36 @@ bool CWallet::Load(std::string& err, bool& firstRun) {
     return true;
 }
 
-bool CWallet::BackupWallet(const std::string& dest) {
+// Copies the wallet store to `dest` (reference CWalletDBWrapper::Backup: a directory
+// destination gets the wallet's file name inside it, and copying onto the live wallet itself
+// fails).
+bool CWallet::BackupWallet(const std::string& destIn) {
+    namespace fs = std::filesystem;
     WalletLock l(*this);
     Flush();
-    KVStore out(dest, false, true);
-    KVBatch b;
-    KVIterator it(db.get());
-    for (it.SeekToFirst(); it.Valid(); it.Next()) {
-        std::string v;
-        if (it.RawValue(v)) b.WriteRaw(it.RawKey(), v);
+    std::error_code ec;
+    fs::path dest(destIn);
+    if (fs::is_directory(dest, ec) && !fs::exists(dest / "MANIFEST", ec)) dest /= strWalletName;
+    if (!strWalletPath.empty()) {
+        const fs::path a = fs::weakly_canonical(dest, ec), b = fs::weakly_canonical(fs::path(strWalletPath), ec);
+        if (a == b) {
+            LogPrintf("BackupWallet: cannot back the wallet up onto itself (%s)\n", destIn.c_str());
+            return false;
+        }
     }
-    return out.WriteBatch(b, true);
+    try {
+        KVStore out(dest.string(), false, true);
+        KVBatch b;
+        KVIterator it(db.get());
+        for (it.SeekToFirst(); it.Valid(); it.Next()) {
+            std::string v;
+            if (it.RawValue(v)) b.WriteRaw(it.RawKey(), v);
+        }
+        return out.WriteBatch(b, true);
+    } catch (const std::exception& e) {
+        LogPrintf("BackupWallet: %s\n", e.what());
+        return false;
+    }
 }
 
 void CWallet::UpdateTimeFirstKey(int64_t nCreateTime) {

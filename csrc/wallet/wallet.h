@@ -440,6 +440,7 @@ private:
     CPubKey DeriveNewChildKey(CKeyMetadata& metadata, CKey& secret);
 
     std::string strWalletName;
+    std::string strWalletPath; // the store's directory (BackupWallet refuses to write onto it)
     uint64_t nLastFlushBytes = 0;
     std::unique_ptr<KVStore> db;
     std::map<unsigned int, CMasterKey> mapMasterKeys;

@@ -6,6 +6,8 @@ Each build is loaded through BCP_NATIVE_PATH (bitcoincashplus_amd/_native.py) in
 process; runs alternate A, B, A, B, ... so clock/thermal drift hits every build alike.
 Prints one JSON line per run and a summary per build: median, min, max and the relative
 spread ((max - min) / median), so a difference smaller than the spread is read as noise.
+A build may carry environment settings for its runs: path.so@NAME=VALUE,NAME2=VALUE2
+(e.g. the same build with BCP_EH_PIPELINE=0 and =1).
 """
 import argparse
 import json
@@ -27,7 +29,11 @@ def main():
     res = {b: [] for b in a.builds}
     for r in range(a.reps):
         for b in a.builds:
-            env = dict(os.environ, BCP_NATIVE_PATH=os.path.abspath(b))
+            path, _, extra = b.partition("@")
+            env = dict(os.environ, BCP_NATIVE_PATH=os.path.abspath(path))
+            for kv in filter(None, extra.split(",")):
+                k, _, v = kv.partition("=")
+                env[k] = v
             out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(a.steps),
                                   "--warmup", str(a.warmup)], env=env, capture_output=True, text=True,
                                  timeout=300)
