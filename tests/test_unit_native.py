@@ -29,7 +29,8 @@ def test_suite_inventory():
         "policyestimator_tests", "txvalidationcache_tests", "addrman_tests", "crypto_tests", "dos_tests", "checkqueue_tests",
         "getarg_tests", "util_tests", "timedata_tests", "netbase_tests", "serialize_tests", "streams_tests",
         "compress_tests", "rpc_tests", "skiplist_tests", "wallet_tests", "walletdb_tests", "connectblock_tests", "blockdecode_tests", "net_tests", "blockcheck_tests",
-        "validation_tests", "modinv_tests", "derlax_tests",
+        "validation_tests", "modinv_tests", "derlax_tests", "scriptnum_tests", "script_sighashtype_tests",
+        "multisig_tests", "shardplan_tests",
     ]:
         assert s in SUITES, s
 
