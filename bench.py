@@ -74,7 +74,7 @@ def parse(argv=None):
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
     ap.add_argument("--solvers", type=int, default=int(os.environ.get("BCP_EH_SOLVERS", "2")),
                     help="solvers in flight per GPU (each its own stream and buffers)")
-    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("BCP_EH_PIPELINE", "1")),
+    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("BCP_EH_PIPELINE", "0")),
                     help="pipeline each batch behind the previous one (generation beside the rounds)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher: ranks rendezvous over gloo, all-reduce, "

@@ -80,6 +80,9 @@
 #ifndef BCP_EH_PRIO // 1: generation runs on a low-priority stream of its own, the rounds on a high-priority one
 #define BCP_EH_PRIO 0 //  (so one solver's generation fills the CUs beside the other solver's resident rounds)
 #endif
+#ifndef BCP_EH_PRUNE_FROM // first round that drops pairs sharing a parent (reads the parent words with the rows)
+#define BCP_EH_PRUNE_FROM 2
+#endif
 #ifndef BCP_EH_GEN_PERSIST // > 0: register generation runs this many persistent workgroups per CU
 #define BCP_EH_GEN_PERSIST 0 //  (each loops over work items) instead of one workgroup per item
 #endif
@@ -586,7 +589,7 @@ template <class C> constexpr int round_lds(int stage, bool prune) {
 }
 // Depth-1 duplicate pruning wherever its parent words fit next to the full rows.
 template <class C> constexpr bool round_prunes(int stage) {
-    return stage >= 2 && round_lds<C>(stage, true) <= C::LDS_BUDGET;
+    return stage >= BCP_EH_PRUNE_FROM && round_lds<C>(stage, true) <= C::LDS_BUDGET;
 }
 
 // STAGE < K: collision round producing stage-STAGE rows. STAGE == K: final round.

@@ -1866,6 +1866,9 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
                          gArgs.GetArg("-mempoolexpiry", (int64_t)DEFAULT_MEMPOOL_EXPIRY) * 60 * 60);
     }
     if (mempool) mempool->check(pcoinsTip.get(), chainActive.Height() + 1);
+    // a new best chain re-evaluates the fork warnings (an invalid branch that is no longer 6+
+    // blocks ahead clears them and leaves safe mode); reference validation.cpp:2758-2762
+    if (!fInvalidFound) CheckForkWarningConditions();
     return true;
 }
 

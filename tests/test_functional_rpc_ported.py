@@ -557,6 +557,7 @@ def test_p2p_feefilter(tmp_path):
     try:
         connect(n1, n0)
         n1.rpc.generate(101)  # out of IBD, spendable coins on node1
+        sync_blocks([n0, n1])
         n0.rpc.generate(101)
         sync_blocks([n0, n1])
         peer = InvPeer().connect("127.0.0.1", n0.p2p_port)
