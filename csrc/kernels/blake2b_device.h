@@ -201,6 +201,73 @@ __device__ __forceinline__ void eh_hash_g_hdr(const EhBaseState& bs, uint32_t g,
     blake2b_compress_final(bs.h, m, bs.t0, out);
 }
 
+// The header specialisation split at its first g-dependent operation. In round 0 only G0's
+// second half reads m[1] (which carries g << 32); G1..G3 and G0's first half depend on the
+// base state alone. eh_hdr_round0_uniform computes that g-independent prefix once (per
+// workgroup) - the 16 state words with v0 already holding a + b + (m[1] without g) - and
+// eh_hash_g_hdr_from finishes each hash from it: the add of g << 32 only touches the high word.
+__device__ __forceinline__ void eh_hdr_round0_uniform(const EhBaseState& bs, uint64_t P[16]) {
+    const uint64_t IV0 = 0x6a09e667f3bcc908ULL, IV1 = 0xbb67ae8584caa73bULL, IV2 = 0x3c6ef372fe94f82bULL,
+                   IV3 = 0xa54ff53a5f1d36f1ULL, IV4 = 0x510e527fade682d1ULL, IV5 = 0x9b05688c2b3e6c1fULL,
+                   IV6 = 0x1f83d9abfb41bd6bULL, IV7 = 0x5be0cd19137e2179ULL;
+    uint64_t v0 = bs.h[0], v1 = bs.h[1], v2 = bs.h[2], v3 = bs.h[3], v4 = bs.h[4], v5 = bs.h[5], v6 = bs.h[6],
+             v7 = bs.h[7];
+    uint64_t v8 = IV0, v9 = IV1, v10 = IV2, v11 = IV3, v12 = IV4 ^ bs.t0, v13 = IV5, v14 = ~IV6, v15 = IV7;
+    // G0, first half (message word m[0])
+    v0 = v0 + v4 + bs.m[0];
+    v12 = rotr64(v12 ^ v0, 32);
+    v8 = v8 + v12;
+    v4 = rotr64(v4 ^ v8, 24);
+    v0 = v0 + v4 + bs.m[1]; // the g-independent part of G0's second add
+    // G1..G3 (message words 2..7 are zero)
+    BCPK_B2G(v1, v5, v9, v13, 0, 0);
+    BCPK_B2G(v2, v6, v10, v14, 0, 0);
+    BCPK_B2G(v3, v7, v11, v15, 0, 0);
+    P[0] = v0, P[1] = v1, P[2] = v2, P[3] = v3, P[4] = v4, P[5] = v5, P[6] = v6, P[7] = v7;
+    P[8] = v8, P[9] = v9, P[10] = v10, P[11] = v11, P[12] = v12, P[13] = v13, P[14] = v14, P[15] = v15;
+}
+
+__device__ __forceinline__ void eh_hash_g_hdr_from(const uint64_t P[16], const EhBaseState& bs, uint32_t g,
+                                                   uint64_t out[8]) {
+    uint64_t v0 = P[0], v1 = P[1], v2 = P[2], v3 = P[3], v4 = P[4], v5 = P[5], v6 = P[6], v7 = P[7];
+    uint64_t v8 = P[8], v9 = P[9], v10 = P[10], v11 = P[11], v12 = P[12], v13 = P[13], v14 = P[14], v15 = P[15];
+    const uint64_t m0 = bs.m[0], m1 = bs.m[1] | ((uint64_t)g << 32);
+    // G0, second half: a += g << 32 (high word only), then the rest of the G
+    v0 = ((uint64_t)((uint32_t)(v0 >> 32) + g) << 32) | (uint32_t)v0;
+    v12 = rotr64(v12 ^ v0, 16);
+    v8 = add64(v8, v12);
+    v4 = rotr64(v4 ^ v8, 63);
+    // round 0, diagonal step (message words 8..15 are zero)
+    BCPK_B2G(v0, v5, v10, v15, 0, 0);
+    BCPK_B2G(v1, v6, v11, v12, 0, 0);
+    BCPK_B2G(v2, v7, v8, v13, 0, 0);
+    BCPK_B2G(v3, v4, v9, v14, 0, 0);
+    uint64_t m[16];
+    m[0] = m0;
+    m[1] = m1;
+#pragma unroll
+    for (int i = 2; i < 16; ++i) m[i] = 0;
+#pragma unroll
+    for (int r = 1; r < 12; ++r) {
+        BCPK_B2G(v0, v4, v8, v12, m[kB2Sigma[r][0]], m[kB2Sigma[r][1]]);
+        BCPK_B2G(v1, v5, v9, v13, m[kB2Sigma[r][2]], m[kB2Sigma[r][3]]);
+        BCPK_B2G(v2, v6, v10, v14, m[kB2Sigma[r][4]], m[kB2Sigma[r][5]]);
+        BCPK_B2G(v3, v7, v11, v15, m[kB2Sigma[r][6]], m[kB2Sigma[r][7]]);
+        BCPK_B2G(v0, v5, v10, v15, m[kB2Sigma[r][8]], m[kB2Sigma[r][9]]);
+        BCPK_B2G(v1, v6, v11, v12, m[kB2Sigma[r][10]], m[kB2Sigma[r][11]]);
+        BCPK_B2G(v2, v7, v8, v13, m[kB2Sigma[r][12]], m[kB2Sigma[r][13]]);
+        BCPK_B2G(v3, v4, v9, v14, m[kB2Sigma[r][14]], m[kB2Sigma[r][15]]);
+    }
+    out[0] = bs.h[0] ^ v0 ^ v8;
+    out[1] = bs.h[1] ^ v1 ^ v9;
+    out[2] = bs.h[2] ^ v2 ^ v10;
+    out[3] = bs.h[3] ^ v3 ^ v11;
+    out[4] = bs.h[4] ^ v4 ^ v12;
+    out[5] = bs.h[5] ^ v5 ^ v13;
+    out[6] = bs.h[6] ^ v6 ^ v14;
+    out[7] = bs.h[7] ^ v7 ^ v15;
+}
+
 // Byte k (0-based) of the digest held in 8 little-endian words.
 __device__ __forceinline__ uint32_t digest_byte(const uint64_t h[8], int k) {
     return (uint32_t)(h[k >> 3] >> ((k & 7) * 8)) & 0xff;

@@ -80,8 +80,11 @@
 #ifndef BCP_EH_PRIO // 1: generation runs on a low-priority stream of its own, the rounds on a high-priority one
 #define BCP_EH_PRIO 0 //  (so one solver's generation fills the CUs beside the other solver's resident rounds)
 #endif
-#ifndef BCP_EH_PRUNE_FROM // first round that drops pairs sharing a parent (reads the parent words with the rows)
-#define BCP_EH_PRUNE_FROM 2
+#ifndef BCP_EH_PRUNE_FROM // first round that drops pairs sharing a parent (reads the parent words with the rows).
+#define BCP_EH_PRUNE_FROM 9 //  9 = the final round only: +4.2% Sol/s over 2 at the same recall (profiles/equihash_r5.md)
+#endif
+#ifndef BCP_EH_GEN_R0 // 1: the header generation starts each hash from the workgroup's precomputed
+#define BCP_EH_GEN_R0 1 //  g-independent part of BLAKE2b round 0 (G1..G3 and half of G0)
 #endif
 #ifndef BCP_EH_GEN_PERSIST // > 0: register generation runs this many persistent workgroups per CU
 #define BCP_EH_GEN_PERSIST 0 //  (each loops over work items) instead of one workgroup per item
@@ -468,6 +471,7 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     constexpr int SW = (C::N + 31) / 32 + 1;
     constexpr uint32_t OCAP = C::cap(1);
     __shared__ uint32_t hist[C::NB], base[C::NB];
+    __shared__ uint64_t r0p[HDR && BCP_EH_GEN_R0 ? 16 : 1]; // the nonce's g-independent round-0 prefix
     const int tid = threadIdx.x;
     // work item b = (nonce, gw); a persistent grid (gridDim.x < items, a multiple of 8) keeps every
     // item of a workgroup on that workgroup's XCD
@@ -482,6 +486,14 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     if (b != (int)blockIdx.x) __syncthreads(); // the previous item's scatter has read base[]
     const EhBaseState& bs = states[nonce];
     for (int i = tid; i < C::NB; i += NTG) hist[i] = 0;
+    if constexpr (HDR && BCP_EH_GEN_R0) {
+        if (tid == 0) {
+            uint64_t P[16];
+            eh_hdr_round0_uniform(bs, P);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) r0p[i] = P[i];
+        }
+    }
     __syncthreads();
     const uint32_t r0 = (uint32_t)gw * G::RPW;
     const uint32_t g0 = r0 / C::IPH;
@@ -491,8 +503,16 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     for (int hh = 0; hh < HPT; ++hh) {
         const uint32_t g = g0 + hh * NTG + tid;
         uint64_t h[8];
-        if constexpr (HDR) eh_hash_g_hdr(bs, g, h);
-        else eh_hash_g(bs, g, h);
+        if constexpr (HDR && BCP_EH_GEN_R0) {
+            uint64_t P[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) P[i] = r0p[i];
+            eh_hash_g_hdr_from(P, bs, g, h);
+        } else if constexpr (HDR) {
+            eh_hash_g_hdr(bs, g, h);
+        } else {
+            eh_hash_g(bs, g, h);
+        }
 #pragma unroll
         for (int s = 0; s < C::IPH; ++s) {
             uint32_t S[SW];

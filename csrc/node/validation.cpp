@@ -614,11 +614,13 @@ bool Chainstate::ProcessNewBlock(const std::shared_ptr<const CBlock>& pblock, bo
         CBlockIndex* pindex = nullptr;
         if (fNewBlock) *fNewBlock = false;
         CValidationState state;
+        const int64_t tAccept = GetTimeMicros();
         // the expensive context-free checks (Equihash, merkle) run before taking cs_main
         bool ret = CheckBlock(*pblock, state);
         std::lock_guard<CCriticalSection> l(cs_main);
         if (ret) ret = AcceptBlock(pblock, state, &pindex, fForceProcessing, nullptr, fNewBlock);
         CheckBlockIndex();
+        phaseMicros[PH_ACCEPT].fetch_add(GetTimeMicros() - tAccept, std::memory_order_relaxed);
         if (!ret) {
             GetMainSignals().BlockChecked(*pblock, state);
             if (stateOut) *stateOut = state;
@@ -1825,7 +1827,10 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
             // several blocks in a row: connect them through the pipeline, then let the caller
             // publish the new tip (one step per batch instead of one per block)
             const std::vector<CBlockIndex*> chain(vpindexToConnect.rbegin(), vpindexToConnect.rend());
-            if (!ConnectTipsPipelined(state, chain, pblock, trace)) {
+            const int64_t tTip = GetTimeMicros();
+            const bool tipsOk = ConnectTipsPipelined(state, chain, pblock, trace);
+            phaseMicros[PH_ABC_TIP].fetch_add(GetTimeMicros() - tTip, std::memory_order_relaxed);
+            if (!tipsOk) {
                 if (state.IsInvalid()) {
                     if (!state.CorruptionPossible()) InvalidChainFound(vpindexToConnect.front());
                     CheckForkWarningConditionsOnNewFork(vpindexToConnect.back());
@@ -1840,8 +1845,11 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
         }
         for (auto it = vpindexToConnect.rbegin(); it != vpindexToConnect.rend(); ++it) {
             CBlockIndex* pindexConnect = *it;
-            if (!ConnectTip(state, pindexConnect, pindexConnect == pindexMostWork ? pblock : std::shared_ptr<const CBlock>(),
-                            trace)) {
+            const int64_t tTip = GetTimeMicros();
+            const bool tipOk = ConnectTip(state, pindexConnect,
+                                          pindexConnect == pindexMostWork ? pblock : std::shared_ptr<const CBlock>(), trace);
+            phaseMicros[PH_ABC_TIP].fetch_add(GetTimeMicros() - tTip, std::memory_order_relaxed);
+            if (!tipOk) {
                 if (state.IsInvalid()) {
                     if (!state.CorruptionPossible()) InvalidChainFound(vpindexToConnect.front());
                     CheckForkWarningConditionsOnNewFork(vpindexToConnect.back());
@@ -1875,6 +1883,12 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
 bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<const CBlock> pblock) {
     CBlockIndex* pindexMostWork = nullptr;
     CBlockIndex* pindexNewTip = nullptr;
+    int64_t tPh = GetTimeMicros();
+    auto phase = [&](ConnectPhase ph) {
+        const int64_t t = GetTimeMicros();
+        phaseMicros[ph].fetch_add(t - tPh, std::memory_order_relaxed);
+        tPh = t;
+    };
     do {
         const CBlockIndex* pindexFork;
         bool fInitialDownload;
@@ -1883,6 +1897,7 @@ bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<cons
             std::lock_guard<CCriticalSection> l(cs_main);
             CBlockIndex* pindexOldTip = chainActive.Tip();
             if (pindexMostWork == nullptr) pindexMostWork = FindMostWorkChain();
+            phase(PH_ABC_FIND);
             if (pindexMostWork == nullptr || pindexMostWork == chainActive.Tip()) return true;
             bool fInvalidFound = false;
             std::shared_ptr<const CBlock> nullBlockPtr;
@@ -1896,22 +1911,28 @@ bool Chainstate::ActivateBestChain(CValidationState& state, std::shared_ptr<cons
             pindexNewTip = chainActive.Tip();
             pindexFork = chainActive.FindFork(pindexOldTip);
             fInitialDownload = IsInitialBlockDownload();
+            phase(PH_ABC_STEP);
             for (const auto& pb : trace.blocksConnected) {
                 std::vector<CTransactionRef> conflicted;
                 GetMainSignals().BlockConnected(pb.second, pb.first, conflicted);
             }
+            phase(PH_ABC_SIGNALS);
         }
         // the connected blocks (a 7.5 MB block is ~100k heap objects) are freed on the reaper
         // thread, not between this block and the next (5-10 ms per block in IBD)
         Reaper::Get().Drop(std::move(trace.blocksConnected));
+        phase(PH_ABC_REAP);
         if (pindexFork != pindexNewTip) {
             GetMainSignals().UpdatedBlockTip(pindexNewTip, pindexFork, fInitialDownload);
             uiInterface.NotifyBlockTip(fInitialDownload, pindexNewTip);
         }
+        phase(PH_ABC_NOTIFY);
     } while (pindexNewTip != pindexMostWork);
     CheckBlockIndex(); // (takes cs_main)
-    if (!FlushStateToDisk(state, FLUSH_STATE_PERIODIC)) return false;
-    return true;
+    phase(PH_ABC_CHECKINDEX);
+    const bool flushed = FlushStateToDisk(state, FLUSH_STATE_PERIODIC);
+    phase(PH_ABC_FLUSH);
+    return flushed;
 }
 
 bool Chainstate::PreciousBlock(CValidationState& state, CBlockIndex* pindex) {

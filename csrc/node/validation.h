@@ -214,9 +214,16 @@ public:
     // the script jobs after it, gathering the deferred checks, and the synchronous batch verify.
     // PH_BLOCKS counts connected blocks, PH_FASTUTXO those whose UTXO pass took the parallel path;
     // PH_FU_* split that parallel pass (setup, checks, undo + jobs, view updates; inside PH_UTXO)
+    // PH_ABC_* split ActivateBestChain (reference validation.cpp:2678-2873) around ConnectTip:
+    // FindMostWorkChain, the steps (PH_ABC_TIP: the ConnectTip calls inside them), the
+    // BlockConnected signals, the hand-off of the connected blocks to the reaper, the tip
+    // notifications, CheckBlockIndex and the periodic flush; PH_ACCEPT is AcceptBlock inside
+    // ProcessNewBlock (CheckBlock, contextual checks, the write to disk).
     enum ConnectPhase {
         PH_CHECK, PH_PRECOMPUTE, PH_UTXO, PH_SCRIPTS, PH_COLLECT, PH_BATCH, PH_BLOCKS, PH_FASTUTXO,
-        PH_FU_SETUP, PH_FU_CHECKS, PH_FU_UNDO, PH_FU_APPLY, PH_COUNT
+        PH_FU_SETUP, PH_FU_CHECKS, PH_FU_UNDO, PH_FU_APPLY,
+        PH_ABC_FIND, PH_ABC_STEP, PH_ABC_TIP, PH_ABC_SIGNALS, PH_ABC_REAP, PH_ABC_NOTIFY, PH_ABC_CHECKINDEX,
+        PH_ABC_FLUSH, PH_ACCEPT, PH_COUNT
     };
     int64_t ConnectPhaseMicros(ConnectPhase ph) const { return phaseMicros[ph].load(std::memory_order_relaxed); }
 

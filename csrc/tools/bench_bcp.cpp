@@ -1160,9 +1160,27 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         CValidationState hs;
         if (!cs.ProcessNewBlockHeaders(hdrs, hs)) throw std::runtime_error("bench: headers " + FormatStateMessage(hs));
         for (size_t i = f.run.size(); i-- > 1;) feed(f.run[i]);
+        int64_t ph0[Chainstate::PH_COUNT];
+        for (int k = 0; k < Chainstate::PH_COUNT; k++) ph0[k] = cs.ConnectPhaseMicros((Chainstate::ConnectPhase)k);
         const int64_t t0 = GetTimeMicros();
         feed(f.run[0]);
         const int64_t t1 = GetTimeMicros();
+        {
+            // where the run's time goes around ConnectTip (ActivateBestChain phases, per block)
+            const double nb = (double)f.run.size();
+            auto ms = [&](Chainstate::ConnectPhase k) { return 0.001 * (cs.ConnectPhaseMicros(k) - ph0[k]) / nb; };
+            const double total = 0.001 * (t1 - t0) / nb;
+            const double tip = ms(Chainstate::PH_ABC_TIP);
+            fprintf(stderr,
+                    "# ibd %s pipeline=%d (ms/block): total %.2f = ConnectTip %.2f + outside %.2f [accept %.2f, find %.3f, "
+                    "step-other %.2f, signals %.2f, reap %.2f, notify %.2f, checkindex %.2f, flush %.2f]; "
+                    "inside ConnectTip: checkblock %.2f, prefetch %.2f, utxo %.2f, scripts %.2f, batch %.2f\n",
+                    useGpu ? "GPU" : "CPU", pipeline, total, tip, total - tip, ms(Chainstate::PH_ACCEPT),
+                    ms(Chainstate::PH_ABC_FIND), ms(Chainstate::PH_ABC_STEP) - tip, ms(Chainstate::PH_ABC_SIGNALS),
+                    ms(Chainstate::PH_ABC_REAP), ms(Chainstate::PH_ABC_NOTIFY), ms(Chainstate::PH_ABC_CHECKINDEX),
+                    ms(Chainstate::PH_ABC_FLUSH), ms(Chainstate::PH_CHECK), ms(Chainstate::PH_PRECOMPUTE),
+                    ms(Chainstate::PH_UTXO), ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_BATCH));
+        }
         if (cs.HeightNow() != f.run.size() + f.setup.size()) {
             fprintf(stderr, "IBD run ended at height %d\n", cs.HeightNow());
             exit(1);
