@@ -80,12 +80,16 @@
 #ifndef BCP_EH_PRIO // 1: generation runs on a low-priority stream of its own, the rounds on a high-priority one
 #define BCP_EH_PRIO 0 //  (so one solver's generation fills the CUs beside the other solver's resident rounds)
 #endif
-#ifndef BCP_EH_PRUNE_FROM // first round that drops pairs sharing a parent (reads the parent words with the rows).
+#ifndef BCP_EH_PRUNE_FROM // first round that drops pairs sharing a parent (reads the parent words with the rows);
+                          // the final round always does.
 #define BCP_EH_PRUNE_FROM 9 //  9 = the final round only: +4.2% Sol/s over 2 at the same recall (profiles/equihash_r5.md)
 #endif
 #ifndef BCP_EH_GEN_R0 // 1: the header generation starts each hash from the workgroup's precomputed
 #define BCP_EH_GEN_R0 1 //  g-independent part of BLAKE2b round 0 (G1..G3 and half of G0)
 #endif
+#ifndef BCP_EH_SORTC // 1 (collision rounds with the key count folded into the commit): rows are written to LDS
+#define BCP_EH_SORTC 0  //  at their key-sorted positions once the key scan is done, so the pair list holds
+#endif                  //  sorted positions (no sidx read while listing); sidx still maps them to slots
 #ifndef BCP_EH_GEN_PERSIST // > 0: register generation runs this many persistent workgroups per CU
 #define BCP_EH_GEN_PERSIST 0 //  (each loops over work items) instead of one workgroup per item
 #endif
@@ -609,7 +613,9 @@ template <class C> constexpr int round_lds(int stage, bool prune) {
 }
 // Depth-1 duplicate pruning wherever its parent words fit next to the full rows.
 template <class C> constexpr bool round_prunes(int stage) {
-    return stage >= BCP_EH_PRUNE_FROM && round_lds<C>(stage, true) <= C::LDS_BUDGET;
+    // (the pruning start was measured on (200,9); the small configurations keep pruning from round 2)
+    constexpr int from = C::K == 9 ? BCP_EH_PRUNE_FROM : 2;
+    return (stage >= from || stage == C::K) && stage >= 2 && round_lds<C>(stage, true) <= C::LDS_BUDGET;
 }
 
 // STAGE < K: collision round producing stage-STAGE rows. STAGE == K: final round.
@@ -656,6 +662,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // pair list, so bend survives the emit and is cleared for the next bucket in D3
     constexpr bool FOLD = BCP_EH_KEY_COMMIT && BCP_EH_PAIRS && !FINAL;
     constexpr bool FGEN = round_fgen<C>(STAGE); // filter pairs while listing them (implies FOLD)
+    constexpr bool SORTC = BCP_EH_SORTC && FOLD && !FGEN; // rows committed at key-sorted LDS positions
     using HT = std::conditional_t<C::H16, uint16_t, uint32_t>;
     __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
     __shared__ uint32_t psig[PRUNE ? CAP : 1];                // the input rows' parent word (j << 16 | i, + d bits)
@@ -813,17 +820,19 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             for (int u = 0; u < RPL; ++u) {
                 const uint32_t r = ot + u * NT;
                 if (r < n) {
-                    if constexpr (WI % 2 == 0) {
+                    if constexpr (!SORTC) {
+                        if constexpr (WI % 2 == 0) {
 #pragma unroll
-                        for (int w = 0; w < WI; w += 2)
-                            *reinterpret_cast<u2v*>(&rows[r * WI + w]) = u2v{nr[u][w], nr[u][w + 1]};
-                    } else {
+                            for (int w = 0; w < WI; w += 2)
+                                *reinterpret_cast<u2v*>(&rows[r * WI + w]) = u2v{nr[u][w], nr[u][w + 1]};
+                        } else {
 #pragma unroll
-                        for (int w = 0; w < WI; ++w) rows[r * WI + w] = nr[u][w];
-                    }
-                    if constexpr (PRUNE) {
-                        psig[r] = nr[u][WI];
-                        if constexpr (!CPI) pdw[r] = (uint16_t)nr[u][WI + 1];
+                            for (int w = 0; w < WI; ++w) rows[r * WI + w] = nr[u][w];
+                        }
+                        if constexpr (PRUNE) {
+                            psig[r] = nr[u][WI];
+                            if constexpr (!CPI) pdw[r] = (uint16_t)nr[u][WI + 1];
+                        }
                     }
                     if constexpr (FOLD) {
                         const uint32_t key = nr[u][0] >> (32 - C::RB);
@@ -857,8 +866,10 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         pf_n = nn;
         const int bn2 = xcd_bucket<C::NB>(blockIdx.x, it + 2, G, nbk);
 #if !BCP_EH_ISSUE_LATE
-        issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
-        fill_next = fill_of(bn2);
+        if constexpr (!SORTC) {
+            issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
+            fill_next = fill_of(bn2);
+        }
 #endif
         __syncthreads();
         EH_STAMP(2);
@@ -884,6 +895,20 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     sidx[pos] = (uint16_t)r;
                     krank[u] = pos;
                     kpairs[u] = min(e - pos - 1, 14u);
+                    if constexpr (SORTC) { // the row goes to its sorted position (its group's rows are adjacent)
+                        if constexpr (WI % 2 == 0) {
+#pragma unroll
+                            for (int w = 0; w < WI; w += 2)
+                                *reinterpret_cast<u2v*>(&rows[pos * WI + w]) = u2v{nr[u][w], nr[u][w + 1]};
+                        } else {
+#pragma unroll
+                            for (int w = 0; w < WI; ++w) rows[pos * WI + w] = nr[u][w];
+                        }
+                        if constexpr (PRUNE) {
+                            psig[pos] = nr[u][WI];
+                            if constexpr (!CPI) pdw[pos] = (uint16_t)nr[u][WI + 1];
+                        }
+                    }
                 }
             }
         } else {
@@ -899,7 +924,12 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         fill_next = fill_of(bn2);
         issue(0, 2 * SLI);
 #else
-        issue(SLI, 2 * SLI);
+        if constexpr (SORTC) { // the prefetch registers are free only now
+            fill_next = fill_of(bn2);
+            issue(0, 2 * SLI);
+        } else {
+            issue(SLI, 2 * SLI);
+        }
 #endif
         __syncthreads();
         EH_STAMP(3);
@@ -949,9 +979,14 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #pragma unroll
             for (int u = 0; u < MPR; ++u) {
                 if (!cpl[u]) continue;
-                const uint32_t p = FOLD ? krank[u] : tid + u * NT, i = FOLD ? tid + u * NT : sidx[p];
+                const uint32_t p = FOLD ? krank[u] : tid + u * NT;
+                const uint32_t i = SORTC ? p : FOLD ? tid + u * NT : sidx[p];
                 for (uint32_t q = p + 1; q <= p + cpl[u]; ++q, ++o) {
                     if (o >= (uint32_t)(MP * NT)) continue;
+                    if constexpr (SORTC) { // both rows by sorted position: no LDS read
+                        plist[o] = (q << 16) | p;
+                        continue;
+                    }
                     if constexpr (FGEN) {
                         // filtered here, on the lane that lists the pair: a dropped pair leaves
                         // a NIL hole in the list
@@ -1081,9 +1116,12 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                 const uint32_t t = tid + u * NT;
 #endif
                 const uint32_t pr = t < np ? spair[t] : 0u;
-                const uint32_t i = pr & 0xffff, j = pr >> 16;
+                const uint32_t si = pr & 0xffff, sj = pr >> 16; // LDS rows
+                // the parents' slots in the input area: the LDS rows themselves, or (SORTC) the
+                // slots the key sort moved them from
+                const uint32_t i = SORTC ? (uint32_t)sidx[si] : si, j = SORTC ? (uint32_t)sidx[sj] : sj;
                 uint32_t x[WI + 1], o[WO];
-                lds_row_xor<WI>(rows, i, j, x);
+                lds_row_xor<WI>(rows, si, sj, x);
                 x[WI - 1] &= ~RMI;
                 x[WI] = 0;
                 const uint32_t b = (x[0] >> (32 - C::DB)) & (C::NB - 1);
