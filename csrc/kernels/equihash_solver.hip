@@ -87,6 +87,12 @@
 #ifndef BCP_EH_GEN_R0 // 1: the header generation starts each hash from the workgroup's precomputed
 #define BCP_EH_GEN_R0 1 //  g-independent part of BLAKE2b round 0 (G1..G3 and half of G0)
 #endif
+#ifndef BCP_EH_MP_LATE // extra pair slots per lane in the late collision rounds (see round_mp)
+#define BCP_EH_MP_LATE 0
+#endif
+#ifndef BCP_EH_MP_LATE_FROM
+#define BCP_EH_MP_LATE_FROM 8
+#endif
 #ifndef BCP_EH_SORTC // 1 (collision rounds with the key count folded into the commit): rows are written to LDS
 #define BCP_EH_SORTC 0  //  at their key-sorted positions once the key scan is done, so the pair list holds
 #endif                  //  sorted positions (no sidx read while listing); sidx still maps them to slots
@@ -590,7 +596,13 @@ template <class C> __host__ __device__ __forceinline__ uint32_t cunpack_d(uint32
 // spair[MP*NT] u32 after it.
 template <class C> constexpr int un_walk_bend(int cap) { return (cap * 2 + 3) / 4 * 4; }
 template <class C> constexpr int un_walk_offp(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
-template <class C> constexpr int round_mp(int stage) { return stage == C::K ? 1 : (C::AREA + C::NT - 1) / C::NT; }
+// Pairs per lane: one lane per LDS row slot, plus BCP_EH_MP_LATE extra from round
+// BCP_EH_MP_LATE_FROM on ((200,9) only): without depth-1 pruning the late rounds' pair lists
+// grow past the row count (duplicate subtrees) and overflowed in round 8.
+template <class C> constexpr int round_mp(int stage) {
+    return stage == C::K ? 1
+                         : (C::AREA + C::NT - 1) / C::NT + (C::K == 9 && stage >= BCP_EH_MP_LATE_FROM ? BCP_EH_MP_LATE : 0);
+}
 template <class C> constexpr int round_un(int stage) {
     const int cap = C::cap(stage);
     if (stage == C::K) return un_walk_offp<C>(cap); // final round: sidx and bend only

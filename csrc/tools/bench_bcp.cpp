@@ -1187,6 +1187,9 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         }
         totalMs += (t1 - t0) / 1000.0;
         iters++;
+        printf("{\"bench\": \"IbdPipelineRun\", \"gpu\": %s, \"pipeline\": %d, \"iter\": %d, \"ms_per_block\": %.2f}\n",
+               useGpu ? "true" : "false", pipeline, iters, (t1 - t0) / 1000.0 / f.run.size());
+        fflush(stdout);
         const std::string cmd = std::string("rm -rf '") + tmpl + "'";
         if (system(cmd.c_str()) != 0) {}
     }
