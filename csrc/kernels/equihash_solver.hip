@@ -88,7 +88,7 @@
 #define BCP_EH_GEN_R0 1 //  g-independent part of BLAKE2b round 0 (G1..G3 and half of G0)
 #endif
 #ifndef BCP_EH_MP_LATE // extra pair slots per lane in the late collision rounds (see round_mp)
-#define BCP_EH_MP_LATE 0
+#define BCP_EH_MP_LATE 1
 #endif
 #ifndef BCP_EH_MP_LATE_FROM
 #define BCP_EH_MP_LATE_FROM 8
@@ -1602,6 +1602,50 @@ std::vector<uint64_t> EquihashGpuSolver::DebugDump() {
     return out;
 }
 size_t EquihashGpuSolver::DeviceBytes() const { return impl->bytes; }
+
+std::vector<uint32_t> EquihashGpuSolver::DebugExpandCorrupt(int mode) {
+    BCP_HIP_CHECK(hipSetDevice(impl->device));
+    BCP_HIP_CHECK(hipStreamSynchronize(impl->stream));
+    Impl& m = *impl;
+    uint32_t nc = 0;
+    BCP_HIP_CHECK(hipMemcpy(&nc, m.d_ncand.p, 4, hipMemcpyDeviceToHost));
+    nc = std::min<uint32_t>(nc, (uint32_t)m.maxcand);
+    if (nc == 0) return {};
+    uint64_t tri = 0;
+    BCP_HIP_CHECK(hipMemcpy(&tri, m.d_cand.p, 8, hipMemcpyDeviceToHost));
+    const size_t st = m.kstages - 1; // the stage the final round read
+    const uint32_t d = (uint32_t)(tri >> 32), i = (uint32_t)tri & 0xffff;
+    uint32_t* slot = m.d_rst[st].p + ((size_t)d * (m.rows / m.nb) + i) * m.slot_words[st] + m.row_words[st];
+    if (mode != 0) {
+        if (m.compact[st]) {
+            // compact word: i | j << 16 with the bucket's bits in the spare high bits of each half
+            uint32_t w = 0;
+            BCP_HIP_CHECK(hipMemcpy(&w, slot, 4, hipMemcpyDeviceToHost));
+            w = mode == 1 ? (w | (m.cp_dhm << m.cp_ib) | (m.cp_dhm << (16 + m.cp_ib))) : (w | ((1u << m.cp_ib) - 1));
+            BCP_HIP_CHECK(hipMemcpy(slot, &w, 4, hipMemcpyHostToDevice));
+        } else {
+            uint32_t w[2];
+            BCP_HIP_CHECK(hipMemcpy(w, slot, 8, hipMemcpyDeviceToHost));
+            if (mode == 1) w[1] = 0xffffu;         // producing bucket far past NB
+            else w[0] = (w[0] & 0xffff0000u) | 0xffffu; // LDS row far past the area
+            BCP_HIP_CHECK(hipMemcpy(slot, w, 8, hipMemcpyHostToDevice));
+        }
+    }
+    BCP_HIP_CHECK(hipMemsetAsync(m.d_nout.p, 0, 4, m.stream));
+    dispatch_cfg(m.n, m.k, [&](auto c) {
+        using C = decltype(c);
+        constexpr int EB = C::L < 64 ? 64 : C::L;
+        bcpk::EhStages stages{};
+        for (int s2 = 0; s2 < C::K; ++s2) stages.r[s2] = m.d_rst[s2].p;
+        hipLaunchKernelGGL((bcpk::eh_expand<C>), dim3(C::MAXCAND), dim3(EB), 0, m.stream, m.d_leaf.p, stages,
+                           m.d_ncand.p, m.d_cand.p, m.d_idx.p, m.d_valid.p, m.d_nout.p, m.d_out.p);
+    });
+    BCP_HIP_CHECK(hipGetLastError());
+    BCP_HIP_CHECK(hipStreamSynchronize(m.stream));
+    std::vector<uint32_t> valid(nc);
+    BCP_HIP_CHECK(hipMemcpy(valid.data(), m.d_valid.p, nc * 4, hipMemcpyDeviceToHost));
+    return valid;
+}
 
 void EquihashGpuSolver::Launch(const std::vector<EhBaseState>& states) {
     if (states.empty() || (int)states.size() > impl->batch) throw std::invalid_argument("bad number of states");

@@ -74,6 +74,11 @@ public:
     void SetDebug(bool on);   // collect per-stage bucket statistics (extra D2H copies)
     void SetStampMode(bool on); // diagnostic: launch phase-timestamped round kernels
     std::vector<uint64_t> DebugDump(); // diagnostic: leaf indices + parent triples of nonce 0
+    // Test hook (after a Solve): re-run the tree expansion of nonce 0's candidates with the first
+    // candidate's left stage-(K-1) parent corrupted - mode 1: bucket out of range, mode 2: LDS
+    // row out of range, 0: untouched. Returns each candidate's valid flag; the expansion must
+    // reject the corrupted candidate without touching memory outside the stage arrays.
+    std::vector<uint32_t> DebugExpandCorrupt(int mode);
     std::vector<std::vector<double>> PhaseCycles(int nonces);
     void ResetStats();
     size_t DeviceBytes() const;

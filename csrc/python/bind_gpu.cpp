@@ -54,6 +54,7 @@ void bind_gpu(pyb::module_& m) {
                 else s.Launch(states_from(sts));
             },
             pyb::arg("states"), pyb::arg("after") = nullptr)
+        .def("debug_expand_corrupt", [](gpu::EquihashGpuSolver& s, int mode) { return s.DebugExpandCorrupt(mode); })
         .def("collect",
              [](gpu::EquihashGpuSolver& s) {
                  std::vector<std::vector<std::vector<uint32_t>>> r;

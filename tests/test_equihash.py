@@ -268,3 +268,30 @@ def test_gpu_miner_search(native, n, k):
     # explicit device list, and an exhausted range reports not found
     r0 = native.eh_search_gpu(n, k, body, nonce0, 0, [0])
     assert not r0["found"] and r0["nonces"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,k", [(96, 5), (200, 9)])
+def test_gpu_expand_rejects_out_of_range_parent(native, n, k):
+    # The tree expansion must reject a candidate whose parent triple points outside the stage
+    # arrays (a bucket >= NB or an LDS row >= AREA) instead of reading through it: the fault of
+    # round 4's timing build (gpurun_out/kt5) came from an unchecked parent. Plant both kinds
+    # in the first candidate's left stage-(K-1) parent and re-run only the expansion.
+    solver = native.EquihashGpuSolver(n, k, 1)
+    for nonce in range(64):
+        st = native.EquihashState(n, k)
+        st.update(header_input(nonce, b"expand-probe"))
+        first = solver.solve([st])
+        base = solver.debug_expand_corrupt(0)
+        if len(base) >= 2:
+            break
+    assert len(base) >= 2, "no nonce with two final-round candidates"
+    for mode in (1, 2):
+        solver.solve([st])  # fresh, uncorrupted stage arrays (candidate order varies per solve)
+        base = solver.debug_expand_corrupt(0)
+        got = solver.debug_expand_corrupt(mode)
+        assert got[0] == 0, (mode, got[:4])  # the corrupted candidate is rejected
+        # no other candidate turns valid (one sharing the corrupted slot may turn invalid too)
+        assert all(g <= b for g, b in zip(got[1:], base[1:]))
+    # and the device is fine afterwards: the same nonce solves to the same solutions
+    assert solver.solve([st]) == first
