@@ -124,6 +124,13 @@ std::vector<uint64_t> ShortTxIdBatch(uint64_t k0, uint64_t k1, const unsigned ch
 std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,
                                       const std::vector<unsigned char>& pub33, int device = -1);
 
+// Batches of at most EcdsaFusedMax() signatures run one fused latency kernel (scalar work,
+// key decompression and the two GLV halves on separate waves, 10 x 26-bit field); larger ones
+// the prep + verify throughput kernels. Process-wide; the default is measured
+// (profiles/ecdsa_r5.md).
+void SetEcdsaFusedMax(size_t n);
+size_t EcdsaFusedMax();
+
 // --------------------------------------------------------------- device-resident entry points
 // The tensor API (bitcoincashplus_amd.ops with torch tensors on the GPU): every pointer is
 // device memory on `device`, the kernels are enqueued on `stream` (a hipStream_t passed as an

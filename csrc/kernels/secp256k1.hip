@@ -24,8 +24,10 @@
 #include "kernels/hip_util.h"
 #include "kernels/der_lax.h"
 #include "kernels/modinv.h"
+#include "kernels/fe10.h"
 #include "secp256k1/secp256k1.h"
 
+#include <atomic>
 #include <chrono>
 #include <cstring>
 #include <mutex>
@@ -495,6 +497,9 @@ constexpr int WG = 128;
 #ifndef BCP_ECDSA_REGULAR // 1: regular window-3 recoding of the GLV halves (uniform additions)
 #define BCP_ECDSA_REGULAR 1
 #endif
+#ifndef BCP_ECDSA_FUSED_MAX // default of EcdsaFusedMax(): batches up to this size run the fused latency kernel
+#define BCP_ECDSA_FUSED_MAX 32768 // fused 2.14 ms vs split 3.03 ms at 32k, split ahead at 64k (profiles/ecdsa_r5.md)
+#endif
 constexpr int WNAF_W = 4;              // odd multiples 1,3,5,7
 constexpr int NPRE = 1 << (WNAF_W - 2); // 4
 
@@ -757,12 +762,8 @@ __device__ __forceinline__ bool sc_is_high(const fe& a) {
 // DER: sig holds [length][72 DER bytes] slots, parsed and low-S normalised here; otherwise
 // 64-byte compact r||s, already normalised by the host.
 template <bool DER>
-__global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs, const unsigned char* __restrict__ msg,
-                                                         const unsigned char* __restrict__ sig,
-                                                         const unsigned char* __restrict__ pub, int n) {
-    const int idx = blockIdx.x * 256 + threadIdx.x;
-    if (idx >= n) return;
-    Job& J = jobs[idx];
+__device__ __forceinline__ void prep_one(Job& J, const unsigned char* __restrict__ msg, const unsigned char* __restrict__ sig,
+                                         const unsigned char* __restrict__ pub, int idx) {
     const unsigned char* pk = pub + (size_t)idx * 33;
     unsigned char c64[64];
     bool parsed = true;
@@ -910,6 +911,15 @@ __global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs,
     J.nwnaf[0] = (unsigned char)wnaf4(J.wnaf[0], m1);
     J.nwnaf[1] = (unsigned char)wnaf4(J.wnaf[1], m2);
 #endif
+}
+
+template <bool DER>
+__global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs, const unsigned char* __restrict__ msg,
+                                                         const unsigned char* __restrict__ sig,
+                                                         const unsigned char* __restrict__ pub, int n) {
+    const int idx = blockIdx.x * 256 + threadIdx.x;
+    if (idx >= n) return;
+    prep_one<DER>(jobs[idx], msg, sig, pub, idx);
 }
 
 __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
@@ -1096,6 +1106,228 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
     out[idx] = (ok && match && J.scalar_ok) ? 1 : 0;
 }
 
+// ------------------------------------------------------------------ fused latency kernel
+// Small batches leave most SIMDs idle and each wave alone on its SIMD, so the verify time is
+// the latency of one lane's chain of field operations. This kernel shortens that chain:
+//   * one 192-thread workgroup per 64 signatures; wave 0 runs the scalar work (prep_one: s^-1,
+//     u1, u2, GLV split, recoding) while waves 1-2 decompress the keys and build the tables,
+//     so the prep and the square root overlap instead of running as two kernels;
+//   * waves 1-2 give each GLV half of u2*Q its own lane (lanes 0-31: k1*Q, 32-63: k2*lambdaQ),
+//     halving the additions on the critical path, while wave 0 runs the u1*G comb;
+//   * the odd multiples Q..7Q are made "affine" without an inversion: they live on the
+//     isomorphic curve scaled by one global z (libsecp256k1's globalz table), whose factor
+//     multiplies the ladder's final z;
+//   * field elements are 10 x 26-bit limbs (fe10.h): products with per-column ILP and
+//     carry-free additions, instead of the 8 x 32 product's serial carry chain.
+// Wave 0 adds the three partial points and checks x(R) == r.
+constexpr int FWG = 192;
+constexpr int FSIG = 64; // signatures per workgroup
+static_assert(BCP_ECDSA_REGULAR, "the fused kernel walks the regular window-3 digits");
+
+using FE = f10::fe;
+using GJ = f10::gej;
+
+__device__ __forceinline__ void f10_load_words(f10::fe& r, const uint32_t* w) {
+    uint32_t t[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) t[k] = w[k];
+    f10::from_words(r, t);
+}
+__device__ __forceinline__ void f10_from_be32(f10::fe& r, const unsigned char* b) {
+    fe t;
+    load_be32(t, b);
+    f10::from_words(r, t.v);
+}
+
+template <bool DER>
+__global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* __restrict__ msg,
+                                                          const unsigned char* __restrict__ sig,
+                                                          const unsigned char* __restrict__ pub,
+                                                          const uint32_t* __restrict__ gtab, uint8_t* __restrict__ out,
+                                                          int n) {
+    __shared__ Job sj[FSIG];
+    __shared__ uint32_t tab[2][NPRE][2][10][64]; // ladder wave, multiple, x|y, limb, lane
+    __shared__ uint32_t res[2][3][10][64];       // ladder wave, x|y|z, limb, lane
+    __shared__ unsigned char rflag[2][64];       // bit 0: point at infinity, bit 1: key decoded
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int base = blockIdx.x * FSIG;
+    GJ acc; // wave 0: u1*G; waves 1-2: one GLV half of u2*Q
+    if (wave == 0) {
+        prep_one<DER>(sj[lane], msg, sig, pub, min(base + lane, n - 1));
+    } else {
+        const int w = wave - 1, slot = w * 32 + (lane & 31), half = lane >> 5;
+        const unsigned char* pk = pub + (size_t)min(base + slot, n - 1) * 33;
+        fe qx8;
+        load_be32(qx8, pk + 1);
+        bool ok = (pk[0] == 2 || pk[0] == 3) && fe_lt_p(qx8);
+        FE qx, qy, t;
+        from_words(qx, qx8.v);
+        sqr(t, qx);
+        mul(t, t, qx);
+        t.n[0] += 7;
+        ok = sqrt_var(qy, t) && ok;
+        normalize(qy);
+        if ((qy.n[0] & 1u) != (uint32_t)(pk[0] & 1)) {
+            neg(qy, qy, 2);
+            norm(qy);
+        }
+        // 2Q, then Q moved to the curve scaled by zeta = z(2Q), where 2Q is affine
+        GJ q1, d;
+        q1.x = qx;
+        q1.y = qy;
+        set_int(q1.z, 1);
+        q1.inf = false;
+        dbl(d, q1);
+        FE z2, z3;
+        sqr(z2, d.z);
+        mul(z3, z2, d.z);
+        GJ P0, P1, P2, P3;
+        mul(P0.x, qx, z2);
+        mul(P0.y, qy, z3);
+        set_int(P0.z, 1);
+        P0.inf = false;
+        FE r0, r1, r2; // z ratios 3Q/Q, 5Q/3Q, 7Q/5Q
+        add_ge(P1, P0, d.x, d.y, &r0);
+        add_ge(P2, P1, d.x, d.y, &r1);
+        add_ge(P3, P2, d.x, d.y, &r2);
+        // every multiple to z(7Q): scale by s = z7 / z_i, (x s^2, y s^3)
+        FE s3, s1;
+        mul(s3, r2, r1);
+        mul(s1, s3, r0);
+        FE bmul; // lambda*Q multiples: x scaled by beta
+        if (half) {
+            uint32_t bw[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) bw[k] = GLV_BETA[k];
+            from_words(bmul, bw);
+        } else {
+            set_int(bmul, 1);
+        }
+        auto put = [&](int m, const GJ& p, const FE* s) {
+            FE x = p.x, y = p.y;
+            if (s) {
+                FE s2, s3c;
+                sqr(s2, *s);
+                mul(s3c, s2, *s);
+                mul(x, p.x, s2);
+                mul(y, p.y, s3c);
+            }
+            mul(x, x, bmul);
+#pragma unroll
+            for (int k = 0; k < 10; k++) {
+                tab[w][m][0][k][lane] = x.n[k];
+                tab[w][m][1][k][lane] = y.n[k];
+            }
+        };
+        put(0, P0, &s1);
+        put(1, P1, &s3);
+        put(2, P2, &r2);
+        put(3, P3, nullptr);
+        mul(acc.z, d.z, P3.z); // the global z, kept in acc.z until the ladder starts
+        acc.inf = !ok;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        // u1*G by the byte-window comb (affine entries of the original curve)
+        const Job& J = sj[lane];
+        acc.inf = true;
+        for (int i = 0; i < 32; i++) {
+            const unsigned byte = J.u1[31 - i];
+            if (!byte) continue;
+            const uint32_t* e = gtab + ((size_t)i * 256 + byte) * 16;
+            FE gx, gy;
+            f10_load_words(gx, e);
+            f10_load_words(gy, e + 8);
+            GJ s;
+            add_ge(s, acc, gx, gy);
+            acc = s;
+        }
+    } else {
+        const int w = wave - 1, slot = w * 32 + (lane & 31), half = lane >> 5;
+        const Job& J = sj[slot];
+        const FE zg = acc.z;
+        const bool ok = !acc.inf;
+        const bool hneg = J.neg[half] != 0;
+        auto add_digit = [&](int dg) {
+            const int m = ((dg < 0 ? -dg : dg) >> 1) & (NPRE - 1);
+            FE tx, ty, ny;
+#pragma unroll
+            for (int k = 0; k < 10; k++) {
+                tx.n[k] = tab[w][m][0][k][lane];
+                ty.n[k] = tab[w][m][1][k][lane];
+            }
+            neg(ny, ty, 2);
+            const bool flip = (dg < 0) != hneg;
+#pragma unroll
+            for (int k = 0; k < 10; k++) ty.n[k] = flip ? ny.n[k] : ty.n[k];
+            GJ s;
+            add_ge(s, acc, tx, ty);
+            acc = s;
+        };
+        acc.inf = true;
+#pragma unroll 1
+        for (int b = REG_DIGITS - 1; b >= 0; b--) {
+            if (b < REG_DIGITS - 1) {
+#pragma unroll 1
+                for (int t = 0; t < 3; t++) {
+                    GJ d;
+                    dbl(d, acc);
+                    acc = d;
+                }
+            }
+            add_digit(wnaf_digit(J, half, b));
+        }
+        if (J.pad[half]) add_digit(-1); // an even half was encoded as k + 1
+        FE z;
+        mul(z, acc.z, zg);
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            res[w][0][k][lane] = acc.x.n[k];
+            res[w][1][k][lane] = acc.y.n[k];
+            res[w][2][k][lane] = z.n[k];
+        }
+        rflag[w][lane] = (unsigned char)((acc.inf ? 1 : 0) | (ok ? 2 : 0));
+    }
+    __syncthreads();
+    if (wave != 0 || base + lane >= n) return;
+    const Job& J = sj[lane];
+    const int w = lane >> 5, l0 = lane & 31;
+    bool ok = (rflag[w][l0] & 2) != 0;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int l = l0 + 32 * h;
+        GJ q;
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            q.x.n[k] = res[w][0][k][l];
+            q.y.n[k] = res[w][1][k][l];
+            q.z.n[k] = res[w][2][k][l];
+        }
+        q.inf = (rflag[w][l] & 1) != 0;
+        GJ s;
+        add_gej(s, acc, q);
+        acc = s;
+    }
+    bool match = false;
+    if (!acc.inf) {
+        FE z2, r, rz, dlt;
+        sqr(z2, acc.z);
+        f10_from_be32(r, J.r);
+        mul(rz, r, z2);
+        sub(dlt, acc.x, rz, 2);
+        norm(dlt);
+        match = is_zero(dlt);
+        if (!match && J.rplusn_ok) {
+            f10_from_be32(r, J.rn);
+            mul(rz, r, z2);
+            sub(dlt, acc.x, rz, 2);
+            norm(dlt);
+            match = is_zero(dlt);
+        }
+    }
+    out[base + lane] = (ok && match && J.scalar_ok) ? 1 : 0;
+}
+
 // Generator comb table, one per HIP device (read-only once built, shared by every lane).
 struct Table {
     std::once_flag once;
@@ -1145,6 +1377,33 @@ void VerifyLane::Ecdsa(const unsigned char* msg32, const unsigned char* sig64, c
         result);
 }
 
+std::atomic<size_t> g_fusedMax{BCP_ECDSA_FUSED_MAX};
+
+namespace {
+// Batches up to EcdsaFusedMax() run the fused latency kernel (no job records); larger ones the
+// prep + verify throughput pair.
+void LaunchVerify(bool der, const unsigned char* dm, const unsigned char* ds, const unsigned char* dp, Job* d_jobs,
+                  const uint32_t* gtab, uint8_t* d_out, size_t n, hipStream_t stream) {
+    if (n <= g_fusedMax.load(std::memory_order_relaxed)) {
+        const dim3 fg((unsigned)((n + FSIG - 1) / FSIG));
+        if (der) hipLaunchKernelGGL(ecdsa_fused_kernel<true>, fg, dim3(FWG), 0, stream, dm, ds, dp, gtab, d_out, (int)n);
+        else hipLaunchKernelGGL(ecdsa_fused_kernel<false>, fg, dim3(FWG), 0, stream, dm, ds, dp, gtab, d_out, (int)n);
+        BCP_HIP_CHECK(hipGetLastError());
+        return;
+    }
+    const dim3 pg((unsigned)((n + 255) / 256));
+    if (der) hipLaunchKernelGGL(ecdsa_prep_kernel<true>, pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
+    else hipLaunchKernelGGL(ecdsa_prep_kernel<false>, pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, stream, d_jobs, gtab,
+                       d_out, (int)n);
+    BCP_HIP_CHECK(hipGetLastError());
+}
+} // namespace
+
+void SetEcdsaFusedMax(size_t n) { g_fusedMax.store(n, std::memory_order_relaxed); }
+size_t EcdsaFusedMax() { return g_fusedMax.load(std::memory_order_relaxed); }
+
 namespace {
 // Shared by EcdsaFill (compact sigs, sigBytes 64) and EcdsaDerFill (DER slots): staging is
 // msg n x 32 | sig n x sigBytes | pub n x 33, one H2D copy, prep + verify, one D2H copy.
@@ -1165,14 +1424,8 @@ void LaneEcdsa(LaneState& L, size_t n, size_t sigBytes,
     Job* d_jobs = reinterpret_cast<Job*>(L.Dev(1, n * sizeof(Job)));
     uint8_t* d_out = L.Dev(2, n);
     BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, bytes, hipMemcpyHostToDevice, L.stream));
-    const dim3 pg((unsigned)((n + 255) / 256));
     const unsigned char *dm = d_in, *ds = d_in + n * 32, *dp = d_in + n * (32 + sigBytes);
-    if (sigBytes == 64) hipLaunchKernelGGL(ecdsa_prep_kernel<false>, pg, dim3(256), 0, L.stream, d_jobs, dm, ds, dp, (int)n);
-    else hipLaunchKernelGGL(ecdsa_prep_kernel<true>, pg, dim3(256), 0, L.stream, d_jobs, dm, ds, dp, (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    const int grid = (int)((n + WG - 1) / WG);
-    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3(grid), dim3(WG), 0, L.stream, d_jobs, tb.d_gtab, d_out, (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
+    LaunchVerify(sigBytes != 64, dm, ds, dp, d_jobs, tb.d_gtab, d_out, n, L.stream);
     BCP_HIP_CHECK(hipMemcpyAsync(h_out, d_out, n, hipMemcpyDeviceToHost, L.stream));
     BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
     memcpy(result, h_out, n);
@@ -1204,14 +1457,9 @@ void EcdsaVerifyDevice(const void* msg32, const void* sig64, const void* pub33, 
     Table& tb = T(ds.device);
     std::call_once(tb.once, [&] { InitTable(tb); });
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    Job* d_jobs = static_cast<Job*>(jobs);
-    hipLaunchKernelGGL(ecdsa_prep_kernel<false>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, d_jobs,
-                       static_cast<const unsigned char*>(msg32), static_cast<const unsigned char*>(sig64),
-                       static_cast<const unsigned char*>(pub33), (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, s, d_jobs, tb.d_gtab,
-                       static_cast<uint8_t*>(result), (int)n);
-    BCP_HIP_CHECK(hipGetLastError());
+    LaunchVerify(false, static_cast<const unsigned char*>(msg32), static_cast<const unsigned char*>(sig64),
+                 static_cast<const unsigned char*>(pub33), static_cast<Job*>(jobs), tb.d_gtab,
+                 static_cast<uint8_t*>(result), n, s);
 }
 
 std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, const std::vector<unsigned char>& sig64,

@@ -53,7 +53,7 @@ std::string HelpMessage() {
         {"-dbcache=<n>", "Set database cache size in megabytes (default: 450)"},
         {"-par=<n>", "Number of script verification threads (0 = auto)"},
         {"-gpu=<0|1>", "Use the MI355X for batched ECDSA / Equihash verification and mining (default: 1)"},
-        {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 512)"},
+        {"-gpusigthreshold=<n>", "Minimum signatures per block routed to the GPU verifier (default: 128)"},
         {"-gpushortidthreshold=<n>", "Smallest mempool whose compact-block short ids are computed on the GPU (default: 16384)"},
         {"-gpudevices=<list>", "Comma-separated GPU indices the built-in Equihash miner runs on, one host thread per device (default: all visible)"},
         {"-gpuvalidationdevices=<list>", "Comma-separated GPU indices that verify block signatures and header solutions, one high-priority stream, service thread and host-fill worker group each; batches are sharded across them. When set, the built-in miner leaves these devices alone if others are available (default: every visible device, two lanes each)"},

@@ -52,9 +52,11 @@ struct SigVerifyStats {
 };
 
 // Smallest batch sent to the GPU (-gpusigthreshold). Below it the CPU pool is faster:
-// profiles/ecdsa_r2_regular.md measures the crossover on MI355X (between 256 and 512 signatures
-// with the regular-recoding verify kernel; it was 1024 before, profiles/ecdsa_crossover.md).
-static const size_t DEFAULT_GPU_SIG_THRESHOLD = 512;
+// profiles/ecdsa_r5.md measures the crossover on MI355X. With the fused latency kernel a batch
+// of up to 8192 signatures takes 0.86-0.98 ms end to end; the 16-thread pool's best rate
+// (139k sig/s) needs 0.92 ms for 128. (It was 512 with the 2.6 ms split kernels,
+// profiles/ecdsa_r2_regular.md, and 1024 before that.)
+static const size_t DEFAULT_GPU_SIG_THRESHOLD = 128;
 // Consecutive device failures after which the GPU signature path is turned off.
 static const int MAX_GPU_SIG_FAILURES = 3;
 

@@ -216,6 +216,9 @@ void bind_gpu(pyb::module_& m) {
         pyb::arg("k0"), pyb::arg("k1"), pyb::arg("in_ptr"), pyb::arg("out_ptr"), pyb::arg("n"), pyb::arg("device"),
         pyb::arg("stream"));
     m.def("ecdsa_job_bytes", &gpu::EcdsaJobBytes);
+    // batches up to n signatures take the fused latency kernel (0: never; tests pin each path)
+    m.def("ecdsa_set_fused_max", &gpu::SetEcdsaFusedMax, pyb::arg("n"));
+    m.def("ecdsa_fused_max", &gpu::EcdsaFusedMax);
     m.def(
         "ecdsa_verify_device",
         [](uintptr_t msg, uintptr_t sig, uintptr_t pub, uintptr_t jobs, uintptr_t result, size_t n, int device,

@@ -48,6 +48,16 @@ def make_items(native, n, seed=7):
     return items, expect
 
 
+@pytest.fixture(params=["fused", "split"])
+def ecdsa_path(request, native):
+    """Pins one GPU path for the test: the fused latency kernel (every batch size) or the
+    prep + verify throughput kernels (never fused)."""
+    old = native.ecdsa_fused_max()
+    native.ecdsa_set_fused_max(1 << 40 if request.param == "fused" else 0)
+    yield request.param
+    native.ecdsa_set_fused_max(old)
+
+
 def test_cpu_batch(native):
     items, expect = make_items(native, 64)
     res, _ = native.ecdsa_verify_batch(items, use_gpu=False)
@@ -55,7 +65,7 @@ def test_cpu_batch(native):
 
 
 @pytest.mark.gpu
-def test_gpu_batch_matches_cpu(native):
+def test_gpu_batch_matches_cpu(native, ecdsa_path):
     items, expect = make_items(native, 300)
     res, _ = native.ecdsa_verify_batch(items, use_gpu=True)
     cpu, _ = native.ecdsa_verify_batch(items, use_gpu=False)
@@ -64,7 +74,7 @@ def test_gpu_batch_matches_cpu(native):
 
 
 @pytest.mark.gpu
-def test_gpu_batch_edge_scalars(native):
+def test_gpu_batch_edge_scalars(native, ecdsa_path):
     # small private keys / messages exercise short wNAF and sparse comb windows
     items = []
     for k in (1, 2, 3, 255, 256, 2**64 + 1):
@@ -110,8 +120,56 @@ def test_cpu_edge_scalars(native):
 
 
 @pytest.mark.gpu
-def test_gpu_edge_scalars_match_cpu(native):
+def test_gpu_edge_scalars_match_cpu(native, ecdsa_path):
     items = _edge_scalar_items(native)
     cpu, _ = native.ecdsa_verify_batch(items, use_gpu=False)
     gpu, _ = native.ecdsa_verify_batch(items, use_gpu=True)
     assert gpu == cpu
+
+
+def _cancelling_items(native):
+    """Signatures whose R = u1*G + u2*Q is the point at infinity or whose partial sums cancel:
+    with Q = G (secret 1) and z = n - r, u1 + u2 = (z + r)/s = 0 (mod n). They must verify false
+    on every path (the GPU's final additions hit H = 0 with R != 0 and return infinity)."""
+    n = ref.N
+    pub = native.ec_pubkey_create((1).to_bytes(32, "big"), True)
+    rng = random.Random(11)
+    items = []
+    for _ in range(6):
+        r = rng.randrange(1, n)
+        s = rng.randrange(1, n // 2)
+        items.append((pub, ref.der_encode(r, s), (n - r).to_bytes(32, "big")))
+    # and a valid signature by the same key, so the batch is not all-false
+    m = hashlib.sha256(b"cancel").digest()
+    items.append((pub, native.ec_sign((1).to_bytes(32, "big"), m), m))
+    return items
+
+
+def test_cpu_cancelling(native):
+    res, _ = native.ecdsa_verify_batch(_cancelling_items(native), use_gpu=False)
+    assert res == [False] * 6 + [True]
+
+
+@pytest.mark.gpu
+def test_gpu_cancelling_match_cpu(native, ecdsa_path):
+    items = _cancelling_items(native)
+    gpu, _ = native.ecdsa_verify_batch(items, use_gpu=True)
+    assert gpu == [False] * 6 + [True]
+
+
+@pytest.mark.gpu
+def test_gpu_fused_partial_workgroups(native):
+    """The fused kernel runs 64 signatures per workgroup: batch sizes around that boundary (and
+    a multi-workgroup batch) against the split kernels and the expected verdicts."""
+    items, expect = make_items(native, 1100, seed=3)
+    old = native.ecdsa_fused_max()
+    try:
+        for n in (1, 63, 64, 65, 1100):
+            native.ecdsa_set_fused_max(1 << 40)
+            fused, _ = native.ecdsa_verify_batch(items[:n], use_gpu=True)
+            native.ecdsa_set_fused_max(0)
+            split, _ = native.ecdsa_verify_batch(items[:n], use_gpu=True)
+            assert fused == expect[:n], n
+            assert split == expect[:n], n
+    finally:
+        native.ecdsa_set_fused_max(old)

@@ -57,7 +57,17 @@ def _variants(r, s):
     yield "huge_len", b"\x30\x06\x02\x88" + b"\x01" * 8 + b"\x02\x01\x01", False
 
 
-def test_device_der_parse_matches_cpu(native):
+@pytest.mark.parametrize("path", ["fused", "split"])
+def test_device_der_parse_matches_cpu(native, path):
+    old = native.ecdsa_fused_max()
+    native.ecdsa_set_fused_max(1 << 40 if path == "fused" else 0)
+    try:
+        _check_der_variants(native)
+    finally:
+        native.ecdsa_set_fused_max(old)
+
+
+def _check_der_variants(native):
     rng = random.Random(21)
     items, labels, expect = [], [], []
     # enough signatures for the GPU path (the batch threshold does not apply to this entry point)

@@ -28,11 +28,12 @@ def test_service_without_gpu_fails_loudly(native):
         native.gpu_verify_ecdsa_packed(b"\0" * 32, b"\0" * 64, b"\2" + b"\0" * 32)
     # the node-level batch verifier falls back to the CPU pool when the device path throws
     items, expect = make_items(native, 600)
+    old = native.get_gpu_sig_threshold()
     native.set_gpu_sig_threshold(1)
     try:
         assert native.sig_batch_verify(items, use_gpu=True) == all(expect)
     finally:
-        native.set_gpu_sig_threshold(512)
+        native.set_gpu_sig_threshold(old)
 
 
 @pytest.fixture

@@ -39,13 +39,28 @@ if b.gpu_available():
     nat.ecdsa_verify_batch(items[:4096], use_gpu=True, threads=threads)  # table upload, code load
 rows = []
 crossover = None
+default_fused = nat.ecdsa_fused_max()
+
+
+def path_ms(n, fused_max, reps):
+    nat.ecdsa_set_fused_max(fused_max)
+    try:
+        return best_ms(n, True, reps)
+    finally:
+        nat.ecdsa_set_fused_max(default_fused)
+
+
 for n in (64, 128, 256, 512, 1024, 2048, 4096, 8192, 16384, 32768, 65536):
     reps = 5 if n <= 4096 else 3
     cpu = best_ms(n, False, reps)
     gpu = best_ms(n, True, reps) if b.gpu_available() else None
-    rows.append({"n": n, "cpu_ms": round(cpu, 3), "gpu_ms": None if gpu is None else round(gpu, 3),
-                 "cpu_sig_per_s": round(n / cpu * 1e3), "gpu_sig_per_s": None if gpu is None else round(n / gpu * 1e3)})
+    row = {"n": n, "cpu_ms": round(cpu, 3), "gpu_ms": None if gpu is None else round(gpu, 3),
+           "cpu_sig_per_s": round(n / cpu * 1e3), "gpu_sig_per_s": None if gpu is None else round(n / gpu * 1e3)}
+    if b.gpu_available():  # both GPU paths pinned (default: fused up to ecdsa_fused_max())
+        row["gpu_fused_ms"] = round(path_ms(n, 1 << 40, reps), 3)
+        row["gpu_split_ms"] = round(path_ms(n, 0, reps), 3)
+    rows.append(row)
     print(json.dumps(rows[-1]), flush=True)
     if gpu is not None and crossover is None and gpu < cpu:
         crossover = n
-print(json.dumps({"threads": threads, "crossover_n": crossover, "rows": rows}))
+print(json.dumps({"threads": threads, "fused_max": default_fused, "crossover_n": crossover, "rows": rows}))
