@@ -130,6 +130,10 @@ std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, c
 // (profiles/ecdsa_r5.md).
 void SetEcdsaFusedMax(size_t n);
 size_t EcdsaFusedMax();
+// Verify kernel of the split (prep + verify) path: 0 = 8 x 32-bit field with an inverted
+// table, 1 = 10 x 26-bit field with the global-z table.
+void SetEcdsaSplitKernel(int k);
+int EcdsaSplitKernel();
 
 // --------------------------------------------------------------- device-resident entry points
 // The tensor API (bitcoincashplus_amd.ops with torch tensors on the GPU): every pointer is

@@ -500,6 +500,9 @@ constexpr int WG = 128;
 #ifndef BCP_ECDSA_FUSED_MAX // default of EcdsaFusedMax(): batches up to this size run the fused latency kernel
 #define BCP_ECDSA_FUSED_MAX 32768 // fused 2.14 ms vs split 3.03 ms at 32k, split ahead at 64k (profiles/ecdsa_r5.md)
 #endif
+#ifndef BCP_ECDSA_SPLIT_KERNEL // verify kernel after the prep kernel: 0 = 8 x 32 (ecdsa_verify_kernel), 1 = 10 x 26
+#define BCP_ECDSA_SPLIT_KERNEL 0
+#endif
 constexpr int WNAF_W = 4;              // odd multiples 1,3,5,7
 constexpr int NPRE = 1 << (WNAF_W - 2); // 4
 
@@ -1328,6 +1331,157 @@ __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* _
     out[base + lane] = (ok && match && J.scalar_ok) ? 1 : 0;
 }
 
+// ------------------------------------------------------------------ throughput kernel, 10 x 26
+// One lane per signature after ecdsa_prep_kernel, like ecdsa_verify_kernel, with the fused
+// kernel's field and table: 10 x 26-bit limbs and the inversion-free global-z multiples of Q
+// (x, y only in LDS: 320 B per lane). Both GLV halves share one accumulator (3 doublings and
+// 2 additions per digit; the lambda half scales x by beta per addition), then z is moved back
+// to the original curve and u1*G is added by the byte comb.
+constexpr int WG10 = 128;
+__global__ __launch_bounds__(WG10, 2) void ecdsa_verify10_kernel(const Job* __restrict__ jobs,
+                                                                 const uint32_t* __restrict__ gtab,
+                                                                 uint8_t* __restrict__ out, int n) {
+    __shared__ uint32_t tab[NPRE][2][10][WG10];
+    const int tid = threadIdx.x;
+    const int idx = blockIdx.x * WG10 + tid;
+    if (idx >= n) return;
+    const Job& J = jobs[idx];
+    fe qx8;
+    load_be32(qx8, J.pub + 1);
+    bool ok = (J.pub[0] == 2 || J.pub[0] == 3) && fe_lt_p(qx8);
+    FE qx, qy, t;
+    from_words(qx, qx8.v);
+    sqr(t, qx);
+    mul(t, t, qx);
+    t.n[0] += 7;
+    ok = sqrt_var(qy, t) && ok;
+    normalize(qy);
+    if ((qy.n[0] & 1u) != (uint32_t)(J.pub[0] & 1)) {
+        neg(qy, qy, 2);
+        norm(qy);
+    }
+    GJ acc;
+    FE zg;
+    {
+        GJ q1, d;
+        q1.x = qx;
+        q1.y = qy;
+        set_int(q1.z, 1);
+        q1.inf = false;
+        dbl(d, q1);
+        FE z2, z3;
+        sqr(z2, d.z);
+        mul(z3, z2, d.z);
+        GJ P0, P1, P2, P3;
+        mul(P0.x, qx, z2);
+        mul(P0.y, qy, z3);
+        set_int(P0.z, 1);
+        P0.inf = false;
+        FE r0, r1, r2;
+        add_ge(P1, P0, d.x, d.y, &r0);
+        add_ge(P2, P1, d.x, d.y, &r1);
+        add_ge(P3, P2, d.x, d.y, &r2);
+        FE s3, s1;
+        mul(s3, r2, r1);
+        mul(s1, s3, r0);
+        auto put = [&](int m, const GJ& p, const FE* s) {
+            FE x = p.x, y = p.y;
+            if (s) {
+                FE s2, s3c;
+                sqr(s2, *s);
+                mul(s3c, s2, *s);
+                mul(x, p.x, s2);
+                mul(y, p.y, s3c);
+            }
+#pragma unroll
+            for (int k = 0; k < 10; k++) {
+                tab[m][0][k][tid] = x.n[k];
+                tab[m][1][k][tid] = y.n[k];
+            }
+        };
+        put(0, P0, &s1);
+        put(1, P1, &s3);
+        put(2, P2, &r2);
+        put(3, P3, nullptr);
+        mul(zg, d.z, P3.z);
+    }
+    FE beta;
+    {
+        uint32_t bw[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) bw[k] = GLV_BETA[k];
+        from_words(beta, bw);
+    }
+    auto add_digit = [&](int h, int dg) {
+        const int m = ((dg < 0 ? -dg : dg) >> 1) & (NPRE - 1);
+        FE tx, ty, ny;
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            tx.n[k] = tab[m][0][k][tid];
+            ty.n[k] = tab[m][1][k][tid];
+        }
+        if (h) mul(tx, tx, beta);
+        neg(ny, ty, 2);
+        const bool flip = (dg < 0) != (J.neg[h] != 0);
+#pragma unroll
+        for (int k = 0; k < 10; k++) ty.n[k] = flip ? ny.n[k] : ty.n[k];
+        GJ s;
+        add_ge(s, acc, tx, ty);
+        acc = s;
+    };
+    acc.inf = true;
+#pragma unroll 1
+    for (int b = REG_DIGITS - 1; b >= 0; b--) {
+        if (b < REG_DIGITS - 1) {
+#pragma unroll 1
+            for (int i = 0; i < 3; i++) {
+                GJ d;
+                dbl(d, acc);
+                acc = d;
+            }
+        }
+#pragma unroll 1
+        for (int h = 0; h < 2; h++) add_digit(h, wnaf_digit(J, h, b));
+    }
+#pragma unroll 1
+    for (int h = 0; h < 2; h++)
+        if (J.pad[h]) add_digit(h, -1);
+    {
+        FE z;
+        mul(z, acc.z, zg); // back to the original curve
+        acc.z = z;
+    }
+    for (int i = 0; i < 32; i++) {
+        const unsigned byte = J.u1[31 - i];
+        if (!byte) continue;
+        const uint32_t* e = gtab + ((size_t)i * 256 + byte) * 16;
+        FE gx, gy;
+        f10_load_words(gx, e);
+        f10_load_words(gy, e + 8);
+        GJ s;
+        add_ge(s, acc, gx, gy);
+        acc = s;
+    }
+    bool match = false;
+    if (!acc.inf) {
+        FE z2, r, rz, dlt;
+        sqr(z2, acc.z);
+        f10_from_be32(r, J.r);
+        mul(rz, r, z2);
+        sub(dlt, acc.x, rz, 2);
+        norm(dlt);
+        match = is_zero(dlt);
+        if (!match && J.rplusn_ok) {
+            f10_from_be32(r, J.rn);
+            mul(rz, r, z2);
+            sub(dlt, acc.x, rz, 2);
+            norm(dlt);
+            match = is_zero(dlt);
+        }
+    }
+    out[idx] = (ok && match && J.scalar_ok) ? 1 : 0;
+}
+
 // Generator comb table, one per HIP device (read-only once built, shared by every lane).
 struct Table {
     std::once_flag once;
@@ -1378,6 +1532,7 @@ void VerifyLane::Ecdsa(const unsigned char* msg32, const unsigned char* sig64, c
 }
 
 std::atomic<size_t> g_fusedMax{BCP_ECDSA_FUSED_MAX};
+std::atomic<int> g_splitKernel{BCP_ECDSA_SPLIT_KERNEL};
 
 namespace {
 // Batches up to EcdsaFusedMax() run the fused latency kernel (no job records); larger ones the
@@ -1395,13 +1550,19 @@ void LaunchVerify(bool der, const unsigned char* dm, const unsigned char* ds, co
     if (der) hipLaunchKernelGGL(ecdsa_prep_kernel<true>, pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
     else hipLaunchKernelGGL(ecdsa_prep_kernel<false>, pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
-    hipLaunchKernelGGL(ecdsa_verify_kernel, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, stream, d_jobs, gtab,
-                       d_out, (int)n);
+    if (g_splitKernel.load(std::memory_order_relaxed) == 1)
+        hipLaunchKernelGGL(ecdsa_verify10_kernel, dim3((unsigned)((n + WG10 - 1) / WG10)), dim3(WG10), 0, stream, d_jobs,
+                           gtab, d_out, (int)n);
+    else
+        hipLaunchKernelGGL(ecdsa_verify_kernel, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, stream, d_jobs, gtab,
+                           d_out, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
 }
 } // namespace
 
 void SetEcdsaFusedMax(size_t n) { g_fusedMax.store(n, std::memory_order_relaxed); }
+void SetEcdsaSplitKernel(int k) { g_splitKernel.store(k == 1 ? 1 : 0, std::memory_order_relaxed); }
+int EcdsaSplitKernel() { return g_splitKernel.load(std::memory_order_relaxed); }
 size_t EcdsaFusedMax() { return g_fusedMax.load(std::memory_order_relaxed); }
 
 namespace {

@@ -109,6 +109,8 @@ std::string HelpMessage() {
         {"-fastprune", "Use 64 KiB block files (regtest only; for pruning tests)"},
         {"-connectpipeline=<n>", "Blocks in flight when connecting several in a row: block N+1's UTXO pass overlaps "
                                  "block N's signature batch (default: 2; 1 = one block at a time)"},
+        {"-blockcachemb=<n>", "Keep blocks accepted out of order in memory until they connect, up to <n> MiB "
+                              "(default: 512; 0 reads them back from disk like the reference)"},
         {"-parallelutxo=<n>", "Run the UTXO pass of blocks with at least <n> transactions on all script threads "
                               "(default: 64; 0 = always serial)"},
         {"-acceptnonstdtxn", "Relay and mine \"non-standard\" transactions (default: 0 on main, 1 on the test chains)"},

@@ -601,11 +601,38 @@ bool Chainstate::AcceptBlock(const std::shared_ptr<const CBlock>& pblock, CValid
             return state.Error("Failed to write block");
         if (!ReceivedBlockTransactions(block, state, pindex, blockPos))
             return error("AcceptBlock(): ReceivedBlockTransactions failed");
+        // kept until it connects (ActivateBestChain hands ConnectTip only the block it was
+        // called with; every other block of the step would be read back from disk)
+        CacheRecentBlock(pindex->GetBlockHash(), pblock, nBlockSize);
     } catch (const std::runtime_error& e) {
         return state.Error(std::string("System error: ") + e.what());
     }
     if (fCheckForPruning) FlushStateToDisk(state, FLUSH_STATE_NONE);
     return true;
+}
+
+void Chainstate::CacheRecentBlock(const uint256& hash, const std::shared_ptr<const CBlock>& pblock, size_t bytes) {
+    if (bytes > opts.recentBlockBytes || recentBlocks.count(hash)) return;
+    while (recentBytes + bytes > opts.recentBlockBytes && !recentOrder.empty()) {
+        auto it = recentBlocks.find(recentOrder.front());
+        recentOrder.pop_front();
+        if (it == recentBlocks.end()) continue; // taken already
+        recentBytes -= it->second.second;
+        recentBlocks.erase(it);
+    }
+    recentBlocks.emplace(hash, std::make_pair(pblock, bytes));
+    recentOrder.push_back(hash);
+    recentBytes += bytes;
+}
+
+std::shared_ptr<const CBlock> Chainstate::TakeRecentBlock(const uint256& hash) {
+    auto it = recentBlocks.find(hash);
+    if (it == recentBlocks.end()) return nullptr;
+    std::shared_ptr<const CBlock> b = std::move(it->second.first);
+    recentBytes -= it->second.second;
+    recentBlocks.erase(it);
+    if (recentBlocks.empty()) recentOrder.clear();
+    return b;
 }
 
 bool Chainstate::ProcessNewBlock(const std::shared_ptr<const CBlock>& pblock, bool fForceProcessing, bool* fNewBlock,
@@ -1569,13 +1596,16 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
     int64_t ph0[PH_COUNT];
     if (bench)
         for (int k = 0; k < PH_COUNT; k++) ph0[k] = ConnectPhaseMicros((ConnectPhase)k);
-    std::shared_ptr<const CBlock> pthisBlock;
-    if (!pblock) {
+    std::shared_ptr<const CBlock> pthisBlock = TakeRecentBlock(pindexNew->GetBlockHash());
+    if (pblock) {
+        pthisBlock = pblock;
+    } else if (pthisBlock) {
+        recentHits.fetch_add(1, std::memory_order_relaxed);
+    } else {
+        recentMisses.fetch_add(1, std::memory_order_relaxed);
         auto pblockNew = std::make_shared<CBlock>();
         if (!ReadBlockFromDisk(*pblockNew, pindexNew, params, true, pool.get())) return state.Error("Failed to read block");
         pthisBlock = pblockNew;
-    } else {
-        pthisBlock = pblock;
     }
     trace.blocksConnected.emplace_back(pindexNew, pthisBlock);
     const CBlock& blockConnecting = *pthisBlock;
@@ -1598,8 +1628,13 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
     const int64_t nTime5 = GetTimeMicros();
     if (mempool) mempool->removeForBlock(blockConnecting.vtx, pindexNew->nHeight);
     UpdateTip(pindexNew);
+    const int64_t nTime6 = GetTimeMicros();
+    phaseMicros[PH_TIP_READ].fetch_add(nTime2 - nTime1, std::memory_order_relaxed);
+    phaseMicros[PH_TIP_CONNECT].fetch_add(nTime3 - nTime2, std::memory_order_relaxed);
+    phaseMicros[PH_TIP_FLUSH].fetch_add(nTime4 - nTime3, std::memory_order_relaxed);
+    phaseMicros[PH_TIP_WRITE].fetch_add(nTime5 - nTime4, std::memory_order_relaxed);
+    phaseMicros[PH_TIP_POST].fetch_add(nTime6 - nTime5, std::memory_order_relaxed);
     if (bench) {
-        const int64_t nTime6 = GetTimeMicros();
         BenchTotals& B = Bench();
         B.blocks++;
         BenchLine("  ", "Load block from disk", nTime2 - nTime1, B.read);
@@ -1636,7 +1671,9 @@ bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector
     auto commitFront = [&]() -> bool {
         AssertLockHeld(cs_main); // runs inside this function's cs_main scope
         Stage& s = inflight.front();
+        const int64_t tc0 = GetTimeMicros();
         const bool rv = ConnectBlockFinish(*s.p, state, false);
+        phaseMicros[PH_TIP_CONNECT].fetch_add(GetTimeMicros() - tc0, std::memory_order_relaxed);
         GetMainSignals().BlockChecked(*s.block, state);
         if (!rv) {
             if (state.IsInvalid()) InvalidBlockFound(s.pindex, state);
@@ -1646,13 +1683,20 @@ bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector
             return error("ConnectTipsPipelined(): block %s failed (%s)", s.pindex->GetBlockHash().ToString().c_str(),
                          FormatStateMessage(state).c_str());
         }
+        const int64_t tf0 = GetTimeMicros();
         s.view->Flush(); // into the coins tip: everything older is committed already
         if (inflight.size() > 1) inflight[1].view->SetBackend(*pcoinsTip);
+        const int64_t tf1 = GetTimeMicros();
         if (mempool) mempool->removeForBlock(s.block->vtx, s.pindex->nHeight);
         UpdateTip(s.pindex);
         inflight.pop_front();
+        const int64_t tf2 = GetTimeMicros();
         CValidationState fs;
-        if (!FlushStateToDisk(fs, FLUSH_STATE_IF_NEEDED)) {
+        const bool flushed = FlushStateToDisk(fs, FLUSH_STATE_IF_NEEDED);
+        phaseMicros[PH_TIP_FLUSH].fetch_add(tf1 - tf0, std::memory_order_relaxed);
+        phaseMicros[PH_TIP_POST].fetch_add(tf2 - tf1, std::memory_order_relaxed);
+        phaseMicros[PH_TIP_WRITE].fetch_add(GetTimeMicros() - tf2, std::memory_order_relaxed);
+        if (!flushed) {
             state = fs;
             for (size_t k = 0; k < inflight.size(); k++) trace.blocksConnected.pop_back();
             inflight.clear();
@@ -1663,11 +1707,19 @@ bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector
     for (CBlockIndex* pindex : chain) {
         Stage st;
         st.pindex = pindex;
+        std::shared_ptr<const CBlock> cached = TakeRecentBlock(pindex->GetBlockHash());
         if (pblock && pblock->GetHash(params.GetConsensus()) == pindex->GetBlockHash()) {
             st.block = pblock;
+        } else if (cached) {
+            recentHits.fetch_add(1, std::memory_order_relaxed);
+            st.block = std::move(cached);
         } else {
+            recentMisses.fetch_add(1, std::memory_order_relaxed);
             auto b = std::make_shared<CBlock>();
-            if (!ReadBlockFromDisk(*b, pindex, params, true, pool.get())) {
+            const int64_t tr0 = GetTimeMicros();
+            const bool read = ReadBlockFromDisk(*b, pindex, params, true, pool.get());
+            phaseMicros[PH_TIP_READ].fetch_add(GetTimeMicros() - tr0, std::memory_order_relaxed);
+            if (!read) {
                 while (!inflight.empty())
                     if (!commitFront()) return false;
                 return state.Error("Failed to read block");
@@ -1678,7 +1730,10 @@ bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector
         st.view.reset(new CCoinsViewCache(base));
         st.p.reset(new PendingConnect());
         trace.blocksConnected.emplace_back(pindex, st.block);
-        if (!ConnectBlockPrepare(*st.block, state, pindex, *st.view, false, true, *st.p)) {
+        const int64_t tp0 = GetTimeMicros();
+        const bool prepared = ConnectBlockPrepare(*st.block, state, pindex, *st.view, false, true, *st.p);
+        phaseMicros[PH_TIP_CONNECT].fetch_add(GetTimeMicros() - tp0, std::memory_order_relaxed);
+        if (!prepared) {
             // the blocks before it may still be valid: settle them first (in order)
             CValidationState failed = state;
             state = CValidationState();

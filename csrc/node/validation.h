@@ -35,6 +35,8 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <deque>
+#include <map>
 #include <memory>
 #include <set>
 #include <string>
@@ -84,6 +86,10 @@ struct ChainstateOptions {
     int connectPipeline = 2;
     // the UTXO pass of a block with at least this many transactions runs in parallel (0: never)
     size_t parallelUtxoMinTx = 64;
+    // -blockcachemb: blocks accepted but not yet connected stay in memory up to this many
+    // serialized bytes (oldest evicted first), so the connect that follows (IBD, blocks arriving
+    // out of order) skips the disk read, the deserialisation and the repeat CheckBlock; 0: off
+    size_t recentBlockBytes = 512u << 20;
 };
 
 // Mempool acceptance outcome.
@@ -223,9 +229,15 @@ public:
         PH_CHECK, PH_PRECOMPUTE, PH_UTXO, PH_SCRIPTS, PH_COLLECT, PH_BATCH, PH_BLOCKS, PH_FASTUTXO,
         PH_FU_SETUP, PH_FU_CHECKS, PH_FU_UNDO, PH_FU_APPLY,
         PH_ABC_FIND, PH_ABC_STEP, PH_ABC_TIP, PH_ABC_SIGNALS, PH_ABC_REAP, PH_ABC_NOTIFY, PH_ABC_CHECKINDEX,
-        PH_ABC_FLUSH, PH_ACCEPT, PH_COUNT
+        PH_ABC_FLUSH, PH_ACCEPT,
+        // inside ConnectTip (and the pipelined commit): block read from disk, ConnectBlock
+        // (prepare + finish), view flush into the coins tip, FlushStateToDisk, mempool + tip update
+        PH_TIP_READ, PH_TIP_CONNECT, PH_TIP_FLUSH, PH_TIP_WRITE, PH_TIP_POST, PH_COUNT
     };
     int64_t ConnectPhaseMicros(ConnectPhase ph) const { return phaseMicros[ph].load(std::memory_order_relaxed); }
+    // connects that found their block in the recent-block cache / had to read it from disk
+    uint64_t RecentBlockHits() const { return recentHits.load(std::memory_order_relaxed); }
+    uint64_t RecentBlockMisses() const { return recentMisses.load(std::memory_order_relaxed); }
 
 private:
     struct WorkComparator {
@@ -317,6 +329,14 @@ private:
     int64_t nLastWrite = 0, nLastFlush = 0, nLastSetChain = 0;
     std::atomic<int64_t> nLastConnectMicros{0};
     std::atomic<int64_t> phaseMicros[PH_COUNT] = {};
+    // accepted, not yet connected blocks (ChainstateOptions::recentBlockBytes), by block hash
+    void CacheRecentBlock(const uint256& hash, const std::shared_ptr<const CBlock>& pblock, size_t bytes)
+        EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    std::shared_ptr<const CBlock> TakeRecentBlock(const uint256& hash) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    std::map<uint256, std::pair<std::shared_ptr<const CBlock>, size_t>> recentBlocks GUARDED_BY(cs_main);
+    std::deque<uint256> recentOrder GUARDED_BY(cs_main);
+    size_t recentBytes GUARDED_BY(cs_main) = 0;
+    std::atomic<uint64_t> recentHits{0}, recentMisses{0};
 
     std::unique_ptr<CBlockTreeDB> pblocktree;
     std::unique_ptr<CCoinsViewDB> pcoinsdbview;

@@ -219,6 +219,8 @@ void bind_gpu(pyb::module_& m) {
     // batches up to n signatures take the fused latency kernel (0: never; tests pin each path)
     m.def("ecdsa_set_fused_max", &gpu::SetEcdsaFusedMax, pyb::arg("n"));
     m.def("ecdsa_fused_max", &gpu::EcdsaFusedMax);
+    m.def("ecdsa_set_split_kernel", &gpu::SetEcdsaSplitKernel, pyb::arg("k"));
+    m.def("ecdsa_split_kernel", &gpu::EcdsaSplitKernel);
     m.def(
         "ecdsa_verify_device",
         [](uintptr_t msg, uintptr_t sig, uintptr_t pub, uintptr_t jobs, uintptr_t result, size_t n, int device,

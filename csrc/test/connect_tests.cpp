@@ -325,3 +325,51 @@ TEST_CASE(connectblock_tests, parallel_pass_with_bip34_active) {
     std::lock_guard<CCriticalSection> l(cs.cs());
     CHECK(cs.Tip()->GetBlockHash() == blk.GetHash());
 }
+
+// Blocks accepted out of order connect from the recent-block cache (no disk read, no second
+// CheckBlock), and the chain is the same with the cache off (-blockcachemb=0 reads them back).
+TEST_CASE(connectblock_tests, recent_block_cache_out_of_order) {
+    test::TestChain100Setup setup;
+    Chainstate& a = *setup.node->chainstate;
+    const CScript spk = P2PK(setup.coinbaseKey);
+    for (int i = 0; i < 3; i++) setup.CreateAndProcessBlock({}, spk);
+    std::vector<std::shared_ptr<const CBlock>> chain; // a's blocks above genesis, in height order
+    for (const CBlockIndex* p = a.TipNow(); p && p->pprev; p = p->pprev) {
+        auto b = std::make_shared<CBlock>();
+        REQUIRE(ReadBlockFromDisk(*b, p, Params(), true));
+        chain.insert(chain.begin(), b);
+    }
+    REQUIRE(chain.size() >= 4);
+    for (size_t cacheBytes : {(size_t)64 << 20, (size_t)0}) {
+        ChainstateOptions o;
+        o.memoryOnly = true;
+        char tmpl[] = "/tmp/bcp_test_recent_XXXXXX";
+        REQUIRE(mkdtemp(tmpl) != nullptr);
+        o.datadir = tmpl;
+        o.useGpu = false;
+        o.recentBlockBytes = cacheBytes;
+        Chainstate b(Params(), o);
+        std::string err;
+        REQUIRE(b.InitBlockIndex(err));
+        auto feed = [&](const std::shared_ptr<const CBlock>& blk) {
+            bool fNew = false;
+            CValidationState st;
+            return b.ProcessNewBlock(blk, true, &fNew, &st);
+        };
+        const size_t n = chain.size();
+        for (size_t i = 0; i + 3 < n; i++) REQUIRE(feed(chain[i]));
+        std::vector<CBlockHeader> hdrs;
+        for (size_t i = n - 3; i < n; i++) hdrs.push_back(chain[i]->GetBlockHeader());
+        CValidationState hs;
+        REQUIRE(b.ProcessNewBlockHeaders(hdrs, hs));
+        const uint64_t h0 = b.RecentBlockHits(), m0 = b.RecentBlockMisses();
+        for (size_t i = n; i-- > n - 3;) REQUIRE(feed(chain[i])); // last to first
+        CHECK(b.TipNow()->GetBlockHash() == a.TipNow()->GetBlockHash());
+        // the step connects all three after the last one arrives; ConnectTip gets none of them
+        // as its argument (it is not the most-work block)
+        CHECK_EQ(b.RecentBlockHits() - h0, cacheBytes ? (uint64_t)3 : (uint64_t)0);
+        CHECK_EQ(b.RecentBlockMisses() - m0, cacheBytes ? (uint64_t)0 : (uint64_t)3);
+        const std::string cmd = std::string("rm -rf '") + tmpl + "'";
+        if (system(cmd.c_str()) != 0) {}
+    }
+}

@@ -48,14 +48,31 @@ def make_items(native, n, seed=7):
     return items, expect
 
 
-@pytest.fixture(params=["fused", "split"])
+PATHS = {"fused": (1 << 40, None), "split8": (0, 0), "split10": (0, 1)}
+
+
+def pin_path(native, name):
+    """Pins one GPU path: the fused latency kernel (every batch size) or the prep + verify
+    throughput kernels (never fused) with the 8 x 32 or the 10 x 26 verify kernel. Returns the
+    previous settings for unpin_path."""
+    old = (native.ecdsa_fused_max(), native.ecdsa_split_kernel())
+    fmax, sk = PATHS[name]
+    native.ecdsa_set_fused_max(fmax)
+    if sk is not None:
+        native.ecdsa_set_split_kernel(sk)
+    return old
+
+
+def unpin_path(native, old):
+    native.ecdsa_set_fused_max(old[0])
+    native.ecdsa_set_split_kernel(old[1])
+
+
+@pytest.fixture(params=list(PATHS))
 def ecdsa_path(request, native):
-    """Pins one GPU path for the test: the fused latency kernel (every batch size) or the
-    prep + verify throughput kernels (never fused)."""
-    old = native.ecdsa_fused_max()
-    native.ecdsa_set_fused_max(1 << 40 if request.param == "fused" else 0)
+    old = pin_path(native, request.param)
     yield request.param
-    native.ecdsa_set_fused_max(old)
+    unpin_path(native, old)
 
 
 def test_cpu_batch(native):
@@ -159,17 +176,15 @@ def test_gpu_cancelling_match_cpu(native, ecdsa_path):
 
 @pytest.mark.gpu
 def test_gpu_fused_partial_workgroups(native):
-    """The fused kernel runs 64 signatures per workgroup: batch sizes around that boundary (and
-    a multi-workgroup batch) against the split kernels and the expected verdicts."""
+    """The fused kernel runs 64 signatures per workgroup, the verify kernels 128: batch sizes
+    around those boundaries (and a multi-workgroup batch) on every path against the expected
+    verdicts."""
     items, expect = make_items(native, 1100, seed=3)
-    old = native.ecdsa_fused_max()
-    try:
-        for n in (1, 63, 64, 65, 1100):
-            native.ecdsa_set_fused_max(1 << 40)
-            fused, _ = native.ecdsa_verify_batch(items[:n], use_gpu=True)
-            native.ecdsa_set_fused_max(0)
-            split, _ = native.ecdsa_verify_batch(items[:n], use_gpu=True)
-            assert fused == expect[:n], n
-            assert split == expect[:n], n
-    finally:
-        native.ecdsa_set_fused_max(old)
+    for n in (1, 63, 64, 65, 127, 129, 1100):
+        for name in PATHS:
+            old = pin_path(native, name)
+            try:
+                got, _ = native.ecdsa_verify_batch(items[:n], use_gpu=True)
+            finally:
+                unpin_path(native, old)
+            assert got == expect[:n], (n, name)

@@ -57,14 +57,14 @@ def _variants(r, s):
     yield "huge_len", b"\x30\x06\x02\x88" + b"\x01" * 8 + b"\x02\x01\x01", False
 
 
-@pytest.mark.parametrize("path", ["fused", "split"])
+@pytest.mark.parametrize("path", ["fused", "split8", "split10"])
 def test_device_der_parse_matches_cpu(native, path):
-    old = native.ecdsa_fused_max()
-    native.ecdsa_set_fused_max(1 << 40 if path == "fused" else 0)
+    from test_ecdsa_batch import pin_path, unpin_path
+    old = pin_path(native, path)
     try:
         _check_der_variants(native)
     finally:
-        native.ecdsa_set_fused_max(old)
+        unpin_path(native, old)
 
 
 def _check_der_variants(native):
