@@ -498,10 +498,10 @@ constexpr int WG = 128;
 #define BCP_ECDSA_REGULAR 1
 #endif
 #ifndef BCP_ECDSA_FUSED_MAX // default of EcdsaFusedMax(): batches up to this size run the fused latency kernel
-#define BCP_ECDSA_FUSED_MAX 32768 // fused 2.14 ms vs split 3.03 ms at 32k, split ahead at 64k (profiles/ecdsa_r5.md)
+#define BCP_ECDSA_FUSED_MAX 16384 // one workgroup per CU at most (profiles/ecdsa_r5.md)
 #endif
 #ifndef BCP_ECDSA_SPLIT_KERNEL // verify kernel after the prep kernel: 0 = 8 x 32 (ecdsa_verify_kernel), 1 = 10 x 26
-#define BCP_ECDSA_SPLIT_KERNEL 0
+#define BCP_ECDSA_SPLIT_KERNEL 1
 #endif
 constexpr int WNAF_W = 4;              // odd multiples 1,3,5,7
 constexpr int NPRE = 1 << (WNAF_W - 2); // 4
@@ -667,6 +667,53 @@ __device__ __forceinline__ void regw3(unsigned char* out, const uint32_t (&m)[5]
     }
 }
 
+// Regular recoding with window 4 for the 10 x 26 kernels: an odd magnitude m < 2^130 becomes
+// REG4_DIGITS odd digits in [-15, 15], m = sum d_i 16^i (d = (m mod 32) - 16, m = (m - d) / 16;
+// the top digit is what remains, 1..3). Each digit is stored as a nibble: bit 3 = sign,
+// bits 0-2 = |d| >> 1 (the index of the odd multiple |d| Q).
+constexpr int REG4_DIGITS = 33;
+constexpr int NPRE4 = 8; // odd multiples Q .. 15Q
+__device__ __forceinline__ void regw4(unsigned char* out, const uint32_t (&m)[5]) {
+    uint32_t k[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) k[i] = m[i];
+    unsigned char cur = 0;
+    for (int b = 0; b < REG4_DIGITS; b++) {
+        int d;
+        if (b == REG4_DIGITS - 1) {
+            d = (int)k[0];
+        } else {
+            d = (int)(k[0] & 31) - 16;
+            const uint32_t addend = (uint32_t)(-d), ext = d > 0 ? 0xFFFFFFFFu : 0u;
+            uint64_t c = 0;
+#pragma unroll
+            for (int i = 0; i < 5; i++) {
+                c += (uint64_t)k[i] + (i == 0 ? addend : ext);
+                k[i] = (uint32_t)c;
+                c >>= 32;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; i++) k[i] = (k[i] >> 4) | (k[i + 1] << 28);
+            k[4] >>= 4;
+        }
+        const unsigned char nib = (unsigned char)(((d < 0) ? 8 : 0) | (((d < 0 ? -d : d) >> 1) & 7));
+        if (b & 1) {
+            out[b >> 1] = cur | (unsigned char)(nib << 4);
+            cur = 0;
+        } else {
+            cur = nib;
+        }
+    }
+    out[REG4_DIGITS >> 1] = cur; // the odd count leaves the top digit in a low nibble
+}
+// digit b of half h of a window-4 job: the signed odd multiple
+__device__ __forceinline__ int reg4_digit(const Job& J, int h, int b) {
+    const int byte = J.wnaf[h][b >> 1];
+    const int nib = (b & 1) ? (byte >> 4) : (byte & 15);
+    const int mag = 2 * (nib & 7) + 1;
+    return (nib & 8) ? -mag : mag;
+}
+
 // 10-limb two's complement -> magnitude (5 limbs) and sign
 __device__ __forceinline__ bool abs10(uint32_t (&m)[5], uint32_t (&v)[10]) {
     const bool neg = (v[9] >> 31) != 0;
@@ -764,7 +811,7 @@ __device__ __forceinline__ bool sc_is_high(const fe& a) {
 // signature: 129 B uploaded instead of a 272 B Job) and builds the Job on the device.
 // DER: sig holds [length][72 DER bytes] slots, parsed and low-S normalised here; otherwise
 // 64-byte compact r||s, already normalised by the host.
-template <bool DER>
+template <bool DER, bool W4>
 __device__ __forceinline__ void prep_one(Job& J, const unsigned char* __restrict__ msg, const unsigned char* __restrict__ sig,
                                          const unsigned char* __restrict__ pub, int idx) {
     const unsigned char* pk = pub + (size_t)idx * 33;
@@ -907,22 +954,28 @@ __device__ __forceinline__ void prep_one(Job& J, const unsigned char* __restrict
     };
     J.pad[0] = make_odd(m1);
     J.pad[1] = make_odd(m2);
-    regw3(J.wnaf[0], m1);
-    regw3(J.wnaf[1], m2);
-    J.nwnaf[0] = J.nwnaf[1] = (unsigned char)REG_DIGITS;
+    if constexpr (W4) {
+        regw4(J.wnaf[0], m1);
+        regw4(J.wnaf[1], m2);
+        J.nwnaf[0] = J.nwnaf[1] = (unsigned char)REG4_DIGITS;
+    } else {
+        regw3(J.wnaf[0], m1);
+        regw3(J.wnaf[1], m2);
+        J.nwnaf[0] = J.nwnaf[1] = (unsigned char)REG_DIGITS;
+    }
 #else
     J.nwnaf[0] = (unsigned char)wnaf4(J.wnaf[0], m1);
     J.nwnaf[1] = (unsigned char)wnaf4(J.wnaf[1], m2);
 #endif
 }
 
-template <bool DER>
+template <bool DER, bool W4>
 __global__ __launch_bounds__(256) void ecdsa_prep_kernel(Job* __restrict__ jobs, const unsigned char* __restrict__ msg,
                                                          const unsigned char* __restrict__ sig,
                                                          const unsigned char* __restrict__ pub, int n) {
     const int idx = blockIdx.x * 256 + threadIdx.x;
     if (idx >= n) return;
-    prep_one<DER>(jobs[idx], msg, sig, pub, idx);
+    prep_one<DER, W4>(jobs[idx], msg, sig, pub, idx);
 }
 
 __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restrict__ jobs, const uint32_t* __restrict__ gtab,
@@ -1109,24 +1162,13 @@ __global__ __launch_bounds__(WG, 2) void ecdsa_verify_kernel(const Job* __restri
     out[idx] = (ok && match && J.scalar_ok) ? 1 : 0;
 }
 
-// ------------------------------------------------------------------ fused latency kernel
-// Small batches leave most SIMDs idle and each wave alone on its SIMD, so the verify time is
-// the latency of one lane's chain of field operations. This kernel shortens that chain:
-//   * one 192-thread workgroup per 64 signatures; wave 0 runs the scalar work (prep_one: s^-1,
-//     u1, u2, GLV split, recoding) while waves 1-2 decompress the keys and build the tables,
-//     so the prep and the square root overlap instead of running as two kernels;
-//   * waves 1-2 give each GLV half of u2*Q its own lane (lanes 0-31: k1*Q, 32-63: k2*lambdaQ),
-//     halving the additions on the critical path, while wave 0 runs the u1*G comb;
-//   * the odd multiples Q..7Q are made "affine" without an inversion: they live on the
-//     isomorphic curve scaled by one global z (libsecp256k1's globalz table), whose factor
-//     multiplies the ladder's final z;
-//   * field elements are 10 x 26-bit limbs (fe10.h): products with per-column ILP and
-//     carry-free additions, instead of the 8 x 32 product's serial carry chain.
-// Wave 0 adds the three partial points and checks x(R) == r.
-constexpr int FWG = 192;
-constexpr int FSIG = 64; // signatures per workgroup
-static_assert(BCP_ECDSA_REGULAR, "the fused kernel walks the regular window-3 digits");
-
+// ------------------------------------------------------------------ 10 x 26 kernels
+// Shared by the fused latency kernel and the one-lane-per-signature throughput kernel below:
+// field elements are 10 x 26-bit limbs (fe10.h: products with per-column ILP, carry-free
+// additions), Q's odd multiples Q..15Q are made "affine" without an inversion (they live on the
+// isomorphic curve scaled by one global z, libsecp256k1's globalz table, whose factor multiplies
+// the ladder's final z), and u2 is walked in regular window-4 digits (33 per GLV half: 128
+// doublings and 33 additions per half).
 using FE = f10::fe;
 using GJ = f10::gej;
 
@@ -1142,6 +1184,169 @@ __device__ __forceinline__ void f10_from_be32(f10::fe& r, const unsigned char* b
     f10::from_words(r, t.v);
 }
 
+// compressed key -> (x, y) with y's parity from the prefix; false if it does not decode
+__device__ __forceinline__ bool f10_decompress(FE& qx, FE& qy, const unsigned char* pk) {
+    fe qx8;
+    load_be32(qx8, pk + 1);
+    bool ok = (pk[0] == 2 || pk[0] == 3) && fe_lt_p(qx8);
+    FE t;
+    f10::from_words(qx, qx8.v);
+    f10::sqr(t, qx);
+    f10::mul(t, t, qx);
+    t.n[0] += 7;
+    ok = f10::sqrt_var(qy, t) && ok;
+    f10::normalize(qy);
+    if ((qy.n[0] & 1u) != (uint32_t)(pk[0] & 1)) {
+        f10::neg(qy, qy, 2);
+        f10::norm(qy);
+    }
+    return ok;
+}
+
+// Q, 3Q, .., 15Q into tab(m, c, k) (m: multiple, c: 0 = x, 1 = y, k: limb), every x times bmul
+// (1, or beta for lambda*Q). Returns the global z.
+//   2Q = d is made affine on the curve scaled by zeta = z(d): Q becomes (x zeta^2, y zeta^3),
+//   each next multiple is one mixed addition of d, and each entry is brought to the last one's z
+//   through the additions' z ratios (s = z(15Q) / z(iQ)): (x s^2, y s^3).
+template <class Tab>
+__device__ __forceinline__ FE f10_odd_multiples(const FE& qx, const FE& qy, const FE& bmul, Tab&& tab) {
+    using namespace f10;
+    GJ q1, d;
+    q1.x = qx;
+    q1.y = qy;
+    set_int(q1.z, 1);
+    q1.inf = false;
+    dbl(d, q1);
+    FE z2, z3;
+    sqr(z2, d.z);
+    mul(z3, z2, d.z);
+    GJ cur;
+    mul(cur.x, qx, z2);
+    mul(cur.y, qy, z3);
+    set_int(cur.z, 1);
+    cur.inf = false;
+    auto put = [&](int m, const FE& x, const FE& y) {
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            tab(m, 0, k) = x.n[k];
+            tab(m, 1, k) = y.n[k];
+        }
+    };
+    put(0, cur.x, cur.y);
+    FE rr[NPRE4 - 1]; // z ratios (2i+3)Q / (2i+1)Q
+#pragma unroll
+    for (int i = 0; i < NPRE4 - 1; i++) {
+        GJ nx;
+        add_ge(nx, cur, d.x, d.y, &rr[i]);
+        cur = nx;
+        put(i + 1, cur.x, cur.y);
+    }
+    FE zg;
+    mul(zg, d.z, cur.z);
+    FE sc = rr[NPRE4 - 2];
+#pragma unroll
+    for (int i = NPRE4 - 2; i >= 0; i--) {
+        FE x, y, s2, s3;
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            x.n[k] = tab(i, 0, k);
+            y.n[k] = tab(i, 1, k);
+        }
+        sqr(s2, sc);
+        mul(s3, s2, sc);
+        mul(x, x, s2);
+        mul(y, y, s3);
+        mul(x, x, bmul);
+        put(i, x, y);
+        if (i > 0) mul(sc, sc, rr[i - 1]);
+    }
+    FE x;
+#pragma unroll
+    for (int k = 0; k < 10; k++) x.n[k] = tab(NPRE4 - 1, 0, k);
+    mul(x, x, bmul);
+#pragma unroll
+    for (int k = 0; k < 10; k++) tab(NPRE4 - 1, 0, k) = x.n[k];
+    return zg;
+}
+
+// acc += dg * P (dg odd, |dg| <= 15) from the table; flip: the half's sign; bmul: x factor applied
+// per addition (nullptr: none)
+template <class Tab>
+__device__ __forceinline__ void f10_add_digit(GJ& acc, int dg, bool hneg, Tab&& tab, const FE* bmul) {
+    using namespace f10;
+    const int m = ((dg < 0 ? -dg : dg) >> 1) & (NPRE4 - 1);
+    FE tx, ty, ny;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        tx.n[k] = tab(m, 0, k);
+        ty.n[k] = tab(m, 1, k);
+    }
+    if (bmul) mul(tx, tx, *bmul);
+    neg(ny, ty, 2);
+    const bool flip = (dg < 0) != hneg;
+#pragma unroll
+    for (int k = 0; k < 10; k++) ty.n[k] = flip ? ny.n[k] : ty.n[k];
+    GJ s;
+    add_ge(s, acc, tx, ty);
+    acc = s;
+}
+
+// acc += u1 * G by the byte-window comb: windows [w0, w1) of the 32 (affine entries, original curve)
+__device__ __forceinline__ void f10_gcomb(GJ& acc, const unsigned char* u1be, const uint32_t* __restrict__ gtab, int w0,
+                                          int w1) {
+    for (int i = w0; i < w1; i++) {
+        const unsigned byte = u1be[31 - i];
+        if (!byte) continue;
+        const uint32_t* e = gtab + ((size_t)i * 256 + byte) * 16;
+        FE gx, gy;
+        f10_load_words(gx, e);
+        f10_load_words(gy, e + 8);
+        GJ s;
+        f10::add_ge(s, acc, gx, gy);
+        acc = s;
+    }
+}
+
+// x(R) == r (mod n), without an inversion: X == r Z^2 or (r + n) Z^2 when r + n < p
+__device__ __forceinline__ bool f10_check_r(const GJ& R, const Job& J) {
+    using namespace f10;
+    if (R.inf) return false;
+    FE z2, r, rz, dlt;
+    sqr(z2, R.z);
+    f10_from_be32(r, J.r);
+    mul(rz, r, z2);
+    sub(dlt, R.x, rz, 2);
+    norm(dlt);
+    if (is_zero(dlt)) return true;
+    if (!J.rplusn_ok) return false;
+    f10_from_be32(r, J.rn);
+    mul(rz, r, z2);
+    sub(dlt, R.x, rz, 2);
+    norm(dlt);
+    return is_zero(dlt);
+}
+
+__device__ __forceinline__ FE f10_beta() {
+    uint32_t bw[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) bw[k] = GLV_BETA[k];
+    FE b;
+    f10::from_words(b, bw);
+    return b;
+}
+
+// ------------------------------------------------------------------ fused latency kernel
+// Small batches leave most SIMDs idle and each wave alone on its SIMD, so the verify time is
+// the latency of one lane's chain of field operations. This kernel shortens that chain:
+//   * one 192-thread workgroup per 64 signatures; wave 0 runs the scalar work (prep_one: s^-1,
+//     u1, u2, GLV split, recoding) while waves 1-2 decompress the keys and build the tables,
+//     so the prep and the square root overlap instead of running as two kernels;
+//   * waves 1-2 give each GLV half of u2*Q its own lane (lanes 0-31: k1*Q, 32-63: k2*lambdaQ),
+//     halving the additions on the critical path, while wave 0 runs the u1*G comb.
+// Wave 0 adds the three partial points and checks x(R) == r.
+constexpr int FWG = 192;
+constexpr int FSIG = 64; // signatures per workgroup
+
 template <bool DER>
 __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* __restrict__ msg,
                                                           const unsigned char* __restrict__ sig,
@@ -1149,140 +1354,50 @@ __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* _
                                                           const uint32_t* __restrict__ gtab, uint8_t* __restrict__ out,
                                                           int n) {
     __shared__ Job sj[FSIG];
-    __shared__ uint32_t tab[2][NPRE][2][10][64]; // ladder wave, multiple, x|y, limb, lane
-    __shared__ uint32_t res[2][3][10][64];       // ladder wave, x|y|z, limb, lane
-    __shared__ unsigned char rflag[2][64];       // bit 0: point at infinity, bit 1: key decoded
+    __shared__ uint32_t tab[2][NPRE4][2][10][64]; // ladder wave, multiple, x|y, limb, lane
+    __shared__ uint32_t res[2][3][10][64];        // ladder wave, x|y|z, limb, lane
+    __shared__ unsigned char rflag[2][64];        // bit 0: point at infinity, bit 1: key decoded
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int base = blockIdx.x * FSIG;
     GJ acc; // wave 0: u1*G; waves 1-2: one GLV half of u2*Q
+    FE zg;
+    bool ok = false;
     if (wave == 0) {
-        prep_one<DER>(sj[lane], msg, sig, pub, min(base + lane, n - 1));
+        prep_one<DER, true>(sj[lane], msg, sig, pub, min(base + lane, n - 1));
     } else {
         const int w = wave - 1, slot = w * 32 + (lane & 31), half = lane >> 5;
-        const unsigned char* pk = pub + (size_t)min(base + slot, n - 1) * 33;
-        fe qx8;
-        load_be32(qx8, pk + 1);
-        bool ok = (pk[0] == 2 || pk[0] == 3) && fe_lt_p(qx8);
-        FE qx, qy, t;
-        from_words(qx, qx8.v);
-        sqr(t, qx);
-        mul(t, t, qx);
-        t.n[0] += 7;
-        ok = sqrt_var(qy, t) && ok;
-        normalize(qy);
-        if ((qy.n[0] & 1u) != (uint32_t)(pk[0] & 1)) {
-            neg(qy, qy, 2);
-            norm(qy);
-        }
-        // 2Q, then Q moved to the curve scaled by zeta = z(2Q), where 2Q is affine
-        GJ q1, d;
-        q1.x = qx;
-        q1.y = qy;
-        set_int(q1.z, 1);
-        q1.inf = false;
-        dbl(d, q1);
-        FE z2, z3;
-        sqr(z2, d.z);
-        mul(z3, z2, d.z);
-        GJ P0, P1, P2, P3;
-        mul(P0.x, qx, z2);
-        mul(P0.y, qy, z3);
-        set_int(P0.z, 1);
-        P0.inf = false;
-        FE r0, r1, r2; // z ratios 3Q/Q, 5Q/3Q, 7Q/5Q
-        add_ge(P1, P0, d.x, d.y, &r0);
-        add_ge(P2, P1, d.x, d.y, &r1);
-        add_ge(P3, P2, d.x, d.y, &r2);
-        // every multiple to z(7Q): scale by s = z7 / z_i, (x s^2, y s^3)
-        FE s3, s1;
-        mul(s3, r2, r1);
-        mul(s1, s3, r0);
-        FE bmul; // lambda*Q multiples: x scaled by beta
-        if (half) {
-            uint32_t bw[8];
-#pragma unroll
-            for (int k = 0; k < 8; k++) bw[k] = GLV_BETA[k];
-            from_words(bmul, bw);
-        } else {
-            set_int(bmul, 1);
-        }
-        auto put = [&](int m, const GJ& p, const FE* s) {
-            FE x = p.x, y = p.y;
-            if (s) {
-                FE s2, s3c;
-                sqr(s2, *s);
-                mul(s3c, s2, *s);
-                mul(x, p.x, s2);
-                mul(y, p.y, s3c);
-            }
-            mul(x, x, bmul);
-#pragma unroll
-            for (int k = 0; k < 10; k++) {
-                tab[w][m][0][k][lane] = x.n[k];
-                tab[w][m][1][k][lane] = y.n[k];
-            }
-        };
-        put(0, P0, &s1);
-        put(1, P1, &s3);
-        put(2, P2, &r2);
-        put(3, P3, nullptr);
-        mul(acc.z, d.z, P3.z); // the global z, kept in acc.z until the ladder starts
-        acc.inf = !ok;
+        FE qx, qy;
+        ok = f10_decompress(qx, qy, pub + (size_t)min(base + slot, n - 1) * 33);
+        FE bmul;
+        if (half) bmul = f10_beta();
+        else f10::set_int(bmul, 1);
+        zg = f10_odd_multiples(qx, qy, bmul, [&](int m, int c, int k) -> uint32_t& { return tab[w][m][c][k][lane]; });
     }
     __syncthreads();
     if (wave == 0) {
-        // u1*G by the byte-window comb (affine entries of the original curve)
-        const Job& J = sj[lane];
         acc.inf = true;
-        for (int i = 0; i < 32; i++) {
-            const unsigned byte = J.u1[31 - i];
-            if (!byte) continue;
-            const uint32_t* e = gtab + ((size_t)i * 256 + byte) * 16;
-            FE gx, gy;
-            f10_load_words(gx, e);
-            f10_load_words(gy, e + 8);
-            GJ s;
-            add_ge(s, acc, gx, gy);
-            acc = s;
-        }
+        f10_gcomb(acc, sj[lane].u1, gtab, 0, 32);
     } else {
         const int w = wave - 1, slot = w * 32 + (lane & 31), half = lane >> 5;
         const Job& J = sj[slot];
-        const FE zg = acc.z;
-        const bool ok = !acc.inf;
         const bool hneg = J.neg[half] != 0;
-        auto add_digit = [&](int dg) {
-            const int m = ((dg < 0 ? -dg : dg) >> 1) & (NPRE - 1);
-            FE tx, ty, ny;
-#pragma unroll
-            for (int k = 0; k < 10; k++) {
-                tx.n[k] = tab[w][m][0][k][lane];
-                ty.n[k] = tab[w][m][1][k][lane];
-            }
-            neg(ny, ty, 2);
-            const bool flip = (dg < 0) != hneg;
-#pragma unroll
-            for (int k = 0; k < 10; k++) ty.n[k] = flip ? ny.n[k] : ty.n[k];
-            GJ s;
-            add_ge(s, acc, tx, ty);
-            acc = s;
-        };
+        auto tb = [&](int m, int c, int k) -> uint32_t& { return tab[w][m][c][k][lane]; };
         acc.inf = true;
 #pragma unroll 1
-        for (int b = REG_DIGITS - 1; b >= 0; b--) {
-            if (b < REG_DIGITS - 1) {
+        for (int b = REG4_DIGITS - 1; b >= 0; b--) {
+            if (b < REG4_DIGITS - 1) {
 #pragma unroll 1
-                for (int t = 0; t < 3; t++) {
+                for (int t = 0; t < 4; t++) {
                     GJ d;
-                    dbl(d, acc);
+                    f10::dbl(d, acc);
                     acc = d;
                 }
             }
-            add_digit(wnaf_digit(J, half, b));
+            f10_add_digit(acc, reg4_digit(J, half, b), hneg, tb, nullptr);
         }
-        if (J.pad[half]) add_digit(-1); // an even half was encoded as k + 1
+        if (J.pad[half]) f10_add_digit(acc, -1, hneg, tb, nullptr); // an even half was encoded as k + 1
         FE z;
-        mul(z, acc.z, zg);
+        f10::mul(z, acc.z, zg);
 #pragma unroll
         for (int k = 0; k < 10; k++) {
             res[w][0][k][lane] = acc.x.n[k];
@@ -1295,7 +1410,7 @@ __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* _
     if (wave != 0 || base + lane >= n) return;
     const Job& J = sj[lane];
     const int w = lane >> 5, l0 = lane & 31;
-    bool ok = (rflag[w][l0] & 2) != 0;
+    ok = (rflag[w][l0] & 2) != 0;
 #pragma unroll
     for (int h = 0; h < 2; h++) {
         const int l = l0 + 32 * h;
@@ -1308,178 +1423,58 @@ __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* _
         }
         q.inf = (rflag[w][l] & 1) != 0;
         GJ s;
-        add_gej(s, acc, q);
+        f10::add_gej(s, acc, q);
         acc = s;
     }
-    bool match = false;
-    if (!acc.inf) {
-        FE z2, r, rz, dlt;
-        sqr(z2, acc.z);
-        f10_from_be32(r, J.r);
-        mul(rz, r, z2);
-        sub(dlt, acc.x, rz, 2);
-        norm(dlt);
-        match = is_zero(dlt);
-        if (!match && J.rplusn_ok) {
-            f10_from_be32(r, J.rn);
-            mul(rz, r, z2);
-            sub(dlt, acc.x, rz, 2);
-            norm(dlt);
-            match = is_zero(dlt);
-        }
-    }
-    out[base + lane] = (ok && match && J.scalar_ok) ? 1 : 0;
+    out[base + lane] = (ok && f10_check_r(acc, J) && J.scalar_ok) ? 1 : 0;
 }
 
 // ------------------------------------------------------------------ throughput kernel, 10 x 26
-// One lane per signature after ecdsa_prep_kernel, like ecdsa_verify_kernel, with the fused
-// kernel's field and table: 10 x 26-bit limbs and the inversion-free global-z multiples of Q
-// (x, y only in LDS: 320 B per lane). Both GLV halves share one accumulator (3 doublings and
-// 2 additions per digit; the lambda half scales x by beta per addition), then z is moved back
-// to the original curve and u1*G is added by the byte comb.
-constexpr int WG10 = 128;
-__global__ __launch_bounds__(WG10, 2) void ecdsa_verify10_kernel(const Job* __restrict__ jobs,
-                                                                 const uint32_t* __restrict__ gtab,
-                                                                 uint8_t* __restrict__ out, int n) {
-    __shared__ uint32_t tab[NPRE][2][10][WG10];
+// One lane per signature after ecdsa_prep_kernel<DER, true>, like ecdsa_verify_kernel, with the
+// 10 x 26 field, the global-z table (x, y only in LDS: 640 B per lane) and window-4 digits.
+// Both GLV halves share one accumulator (4 doublings and 2 additions per digit; the lambda half
+// scales x by beta per addition); then z is moved back to the original curve and u1*G is added
+// by the byte comb.
+constexpr int WG10 = 64;
+__global__ __launch_bounds__(WG10) void ecdsa_verify10_kernel(const Job* __restrict__ jobs,
+                                                              const uint32_t* __restrict__ gtab,
+                                                              uint8_t* __restrict__ out, int n) {
+    __shared__ uint32_t tab[NPRE4][2][10][WG10];
     const int tid = threadIdx.x;
     const int idx = blockIdx.x * WG10 + tid;
     if (idx >= n) return;
     const Job& J = jobs[idx];
-    fe qx8;
-    load_be32(qx8, J.pub + 1);
-    bool ok = (J.pub[0] == 2 || J.pub[0] == 3) && fe_lt_p(qx8);
-    FE qx, qy, t;
-    from_words(qx, qx8.v);
-    sqr(t, qx);
-    mul(t, t, qx);
-    t.n[0] += 7;
-    ok = sqrt_var(qy, t) && ok;
-    normalize(qy);
-    if ((qy.n[0] & 1u) != (uint32_t)(J.pub[0] & 1)) {
-        neg(qy, qy, 2);
-        norm(qy);
-    }
+    FE qx, qy, one;
+    const bool ok = f10_decompress(qx, qy, J.pub);
+    f10::set_int(one, 1);
+    auto tb = [&](int m, int c, int k) -> uint32_t& { return tab[m][c][k][tid]; };
+    const FE zg = f10_odd_multiples(qx, qy, one, tb);
+    const FE beta = f10_beta();
+    const bool hneg0 = J.neg[0] != 0, hneg1 = J.neg[1] != 0;
     GJ acc;
-    FE zg;
-    {
-        GJ q1, d;
-        q1.x = qx;
-        q1.y = qy;
-        set_int(q1.z, 1);
-        q1.inf = false;
-        dbl(d, q1);
-        FE z2, z3;
-        sqr(z2, d.z);
-        mul(z3, z2, d.z);
-        GJ P0, P1, P2, P3;
-        mul(P0.x, qx, z2);
-        mul(P0.y, qy, z3);
-        set_int(P0.z, 1);
-        P0.inf = false;
-        FE r0, r1, r2;
-        add_ge(P1, P0, d.x, d.y, &r0);
-        add_ge(P2, P1, d.x, d.y, &r1);
-        add_ge(P3, P2, d.x, d.y, &r2);
-        FE s3, s1;
-        mul(s3, r2, r1);
-        mul(s1, s3, r0);
-        auto put = [&](int m, const GJ& p, const FE* s) {
-            FE x = p.x, y = p.y;
-            if (s) {
-                FE s2, s3c;
-                sqr(s2, *s);
-                mul(s3c, s2, *s);
-                mul(x, p.x, s2);
-                mul(y, p.y, s3c);
-            }
-#pragma unroll
-            for (int k = 0; k < 10; k++) {
-                tab[m][0][k][tid] = x.n[k];
-                tab[m][1][k][tid] = y.n[k];
-            }
-        };
-        put(0, P0, &s1);
-        put(1, P1, &s3);
-        put(2, P2, &r2);
-        put(3, P3, nullptr);
-        mul(zg, d.z, P3.z);
-    }
-    FE beta;
-    {
-        uint32_t bw[8];
-#pragma unroll
-        for (int k = 0; k < 8; k++) bw[k] = GLV_BETA[k];
-        from_words(beta, bw);
-    }
-    auto add_digit = [&](int h, int dg) {
-        const int m = ((dg < 0 ? -dg : dg) >> 1) & (NPRE - 1);
-        FE tx, ty, ny;
-#pragma unroll
-        for (int k = 0; k < 10; k++) {
-            tx.n[k] = tab[m][0][k][tid];
-            ty.n[k] = tab[m][1][k][tid];
-        }
-        if (h) mul(tx, tx, beta);
-        neg(ny, ty, 2);
-        const bool flip = (dg < 0) != (J.neg[h] != 0);
-#pragma unroll
-        for (int k = 0; k < 10; k++) ty.n[k] = flip ? ny.n[k] : ty.n[k];
-        GJ s;
-        add_ge(s, acc, tx, ty);
-        acc = s;
-    };
     acc.inf = true;
 #pragma unroll 1
-    for (int b = REG_DIGITS - 1; b >= 0; b--) {
-        if (b < REG_DIGITS - 1) {
+    for (int b = REG4_DIGITS - 1; b >= 0; b--) {
+        if (b < REG4_DIGITS - 1) {
 #pragma unroll 1
-            for (int i = 0; i < 3; i++) {
+            for (int i = 0; i < 4; i++) {
                 GJ d;
-                dbl(d, acc);
+                f10::dbl(d, acc);
                 acc = d;
             }
         }
-#pragma unroll 1
-        for (int h = 0; h < 2; h++) add_digit(h, wnaf_digit(J, h, b));
+        f10_add_digit(acc, reg4_digit(J, 0, b), hneg0, tb, nullptr);
+        f10_add_digit(acc, reg4_digit(J, 1, b), hneg1, tb, &beta);
     }
-#pragma unroll 1
-    for (int h = 0; h < 2; h++)
-        if (J.pad[h]) add_digit(h, -1);
+    if (J.pad[0]) f10_add_digit(acc, -1, hneg0, tb, nullptr);
+    if (J.pad[1]) f10_add_digit(acc, -1, hneg1, tb, &beta);
     {
         FE z;
-        mul(z, acc.z, zg); // back to the original curve
+        f10::mul(z, acc.z, zg); // back to the original curve
         acc.z = z;
     }
-    for (int i = 0; i < 32; i++) {
-        const unsigned byte = J.u1[31 - i];
-        if (!byte) continue;
-        const uint32_t* e = gtab + ((size_t)i * 256 + byte) * 16;
-        FE gx, gy;
-        f10_load_words(gx, e);
-        f10_load_words(gy, e + 8);
-        GJ s;
-        add_ge(s, acc, gx, gy);
-        acc = s;
-    }
-    bool match = false;
-    if (!acc.inf) {
-        FE z2, r, rz, dlt;
-        sqr(z2, acc.z);
-        f10_from_be32(r, J.r);
-        mul(rz, r, z2);
-        sub(dlt, acc.x, rz, 2);
-        norm(dlt);
-        match = is_zero(dlt);
-        if (!match && J.rplusn_ok) {
-            f10_from_be32(r, J.rn);
-            mul(rz, r, z2);
-            sub(dlt, acc.x, rz, 2);
-            norm(dlt);
-            match = is_zero(dlt);
-        }
-    }
-    out[idx] = (ok && match && J.scalar_ok) ? 1 : 0;
+    f10_gcomb(acc, J.u1, gtab, 0, 32);
+    out[idx] = (ok && f10_check_r(acc, J) && J.scalar_ok) ? 1 : 0;
 }
 
 // Generator comb table, one per HIP device (read-only once built, shared by every lane).
@@ -1547,10 +1542,13 @@ void LaunchVerify(bool der, const unsigned char* dm, const unsigned char* ds, co
         return;
     }
     const dim3 pg((unsigned)((n + 255) / 256));
-    if (der) hipLaunchKernelGGL(ecdsa_prep_kernel<true>, pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
-    else hipLaunchKernelGGL(ecdsa_prep_kernel<false>, pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
+    const bool k10 = g_splitKernel.load(std::memory_order_relaxed) == 1; // window-4 digits for the 10 x 26 kernel
+    if (der && k10) hipLaunchKernelGGL((ecdsa_prep_kernel<true, true>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
+    else if (der) hipLaunchKernelGGL((ecdsa_prep_kernel<true, false>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
+    else if (k10) hipLaunchKernelGGL((ecdsa_prep_kernel<false, true>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
+    else hipLaunchKernelGGL((ecdsa_prep_kernel<false, false>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
-    if (g_splitKernel.load(std::memory_order_relaxed) == 1)
+    if (k10)
         hipLaunchKernelGGL(ecdsa_verify10_kernel, dim3((unsigned)((n + WG10 - 1) / WG10)), dim3(WG10), 0, stream, d_jobs,
                            gtab, d_out, (int)n);
     else

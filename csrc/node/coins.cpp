@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include "util/memusage.h"
+#include "util/reaper.h"
 #include "keys/key.h"
 #include "secp256k1/secp256k1.h"
 
@@ -302,7 +303,8 @@ void CCoinsViewCache::ForEachShard(const std::function<void(unsigned)>& fn, Work
 void CCoinsViewCache::MergeShard(CCoinsMap::Shard& from, unsigned s) {
     CCoinsMap::Shard& ours = cacheCoins.shard(s);
     size_t& used = usage[s].bytes;
-    for (auto it = from.begin(); it != from.end(); it = from.erase(it)) {
+    // the child's entries are left in place (moved-from) and freed with the child's map
+    for (auto it = from.begin(); it != from.end(); ++it) {
         if (!(it->second.flags & CCoinsCacheEntry::DIRTY)) continue; // non-dirty: nothing to merge
         auto itUs = ours.find(it->first);
         if (itUs == ours.end()) {
@@ -353,7 +355,15 @@ bool CCoinsViewCache::BatchWrite(CCoinsMap& mapCoins, const uint256& hashBlockIn
 
 bool CCoinsViewCache::Flush() {
     const bool ok = base->BatchWrite(cacheCoins, hashBlock);
-    cacheCoins.clear();
+    if (cacheCoins.size() >= 4096) {
+        // a block's worth of merged-away entries (moved-from coins, ~80k nodes for an 8 MB
+        // block) is freed on the reaper thread instead of the connecting one
+        std::unique_ptr<CCoinsMap> dead(new CCoinsMap);
+        dead->swap(cacheCoins);
+        Reaper::Get().Drop(std::move(dead));
+    } else {
+        cacheCoins.clear();
+    }
     for (ShardUsage& u : usage) u.bytes = 0;
     return ok;
 }

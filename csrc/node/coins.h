@@ -245,6 +245,10 @@ public:
             s.swap(fresh);
         }
     }
+    // exchanges every shard (and its arena) with o's
+    void swap(CCoinsMap& o) {
+        for (unsigned i = 0; i < SHARDS; i++) shards[i].swap(o.shards[i]);
+    }
     // room for n entries spread over the shards (with slack for an uneven split)
     void reserve(size_t n) {
         for (Shard& s : shards) s.reserve(n / SHARDS + n / (4 * SHARDS) + 16);

@@ -468,21 +468,30 @@ bool ReadRawBlockFromDisk(std::vector<unsigned char>& out, const CDiskBlockPos& 
     return ok;
 }
 
-bool UndoWriteToDisk(const CBlockUndo& undo, CDiskBlockPos& pos, const uint256& hashBlock,
+bool UndoWriteToDisk(const std::vector<unsigned char>& ser, CDiskBlockPos& pos, const uint256& hashBlock,
                      const unsigned char diskMagic[4]) {
+    // one serialisation, one hash pass and one write: the undo record is serialised once by the
+    // caller (the reference serialises it three times - size, file, checksum - through small
+    // buffered writes). The checksum is SHA256d(hashBlock || record), as the reference's.
     FileStream out(OpenUndoFile(pos), SER_DISK, PROTOCOL_VERSION);
     if (!out.Get()) return false;
-    const uint32_t nSize = (uint32_t)GetSerializeSize(undo, PROTOCOL_VERSION);
+    const uint32_t nSize = (uint32_t)ser.size();
     out.write((const char*)diskMagic, 4);
     out << nSize;
     const long p = ftell(out.Get());
     if (p < 0) return false;
     pos.nPos = (unsigned)p;
-    out << undo;
+    out.write((const char*)ser.data(), ser.size());
     HashWriter hasher;
-    hasher << hashBlock << undo;
+    hasher << hashBlock;
+    hasher.write((const char*)ser.data(), ser.size());
     out << hasher.GetHash();
     return true;
+}
+
+bool UndoWriteToDisk(const CBlockUndo& undo, CDiskBlockPos& pos, const uint256& hashBlock,
+                     const unsigned char diskMagic[4]) {
+    return UndoWriteToDisk(SerializeToBytes(undo, SER_DISK, PROTOCOL_VERSION), pos, hashBlock, diskMagic);
 }
 
 bool UndoReadFromDisk(CBlockUndo& undo, const CDiskBlockPos& pos, const uint256& hashBlock) {

@@ -1321,13 +1321,16 @@ bool Chainstate::ConnectBlockFinish(PendingConnect& p, CValidationState& state, 
 
     if (pindex->GetUndoPos().IsNull() || !pindex->IsValid(BLOCK_VALID_SCRIPTS)) {
         if (pindex->GetUndoPos().IsNull()) {
+            const int64_t tu = GetTimeMicros();
             CDiskBlockPos upos;
-            if (!FindUndoPos(state, pindex->nFile, upos, (unsigned)GetSerializeSize(blockundo, PROTOCOL_VERSION) + 40))
+            const std::vector<unsigned char> ser = SerializeToBytes(blockundo, SER_DISK, PROTOCOL_VERSION);
+            if (!FindUndoPos(state, pindex->nFile, upos, (unsigned)ser.size() + 40))
                 return error("ConnectBlock(): FindUndoPos failed");
-            if (!UndoWriteToDisk(blockundo, upos, pindex->pprev->GetBlockHash(), params.DiskMagic()))
+            if (!UndoWriteToDisk(ser, upos, pindex->pprev->GetBlockHash(), params.DiskMagic()))
                 return state.Error("Failed to write undo data");
             pindex->nUndoPos = upos.nPos;
             pindex->nStatus |= BLOCK_HAVE_UNDO;
+            phaseMicros[PH_UNDO].fetch_add(GetTimeMicros() - tu, std::memory_order_relaxed);
         }
         pindex->RaiseValidity(BLOCK_VALID_SCRIPTS);
         setDirtyBlockIndex.insert(pindex);
@@ -1689,6 +1692,10 @@ bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector
         const int64_t tf1 = GetTimeMicros();
         if (mempool) mempool->removeForBlock(s.block->vtx, s.pindex->nHeight);
         UpdateTip(s.pindex);
+        // the block's undo records (21k+ vectors for a big block) and its emptied view are freed
+        // on the reaper thread, as ConnectBlock does for the one-at-a-time path
+        Reaper::Get().Drop(std::move(s.p->blockundo));
+        Reaper::Get().Drop(std::move(s.view));
         inflight.pop_front();
         const int64_t tf2 = GetTimeMicros();
         CValidationState fs;

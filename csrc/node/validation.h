@@ -232,7 +232,9 @@ public:
         PH_ABC_FLUSH, PH_ACCEPT,
         // inside ConnectTip (and the pipelined commit): block read from disk, ConnectBlock
         // (prepare + finish), view flush into the coins tip, FlushStateToDisk, mempool + tip update
-        PH_TIP_READ, PH_TIP_CONNECT, PH_TIP_FLUSH, PH_TIP_WRITE, PH_TIP_POST, PH_COUNT
+        PH_TIP_READ, PH_TIP_CONNECT, PH_TIP_FLUSH, PH_TIP_WRITE, PH_TIP_POST,
+        PH_UNDO, // inside ConnectBlockFinish: the block's undo data serialised and written
+        PH_COUNT
     };
     int64_t ConnectPhaseMicros(ConnectPhase ph) const { return phaseMicros[ph].load(std::memory_order_relaxed); }
     // connects that found their block in the recent-block cache / had to read it from disk

@@ -1175,14 +1175,14 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
                     "# ibd %s pipeline=%d (ms/block): total %.2f = ConnectTip %.2f + outside %.2f [accept %.2f, find %.3f, "
                     "step-other %.2f, signals %.2f, reap %.2f, notify %.2f, checkindex %.2f, flush %.2f]; "
                     "inside ConnectTip: read %.2f, connectblock %.2f [checkblock %.2f, prefetch %.2f, utxo %.2f, "
-                    "scripts %.2f, batch %.2f], view-flush %.2f, flushstate %.2f, post %.2f; recent-block cache "
+                    "scripts %.2f, batch %.2f, undo %.2f], view-flush %.2f, flushstate %.2f, post %.2f; recent-block cache "
                     "hits %llu, misses %llu\n",
                     useGpu ? "GPU" : "CPU", pipeline, total, tip, total - tip, ms(Chainstate::PH_ACCEPT),
                     ms(Chainstate::PH_ABC_FIND), ms(Chainstate::PH_ABC_STEP) - tip, ms(Chainstate::PH_ABC_SIGNALS),
                     ms(Chainstate::PH_ABC_REAP), ms(Chainstate::PH_ABC_NOTIFY), ms(Chainstate::PH_ABC_CHECKINDEX),
                     ms(Chainstate::PH_ABC_FLUSH), ms(Chainstate::PH_TIP_READ), ms(Chainstate::PH_TIP_CONNECT),
                     ms(Chainstate::PH_CHECK), ms(Chainstate::PH_PRECOMPUTE), ms(Chainstate::PH_UTXO),
-                    ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_BATCH), ms(Chainstate::PH_TIP_FLUSH),
+                    ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_BATCH), ms(Chainstate::PH_UNDO), ms(Chainstate::PH_TIP_FLUSH),
                     ms(Chainstate::PH_TIP_WRITE), ms(Chainstate::PH_TIP_POST),
                     (unsigned long long)cs.RecentBlockHits(), (unsigned long long)cs.RecentBlockMisses());
         }
