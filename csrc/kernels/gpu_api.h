@@ -131,7 +131,9 @@ std::vector<uint8_t> EcdsaVerifyBatch(const std::vector<unsigned char>& msg32, c
 void SetEcdsaFusedMax(size_t n);
 size_t EcdsaFusedMax();
 // Verify kernel of the split (prep + verify) path: 0 = 8 x 32-bit field with an inverted
-// table, 1 = 10 x 26-bit field with the global-z table.
+// table, 1 = 10 x 26-bit field with the global-z table (one lane per signature for whole rounds
+// of the device, one GLV half per lane for a last round at most half full), 2 / 3 = only the
+// one-lane / only the half-lane 10 x 26 kernel (tests pin each).
 void SetEcdsaSplitKernel(int k);
 int EcdsaSplitKernel();
 

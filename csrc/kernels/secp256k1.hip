@@ -501,6 +501,8 @@ constexpr int WG = 128;
 #define BCP_ECDSA_FUSED_MAX 16384 // one workgroup per CU at most (profiles/ecdsa_r5.md)
 #endif
 #ifndef BCP_ECDSA_SPLIT_KERNEL // verify kernel after the prep kernel: 0 = 8 x 32 (ecdsa_verify_kernel), 1 = 10 x 26
+                               // (one lane per signature for whole rounds, a half-lane tail), 2 / 3 = only
+                               // the one-lane / the half-lane 10 x 26 kernel (tests)
 #define BCP_ECDSA_SPLIT_KERNEL 1
 #endif
 constexpr int WNAF_W = 4;              // odd multiples 1,3,5,7
@@ -1291,13 +1293,18 @@ __device__ __forceinline__ void f10_add_digit(GJ& acc, int dg, bool hneg, Tab&& 
     acc = s;
 }
 
-// acc += u1 * G by the byte-window comb: windows [w0, w1) of the 32 (affine entries, original curve)
-__device__ __forceinline__ void f10_gcomb(GJ& acc, const unsigned char* u1be, const uint32_t* __restrict__ gtab, int w0,
-                                          int w1) {
+// acc += u1 * G by the 11-bit comb (gtab11: 24 windows x 2048 affine entries): windows [w0, w1)
+constexpr int G11_WINDOWS = 24;
+__device__ __forceinline__ void f10_gcomb11(GJ& acc, const unsigned char* u1be, const uint32_t* __restrict__ gtab11,
+                                            int w0, int w1) {
+    fe u;
+    load_be32(u, u1be); // little-endian words
     for (int i = w0; i < w1; i++) {
-        const unsigned byte = u1be[31 - i];
-        if (!byte) continue;
-        const uint32_t* e = gtab + ((size_t)i * 256 + byte) * 16;
+        const int bit = 11 * i, q = bit >> 5, sh = bit & 31;
+        const uint32_t lo = u.v[q], hi = q + 1 < 8 ? u.v[q + 1] : 0u;
+        const unsigned win = (unsigned)(((uint64_t)hi << 32 | lo) >> sh) & 2047u;
+        if (!win) continue;
+        const uint32_t* e = gtab11 + ((size_t)i * 2048 + win) * 16;
         FE gx, gy;
         f10_load_words(gx, e);
         f10_load_words(gy, e + 8);
@@ -1351,7 +1358,7 @@ template <bool DER>
 __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* __restrict__ msg,
                                                           const unsigned char* __restrict__ sig,
                                                           const unsigned char* __restrict__ pub,
-                                                          const uint32_t* __restrict__ gtab, uint8_t* __restrict__ out,
+                                                          const uint32_t* __restrict__ gtab11, uint8_t* __restrict__ out,
                                                           int n) {
     __shared__ Job sj[FSIG];
     __shared__ uint32_t tab[2][NPRE4][2][10][64]; // ladder wave, multiple, x|y, limb, lane
@@ -1376,7 +1383,7 @@ __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* _
     __syncthreads();
     if (wave == 0) {
         acc.inf = true;
-        f10_gcomb(acc, sj[lane].u1, gtab, 0, 32);
+        f10_gcomb11(acc, sj[lane].u1, gtab11, 0, G11_WINDOWS);
     } else {
         const int w = wave - 1, slot = w * 32 + (lane & 31), half = lane >> 5;
         const Job& J = sj[slot];
@@ -1437,7 +1444,7 @@ __global__ __launch_bounds__(FWG) void ecdsa_fused_kernel(const unsigned char* _
 // by the byte comb.
 constexpr int WG10 = 64;
 __global__ __launch_bounds__(WG10) void ecdsa_verify10_kernel(const Job* __restrict__ jobs,
-                                                              const uint32_t* __restrict__ gtab,
+                                                              const uint32_t* __restrict__ gtab11,
                                                               uint8_t* __restrict__ out, int n) {
     __shared__ uint32_t tab[NPRE4][2][10][WG10];
     const int tid = threadIdx.x;
@@ -1473,14 +1480,83 @@ __global__ __launch_bounds__(WG10) void ecdsa_verify10_kernel(const Job* __restr
         f10::mul(z, acc.z, zg); // back to the original curve
         acc.z = z;
     }
-    f10_gcomb(acc, J.u1, gtab, 0, 32);
+    f10_gcomb11(acc, J.u1, gtab11, 0, G11_WINDOWS);
     out[idx] = (ok && f10_check_r(acc, J) && J.scalar_ok) ? 1 : 0;
+}
+
+// The same work with one GLV half per lane (32 signatures per wave): lanes 0-31 run k1*Q plus
+// comb windows 0-11, lanes 32-63 k2*lambdaQ plus windows 12-23, and lane l adds lane l+32's point.
+// A wave takes about two thirds of ecdsa_verify10_kernel's time for half the signatures: the
+// launcher gives it the last, partly filled round of a batch (at most half a round), which the
+// one-lane kernel would stretch to a whole round (199,680 signatures = 3.05 rounds of 65,536).
+__global__ __launch_bounds__(WG10) void ecdsa_verify10h_kernel(const Job* __restrict__ jobs,
+                                                               const uint32_t* __restrict__ gtab11,
+                                                               uint8_t* __restrict__ out, int lo, int n) {
+    // lanes 32-63 hand their points over through the table's LDS once the table is dead (40 KiB
+    // per workgroup in all: 4 workgroups, one wave per SIMD, per CU)
+    __shared__ uint32_t tab[NPRE4][2][10][WG10];
+    uint32_t(&xr)[3][10][32] = *reinterpret_cast<uint32_t(*)[3][10][32]>(&tab[0][0][0][0]);
+    unsigned char* xinf = reinterpret_cast<unsigned char*>(&tab[0][0][0][0]) + sizeof(xr);
+    const int tid = threadIdx.x, half = tid >> 5, l0 = tid & 31;
+    const int idx = min(lo + (int)blockIdx.x * 32 + l0, n - 1); // past n: recompute the last one
+    const Job& J = jobs[idx];
+    FE qx, qy, bmul;
+    const bool ok = f10_decompress(qx, qy, J.pub);
+    if (half) bmul = f10_beta();
+    else f10::set_int(bmul, 1);
+    auto tb = [&](int m, int c, int k) -> uint32_t& { return tab[m][c][k][tid]; };
+    const FE zg = f10_odd_multiples(qx, qy, bmul, tb);
+    const bool hneg = J.neg[half] != 0;
+    GJ acc;
+    acc.inf = true;
+#pragma unroll 1
+    for (int b = REG4_DIGITS - 1; b >= 0; b--) {
+        if (b < REG4_DIGITS - 1) {
+#pragma unroll 1
+            for (int i = 0; i < 4; i++) {
+                GJ d;
+                f10::dbl(d, acc);
+                acc = d;
+            }
+        }
+        f10_add_digit(acc, reg4_digit(J, half, b), hneg, tb, nullptr);
+    }
+    if (J.pad[half]) f10_add_digit(acc, -1, hneg, tb, nullptr);
+    {
+        FE z;
+        f10::mul(z, acc.z, zg);
+        acc.z = z;
+    }
+    f10_gcomb11(acc, J.u1, gtab11, 12 * half, 12 * half + 12);
+    __syncthreads(); // every lane is past its last table read
+    if (half) {
+#pragma unroll
+        for (int k = 0; k < 10; k++) {
+            xr[0][k][l0] = acc.x.n[k];
+            xr[1][k][l0] = acc.y.n[k];
+            xr[2][k][l0] = acc.z.n[k];
+        }
+        xinf[l0] = acc.inf ? 1 : 0;
+    }
+    __syncthreads();
+    if (half || lo + (int)blockIdx.x * 32 + l0 >= n) return;
+    GJ q, s;
+#pragma unroll
+    for (int k = 0; k < 10; k++) {
+        q.x.n[k] = xr[0][k][l0];
+        q.y.n[k] = xr[1][k][l0];
+        q.z.n[k] = xr[2][k][l0];
+    }
+    q.inf = xinf[l0] != 0;
+    f10::add_gej(s, acc, q);
+    out[idx] = (ok && f10_check_r(s, J) && J.scalar_ok) ? 1 : 0;
 }
 
 // Generator comb table, one per HIP device (read-only once built, shared by every lane).
 struct Table {
     std::once_flag once;
-    uint32_t* d_gtab = nullptr;
+    uint32_t* d_gtab = nullptr;   // 8-bit comb (ecdsa_verify_kernel)
+    uint32_t* d_gtab11 = nullptr; // 11-bit comb (the 10 x 26 kernels)
 };
 constexpr int MAX_DEVICES = 64;
 Table& T(int device) {
@@ -1490,10 +1566,9 @@ Table& T(int device) {
 }
 
 // Builds the table on the current device (the caller made `tb`'s device current).
-void InitTable(Table& tb) {
-    // 32 x 256 affine points, 8 LE limbs for x then y
-    const std::vector<secp::Ge>& t = secp::generator_table();
-    std::vector<uint32_t> h(32 * 256 * 16, 0);
+// affine points as 8 LE limbs of x then 8 of y (the point at infinity stays zero, never read)
+std::vector<uint32_t> TableWords(const std::vector<secp::Ge>& t) {
+    std::vector<uint32_t> h(t.size() * 16, 0);
     for (size_t e = 0; e < t.size(); e++) {
         unsigned char bx[32], by[32];
         if (t[e].inf) continue;
@@ -1506,8 +1581,17 @@ void InitTable(Table& tb) {
             h[e * 16 + 8 + k] = ((uint32_t)q[0] << 24) | ((uint32_t)q[1] << 16) | ((uint32_t)q[2] << 8) | q[3];
         }
     }
+    return h;
+}
+
+// Builds the tables on the current device (the caller made `tb`'s device current).
+void InitTable(Table& tb) {
+    const std::vector<uint32_t> h = TableWords(secp::generator_table());     // 32 x 256
+    const std::vector<uint32_t> h11 = TableWords(secp::generator_table11()); // 24 x 2048
     BCP_HIP_CHECK(hipMalloc(&tb.d_gtab, h.size() * 4));
     BCP_HIP_CHECK(hipMemcpy(tb.d_gtab, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+    BCP_HIP_CHECK(hipMalloc(&tb.d_gtab11, h11.size() * 4));
+    BCP_HIP_CHECK(hipMemcpy(tb.d_gtab11, h11.data(), h11.size() * 4, hipMemcpyHostToDevice));
 }
 
 } // namespace
@@ -1530,28 +1614,55 @@ std::atomic<size_t> g_fusedMax{BCP_ECDSA_FUSED_MAX};
 std::atomic<int> g_splitKernel{BCP_ECDSA_SPLIT_KERNEL};
 
 namespace {
+// compute units of the current device (cached per device)
+int DeviceCUs() {
+    static std::atomic<int> cus[MAX_DEVICES];
+    int dev = 0;
+    BCP_HIP_CHECK(hipGetDevice(&dev));
+    if (dev < 0 || dev >= MAX_DEVICES) return 256;
+    int c = cus[dev].load(std::memory_order_relaxed);
+    if (!c) {
+        BCP_HIP_CHECK(hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev));
+        cus[dev].store(c, std::memory_order_relaxed);
+    }
+    return c;
+}
 // Batches up to EcdsaFusedMax() run the fused latency kernel (no job records); larger ones the
 // prep + verify throughput pair.
 void LaunchVerify(bool der, const unsigned char* dm, const unsigned char* ds, const unsigned char* dp, Job* d_jobs,
-                  const uint32_t* gtab, uint8_t* d_out, size_t n, hipStream_t stream) {
+                  const Table& tb, uint8_t* d_out, size_t n, hipStream_t stream) {
+    const uint32_t* gtab = tb.d_gtab;
+    const uint32_t* gtab11 = tb.d_gtab11;
     if (n <= g_fusedMax.load(std::memory_order_relaxed)) {
         const dim3 fg((unsigned)((n + FSIG - 1) / FSIG));
-        if (der) hipLaunchKernelGGL(ecdsa_fused_kernel<true>, fg, dim3(FWG), 0, stream, dm, ds, dp, gtab, d_out, (int)n);
-        else hipLaunchKernelGGL(ecdsa_fused_kernel<false>, fg, dim3(FWG), 0, stream, dm, ds, dp, gtab, d_out, (int)n);
+        if (der) hipLaunchKernelGGL(ecdsa_fused_kernel<true>, fg, dim3(FWG), 0, stream, dm, ds, dp, gtab11, d_out, (int)n);
+        else hipLaunchKernelGGL(ecdsa_fused_kernel<false>, fg, dim3(FWG), 0, stream, dm, ds, dp, gtab11, d_out, (int)n);
         BCP_HIP_CHECK(hipGetLastError());
         return;
     }
     const dim3 pg((unsigned)((n + 255) / 256));
-    const bool k10 = g_splitKernel.load(std::memory_order_relaxed) == 1; // window-4 digits for the 10 x 26 kernel
+    const int sk = g_splitKernel.load(std::memory_order_relaxed);
+    const bool k10 = sk != 0; // window-4 digits for the 10 x 26 kernels
     if (der && k10) hipLaunchKernelGGL((ecdsa_prep_kernel<true, true>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
     else if (der) hipLaunchKernelGGL((ecdsa_prep_kernel<true, false>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
     else if (k10) hipLaunchKernelGGL((ecdsa_prep_kernel<false, true>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
     else hipLaunchKernelGGL((ecdsa_prep_kernel<false, false>), pg, dim3(256), 0, stream, d_jobs, dm, ds, dp, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
-    if (k10)
-        hipLaunchKernelGGL(ecdsa_verify10_kernel, dim3((unsigned)((n + WG10 - 1) / WG10)), dim3(WG10), 0, stream, d_jobs,
-                           gtab, d_out, (int)n);
-    else
+    if (k10) {
+        // one-lane kernel for whole rounds (one wave per SIMD: CUs x 4 x 64 signatures), the
+        // half-lane kernel for a last round at most half full
+        const size_t round = (size_t)DeviceCUs() * 4 * 64;
+        size_t nf = n / round * round;
+        if (n - nf > round / 2) nf = n;
+        if (sk == 2) nf = n; // pinned: one-lane kernel only
+        if (sk == 3) nf = 0; // pinned: half-lane kernel only
+        if (nf)
+            hipLaunchKernelGGL(ecdsa_verify10_kernel, dim3((unsigned)((nf + WG10 - 1) / WG10)), dim3(WG10), 0, stream,
+                               d_jobs, gtab11, d_out, (int)nf);
+        if (nf < n)
+            hipLaunchKernelGGL(ecdsa_verify10h_kernel, dim3((unsigned)((n - nf + 31) / 32)), dim3(WG10), 0, stream,
+                               d_jobs, gtab11, d_out, (int)nf, (int)n);
+    } else
         hipLaunchKernelGGL(ecdsa_verify_kernel, dim3((unsigned)((n + WG - 1) / WG)), dim3(WG), 0, stream, d_jobs, gtab,
                            d_out, (int)n);
     BCP_HIP_CHECK(hipGetLastError());
@@ -1559,7 +1670,7 @@ void LaunchVerify(bool der, const unsigned char* dm, const unsigned char* ds, co
 } // namespace
 
 void SetEcdsaFusedMax(size_t n) { g_fusedMax.store(n, std::memory_order_relaxed); }
-void SetEcdsaSplitKernel(int k) { g_splitKernel.store(k == 1 ? 1 : 0, std::memory_order_relaxed); }
+void SetEcdsaSplitKernel(int k) { g_splitKernel.store(k >= 0 && k <= 3 ? k : 1, std::memory_order_relaxed); }
 int EcdsaSplitKernel() { return g_splitKernel.load(std::memory_order_relaxed); }
 size_t EcdsaFusedMax() { return g_fusedMax.load(std::memory_order_relaxed); }
 
@@ -1584,7 +1695,7 @@ void LaneEcdsa(LaneState& L, size_t n, size_t sigBytes,
     uint8_t* d_out = L.Dev(2, n);
     BCP_HIP_CHECK(hipMemcpyAsync(d_in, h_in, bytes, hipMemcpyHostToDevice, L.stream));
     const unsigned char *dm = d_in, *ds = d_in + n * 32, *dp = d_in + n * (32 + sigBytes);
-    LaunchVerify(sigBytes != 64, dm, ds, dp, d_jobs, tb.d_gtab, d_out, n, L.stream);
+    LaunchVerify(sigBytes != 64, dm, ds, dp, d_jobs, tb, d_out, n, L.stream);
     BCP_HIP_CHECK(hipMemcpyAsync(h_out, d_out, n, hipMemcpyDeviceToHost, L.stream));
     BCP_HIP_CHECK(hipStreamSynchronize(L.stream));
     memcpy(result, h_out, n);
@@ -1617,7 +1728,7 @@ void EcdsaVerifyDevice(const void* msg32, const void* sig64, const void* pub33, 
     std::call_once(tb.once, [&] { InitTable(tb); });
     const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     LaunchVerify(false, static_cast<const unsigned char*>(msg32), static_cast<const unsigned char*>(sig64),
-                 static_cast<const unsigned char*>(pub33), static_cast<Job*>(jobs), tb.d_gtab,
+                 static_cast<const unsigned char*>(pub33), static_cast<Job*>(jobs), tb,
                  static_cast<uint8_t*>(result), n, s);
 }
 

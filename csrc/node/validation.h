@@ -99,6 +99,9 @@ struct MempoolAcceptResult {
     Amount fee = 0;
 };
 
+// A block's undo record serialised for disk (the bytes of SerializeToBytes(undo, SER_DISK)),
+// transaction chunks in parallel on `pool` when given.
+std::vector<unsigned char> SerializeBlockUndo(const CBlockUndo& undo, WorkerPool* pool);
 // GetSerializeSize(block, version) from the transactions' cached sizes.
 uint64_t BlockSerializeSize(const CBlock& block, int version);
 // -maxscriptcachesize (MiB): resize the script-execution cache; returns its capacity.

@@ -88,6 +88,8 @@ struct EcmultGenTrace {
 void ecmult_gen_trace(EcmultGenTrace* t);
 // Affine comb table, entry [i*256 + j] = j * 256^i * G (j = 0 is the point at infinity).
 const std::vector<Ge>& generator_table();                                  // k*G
+// Entry [i*2048 + j] = j * 2^(11 i) * G, i < 24 (the GPU's 11-bit comb; j = 0 is infinity).
+const std::vector<Ge>& generator_table11();
 void ecmult(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng);     // na*A + ng*G (GLV)
 void ecmult_plain(Gej& r, const Gej& a, const Scalar& na, const Scalar& ng); // same, no endomorphism
 bool glv_check(const Scalar& k); // the GLV split of k recombines to k with halves < 2^130 (tests)

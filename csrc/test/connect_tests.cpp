@@ -373,3 +373,30 @@ TEST_CASE(connectblock_tests, recent_block_cache_out_of_order) {
         if (system(cmd.c_str()) != 0) {}
     }
 }
+
+// The parallel undo serialiser writes the same bytes as the plain serialiser (the on-disk
+// record's checksum and every later DisconnectBlock depend on it).
+TEST_CASE(connectblock_tests, undo_serialisation_parallel_matches) {
+    std::mt19937_64 rng(7);
+    CBlockUndo undo;
+    undo.vtxundo.resize(5000);
+    for (CTxUndo& tu : undo.vtxundo) {
+        tu.vprevout.resize(1 + rng() % 3);
+        for (Coin& c : tu.vprevout) {
+            c.nHeight = (uint32_t)(rng() % 700000);
+            c.fCoinBase = rng() % 7 == 0;
+            c.out.nValue = (Amount)(rng() % 2100000000000000ULL);
+            std::vector<unsigned char> h(20);
+            for (auto& b : h) b = (unsigned char)rng();
+            if (rng() % 4) c.out.scriptPubKey = CScript() << OP_DUP << OP_HASH160 << h << OP_EQUALVERIFY << OP_CHECKSIG;
+            else c.out.scriptPubKey = CScript() << OP_RETURN << std::vector<unsigned char>(rng() % 80, 0xab);
+        }
+    }
+    WorkerPool pool(4);
+    const std::vector<unsigned char> plain = SerializeToBytes(undo, SER_DISK, PROTOCOL_VERSION);
+    CHECK(SerializeBlockUndo(undo, &pool) == plain);
+    CHECK(SerializeBlockUndo(undo, nullptr) == plain);
+    CBlockUndo small;
+    small.vtxundo.assign(undo.vtxundo.begin(), undo.vtxundo.begin() + 10);
+    CHECK(SerializeBlockUndo(small, &pool) == SerializeToBytes(small, SER_DISK, PROTOCOL_VERSION));
+}

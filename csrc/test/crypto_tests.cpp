@@ -352,3 +352,39 @@ TEST_CASE(crypto_tests, secp256k1_branchfree_field_scalar) {
         CHECK_EQ(shex(p), std::string(63, '0') + "1");
     }
 }
+
+// The GPU's 11-bit comb table: entry [i*2048 + j] = j * 2^(11 i) * G, checked against
+// ecmult_gen_var of the same scalar (j = 0 is the point at infinity).
+TEST_CASE(crypto_tests, secp256k1_generator_table11) {
+    const std::vector<secp::Ge>& t = secp::generator_table11();
+    REQUIRE(t.size() == (size_t)24 * 2048);
+    for (int i : {0, 1, 7, 22, 23}) {
+        for (int j : {0, 1, 2, 3, 1000, 2047}) {
+            const secp::Ge& e = t[(size_t)i * 2048 + j];
+            if (j == 0) {
+                CHECK(e.inf);
+                continue;
+            }
+            // k = j << 11i as a big-endian 32-byte scalar (< 2^264 only for i = 23, j >= 8:
+            // reduced mod n by sc_set_b32 like the table's own doublings)
+            unsigned char b[33] = {0};
+            const int bit = 11 * i;
+            for (int q = 0; q < 12; q++) {
+                const int pos = bit + q; // bit position of bit q of j
+                if (!((j >> q) & 1) || pos >= 256) continue;
+                b[32 - pos / 8] |= (unsigned char)(1u << (pos % 8));
+            }
+            const bool overflowBits = i == 23 && (j >> 3) != 0; // bits past 2^256: skip (not used by u1 < n)
+            if (overflowBits) continue;
+            secp::Scalar k;
+            secp::sc_set_b32(k, b + 1);
+            secp::Gej r;
+            secp::ecmult_gen_var(r, k);
+            secp::Ge a;
+            secp::ge_set_gej(a, r);
+            CHECK(!e.inf);
+            CHECK(secp::fe_equal(a.x, e.x));
+            CHECK(secp::fe_equal(a.y, e.y));
+        }
+    }
+}

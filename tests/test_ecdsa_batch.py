@@ -48,13 +48,13 @@ def make_items(native, n, seed=7):
     return items, expect
 
 
-PATHS = {"fused": (1 << 40, None), "split8": (0, 0), "split10": (0, 1)}
+PATHS = {"fused": (1 << 40, None), "split8": (0, 0), "split10": (0, 2), "split10h": (0, 3)}
 
 
 def pin_path(native, name):
     """Pins one GPU path: the fused latency kernel (every batch size) or the prep + verify
-    throughput kernels (never fused) with the 8 x 32 or the 10 x 26 verify kernel. Returns the
-    previous settings for unpin_path."""
+    throughput kernels (never fused) with the 8 x 32, the one-lane 10 x 26 or the half-lane
+    10 x 26 verify kernel. Returns the previous settings for unpin_path."""
     old = (native.ecdsa_fused_max(), native.ecdsa_split_kernel())
     fmax, sk = PATHS[name]
     native.ecdsa_set_fused_max(fmax)
@@ -188,3 +188,25 @@ def test_gpu_fused_partial_workgroups(native):
             finally:
                 unpin_path(native, old)
             assert got == expect[:n], (n, name)
+
+
+@pytest.mark.gpu
+def test_gpu_split10_rounds_and_tail(native):
+    """The 10 x 26 split path gives whole device rounds (one wave per SIMD: CUs x 256
+    signatures) to the one-lane kernel and a last round at most half full to the half-lane
+    kernel: a batch of one round plus 1000 takes both kernels (on 256 CUs), and every path
+    agrees with the expected verdicts."""
+    items, expect = make_items(native, 1100, seed=5)
+    n = 65536 + 1000
+    reps = n // len(items) + 1
+    big, want = (items * reps)[:n], (expect * reps)[:n]
+    for name, sk in (("auto", 1), ("split8", 0)):
+        old = (native.ecdsa_fused_max(), native.ecdsa_split_kernel())
+        native.ecdsa_set_fused_max(0)
+        native.ecdsa_set_split_kernel(sk)
+        try:
+            got, _ = native.ecdsa_verify_batch(big, use_gpu=True, threads=16)
+        finally:
+            unpin_path(native, old)
+        bad = [i for i in range(n) if got[i] != want[i]]
+        assert not bad, (name, bad[:10])

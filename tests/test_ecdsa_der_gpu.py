@@ -57,7 +57,7 @@ def _variants(r, s):
     yield "huge_len", b"\x30\x06\x02\x88" + b"\x01" * 8 + b"\x02\x01\x01", False
 
 
-@pytest.mark.parametrize("path", ["fused", "split8", "split10"])
+@pytest.mark.parametrize("path", ["fused", "split8", "split10", "split10h"])
 def test_device_der_parse_matches_cpu(native, path):
     from test_ecdsa_batch import pin_path, unpin_path
     old = pin_path(native, path)

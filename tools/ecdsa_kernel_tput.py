@@ -4,7 +4,9 @@ already sit on the GPU (no host parse, no copies), timed with HIP events, best o
 For each batch size it times the three device paths:
   fused    ecdsa_fused_kernel (ecdsa_set_fused_max(huge))
   split8   ecdsa_prep_kernel + ecdsa_verify_kernel (8 x 32 field)
-  split10  ecdsa_prep_kernel + ecdsa_verify10_kernel (10 x 26 field, global-z table)
+  split10  ecdsa_prep_kernel + ecdsa_verify10_kernel (10 x 26 field, global-z table) for whole
+           rounds of the device and ecdsa_verify10h_kernel (one GLV half per lane) for the rest
+  split10-1lane  the one-lane kernel for the whole batch
 and checks that every signature verified. One JSON line per (n, path), then a summary line.
 Usage: python tools/ecdsa_kernel_tput.py [n ...]
 """
@@ -50,7 +52,7 @@ jobs = torch.empty(nmax * nat.ecdsa_job_bytes(), dtype=torch.uint8, device=dev)
 out = torch.empty(nmax, dtype=torch.uint8, device=dev)
 stream = torch.cuda.current_stream().cuda_stream
 fused0, split0 = nat.ecdsa_fused_max(), nat.ecdsa_split_kernel()
-paths = {"fused": (1 << 40, split0), "split8": (0, 0), "split10": (0, 1)}
+paths = {"fused": (1 << 40, split0), "split8": (0, 0), "split10": (0, 1), "split10-1lane": (0, 2)}
 rows = []
 try:
     for n in sizes:
