@@ -306,17 +306,25 @@ void CCoinsViewCache::MergeShard(CCoinsMap::Shard& from, unsigned s) {
     // the child's entries are left in place (moved-from) and freed with the child's map
     for (auto it = from.begin(); it != from.end(); ++it) {
         if (!(it->second.flags & CCoinsCacheEntry::DIRTY)) continue; // non-dirty: nothing to merge
-        auto itUs = ours.find(it->first);
-        if (itUs == ours.end()) {
-            // child has a modified entry the parent lacks; a FRESH spent one can be dropped
-            if (!(it->second.flags & CCoinsCacheEntry::FRESH && it->second.coin.IsSpent())) {
-                CCoinsCacheEntry& entry = ours[it->first];
+        CCoinsMap::Shard::iterator itUs;
+        if (it->second.flags & CCoinsCacheEntry::FRESH && it->second.coin.IsSpent()) {
+            // created and spent in the child: nothing to add; only a spent parent copy matters
+            itUs = ours.find(it->first);
+            if (itUs == ours.end()) continue;
+        } else {
+            // one hash and probe for the common insert (a coin the block created)
+            bool inserted;
+            std::tie(itUs, inserted) = ours.try_emplace(it->first);
+            if (inserted) {
+                CCoinsCacheEntry& entry = itUs->second;
                 entry.coin = std::move(it->second.coin);
                 used += entry.coin.DynamicMemoryUsage();
                 entry.flags = CCoinsCacheEntry::DIRTY;
                 if (it->second.flags & CCoinsCacheEntry::FRESH) entry.flags |= CCoinsCacheEntry::FRESH;
+                continue;
             }
-        } else {
+        }
+        {
             if ((it->second.flags & CCoinsCacheEntry::FRESH) && !itUs->second.coin.IsSpent())
                 throw std::logic_error("FRESH flag misapplied to cache entry for base transaction with spendable outputs");
             if ((itUs->second.flags & CCoinsCacheEntry::FRESH) && it->second.coin.IsSpent()) {
