@@ -4,9 +4,14 @@
 // and destdata, which the reference reads back through a fresh CWalletDB). Coins here are
 // in-memory wallet transactions; "from me" coins really spend one of the wallet's own outputs.
 #include "test/unittest.h"
+#include "node/kvstore.h"
+#include "wallet/bdbimport.h"
 #include "wallet/wallet.h"
 
 #include <cmath>
+#include <fstream>
+#include <set>
+#include <sstream>
 #include <deque>
 #include <unistd.h>
 
@@ -234,6 +239,226 @@ TEST_CASE(walletdb_tests, address_book_records_persist) {
         CHECK(!w.GetDestData(b, "rr1", &v));
     }
     std::string cmd = std::string("rm -rf '") + tmpl + "'";
+    CHECK(std::system(cmd.c_str()) == 0);
+}
+
+namespace {
+// A Berkeley DB 4.x btree file as the reference's wallet.dat has it (a master database listing
+// the sub-database "main", whose tree is an internal page over leaf pages, big items in overflow
+// chains), written from the page layout of db_page.h. No libdb exists here to write a real one,
+// so this pins the reader against that layout only.
+struct BdbWriter {
+    explicit BdbWriter(size_t pagesize) : P(pagesize) {}
+    size_t P;
+    std::vector<std::string> pages;
+    static void put16(std::string& pg, size_t off, uint32_t v) {
+        pg[off] = (char)(v & 0xff);
+        pg[off + 1] = (char)((v >> 8) & 0xff);
+    }
+    static void put32(std::string& pg, size_t off, uint32_t v) {
+        for (int i = 0; i < 4; i++) pg[off + i] = (char)((v >> (8 * i)) & 0xff);
+    }
+    uint32_t NewPage(uint8_t type) {
+        pages.emplace_back(P, '\0');
+        const uint32_t pg = (uint32_t)pages.size() - 1;
+        put32(pages[pg], 8, pg);
+        pages[pg][25] = (char)type;
+        return pg;
+    }
+    void Meta(uint32_t pg, uint32_t root, bool subdbs) {
+        std::string& m = pages[pg];
+        put32(m, 12, 0x053162);
+        put32(m, 16, 9); // btree version
+        put32(m, 20, (uint32_t)P);
+        m[25] = 9;
+        put32(m, 48, subdbs ? 0x20 : 0);
+        put32(m, 88, root);
+    }
+    // item bytes: inline B_KEYDATA, or a B_OVERFLOW reference to a new overflow chain
+    std::string Item(const std::string& v) {
+        if (3 + v.size() <= P / 4) {
+            std::string it(3, '\0');
+            put16(it, 0, (uint32_t)v.size());
+            it[2] = 1;
+            return it + v;
+        }
+        uint32_t first = 0, prev = 0;
+        for (size_t off = 0; off < v.size(); off += P - 26) {
+            const uint32_t pg = NewPage(7);
+            const size_t len = std::min(P - 26, v.size() - off);
+            put16(pages[pg], 22, (uint32_t)len);
+            pages[pg].replace(26, len, v.substr(off, len));
+            if (off == 0) first = pg;
+            else put32(pages[prev], 16, pg);
+            prev = pg;
+        }
+        std::string it(12, '\0');
+        it[2] = 3;
+        put32(it, 4, first);
+        put32(it, 8, (uint32_t)v.size());
+        return it;
+    }
+    // leaf pages of (key, value) pairs; returns their page numbers
+    std::vector<uint32_t> Leaves(const std::vector<std::pair<std::string, std::string>>& recs) {
+        std::vector<uint32_t> leaves;
+        uint32_t pg = 0;
+        size_t n = 0, top = P;
+        for (const auto& kv : recs) {
+            const std::string a = Item(kv.first), b = Item(kv.second);
+            if (!leaves.size() || 26 + 2 * (n + 2) + (a.size() + b.size()) > top) {
+                pg = NewPage(5);
+                leaves.push_back(pg);
+                n = 0;
+                top = P;
+            }
+            for (const std::string* it : {&a, &b}) {
+                top -= it->size();
+                pages[pg].replace(top, it->size(), *it);
+                put16(pages[pg], 26 + 2 * n, (uint32_t)top);
+                put16(pages[pg], 20, (uint32_t)++n);
+            }
+        }
+        return leaves;
+    }
+    uint32_t Internal(const std::vector<uint32_t>& children) {
+        const uint32_t pg = NewPage(3);
+        size_t top = P;
+        for (size_t i = 0; i < children.size(); i++) {
+            std::string it(12, '\0');
+            it[2] = 1;
+            put32(it, 4, children[i]);
+            top -= it.size();
+            pages[pg].replace(top, it.size(), it);
+            put16(pages[pg], 26 + 2 * i, (uint32_t)top);
+        }
+        put16(pages[pg], 20, (uint32_t)children.size());
+        pages[pg][24] = 2; // level
+        return pg;
+    }
+    std::string File(const std::vector<std::pair<std::string, std::string>>& recs) {
+        NewPage(9); // 0: master meta
+        const uint32_t mleaf = NewPage(5), smeta = NewPage(9);
+        const std::vector<uint32_t> leaves = Leaves(recs);
+        const uint32_t root = Internal(leaves);
+        Meta(smeta, root, false);
+        // master leaf: "main" -> the sub-database's meta page
+        std::string pg4(4, '\0');
+        put32(pg4, 0, smeta);
+        const std::string a = Item("main"), b = Item(pg4);
+        pages[mleaf].replace(P - a.size(), a.size(), a);
+        pages[mleaf].replace(P - a.size() - b.size(), b.size(), b);
+        put16(pages[mleaf], 26, (uint32_t)(P - a.size()));
+        put16(pages[mleaf], 28, (uint32_t)(P - a.size() - b.size()));
+        put16(pages[mleaf], 20, 2);
+        Meta(0, mleaf, true);
+        put32(pages[0], 32, (uint32_t)pages.size() - 1); // last_pgno
+        std::string f;
+        for (const auto& p : pages) f += p;
+        return f;
+    }
+};
+
+std::string HexOf(const std::string& s) {
+    static const char* d = "0123456789abcdef";
+    std::string o;
+    for (unsigned char c : s) {
+        o += d[c >> 4];
+        o += d[c & 15];
+    }
+    return o;
+}
+} // namespace
+
+// A wallet's records written as a reference wallet.dat (BDB btree file, and db_dump text) are
+// imported by the loader's conversion and load back with the same keys, names and data.
+TEST_CASE(walletdb_tests, bdb_wallet_import) {
+    char tmpl[] = "/tmp/bcp_bdbimport_XXXXXX";
+    REQUIRE(mkdtemp(tmpl) != nullptr);
+    const std::string dir = tmpl;
+    std::set<CKeyID> keys;
+    CKey k;
+    k.MakeNewKey(true);
+    const CTxDestination a = k.GetPubKey().GetID();
+    const std::string big(6000, 'z'); // an overflow item in a 4 KiB page file
+    {
+        CWallet w("src", dir + "/src", false);
+        std::string err;
+        bool first = false;
+        REQUIRE(w.Load(err, first));
+        REQUIRE(w.SetHDMasterKey(w.GenerateNewHDMasterKey()));
+        REQUIRE(w.TopUpKeyPool(30));
+        CHECK(w.SetAddressBook(a, "alice", "receive"));
+        CHECK(w.AddDestData(a, "rr0", big));
+        keys = w.GetKeys();
+        w.Flush();
+    }
+    REQUIRE(keys.size() >= 30);
+    std::vector<std::pair<std::string, std::string>> recs;
+    {
+        KVStore db(dir + "/src", false, false);
+        KVIterator it(&db);
+        for (it.SeekToFirst(); it.Valid(); it.Next()) {
+            std::string v;
+            it.RawValue(v);
+            recs.emplace_back(it.RawKey(), v);
+        }
+    }
+    REQUIRE(recs.size() > 60);
+    // the btree file
+    {
+        std::ofstream f(dir + "/wallet.dat", std::ios::binary);
+        const std::string bytes = BdbWriter(4096).File(recs);
+        f.write(bytes.data(), bytes.size());
+    }
+    BdbRecords got;
+    std::string err;
+    REQUIRE(ReadBdbBtree(dir + "/wallet.dat", got, err));
+    CHECK(got == recs);
+    CHECK_EQ(BdbFileKind(dir + "/wallet.dat"), std::string("btree"));
+    size_t n = 0;
+    REQUIRE(ImportBdbWalletFile(dir + "/wallet.dat", n, err));
+    CHECK_EQ(n, recs.size());
+    CHECK(BdbFileKind(dir + "/wallet.dat").empty()); // now this wallet's store
+    {
+        CWallet w("wallet.dat", dir + "/wallet.dat", false);
+        bool first = true;
+        REQUIRE(w.Load(err, first));
+        CHECK(!first);
+        CHECK(w.GetKeys() == keys);
+        CHECK(w.IsHDEnabled());
+        CHECK_EQ(w.mapAddressBook[a].name, std::string("alice"));
+        std::string v;
+        CHECK(w.GetDestData(a, "rr0", &v) && v == big);
+    }
+    // the db_dump text of the same records
+    {
+        std::ofstream f(dir + "/dump.dat");
+        f << "VERSION=3\nformat=bytevalue\ndatabase=main\ntype=btree\ndb_pagesize=4096\nHEADER=END\n";
+        for (const auto& kv : recs) f << " " << HexOf(kv.first) << "\n " << HexOf(kv.second) << "\n";
+        f << "DATA=END\n";
+    }
+    CHECK_EQ(BdbFileKind(dir + "/dump.dat"), std::string("dump"));
+    REQUIRE(ImportBdbWalletFile(dir + "/dump.dat", n, err));
+    CHECK_EQ(n, recs.size());
+    {
+        CWallet w("dump.dat", dir + "/dump.dat", false);
+        bool first = true;
+        REQUIRE(w.Load(err, first));
+        CHECK(w.GetKeys() == keys);
+    }
+    // damaged files fail cleanly
+    {
+        std::string bytes = BdbWriter(4096).File(recs);
+        std::ofstream(dir + "/trunc.dat", std::ios::binary).write(bytes.data(), 4096 * 3);
+        CHECK(!ReadBdbBtree(dir + "/trunc.dat", got, err));
+        for (size_t i = 4096; i < bytes.size(); i += 97) bytes[i] = (char)(bytes[i] ^ 0x5a); // scribble on every page
+        std::ofstream(dir + "/bad.dat", std::ios::binary).write(bytes.data(), bytes.size());
+        got.clear();
+        ReadBdbBtree(dir + "/bad.dat", got, err); // any verdict, but bounded and no crash
+        std::istringstream dump("VERSION=3\nHEADER=END\n 00\nDATA=END\n");
+        CHECK(!ReadBdbDump(dump, got, err)); // a key without a value
+    }
+    std::string cmd = "rm -rf '" + dir + "'";
     CHECK(std::system(cmd.c_str()) == 0);
 }
 

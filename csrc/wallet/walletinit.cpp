@@ -8,6 +8,7 @@
 #include "node/validation.h"
 #include "rpc/server.h"
 #include "util/strencodings.h"
+#include "wallet/bdbimport.h"
 #include "wallet/wallet.h"
 
 #include <cstdio>
@@ -101,6 +102,14 @@ static bool SalvageWallet(const std::string& path, std::string& err) {
 static bool LoadOneWallet(NodeContext& node, const std::string& name, std::string& err) {
     Chainstate& cs = *node.chainstate;
     const std::string path = node.datadir + "/" + name;
+    if (!BdbFileKind(path).empty()) {
+        // a reference wallet.dat (Berkeley DB file or db_dump text): its records become this store
+        size_t n = 0;
+        if (!ImportBdbWalletFile(path, n, err)) {
+            err = "Error importing Berkeley DB wallet " + name + ": " + err;
+            return false;
+        }
+    }
     if (gArgs.GetBoolArg("-salvagewallet", false) && !SalvageWallet(path, err)) return false;
     std::unique_ptr<CWallet> w(new CWallet(name, path, false));
     bool firstRun = false;
