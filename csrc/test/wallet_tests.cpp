@@ -404,6 +404,39 @@ TEST_CASE(walletdb_tests, bdb_wallet_import) {
         }
     }
     REQUIRE(recs.size() > 60);
+    // unencrypted keys as the reference writes them: the DER SEC1 ECPrivateKey (version 1, the
+    // secret, tagged curve parameters, the public key) plus a trailing 32-byte hash
+    size_t nKeyRecs = 0;
+    for (auto& kv : recs) {
+        SpanReader kr((const unsigned char*)kv.first.data(), kv.first.size(), SER_DISK, PROTOCOL_VERSION);
+        std::string type;
+        kr >> type;
+        if (type != "key") continue;
+        CPubKey pub;
+        kr >> pub;
+        SpanReader vr((const unsigned char*)kv.second.data(), kv.second.size(), SER_DISK, PROTOCOL_VERSION);
+        std::vector<unsigned char> secret;
+        vr >> secret;
+        REQUIRE(secret.size() == 32);
+        std::vector<unsigned char> inner = {0x02, 0x01, 0x01, 0x04, 0x20};
+        inner.insert(inner.end(), secret.begin(), secret.end());
+        const std::vector<unsigned char> params = {0xa0, 0x03, 0x06, 0x01, 0x00};
+        inner.insert(inner.end(), params.begin(), params.end());
+        inner.push_back(0xa1);
+        inner.push_back((unsigned char)(pub.size() + 3));
+        inner.push_back(0x03);
+        inner.push_back((unsigned char)(pub.size() + 1));
+        inner.push_back(0x00);
+        inner.insert(inner.end(), pub.begin(), pub.end());
+        std::vector<unsigned char> der = {0x30, 0x81, (unsigned char)inner.size()};
+        der.insert(der.end(), inner.begin(), inner.end());
+        std::vector<unsigned char> v;
+        VectorWriter w(v, SER_DISK, PROTOCOL_VERSION);
+        w << der << uint256();
+        kv.second.assign(v.begin(), v.end());
+        nKeyRecs++;
+    }
+    REQUIRE(nKeyRecs >= 30);
     // the btree file
     {
         std::ofstream f(dir + "/wallet.dat", std::ios::binary);

@@ -235,12 +235,67 @@ bool ReadBdbDump(std::istream& in, BdbRecords& out, std::string& err) {
 } // namespace bcp
 
 #include "node/kvstore.h"
+#include "crypto/common.h"
+#include "primitives/serialize.h"
 #include "util/strencodings.h"
 #include "util/util.h"
 
 #include <cstdio>
 
 namespace bcp {
+
+namespace {
+// The reference stores an unencrypted wallet key ("key" record) as the DER SEC1 ECPrivateKey
+// its CKey::GetPrivKey exports (src/key.cpp ec_privkey_export_der: SEQUENCE { INTEGER 1,
+// OCTET STRING secret, [0] curve parameters, [1] public key }), optionally followed by a hash;
+// this wallet stores the 32-byte secret. The secret is the OCTET STRING after the version.
+bool Sec1Secret(const std::vector<unsigned char>& der, std::vector<unsigned char>& secret) {
+    size_t p = 0;
+    const size_t n = der.size();
+    auto len = [&](size_t& out) -> bool {
+        if (p >= n) return false;
+        const unsigned b = der[p++];
+        if (b < 0x80) {
+            out = b;
+            return true;
+        }
+        const unsigned k = b & 0x7f;
+        if (k == 0 || k > 2 || p + k > n) return false;
+        out = 0;
+        for (unsigned i = 0; i < k; i++) out = (out << 8) | der[p++];
+        return true;
+    };
+    size_t l = 0;
+    if (p >= n || der[p++] != 0x30 || !len(l) || p + l > n) return false;
+    if (p + 3 > n || der[p] != 0x02 || der[p + 1] != 0x01 || der[p + 2] != 0x01) return false;
+    p += 3;
+    if (p >= n || der[p++] != 0x04 || !len(l) || l == 0 || l > 32 || p + l > n) return false;
+    secret.assign(32 - l, 0);
+    secret.insert(secret.end(), der.begin() + p, der.begin() + p + l);
+    return true;
+}
+
+// A "key" record's value in this wallet's form (the 32-byte secret); other records unchanged.
+void ConvertRecord(const std::string& key, std::string& value) {
+    std::string type;
+    try {
+        SpanReader r((const unsigned char*)key.data(), key.size(), SER_DISK, PROTOCOL_VERSION);
+        r >> type;
+        if (type != "key") return;
+        SpanReader v((const unsigned char*)value.data(), value.size(), SER_DISK, PROTOCOL_VERSION);
+        std::vector<unsigned char> der, secret;
+        v >> der;
+        if (der.size() == 32 || !Sec1Secret(der, secret)) return; // already a bare secret, or unknown
+        std::vector<unsigned char> out;
+        VectorWriter w(out, SER_DISK, PROTOCOL_VERSION);
+        w << secret;
+        value.assign(out.begin(), out.end());
+        memory_cleanse(secret.data(), secret.size());
+        memory_cleanse(der.data(), der.size());
+    } catch (const std::exception&) {
+    }
+}
+} // namespace
 
 bool ImportBdbWalletFile(const std::string& path, size_t& imported, std::string& err) {
     const std::string kind = BdbFileKind(path);
@@ -261,7 +316,10 @@ bool ImportBdbWalletFile(const std::string& path, size_t& imported, std::string&
     }
     KVStore fresh(path, false, true);
     KVBatch b;
-    for (const auto& kv : recs) b.WriteRaw(kv.first, kv.second);
+    for (auto& kv : recs) {
+        ConvertRecord(kv.first, kv.second);
+        b.WriteRaw(kv.first, kv.second);
+    }
     if (!fresh.WriteBatch(b, true)) {
         err = "writing the imported wallet failed";
         return false;
