@@ -82,8 +82,9 @@ struct ChainstateOptions {
     int64_t maxTipAge = DEFAULT_MAX_TIP_AGE;
     // -connectpipeline: when several blocks connect in a row (IBD, reorgs), block N+1's UTXO pass
     // runs while block N's signature batch is on the GPU (at most this many blocks in flight;
-    // <= 1 connects one block at a time like the reference)
-    int connectPipeline = 2;
+    // <= 1 connects one block at a time like the reference, the default: with a 2 ms batch the
+    // layered views cost more than the overlap gains, profiles/connect_r5.md)
+    int connectPipeline = 1;
     // the UTXO pass of a block with at least this many transactions runs in parallel (0: never)
     size_t parallelUtxoMinTx = 64;
     // -blockcachemb: blocks accepted but not yet connected stay in memory up to this many
