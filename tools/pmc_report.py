@@ -32,7 +32,8 @@ def kname(name):
     m = re.search(r"eh_round<[^>]*>, (\d+), (?:false|true)>", name)
     if m:
         return "eh_round<%s>" % m.group(1)
-    for k in ("eh_gen_reg", "eh_gen", "eh_expand", "eh_verify", "ecdsa_verify_kernel", "ecdsa_prep_kernel"):
+    for k in ("eh_gen_reg", "eh_gen", "eh_expand", "eh_verify", "ecdsa_verify_kernel", "ecdsa_verify10h_kernel",
+              "ecdsa_verify10_kernel", "ecdsa_fused_kernel", "ecdsa_prep_kernel"):
         if k in name:
             return k
     return re.sub(r"\(.*", "", name)[:40]
