@@ -87,6 +87,12 @@
 #ifndef BCP_EH_GEN_R0 // 1: the header generation starts each hash from the workgroup's precomputed
 #define BCP_EH_GEN_R0 1 //  g-independent part of BLAKE2b round 0 (G1..G3 and half of G0)
 #endif
+#ifndef BCP_EH_PL_CH // payload-light emit: output rows per load batch (0 = by row width)
+#define BCP_EH_PL_CH 0
+#endif
+#ifndef BCP_EH_PL_FROM // payload-light collision rounds from this round on ((200,9), rounds that do not prune; 0 = off):
+#define BCP_EH_PL_FROM 0 //   LDS keeps only word 0 of each row, the emit reads both rows from the bucket's global copy,
+#endif                   //   and two 1024-thread workgroups fit per CU (see round_pl)
 #ifndef BCP_EH_MP_LATE // extra pair slots per lane in the late collision rounds (see round_mp)
 #define BCP_EH_MP_LATE 1
 #endif
@@ -614,8 +620,19 @@ template <class C> constexpr int round_un(int stage) {
 template <class C> constexpr bool round_fgen(int stage) {
     return BCP_EH_FILTER_GEN && BCP_EH_KEY_COMMIT && BCP_EH_PAIRS && stage < C::K;
 }
+// Payload-light round (BCP_EH_PL_FROM): the collision search needs only each row's first word
+// (the key and the next digit), so LDS keeps that word alone; the rare full comparison of a pair
+// whose first words match and the emit's XOR read both rows from the bucket's input area in
+// global memory (just streamed in, so mostly L2-resident). LDS then drops below 80 KiB, and two
+// 1024-thread workgroups (32 waves) share a CU: one's barrier-bound phases overlap the other's.
+// Rounds that prune keep their rows in LDS (the parent words are compared there).
+template <class C> constexpr bool round_pl(int stage) {
+    return BCP_EH_PL_FROM > 0 && C::K == 9 && stage >= BCP_EH_PL_FROM && stage < C::K && stage < BCP_EH_PRUNE_FROM &&
+           !BCP_EH_SORTC;
+}
+template <class C> constexpr int round_wgcu(int stage) { return round_pl<C>(stage) ? 2 : C::WGCU; }
 template <class C> constexpr int round_lds(int stage, bool prune) {
-    const int WI = C::words(stage - 1);
+    const int WI = round_pl<C>(stage) ? 1 : C::words(stage - 1); // LDS words per row
     const int cap = C::cap(stage);
     const int marks = stage == C::K || BCP_EH_PAIRS ? 4 : (round_mp<C>(stage) * C::NT * 2 + 3) / 4 * 4;
     const int pruneb = prune ? cap * 4 + (C::cp(stage - 1) ? 0 : (cap * 2 + 3) / 4 * 4) : 0;
@@ -649,7 +666,7 @@ template <class C> constexpr bool round_prunes(int stage) {
 // Input rows whose slots carry compact parents keep the parent-bucket bits in their padding in
 // LDS (the prune check reads them); every comparison and the emit XOR mask them out (RMI).
 template <class C, int STAGE, bool STAMP>
-__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::WGCU * C::NT / 256)))
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(round_wgcu<C>(STAGE) * C::NT / 256)))
 void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTRin, uint32_t* __restrict__ Rout,
               uint32_t* __restrict__ CTRout, uint32_t* __restrict__ ncand, uint64_t* __restrict__ cand,
               uint64_t* __restrict__ stamps, uint32_t* __restrict__ pdrop, int nbk) {
@@ -658,7 +675,10 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     constexpr int CAP = C::cap(STAGE);                        // LDS rows / pair-list entries
     constexpr bool FINAL = STAGE == C::K;
     constexpr bool PRUNE = round_prunes<C>(STAGE);
-    static_assert(round_lds<C>(STAGE, PRUNE) <= C::LDS_BUDGET, "round LDS budget");
+    constexpr bool PL = round_pl<C>(STAGE);                  // payload-light (LDS holds row word 0 only)
+    constexpr int WL = PL ? 1 : WI;                           // LDS words per row
+    static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024 / round_wgcu<C>(STAGE), "round LDS budget");
+    static_assert(!PL || (!PRUNE && !FINAL), "payload-light rounds neither prune nor finish");
     constexpr int NT = C::NT;
     constexpr int RPL = (CAP + NT - 1) / NT;                // prefetched rows per lane
     constexpr int MP = round_mp<C>(STAGE);                  // pairs per lane (registers)
@@ -676,7 +696,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     constexpr bool FGEN = round_fgen<C>(STAGE); // filter pairs while listing them (implies FOLD)
     constexpr bool SORTC = BCP_EH_SORTC && FOLD && !FGEN; // rows committed at key-sorted LDS positions
     using HT = std::conditional_t<C::H16, uint16_t, uint32_t>;
-    __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
+    __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WL + 3) / 4 * 4];
     __shared__ uint32_t psig[PRUNE ? CAP : 1];                // the input rows' parent word (j << 16 | i, + d bits)
     __shared__ uint16_t pdw[PRUNE && !CPI ? CAP : 1];         // two-word parents: the producing bucket
     __shared__ uint16_t pmark[FINAL || BCP_EH_PAIRS ? 2 : MP * NT]; // pair index -> first sorted position
@@ -710,6 +730,11 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             return atomicAdd(&h[b], 1u);
         }
     };
+    // PL: the current bucket's input area (the full rows the LDS words came from)
+    __amdgpu_buffer_rsrc_t rs_cur = buf_rsrc(Rin, 0);
+    auto grow = [&](uint32_t i, int w) -> uint32_t {
+        return __builtin_amdgcn_raw_buffer_load_b32(rs_cur, (i * SWI + w) * 4, 0, 0);
+    };
     // rows i and j share a parent (depth-1 duplicate): equal producing bucket and a common LDS row
     auto shares_parent = [&](uint32_t i, uint32_t j) -> bool {
         const uint32_t a = psig[i], b = psig[j];
@@ -726,15 +751,17 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // a collision pair (LDS rows i, j) is kept unless the rows are identical or share a parent;
     // dest = its destination bucket
     auto pair_keep = [&](uint32_t i, uint32_t j, uint32_t& dest) -> bool {
-        uint32_t x0 = rows[i * WI] ^ rows[j * WI];
+        uint32_t x0 = rows[i * WL] ^ rows[j * WL];
         if constexpr (WI == 1) x0 &= ~RMI;
         // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the pairs, so the
-        // remaining words are read only when it matches
+        // remaining words are read only when it matches (PL: from global memory)
         bool keep = x0 != 0;
         if (!keep) {
 #pragma unroll
             for (int w = 1; w < WI; ++w) {
-                uint32_t y = rows[i * WI + w] ^ rows[j * WI + w];
+                uint32_t y;
+                if constexpr (PL) y = grow(i, w) ^ grow(j, w);
+                else y = rows[i * WI + w] ^ rows[j * WI + w];
                 if (w == WI - 1) y &= ~RMI;
                 keep |= y != 0;
             }
@@ -755,7 +782,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         return t;
     };
     // (a round that does not prune loads only the row words of each slot)
-    constexpr int LWI = PRUNE ? (CPI ? WI + 1 : WI + 2) : (BCP_EH_ROWONLY_LOAD ? WI : SWI);
+    constexpr int LWI = PL ? 1 : PRUNE ? (CPI ? WI + 1 : WI + 2) : (BCP_EH_ROWONLY_LOAD ? WI : SWI);
     uint32_t nr[RPL][LWI];
     uint32_t krank[FOLD ? RPL : 1]; // FOLD: (key << 16) | rank in the key group of each committed row
     int pf_bk = bk;
@@ -824,6 +851,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 
     for (;;) {
         const int nonce = bk / C::NB, d = bk % C::NB;
+        if constexpr (PL) rs_cur = buf_rsrc(Rin + ((size_t)nonce * C::ROWS + (size_t)d * C::AREA) * SWI, CAP * SWI * 4);
         EH_STAMP(0);
         // A. commit the prefetched bucket (one row per lane per unit)
         {
@@ -832,7 +860,9 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             for (int u = 0; u < RPL; ++u) {
                 const uint32_t r = ot + u * NT;
                 if (r < n) {
-                    if constexpr (!SORTC) {
+                    if constexpr (PL) {
+                        rows[r] = nr[u][0];
+                    } else if constexpr (!SORTC) {
                         if constexpr (WI % 2 == 0) {
 #pragma unroll
                             for (int w = 0; w < WI; w += 2)
@@ -888,7 +918,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 
         // D1. counting sort of the rows by their RB key: sidx = row ids grouped by key,
         //     bend[key] = end of the key's group
-        auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WI] >> (32 - C::RB); };
+        auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WL] >> (32 - C::RB); };
         // FOLD: each lane's committed rows: sorted position (krank, reused) and the number of
         // later positions in the row's key group (its pairs, capped at 14 as below)
         uint32_t kpairs[FOLD ? RPL : 1];
@@ -1120,20 +1150,50 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             constexpr uint32_t OCAP = C::cap(STAGE + 1 <= C::K ? STAGE + 1 : C::K);
             constexpr uint32_t RMO = C::rmask(STAGE);
             const auto rs_out = buf_rsrc(Rout + (size_t)nonce * C::ROWS * SWO, (uint32_t)(C::ROWS * SWO * 4));
-#pragma unroll
-            for (int u = 0; u < MP; ++u) { // fixed trip count, unconditional stores (see issue())
+            auto out_t = [&](int u) -> uint32_t {
 #if BCP_EH_EXP_STORE == 5 // experiment: the lanes of a wave take output rows MP*NT/64 apart (scattered stores)
-                const uint32_t t0 = tid + u * NT, t = (t0 % (MP * NT / 64)) * 64 + t0 / (MP * NT / 64);
+                const uint32_t t0 = tid + u * NT;
+                return (t0 % (MP * NT / 64)) * 64 + t0 / (MP * NT / 64);
 #else
-                const uint32_t t = tid + u * NT;
+                return tid + u * NT;
 #endif
+            };
+            // payload-light: the parents' full rows come from global memory, CH output rows'
+            // worth of loads issued together before their XORs and stores (the stores may alias
+            // the loads as far as the compiler knows, so it would not hoist them itself)
+            constexpr int CH = PL ? (BCP_EH_PL_CH > 0 ? BCP_EH_PL_CH : (WI >= 4 ? 2 : 3)) : 1;
+#pragma unroll
+            for (int u0 = 0; u0 < MP; u0 += CH) {
+            uint32_t pa[CH][PL ? WI : 1], pb[CH][PL ? WI : 1];
+            if constexpr (PL) {
+#pragma unroll
+                for (int c = 0; c < CH; ++c)
+                    if (u0 + c < MP) {
+                        const uint32_t t = out_t(u0 + c);
+                        const uint32_t pr = t < np ? spair[t] : 0u;
+                        const uint32_t si = pr & 0xffff, sj = pr >> 16;
+                        const uint32_t i = SORTC ? (uint32_t)sidx[si] : si, j = SORTC ? (uint32_t)sidx[sj] : sj;
+                        row_load<WI>(rs_cur, t < np ? i * (SWI * 4) : OOB, pa[c]);
+                        row_load<WI>(rs_cur, t < np ? j * (SWI * 4) : OOB, pb[c]);
+                    }
+            }
+#pragma unroll
+            for (int c = 0; c < CH; ++c) { // fixed trip count, unconditional stores (see issue())
+                const int u = u0 + c;
+                if (u >= MP) break;
+                const uint32_t t = out_t(u);
                 const uint32_t pr = t < np ? spair[t] : 0u;
                 const uint32_t si = pr & 0xffff, sj = pr >> 16; // LDS rows
                 // the parents' slots in the input area: the LDS rows themselves, or (SORTC) the
                 // slots the key sort moved them from
                 const uint32_t i = SORTC ? (uint32_t)sidx[si] : si, j = SORTC ? (uint32_t)sidx[sj] : sj;
                 uint32_t x[WI + 1], o[WO];
-                lds_row_xor<WI>(rows, si, sj, x);
+                if constexpr (PL) { // both full rows, loaded above
+#pragma unroll
+                    for (int w = 0; w < WI; ++w) x[w] = pa[c][w] ^ pb[c][w];
+                } else {
+                    lds_row_xor<WI>(rows, si, sj, x);
+                }
                 x[WI - 1] &= ~RMI;
                 x[WI] = 0;
                 const uint32_t b = (x[0] >> (32 - C::DB)) & (C::NB - 1);
@@ -1163,6 +1223,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #else
                 row_store<SWO>(rs_out, ok ? slot * (SWO * 4) : OOB, ov);
 #endif
+            }
             }
         }
         __syncthreads();
