@@ -430,16 +430,18 @@ int AppMain(int argc, char* argv[]) {
         LogPrintf("HTTP: creating work queue of depth %d\n", ho.workQueueDepth);
         http.reset(new HTTPServer(ho));
         std::string err;
-        if (!http->Start(err)) {
-            InitError(err);
-            return 1;
-        }
+        // handlers first, then the listener (reference AppInitServers: StartHTTPRPC and StartREST
+        // before StartHTTPServer), so no early request meets an empty 404
         if (!StartHTTPRPC(*http, datadir, err)) {
             InitError(err);
             return 1;
         }
         if (gArgs.GetBoolArg("-rest", false)) StartREST(*http);
         if (gArgs.GetBoolArg("-webgui", false)) StartWebGUI(*http);
+        if (!http->Start(err)) {
+            InitError(err);
+            return 1;
+        }
     }
 
     // ---- chainstate

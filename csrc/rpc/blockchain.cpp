@@ -374,7 +374,7 @@ static UniValue gettxoutsetinfo(const JSONRPCRequest& req) {
             ss << VARINT((uint64_t)o.second.out.nValue);
             nTransactionOutputs++;
             nTotalAmount += o.second.out.nValue;
-            nBogoSize += 32 + 4 + 4 + 8 + o.second.out.scriptPubKey.size() + 4;
+            nBogoSize += 32 + 4 + 4 + 8 + 2 + o.second.out.scriptPubKey.size(); // txid, n, height, value, script length
         }
         ss << VARINT(0u);
         outputs.clear();

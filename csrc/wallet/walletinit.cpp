@@ -224,7 +224,8 @@ bool StartWallet(NodeContext& node, std::string& err) {
         CPubKey pub;
         if (!rk.GetReservedKey(pub)) ThrowRPC(RPC_WALLET_KEYPOOL_RAN_OUT, "Error: Keypool ran out, please call keypoolrefill first");
         rk.KeepKey();
-        return GetScriptForDestination(pub.GetID());
+        // pay-to-pubkey, as the reference's CWallet::GetScriptForMining (src/wallet/wallet.cpp:3711)
+        return GetScriptForRawPubKey(pub);
     };
     g_walletGetInfo = [w](UniValue& obj) {
         obj.pushKV("walletversion", w->GetVersion());
