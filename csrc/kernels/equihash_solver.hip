@@ -43,6 +43,7 @@
 #include "kernels/hip_util.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 #include <utility>
@@ -1393,6 +1394,7 @@ struct EquihashGpuSolver::Impl {
     std::vector<bool> compact;                  // per stage: compact parent word                 // > 0: stage-0 slots carry the leaf index last
     int inflight = 0;
     int ncu = 1;
+    int ncu_round = 1; // CUs the round kernels' stream may use (BCP_EH_GEN_CUS splits the device)
     bool debug = false, stamp_mode = false;
     DevBuf<uint64_t> d_stamps;
     EhGpuStats stats;
@@ -1448,7 +1450,7 @@ struct EquihashGpuSolver::Impl {
             BCP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bcpk::eh_round<C, S, ST>, C::NT, 0));
             per_cu = std::max(occ, 1);
         }
-        return std::min(nbk, ncu * per_cu);
+        return std::min(nbk, ncu_round * per_cu);
     }
     template <class C, int S> void launch_round(int nstates) {
         const uint32_t* rin = d_rst[S - 1].p;
@@ -1559,7 +1561,22 @@ EquihashGpuSolver::EquihashGpuSolver(unsigned n, unsigned k, int batch, int devi
     impl->batch = batch;
     impl->device = UseDevice(device);
     BCP_HIP_CHECK(hipDeviceGetAttribute(&impl->ncu, hipDeviceAttributeMultiprocessorCount, impl->device));
-    if (BCP_EH_PRIO) {
+    impl->ncu_round = impl->ncu;
+    // BCP_EH_GEN_CUS=G (a multiple of 8, below the CU count): generation gets a stream of its own
+    // restricted to G CUs and the rounds one restricted to the others, so a pipelined batch's
+    // generation runs on its CUs while the previous batch's rounds hold the rest. CU-mask bit i
+    // lands on XCD i % 8, so the low G bits give every XCD G / 8 generation CUs.
+    const char* gcus = getenv("BCP_EH_GEN_CUS");
+    const int G = gcus ? atoi(gcus) : 0;
+    if (G > 0 && G % 8 == 0 && G < impl->ncu) {
+        std::vector<uint32_t> rmask((impl->ncu + 31) / 32, 0u), gmask((impl->ncu + 31) / 32, 0u);
+        for (int i = 0; i < impl->ncu; ++i) (i < G ? gmask : rmask)[i / 32] |= 1u << (i % 32);
+        BCP_HIP_CHECK(hipExtStreamCreateWithCUMask(&impl->stream, (uint32_t)rmask.size(), rmask.data()));
+        BCP_HIP_CHECK(hipExtStreamCreateWithCUMask(&impl->gstream, (uint32_t)gmask.size(), gmask.data()));
+        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evs, hipEventDisableTiming));
+        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evg, hipEventDisableTiming));
+        impl->ncu_round = impl->ncu - G;
+    } else if (BCP_EH_PRIO) {
         int least = 0, greatest = 0;
         BCP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
         BCP_HIP_CHECK(hipStreamCreateWithPriority(&impl->stream, hipStreamNonBlocking, greatest));
