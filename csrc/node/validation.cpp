@@ -1413,17 +1413,8 @@ static DisconnectResult UndoCoinSpend(const Coin& undo, CCoinsViewCache& view, c
     return fClean ? DISCONNECT_OK : DISCONNECT_UNCLEAN;
 }
 
-DisconnectResult Chainstate::DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view) {
-    CBlockUndo blockUndo;
-    CDiskBlockPos pos = pindex->GetUndoPos();
-    if (pos.IsNull()) {
-        error("DisconnectBlock(): no undo data available");
-        return DISCONNECT_FAILED;
-    }
-    if (!UndoReadFromDisk(blockUndo, pos, pindex->pprev->GetBlockHash())) {
-        error("DisconnectBlock(): failure reading undo data");
-        return DISCONNECT_FAILED;
-    }
+DisconnectResult ApplyBlockUndo(const CBlockUndo& blockUndo, const CBlock& block, const CBlockIndex* pindex,
+                                CCoinsViewCache& view) {
     if (blockUndo.vtxundo.size() + 1 != block.vtx.size()) {
         error("DisconnectBlock(): block and undo data inconsistent");
         return DISCONNECT_FAILED;
@@ -1455,8 +1446,39 @@ DisconnectResult Chainstate::DisconnectBlock(const CBlock& block, const CBlockIn
             }
         }
     }
-    view.SetBestBlock(pindex->pprev->GetBlockHash());
+    view.SetBestBlock(block.hashPrevBlock);
     return fClean ? DISCONNECT_OK : DISCONNECT_UNCLEAN;
+}
+
+void UpdateCoins(const CTransaction& tx, CCoinsViewCache& view, CTxUndo& txundo, int nHeight) {
+    if (!tx.IsCoinBase()) {
+        txundo.vprevout.reserve(tx.vin.size());
+        for (const CTxIn& in : tx.vin) {
+            txundo.vprevout.emplace_back();
+            const bool spent = view.SpendCoin(in.prevout, &txundo.vprevout.back());
+            assert(spent);
+        }
+    }
+    AddCoins(view, tx, nHeight);
+}
+
+void UpdateCoins(const CTransaction& tx, CCoinsViewCache& view, int nHeight) {
+    CTxUndo txundo;
+    UpdateCoins(tx, view, txundo, nHeight);
+}
+
+DisconnectResult Chainstate::DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view) {
+    CBlockUndo blockUndo;
+    CDiskBlockPos pos = pindex->GetUndoPos();
+    if (pos.IsNull()) {
+        error("DisconnectBlock(): no undo data available");
+        return DISCONNECT_FAILED;
+    }
+    if (!UndoReadFromDisk(blockUndo, pos, pindex->pprev->GetBlockHash())) {
+        error("DisconnectBlock(): failure reading undo data");
+        return DISCONNECT_FAILED;
+    }
+    return ApplyBlockUndo(blockUndo, block, pindex, view);
 }
 
 // ------------------------------------------------------------------ flushing

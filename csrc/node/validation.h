@@ -66,6 +66,16 @@ static const Amount DEFAULT_TRANSACTION_MAXFEE = COIN / 10;
 enum FlushStateMode { FLUSH_STATE_NONE, FLUSH_STATE_IF_NEEDED, FLUSH_STATE_PERIODIC, FLUSH_STATE_ALWAYS };
 enum DisconnectResult { DISCONNECT_OK, DISCONNECT_UNCLEAN, DISCONNECT_FAILED };
 
+// Reverts a connected block's coin changes from its undo record: its outputs are spent, the
+// coins its inputs spent come back, and the view's best block becomes the block's parent
+// (reference src/validation.cpp ApplyBlockUndo, the part of DisconnectBlock after the undo read).
+DisconnectResult ApplyBlockUndo(const CBlockUndo& blockUndo, const CBlock& block, const CBlockIndex* pindex,
+                                CCoinsViewCache& view);
+// Spends tx's inputs (recording the spent coins in txundo) and adds its outputs at nHeight
+// (reference UpdateCoins); the inputs must exist in the view.
+void UpdateCoins(const CTransaction& tx, CCoinsViewCache& view, CTxUndo& txundo, int nHeight);
+void UpdateCoins(const CTransaction& tx, CCoinsViewCache& view, int nHeight);
+
 struct ChainstateOptions {
     std::string datadir;            // <datadir> (net specific); blocks/ chainstate/ blocks/index/
     bool memoryOnly = false;        // in-memory databases (tests)

@@ -51,6 +51,14 @@ public:
     bool isNum() const { return typ == VNUM; }
     bool isArray() const { return typ == VARR; }
     bool isObject() const { return typ == VOBJ; }
+    bool getBool() const { return isTrue(); }
+    // every named key exists with the given type
+    bool checkObject(const std::map<std::string, VType>& memberTypes) const {
+        for (const auto& m : memberTypes) {
+            if (!exists(m.first) || (*this)[m.first].getType() != m.second) return false;
+        }
+        return true;
+    }
 
     bool push_back(const UniValue& v);
     bool push_backV(const std::vector<UniValue>& vec);
