@@ -257,6 +257,29 @@ static void GetOSRand(unsigned char* buf, size_t num) {
 
 void GetRandBytes(unsigned char* buf, size_t num) { GetOSRand(buf, num); }
 
+bool Random_SanityCheck() {
+    // not a quality test: every byte must change at least once within the try budget
+    unsigned char data[32];
+    bool overwritten[32] = {};
+    int num = 0;
+    for (int tries = 0; tries < 1024 && num < 32; tries++) {
+        memset(data, 0, sizeof(data));
+        GetOSRand(data, sizeof(data));
+        num = 0;
+        for (int x = 0; x < 32; x++) {
+            overwritten[x] |= data[x] != 0;
+            num += overwritten[x];
+        }
+    }
+    return num == 32;
+}
+
+bool ECC_InitSanityCheck() {
+    CKey key;
+    key.MakeNewKey(true);
+    return key.VerifyPubKey(key.GetPubKey());
+}
+
 void GetStrongRandBytes(unsigned char* buf, size_t num) {
     // Hash OS randomness together with a timestamp so a weak OS source alone
     // does not determine the output.
@@ -310,9 +333,9 @@ uint64_t FastRandomContext::rand64() {
     avail -= 8;
     return v;
 }
-uint32_t FastRandomContext::randbits(int bits) {
+uint64_t FastRandomContext::randbits(int bits) {
     if (bits == 0) return 0;
-    return (uint32_t)(rand64() >> (64 - bits));
+    return rand64() >> (64 - bits);
 }
 uint64_t FastRandomContext::randrange(uint64_t range) {
     if (range <= 1) return 0;

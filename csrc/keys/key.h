@@ -152,6 +152,11 @@ struct CExtKey {
 // ---------------------------------------------------------------- random
 void GetRandBytes(unsigned char* buf, size_t num);
 void GetStrongRandBytes(unsigned char* buf, size_t num);
+// Start-up checks (reference init.cpp InitSanityCheck): a fresh key's public key verifies
+// against it (ECC_InitSanityCheck, key.cpp:336), and the OS RNG overwrites every byte of a
+// 32-byte buffer within 1024 reads (Random_SanityCheck, random.cpp:253).
+bool ECC_InitSanityCheck();
+bool Random_SanityCheck();
 uint64_t GetRand(uint64_t nMax);
 int GetRandInt(int nMax);
 uint256 GetRandHash();
@@ -160,7 +165,7 @@ public:
     explicit FastRandomContext(bool fDeterministic = false);
     explicit FastRandomContext(const uint256& seed);
     uint64_t rand64();
-    uint32_t randbits(int bits);
+    uint64_t randbits(int bits); // bits in [0, 64]
     std::vector<unsigned char> randbytes(size_t len);
     uint32_t rand32() { return (uint32_t)rand64(); }
     uint64_t randrange(uint64_t range);

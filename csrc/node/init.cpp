@@ -266,6 +266,15 @@ int AppMain(int argc, char* argv[]) {
         if (pid > 0) return 0;
         setsid();
     }
+    // sanity checks (reference AppInitSanityChecks / InitSanityCheck)
+    if (!ECC_InitSanityCheck()) {
+        InitError("Elliptic curve cryptography sanity check failure. Aborting.");
+        return 1;
+    }
+    if (!Random_SanityCheck()) {
+        InitError("OS cryptographic RNG sanity check failure. Aborting.");
+        return 1;
+    }
     if (!LockDataDirectory(datadir)) {
         fprintf(stderr, "Error: Cannot obtain a lock on data directory %s. Bitcoin Cash Plus is probably already running.\n",
                 datadir.c_str());
