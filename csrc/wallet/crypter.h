@@ -57,6 +57,7 @@ public:
     void Clear();
 
 private:
+    friend struct CrypterTestAccess; // wallet_crypto tests compare the derived key and IV with OpenSSL
     unsigned char vchKey[WALLET_CRYPTO_KEY_SIZE];
     unsigned char vchIV[WALLET_CRYPTO_IV_SIZE];
     bool fKeySet = false;
