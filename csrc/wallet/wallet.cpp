@@ -414,12 +414,18 @@ bool CWallet::Load(std::string& err, bool& firstRun) {
     for (const auto& kv : pendingCrypted) CCryptoKeyStore::AddCryptedKey(kv.first, kv.second);
     if (nWalletVersion == 0) nWalletVersion = nWalletMaxVersion = WALLET_FEATURE_BASE;
     // order index and spend map
+    bool fAnyUnordered = false;
     for (auto& kv : mapWallet) {
-        CWalletTx& wtx = kv.second;
-        if (wtx.nOrderPos == -1) wtx.nOrderPos = IncOrderPosNext();
-        wtxOrdered.insert({wtx.nOrderPos, TxPair(&wtx, nullptr)});
+        fAnyUnordered |= kv.second.nOrderPos == -1;
         AddToSpends(kv.first);
     }
+    for (const CAccountingEntry& e : laccentries) fAnyUnordered |= e.nOrderPos == -1;
+    if (fAnyUnordered && !ReorderTransactions()) {
+        err = "Error loading " + strWalletName + ": cannot write the transaction order";
+        return false;
+    }
+    wtxOrdered.clear();
+    for (auto& kv : mapWallet) wtxOrdered.insert({kv.second.nOrderPos, TxPair(&kv.second, nullptr)});
     for (CAccountingEntry& e : laccentries) wtxOrdered.insert({e.nOrderPos, TxPair(nullptr, &e)});
     LogPrintf("Wallet %s: %d keys, %d encrypted keys, %d transactions, %zu pool keys\n", strWalletName.c_str(), nKeys,
               nCKeys, nTx, setKeyPool.size());
@@ -1010,6 +1016,42 @@ bool CWallet::ScanForWalletTransactions(const CBlockIndex* pindex, bool fUpdate,
     uiInterface.ShowProgress("Rescanning...", 100);
     if (pnFound) *pnFound = found;
     LogPrintf("Rescan completed in %15dms (%d wallet txs)\n", (int)(GetTimeMillis() - start), found);
+    return true;
+}
+
+bool CWallet::ReorderTransactions() {
+    WalletLock l(*this);
+    // everything by time; equal times keep the order they were gathered in
+    std::multimap<int64_t, TxPair> txByTime;
+    for (auto& kv : mapWallet) txByTime.insert({(int64_t)kv.second.nTimeReceived, TxPair(&kv.second, nullptr)});
+    // the reference reads the entries with ListAccountCreditDebit(""): account "" only
+    for (CAccountingEntry& e : laccentries)
+        if (e.strAccount.empty()) txByTime.insert({e.nTime, TxPair(nullptr, &e)});
+    nOrderPosNext = 0;
+    std::vector<int64_t> offsets; // positions handed to unordered records, in increasing order
+    for (auto& it : txByTime) {
+        CWalletTx* const pwtx = it.second.first;
+        CAccountingEntry* const pae = it.second.second;
+        int64_t& pos = pwtx ? pwtx->nOrderPos : pae->nOrderPos;
+        if (pos == -1) {
+            pos = nOrderPosNext++;
+            offsets.push_back(pos);
+        } else {
+            int64_t off = 0;
+            for (int64_t start : offsets)
+                if (pos >= start) ++off;
+            pos += off;
+            nOrderPosNext = std::max(nOrderPosNext, pos + 1);
+            if (!off) continue;
+        }
+        const bool ok = pwtx ? db->Write(K("tx", pwtx->GetHash()), *pwtx)
+                             : db->Write(K("acentry", std::make_pair(pae->strAccount, pae->nEntryNo)), *pae);
+        if (!ok) return false;
+    }
+    db->Write(std::string("orderposnext"), nOrderPosNext);
+    wtxOrdered.clear();
+    for (auto& kv : mapWallet) wtxOrdered.insert({kv.second.nOrderPos, TxPair(&kv.second, nullptr)});
+    for (CAccountingEntry& e : laccentries) wtxOrdered.insert({e.nOrderPos, TxPair(nullptr, &e)});
     return true;
 }
 

@@ -352,6 +352,11 @@ public:
     void SyncTransaction(const CTransactionRef& tx, const CBlockIndex* pindex = nullptr, int posInBlock = 0);
     std::vector<uint256> ResendWalletTransactionsBefore(int64_t nTime);
     bool AddAccountingEntry(const CAccountingEntry& entry);
+    // Gives unordered transactions and account-"" accounting entries (nOrderPos -1: wallets
+    // from before ordering existed) positions by receive time, shifting the ordered ones past
+    // them, and writes back what moved (reference CWallet::ReorderTransactions, run by
+    // LoadWallet when any record is unordered).
+    bool ReorderTransactions();
 
     // ---- ownership / amounts
     isminetype IsMine(const CTxIn& txin) const;
