@@ -214,7 +214,13 @@ public:
     int32_t ComputeBlockVersion(const CBlockIndex* pindexPrev);
     VersionBitsCache& VersionBits() { return versionbitscache; }
     uint64_t MaxBlockSize() const { return opts.maxBlockSize; }
-    void SetMaxBlockSize(uint64_t n) { opts.maxBlockSize = n; }
+    // Sizes up to the legacy 1 MB limit are refused and leave the setting unchanged (reference
+    // GlobalConfig::SetMaxBlockSize, src/config.cpp).
+    bool SetMaxBlockSize(uint64_t n) {
+        if (n <= LEGACY_MAX_BLOCK_SIZE) return false;
+        opts.maxBlockSize = n;
+        return true;
+    }
     bool TxIndexEnabled() const { return opts.txindex; }
     bool PruneMode() const { return opts.pruneTarget > 0; }
     bool HavePruned() const { return fHavePruned; }

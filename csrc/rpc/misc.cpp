@@ -263,10 +263,9 @@ static UniValue setexcessiveblock(const JSONRPCRequest& req) {
         if (temp[0] == '-') throw std::runtime_error("setexcessiveblock blockSize");
         ebs = (uint64_t)atoi64(temp);
     }
-    if (ebs <= LEGACY_MAX_BLOCK_SIZE)
+    if (!Node().chainstate->SetMaxBlockSize(ebs))
         ThrowRPC(RPC_INVALID_PARAMETER, strprintf("Invalid parameter, excessiveblock must be larger than %llu",
                                                   (unsigned long long)LEGACY_MAX_BLOCK_SIZE));
-    Node().chainstate->SetMaxBlockSize(ebs);
     return "Excessive Block set to " + std::to_string(ebs) + " bytes.";
 }
 
