@@ -95,3 +95,16 @@ TEST_CASE(random_tests, fastrandom_randbits) {
 }
 
 TEST_CASE(sanity_tests, basic_sanity) { CHECK(ECC_InitSanityCheck()); }
+
+// Parity: reference src/test/base64_tests.cpp (base64_testvectors, RFC 4648).
+TEST_CASE(base64_tests, base64_testvectors) {
+    const char* in[] = {"", "f", "fo", "foo", "foob", "fooba", "foobar"};
+    const char* out[] = {"", "Zg==", "Zm8=", "Zm9v", "Zm9vYg==", "Zm9vYmE=", "Zm9vYmFy"};
+    for (int i = 0; i < 7; i++) {
+        CHECK_EQ(EncodeBase64(std::string(in[i])), std::string(out[i]));
+        bool invalid = false;
+        const std::vector<unsigned char> dec = DecodeBase64(out[i], &invalid);
+        CHECK(!invalid);
+        CHECK_EQ(std::string(dec.begin(), dec.end()), std::string(in[i]));
+    }
+}

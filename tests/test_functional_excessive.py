@@ -1,4 +1,5 @@
-"""Excessive block size (reference test/functional/bcp-rpc.py and bcp-cmdline.py):
+"""Excessive block size (reference test/functional/bcp-rpc.py and bcp-cmdline.py, and the RPC
+bounds of src/test/excessiveblock_tests.cpp):
 get/setexcessiveblock bounds, the EB<n> comment in the user agent, and the startup checks
 for -excessiveblocksize <= 1MB and -blockmaxsize above the excessive size."""
 import re
