@@ -1379,6 +1379,11 @@ struct EquihashGpuSolver::Impl {
     hipStream_t gstream = nullptr;                // BCP_EH_PRIO: generation's own low-priority stream
     hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evg = nullptr;
     hipEvent_t ev_gen = nullptr, ev_rounds = nullptr; // this solver's last generation / rounds done (pipelining)
+    hipEvent_t ev_mid = nullptr; // this solver's round `pipe_round` done: the next batch's generation may start
+    // Pipelined launches: the next batch's generation waits for this batch's round pipe_round
+    // (BCP_EH_PIPE_ROUND, default 0 = only for this batch's generation). Rounds whose LDS leaves
+    // no room for a generation workgroup beside them (rounds 1-2 of (200,9)) are then not shared.
+    int pipe_round = 0;
     const Impl* after = nullptr;                        // Launch(states, prev): the batch to pipeline behind
     DevBuf<bcpk::EhBaseState> d_states;
     DevBuf<uint32_t> d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
@@ -1467,8 +1472,12 @@ struct EquihashGpuSolver::Impl {
                                stream, rin, cin, rout, cout, d_ncand.p, d_cand.p, nullptr, d_pdrop.p, nbk);
         }
     }
+    template <class C, int S> void launch_round_mark(int nstates) {
+        launch_round<C, S>(nstates);
+        if (S == pipe_round || (S == C::K && pipe_round > C::K)) BCP_HIP_CHECK(hipEventRecord(ev_mid, stream));
+    }
     template <class C, int... S> void launch_rounds(int nstates, std::integer_sequence<int, S...>) {
-        (launch_round<C, S + 1>(nstates), ...);
+        (launch_round_mark<C, S + 1>(nstates), ...);
     }
 
     template <class C> void launch(size_t nstates) {
@@ -1500,6 +1509,7 @@ struct EquihashGpuSolver::Impl {
             gs = gstream;
         }
         if (after) BCP_HIP_CHECK(hipStreamWaitEvent(gs, after->ev_gen, 0)); // one generation at a time
+        if (after && after->pipe_round > 0) BCP_HIP_CHECK(hipStreamWaitEvent(gs, after->ev_mid, 0));
         constexpr bool reg = bcpk::GenReg<C, C::GNT, C::GHPT>::OK;
         if constexpr (reg) {
             using GR = bcpk::GenReg<C, C::GNT, C::GHPT>;
@@ -1588,6 +1598,8 @@ EquihashGpuSolver::EquihashGpuSolver(unsigned n, unsigned k, int batch, int devi
     }
     BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_gen, hipEventDisableTiming));
     BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_rounds, hipEventDisableTiming));
+    BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_mid, hipEventDisableTiming));
+    if (const char* pr = getenv("BCP_EH_PIPE_ROUND")) impl->pipe_round = std::max(0, atoi(pr));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev0));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev1));
     dispatch_cfg(n, k, [&](auto c) { impl->alloc<decltype(c)>(); });
@@ -1604,6 +1616,7 @@ EquihashGpuSolver::~EquihashGpuSolver() {
         if (impl->evs) (void)hipEventDestroy(impl->evs);
         if (impl->ev_gen) (void)hipEventDestroy(impl->ev_gen);
         if (impl->ev_rounds) (void)hipEventDestroy(impl->ev_rounds);
+        if (impl->ev_mid) (void)hipEventDestroy(impl->ev_mid);
         if (impl->evg) (void)hipEventDestroy(impl->evg);
     }
 }
@@ -1798,7 +1811,12 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
         }
     }
     uint64_t cands = 0;
-    for (int nn = 0; nn < ns; ++nn) cands += std::min<uint32_t>(impl->h_ncand.p[nn], (uint32_t)impl->maxcand);
+    for (int nn = 0; nn < ns; ++nn) {
+        const uint32_t c = impl->h_ncand.p[nn];
+        cands += std::min<uint32_t>(c, (uint32_t)impl->maxcand);
+        impl->stats.cand_max = std::max<uint64_t>(impl->stats.cand_max, c);
+        if (c > impl->maxcand) impl->stats.cand_dropped += c - impl->maxcand; // lost candidates, maybe solutions
+    }
     impl->stats.candidates += cands;
     impl->stats.duplicates += cands - nout;
     // the list is in completion order: put every nonce's solutions in candidate order

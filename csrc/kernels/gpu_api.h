@@ -41,6 +41,8 @@ struct EhGpuStats {
     uint64_t duplicates = 0;
     uint64_t solutions = 0;
     uint64_t dropped_rows = 0;   // rows lost to bucket overflow (debug mode, nonce 0 of each batch)
+    uint64_t cand_dropped = 0;   // final-round candidates past the per-nonce list (MAXCAND), every nonce
+    uint64_t cand_max = 0;       // largest per-nonce final-round candidate count seen
     double gpu_ms = 0;
     std::vector<uint64_t> stage_rows, stage_dropped, stage_maxfill; // debug mode, last batch
     std::vector<std::vector<uint64_t>> stage_top;

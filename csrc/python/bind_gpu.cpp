@@ -94,6 +94,8 @@ void bind_gpu(pyb::module_& m) {
                  d["duplicates"] = st.duplicates;
                  d["solutions"] = st.solutions;
                  d["dropped_rows_sampled"] = st.dropped_rows;
+                 d["cand_dropped"] = st.cand_dropped;
+                 d["cand_max"] = st.cand_max;
                  d["gpu_ms"] = st.gpu_ms;
                  d["stage_rows"] = st.stage_rows;
                  d["stage_dropped"] = st.stage_dropped;

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Pipelined-launch A/B (round 5): the same builds with BCP_EH_PIPELINE=0/1, interleaved, plus a
-# kernel timeline of each pipelined build. Run on the GPU box: bash tools/eh_pipe_ab.sh TAG REPS
+# kernel timeline of each build with pipelined launches (tools/eh_pipe_trace.sh). Run on the GPU box: bash tools/eh_pipe_ab.sh TAG REPS
 set -e
 cd "$GRAFT_REPO_ROOT"
 R=$GRAFT_REPO_ROOT
@@ -16,10 +16,4 @@ for b in $(ls ab); do B="$B ab/$b/$EXT@BCP_EH_PIPELINE=1"; done
 B="$B ab/base/$EXT@BCP_EH_PIPELINE=0"
 timeout -k 10 900 python -u tools/ab_bench.py --reps "${2:-6}" $B > "$O/ab.log" 2>&1
 tail -n 1 "$O/ab.log"
-for b in $(ls ab); do
-  (cd /tmp && BCP_NATIVE_PATH=$R/ab/$b/$EXT timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d "$O/$b" -o run -- \
-    python3 "$R/bench.py" --steps 6 --warmup 2 > "$O/$b.log" 2>&1)
-  python3 tools/eh_timeline.py "$O/$b" 60 > "$O/$b.txt"
-  head -n 3 "$O/$b.txt"
-done
-echo DONE
+bash tools/eh_pipe_trace.sh "$TAG/trace"

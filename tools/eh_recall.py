@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--salt", default="main")
+    ap.add_argument("--repeat", type=int, default=0)
     ap.add_argument("--json", default="")
     args = ap.parse_args()
     from bitcoincashplus_amd import native
@@ -49,14 +50,27 @@ def main():
         gpu += [set(x) for x in solver.solve(states[b0:b0 + args.batch])]
         if dbg is None:
             s = solver.stats()
-            dbg = {key: s[key] for key in ("stage_dropped", "pair_dropped", "stage_maxfill") if key in s}
+            dbg = {key: s[key] for key in ("stage_dropped", "pair_dropped", "stage_maxfill", "cand_max", "cand_dropped") if key in s}
     extra = sum(len(g - c) for g, c in zip(gpu, cpu))
     tc, tg = sum(map(len, cpu)), sum(len(g & c) for g, c in zip(gpu, cpu))
     for i, (c, g) in enumerate(zip(cpu, gpu)):
         if len(g & c) != len(c):
             print(f"nonce {i}: cpu {len(c)} gpu {len(g & c)} missing {len(c - g)}")
+    st = solver.stats()
     res = {"n": n, "k": k, "nonces": args.nonces, "cpu_solutions": tc, "gpu_found": tg,
-           "recall": round(tg / max(tc, 1), 4), "gpu_not_in_cpu": extra, "debug_first_batch": dbg}
+           "recall": round(tg / max(tc, 1), 4), "gpu_not_in_cpu": extra, "debug_first_batch": dbg,
+           "cand_max": st.get("cand_max"), "cand_dropped": st.get("cand_dropped")}
+    # the solver is not deterministic (row order inside a bucket follows the atomics): solve the
+    # same nonces again and report what each repeat found
+    reps = []
+    for _ in range(args.repeat):
+        g2 = []
+        for b0 in range(0, args.nonces, args.batch):
+            g2 += [set(x) for x in solver.solve(states[b0:b0 + args.batch])]
+        reps.append(sum(len(g & c) for g, c in zip(g2, cpu)))
+    if reps:
+        st = solver.stats()
+        res.update(repeat_found=reps, cand_max=st.get("cand_max"), cand_dropped=st.get("cand_dropped"))
     print(json.dumps(res))
     if args.json:
         with open(args.json, "w") as f:
