@@ -1390,7 +1390,7 @@ struct EquihashGpuSolver::Impl {
     DevBuf<uint64_t> d_cand;
     DevBuf<uint32_t> d_rst[16]; // merged layout: stage-s slot arrays (s = 0..K-1)
     HostBuf<bcpk::EhBaseState> h_states;
-    HostBuf<uint32_t> h_ncand, h_idx, h_ctr0, h_pdrop, h_nout, h_out;
+    HostBuf<uint32_t> h_ncand, h_idx, h_ctr0, h_ctr_all, h_pdrop, h_nout, h_out;
     size_t outq = 0; // compact-list entries copied back with every batch (more: a second copy)
     size_t rows = 0, L = 0, maxcand = 0, nb = 0, kstages = 0;
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
@@ -1442,6 +1442,7 @@ struct EquihashGpuSolver::Impl {
         outq = std::min<size_t>((size_t)batch * 4 + 16, (size_t)batch * C::MAXCAND);
         h_idx.alloc((size_t)C::MAXCAND * C::L);
         h_ctr0.alloc((size_t)C::K * C::NB);
+        h_ctr_all.alloc((size_t)C::K * batch * C::NB);
         d_stamps.alloc((size_t)C::K * batch * C::NB * 16);
         bytes = d_leaf.n * 4 + d_ctr.n * 4 + d_idx.n * 4;
         for (int s = 0; s < C::K; ++s) bytes += d_rst[s].n * 4;
@@ -1547,6 +1548,7 @@ struct EquihashGpuSolver::Impl {
                                              C::NB * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
             BCP_HIP_CHECK(hipMemcpyAsync(h_pdrop.p, d_pdrop.p, (C::K + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                          stream));
+            BCP_HIP_CHECK(hipMemcpyAsync(h_ctr_all.p, d_ctr.p, d_ctr.n * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         }
         BCP_HIP_CHECK(hipMemcpyAsync(h_nout.p, d_nout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         BCP_HIP_CHECK(hipMemcpyAsync(h_out.p, d_out.p, outq * (C::L + 2) * sizeof(uint32_t), hipMemcpyDeviceToHost,
@@ -1779,6 +1781,16 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
         impl->stats.stage_maxfill.assign(impl->kstages, 0);
         impl->stats.stage_top.assign(impl->kstages, {});
         impl->stats.pair_dropped.assign(impl->h_pdrop.p, impl->h_pdrop.p + impl->kstages + 1);
+        // every nonce of the batch: rows past a round's capacity, per stage (accumulated) and the
+        // fullest bucket of the batch
+        impl->stats.stage_dropped_all.resize(impl->kstages, 0);
+        impl->stats.stage_maxfill_all.assign(impl->kstages, 0);
+        for (size_t s = 0; s < impl->kstages; ++s)
+            for (size_t x = 0; x < (size_t)ns * NB; ++x) {
+                const uint64_t fill = impl->h_ctr_all.p[(s * impl->batch) * NB + x];
+                impl->stats.stage_maxfill_all[s] = std::max<uint64_t>(impl->stats.stage_maxfill_all[s], fill);
+                if (fill > impl->caps[s]) impl->stats.stage_dropped_all[s] += fill - impl->caps[s];
+            }
         for (size_t s = 0; s < impl->kstages; ++s) {
             std::vector<uint64_t> fills;
             for (size_t dd = 0; dd < NB; ++dd) {

@@ -47,6 +47,7 @@ struct EhGpuStats {
     std::vector<uint64_t> stage_rows, stage_dropped, stage_maxfill; // debug mode, last batch
     std::vector<std::vector<uint64_t>> stage_top;
     std::vector<uint64_t> pair_dropped;
+    std::vector<uint64_t> stage_dropped_all, stage_maxfill_all;     // debug: every nonce (dropped: accumulated)
     std::vector<std::vector<uint32_t>> debug_cands;                  // debug: every candidate of nonce 0 (valid or not)                              // debug: pair-list overflow per round (batch total)                    // debug: 8 fullest buckets per stage
 };
 

@@ -102,6 +102,8 @@ void bind_gpu(pyb::module_& m) {
                  d["stage_maxfill"] = st.stage_maxfill;
                  d["stage_top"] = st.stage_top;
                  d["pair_dropped"] = st.pair_dropped;
+                 d["stage_dropped_all"] = st.stage_dropped_all;
+                 d["stage_maxfill_all"] = st.stage_maxfill_all;
                  d["debug_cands"] = st.debug_cands;
                  return d;
              })

@@ -258,7 +258,9 @@ def test_listtransactions(tmp_path):
     try:
         connect(n1, n0)
         n0.rpc.generate(101)
+        sync_blocks([n0, n1])  # n1 mines on n0's tip (a block on a stale tip is reorged away)
         n1.rpc.generate(1)
+        sync_blocks([n0, n1])
         n0.rpc.generate(100)
         sync_blocks([n0, n1])
         r0, r1 = n0.rpc, n1.rpc

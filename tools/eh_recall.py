@@ -62,15 +62,18 @@ def main():
            "cand_max": st.get("cand_max"), "cand_dropped": st.get("cand_dropped")}
     # the solver is not deterministic (row order inside a bucket follows the atomics): solve the
     # same nonces again and report what each repeat found
-    reps = []
+    reps, drops = [], []
     for _ in range(args.repeat):
         g2 = []
         for b0 in range(0, args.nonces, args.batch):
             g2 += [set(x) for x in solver.solve(states[b0:b0 + args.batch])]
         reps.append(sum(len(g & c) for g, c in zip(g2, cpu)))
+        drops.append(list(solver.stats().get("stage_dropped_all") or []))
     if reps:
         st = solver.stats()
-        res.update(repeat_found=reps, cand_max=st.get("cand_max"), cand_dropped=st.get("cand_dropped"))
+        res.update(repeat_found=reps, repeat_stage_dropped_cum=drops, cand_max=st.get("cand_max"), cand_dropped=st.get("cand_dropped"))
+    st = solver.stats()
+    res.update(stage_dropped_all=st.get("stage_dropped_all"), stage_maxfill_all=st.get("stage_maxfill_all"))
     print(json.dumps(res))
     if args.json:
         with open(args.json, "w") as f:
