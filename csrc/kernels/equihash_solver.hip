@@ -144,7 +144,7 @@ namespace bcpk {
 // the LDS budget must allow. GENWG/NTG: LDS-sorted generation geometry; GNT x GHPT: register
 // generation (threads x hashes per thread; 0 = use the LDS-sorted kernel).
 template <int N_, int K_, int BB_, int CAP_, int NT_, int GENWG_, int NTG_, int MAXCAND_, int CAP4_ = CAP_,
-          int CAP3_ = CAP_, int WGCU_ = 1, int GNT_ = 512, int GHPT_ = 2>
+          int CAP3_ = CAP_, int WGCU_ = 1, int GNT_ = 512, int GHPT_ = 2, int CAPF_ = 0>
 struct EhCfg {
     static constexpr int N = N_, K = K_;
     static constexpr int DB = N / (K + 1);           // digit bits
@@ -155,10 +155,16 @@ struct EhCfg {
     // LDS row capacity of a round by the width of the rows it reads: the narrow late rounds
     // hold more rows (their buckets and pair lists overflow most, from duplicate subtrees)
     static constexpr int CAP = CAP_;                 // rounds reading >= 5-word rows
+    // CAPF: the final round's capacity (0 = CAP3). Without depth-1 pruning before the final round,
+    // duplicate subtrees pile up in a few stage-(K-1) buckets; a larger final area keeps the valid
+    // rows of such a bucket from being crowded out (which rows are dropped follows the atomics).
+    static constexpr int CAPF = CAPF_ > 0 ? CAPF_ : CAP3_;
     static constexpr int cap(int round) {
-        return words(round - 1) >= 5 ? CAP_ : words(round - 1) == 4 ? CAP4_ : CAP3_;
+        return round == K_ ? CAPF : words(round - 1) >= 5 ? CAP_ : words(round - 1) == 4 ? CAP4_ : CAP3_;
     }
-    static constexpr int AREA = CAP_ > CAP4_ ? (CAP_ > CAP3_ ? CAP_ : CAP3_) : (CAP4_ > CAP3_ ? CAP4_ : CAP3_);
+    // largest non-final capacity (sizes the per-lane pair registers) and the area of every stage
+    static constexpr int AREA_NF = CAP_ > CAP4_ ? (CAP_ > CAP3_ ? CAP_ : CAP3_) : (CAP4_ > CAP3_ ? CAP4_ : CAP3_);
+    static constexpr int AREA = AREA_NF > CAPF ? AREA_NF : CAPF;
     static constexpr int NT = NT_;                   // threads per round workgroup
     static constexpr int NW = NT_ / 64;
     static constexpr int WGCU = WGCU_;
@@ -206,7 +212,10 @@ struct EhCfg {
 // Mainnet/testnet (200,9): 512 buckets x ~4096 rows, one 1024-thread round workgroup per CU
 // (BCP_EH_BB=10: 1024 buckets x ~2048 rows, two 512-thread workgroups per CU); (96,5); regtest (48,5).
 using Cfg200_9_bb10 = EhCfg<200, 9, 10, 2304, 512, 512, 1024, 256, 2560, 2688, 2, 1024, 2>;
-using Cfg200_9_bb9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, BCP_EH_GEN_NT, BCP_EH_GEN_HPT>;
+#ifndef BCP_EH_CAPF // (200,9) final-round capacity (rows per bucket; the stage areas grow to match)
+#define BCP_EH_CAPF 0
+#endif
+using Cfg200_9_bb9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, BCP_EH_GEN_NT, BCP_EH_GEN_HPT, BCP_EH_CAPF>;
 using Cfg200_9 = std::conditional_t<BCP_EH_BB == 10, Cfg200_9_bb10, Cfg200_9_bb9>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
 using Cfg48_5 = EhCfg<48, 5, 3, 512, 64, 8, 64, 256>; // 512-slot areas: 8 pairs per lane (a 256-pair list overflowed on duplicate-heavy nonces)
@@ -608,7 +617,7 @@ template <class C> constexpr int un_walk_offp(int cap) { return un_walk_bend<C>(
 // grow past the row count (duplicate subtrees) and overflowed in round 8.
 template <class C> constexpr int round_mp(int stage) {
     return stage == C::K ? 1
-                         : (C::AREA + C::NT - 1) / C::NT + (C::K == 9 && stage >= BCP_EH_MP_LATE_FROM ? BCP_EH_MP_LATE : 0);
+                         : (C::AREA_NF + C::NT - 1) / C::NT + (C::K == 9 && stage >= BCP_EH_MP_LATE_FROM ? BCP_EH_MP_LATE : 0);
 }
 template <class C> constexpr int round_un(int stage) {
     const int cap = C::cap(stage);
@@ -1789,7 +1798,10 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
             for (size_t x = 0; x < (size_t)ns * NB; ++x) {
                 const uint64_t fill = impl->h_ctr_all.p[(s * impl->batch) * NB + x];
                 impl->stats.stage_maxfill_all[s] = std::max<uint64_t>(impl->stats.stage_maxfill_all[s], fill);
-                if (fill > impl->caps[s]) impl->stats.stage_dropped_all[s] += fill - impl->caps[s];
+                if (fill > impl->caps[s]) {
+                    impl->stats.stage_dropped_all[s] += fill - impl->caps[s];
+                    impl->stats.overflow_fills.push_back((uint64_t)s << 32 | fill);
+                }
             }
         for (size_t s = 0; s < impl->kstages; ++s) {
             std::vector<uint64_t> fills;

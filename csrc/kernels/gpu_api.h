@@ -48,6 +48,7 @@ struct EhGpuStats {
     std::vector<std::vector<uint64_t>> stage_top;
     std::vector<uint64_t> pair_dropped;
     std::vector<uint64_t> stage_dropped_all, stage_maxfill_all;     // debug: every nonce (dropped: accumulated)
+    std::vector<uint64_t> overflow_fills; // debug: (stage << 32 | fill) of every bucket past its capacity (accumulated)
     std::vector<std::vector<uint32_t>> debug_cands;                  // debug: every candidate of nonce 0 (valid or not)                              // debug: pair-list overflow per round (batch total)                    // debug: 8 fullest buckets per stage
 };
 

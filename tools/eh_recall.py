@@ -73,7 +73,8 @@ def main():
         st = solver.stats()
         res.update(repeat_found=reps, repeat_stage_dropped_cum=drops, cand_max=st.get("cand_max"), cand_dropped=st.get("cand_dropped"))
     st = solver.stats()
-    res.update(stage_dropped_all=st.get("stage_dropped_all"), stage_maxfill_all=st.get("stage_maxfill_all"))
+    res.update(stage_dropped_all=st.get("stage_dropped_all"), stage_maxfill_all=st.get("stage_maxfill_all"),
+               overflow_fills=[(f >> 32, f & 0xffffffff) for f in (st.get("overflow_fills") or [])][:64])
     print(json.dumps(res))
     if args.json:
         with open(args.json, "w") as f:
