@@ -213,7 +213,7 @@ struct EhCfg {
 // (BCP_EH_BB=10: 1024 buckets x ~2048 rows, two 512-thread workgroups per CU); (96,5); regtest (48,5).
 using Cfg200_9_bb10 = EhCfg<200, 9, 10, 2304, 512, 512, 1024, 256, 2560, 2688, 2, 1024, 2>;
 #ifndef BCP_EH_CAPF // (200,9) final-round capacity (rows per bucket; the stage areas grow to match)
-#define BCP_EH_CAPF 0
+#define BCP_EH_CAPF 6016 // 5120 overflowed by 2-140 rows in ~12 buckets per 32 nonces (recall_base.json, round 5); 6016 keeps two final-round WGs per CU
 #endif
 using Cfg200_9_bb9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, BCP_EH_GEN_NT, BCP_EH_GEN_HPT, BCP_EH_CAPF>;
 using Cfg200_9 = std::conditional_t<BCP_EH_BB == 10, Cfg200_9_bb10, Cfg200_9_bb9>;

@@ -13,7 +13,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-GEOM = {(48, 5): (8, 512), (96, 5): (128, 1280), (200, 9): (512, int(os.environ.get('BCP_EH_AREA', 5120)))}  # (NB, AREA)
+GEOM = {(48, 5): (8, 512), (96, 5): (128, 1280), (200, 9): (512, int(os.environ.get('BCP_EH_AREA', 6016)))}  # (NB, AREA)
 
 
 def trace_missing(dump, n, k, idx):
