@@ -194,6 +194,29 @@ def test_gpu_solver_200_9(native):
 
 
 @pytest.mark.gpu
+def test_gpu_solver_200_9_no_overflow(native):
+    """No row of any nonce is dropped at a bucket's capacity and no final candidate past the list,
+    on the 32 nonces of tools/eh_recall.py. The bucket fills do not depend on the order of the
+    atomics, so this is deterministic. With the final round at 5120 rows, about 12 stage-8 buckets
+    of these nonces overflowed by 2-140 rows, and the dropped rows, chosen by the atomics, cost a
+    solution in 3 of 17 solves (profiles/equihash_r5.md, final-round capacity)."""
+    states = []
+    for nonce in range(32):
+        st = native.EquihashState(200, 9)
+        st.update(header_input(nonce, b"main"))
+        states.append(st)
+    solver = native.EquihashGpuSolver(200, 9, 8)
+    solver.set_debug(True)
+    found = 0
+    for b0 in range(0, 32, 8):
+        found += sum(map(len, solver.solve(states[b0:b0 + 8])))
+    st = solver.stats()
+    assert sum(st["stage_dropped_all"]) == 0, (st["stage_dropped_all"], st["overflow_fills"][:16])
+    assert st["cand_dropped"] == 0 and st["cand_max"] < 256
+    assert found >= 50  # 54 from the CPU solver
+
+
+@pytest.mark.gpu
 def test_gpu_solver_recall_small(native):
     """(48,5) / (96,5): GPU recall >= 0.97 of the CPU solver over 64 nonces."""
     for n, k in [(48, 5), (96, 5)]:
