@@ -212,6 +212,9 @@ struct EhCfg {
 // Mainnet/testnet (200,9): 512 buckets x ~4096 rows, one 1024-thread round workgroup per CU
 // (BCP_EH_BB=10: 1024 buckets x ~2048 rows, two 512-thread workgroups per CU); (96,5); regtest (48,5).
 using Cfg200_9_bb10 = EhCfg<200, 9, 10, 2304, 512, 512, 1024, 256, 2560, 2688, 2, 1024, 2>;
+#ifndef BCP_EH_PAD_ODD // odd-width rows take an even LDS stride (8-byte LDS reads and writes): 1 = all odd widths, 3 or 5 = that width only
+#define BCP_EH_PAD_ODD 0
+#endif
 #ifndef BCP_EH_CAPF // (200,9) final-round capacity (rows per bucket; the stage areas grow to match)
 #define BCP_EH_CAPF 6016 // 5120 overflowed by 2-140 rows in ~12 buckets per 32 nonces (recall_base.json, round 5); 6016 keeps two final-round WGs per CU
 #endif
@@ -361,12 +364,14 @@ template <int W> __device__ __forceinline__ void row_load(__amdgpu_buffer_rsrc_t
 // x = LDS row i XOR LDS row j (rows of WI words): 8-byte LDS reads when rows are 8-byte aligned
 // (even WI). Rows are random here, so every read is bank-conflict bound; a ds_read_b64 spreads its
 // lanes over 64 banks where a ds_read2_b32 pays two 32-bank conflict rounds.
-template <int WI> __device__ __forceinline__ void lds_row_xor(const uint32_t* rows, uint32_t i, uint32_t j, uint32_t* x) {
-    if constexpr (WI % 2 == 0) {
+// LS: the LDS row stride in words (WI, or WI + 1 for odd WI under BCP_EH_PAD_ODD; x then has room
+// for the pad word, which is zero).
+template <int WI, int LS = WI> __device__ __forceinline__ void lds_row_xor(const uint32_t* rows, uint32_t i, uint32_t j, uint32_t* x) {
+    if constexpr (LS % 2 == 0) {
         const u2v* r2 = reinterpret_cast<const u2v*>(rows);
 #pragma unroll
-        for (int w = 0; w < WI / 2; ++w) {
-            const u2v a = r2[i * (WI / 2) + w], b = r2[j * (WI / 2) + w];
+        for (int w = 0; w < LS / 2; ++w) {
+            const u2v a = r2[i * (LS / 2) + w], b = r2[j * (LS / 2) + w];
             x[2 * w] = a.x ^ b.x;
             x[2 * w + 1] = a.y ^ b.y;
         }
@@ -642,7 +647,8 @@ template <class C> constexpr bool round_pl(int stage) {
 }
 template <class C> constexpr int round_wgcu(int stage) { return round_pl<C>(stage) ? 2 : C::WGCU; }
 template <class C> constexpr int round_lds(int stage, bool prune) {
-    const int WI = round_pl<C>(stage) ? 1 : C::words(stage - 1); // LDS words per row
+    const int WR = C::words(stage - 1);
+    const int WI = round_pl<C>(stage) ? 1 : (BCP_EH_PAD_ODD && WR > 1 && WR % 2 && (BCP_EH_PAD_ODD == 1 || BCP_EH_PAD_ODD == WR)) ? WR + 1 : WR; // LDS words per row
     const int cap = C::cap(stage);
     const int marks = stage == C::K || BCP_EH_PAIRS ? 4 : (round_mp<C>(stage) * C::NT * 2 + 3) / 4 * 4;
     const int pruneb = prune ? cap * 4 + (C::cp(stage - 1) ? 0 : (cap * 2 + 3) / 4 * 4) : 0;
@@ -686,7 +692,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     constexpr bool FINAL = STAGE == C::K;
     constexpr bool PRUNE = round_prunes<C>(STAGE);
     constexpr bool PL = round_pl<C>(STAGE);                  // payload-light (LDS holds row word 0 only)
-    constexpr int WL = PL ? 1 : WI;                           // LDS words per row
+    constexpr int WL = PL ? 1 : (BCP_EH_PAD_ODD && WI > 1 && WI % 2 && (BCP_EH_PAD_ODD == 1 || BCP_EH_PAD_ODD == WI)) ? WI + 1 : WI; // LDS words per row (stride)
     static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024 / round_wgcu<C>(STAGE), "round LDS budget");
     static_assert(!PL || (!PRUNE && !FINAL), "payload-light rounds neither prune nor finish");
     constexpr int NT = C::NT;
@@ -753,7 +759,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                          (ai >> 16) == (bi & 0xffff) || (ai >> 16) == (bi >> 16);
         if (!hit) return false;
         if constexpr (CPI)
-            return ((a ^ b) & ~C::IMASK) == 0 && ((rows[i * WI + WI - 1] ^ rows[j * WI + WI - 1]) & RMI) == 0;
+            return ((a ^ b) & ~C::IMASK) == 0 && ((rows[i * WL + WI - 1] ^ rows[j * WL + WI - 1]) & RMI) == 0;
         else
             return pdw[i] == pdw[j];
     };
@@ -771,7 +777,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             for (int w = 1; w < WI; ++w) {
                 uint32_t y;
                 if constexpr (PL) y = grow(i, w) ^ grow(j, w);
-                else y = rows[i * WI + w] ^ rows[j * WI + w];
+                else y = rows[i * WL + w] ^ rows[j * WL + w];
                 if (w == WI - 1) y &= ~RMI;
                 keep |= y != 0;
             }
@@ -873,13 +879,13 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     if constexpr (PL) {
                         rows[r] = nr[u][0];
                     } else if constexpr (!SORTC) {
-                        if constexpr (WI % 2 == 0) {
+                        if constexpr (WL % 2 == 0) {
 #pragma unroll
-                            for (int w = 0; w < WI; w += 2)
-                                *reinterpret_cast<u2v*>(&rows[r * WI + w]) = u2v{nr[u][w], nr[u][w + 1]};
+                            for (int w = 0; w < WL; w += 2)
+                                *reinterpret_cast<u2v*>(&rows[r * WL + w]) = u2v{nr[u][w], w + 1 < WI ? nr[u][w + 1 < WI ? w + 1 : 0] : 0u};
                         } else {
 #pragma unroll
-                            for (int w = 0; w < WI; ++w) rows[r * WI + w] = nr[u][w];
+                            for (int w = 0; w < WI; ++w) rows[r * WL + w] = nr[u][w];
                         }
                         if constexpr (PRUNE) {
                             psig[r] = nr[u][WI];
@@ -948,13 +954,13 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     krank[u] = pos;
                     kpairs[u] = min(e - pos - 1, 14u);
                     if constexpr (SORTC) { // the row goes to its sorted position (its group's rows are adjacent)
-                        if constexpr (WI % 2 == 0) {
+                        if constexpr (WL % 2 == 0) {
 #pragma unroll
-                            for (int w = 0; w < WI; w += 2)
-                                *reinterpret_cast<u2v*>(&rows[pos * WI + w]) = u2v{nr[u][w], nr[u][w + 1]};
+                            for (int w = 0; w < WL; w += 2)
+                                *reinterpret_cast<u2v*>(&rows[pos * WL + w]) = u2v{nr[u][w], w + 1 < WI ? nr[u][w + 1 < WI ? w + 1 : 0] : 0u};
                         } else {
 #pragma unroll
-                            for (int w = 0; w < WI; ++w) rows[pos * WI + w] = nr[u][w];
+                            for (int w = 0; w < WI; ++w) rows[pos * WL + w] = nr[u][w];
                         }
                         if constexpr (PRUNE) {
                             psig[pos] = nr[u][WI];
@@ -1202,7 +1208,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
 #pragma unroll
                     for (int w = 0; w < WI; ++w) x[w] = pa[c][w] ^ pb[c][w];
                 } else {
-                    lds_row_xor<WI>(rows, si, sj, x);
+                    lds_row_xor<WI, WL>(rows, si, sj, x);
                 }
                 x[WI - 1] &= ~RMI;
                 x[WI] = 0;
