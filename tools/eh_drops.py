@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Row and pair losses of the (200,9) GPU solver over many nonces: per round, the rows dropped for
 LDS capacity (sampled: nonce 0 of each batch) and the pairs dropped when a bucket's pair list
-overflowed (every bucket), with candidates, duplicates and solutions per nonce.
+overflowed (every bucket), the same row losses over every nonce, with candidates, duplicates and solutions per nonce.
 
 python tools/eh_drops.py [--batches 8] [--batch 32]
 """
@@ -41,7 +41,13 @@ def main():
     n = a.batches * a.batch
     print(json.dumps({"nonces": n, "solutions_per_nonce": round(sols / n, 4),
                       "pair_dropped_per_round": pair_drop, "rows_dropped_sampled": row_drop,
-                      "candidates": st["candidates"], "duplicates": st["duplicates"]}))
+                      "candidates": st["candidates"], "duplicates": st["duplicates"],
+                      # every nonce (accumulated over the run): rows past a round's capacity,
+                      # the buckets that overflowed, and final candidates past the list
+                      "rows_dropped_all": st.get("stage_dropped_all"),
+                      "overflow_buckets": len(st.get("overflow_fills") or []),
+                      "overflow_fills_first": [(f >> 32, f & 0xFFFFFFFF) for f in (st.get("overflow_fills") or [])][:32],
+                      "cand_max": st.get("cand_max"), "cand_dropped": st.get("cand_dropped")}))
 
 
 if __name__ == "__main__":
