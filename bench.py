@@ -71,7 +71,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "32")))
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "48")))
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
     ap.add_argument("--solvers", type=int, default=int(os.environ.get("BCP_EH_SOLVERS", "2")),
                     help="solvers in flight per GPU (each its own stream and buffers)")
