@@ -217,7 +217,7 @@ void GpuVerifyService::RunSharded(size_t n, bool equihash,
     for (size_t s = 0; s < shards; s++) {
         const size_t lo = plan[s].lo, hi = plan[s].hi;
         Lane* L = ls[plan[s].lane].get();
-        auto task = [&fn, &latch, L, lo, hi]() {
+        auto task = [&fn, &latch, L, lo, hi, equihash]() {
             std::exception_ptr e;
             try {
                 if (!L->gl) throw std::runtime_error("GPU verify lane on device " + std::to_string(L->device) +
@@ -225,6 +225,7 @@ void GpuVerifyService::RunSharded(size_t n, bool equihash,
                 fn(*L->gl, lo, hi, *L->fill);
                 L->batches++;
                 L->items += hi - lo;
+                (equihash ? L->equihashItems : L->ecdsaItems) += hi - lo;
                 L->fillMicros = L->gl->FillMicros(); // published for Stats() (this is the lane's thread)
                 L->deviceMicros = L->gl->DeviceMicros();
             } catch (...) {
@@ -313,7 +314,8 @@ std::vector<GpuVerifyService::LaneStats> GpuVerifyService::Stats() const {
     std::lock_guard<std::mutex> l(m);
     for (const auto& L : lanes) {
         out.push_back(LaneStats{L->device, L->priority.load(), L->batches.load(), L->items.load(),
-                                L->fillMicros.load(), L->deviceMicros.load()});
+                                L->fillMicros.load(), L->deviceMicros.load(), L->ecdsaItems.load(),
+                                L->equihashItems.load()});
     }
     return out;
 }

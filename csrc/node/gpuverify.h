@@ -93,6 +93,7 @@ public:
         int priority;
         uint64_t batches, items;
         uint64_t fillMicros, deviceMicros; // host fill vs device share of the lane's batches
+        uint64_t ecdsaItems, equihashItems; // items by kind (signatures / header solutions)
     };
     std::vector<LaneStats> Stats() const;
     uint64_t ShardedBatches() const;
@@ -112,6 +113,7 @@ private:
         std::string initError;
         std::atomic<int> priority{0};
         std::atomic<uint64_t> batches{0}, items{0};
+        std::atomic<uint64_t> ecdsaItems{0}, equihashItems{0};
         std::atomic<uint64_t> fillMicros{0}, deviceMicros{0}; // the lane's host fill vs device time
         std::unique_ptr<WorkerPool> fill; // this lane's host-fill workers
     };

@@ -131,6 +131,8 @@ static UniValue getgpuinfo(const JSONRPCRequest& req) {
         o.pushKV("stream_priority", L.priority);
         o.pushKV("batches", L.batches);
         o.pushKV("items", L.items);
+        o.pushKV("ecdsa_items", L.ecdsaItems);
+        o.pushKV("equihash_items", L.equihashItems);
         lanes.push_back(o);
     }
     obj.pushKV("validation_lanes", lanes);
