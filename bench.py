@@ -246,7 +246,16 @@ def run(args, world):
                   file=sys.stderr, flush=True)
         verified = nbad == 0
 
+    # candidate losses over EVERY nonce of the timed steps (device counters, all solvers): rows past a
+    # round's capacity, pairs past a round's pair list, final candidates past the per-nonce list
+    rows_lost = sum(sum(sv.stats()["stage_dropped_all"] or [0]) for sv in solvers)
+    pairs_lost = sum(sum(sv.stats()["pair_dropped_all"] or [0]) for sv in solvers)
+    cands_lost = sum(sv.stats()["cand_dropped"] for sv in solvers)
     total_sols, max_dt, total_bad = aggregate(nsol, dt, nbad, world, red_dev)
+    if world > 1:
+        lost = torch.tensor([rows_lost, pairs_lost, cands_lost], dtype=torch.float64, device=red_dev)
+        dist.all_reduce(lost, op=dist.ReduceOp.SUM)
+        rows_lost, pairs_lost, cands_lost = (int(x) for x in lost.tolist())
     if total_bad:
         raise SystemExit(f"bench: GPU and CPU verifiers rejected {int(total_bad)} solver solution(s)")
     nonces = args.steps * args.batch * world
@@ -255,7 +264,6 @@ def run(args, world):
         raise SystemExit(f"bench: solver recall too low: {per_nonce:.3f} solutions/nonce "
                          f"< {MIN_SOLUTIONS_PER_NONCE}")
 
-    st = solvers[0].stats()
     if rank == 0:
         value = total_sols / max_dt
         out = {
@@ -282,7 +290,9 @@ def run(args, world):
                 "verified": verified,
                 "verified_solutions": int(total_sols) if verified else 0,
                 "gpu_cpu_verifier_disagreements": gpu_cpu_disagree,
-                "rank0_dropped_rows_sampled": st["dropped_rows_sampled"],
+                "rows_dropped_all_nonces": int(rows_lost),
+                "pairs_dropped_all_nonces": int(pairs_lost),
+                "candidates_dropped_all_nonces": int(cands_lost),
             },
         }
         print(json.dumps(out), flush=True)

@@ -6,9 +6,9 @@
 //
 //  * Rows are bucketed on the top BB bits of the current digit (NB = 2^BB buckets, ~INIT/NB rows
 //    each). (200,9) runs BB = 9: 512 buckets of ~4096 rows, one 1024-thread round workgroup per
-//    CU (145 KiB of LDS). BCP_EH_BB=10 builds 1024 buckets of ~2048 rows with two 512-thread
-//    workgroups (<= 80 KiB each) per CU; it measured slower (the phases are latency-bound per
-//    lane, and the producer runs are 4x shorter), profiles/equihash_r4.md.
+//    CU (145 KiB of LDS). 1024 buckets of ~2048 rows with two 512-thread workgroups (<= 80 KiB
+//    each) per CU measured slower (the phases are latency-bound per lane, and the producer runs
+//    are 4x shorter), profiles/equihash_r4.md.
 //    Every stage keeps each bucket CONTIGUOUS in its own area of AREA row slots.
 //  * Every kernel works "one workgroup per bucket". A producer workgroup counting-sorts its
 //    output rows by destination bucket in LDS, then claims one run per destination with ONE
@@ -48,29 +48,14 @@
 #include <stdexcept>
 #include <utility>
 
-#ifndef BCP_EH_BB // bucket bits of the (200,9) solver: 9 (one 1024-thread round workgroup per CU) or
-#define BCP_EH_BB 9 //  10 (two 512-thread workgroups per CU; measured slower, profiles/equihash_r4.md)
-#endif
-#ifndef BCP_EH_ROWONLY_LOAD // non-pruning rounds skip the parent words of a slot
-#define BCP_EH_ROWONLY_LOAD 1
-#endif
-#ifndef BCP_EH_COMPACT_PARENT // 1: one parent word where the row has spare padding bits
-#define BCP_EH_COMPACT_PARENT 1
-#endif
-#ifndef BCP_EH_ST_CPOL // cache-policy bits of the slot stores (gfx950: 1 = sc0, 2 = nt, 16 = sc1)
-#define BCP_EH_ST_CPOL 0
-#endif
-#ifndef BCP_EH_LD_CPOL // cache-policy bits of the slot loads
-#define BCP_EH_LD_CPOL 0
-#endif
+// Build options (each either the measured default or covered by the GPU tests; the variants that
+// were measured and rejected in rounds 3-5 are at git tag solver-r5-knobs, profiles/equihash_r4.md
+// and profiles/equihash_r5.md):
 #ifndef BCP_EH_XCD_MAP // 1: every kernel of a nonce runs on one XCD (nonce % 8), so the run writes
 #define BCP_EH_XCD_MAP 1  //    of a nonce meet in one L2 (batches that are a multiple of 8 nonces)
 #endif
 #ifndef BCP_EH_PF_SLICES // the next bucket's rows are prefetched in this many slices
 #define BCP_EH_PF_SLICES 3
-#endif
-#ifndef BCP_EH_GEN_WPE // minimum waves per SIMD the generation kernel's registers must allow
-#define BCP_EH_GEN_WPE 1
 #endif
 #ifndef BCP_EH_GEN_HPT // (200,9) register generation: hashes per thread
 #define BCP_EH_GEN_HPT 2
@@ -78,63 +63,15 @@
 #ifndef BCP_EH_GEN_NT // (200,9) register generation: threads per workgroup
 #define BCP_EH_GEN_NT 512
 #endif
-#ifndef BCP_EH_PRIO // 1: generation runs on a low-priority stream of its own, the rounds on a high-priority one
-#define BCP_EH_PRIO 0 //  (so one solver's generation fills the CUs beside the other solver's resident rounds)
-#endif
 #ifndef BCP_EH_PRUNE_FROM // first round that drops pairs sharing a parent (reads the parent words with the rows);
                           // the final round always does.
 #define BCP_EH_PRUNE_FROM 9 //  9 = the final round only: +4.2% Sol/s over 2 at the same recall (profiles/equihash_r5.md)
 #endif
-#ifndef BCP_EH_GEN_R0 // 1: the header generation starts each hash from the workgroup's precomputed
-#define BCP_EH_GEN_R0 1 //  g-independent part of BLAKE2b round 0 (G1..G3 and half of G0)
-#endif
-#ifndef BCP_EH_PL_CH // payload-light emit: output rows per load batch (0 = by row width)
-#define BCP_EH_PL_CH 0
-#endif
-#ifndef BCP_EH_PL_FROM // payload-light collision rounds from this round on ((200,9), rounds that do not prune; 0 = off):
-#define BCP_EH_PL_FROM 0 //   LDS keeps only word 0 of each row, the emit reads both rows from the bucket's global copy,
-#endif                   //   and two 1024-thread workgroups fit per CU (see round_pl)
 #ifndef BCP_EH_MP_LATE // extra pair slots per lane in the late collision rounds (see round_mp)
 #define BCP_EH_MP_LATE 1
 #endif
 #ifndef BCP_EH_MP_LATE_FROM
 #define BCP_EH_MP_LATE_FROM 8
-#endif
-#ifndef BCP_EH_SORTC // 1 (collision rounds with the key count folded into the commit): rows are written to LDS
-#define BCP_EH_SORTC 0  //  at their key-sorted positions once the key scan is done, so the pair list holds
-#endif                  //  sorted positions (no sidx read while listing); sidx still maps them to slots
-#ifndef BCP_EH_GEN_PERSIST // > 0: register generation runs this many persistent workgroups per CU
-#define BCP_EH_GEN_PERSIST 0 //  (each loops over work items) instead of one workgroup per item
-#endif
-#ifndef BCP_EH_EXP_STORE // timing experiments only (tools/build_variant.sh): 1 = drop the emit stores,
-#define BCP_EH_EXP_STORE 0 // 2 = store each bucket's output rows contiguously (no scatter; wrong results)
-#endif
-#ifndef BCP_EH_PAIRS // pair enumeration: 1 = per-wave compaction into an LDS pair list (one barrier),
-#define BCP_EH_PAIRS 1 //  0 = block scan + max-scan over pair indices (four barriers)
-#endif
-#ifndef BCP_EH_EXP_LOAD // timing experiment only: 1 = every round bucket loads one of its nonce's first 8
-#define BCP_EH_EXP_LOAD 0 //  areas (L2-resident) instead of its own (wrong results); 2 = gather the
-#endif                    //  bucket from 512 runs of 8 rows spread over the nonce's areas
-#ifndef BCP_EH_ISSUE_LATE // 1: a round issues its next-bucket loads after the key sort, not at the commit
-#define BCP_EH_ISSUE_LATE 0
-#endif
-#ifndef BCP_EH_KEY_COMMIT // 1: a collision round counts its rows' keys while committing them to LDS
-#define BCP_EH_KEY_COMMIT 1 //  (the rank comes back from that atomic): one LDS pass and one barrier less
-#endif
-#ifndef BCP_EH_DEST_RANK // 1: a pair keeps its rank in its destination from the histogram atomic and is
-#define BCP_EH_DEST_RANK 0 //  placed by it after the scan (no second atomic per pair); measured 0.3% slower
-#endif
-#ifndef BCP_EH_FILTER_GEN // 1 (with BCP_EH_KEY_COMMIT): pairs are filtered (identical subtrees, shared
-#define BCP_EH_FILTER_GEN 0 //  parents) and counted by destination as they are listed, not on read-back; measured 20% slower
-#endif
-#ifndef BCP_EH_VMEM_FILL // 1: a round reads the next-but-one bucket's fill with a vector (buffer) load.
-#define BCP_EH_VMEM_FILL 1 //  A scalar load shares lgkmcnt with LDS, so the barrier's lgkmcnt(0) waited on it
-#endif
-#ifndef BCP_EH_COMMIT_USE // 1: every prefetched register is used once, unconditionally, after the commit
-#define BCP_EH_COMMIT_USE 0 //  (see the commit): the compiler then knows the loads are done on every path; no change measured
-#endif
-#ifndef BCP_EH_GEN_LDS // 1: force the LDS-sorted generation kernel everywhere (A/B builds)
-#define BCP_EH_GEN_LDS 0
 #endif
 
 namespace bcpk {
@@ -192,7 +129,7 @@ struct EhCfg {
     static constexpr uint32_t RMASK = (1u << DR) - 1;
     static constexpr uint32_t IMASK = ((1u << IB) - 1) * 0x10001u;
     static constexpr bool cp(int stage) {
-        return BCP_EH_COMPACT_PARENT && stage >= 1 && stage < K && 32 * words(stage) - bits(stage) >= DR;
+        return stage >= 1 && stage < K && 32 * words(stage) - bits(stage) >= DR;
     }
     static constexpr uint32_t rmask(int stage) { return cp(stage) ? RMASK : 0u; } // parent bits in a row's padding
     // words per slot of stage s: the row, plus (s >= 1) its parent word(s)
@@ -209,17 +146,12 @@ struct EhCfg {
     static_assert(words(K - 1) == 1, "final round keeps whole rows in one LDS word");
 };
 
-// Mainnet/testnet (200,9): 512 buckets x ~4096 rows, one 1024-thread round workgroup per CU
-// (BCP_EH_BB=10: 1024 buckets x ~2048 rows, two 512-thread workgroups per CU); (96,5); regtest (48,5).
-using Cfg200_9_bb10 = EhCfg<200, 9, 10, 2304, 512, 512, 1024, 256, 2560, 2688, 2, 1024, 2>;
-#ifndef BCP_EH_PAD_ODD // odd-width rows take an even LDS stride (8-byte LDS reads and writes): 1 = all odd widths, 3 or 5 = that width only
-#define BCP_EH_PAD_ODD 0
-#endif
+// Mainnet/testnet (200,9): 512 buckets x ~4096 rows, one 1024-thread round workgroup per CU;
+// (96,5); regtest (48,5).
 #ifndef BCP_EH_CAPF // (200,9) final-round capacity (rows per bucket; the stage areas grow to match)
 #define BCP_EH_CAPF 6016 // 5120 overflowed by 2-140 rows in ~12 buckets per 32 nonces (recall_base.json, round 5); 6016 keeps two final-round WGs per CU
 #endif
-using Cfg200_9_bb9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, BCP_EH_GEN_NT, BCP_EH_GEN_HPT, BCP_EH_CAPF>;
-using Cfg200_9 = std::conditional_t<BCP_EH_BB == 10, Cfg200_9_bb10, Cfg200_9_bb9>;
+using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, BCP_EH_GEN_NT, BCP_EH_GEN_HPT, BCP_EH_CAPF>;
 using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
 using Cfg48_5 = EhCfg<48, 5, 3, 512, 64, 8, 64, 256>; // 512-slot areas: 8 pairs per lane (a 256-pair list overflowed on duplicate-heavy nonces)
 
@@ -332,46 +264,44 @@ __device__ void block_maxscan(T* v, int n, uint32_t* wsum) {
 template <int W> __device__ __forceinline__ void row_store(__amdgpu_buffer_rsrc_t rs, uint32_t off, const uint32_t* v) {
     if constexpr (W >= 4) {
         const u4v x = {v[0], v[1], v[2], v[3]};
-        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, BCP_EH_ST_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b128(x, rs, off, 0, 0);
         row_store<W - 4>(rs, off + 16, v + 4);
     } else if constexpr (W == 3) {
         const u3v x = {v[0], v[1], v[2]};
-        __builtin_amdgcn_raw_buffer_store_b96(x, rs, off, 0, BCP_EH_ST_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b96(x, rs, off, 0, 0);
     } else if constexpr (W == 2) {
         const u2v x = {v[0], v[1]};
-        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, BCP_EH_ST_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b64(x, rs, off, 0, 0);
     } else if constexpr (W == 1) {
-        __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, BCP_EH_ST_CPOL);
+        __builtin_amdgcn_raw_buffer_store_b32(v[0], rs, off, 0, 0);
     }
 }
 
 template <int W> __device__ __forceinline__ void row_load(__amdgpu_buffer_rsrc_t rs, uint32_t off, uint32_t* v) {
     if constexpr (W >= 4) {
-        const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, BCP_EH_LD_CPOL);
+        const u4v x = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0);
         v[0] = x.x, v[1] = x.y, v[2] = x.z, v[3] = x.w;
         row_load<W - 4>(rs, off + 16, v + 4);
     } else if constexpr (W == 3) {
-        const u3v x = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, BCP_EH_LD_CPOL);
+        const u3v x = __builtin_amdgcn_raw_buffer_load_b96(rs, off, 0, 0);
         v[0] = x.x, v[1] = x.y, v[2] = x.z;
     } else if constexpr (W == 2) {
-        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, BCP_EH_LD_CPOL);
+        const u2v x = __builtin_amdgcn_raw_buffer_load_b64(rs, off, 0, 0);
         v[0] = x.x, v[1] = x.y;
     } else if constexpr (W == 1) {
-        v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, BCP_EH_LD_CPOL);
+        v[0] = __builtin_amdgcn_raw_buffer_load_b32(rs, off, 0, 0);
     }
 }
 
 // x = LDS row i XOR LDS row j (rows of WI words): 8-byte LDS reads when rows are 8-byte aligned
 // (even WI). Rows are random here, so every read is bank-conflict bound; a ds_read_b64 spreads its
 // lanes over 64 banks where a ds_read2_b32 pays two 32-bank conflict rounds.
-// LS: the LDS row stride in words (WI, or WI + 1 for odd WI under BCP_EH_PAD_ODD; x then has room
-// for the pad word, which is zero).
-template <int WI, int LS = WI> __device__ __forceinline__ void lds_row_xor(const uint32_t* rows, uint32_t i, uint32_t j, uint32_t* x) {
-    if constexpr (LS % 2 == 0) {
+template <int WI> __device__ __forceinline__ void lds_row_xor(const uint32_t* rows, uint32_t i, uint32_t j, uint32_t* x) {
+    if constexpr (WI % 2 == 0) {
         const u2v* r2 = reinterpret_cast<const u2v*>(rows);
 #pragma unroll
-        for (int w = 0; w < LS / 2; ++w) {
-            const u2v a = r2[i * (LS / 2) + w], b = r2[j * (LS / 2) + w];
+        for (int w = 0; w < WI / 2; ++w) {
+            const u2v a = r2[i * (WI / 2) + w], b = r2[j * (WI / 2) + w];
             x[2 * w] = a.x ^ b.x;
             x[2 * w + 1] = a.y ^ b.y;
         }
@@ -490,11 +420,11 @@ __global__ __launch_bounds__(C::NTG) void eh_gen(const EhBaseState* __restrict__
 template <class C, int NTG, int HPT> struct GenReg {
     static constexpr int RPT = HPT * C::IPH;            // rows per thread
     static constexpr int RPW = NTG > 0 ? NTG * RPT : 1; // rows per workgroup
-    static constexpr bool OK = !BCP_EH_GEN_LDS && NTG > 0 && C::INIT % RPW == 0;
+    static constexpr bool OK = NTG > 0 && C::INIT % RPW == 0;
     static constexpr int GWG = OK ? C::INIT / RPW : 1;  // workgroups per nonce
 };
 template <class C, bool HDR, int NTG, int HPT>
-__global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_WPE))) void eh_gen_reg(const EhBaseState* __restrict__ states, uint32_t* __restrict__ R,
+__global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(1))) void eh_gen_reg(const EhBaseState* __restrict__ states, uint32_t* __restrict__ R,
                                                   uint32_t* __restrict__ LEAF, uint32_t* __restrict__ CTR0, int items) {
     using G = GenReg<C, NTG, HPT>;
     static_assert(G::OK, "register generation geometry");
@@ -502,7 +432,7 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     constexpr int SW = (C::N + 31) / 32 + 1;
     constexpr uint32_t OCAP = C::cap(1);
     __shared__ uint32_t hist[C::NB], base[C::NB];
-    __shared__ uint64_t r0p[HDR && BCP_EH_GEN_R0 ? 16 : 1]; // the nonce's g-independent round-0 prefix
+    __shared__ uint64_t r0p[HDR ? 16 : 1]; // the nonce's g-independent round-0 prefix
     const int tid = threadIdx.x;
     // work item b = (nonce, gw); a persistent grid (gridDim.x < items, a multiple of 8) keeps every
     // item of a workgroup on that workgroup's XCD
@@ -517,7 +447,7 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     if (b != (int)blockIdx.x) __syncthreads(); // the previous item's scatter has read base[]
     const EhBaseState& bs = states[nonce];
     for (int i = tid; i < C::NB; i += NTG) hist[i] = 0;
-    if constexpr (HDR && BCP_EH_GEN_R0) {
+    if constexpr (HDR) {
         if (tid == 0) {
             uint64_t P[16];
             eh_hdr_round0_uniform(bs, P);
@@ -534,13 +464,11 @@ __global__ __launch_bounds__(NTG) __attribute__((amdgpu_waves_per_eu(BCP_EH_GEN_
     for (int hh = 0; hh < HPT; ++hh) {
         const uint32_t g = g0 + hh * NTG + tid;
         uint64_t h[8];
-        if constexpr (HDR && BCP_EH_GEN_R0) {
+        if constexpr (HDR) {
             uint64_t P[16];
 #pragma unroll
             for (int i = 0; i < 16; ++i) P[i] = r0p[i];
             eh_hash_g_hdr_from(P, bs, g, h);
-        } else if constexpr (HDR) {
-            eh_hash_g_hdr(bs, g, h);
         } else {
             eh_hash_g(bs, g, h);
         }
@@ -612,11 +540,11 @@ template <class C> __host__ __device__ __forceinline__ uint32_t cunpack_d(uint32
         }                                                                                            \
     } while (0)
 
-// LDS bytes of a round. Phase-D union `un` (bytes): {sidx[CAP] u16, bend[NRESTS] u32, then
-// offp[CAP] u16 or plist[MP*NT] u32} during the collision search, the slot -> pair table
-// spair[MP*NT] u32 after it.
+// LDS bytes of a round. Phase-D union `un` (bytes): {sidx[CAP] u16, bend[NRESTS] u32, then the
+// pair list plist[MP*NT] u32} during the collision search; the slot -> pair table spair[MP*NT]
+// u32 (aliasing plist) after it.
 template <class C> constexpr int un_walk_bend(int cap) { return (cap * 2 + 3) / 4 * 4; }
-template <class C> constexpr int un_walk_offp(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
+template <class C> constexpr int un_walk_list(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
 // Pairs per lane: one lane per LDS row slot, plus BCP_EH_MP_LATE extra from round
 // BCP_EH_MP_LATE_FROM on ((200,9) only): without depth-1 pruning the late rounds' pair lists
 // grow past the row count (duplicate subtrees) and overflowed in round 8.
@@ -626,35 +554,18 @@ template <class C> constexpr int round_mp(int stage) {
 }
 template <class C> constexpr int round_un(int stage) {
     const int cap = C::cap(stage);
-    if (stage == C::K) return un_walk_offp<C>(cap); // final round: sidx and bend only
-    // offp[CAP] u16 (scan enumeration) or the pair list plist[MP*NT] u32 (wave compaction)
-    const int walk = un_walk_offp<C>(cap) + (BCP_EH_PAIRS && stage < C::K ? round_mp<C>(stage) * C::NT * 4 : cap * 2);
+    if (stage == C::K) return un_walk_list<C>(cap); // final round: sidx and bend only
+    const int walk = un_walk_list<C>(cap) + round_mp<C>(stage) * C::NT * 4; // + the pair list
     const int pairs = round_mp<C>(stage) * C::NT * 4; // spair: every pair a lane may hold
     return walk > pairs ? walk : pairs;
 }
-template <class C> constexpr bool round_fgen(int stage) {
-    return BCP_EH_FILTER_GEN && BCP_EH_KEY_COMMIT && BCP_EH_PAIRS && stage < C::K;
-}
-// Payload-light round (BCP_EH_PL_FROM): the collision search needs only each row's first word
-// (the key and the next digit), so LDS keeps that word alone; the rare full comparison of a pair
-// whose first words match and the emit's XOR read both rows from the bucket's input area in
-// global memory (just streamed in, so mostly L2-resident). LDS then drops below 80 KiB, and two
-// 1024-thread workgroups (32 waves) share a CU: one's barrier-bound phases overlap the other's.
-// Rounds that prune keep their rows in LDS (the parent words are compared there).
-template <class C> constexpr bool round_pl(int stage) {
-    return BCP_EH_PL_FROM > 0 && C::K == 9 && stage >= BCP_EH_PL_FROM && stage < C::K && stage < BCP_EH_PRUNE_FROM &&
-           !BCP_EH_SORTC;
-}
-template <class C> constexpr int round_wgcu(int stage) { return round_pl<C>(stage) ? 2 : C::WGCU; }
 template <class C> constexpr int round_lds(int stage, bool prune) {
     const int WR = C::words(stage - 1);
-    const int WI = round_pl<C>(stage) ? 1 : (BCP_EH_PAD_ODD && WR > 1 && WR % 2 && (BCP_EH_PAD_ODD == 1 || BCP_EH_PAD_ODD == WR)) ? WR + 1 : WR; // LDS words per row
+    const int WI = WR; // LDS words per row
     const int cap = C::cap(stage);
-    const int marks = stage == C::K || BCP_EH_PAIRS ? 4 : (round_mp<C>(stage) * C::NT * 2 + 3) / 4 * 4;
     const int pruneb = prune ? cap * 4 + (C::cp(stage - 1) ? 0 : (cap * 2 + 3) / 4 * 4) : 0;
     const int hists = stage == C::K ? 12 : 2 * C::HW * 4 + (C::NB * (C::H16 ? 2 : 4) + 3) / 4 * 4;
-    const int pdlb = round_fgen<C>(stage) ? (round_mp<C>(stage) * C::NT * 2 + 3) / 4 * 4 : 0;
-    return (cap * WI + 3) / 4 * 16 + pruneb + marks + round_un<C>(stage) + hists + pdlb + (C::NW + 1) * 4;
+    return (cap * WI + 3) / 4 * 16 + pruneb + 4 + round_un<C>(stage) + hists + (C::NW + 1) * 4;
 }
 // Depth-1 duplicate pruning wherever its parent words fit next to the full rows.
 template <class C> constexpr bool round_prunes(int stage) {
@@ -667,22 +578,28 @@ template <class C> constexpr bool round_prunes(int stage) {
 // Bucket bk = nonce*NB + d holds the stage STAGE-1 rows whose top digit bits are d (area d of
 // that stage, CTRin[bk] rows).
 //
-// The kernel is PERSISTENT and software-pipelined: WGCU workgroups per CU walk buckets
-// blockIdx.x, +gridDim.x, ... While one collides bucket b out of LDS, the rows of its next
+// The kernel is PERSISTENT and software-pipelined: one workgroup per CU walks buckets
+// blockIdx.x, +gridDim.x, ... While it collides bucket b out of LDS, the rows of its next
 // bucket are in flight into VGPRs (lane-flat row loads of the contiguous area, issued in slices
 // across the phases; plain loads are not drained by a bare barrier). Per bucket:
-//   A. commit: prefetched rows (VGPRs) -> LDS rows (+ parent words when pruning);
+//   A. commit: prefetched rows (VGPRs) -> LDS rows (+ parent words when pruning), counting each
+//      row's RB-bit key with a returning LDS atomic (its rank in the key group);
 //      issue the first slice of the next bucket's loads;
-//   D1. counting sort of the rows by their RB bits;
-//   D2. atomic-free pair enumeration (scan + max-scan, one lane per pair; depth-1 pruning);
-//   D3. destination histogram -> one atomicAdd per destination bucket claims this bucket's
-//       runs there; counting sort of the pairs by destination;
+//   D1. key scan: every committed row learns its sorted position;
+//   D2. pair list by per-wave compaction (one barrier), then the pair filter (identical
+//       subtrees; depth-1 pruning where the round prunes) and the destination histogram;
+//   D3. one atomicAdd per destination bucket claims this bucket's runs there; counting sort of
+//       the pairs by destination;
 //   D4. one-lane-per-row emit (XOR, shift one digit, 16-byte stores) into the claimed runs,
 //       plus the parent word(s).
+// The final round (STAGE == K) sorts its one-word rows by key and lists the candidates: pairs
+// equal on all remaining bits.
 // Input rows whose slots carry compact parents keep the parent-bucket bits in their padding in
 // LDS (the prune check reads them); every comparison and the emit XOR mask them out (RMI).
+// pdrop[STAGE]: pairs lost to a full pair list; pdrop[K + STAGE]: stage-(STAGE-1) rows past the
+// round's capacity (offered to a bucket but never read), counted for every nonce.
 template <class C, int STAGE, bool STAMP>
-__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(round_wgcu<C>(STAGE) * C::NT / 256)))
+__global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::WGCU * C::NT / 256)))
 void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTRin, uint32_t* __restrict__ Rout,
               uint32_t* __restrict__ CTRout, uint32_t* __restrict__ ncand, uint64_t* __restrict__ cand,
               uint64_t* __restrict__ stamps, uint32_t* __restrict__ pdrop, int nbk) {
@@ -691,41 +608,32 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     constexpr int CAP = C::cap(STAGE);                        // LDS rows / pair-list entries
     constexpr bool FINAL = STAGE == C::K;
     constexpr bool PRUNE = round_prunes<C>(STAGE);
-    constexpr bool PL = round_pl<C>(STAGE);                  // payload-light (LDS holds row word 0 only)
-    constexpr int WL = PL ? 1 : (BCP_EH_PAD_ODD && WI > 1 && WI % 2 && (BCP_EH_PAD_ODD == 1 || BCP_EH_PAD_ODD == WI)) ? WI + 1 : WI; // LDS words per row (stride)
-    static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024 / round_wgcu<C>(STAGE), "round LDS budget");
-    static_assert(!PL || (!PRUNE && !FINAL), "payload-light rounds neither prune nor finish");
+    static_assert(round_lds<C>(STAGE, PRUNE) <= 160 * 1024 / C::WGCU, "round LDS budget");
     constexpr int NT = C::NT;
     constexpr int RPL = (CAP + NT - 1) / NT;                // prefetched rows per lane
     constexpr int MP = round_mp<C>(STAGE);                  // pairs per lane (registers)
-    constexpr int MPR = (CAP + NT - 1) / NT;                 // LDS rows per lane (scans)
     constexpr int SWI = C::sw(STAGE - 1);                  // words per input slot
     constexpr int SWO = STAGE < C::K ? C::sw(STAGE) : 1;   // words per output slot
     constexpr bool CPI = C::cp(STAGE - 1);                 // input slots carry one compact parent word
     constexpr uint32_t RMI = C::rmask(STAGE - 1);          // parent bits in the input rows' padding
     constexpr int SLI = (RPL + BCP_EH_PF_SLICES - 1) / BCP_EH_PF_SLICES; // prefetch slice (rows per phase)
     constexpr int BPT = (C::NB + NT - 1) / NT;             // destination buckets per thread (claims)
-    // key counting folded into the commit (non-final rounds with the wave-compacted pair list):
-    // bend holds counts after the commit and group starts after the scan; spair then aliases the
-    // pair list, so bend survives the emit and is cleared for the next bucket in D3
-    constexpr bool FOLD = BCP_EH_KEY_COMMIT && BCP_EH_PAIRS && !FINAL;
-    constexpr bool FGEN = round_fgen<C>(STAGE); // filter pairs while listing them (implies FOLD)
-    constexpr bool SORTC = BCP_EH_SORTC && FOLD && !FGEN; // rows committed at key-sorted LDS positions
+    // key counting folded into the commit (collision rounds): bend holds counts after the commit
+    // and group starts after the scan; spair then aliases the pair list, so bend survives the
+    // emit and is cleared for the next bucket in D3
+    constexpr bool FOLD = !FINAL;
     using HT = std::conditional_t<C::H16, uint16_t, uint32_t>;
-    __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WL + 3) / 4 * 4];
+    __shared__ __attribute__((aligned(16))) uint32_t rows[(CAP * WI + 3) / 4 * 4];
     __shared__ uint32_t psig[PRUNE ? CAP : 1];                // the input rows' parent word (j << 16 | i, + d bits)
     __shared__ uint16_t pdw[PRUNE && !CPI ? CAP : 1];         // two-word parents: the producing bucket
-    __shared__ uint16_t pmark[FINAL || BCP_EH_PAIRS ? 2 : MP * NT]; // pair index -> first sorted position
     __shared__ uint32_t npairs;                                // wave-compaction pair list fill
-    __shared__ uint16_t pdl[FGEN ? MP * NT : 1];              // FGEN: destination bucket of each listed pair
     __shared__ __attribute__((aligned(16))) uint8_t un[round_un<C>(STAGE)];
     __shared__ uint32_t hist_[FINAL ? 1 : C::HW], cur_[FINAL ? 1 : C::HW]; // H16: two 16-bit counters per word
     __shared__ HT base[FINAL ? 1 : C::NB];
     __shared__ uint32_t wsum[C::NW + 1];
     uint16_t* sidx = reinterpret_cast<uint16_t*>(un);
     uint32_t* bend = reinterpret_cast<uint32_t*>(un + un_walk_bend<C>(CAP));
-    uint16_t* offp = reinterpret_cast<uint16_t*>(un + un_walk_offp<C>(CAP));
-    uint32_t* plist = reinterpret_cast<uint32_t*>(un + un_walk_offp<C>(CAP));
+    uint32_t* plist = reinterpret_cast<uint32_t*>(un + un_walk_list<C>(CAP));
     uint32_t* spair = FOLD ? plist : reinterpret_cast<uint32_t*>(un);
     const int tid = threadIdx.x;
     const int G = gridDim.x;
@@ -746,11 +654,6 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             return atomicAdd(&h[b], 1u);
         }
     };
-    // PL: the current bucket's input area (the full rows the LDS words came from)
-    __amdgpu_buffer_rsrc_t rs_cur = buf_rsrc(Rin, 0);
-    auto grow = [&](uint32_t i, int w) -> uint32_t {
-        return __builtin_amdgcn_raw_buffer_load_b32(rs_cur, (i * SWI + w) * 4, 0, 0);
-    };
     // rows i and j share a parent (depth-1 duplicate): equal producing bucket and a common LDS row
     auto shares_parent = [&](uint32_t i, uint32_t j) -> bool {
         const uint32_t a = psig[i], b = psig[j];
@@ -759,7 +662,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                          (ai >> 16) == (bi & 0xffff) || (ai >> 16) == (bi >> 16);
         if (!hit) return false;
         if constexpr (CPI)
-            return ((a ^ b) & ~C::IMASK) == 0 && ((rows[i * WL + WI - 1] ^ rows[j * WL + WI - 1]) & RMI) == 0;
+            return ((a ^ b) & ~C::IMASK) == 0 && ((rows[i * WI + WI - 1] ^ rows[j * WI + WI - 1]) & RMI) == 0;
         else
             return pdw[i] == pdw[j];
     };
@@ -767,17 +670,15 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // a collision pair (LDS rows i, j) is kept unless the rows are identical or share a parent;
     // dest = its destination bucket
     auto pair_keep = [&](uint32_t i, uint32_t j, uint32_t& dest) -> bool {
-        uint32_t x0 = rows[i * WL] ^ rows[j * WL];
+        uint32_t x0 = rows[i * WI] ^ rows[j * WI];
         if constexpr (WI == 1) x0 &= ~RMI;
         // identical subtrees are dropped; word 0 differs in all but ~2^-21 of the pairs, so the
-        // remaining words are read only when it matches (PL: from global memory)
+        // remaining words are read only when it matches
         bool keep = x0 != 0;
         if (!keep) {
 #pragma unroll
             for (int w = 1; w < WI; ++w) {
-                uint32_t y;
-                if constexpr (PL) y = grow(i, w) ^ grow(j, w);
-                else y = rows[i * WL + w] ^ rows[j * WL + w];
+                uint32_t y = rows[i * WI + w] ^ rows[j * WI + w];
                 if (w == WI - 1) y &= ~RMI;
                 keep |= y != 0;
             }
@@ -798,7 +699,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         return t;
     };
     // (a round that does not prune loads only the row words of each slot)
-    constexpr int LWI = PL ? 1 : PRUNE ? (CPI ? WI + 1 : WI + 2) : (BCP_EH_ROWONLY_LOAD ? WI : SWI);
+    constexpr int LWI = PRUNE ? (CPI ? WI + 1 : WI + 2) : WI;
     uint32_t nr[RPL][LWI];
     uint32_t krank[FOLD ? RPL : 1]; // FOLD: (key << 16) | rank in the key group of each committed row
     int pf_bk = bk;
@@ -809,21 +710,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // operations and wait for the prefetched words with a precise vmcnt(N) instead of vmcnt(0): a
     // vmcnt(0) at the commit would wait for the acks of the previous bucket's emit stores as well.
     auto issue = [&](int u0, int u1) {
-#if BCP_EH_EXP_LOAD == 2
-        // timing experiment: gather the bucket from 512 source runs of 8 rows (as a layout that
-        // writes every producer's output contiguously would have to), wrong results
         const int nonce = pf_bk / C::NB, d = pf_bk % C::NB;
-        const auto rs = buf_rsrc(Rin + (size_t)nonce * C::ROWS * SWI, (uint32_t)(C::ROWS * SWI * 4));
-        const uint32_t ot = opaque_tid();
-#pragma unroll
-        for (int u = 0; u < RPL; ++u) {
-            if (u < u0 || u >= u1) continue;
-            const uint32_t r = ot + u * NT;
-            const uint32_t src = (r >> 3) & (C::NB - 1), pos = ((uint32_t)d * 8 + (r & 7)) % (uint32_t)C::AREA;
-            row_load<LWI>(rs, r < pf_n ? (src * C::AREA + pos) * (SWI * 4) : OOB, nr[u]);
-        }
-#else
-        const int nonce = pf_bk / C::NB, d = BCP_EH_EXP_LOAD ? pf_bk % 8 : pf_bk % C::NB;
         const auto rs = buf_rsrc(Rin + ((size_t)nonce * C::ROWS + (size_t)d * C::AREA) * SWI, CAP * SWI * 4);
         const uint32_t ot = opaque_tid();
 #pragma unroll
@@ -832,11 +719,11 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             const uint32_t r = ot + u * NT;
             row_load<LWI>(rs, r < pf_n ? r * (SWI * 4) : OOB, nr[u]);
         }
-#endif
     };
 
     // prologue: first bucket in flight, fill of the second known
-    uint32_t n = min(CTRin[bk], (uint32_t)CAP);
+    uint32_t fill = CTRin[bk]; // rows offered to the current bucket (more than CAP: the rest were dropped)
+    uint32_t n = min(fill, (uint32_t)CAP);
     pf_n = n;
     issue(0, RPL);
     if constexpr (!FINAL) {
@@ -861,14 +748,13 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
     // waited for the prefetched rows that were issued around it.
     const auto ctr_rs = buf_rsrc(CTRin, (uint32_t)nbk * 4);
     auto fill_of = [&](int b) -> uint32_t {
-        if constexpr (BCP_EH_VMEM_FILL) return __builtin_amdgcn_raw_buffer_load_b32(ctr_rs, b >= 0 ? (uint32_t)b * 4 : OOB, 0, 0);
-        else return b >= 0 ? CTRin[b] : 0u;
+        return __builtin_amdgcn_raw_buffer_load_b32(ctr_rs, b >= 0 ? (uint32_t)b * 4 : OOB, 0, 0);
     };
 
     for (;;) {
         const int nonce = bk / C::NB, d = bk % C::NB;
-        if constexpr (PL) rs_cur = buf_rsrc(Rin + ((size_t)nonce * C::ROWS + (size_t)d * C::AREA) * SWI, CAP * SWI * 4);
         EH_STAMP(0);
+        if (tid == 0 && fill > (uint32_t)CAP) atomicAdd(&pdrop[C::K + STAGE], fill - CAP); // rare
         // A. commit the prefetched bucket (one row per lane per unit)
         {
             const uint32_t ot = opaque_tid();
@@ -876,21 +762,17 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             for (int u = 0; u < RPL; ++u) {
                 const uint32_t r = ot + u * NT;
                 if (r < n) {
-                    if constexpr (PL) {
-                        rows[r] = nr[u][0];
-                    } else if constexpr (!SORTC) {
-                        if constexpr (WL % 2 == 0) {
+                    if constexpr (WI % 2 == 0) {
 #pragma unroll
-                            for (int w = 0; w < WL; w += 2)
-                                *reinterpret_cast<u2v*>(&rows[r * WL + w]) = u2v{nr[u][w], w + 1 < WI ? nr[u][w + 1 < WI ? w + 1 : 0] : 0u};
-                        } else {
+                        for (int w = 0; w < WI; w += 2)
+                            *reinterpret_cast<u2v*>(&rows[r * WI + w]) = u2v{nr[u][w], nr[u][w + 1]};
+                    } else {
 #pragma unroll
-                            for (int w = 0; w < WI; ++w) rows[r * WL + w] = nr[u][w];
-                        }
-                        if constexpr (PRUNE) {
-                            psig[r] = nr[u][WI];
-                            if constexpr (!CPI) pdw[r] = (uint16_t)nr[u][WI + 1];
-                        }
+                        for (int w = 0; w < WI; ++w) rows[r * WI + w] = nr[u][w];
+                    }
+                    if constexpr (PRUNE) {
+                        psig[r] = nr[u][WI];
+                        if constexpr (!CPI) pdw[r] = (uint16_t)nr[u][WI + 1];
                     }
                     if constexpr (FOLD) {
                         const uint32_t key = nr[u][0] >> (32 - C::RB);
@@ -898,18 +780,6 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     }
                 }
             }
-        }
-        if constexpr (BCP_EH_COMMIT_USE) {
-            // The commit consumes the prefetched registers under `r < n`, and a wave whose lanes all
-            // skip a unit branches past that unit's vmcnt wait. The compiler's wait counting then
-            // treats those loads as possibly in flight on the join path, and the next write to
-            // one of those registers (the next issue, or a temporary) waits for them with a count
-            // that also drains this wave's older emit stores. One empty use of every register,
-            // outside the branches, settles the loads here instead, where they have landed anyway.
-#pragma unroll
-            for (int u = 0; u < RPL; ++u)
-#pragma unroll
-                for (int w = 0; w < LWI; ++w) asm volatile("" ::"v"(nr[u][w]));
         }
         if constexpr (!FINAL)
             for (int b = tid; b < C::HW; b += NT) hist_[b] = 0;
@@ -919,27 +789,23 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         EH_STAMP(1);
         const int bn = xcd_bucket<C::NB>(blockIdx.x, it + 1, G, nbk);
         const bool more = bn >= 0; // uniform
-        const uint32_t nn = more ? min((uint32_t)__builtin_amdgcn_readfirstlane(fill_next), (uint32_t)CAP) : 0u;
+        const uint32_t fn = more ? (uint32_t)__builtin_amdgcn_readfirstlane(fill_next) : 0u;
+        const uint32_t nn = min(fn, (uint32_t)CAP);
         pf_bk = more ? bn : bk;
         pf_n = nn;
         const int bn2 = xcd_bucket<C::NB>(blockIdx.x, it + 2, G, nbk);
-#if !BCP_EH_ISSUE_LATE
-        if constexpr (!SORTC) {
-            issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
-            fill_next = fill_of(bn2);
-        }
-#endif
+        issue(0, SLI); // nothing moves when !more (pf_n = 0), but the instruction count stays fixed
+        fill_next = fill_of(bn2);
         __syncthreads();
         EH_STAMP(2);
 
-        // D1. counting sort of the rows by their RB key: sidx = row ids grouped by key,
-        //     bend[key] = end of the key's group
-        auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WL] >> (32 - C::RB); };
-        // FOLD: each lane's committed rows: sorted position (krank, reused) and the number of
-        // later positions in the row's key group (its pairs, capped at 14 as below)
+        // D1. key sort. FOLD: the commit counted the keys; scan to group starts and place each
+        //     row by its rank: sorted position (krank, reused) and the number of later positions
+        //     in the row's key group (its pairs, capped at 14 as below). Final round: count,
+        //     scan, then place (sidx = row ids grouped by key, bend[key] = end of the key's group).
+        auto key_of = [&](uint32_t i) -> uint32_t { return rows[i * WI] >> (32 - C::RB); };
         uint32_t kpairs[FOLD ? RPL : 1];
         if constexpr (FOLD) {
-            // the commit counted the keys: scan to group starts, place each row by its rank
             block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
             const uint32_t ot = opaque_tid();
 #pragma unroll
@@ -953,20 +819,6 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     sidx[pos] = (uint16_t)r;
                     krank[u] = pos;
                     kpairs[u] = min(e - pos - 1, 14u);
-                    if constexpr (SORTC) { // the row goes to its sorted position (its group's rows are adjacent)
-                        if constexpr (WL % 2 == 0) {
-#pragma unroll
-                            for (int w = 0; w < WL; w += 2)
-                                *reinterpret_cast<u2v*>(&rows[pos * WL + w]) = u2v{nr[u][w], w + 1 < WI ? nr[u][w + 1 < WI ? w + 1 : 0] : 0u};
-                        } else {
-#pragma unroll
-                            for (int w = 0; w < WI; ++w) rows[pos * WL + w] = nr[u][w];
-                        }
-                        if constexpr (PRUNE) {
-                            psig[pos] = nr[u][WI];
-                            if constexpr (!CPI) pdw[pos] = (uint16_t)nr[u][WI + 1];
-                        }
-                    }
                 }
             }
         } else {
@@ -975,20 +827,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             block_exscan<NT, (C::NRESTS + NT - 1) / NT>(bend, C::NRESTS, wsum);
             for (uint32_t i = tid; i < n; i += NT) sidx[atomicAdd(&bend[key_of(i)], 1u)] = (uint16_t)i;
         }
-
-#if BCP_EH_ISSUE_LATE
-        // the first vector-memory instructions after the previous bucket's emit: issued once the
-        // key sort (LDS only) has given that emit's stores time to drain, so they do not stall
-        fill_next = fill_of(bn2);
-        issue(0, 2 * SLI);
-#else
-        if constexpr (SORTC) { // the prefetch registers are free only now
-            fill_next = fill_of(bn2);
-            issue(0, 2 * SLI);
-        } else {
-            issue(SLI, 2 * SLI);
-        }
-#endif
+        issue(SLI, 2 * SLI);
         __syncthreads();
         EH_STAMP(3);
 
@@ -1011,58 +850,31 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             }
             issue(2 * SLI, RPL);
         } else {
-#if BCP_EH_PAIRS
             // D2. pair list by per-wave compaction. Sorted position p pairs with every later
             //     position of its key group: c_p = bend[key] - p - 1 pairs (capped at 14; a group
-            //     of 16+ rows is ~1e-8 likely). Each lane counts the pairs of its positions, a DPP
-            //     wave scan gives the lane's offset inside its wave, ONE LDS atomic per wave claims
-            //     the wave's block of the list, and the lane writes its (j << 16 | i) pairs there:
-            //     one barrier. The list holds MP*NT pairs (above the row capacity: capped pair
-            //     lists lost ~9% of the solutions); identical subtrees and pairs that share a
-            //     parent are dropped when the pairs are read back.
-            // (FOLD: a lane takes the pairs of the rows it committed, from registers)
-            uint32_t cpl[MPR];
+            //     of 16+ rows is ~1e-8 likely). Each lane counts the pairs of the rows it
+            //     committed (from registers), a DPP wave scan gives the lane's offset inside its
+            //     wave, ONE LDS atomic per wave claims the wave's block of the list, and the lane
+            //     writes its (j << 16 | i) pairs there: one barrier. The list holds MP*NT pairs
+            //     (above the row capacity: capped pair lists lost ~9% of the solutions); identical
+            //     subtrees and pairs that share a parent are dropped when the pairs are read back.
             uint32_t cnt = 0;
 #pragma unroll
-            for (int u = 0; u < MPR; ++u) {
-                const uint32_t p = tid + u * NT;
-                if constexpr (FOLD) cpl[u] = kpairs[u];
-                else cpl[u] = p < n ? min(bend[key_of(sidx[p])] - p - 1, 14u) : 0u;
-                cnt += cpl[u];
-            }
+            for (int u = 0; u < RPL; ++u) cnt += kpairs[u];
             const uint32_t incl = wave_incl<false>(cnt);
             uint32_t wb = 0;
             if ((tid & 63) == 63) wb = atomicAdd(&npairs, incl);
             uint32_t o = __builtin_amdgcn_readlane(wb, 63) + incl - cnt;
 #pragma unroll
-            for (int u = 0; u < MPR; ++u) {
-                if (!cpl[u]) continue;
-                const uint32_t p = FOLD ? krank[u] : tid + u * NT;
-                const uint32_t i = SORTC ? p : FOLD ? tid + u * NT : sidx[p];
-                for (uint32_t q = p + 1; q <= p + cpl[u]; ++q, ++o) {
+            for (int u = 0; u < RPL; ++u) {
+                if (!kpairs[u]) continue;
+                const uint32_t p = krank[u];
+                const uint32_t i = tid + u * NT;
+                for (uint32_t q = p + 1; q <= p + kpairs[u]; ++q, ++o) {
                     if (o >= (uint32_t)(MP * NT)) continue;
-                    if constexpr (SORTC) { // both rows by sorted position: no LDS read
-                        plist[o] = (q << 16) | p;
-                        continue;
-                    }
-                    if constexpr (FGEN) {
-                        // filtered here, on the lane that lists the pair: a dropped pair leaves
-                        // a NIL hole in the list
-                        const uint32_t j = sidx[q];
-                        uint32_t dest;
-                        const bool keep = pair_keep(i, j, dest);
-                        plist[o] = keep ? (j << 16) | i : NIL;
-                        if (keep) {
-                            pdl[o] = (uint16_t)dest;
-                            hinc(hist_, dest);
-                        }
-                    } else {
-                        plist[o] = ((uint32_t)sidx[q] << 16) | i;
-                    }
+                    plist[o] = ((uint32_t)sidx[q] << 16) | i;
                 }
             }
-            if constexpr (FGEN) // bend's last reads were before the barrier above
-                for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
             __syncthreads();
             EH_STAMP(7); // pair list complete (splits D2 into listing and filtering)
             const uint32_t P = npairs;
@@ -1074,57 +886,20 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                 const uint32_t k = tid + u * NT;
                 pv[u] = NIL;
                 pd[u] = 0;
-                if (FGEN && k < Pc) { // filtered and counted when listed
-                    pv[u] = plist[k];
-                    if (pv[u] != NIL) pd[u] = pdl[k];
-                } else if (!FGEN && k < Pc) {
+                if (k < Pc) {
                     const uint32_t pr = plist[k];
                     const uint32_t i = pr & 0xffff, j = pr >> 16;
-#else
-            // D2. atomic-free pair enumeration. Sorted position p pairs with every later position
-            //     of its group: c_p = bend[key] - p - 1 pairs, first pair index offp[p] (exclusive
-            //     scan). A mark p at each group's first pair index, spread by an inclusive
-            //     max-scan, tells every pair index k its p; q = p + 1 + (k - offp[p]). Pairs live
-            //     in registers (MP per lane: up to MP*NT per bucket, above the row capacity:
-            //     capped pair lists lost ~9% of the solutions); identical subtrees and pairs that
-            //     share a parent are dropped.
-            // c_p is capped at 14 so every prefix fits the u16 offsets (a key group of 16+ rows is
-            // ~1e-8 likely; it only loses a few pairs)
-            for (uint32_t p = tid; p < n; p += NT) offp[p] = (uint16_t)min(bend[key_of(sidx[p])] - p - 1, 14u);
-            for (uint32_t k = tid; k < (uint32_t)(MP * NT); k += NT) pmark[k] = 0;
-            __syncthreads();
-            const uint32_t P = block_exscan<NT, MPR>(offp, (int)n, wsum);
-            const uint32_t Pc = min(P, (uint32_t)(MP * NT));
-            if (tid == 0 && P > (uint32_t)(MP * NT)) atomicAdd(&pdrop[STAGE], P - MP * NT); // rare
-            for (uint32_t p = tid; p < n; p += NT) {
-                const uint32_t o = offp[p], e = (p + 1 < n) ? offp[p + 1] : P;
-                if (e > o && o < Pc) pmark[o] = (uint16_t)p;
-            }
-            __syncthreads();
-            block_maxscan<NT, MP>(pmark, (int)Pc, wsum);
-            uint32_t pv[MP], pd[MP];
-#pragma unroll
-            for (int u = 0; u < MP; ++u) {
-                const uint32_t k = tid + u * NT;
-                pv[u] = NIL;
-                pd[u] = 0;
-                if (k < Pc) {
-                    const uint32_t p = pmark[k], q = p + 1 + (k - offp[p]);
-                    const uint32_t i = sidx[p], j = sidx[q];
-#endif
                     uint32_t dest;
                     if (pair_keep(i, j, dest)) {
                         pv[u] = (j << 16) | i;
                         pd[u] = dest; // destination bucket
-                        if constexpr (BCP_EH_DEST_RANK) pd[u] |= hinc(hist_, pd[u]) << 16; // rank in the destination
-                        else hinc(hist_, pd[u]);
+                        hinc(hist_, pd[u]);
                     }
                 }
             }
-            if constexpr (FOLD && !FGEN) // bend's last reads were before the barrier above; next commit counts here
-                for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
-            if constexpr (!FGEN) // FGEN: the histogram was complete at the list barrier
-                __syncthreads();
+            // bend's last reads were before the barrier above; the next commit counts here
+            for (int k = tid; k < C::NRESTS; k += NT) bend[k] = 0;
+            __syncthreads();
             EH_STAMP(4);
             // D3. claim this bucket's runs in the destination areas (device-scope atomics whose
             //     latency hides behind the scan and the scatter), then sort the pairs by
@@ -1147,10 +922,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                 np = block_exscan<NT, BPT>(hist_, cur_, C::NB, wsum, &start);
 #pragma unroll
             for (int u = 0; u < MP; ++u)
-                if (pv[u] != NIL) {
-                    if constexpr (BCP_EH_DEST_RANK) spair[hget(cur_, pd[u] & 0xffff) + (pd[u] >> 16)] = pv[u];
-                    else spair[hinc(cur_, pd[u])] = pv[u];
-                }
+                if (pv[u] != NIL) spair[hinc(cur_, pd[u])] = pv[u];
 #pragma unroll
             for (int k = 0; k < BPT; ++k) { // LDS slot t of destination b -> run position base[b] + t
                 const int b = tid * BPT + k;
@@ -1166,50 +938,13 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
             constexpr uint32_t OCAP = C::cap(STAGE + 1 <= C::K ? STAGE + 1 : C::K);
             constexpr uint32_t RMO = C::rmask(STAGE);
             const auto rs_out = buf_rsrc(Rout + (size_t)nonce * C::ROWS * SWO, (uint32_t)(C::ROWS * SWO * 4));
-            auto out_t = [&](int u) -> uint32_t {
-#if BCP_EH_EXP_STORE == 5 // experiment: the lanes of a wave take output rows MP*NT/64 apart (scattered stores)
-                const uint32_t t0 = tid + u * NT;
-                return (t0 % (MP * NT / 64)) * 64 + t0 / (MP * NT / 64);
-#else
-                return tid + u * NT;
-#endif
-            };
-            // payload-light: the parents' full rows come from global memory, CH output rows'
-            // worth of loads issued together before their XORs and stores (the stores may alias
-            // the loads as far as the compiler knows, so it would not hoist them itself)
-            constexpr int CH = PL ? (BCP_EH_PL_CH > 0 ? BCP_EH_PL_CH : (WI >= 4 ? 2 : 3)) : 1;
 #pragma unroll
-            for (int u0 = 0; u0 < MP; u0 += CH) {
-            uint32_t pa[CH][PL ? WI : 1], pb[CH][PL ? WI : 1];
-            if constexpr (PL) {
-#pragma unroll
-                for (int c = 0; c < CH; ++c)
-                    if (u0 + c < MP) {
-                        const uint32_t t = out_t(u0 + c);
-                        const uint32_t pr = t < np ? spair[t] : 0u;
-                        const uint32_t si = pr & 0xffff, sj = pr >> 16;
-                        const uint32_t i = SORTC ? (uint32_t)sidx[si] : si, j = SORTC ? (uint32_t)sidx[sj] : sj;
-                        row_load<WI>(rs_cur, t < np ? i * (SWI * 4) : OOB, pa[c]);
-                        row_load<WI>(rs_cur, t < np ? j * (SWI * 4) : OOB, pb[c]);
-                    }
-            }
-#pragma unroll
-            for (int c = 0; c < CH; ++c) { // fixed trip count, unconditional stores (see issue())
-                const int u = u0 + c;
-                if (u >= MP) break;
-                const uint32_t t = out_t(u);
+            for (int u = 0; u < MP; ++u) { // fixed trip count, unconditional stores (see issue())
+                const uint32_t t = tid + u * NT;
                 const uint32_t pr = t < np ? spair[t] : 0u;
-                const uint32_t si = pr & 0xffff, sj = pr >> 16; // LDS rows
-                // the parents' slots in the input area: the LDS rows themselves, or (SORTC) the
-                // slots the key sort moved them from
-                const uint32_t i = SORTC ? (uint32_t)sidx[si] : si, j = SORTC ? (uint32_t)sidx[sj] : sj;
+                const uint32_t i = pr & 0xffff, j = pr >> 16; // LDS rows = the parents' slots in the input area
                 uint32_t x[WI + 1], o[WO];
-                if constexpr (PL) { // both full rows, loaded above
-#pragma unroll
-                    for (int w = 0; w < WI; ++w) x[w] = pa[c][w] ^ pb[c][w];
-                } else {
-                    lds_row_xor<WI, WL>(rows, si, sj, x);
-                }
+                lds_row_xor<WI>(rows, i, j, x);
                 x[WI - 1] &= ~RMI;
                 x[WI] = 0;
                 const uint32_t b = (x[0] >> (32 - C::DB)) & (C::NB - 1);
@@ -1228,18 +963,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     ov[WO] = (j << 16) | i;
                     ov[WO + 1] = d;
                 }
-#if BCP_EH_EXP_STORE == 1 // timing experiment: no emit stores
-                row_store<SWO>(rs_out, OOB, ov);
-#elif BCP_EH_EXP_STORE == 2 // timing experiment: emit rows in LDS order to the producer's own area
-                row_store<SWO>(rs_out, t < OCAP ? (d * C::AREA + t) * (SWO * 4) : OOB, ov);
-#elif BCP_EH_EXP_STORE == 4 // timing experiment: same bytes as dword stores, lane-contiguous
-#pragma unroll
-                for (int w = 0; w < SWO; ++w)
-                    __builtin_amdgcn_raw_buffer_store_b32(ov[w], rs_out, t < OCAP ? ((d * C::AREA + u * NT) * SWO + w * NT + tid) * 4 : OOB, 0, 0);
-#else
                 row_store<SWO>(rs_out, ok ? slot * (SWO * 4) : OOB, ov);
-#endif
-            }
             }
         }
         __syncthreads();
@@ -1247,6 +971,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
         if (!more) break;
         bk = bn;
         ++it;
+        fill = fn;
         n = nn;
     }
 }
@@ -1391,14 +1116,8 @@ struct EquihashGpuSolver::Impl {
     unsigned n, k;
     int batch, device;
     hipStream_t stream = nullptr;
-    hipStream_t gstream = nullptr;                // BCP_EH_PRIO: generation's own low-priority stream
-    hipEvent_t ev0 = nullptr, ev1 = nullptr, evs = nullptr, evg = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
     hipEvent_t ev_gen = nullptr, ev_rounds = nullptr; // this solver's last generation / rounds done (pipelining)
-    hipEvent_t ev_mid = nullptr; // this solver's round `pipe_round` done: the next batch's generation may start
-    // Pipelined launches: the next batch's generation waits for this batch's round pipe_round
-    // (BCP_EH_PIPE_ROUND, default 0 = only for this batch's generation). Rounds whose LDS leaves
-    // no room for a generation workgroup beside them (rounds 1-2 of (200,9)) are then not shared.
-    int pipe_round = 0;
     const Impl* after = nullptr;                        // Launch(states, prev): the batch to pipeline behind
     DevBuf<bcpk::EhBaseState> d_states;
     DevBuf<uint32_t> d_ctr, d_leaf, d_ncand, d_idx, d_valid, d_pdrop, d_nout, d_out;
@@ -1411,10 +1130,9 @@ struct EquihashGpuSolver::Impl {
     std::vector<size_t> caps; // caps[s]: LDS capacity of the round that reads stage-s rows
     std::vector<size_t> slot_words, row_words; // per stage
     uint32_t cp_ib = 0, cp_dh = 0, cp_dhm = 0, cp_dx = 0, cp_rmask = 0, cp_imask = 0; // compact parent layout
-    std::vector<bool> compact;                  // per stage: compact parent word                 // > 0: stage-0 slots carry the leaf index last
+    std::vector<bool> compact;                  // per stage: compact parent word
     int inflight = 0;
     int ncu = 1;
-    int ncu_round = 1; // CUs the round kernels' stream may use (BCP_EH_GEN_CUS splits the device)
     bool debug = false, stamp_mode = false;
     DevBuf<uint64_t> d_stamps;
     EhGpuStats stats;
@@ -1444,8 +1162,8 @@ struct EquihashGpuSolver::Impl {
         d_leaf.alloc((size_t)batch * C::ROWS);
         cp_ib = C::IB, cp_dh = C::DH, cp_dhm = C::DHM, cp_dx = C::DX, cp_rmask = C::RMASK, cp_imask = C::IMASK;
         d_ncand.alloc(batch);
-        d_pdrop.alloc(C::K + 1);
-        h_pdrop.alloc(C::K + 1);
+        d_pdrop.alloc(2 * C::K + 2); // [1..K]: pair-list drops per round, [K+1..2K]: row drops per stage
+        h_pdrop.alloc(2 * C::K + 2);
         d_cand.alloc((size_t)batch * C::MAXCAND);
         d_idx.alloc((size_t)batch * C::MAXCAND * C::L);
         d_valid.alloc((size_t)batch * C::MAXCAND);
@@ -1471,7 +1189,7 @@ struct EquihashGpuSolver::Impl {
             BCP_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, bcpk::eh_round<C, S, ST>, C::NT, 0));
             per_cu = std::max(occ, 1);
         }
-        return std::min(nbk, ncu_round * per_cu);
+        return std::min(nbk, ncu * per_cu);
     }
     template <class C, int S> void launch_round(int nstates) {
         const uint32_t* rin = d_rst[S - 1].p;
@@ -1488,12 +1206,8 @@ struct EquihashGpuSolver::Impl {
                                stream, rin, cin, rout, cout, d_ncand.p, d_cand.p, nullptr, d_pdrop.p, nbk);
         }
     }
-    template <class C, int S> void launch_round_mark(int nstates) {
-        launch_round<C, S>(nstates);
-        if (S == pipe_round || (S == C::K && pipe_round > C::K)) BCP_HIP_CHECK(hipEventRecord(ev_mid, stream));
-    }
     template <class C, int... S> void launch_rounds(int nstates, std::integer_sequence<int, S...>) {
-        (launch_round_mark<C, S + 1>(nstates), ...);
+        (launch_round<C, S + 1>(nstates), ...);
     }
 
     template <class C> void launch(size_t nstates) {
@@ -1501,7 +1215,7 @@ struct EquihashGpuSolver::Impl {
                                      hipMemcpyHostToDevice, stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ncand.p, 0, batch * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_nout.p, 0, sizeof(uint32_t), stream));
-        BCP_HIP_CHECK(hipMemsetAsync(d_pdrop.p, 0, (C::K + 1) * sizeof(uint32_t), stream));
+        BCP_HIP_CHECK(hipMemsetAsync(d_pdrop.p, 0, d_pdrop.n * sizeof(uint32_t), stream));
         BCP_HIP_CHECK(hipMemsetAsync(d_ctr.p, 0, d_ctr.n * sizeof(uint32_t), stream));
         if (debug) {
             if (d_leaf.n) BCP_HIP_CHECK(hipMemsetAsync(d_leaf.p, 0xff, d_leaf.n * sizeof(uint32_t), stream));
@@ -1519,18 +1233,12 @@ struct EquihashGpuSolver::Impl {
         }
         uint32_t* r0 = d_rst[0].p;
         hipStream_t gs = stream;
-        if (gstream) { // generation on its own stream, the rounds wait for it
-            BCP_HIP_CHECK(hipEventRecord(evs, stream));
-            BCP_HIP_CHECK(hipStreamWaitEvent(gstream, evs, 0));
-            gs = gstream;
-        }
         if (after) BCP_HIP_CHECK(hipStreamWaitEvent(gs, after->ev_gen, 0)); // one generation at a time
-        if (after && after->pipe_round > 0) BCP_HIP_CHECK(hipStreamWaitEvent(gs, after->ev_mid, 0));
         constexpr bool reg = bcpk::GenReg<C, C::GNT, C::GHPT>::OK;
         if constexpr (reg) {
             using GR = bcpk::GenReg<C, C::GNT, C::GHPT>;
             const int items = GR::GWG * (int)nstates;
-            const int grid = BCP_EH_GEN_PERSIST > 0 ? std::min(items, ncu * BCP_EH_GEN_PERSIST) : items;
+            const int grid = items;
             if (hdr)
                 hipLaunchKernelGGL((bcpk::eh_gen_reg<C, true, C::GNT, C::GHPT>), dim3(grid), dim3(C::GNT), 0, gs,
                                    d_states.p, r0, d_leaf.p, d_ctr.p, items);
@@ -1544,7 +1252,6 @@ struct EquihashGpuSolver::Impl {
             hipLaunchKernelGGL((bcpk::eh_gen<C, false>), dim3(C::GENWG * nstates), dim3(C::NTG), 0, gs,
                                d_states.p, r0, d_leaf.p, d_ctr.p);
         BCP_HIP_CHECK(hipEventRecord(ev_gen, gs));
-        if (gstream) BCP_HIP_CHECK(hipStreamWaitEvent(stream, ev_gen, 0));
         if (after) BCP_HIP_CHECK(hipStreamWaitEvent(stream, after->ev_rounds, 0)); // one round chain at a time
         launch_rounds<C>((int)nstates, std::make_integer_sequence<int, C::K>{});
         constexpr int EB = C::L < 64 ? 64 : C::L;
@@ -1557,12 +1264,12 @@ struct EquihashGpuSolver::Impl {
         BCP_HIP_CHECK(hipEventRecord(ev1, stream));
         BCP_HIP_CHECK(
             hipMemcpyAsync(h_ncand.p, d_ncand.p, nstates * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-        if (debug) { // per-stage fills of nonce 0's buckets, and pair-list overflow
+        // pair-list and row drops of every nonce (a few words)
+        BCP_HIP_CHECK(hipMemcpyAsync(h_pdrop.p, d_pdrop.p, d_pdrop.n * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
+        if (debug) { // per-stage fills of nonce 0's buckets
             for (int s = 0; s < C::K; ++s)
                 BCP_HIP_CHECK(hipMemcpyAsync(h_ctr0.p + (size_t)s * C::NB, d_ctr.p + (size_t)s * batch * C::NB,
                                              C::NB * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
-            BCP_HIP_CHECK(hipMemcpyAsync(h_pdrop.p, d_pdrop.p, (C::K + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                         stream));
             BCP_HIP_CHECK(hipMemcpyAsync(h_ctr_all.p, d_ctr.p, d_ctr.n * sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
         }
         BCP_HIP_CHECK(hipMemcpyAsync(h_nout.p, d_nout.p, sizeof(uint32_t), hipMemcpyDeviceToHost, stream));
@@ -1588,35 +1295,9 @@ EquihashGpuSolver::EquihashGpuSolver(unsigned n, unsigned k, int batch, int devi
     impl->batch = batch;
     impl->device = UseDevice(device);
     BCP_HIP_CHECK(hipDeviceGetAttribute(&impl->ncu, hipDeviceAttributeMultiprocessorCount, impl->device));
-    impl->ncu_round = impl->ncu;
-    // BCP_EH_GEN_CUS=G (a multiple of 8, below the CU count): generation gets a stream of its own
-    // restricted to G CUs and the rounds one restricted to the others, so a pipelined batch's
-    // generation runs on its CUs while the previous batch's rounds hold the rest. CU-mask bit i
-    // lands on XCD i % 8, so the low G bits give every XCD G / 8 generation CUs.
-    const char* gcus = getenv("BCP_EH_GEN_CUS");
-    const int G = gcus ? atoi(gcus) : 0;
-    if (G > 0 && G % 8 == 0 && G < impl->ncu) {
-        std::vector<uint32_t> rmask((impl->ncu + 31) / 32, 0u), gmask((impl->ncu + 31) / 32, 0u);
-        for (int i = 0; i < impl->ncu; ++i) (i < G ? gmask : rmask)[i / 32] |= 1u << (i % 32);
-        BCP_HIP_CHECK(hipExtStreamCreateWithCUMask(&impl->stream, (uint32_t)rmask.size(), rmask.data()));
-        BCP_HIP_CHECK(hipExtStreamCreateWithCUMask(&impl->gstream, (uint32_t)gmask.size(), gmask.data()));
-        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evs, hipEventDisableTiming));
-        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evg, hipEventDisableTiming));
-        impl->ncu_round = impl->ncu - G;
-    } else if (BCP_EH_PRIO) {
-        int least = 0, greatest = 0;
-        BCP_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-        BCP_HIP_CHECK(hipStreamCreateWithPriority(&impl->stream, hipStreamNonBlocking, greatest));
-        BCP_HIP_CHECK(hipStreamCreateWithPriority(&impl->gstream, hipStreamNonBlocking, least));
-        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evs, hipEventDisableTiming));
-        BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->evg, hipEventDisableTiming));
-    } else {
-        BCP_HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
-    }
+    BCP_HIP_CHECK(hipStreamCreateWithFlags(&impl->stream, hipStreamNonBlocking));
     BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_gen, hipEventDisableTiming));
     BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_rounds, hipEventDisableTiming));
-    BCP_HIP_CHECK(hipEventCreateWithFlags(&impl->ev_mid, hipEventDisableTiming));
-    if (const char* pr = getenv("BCP_EH_PIPE_ROUND")) impl->pipe_round = std::max(0, atoi(pr));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev0));
     BCP_HIP_CHECK(hipEventCreate(&impl->ev1));
     dispatch_cfg(n, k, [&](auto c) { impl->alloc<decltype(c)>(); });
@@ -1629,12 +1310,8 @@ EquihashGpuSolver::~EquihashGpuSolver() {
         if (impl->ev0) (void)hipEventDestroy(impl->ev0);
         if (impl->ev1) (void)hipEventDestroy(impl->ev1);
         if (impl->stream) (void)hipStreamDestroy(impl->stream);
-        if (impl->gstream) (void)hipStreamSynchronize(impl->gstream), (void)hipStreamDestroy(impl->gstream);
-        if (impl->evs) (void)hipEventDestroy(impl->evs);
         if (impl->ev_gen) (void)hipEventDestroy(impl->ev_gen);
         if (impl->ev_rounds) (void)hipEventDestroy(impl->ev_rounds);
-        if (impl->ev_mid) (void)hipEventDestroy(impl->ev_mid);
-        if (impl->evg) (void)hipEventDestroy(impl->evg);
     }
 }
 
@@ -1787,6 +1464,14 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
     BCP_HIP_CHECK(hipEventElapsedTime(&ms, impl->ev0, impl->ev1));
     impl->stats.gpu_ms += ms;
     impl->stats.nonces += ns;
+    {
+        // every nonce: pair-list drops per round and rows past a round's capacity per stage (accumulated)
+        const size_t K = impl->kstages;
+        impl->stats.pair_dropped_all.resize(K + 1, 0);
+        impl->stats.stage_dropped_all.resize(K, 0);
+        for (size_t r = 0; r <= K; ++r) impl->stats.pair_dropped_all[r] += impl->h_pdrop.p[r];
+        for (size_t s = 0; s < K; ++s) impl->stats.stage_dropped_all[s] += impl->h_pdrop.p[K + 1 + s];
+    }
     if (impl->debug) {
         // nonce 0: per stage, rows offered to each bucket (its fill counter) vs the LDS capacity
         // of the round that reads it
@@ -1796,18 +1481,13 @@ std::vector<std::vector<std::vector<uint32_t>>> EquihashGpuSolver::Collect() {
         impl->stats.stage_maxfill.assign(impl->kstages, 0);
         impl->stats.stage_top.assign(impl->kstages, {});
         impl->stats.pair_dropped.assign(impl->h_pdrop.p, impl->h_pdrop.p + impl->kstages + 1);
-        // every nonce of the batch: rows past a round's capacity, per stage (accumulated) and the
-        // fullest bucket of the batch
-        impl->stats.stage_dropped_all.resize(impl->kstages, 0);
+        // every nonce of the batch: the fullest bucket per stage and the buckets past capacity
         impl->stats.stage_maxfill_all.assign(impl->kstages, 0);
         for (size_t s = 0; s < impl->kstages; ++s)
             for (size_t x = 0; x < (size_t)ns * NB; ++x) {
                 const uint64_t fill = impl->h_ctr_all.p[(s * impl->batch) * NB + x];
                 impl->stats.stage_maxfill_all[s] = std::max<uint64_t>(impl->stats.stage_maxfill_all[s], fill);
-                if (fill > impl->caps[s]) {
-                    impl->stats.stage_dropped_all[s] += fill - impl->caps[s];
-                    impl->stats.overflow_fills.push_back((uint64_t)s << 32 | fill);
-                }
+                if (fill > impl->caps[s]) impl->stats.overflow_fills.push_back((uint64_t)s << 32 | fill);
             }
         for (size_t s = 0; s < impl->kstages; ++s) {
             std::vector<uint64_t> fills;

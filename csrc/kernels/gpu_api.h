@@ -47,9 +47,11 @@ struct EhGpuStats {
     std::vector<uint64_t> stage_rows, stage_dropped, stage_maxfill; // debug mode, last batch
     std::vector<std::vector<uint64_t>> stage_top;
     std::vector<uint64_t> pair_dropped;
-    std::vector<uint64_t> stage_dropped_all, stage_maxfill_all;     // debug: every nonce (dropped: accumulated)
+    std::vector<uint64_t> stage_dropped_all;  // every nonce: rows past a round's capacity per stage (accumulated)
+    std::vector<uint64_t> pair_dropped_all;   // every nonce: pairs past a round's pair list, per round (accumulated)
+    std::vector<uint64_t> stage_maxfill_all;  // debug: fullest bucket per stage, last batch
     std::vector<uint64_t> overflow_fills; // debug: (stage << 32 | fill) of every bucket past its capacity (accumulated)
-    std::vector<std::vector<uint32_t>> debug_cands;                  // debug: every candidate of nonce 0 (valid or not)                              // debug: pair-list overflow per round (batch total)                    // debug: 8 fullest buckets per stage
+    std::vector<std::vector<uint32_t>> debug_cands;                  // debug: every candidate of nonce 0 (valid or not)
 };
 
 // Batched Equihash solver: one launch sequence solves `batch` nonces at once

@@ -103,6 +103,7 @@ void bind_gpu(pyb::module_& m) {
                  d["stage_top"] = st.stage_top;
                  d["pair_dropped"] = st.pair_dropped;
                  d["stage_dropped_all"] = st.stage_dropped_all;
+                 d["pair_dropped_all"] = st.pair_dropped_all;
                  d["stage_maxfill_all"] = st.stage_maxfill_all;
                  d["overflow_fills"] = st.overflow_fills;
                  d["debug_cands"] = st.debug_cands;
