@@ -5,6 +5,7 @@
 #include "consensus/merkle.h"
 #include "consensus/pow.h"
 #include "keys/key.h"
+#include "net/net.h"
 #include "node/miner.h"
 #include "node/node.h"
 #include "node/signals.h"
@@ -135,23 +136,39 @@ static UniValue BIP22ValidationResult(const CValidationState& state) {
     return "valid?";
 }
 
+// BIP9 deployment name as getblocktemplate shows it: '!' marks a rule the client must
+// understand (reference src/rpc/mining.cpp:419-426 gbt_vb_name)
+static std::string gbt_vb_name(Consensus::DeploymentPos pos) {
+    const VBDeploymentInfo& vbinfo = VersionBitsDeploymentInfo[pos];
+    std::string s = vbinfo.name;
+    if (!vbinfo.gbt_force) s.insert(s.begin(), '!');
+    return s;
+}
+
+// Parity: reference src/rpc/mining.cpp:428-897 (BIP22/BIP23/BIP9 getblocktemplate), including
+// the proposal_legacy mode (an 80-byte-header block), the next-height check of proposals,
+// maxversion -> version/force for pre-versionbits clients, and the refusals of a node without
+// peers (-9) or in initial block download (-10, regtest included).
 static UniValue getblocktemplate(const JSONRPCRequest& req) {
     NodeContext& n = Node();
     Chainstate& cs = *n.chainstate;
     std::string strMode = "template";
     UniValue lpval = UniValue::NullUniValue;
     std::set<std::string> setClientRules;
+    int64_t nMaxVersionPreVB = -1;
     if (req.params.size() > 0 && !req.params[0].isNull()) {
         const UniValue& oparam = req.params[0].get_obj();
         const UniValue& modeval = oparam["mode"];
         if (modeval.isStr()) strMode = modeval.get_str();
         else if (!modeval.isNull()) ThrowRPC(RPC_INVALID_PARAMETER, "Invalid mode");
         lpval = oparam["longpollid"];
-        if (strMode == "proposal") {
+        if (strMode == "proposal" || strMode == "proposal_legacy") {
             const UniValue& dataval = oparam["data"];
             if (!dataval.isStr()) ThrowRPC(RPC_TYPE_ERROR, "Missing data String key for proposal");
             CBlock block;
-            if (!DecodeHexBlk(block, dataval.get_str())) ThrowRPC(RPC_DESERIALIZATION_ERROR, "Block decode failed");
+            const bool legacy_format = strMode == "proposal_legacy";
+            if (!DecodeHexBlk(block, dataval.get_str(), legacy_format))
+                ThrowRPC(RPC_DESERIALIZATION_ERROR, "Block decode failed");
             std::lock_guard<CCriticalSection> l(cs.cs());
             const uint256 hash = block.GetHash(cs.Params().GetConsensus());
             CBlockIndex* pindex = cs.LookupBlockIndex(hash);
@@ -160,18 +177,30 @@ static UniValue getblocktemplate(const JSONRPCRequest& req) {
                 if (pindex->nStatus & BLOCK_FAILED_MASK) return "duplicate-invalid";
                 return "duplicate-inconclusive";
             }
-            if (block.hashPrevBlock != cs.Tip()->GetBlockHash()) return "inconclusive-not-best-prevblk";
+            CBlockIndex* const pindexPrev = cs.Tip();
+            // TestBlockValidity only supports blocks built on the current tip
+            if (block.hashPrevBlock != pindexPrev->GetBlockHash()) return "inconclusive-not-best-prevblk";
+            // the header's height must be the next one (a legacy-format block carries none, so
+            // proposal_legacy always ends here, as in the reference)
+            if (block.nHeight != (uint32_t)pindexPrev->nHeight + 1) return "inconclusive-bad-height";
             CValidationState state;
-            cs.TestBlockValidity(state, block, cs.Tip(), false, true);
+            cs.TestBlockValidity(state, block, pindexPrev, false, true);
             return BIP22ValidationResult(state);
         }
         const UniValue& aClientRules = oparam["rules"];
-        if (aClientRules.isArray())
+        if (aClientRules.isArray()) {
             for (size_t i = 0; i < aClientRules.size(); ++i) setClientRules.insert(aClientRules[i].get_str());
+        } else {
+            // read only from clients that do not speak versionbits
+            const UniValue& uvMaxVersion = oparam["maxversion"];
+            if (uvMaxVersion.isNum()) nMaxVersionPreVB = uvMaxVersion.get_int64();
+        }
     }
     if (strMode != "template") ThrowRPC(RPC_INVALID_PARAMETER, "Invalid mode");
-    if (cs.IsInitialBlockDownload() && !cs.Params().MineBlocksOnDemand())
-        ThrowRPC(RPC_CLIENT_IN_INITIAL_DOWNLOAD, "Bitcoin is downloading blocks...");
+    CConnman* connman = GetConnman();
+    if (!connman) ThrowRPC(RPC_CLIENT_P2P_DISABLED, "Error: Peer-to-peer functionality missing or disabled");
+    if (connman->GetNodeCount(CONNECTIONS_ALL) == 0) ThrowRPC(RPC_CLIENT_NOT_CONNECTED, "Bitcoin is not connected!");
+    if (cs.IsInitialBlockDownload()) ThrowRPC(RPC_CLIENT_IN_INITIAL_DOWNLOAD, "Bitcoin is downloading blocks...");
 
     static unsigned nTransactionsUpdatedLast;
     if (!lpval.isNull()) {
@@ -263,17 +292,26 @@ static UniValue getblocktemplate(const JSONRPCRequest& req) {
             pblock->nVersion |= VersionBitsMask(cs.Params().GetConsensus(), pos);
             // fallthrough
         case THRESHOLD_STARTED:
-            vbavailable.pushKV(vbinfo.name, cs.Params().GetConsensus().vDeployments[pos].bit);
+            vbavailable.pushKV(gbt_vb_name(pos), cs.Params().GetConsensus().vDeployments[pos].bit);
             if (setClientRules.find(vbinfo.name) == setClientRules.end() && !vbinfo.gbt_force)
                 pblock->nVersion &= ~VersionBitsMask(cs.Params().GetConsensus(), pos);
             break;
-        case THRESHOLD_ACTIVE: aRules.push_back(vbinfo.name); break;
+        case THRESHOLD_ACTIVE:
+            aRules.push_back(gbt_vb_name(pos));
+            // an active rule the client does not know: only safe when it is gbt_force
+            if (setClientRules.find(vbinfo.name) == setClientRules.end() && !vbinfo.gbt_force)
+                ThrowRPC(RPC_INVALID_PARAMETER,
+                         strprintf("Support for '%s' rule requires explicit client support", vbinfo.name));
+            break;
         }
     }
     result.pushKV("version", pblock->nVersion);
     result.pushKV("rules", aRules);
     result.pushKV("vbavailable", vbavailable);
     result.pushKV("vbrequired", 0);
+    // a pre-versionbits client (maxversion, no rules) may change the version back to v2: safe
+    // only because a non-force active deployment threw above (BIP34 fixed the coinbase layout)
+    if (nMaxVersionPreVB >= 2) aMutable.push_back("version/force");
     result.pushKV("previousblockhash", pblock->hashPrevBlock.GetHex());
     result.pushKV("transactions", transactions);
     result.pushKV("coinbaseaux", aux);
@@ -283,8 +321,9 @@ static UniValue getblocktemplate(const JSONRPCRequest& req) {
     result.pushKV("mintime", (int64_t)pindexPrev->GetMedianTimePast() + 1);
     result.pushKV("mutable", aMutable);
     result.pushKV("noncerange", "00000000ffffffff");
-    result.pushKV("sigoplimit", (int64_t)GetMaxBlockSigOpsCount(cs.MaxBlockSize()));
-    result.pushKV("sizelimit", (int64_t)cs.MaxBlockSize());
+    // the reference reports the default 8 MB limits here, whatever -excessiveblocksize is
+    result.pushKV("sigoplimit", (int64_t)GetMaxBlockSigOpsCount(DEFAULT_MAX_BLOCK_SIZE));
+    result.pushKV("sizelimit", (int64_t)DEFAULT_MAX_BLOCK_SIZE);
     result.pushKV("curtime", pblock->GetBlockTime());
     result.pushKV("bits", strprintf("%08x", pblock->nBits));
     result.pushKV("height", (int64_t)(pindexPrev->nHeight + 1));

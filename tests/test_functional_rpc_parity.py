@@ -267,7 +267,10 @@ def test_prioritisetransaction(tmp_path):
         # deltas accumulate
         a.rpc.prioritisetransaction(high, 0, 5 * 10**7)
         assert D(a.rpc.getmempoolentry(high)["modifiedfee"]) == base[high] + D("1.5")
+        from bitcoincashplus_amd.testing.p2p import P2PPeer
+        peer = P2PPeer().connect("127.0.0.1", a.p2p_port)  # templates need a connected node
         tmpl = a.rpc.getblocktemplate()
+        peer.close()
         picked = [t["txid"] for t in tmpl["transactions"]]
         assert high in picked and low not in picked
         assert picked[0] == high  # highest modified fee rate first

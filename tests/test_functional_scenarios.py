@@ -19,6 +19,7 @@ import pytest
 from bitcoincashplus_amd.node.process import BIN_DIR, BcpdProcess
 from bitcoincashplus_amd.testing.blocktools import create_block, create_coinbase
 from bitcoincashplus_amd.testing.messages import CTransaction, from_hex
+from bitcoincashplus_amd.testing.p2p import P2PPeer
 
 pytestmark = pytest.mark.functional
 
@@ -135,8 +136,11 @@ def test_mempool_reorg_returns_transactions(tmp_path):
 
 def test_getblocktemplate_longpoll_and_proposals(tmp_path):
     n = start(tmp_path, "g")
+    peer = None
     try:
         n.rpc.generate(105)
+        # templates are refused to a node without peers (-9): a P2P peer keeps one connection up
+        peer = P2PPeer().connect("127.0.0.1", n.p2p_port)
         tmpl = n.rpc.getblocktemplate()
         lp = tmpl["longpollid"]
         result = {}
@@ -177,6 +181,8 @@ def test_getblocktemplate_longpoll_and_proposals(tmp_path):
         assert n.rpc.getblocktemplate({"mode": "proposal", "data": stale.serialize().hex()}) == \
             "inconclusive-not-best-prevblk"
     finally:
+        if peer:
+            peer.close()
         n.stop()
 
 
