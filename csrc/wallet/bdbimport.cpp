@@ -1,4 +1,5 @@
 #include "wallet/bdbimport.h"
+#include "util/lockedpool.h"
 
 #include <cstdint>
 #include <cstring>
@@ -26,6 +27,7 @@ uint32_t U32(const unsigned char* p) { return (uint32_t)p[0] | ((uint32_t)p[1] <
 class BtreeFile {
 public:
     explicit BtreeFile(std::string bytes) : f(std::move(bytes)) {}
+    ~BtreeFile() { memory_cleanse(&f[0], f.size()); } // the file holds plaintext key records
 
     bool Open(std::string& err) {
         if (f.size() < 512) return Fail(err, "file too short for a database");
@@ -241,6 +243,7 @@ bool ReadBdbDump(std::istream& in, BdbRecords& out, std::string& err) {
 #include "util/util.h"
 
 #include <cstdio>
+#include <filesystem>
 
 namespace bcp {
 
@@ -309,19 +312,42 @@ bool ImportBdbWalletFile(const std::string& path, size_t& imported, std::string&
         err = path + " is not a Berkeley DB wallet";
         return false;
     }
+    // Build the converted store beside the original and only then swap: a failed write, or a
+    // process that dies before the renames, leaves wallet.dat untouched (and the next start
+    // imports it again) instead of an empty native store at the wallet path.
+    const std::string tmp = path + ".import.tmp";
+    std::error_code ec;
+    std::filesystem::remove_all(tmp, ec);
+    bool written = false;
+    {
+        KVStore fresh(tmp, false, true);
+        KVBatch b;
+        for (auto& kv : recs) {
+            ConvertRecord(kv.first, kv.second);
+            b.WriteRaw(kv.first, kv.second);
+        }
+        written = fresh.WriteBatch(b, true);
+    }
+    // the records (plaintext key material among them) are not needed past the batch
+    for (auto& kv : recs) {
+        memory_cleanse(&kv.second[0], kv.second.size());
+        memory_cleanse(&kv.first[0], kv.first.size());
+    }
+    if (!written) {
+        std::filesystem::remove_all(tmp, ec);
+        err = "writing the imported wallet failed";
+        return false;
+    }
     const std::string bak = strprintf("%s.bdb.%lld", path.c_str(), (long long)GetTime());
     if (rename(path.c_str(), bak.c_str()) != 0) {
+        std::filesystem::remove_all(tmp, ec);
         err = "cannot move " + path + " aside to " + bak;
         return false;
     }
-    KVStore fresh(path, false, true);
-    KVBatch b;
-    for (auto& kv : recs) {
-        ConvertRecord(kv.first, kv.second);
-        b.WriteRaw(kv.first, kv.second);
-    }
-    if (!fresh.WriteBatch(b, true)) {
-        err = "writing the imported wallet failed";
+    if (rename(tmp.c_str(), path.c_str()) != 0) {
+        rename(bak.c_str(), path.c_str()); // put the original back
+        std::filesystem::remove_all(tmp, ec);
+        err = "cannot move the imported wallet into place at " + path;
         return false;
     }
     imported = recs.size();
