@@ -1,9 +1,15 @@
-"""Headers announcements after reorgs, direct fetch, and unconnecting headers.
+"""Headers announcements (before and after sendheaders, after reorgs), direct fetch, and
+unconnecting headers.
 
-Parity: reference test/functional/sendheaders.py Parts 3-5 (Parts 1-2 are in
-tests/test_p2p_compactblocks.py::test_sendheaders_announcements), driven as there by an
+Parity: reference test/functional/sendheaders.py Parts 1-5, driven as there by an
 "inv node" (never sends sendheaders) and a "test node" (sendheaders, nServices 0 so the node
 fetches blocks from it only by direct fetch):
+* Part 1 (:300-334): before sendheaders every block is announced by inv, whatever the peer
+  requests meanwhile (getdata, getheaders + getdata, its own header announcement);
+* Part 2 (:336-402): after sendheaders and a getheaders from the tip, new blocks are announced by
+  header, also after the peer mined 1..10 blocks of its own and announced them by inv (the node
+  answers with getheaders, then getdata) or by headers (getdata); duplicate inv / headers
+  announcements from the inv node bring no second getdata;
 * Part 3 (:405-476): a reorg of up to 8 new blocks is announced to the test node by headers,
   a longer one by a single inv; headers announcements then stay off through getblocks,
   getdata and a getheaders whose best header is too old, and resume after a getheaders from
@@ -178,20 +184,80 @@ def new_blocks(tip, height, block_time, count):
     return out
 
 
-def test_sendheaders_parts_3_to_5(net):
+def test_sendheaders_parts_1_to_5(net):
     a, b, inv_node, test_node = net
     peers = [inv_node, test_node]
     a.rpc.generate(101)  # out of initial block download
     sync(a, b)
-    # Parts 1-2 preconditions: the test node announced sendheaders and the node knows its
-    # best header; from here on the test node gets headers announcements
     tip = int(a.rpc.getbestblockhash(), 16)
-    test_node.send(msg_getheaders([tip], 0))
+
+    # ---- Part 1: no headers announcements before sendheaders, whatever the peer requests
+    for i in range(4):
+        old_tip = tip
+        tip = mine_blocks(a, peers, 1)
+        assert inv_node.check_last_announcement(inv=[tip])
+        assert test_node.check_last_announcement(inv=[tip])
+        if i == 0:  # request the block
+            test_node.get_data([tip])
+            test_node.wait_for_block(tip)
+        elif i == 1:  # request header and block
+            test_node.send(msg_getheaders([old_tip], tip))
+            test_node.get_data([tip])
+            test_node.wait_for_block(tip)
+            test_node.reset_announcement()  # (the headers reply)
+        elif i == 2:  # announce a block of our own by header
+            height = a.rpc.getblockcount()
+            block_time = a.rpc.getblock(a.rpc.getbestblockhash())["time"] + 1
+            nb = new_blocks(tip, height + 1, block_time, 1)[0]
+            test_node.send_header_for_blocks([nb])
+            test_node.wait_for_getdata([nb.sha256], DIRECT_FETCH_TIMEOUT)
+            test_node.send(msg_block(nb))
+            test_node.sync_with_ping()
+            inv_node.reset_announcement()
+            test_node.reset_announcement()
+    sync(a, b)
+
+    # ---- Part 2: after sendheaders (and a getheaders from the tip), announcements are headers
     test_node.send(msg_sendheaders())
+    test_node.send(msg_getheaders([int(a.rpc.getbestblockhash(), 16)], 0))
     test_node.sync_with_ping()
     tip = mine_blocks(a, peers, 1)
     assert inv_node.check_last_announcement(inv=[tip])
     assert test_node.check_last_announcement(headers=[tip])
+    height = a.rpc.getblockcount() + 1
+    block_time = a.rpc.getblock(a.rpc.getbestblockhash())["time"] + 10
+    for i in range(10):
+        # the peer mines i + 1 blocks and announces them by inv of the tip or by headers;
+        # the node's next block is still announced to it by header
+        for j in range(2):
+            blocks = new_blocks(tip, height, block_time, i + 1)
+            tip, height, block_time = blocks[-1].sha256, height + i + 1, block_time + i + 1
+            if j == 0:
+                test_node.last_getheaders = None
+                test_node.send(msg_inv([CInv(MSG_BLOCK, tip)]))
+                test_node.wait_for_getheaders(DIRECT_FETCH_TIMEOUT)
+                test_node.send_header_for_blocks(blocks)
+                for x in blocks:  # duplicate invs bring no duplicate getdata or announcements
+                    inv_node.send(msg_inv([CInv(MSG_BLOCK, x.sha256)]))
+                test_node.wait_for_getdata([x.sha256 for x in blocks], DIRECT_FETCH_TIMEOUT)
+                inv_node.sync_with_ping()
+            else:
+                test_node.send_header_for_blocks(blocks)
+                test_node.wait_for_getdata([x.sha256 for x in blocks], DIRECT_FETCH_TIMEOUT)
+                inv_node.send_header_for_blocks(blocks)  # duplicate headers: no second getdata
+                inv_node.sync_with_ping()
+            for x in blocks:
+                test_node.send(msg_block(x))
+            test_node.sync_with_ping()
+            inv_node.sync_with_ping()
+            # not announced to the inv node, which announced them itself
+            assert inv_node.last_inv is None and inv_node.last_headers is None
+            tip = mine_blocks(a, peers, 1)
+            assert inv_node.check_last_announcement(inv=[tip])
+            assert test_node.check_last_announcement(headers=[tip])
+            height += 1
+            block_time += 1
+    sync(a, b)
 
     # ---- Part 3: headers announcements stop after a large reorg and resume after getheaders/inv
     for j in range(2):
