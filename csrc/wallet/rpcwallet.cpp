@@ -311,6 +311,20 @@ static UniValue fundrawtransaction(const JSONRPCRequest& req) {
             includeWatching = req.params[1].get_bool();
         } else {
             const UniValue& o = req.params[1].get_obj();
+            // reference RPCTypeCheckObj(options, {...}, fAllowNull = true, fStrict = true)
+            static const std::map<std::string, std::vector<UniValue::VType>> known = {
+                {"changeAddress", {UniValue::VSTR}},   {"changePosition", {UniValue::VNUM}},
+                {"includeWatching", {UniValue::VBOOL}}, {"lockUnspents", {UniValue::VBOOL}},
+                {"reserveChangeKey", {UniValue::VBOOL}}, {"feeRate", {UniValue::VNUM, UniValue::VSTR}},
+                {"subtractFeeFromOutputs", {UniValue::VARR}}};
+            for (const std::string& k : o.getKeys()) {
+                auto it = known.find(k);
+                if (it == known.end()) ThrowRPC(RPC_TYPE_ERROR, strprintf("Unexpected key %s", k.c_str()));
+                const UniValue& v = o[k];
+                if (!v.isNull() && std::find(it->second.begin(), it->second.end(), v.getType()) == it->second.end())
+                    ThrowRPC(RPC_TYPE_ERROR, strprintf("Expected type %s for %s, got %s", uvTypeName(it->second[0]),
+                                                       k.c_str(), uvTypeName(v.getType())));
+            }
             if (o.exists("changeAddress")) {
                 changeAddress = DecodeDestination(o["changeAddress"].get_str(), P());
                 if (!changeAddress.IsValid()) ThrowRPC(RPC_INVALID_ADDRESS_OR_KEY, "changeAddress must be a valid bitcoin address");
