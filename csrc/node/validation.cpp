@@ -1366,7 +1366,9 @@ bool Chainstate::ConnectBlockFinish(PendingConnect& p, CValidationState& state, 
     const CBlockUndo& blockundo = p.blockundo;
     bool ok = p.sigsOk;
     if (p.sigs.valid()) ok = p.sigs.get() && ok;
-    // Before the fork script failures do not invalidate blocks (reference validation.cpp:2121-2126).
+    // Before the fork script failures do not invalidate blocks (reference validation.cpp:2121-2126:
+    // control.Wait() is ignored below BCPHeight; the checks always go through the queue control,
+    // :2010-2011 and :2080-2087, whatever -par says, so this holds for every thread count).
     if (p.nJobs > 0 && !ok && p.postfork)
         return state.DoS(100, false, REJECT_INVALID, "blk-bad-inputs", false, "parallel script check failed");
     const int64_t nTime4 = GetTimeMicros();
