@@ -111,7 +111,8 @@ std::string HelpMessage() {
                                  "block N's signature batch (default: 1, one block at a time; measured faster since the "
                                  "signature batch takes 2 ms, profiles/connect_r5.md)"},
         {"-blockcachemb=<n>", "Keep blocks accepted out of order in memory until they connect, up to <n> MiB "
-                              "(default: 512; 0 reads them back from disk like the reference)"},
+                              "(decoded in-memory size, several times the serialized size; default: 512; 0 reads them back "
+                              "from disk like the reference)"},
         {"-parallelutxo=<n>", "Run the UTXO pass of blocks with at least <n> transactions on all script threads "
                               "(default: 64; 0 = always serial)"},
         {"-acceptnonstdtxn", "Relay and mine \"non-standard\" transactions (default: 0 on main, 1 on the test chains)"},

@@ -12,6 +12,7 @@
 #include "node/txmempool.h"
 #include "script/interpreter.h"
 #include "util/strencodings.h"
+#include "util/memusage.h"
 #include "util/reaper.h"
 
 #include <algorithm>
@@ -611,7 +612,23 @@ bool Chainstate::AcceptBlock(const std::shared_ptr<const CBlock>& pblock, CValid
     return true;
 }
 
-void Chainstate::CacheRecentBlock(const uint256& hash, const std::shared_ptr<const CBlock>& pblock, size_t bytes) {
+// Heap bytes a decoded block holds (the transactions, their input/output vectors and scripts,
+// the shared_ptr control blocks): several times its serialized size, and what -blockcachemb
+// counts.
+static size_t BlockMemoryUsage(const CBlock& block) {
+    size_t m = memusage::DynamicUsage(block.vtx);
+    for (const CTransactionRef& tx : block.vtx) {
+        m += memusage::MallocUsage(sizeof(CTransaction) + 16); // object + control block (make_shared)
+        m += memusage::DynamicUsage(tx->vin) + memusage::DynamicUsage(tx->vout);
+        for (const CTxIn& in : tx->vin) m += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(in.scriptSig));
+        for (const CTxOut& out : tx->vout)
+            m += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(out.scriptPubKey));
+    }
+    return m;
+}
+
+void Chainstate::CacheRecentBlock(const uint256& hash, const std::shared_ptr<const CBlock>& pblock, size_t) {
+    const size_t bytes = BlockMemoryUsage(*pblock);
     if (bytes > opts.recentBlockBytes || recentBlocks.count(hash)) return;
     while (recentBytes + bytes > opts.recentBlockBytes && !recentOrder.empty()) {
         auto it = recentBlocks.find(recentOrder.front());
@@ -631,7 +648,14 @@ std::shared_ptr<const CBlock> Chainstate::TakeRecentBlock(const uint256& hash) {
     std::shared_ptr<const CBlock> b = std::move(it->second.first);
     recentBytes -= it->second.second;
     recentBlocks.erase(it);
-    if (recentBlocks.empty()) recentOrder.clear();
+    // taken blocks leave their hash in the eviction order; drop those once they outnumber the
+    // cached blocks (a stale-fork block that never connects keeps the map non-empty forever)
+    if (recentOrder.size() > 2 * recentBlocks.size() + 64) {
+        std::deque<uint256> keep;
+        for (const uint256& h : recentOrder)
+            if (recentBlocks.count(h)) keep.push_back(h);
+        recentOrder.swap(keep);
+    }
     return b;
 }
 
@@ -762,14 +786,15 @@ private:
 std::vector<unsigned char> SerializeBlockUndo(const CBlockUndo& undo, WorkerPool* pool) {
     const size_t n = undo.vtxundo.size();
     std::vector<unsigned char> out;
+    const bool serial = !pool || n < 1024;
     {
+        // the writer trims `out` to what it wrote when it goes out of scope: return only after
         FastVectorWriter w(out);
         WriteCompactSize(w, n);
-        if (!pool || n < 1024) {
+        if (serial)
             for (const CTxUndo& u : undo.vtxundo) w << u;
-            return out;
-        }
     }
+    if (serial) return out;
     const size_t chunks = std::min<size_t>(64, n / 256);
     std::vector<std::vector<unsigned char>> parts(chunks);
     pool->ParallelFor(chunks, [&](size_t c) {

@@ -326,6 +326,120 @@ TEST_CASE(connectblock_tests, parallel_pass_with_bip34_active) {
     CHECK(cs.Tip()->GetBlockHash() == blk.GetHash());
 }
 
+// After the BIP34 block BIP30 is no longer checked, so a coinbase whose first output is already
+// an unspent coin replaces it (AddCoins with possible_overwrite, reference src/coins.cpp:97-134 and
+// src/validation.cpp:1952-1990). The same post-BIP34 block is connected by two fresh chainstates,
+// one through the parallel UTXO pass and one through the serial pass: the verdicts, the coins the
+// block touches (the overwritten coin included) and the undo bytes on disk are identical, and a
+// variant that double-spends gets the same reject reason from both.
+TEST_CASE(connectblock_tests, post_bip34_coinbase_overwrite_both_paths) {
+    test::TestChain100Setup setup;
+    Chainstate& a = *setup.node->chainstate;
+    Consensus::Params& cons = const_cast<CChainParams&>(Params()).MutableConsensus();
+    const int savedHeight = cons.BIP34Height;
+    const uint256 savedHash = cons.BIP34Hash;
+    cons.BIP34Height = 5;
+    {
+        std::lock_guard<CCriticalSection> l(a.cs());
+        cons.BIP34Hash = a.ActiveChain()[5]->GetBlockHash();
+    }
+    struct Restore {
+        Consensus::Params& c;
+        int h;
+        uint256 hh;
+        ~Restore() {
+            c.BIP34Height = h;
+            c.BIP34Hash = hh;
+        }
+    } restore{cons, savedHeight, savedHash};
+    const CKey& key = setup.coinbaseKey;
+    const CScript spk = P2PK(key);
+    for (int i = 0; i < 3; i++) setup.CreateAndProcessBlock({}, spk);
+    std::vector<std::shared_ptr<const CBlock>> chain; // a's blocks above genesis, in height order
+    for (const CBlockIndex* p = a.TipNow(); p && p->pprev; p = p->pprev) {
+        auto b = std::make_shared<CBlock>();
+        REQUIRE(ReadBlockFromDisk(*b, p, Params(), true));
+        chain.insert(chain.begin(), b);
+    }
+    std::vector<CMutableTransaction> txs;
+    const Amount each = (setup.coinbaseTxns[0].vout[0].nValue - 100000) / 80;
+    txs.push_back(Make({{setup.coinbaseTxns[0], 0}}, std::vector<CTxOut>(80, CTxOut(each, spk)), key));
+    const CTransaction fan(txs[0]);
+    for (uint32_t i = 0; i < 70; i++) txs.push_back(Make({{fan, i}}, {CTxOut(each - 1000, spk)}, key));
+    CBlock blk = Assemble(a, txs, spk);
+    uint64_t tries = 1u << 30;
+    REQUIRE(SolveBlock(blk, Params(), tries, false));
+    const COutPoint cbOut(blk.vtx[0]->GetHash(), 0);
+    // the double-spending variant: one more transaction spending fan output 0 again
+    std::vector<CMutableTransaction> bad = txs;
+    bad.push_back(Make({{fan, 0}}, {CTxOut(each - 2000, spk)}, key));
+    const CBlock badBlk = Assemble(a, bad, spk);
+
+    struct Result {
+        std::pair<std::string, std::string> verdict, badVerdict;
+        std::map<std::string, std::string> coins;
+        std::vector<unsigned char> undo;
+        int64_t fast = 0;
+    } res[2];
+    for (int par = 0; par < 2; par++) {
+        ChainstateOptions o;
+        o.memoryOnly = true;
+        char tmpl[] = "/tmp/bcp_test_bip34ow_XXXXXX";
+        REQUIRE(mkdtemp(tmpl) != nullptr);
+        o.datadir = tmpl;
+        o.useGpu = false;
+        Chainstate b(Params(), o);
+        std::string err;
+        REQUIRE(b.InitBlockIndex(err));
+        for (const auto& c : chain) {
+            bool fNew = false;
+            CValidationState st;
+            REQUIRE(b.ProcessNewBlock(c, true, &fNew, &st));
+        }
+        REQUIRE(b.TipNow()->GetBlockHash() == a.TipNow()->GetBlockHash());
+        {
+            // an earlier coinbase with this txid whose first output is still unspent
+            std::lock_guard<CCriticalSection> l(b.cs());
+            b.CoinsTip().AddCoin(cbOut, Coin(CTxOut(12345, spk), 7, true), true);
+        }
+        Result& r = res[par];
+        r.verdict = Verdicts(b, blk);
+        r.badVerdict = Verdicts(b, badBlk);
+        b.SetParallelUtxoMinTx(par ? 1 : 0);
+        const int64_t fast0 = b.ConnectPhaseMicros(Chainstate::PH_FASTUTXO);
+        bool fNew = false;
+        CValidationState st;
+        REQUIRE(b.ProcessNewBlock(std::make_shared<const CBlock>(blk), true, &fNew, &st));
+        r.fast = b.ConnectPhaseMicros(Chainstate::PH_FASTUTXO) - fast0;
+        {
+            std::lock_guard<CCriticalSection> l(b.cs());
+            CHECK(b.Tip()->GetBlockHash() == blk.GetHash());
+            r.coins = Snapshot(b, txs, {cbOut});
+            const CBlockIndex* tip = b.Tip();
+            CBlockUndo undo;
+            REQUIRE(UndoReadFromDisk(undo, tip->GetUndoPos(), tip->pprev->GetBlockHash()));
+            r.undo = SerializeToBytes(undo, SER_DISK, PROTOCOL_VERSION);
+        }
+        const std::string cmd = std::string("rm -rf '") + tmpl + "'";
+        if (system(cmd.c_str()) != 0) {}
+    }
+    // serial (par 0) and parallel (par 1) runs; within each, Verdicts ran both passes too
+    CHECK_EQ(res[0].fast, (int64_t)0);
+    CHECK_EQ(res[1].fast, (int64_t)1);
+    for (const Result& r : res) {
+        CHECK_EQ(r.verdict.first, std::string("valid"));
+        CHECK_EQ(r.verdict.second, std::string("valid"));
+        CHECK_EQ(r.badVerdict.first, std::string("bad-txns-inputs-missingorspent"));
+        CHECK_EQ(r.badVerdict.second, r.badVerdict.first);
+    }
+    CHECK(Same(res[0].coins, res[1].coins));
+    // the coinbase's output replaced the old coin (height and value of the new block)
+    CHECK(res[1].coins.at(cbOut.ToString()).find("/7/") == std::string::npos);
+    CHECK(!res[1].coins.at(cbOut.ToString()).empty());
+    CHECK(res[0].undo == res[1].undo);
+    CHECK_EQ(res[0].undo.size() > 0, true);
+}
+
 // Blocks accepted out of order connect from the recent-block cache (no disk read, no second
 // CheckBlock), and the chain is the same with the cache off (-blockcachemb=0 reads them back).
 TEST_CASE(connectblock_tests, recent_block_cache_out_of_order) {
