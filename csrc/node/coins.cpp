@@ -246,6 +246,23 @@ void CCoinsViewCache::SpendFetchedMoved(const COutPoint& outpoint) {
     ins.first->second.flags = CCoinsCacheEntry::DIRTY; // not FRESH: the base holds the coin
 }
 
+void CCoinsViewCache::SpendPeeked(const COutPoint& outpoint) {
+    const unsigned s = CCoinsMap::ShardOf(outpoint);
+    auto ins = cacheCoins.shard(s).try_emplace(outpoint); // no node is made when the entry exists
+    if (ins.second) {
+        ins.first->second.flags = CCoinsCacheEntry::DIRTY; // not FRESH: the base holds the coin
+        return;
+    }
+    auto it = ins.first;
+    usage[s].bytes -= it->second.coin.DynamicMemoryUsage();
+    if (it->second.flags & CCoinsCacheEntry::FRESH) {
+        cacheCoins.shard(s).erase(it);
+    } else {
+        it->second.flags |= CCoinsCacheEntry::DIRTY;
+        it->second.coin.Clear();
+    }
+}
+
 bool CCoinsViewCache::HaveCoin(const COutPoint& outpoint) const {
     auto it = FetchCoin(outpoint);
     return it != cacheCoins.end() && !it->second.coin.IsSpent();

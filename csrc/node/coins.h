@@ -344,6 +344,11 @@ public:
     // The same entry when the caller already moved the base's copy of the coin elsewhere (into
     // an undo record): a spent, DIRTY, not FRESH entry.
     void SpendFetchedMoved(const COutPoint& outpoint);
+    // Spends an unspent coin the caller read through PeekCoins and already moved elsewhere (into
+    // an undo record), whether or not this cache holds it: its own entry is erased when FRESH and
+    // otherwise left spent and DIRTY (SpendCoin); with no entry, a spent, DIRTY, not FRESH one is
+    // added (SpendFetchedMoved). Never reads the base. Safe under ForEachShard.
+    void SpendPeeked(const COutPoint& outpoint);
     void AddCoin(const COutPoint& outpoint, Coin&& coin, bool possible_overwrite);
     bool SpendCoin(const COutPoint& outpoint, Coin* moveto = nullptr);
     bool Flush();

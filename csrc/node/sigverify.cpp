@@ -151,7 +151,10 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
     uint64_t hits = 0;
     // cache keys are one SHA-256 each: on the pool, in chunks whose lookups share one lock
     const size_t PROBE_CHUNK = 256;
+    // nothing was ever stored and nothing will be: every probe would miss (initial sync)
+    const bool skipProbes = !cacheStore && !cache.MayHold();
     auto probe = [&](size_t chunk) {
+        if (skipProbes) return;
         const size_t lo = chunk * PROBE_CHUNK, hi = std::min(checks.size(), lo + PROBE_CHUNK);
         for (size_t i = lo; i < hi; i++) {
             const DeferredSigCheck& c = *checks[i];
@@ -175,9 +178,13 @@ bool BatchVerifySignatures(const std::vector<const DeferredSigCheck*>& checks,
         if (sampleHits * 2 < PROBE_CHUNK) {
             auto gpuRun = std::async(std::launch::async, [&checks] { return GpuVerifyDeferred(checks); });
             const int64_t t0 = GetTimeMicros();
-            if (pool) pool->ParallelFor(nChunks - 1, [&](size_t k) { probe(k + 1); }, 1);
-            else
+            if (skipProbes) {
+                // nothing to probe: the pool stays free for other work while the GPU runs
+            } else if (pool) {
+                pool->ParallelFor(nChunks - 1, [&](size_t k) { probe(k + 1); }, 1);
+            } else {
                 for (size_t k = 1; k < nChunks; k++) probe(k);
+            }
             std::vector<uint8_t> r;
             bool gpuOk = true;
             try {

@@ -5,6 +5,7 @@
 // runs on the CPU pool and the deferred ECDSA checks (interpreter.h) are verified in
 // one batch: on the GPU when available and the batch is large enough, else on the pool.
 #pragma once
+#include <atomic>
 #include "script/interpreter.h"
 #include "util/cuckoocache.h"
 #include "util/util.h"
@@ -23,7 +24,13 @@ class SignatureCache {
 public:
     SignatureCache();
     bool Get(const uint256& entry, bool erase) const { return set.contains(entry, erase); }
-    void Set(const uint256& entry) { set.insert(entry); }
+    void Set(const uint256& entry) {
+        if (!everSet.load(std::memory_order_relaxed)) everSet.store(true, std::memory_order_relaxed);
+        set.insert(entry);
+    }
+    // false while nothing was ever stored (a node in initial sync, whose blocks' signatures were
+    // never seen in its mempool): a probe could only miss, so a batch skips the probes
+    bool MayHold() const { return everSet.load(std::memory_order_relaxed); }
     void GetMany(const uint256* entries, size_t n, bool erase, uint8_t* hit) const {
         set.contains_many(entries, n, erase, hit);
     }
@@ -40,6 +47,7 @@ public:
 private:
     uint256 nonce;
     SharedCuckooSet set;
+    std::atomic<bool> everSet{false};
 };
 SignatureCache& GetSignatureCache();
 // -maxsigcachesize / -maxscriptcachesize (MiB); returns element capacities.

@@ -468,8 +468,15 @@ bool ReadRawBlockFromDisk(std::vector<unsigned char>& out, const CDiskBlockPos& 
     return ok;
 }
 
+uint256 UndoChecksum(const std::vector<unsigned char>& ser, const uint256& hashBlock) {
+    HashWriter hasher;
+    hasher << hashBlock;
+    hasher.write((const char*)ser.data(), ser.size());
+    return hasher.GetHash();
+}
+
 bool UndoWriteToDisk(const std::vector<unsigned char>& ser, CDiskBlockPos& pos, const uint256& hashBlock,
-                     const unsigned char diskMagic[4]) {
+                     const unsigned char diskMagic[4], const uint256* checksum) {
     // one serialisation, one hash pass and one write: the undo record is serialised once by the
     // caller (the reference serialises it three times - size, file, checksum - through small
     // buffered writes). The checksum is SHA256d(hashBlock || record), as the reference's.
@@ -482,10 +489,7 @@ bool UndoWriteToDisk(const std::vector<unsigned char>& ser, CDiskBlockPos& pos, 
     if (p < 0) return false;
     pos.nPos = (unsigned)p;
     out.write((const char*)ser.data(), ser.size());
-    HashWriter hasher;
-    hasher << hashBlock;
-    hasher.write((const char*)ser.data(), ser.size());
-    out << hasher.GetHash();
+    out << (checksum ? *checksum : UndoChecksum(ser, hashBlock));
     return true;
 }
 

@@ -133,9 +133,12 @@ bool ReadBlockFromDisk(CBlock& block, const CBlockIndex* pindex, const CChainPar
 // error (truncation, trailing bytes inside a transaction's span) fails the whole block.
 bool DecodeBlock(const unsigned char* data, size_t len, CBlock& block, WorkerPool* pool);
 bool ReadRawBlockFromDisk(std::vector<unsigned char>& out, const CDiskBlockPos& pos);
-// the same for an already serialised (SER_DISK) undo record
+// the same for an already serialised (SER_DISK) undo record; `checksum`, when given, is its
+// UndoChecksum (computed off the caller's critical path)
 bool UndoWriteToDisk(const std::vector<unsigned char>& ser, CDiskBlockPos& pos, const uint256& hashBlock,
-                     const unsigned char diskMagic[4]);
+                     const unsigned char diskMagic[4], const uint256* checksum = nullptr);
+// SHA256d(hashBlock || record): the checksum stored after an undo record
+uint256 UndoChecksum(const std::vector<unsigned char>& ser, const uint256& hashBlock);
 bool UndoWriteToDisk(const CBlockUndo& undo, CDiskBlockPos& pos, const uint256& hashBlock,
                      const unsigned char diskMagic[4]);
 bool UndoReadFromDisk(CBlockUndo& undo, const CDiskBlockPos& pos, const uint256& hashBlock);

@@ -19,6 +19,7 @@
 #include <thread>
 #include <deque>
 #include <future>
+#include <tuple>
 #include <unistd.h>
 #include <cassert>
 #include <cmath>
@@ -64,7 +65,13 @@ struct ScriptCache {
         return r;
     }
     bool Has(const uint256& k, bool erase) { return set.contains(k, erase); }
-    void Add(const uint256& k) { set.insert(k); }
+    void Add(const uint256& k) {
+        if (!everAdded.load(std::memory_order_relaxed)) everAdded.store(true, std::memory_order_relaxed);
+        set.insert(k);
+    }
+    // false while no key was ever added (only mempool acceptance adds): lookups could only miss
+    bool MayHold() const { return everAdded.load(std::memory_order_relaxed); }
+    std::atomic<bool> everAdded{false};
 };
 ScriptCache& GetScriptCache() {
     static ScriptCache c;
@@ -753,6 +760,14 @@ struct Chainstate::PendingConnect {
     std::vector<std::pair<uint256, CDiskTxPos>> vPos;
     int64_t nTimeStart = 0, nTime2 = 0;
     int nInputs = 0;
+    // The coins tip under the (empty) view, when the caller lets the parallel UTXO pass update
+    // it in place instead of the view (ConnectTip); `tipApplied` once it did, so that a verdict
+    // that fails afterwards undoes the block on the tip from its undo records.
+    CCoinsViewCache* directTip = nullptr;
+    bool tipApplied = false;
+    // the undo record serialised and checksummed on a helper thread while the signature batch
+    // runs on the GPU (joined before blockundo may move or die)
+    std::future<std::pair<std::vector<unsigned char>, uint256>> undoSer;
 };
 
 namespace {
@@ -812,9 +827,18 @@ std::vector<unsigned char> SerializeBlockUndo(const CBlockUndo& undo, WorkerPool
 }
 
 bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
-                              bool fJustCheck) {
+                              bool fJustCheck, CCoinsViewCache* directTip) {
     PendingConnect p;
+    p.directTip = fJustCheck ? nullptr : directTip;
     const bool ok = ConnectBlockPrepare(block, state, pindex, view, fJustCheck, false, p) && ConnectBlockFinish(p, state, fJustCheck);
+    if (p.undoSer.valid()) p.undoSer.wait(); // it reads blockundo
+    if (!ok && p.tipApplied) {
+        // a verdict after the in-place update failed: take the block back off the tip (its outputs
+        // removed, the spent coins restored from the undo records), as DisconnectBlock would
+        if (ApplyBlockUndo(p.blockundo, block, pindex, *p.directTip) != DISCONNECT_OK)
+            LogPrintf("ConnectBlock: undoing the failed block %s on the coins tip was not clean\n",
+                      pindex->GetBlockHash().ToString().c_str());
+    }
     Reaper::Get().Drop(std::move(p.blockundo)); // 21k+ undo vectors for a big block
     return ok;
 }
@@ -885,6 +909,9 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     blockundo.vtxundo.reserve(block.vtx.size() - 1);
     const size_t ntx = block.vtx.size();
     ScriptCache& sc = GetScriptCache();
+    // ConnectBlock only reads the script cache (mempool acceptance fills it, under cs_main as
+    // this is): while it was never filled every lookup would miss, so no key is computed
+    const bool scMayHold = sc.MayHold();
 
     // One parallel, read-only pass over the block before anything writes the view stack:
     //  * BIP30: no output of the block may already exist unspent;
@@ -939,7 +966,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 txSizes[i] = tx.GetTotalSize();
                 legacySigOps[i] = (uint32_t)GetSigOpCountWithoutP2SH(tx);
                 if (i > 0 && fScriptChecks) {
-                    scKeys[i] = sc.Key(tx, flags);
+                    if (scMayHold) scKeys[i] = sc.Key(tx, flags);
                     txdatas[i].reset(new PrecomputedTransactionData(tx));
                 }
             }
@@ -947,8 +974,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         1);
     if (bip30Clash)
         return state.DoS(100, error("ConnectBlock(): tried to overwrite transaction"), REJECT_INVALID, "bad-txns-BIP30");
-    // the view gains about one entry per input and output: size its table once
-    view.Reserve(view.GetCacheSize() + maxJobs + nOutputs);
     phase(PH_PRECOMPUTE);
 
     // Script checks overlap the UTXO pass (reference CCheckQueue: the master keeps connecting
@@ -1125,6 +1150,18 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             sigTotal += txSigOps[i];
             if (sigTotal > nMaxSigOpsCount) bad = true;
         }
+        // In place on the coins tip (ConnectTip): the view is empty, so every input was fetched
+        // and nothing of the block is in the view yet. Not when the coinbase would overwrite a
+        // coin (a duplicate coinbase after BIP34; undoing it could not bring that coin back).
+        CCoinsViewCache* tip = p.directTip;
+        if (!bad.load() && tip && view.GetCacheSize() == 0) {
+            const CTransaction& cb = *block.vtx[0];
+            for (size_t o = 0; o < cb.vout.size() && tip; o++)
+                if (tip->HaveCoin(COutPoint(cb.GetHash(), (uint32_t)o))) tip = nullptr;
+        } else {
+            tip = nullptr;
+        }
+        CCoinsViewCache& target = tip ? *tip : view;
         if (!bad.load()) {
             fastDone = true;
             phaseMicros[PH_FASTUTXO].fetch_add(1, std::memory_order_relaxed);
@@ -1146,7 +1183,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                             else if (src[k] == SRC_BLOCK) undo.vprevout[j] = std::move(made[k]);
                             else undo.vprevout[j] = *coinOf[k];
                         }
-                        needScripts[i] = fScriptChecks && !sc.Has(scKeys[i], !fJustCheck);
+                        needScripts[i] = fScriptChecks && !(scMayHold && sc.Has(scKeys[i], !fJustCheck));
                     }
                     for (size_t i = chunk * TCHUNK; i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
                         const CTransaction& tx = *block.vtx[i];
@@ -1190,18 +1227,21 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 pos.nTxOffset += txSizes[i];
             }
             nSigOpsCount = sigTotal;
-            // The view updates, one coins-map shard per task (CCoinsMap): spends of fetched coins
-            // and of the view's own coins, then the block's outputs that stay unspent. The scripts
-            // published above run meanwhile; nothing they read is in the view.
+            // The view updates (or the tip's), one coins-map shard per task (CCoinsMap): spends of
+            // fetched coins and of the view's own coins, then the block's outputs that stay
+            // unspent. The scripts published above run meanwhile; nothing they read is in the view.
+            if (!tip) view.Reserve(view.GetCacheSize() + maxJobs + nOutputs);
+            p.tipApplied = tip != nullptr;
             std::string applyError;
             std::mutex applyMu;
-            view.ForEachShard(
+            target.ForEachShard(
                 [&](unsigned sh) {
                     try {
                         for (size_t k = 0; k < maxJobs; k++) {
                             if (inShard[k] != sh) continue;
                             const COutPoint& op = prevoutOf(k);
-                            if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(op);
+                            if (tip) tip->SpendPeeked(op);
+                            else if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(op);
                             else if (src[k] == SRC_VIEW && !view.SpendCoin(op)) throw std::runtime_error("view spend failed");
                         }
                         for (size_t i = 0; i < ntx; i++) {
@@ -1209,7 +1249,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                             for (size_t o = 0; o < tx.vout.size(); o++) {
                                 const size_t q = firstOutput[i] + o;
                                 if (outShard[q] == sh && !newCoins[q].IsSpent())
-                                    view.AddCoin(COutPoint(tx.GetHash(), (uint32_t)o), std::move(newCoins[q]), i == 0);
+                                    target.AddCoin(COutPoint(tx.GetHash(), (uint32_t)o), std::move(newCoins[q]), i == 0);
                             }
                         }
                     } catch (const std::exception& e) {
@@ -1223,6 +1263,8 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         }
     }
     if (!fastDone) {
+        // the view gains about one entry per input and output: size its table once
+        view.Reserve(view.GetCacheSize() + maxJobs + nOutputs);
         // The serial UTXO pass. Each input's coin is taken from the view (or the prefetch) once; the
         // checks below used to go back to the view for it six times (HaveInputs, the height list,
         // the P2SH sigop count, GetValueIn, CheckTxInputs, SpendCoin). The references stay valid
@@ -1298,7 +1340,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 // transactions fully validated under these flags in the mempool skip re-execution; the
                 // jobs read the spent coins from the undo record (reserved up front: the addresses are
                 // stable for the whole block) instead of copying each script
-                if (fScriptChecks && !sc.Has(scKeys[i], !fJustCheck)) {
+                if (fScriptChecks && !(scMayHold && sc.Has(scKeys[i], !fJustCheck))) {
                     for (size_t j = 0; j < tx.vin.size(); j++) {
                         const CTxOut& out = undo.vprevout[j].GetTxOut();
                         jobs[nProduced + j] = ScriptJob{&tx, (unsigned)j, &out.scriptPubKey, out.nValue, txdatas[i].get()};
@@ -1365,6 +1407,18 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                     return BatchVerifySignatures(all, groups, wp, useGpu, false, erase);
                 });
             } else {
+                // While the GPU checks the signatures the CPU is idle: the undo record is
+                // serialised and checksummed meanwhile (written once the verdict is in)
+                if (!fJustCheck && pindex->GetUndoPos().IsNull() && ntx >= 1024 && GpuBatchesExpected(opts.useGpu)) {
+                    const CBlockUndo* u = &blockundo;
+                    const uint256 prevHash = pindex->pprev->GetBlockHash();
+                    WorkerPool* wp = pool.get(); // idle meanwhile unless the batch probes the cache
+                    p.undoSer = std::async(std::launch::async, [u, prevHash, wp]() {
+                        std::vector<unsigned char> ser = SerializeBlockUndo(*u, wp);
+                        const uint256 sum = UndoChecksum(ser, prevHash);
+                        return std::make_pair(std::move(ser), sum);
+                    });
+                }
                 ok = BatchVerifySignatures(all, groups, pool.get(), opts.useGpu, false, !fJustCheck);
                 phase(PH_BATCH);
             }
@@ -1405,10 +1459,14 @@ bool Chainstate::ConnectBlockFinish(PendingConnect& p, CValidationState& state, 
         if (pindex->GetUndoPos().IsNull()) {
             const int64_t tu = GetTimeMicros();
             CDiskBlockPos upos;
-            const std::vector<unsigned char> ser = SerializeBlockUndo(blockundo, pool.get());
+            std::vector<unsigned char> ser;
+            uint256 sum;
+            const bool early = p.undoSer.valid();
+            if (early) std::tie(ser, sum) = p.undoSer.get();
+            else ser = SerializeBlockUndo(blockundo, pool.get());
             if (!FindUndoPos(state, pindex->nFile, upos, (unsigned)ser.size() + 40))
                 return error("ConnectBlock(): FindUndoPos failed");
-            if (!UndoWriteToDisk(ser, upos, pindex->pprev->GetBlockHash(), params.DiskMagic()))
+            if (!UndoWriteToDisk(ser, upos, pindex->pprev->GetBlockHash(), params.DiskMagic(), early ? &sum : nullptr))
                 return state.Error("Failed to write undo data");
             pindex->nUndoPos = upos.nPos;
             pindex->nStatus |= BLOCK_HAVE_UNDO;
@@ -1719,8 +1777,10 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
     const int64_t nTime2 = GetTimeMicros();
     int64_t nTime3, nTime4;
     {
+        // a block that takes the parallel UTXO pass updates the tip in place (undone on failure);
+        // the view then only carries the new best block
         CCoinsViewCache view(pcoinsTip.get());
-        const bool rv = ConnectBlock(blockConnecting, state, pindexNew, view);
+        const bool rv = ConnectBlock(blockConnecting, state, pindexNew, view, false, opts.connectInPlace ? pcoinsTip.get() : nullptr);
         GetMainSignals().BlockChecked(blockConnecting, state);
         if (!rv) {
             if (state.IsInvalid()) InvalidBlockFound(pindexNew, state);

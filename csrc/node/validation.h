@@ -97,6 +97,9 @@ struct ChainstateOptions {
     int connectPipeline = 1;
     // the UTXO pass of a block with at least this many transactions runs in parallel (0: never)
     size_t parallelUtxoMinTx = 64;
+    // that pass updates the coins tip in place (undone from the undo records if a later check
+    // fails) instead of a per-block view merged into the tip afterwards (-connectinplace)
+    bool connectInPlace = true;
     // -blockcachemb: blocks accepted but not yet connected stay in memory up to this many
     // serialized bytes (oldest evicted first), so the connect that follows (IBD, blocks arriving
     // out of order) skips the disk read, the deserialisation and the repeat CheckBlock; 0: off
@@ -290,7 +293,7 @@ private:
                               const std::shared_ptr<const CBlock>& pblock, ConnectTrace& trace)
         EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
-                      bool fJustCheck = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+                      bool fJustCheck = false, CCoinsViewCache* directTip = nullptr) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     DisconnectResult DisconnectBlock(const CBlock& block, const CBlockIndex* pindex, CCoinsViewCache& view) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool DisconnectTip(CValidationState& state, bool fBare = false) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ConnectTip(CValidationState& state, CBlockIndex* pindexNew, const std::shared_ptr<const CBlock>& pblock,

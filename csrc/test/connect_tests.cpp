@@ -8,6 +8,7 @@
 #include "test/unittest.h"
 #include "util/sync.h"
 
+#include "consensus/merkle.h"
 #include "node/miner.h"
 #include "node/txdb.h"
 #include "node/validation.h"
@@ -324,6 +325,59 @@ TEST_CASE(connectblock_tests, parallel_pass_with_bip34_active) {
     CHECK_EQ(cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO), fastBefore + 1);
     std::lock_guard<CCriticalSection> l(cs.cs());
     CHECK(cs.Tip()->GetBlockHash() == blk.GetHash());
+}
+
+// ConnectTip lets the parallel UTXO pass update the coins tip in place (no per-block view to
+// merge). A block that fails after that update (here: its coinbase claims more than subsidy plus
+// fees, checked after the UTXO pass) must leave the tip exactly as it was, and the chain then
+// connects the honest version of the same block through the same path.
+TEST_CASE(connectblock_tests, in_place_tip_update_undone_on_failure) {
+    test::TestChain100Setup setup;
+    Chainstate& cs = *setup.node->chainstate;
+    const CKey& key = setup.coinbaseKey;
+    const CScript spk = P2PK(key);
+    for (int i = 0; i < 3; i++) setup.CreateAndProcessBlock({}, spk);
+    std::vector<CMutableTransaction> txs;
+    const Amount each = (setup.coinbaseTxns[0].vout[0].nValue - 100000) / 80;
+    txs.push_back(Make({{setup.coinbaseTxns[0], 0}}, std::vector<CTxOut>(80, CTxOut(each, spk)), key));
+    const CTransaction fan(txs[0]);
+    for (uint32_t i = 0; i < 70; i++) txs.push_back(Make({{fan, i}}, {CTxOut(each - 1000, spk)}, key));
+    for (int c = 1; c <= 2; c++) // mature coinbases (heights 2 and 3; the block is at 104)
+        txs.push_back(Make({{setup.coinbaseTxns[c], 0}}, {CTxOut(setup.coinbaseTxns[c].vout[0].nValue - 2000, spk)}, key));
+    const std::vector<COutPoint> none;
+    std::map<std::string, std::string> before;
+    uint256 tipBefore;
+    {
+        std::lock_guard<CCriticalSection> l(cs.cs());
+        before = Snapshot(cs, txs, none);
+        tipBefore = cs.Tip()->GetBlockHash();
+    }
+    CBlock greedy = Assemble(cs, txs, spk);
+    CMutableTransaction cb(*greedy.vtx[0]);
+    cb.vout[0].nValue += 50 * COIN;
+    greedy.vtx[0] = MakeTransactionRef(cb);
+    greedy.hashMerkleRoot = BlockMerkleRoot(greedy);
+    uint64_t tries = 1u << 30;
+    REQUIRE(SolveBlock(greedy, Params(), tries, false));
+    const int64_t fast0 = cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO);
+    bool fNew = false;
+    CValidationState st;
+    cs.ProcessNewBlock(std::make_shared<const CBlock>(greedy), true, &fNew, &st);
+    CHECK_EQ(cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO), fast0 + 1); // it got to the in-place update
+    {
+        std::lock_guard<CCriticalSection> l(cs.cs());
+        CHECK(cs.Tip()->GetBlockHash() == tipBefore);
+        CHECK(Same(before, Snapshot(cs, txs, none)));
+        CHECK_EQ(Snapshot(cs, {}, {COutPoint(greedy.vtx[0]->GetHash(), 0)}).begin()->second, std::string());
+        CHECK(cs.CoinsTip().GetBestBlock() == tipBefore);
+    }
+    const CBlock honest = setup.CreateAndProcessBlock(txs, spk);
+    CHECK_EQ(cs.ConnectPhaseMicros(Chainstate::PH_FASTUTXO), fast0 + 2);
+    std::lock_guard<CCriticalSection> l(cs.cs());
+    CHECK(cs.Tip()->GetBlockHash() == honest.GetHash());
+    const auto after = Snapshot(cs, txs, none);
+    for (const CMutableTransaction& m : txs)
+        for (const CTxIn& in : m.vin) CHECK_EQ(after.at(in.prevout.ToString()), std::string());
 }
 
 // After the BIP34 block BIP30 is no longer checked, so a coinbase whose first output is already

@@ -389,6 +389,46 @@ static void CoinsApply84k_Sharded(State& st) {
 }
 BENCHMARK(CoinsApply84k_Sharded);
 
+// One block's updates applied to a large coins tip in place (ConnectTip's parallel UTXO pass):
+// 42k spends of the previous block's outputs (FRESH entries, erased) and 42k new outputs, one
+// shard per pool task, on a tip that already holds -tipcoins entries (default 400k)
+static void CoinsTipApply84k_Sharded(State& st) {
+    CCoinsView base;
+    CCoinsViewCache tip(&base);
+    const size_t N = 42000, held = (size_t)gArgs.GetArg("-tipcoins", (int64_t)400000);
+    FastRandomContext rng(true);
+    const CScript spk = CScript() << OP_DUP << OP_HASH160 << std::vector<unsigned char>(20, 7) << OP_EQUALVERIFY
+                                  << OP_CHECKSIG;
+    for (size_t i = 0; i < held; i++) tip.AddCoin(COutPoint(rng.rand256(), 0), Coin(CTxOut(1000, spk), 1, false), false);
+    std::vector<COutPoint> prev(N);
+    for (size_t i = 0; i < N; i++) {
+        prev[i] = COutPoint(rng.rand256(), (uint32_t)(i & 1));
+        tip.AddCoin(prev[i], Coin(CTxOut(1000, spk), 2, false), false);
+    }
+    WorkerPool pool(std::min(16, std::max(2, GetNumCores())));
+    while (st.KeepRunning()) {
+        std::vector<COutPoint> made(N);
+        for (size_t i = 0; i < N; i++) made[i] = COutPoint(rng.rand256(), (uint32_t)(i & 1));
+        std::vector<uint8_t> ss(N), ms(N);
+        for (size_t i = 0; i < N; i++) {
+            ss[i] = (uint8_t)CCoinsMap::ShardOf(prev[i]);
+            ms[i] = (uint8_t)CCoinsMap::ShardOf(made[i]);
+        }
+        const int64_t t0 = GetTimeMicros();
+        tip.ForEachShard(
+            [&](unsigned sh) {
+                for (size_t i = 0; i < N; i++)
+                    if (ss[i] == sh) tip.SpendPeeked(prev[i]);
+                for (size_t i = 0; i < N; i++)
+                    if (ms[i] == sh) tip.AddCoin(made[i], Coin(CTxOut(1000, spk), 3, false), false);
+            },
+            &pool);
+        fprintf(stderr, "# tip apply %.2f ms (tip %u entries)\n", (GetTimeMicros() - t0) / 1000.0, tip.GetCacheSize());
+        prev.swap(made);
+    }
+}
+BENCHMARK(CoinsTipApply84k_Sharded);
+
 static void CoinSelection(State& st) {
     SelectParams("regtest");
     CWallet wallet("bench", "", true);
@@ -1143,6 +1183,10 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         o.datadir = tmpl;
         o.useGpu = useGpu;
         o.connectPipeline = pipeline;
+        o.connectInPlace = gArgs.GetBoolArg("-connectinplace", o.connectInPlace);
+        // -ibdab: alternate in-place (odd runs) and merged-view (even runs) connects, for an
+        // interleaved A/B in one process over one fixture
+        if (gArgs.GetBoolArg("-ibdab", false)) o.connectInPlace = iters % 2 == 1;
         o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
         o.parallelUtxoMinTx = (size_t)gArgs.GetArg("-parallelutxo", (int64_t)o.parallelUtxoMinTx);
         Chainstate cs(Params(), o);
@@ -1172,12 +1216,12 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
             const double total = 0.001 * (t1 - t0) / nb;
             const double tip = ms(Chainstate::PH_ABC_TIP);
             fprintf(stderr,
-                    "# ibd %s pipeline=%d (ms/block): total %.2f = ConnectTip %.2f + outside %.2f [accept %.2f, find %.3f, "
+                    "# ibd %s pipeline=%d in_place=%d (ms/block): total %.2f = ConnectTip %.2f + outside %.2f [accept %.2f, find %.3f, "
                     "step-other %.2f, signals %.2f, reap %.2f, notify %.2f, checkindex %.2f, flush %.2f]; "
                     "inside ConnectTip: read %.2f, connectblock %.2f [checkblock %.2f, prefetch %.2f, utxo %.2f, "
                     "scripts %.2f, batch %.2f, undo %.2f], view-flush %.2f, flushstate %.2f, post %.2f; recent-block cache "
                     "hits %llu, misses %llu\n",
-                    useGpu ? "GPU" : "CPU", pipeline, total, tip, total - tip, ms(Chainstate::PH_ACCEPT),
+                    useGpu ? "GPU" : "CPU", pipeline, (int)o.connectInPlace, total, tip, total - tip, ms(Chainstate::PH_ACCEPT),
                     ms(Chainstate::PH_ABC_FIND), ms(Chainstate::PH_ABC_STEP) - tip, ms(Chainstate::PH_ABC_SIGNALS),
                     ms(Chainstate::PH_ABC_REAP), ms(Chainstate::PH_ABC_NOTIFY), ms(Chainstate::PH_ABC_CHECKINDEX),
                     ms(Chainstate::PH_ABC_FLUSH), ms(Chainstate::PH_TIP_READ), ms(Chainstate::PH_TIP_CONNECT),
@@ -1185,15 +1229,29 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
                     ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_BATCH), ms(Chainstate::PH_UNDO), ms(Chainstate::PH_TIP_FLUSH),
                     ms(Chainstate::PH_TIP_WRITE), ms(Chainstate::PH_TIP_POST),
                     (unsigned long long)cs.RecentBlockHits(), (unsigned long long)cs.RecentBlockMisses());
+            fprintf(stderr, "# ibd fast-utxo sub-phases (ms/block): setup %.2f checks %.2f undo %.2f apply %.2f\n",
+                    ms(Chainstate::PH_FU_SETUP), ms(Chainstate::PH_FU_CHECKS), ms(Chainstate::PH_FU_UNDO),
+                    ms(Chainstate::PH_FU_APPLY));
         }
         if (cs.HeightNow() != f.run.size() + f.setup.size()) {
             fprintf(stderr, "IBD run ended at height %d\n", cs.HeightNow());
             exit(1);
         }
+        {
+            // the undo records written during the run read back with matching checksums
+            std::lock_guard<CCriticalSection> l(cs.cs());
+            for (const CBlockIndex* p = cs.Tip(); p && p->nHeight > (int)f.setup.size(); p = p->pprev) {
+                CBlockUndo u;
+                if (!UndoReadFromDisk(u, p->GetUndoPos(), p->pprev->GetBlockHash()) || u.vtxundo.size() < 20000) {
+                    fprintf(stderr, "IBD run: undo record of height %d unreadable\n", p->nHeight);
+                    exit(1);
+                }
+            }
+        }
         totalMs += (t1 - t0) / 1000.0;
         iters++;
-        printf("{\"bench\": \"IbdPipelineRun\", \"gpu\": %s, \"pipeline\": %d, \"iter\": %d, \"ms_per_block\": %.2f}\n",
-               useGpu ? "true" : "false", pipeline, iters, (t1 - t0) / 1000.0 / f.run.size());
+        printf("{\"bench\": \"IbdPipelineRun\", \"gpu\": %s, \"pipeline\": %d, \"in_place\": %s, \"iter\": %d, \"ms_per_block\": %.2f}\n",
+               useGpu ? "true" : "false", pipeline, o.connectInPlace ? "true" : "false", iters, (t1 - t0) / 1000.0 / f.run.size());
         fflush(stdout);
         const std::string cmd = std::string("rm -rf '") + tmpl + "'";
         if (system(cmd.c_str()) != 0) {}
