@@ -117,6 +117,8 @@ std::string HelpMessage() {
                               "(default: 64; 0 = always serial)"},
         {"-connectinplace", "Let that parallel UTXO pass update the coins tip in place, undone from the block's undo "
                             "data if a later check fails, instead of merging a per-block view into it (default: 1)"},
+        {"-connectlookahead", "While a block's signatures are checked on the GPU, fetch the next block's input coins and "
+                              "precompute its transactions on the idle script threads (default: 1)"},
         {"-acceptnonstdtxn", "Relay and mine \"non-standard\" transactions (default: 0 on main, 1 on the test chains)"},
         {"-assumevalid=<hex>", "If this block is in the chain assume that it and its ancestors are valid and potentially skip their script verification (0 to verify all)"},
         {"-bytespersigop=<n>", "Equivalent bytes per sigop in transactions for relay and mining (default: 20)"},

@@ -34,6 +34,7 @@ std::unique_ptr<NodeContext> BuildNode(const std::string& chain, const std::stri
     o.connectPipeline = (int)gArgs.GetArg("-connectpipeline", (int64_t)o.connectPipeline);
     o.parallelUtxoMinTx = (size_t)std::max<int64_t>(0, gArgs.GetArg("-parallelutxo", (int64_t)o.parallelUtxoMinTx));
     o.connectInPlace = gArgs.GetBoolArg("-connectinplace", o.connectInPlace);
+    o.connectLookahead = gArgs.GetBoolArg("-connectlookahead", o.connectLookahead);
     o.recentBlockBytes = (size_t)std::max<int64_t>(0, gArgs.GetArg("-blockcachemb", (int64_t)(o.recentBlockBytes >> 20))) << 20;
     SetFastPrune(gArgs.GetBoolArg("-fastprune", false) && node->params->NetworkIDString() == "regtest");
     const int64_t prune = gArgs.GetArg("-prune", (int64_t)0);

@@ -78,6 +78,91 @@ ScriptCache& GetScriptCache() {
     return c;
 }
 } // namespace
+
+// ConnectBlockPrepare's read-only pass over a block, in chunks of transactions that any thread
+// may run: BIP30 (no output of the block may already exist unspent), every input's coin fetched
+// through `view` (PeekCoins: through the caches to the database without filling them), and the
+// per-transaction work that needs no coins - the BIP143-style sighash midstates, the script-cache
+// key, the serialized size and the legacy sigop count.
+struct Chainstate::BlockPrefetch {
+    static constexpr size_t CHUNK = 48; // one batch of coin lookups down the view stack
+    std::shared_ptr<const CBlock> hold; // a lookahead's block, kept alive while its chunks run
+    const CBlock* block = nullptr;
+    const CCoinsView* view = nullptr;
+    bool fEnforceBIP30 = false, fScriptChecks = true, scMayHold = false;
+    uint32_t flags = 0;
+    size_t ntx = 0, maxJobs = 0, nOutputs = 0;
+    std::vector<std::unique_ptr<PrecomputedTransactionData>> txdatas;
+    std::vector<uint256> scKeys;
+    std::vector<uint32_t> txSizes, legacySigOps;
+    std::vector<size_t> firstInput; // tx i's inputs are [firstInput[i], firstInput[i+1])
+    std::vector<Coin> prefetched;
+    std::unique_ptr<uint8_t[]> prefetchedFound;
+    std::atomic<bool> bip30Clash{false};
+
+    void Init(const CBlock& b, const CCoinsView& v, bool bip30, bool scripts, bool scHold, uint32_t fl) {
+        block = &b;
+        view = &v;
+        fEnforceBIP30 = bip30;
+        fScriptChecks = scripts;
+        scMayHold = scHold;
+        flags = fl;
+        ntx = b.vtx.size();
+        txdatas.resize(ntx);
+        scKeys.resize(ntx);
+        txSizes.resize(ntx);
+        legacySigOps.resize(ntx);
+        firstInput.assign(ntx + 1, 0);
+        nOutputs = 0;
+        for (size_t i = 0; i < ntx; i++) {
+            firstInput[i + 1] = firstInput[i] + (i > 0 ? b.vtx[i]->vin.size() : 0);
+            nOutputs += b.vtx[i]->vout.size();
+        }
+        maxJobs = firstInput[ntx];
+        prefetched.resize(maxJobs);
+        prefetchedFound.reset(new uint8_t[maxJobs + 1]);
+    }
+    size_t Chunks() const { return (ntx + CHUNK - 1) / CHUNK; }
+    void Chunk(size_t chunk, ScriptCache& sc) {
+        const CBlock& blk = *block;
+        const size_t lo = chunk * CHUNK, hi = std::min(ntx, lo + CHUNK);
+        std::vector<COutPoint> keys;
+        for (size_t i = lo; i < hi; i++) {
+            const CTransaction& tx = *blk.vtx[i];
+            if (fEnforceBIP30)
+                for (size_t o = 0; o < tx.vout.size(); o++) keys.emplace_back(tx.GetHash(), (uint32_t)o);
+            if (i > 0)
+                for (const CTxIn& in : tx.vin) keys.push_back(in.prevout);
+        }
+        std::vector<Coin> got(keys.size());
+        std::unique_ptr<uint8_t[]> found(new uint8_t[keys.size() + 1]);
+        view->PeekCoins(keys.data(), keys.size(), got.data(), found.get());
+        size_t q = 0;
+        for (size_t i = lo; i < hi; i++) {
+            const CTransaction& tx = *blk.vtx[i];
+            if (fEnforceBIP30)
+                for (size_t o = 0; o < tx.vout.size(); o++, q++)
+                    if (found[q] && !got[q].IsSpent()) bip30Clash = true;
+            if (i > 0)
+                for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++, q++) {
+                    prefetchedFound[k] = found[q];
+                    if (found[q]) prefetched[k] = std::move(got[q]);
+                }
+            txSizes[i] = tx.GetTotalSize();
+            legacySigOps[i] = (uint32_t)GetSigOpCountWithoutP2SH(tx);
+            if (i > 0 && fScriptChecks) {
+                if (scMayHold) scKeys[i] = sc.Key(tx, flags);
+                txdatas[i].reset(new PrecomputedTransactionData(tx));
+            }
+        }
+    }
+};
+
+struct Chainstate::Lookahead {
+    uint256 forHash, afterHash; // block N+1, and the block N whose in-place update it read
+    BlockPrefetch pf;
+    bool open = false; // its chunks are on the script queue (a session this thread must close)
+};
 size_t InitScriptExecutionCache(int64_t mib) {
     mib = std::min(std::max<int64_t>(0, mib), MAX_MAX_SCRIPT_CACHE_SIZE);
     const size_t n = GetScriptCache().set.setup_bytes((size_t)mib << 20);
@@ -826,11 +911,91 @@ std::vector<unsigned char> SerializeBlockUndo(const CBlockUndo& undo, WorkerPool
     return out;
 }
 
+// BIP30 exceptions: the two historic duplicate coinbases
+static bool IsBIP30Exception(const CBlockIndex* pindex) {
+    return pindex->phashBlock &&
+           ((pindex->nHeight == 91842 &&
+             pindex->GetBlockHash() == uint256S("0x00000000000a4d0a398161ffc163c503763b1f4360639393e0e4c8e300e0caec")) ||
+            (pindex->nHeight == 91880 &&
+             pindex->GetBlockHash() == uint256S("0x00000000000743f190a18c5577a3c2d2a1f610ae9601ac046a38084ccb7cd721")));
+}
+
+// BIP30 is checked except for the two exceptions and after the BIP34 block (reference
+// validation.cpp:1952-1980)
+bool Chainstate::EnforceBIP30For(const CBlockIndex* pindex) const {
+    const Consensus::Params& cp = params.GetConsensus();
+    const CBlockIndex* pindexBIP34height = pindex->pprev->GetAncestor(cp.BIP34Height);
+    return !IsBIP30Exception(pindex) && (!pindexBIP34height || !(pindexBIP34height->GetBlockHash() == cp.BIP34Hash));
+}
+
+// -assumevalid: scripts are skipped for an ancestor of the assumed-valid block that is buried
+// under two weeks of work below the best header (reference validation.cpp:1925-1948)
+bool Chainstate::ScriptChecksFor(const CBlockIndex* pindex) const {
+    if (opts.assumeValid.IsNull()) return true;
+    const Consensus::Params& cp = params.GetConsensus();
+    auto it = mapBlockIndex.find(opts.assumeValid);
+    if (it != mapBlockIndex.end() && it->second->GetAncestor(pindex->nHeight) == pindex && pindexBestHeader &&
+        pindexBestHeader->GetAncestor(pindex->nHeight) == pindex &&
+        pindexBestHeader->nChainWork >= UintToArith256(cp.nMinimumChainWork))
+        return GetBlockProofEquivalentTime(*pindexBestHeader, *pindex, *pindexBestHeader, cp) <= 60 * 60 * 24 * 7 * 2;
+    return true;
+}
+
+std::shared_ptr<const CBlock> Chainstate::PeekRecentBlock(const uint256& hash) const {
+    auto it = recentBlocks.find(hash);
+    return it == recentBlocks.end() ? nullptr : it->second.first;
+}
+
+// Called by block N's connect once its UTXO pass has updated the coins tip in place and its
+// signatures are about to go to the GPU: block N+1 (the next block ActivateBestChainStep will
+// connect, if it is in the recent-block cache) gets its read-only pass on the script threads,
+// which are idle until N+1's scripts. Every coin it fetches is read from the tip as N left it.
+void Chainstate::StartLookahead(const CBlockIndex* pindex) {
+    lookahead.reset();
+    const CBlockIndex* next = pindexConnectNext;
+    if (!next || next->pprev != pindex) return;
+    std::shared_ptr<const CBlock> nb = PeekRecentBlock(next->GetBlockHash());
+    if (!nb || nb->vtx.size() < 1024) return;
+    std::unique_ptr<Lookahead> la(new Lookahead());
+    la->forHash = next->GetBlockHash();
+    la->afterHash = pindex->GetBlockHash();
+    la->pf.hold = nb;
+    la->pf.Init(*nb, *pcoinsTip, EnforceBIP30For(next), ScriptChecksFor(next), GetScriptCache().MayHold(),
+                GetBlockScriptFlags(next));
+    Lookahead* raw = la.get();
+    scriptQueue->Begin([raw](size_t chunk) { raw->pf.Chunk(chunk, GetScriptCache()); });
+    scriptQueue->Publish(raw->pf.Chunks());
+    la->open = true;
+    lookahead = std::move(la);
+}
+
+// Closes the lookahead's script-queue session (this thread runs what is left of it). Must run
+// before anything writes the coins tip or opens another session on the queue.
+void Chainstate::JoinLookahead() {
+    if (!lookahead || !lookahead->open) return;
+    const int64_t t = GetTimeMicros();
+    scriptQueue->Complete();
+    lookahead->open = false;
+    phaseMicros[PH_LA_WAIT].fetch_add(GetTimeMicros() - t, std::memory_order_relaxed);
+}
+
 bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
                               bool fJustCheck, CCoinsViewCache* directTip) {
     PendingConnect p;
     p.directTip = fJustCheck ? nullptr : directTip;
-    const bool ok = ConnectBlockPrepare(block, state, pindex, view, fJustCheck, false, p) && ConnectBlockFinish(p, state, fJustCheck);
+    bool ok = false;
+    try {
+        ok = ConnectBlockPrepare(block, state, pindex, view, fJustCheck, false, p) && ConnectBlockFinish(p, state, fJustCheck);
+    } catch (...) {
+        JoinLookahead();
+        lookahead.reset();
+        if (p.undoSer.valid()) p.undoSer.wait();
+        throw;
+    }
+    // the lookahead for the next block ran through the verdict and the undo write; it read the
+    // tip as this block left it, so it goes if this block is taken back off the tip
+    JoinLookahead();
+    if (!ok) lookahead.reset();
     if (p.undoSer.valid()) p.undoSer.wait(); // it reads blockundo
     if (!ok && p.tipApplied) {
         // a verdict after the in-place update failed: take the block back off the tip (its outputs
@@ -849,6 +1014,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
 // (best block included) when this returns; the block is valid only once Finish agrees.
 bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& state, CBlockIndex* pindex,
                                      CCoinsViewCache& view, bool fJustCheck, bool async, PendingConnect& p) {
+    JoinLookahead(); // normally closed already (ConnectBlock joins it after the previous block)
     const int64_t nTimeStart = GetTimeMicros();
     p.pindex = pindex;
     p.nTimeStart = nTimeStart;
@@ -870,26 +1036,9 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         p.genesis = true;
         return true;
     }
-    bool fScriptChecks = true;
-    if (!opts.assumeValid.IsNull()) {
-        auto it = mapBlockIndex.find(opts.assumeValid);
-        if (it != mapBlockIndex.end() && it->second->GetAncestor(pindex->nHeight) == pindex && pindexBestHeader &&
-            pindexBestHeader->GetAncestor(pindex->nHeight) == pindex &&
-            pindexBestHeader->nChainWork >= UintToArith256(cp.nMinimumChainWork)) {
-            fScriptChecks = GetBlockProofEquivalentTime(*pindexBestHeader, *pindex, *pindexBestHeader, cp) <=
-                            60 * 60 * 24 * 7 * 2;
-        }
-    }
-    // BIP30 (exceptions for the two historic duplicate coinbases; moot after BIP34 block)
-    const bool fBIP30Exception =
-        pindex->phashBlock &&
-        ((pindex->nHeight == 91842 &&
-          pindex->GetBlockHash() == uint256S("0x00000000000a4d0a398161ffc163c503763b1f4360639393e0e4c8e300e0caec")) ||
-         (pindex->nHeight == 91880 &&
-          pindex->GetBlockHash() == uint256S("0x00000000000743f190a18c5577a3c2d2a1f610ae9601ac046a38084ccb7cd721")));
-    const CBlockIndex* pindexBIP34height = pindex->pprev->GetAncestor(cp.BIP34Height);
-    const bool fEnforceBIP30 =
-        !fBIP30Exception && (!pindexBIP34height || !(pindexBIP34height->GetBlockHash() == cp.BIP34Hash));
+    const bool fScriptChecks = ScriptChecksFor(pindex);
+    const bool fBIP30Exception = IsBIP30Exception(pindex);
+    const bool fEnforceBIP30 = EnforceBIP30For(pindex);
     int nLockTimeFlags = 0;
     if (VersionBitsState(pindex->pprev, cp, Consensus::DEPLOYMENT_CSV, versionbitscache) == THRESHOLD_ACTIVE)
         nLockTimeFlags |= LOCKTIME_VERIFY_SEQUENCE;
@@ -913,66 +1062,35 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // this is): while it was never filled every lookup would miss, so no key is computed
     const bool scMayHold = sc.MayHold();
 
-    // One parallel, read-only pass over the block before anything writes the view stack:
-    //  * BIP30: no output of the block may already exist unspent;
-    //  * every input's coin is fetched (PeekCoin: through the caches to the database without
-    //    filling them), so the serial pass below inserts it into the view instead of walking the
-    //    view stack itself - a coin created or spent earlier in this block is found in the view
-    //    first, so the prefetched copy of an outpoint is only used while it is still current;
-    //  * the per-transaction work that needs no coins: the BIP143-style sighash midstates
-    //    (PrecomputedTransactionData), the script-cache key, the serialized size and the legacy
-    //    sigop count.
-    std::vector<std::unique_ptr<PrecomputedTransactionData>> txdatas(ntx);
-    std::vector<uint256> scKeys(ntx);
-    std::vector<uint32_t> txSizes(ntx), legacySigOps(ntx);
-    std::vector<size_t> firstInput(ntx + 1, 0); // tx i's inputs are [firstInput[i], firstInput[i+1])
-    size_t nOutputs = 0;
-    for (size_t i = 0; i < ntx; i++) {
-        firstInput[i + 1] = firstInput[i] + (i > 0 ? block.vtx[i]->vin.size() : 0);
-        nOutputs += block.vtx[i]->vout.size();
+    // One parallel, read-only pass over the block before anything writes the view stack
+    // (BlockPrefetch): so the UTXO pass below inserts each input's coin into the view instead of
+    // walking the view stack itself - a coin created or spent earlier in this block is found in
+    // the view first, so the prefetched copy of an outpoint is only used while it is still
+    // current. The previous block's connect may have run it already (the lookahead): adopted
+    // when it is this block's, read the tip as it is now, and under this block's flags.
+    std::unique_ptr<Lookahead> la = std::move(lookahead);
+    std::unique_ptr<BlockPrefetch> own;
+    BlockPrefetch* pf = nullptr;
+    if (la && !fJustCheck && la->forHash == pindex->GetBlockHash() && la->afterHash == hashPrevBlock &&
+        view.GetCacheSize() == 0 && la->pf.ntx == ntx && la->pf.flags == flags &&
+        la->pf.fEnforceBIP30 == fEnforceBIP30 && la->pf.fScriptChecks == fScriptChecks && la->pf.scMayHold == scMayHold) {
+        pf = &la->pf;
+        phaseMicros[PH_LA_USED].fetch_add(1, std::memory_order_relaxed);
+    } else {
+        own.reset(new BlockPrefetch());
+        own->Init(block, view, fEnforceBIP30, fScriptChecks, scMayHold, flags);
+        pool->ParallelFor(own->Chunks(), [&](size_t chunk) { own->Chunk(chunk, sc); }, 1);
+        pf = own.get();
     }
-    const size_t maxJobs = firstInput[ntx];
-    std::vector<Coin> prefetched(maxJobs);
-    std::unique_ptr<uint8_t[]> prefetchedFound(new uint8_t[maxJobs + 1]);
-    std::atomic<bool> bip30Clash{false};
-    // chunks of transactions, each chunk's coin lookups sent down the view stack as one batch
-    const size_t CHUNK = 48;
-    pool->ParallelFor(
-        (ntx + CHUNK - 1) / CHUNK,
-        [&](size_t chunk) {
-            const size_t lo = chunk * CHUNK, hi = std::min(ntx, lo + CHUNK);
-            std::vector<COutPoint> keys;
-            for (size_t i = lo; i < hi; i++) {
-                const CTransaction& tx = *block.vtx[i];
-                if (fEnforceBIP30)
-                    for (size_t o = 0; o < tx.vout.size(); o++) keys.emplace_back(tx.GetHash(), (uint32_t)o);
-                if (i > 0)
-                    for (const CTxIn& in : tx.vin) keys.push_back(in.prevout);
-            }
-            std::vector<Coin> got(keys.size());
-            std::unique_ptr<uint8_t[]> found(new uint8_t[keys.size() + 1]);
-            view.PeekCoins(keys.data(), keys.size(), got.data(), found.get());
-            size_t q = 0;
-            for (size_t i = lo; i < hi; i++) {
-                const CTransaction& tx = *block.vtx[i];
-                if (fEnforceBIP30)
-                    for (size_t o = 0; o < tx.vout.size(); o++, q++)
-                        if (found[q] && !got[q].IsSpent()) bip30Clash = true;
-                if (i > 0)
-                    for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++, q++) {
-                        prefetchedFound[k] = found[q];
-                        if (found[q]) prefetched[k] = std::move(got[q]);
-                    }
-                txSizes[i] = tx.GetTotalSize();
-                legacySigOps[i] = (uint32_t)GetSigOpCountWithoutP2SH(tx);
-                if (i > 0 && fScriptChecks) {
-                    if (scMayHold) scKeys[i] = sc.Key(tx, flags);
-                    txdatas[i].reset(new PrecomputedTransactionData(tx));
-                }
-            }
-        },
-        1);
-    if (bip30Clash)
+    std::vector<std::unique_ptr<PrecomputedTransactionData>>& txdatas = pf->txdatas;
+    const std::vector<uint256>& scKeys = pf->scKeys;
+    const std::vector<uint32_t>& txSizes = pf->txSizes;
+    const std::vector<uint32_t>& legacySigOps = pf->legacySigOps;
+    const std::vector<size_t>& firstInput = pf->firstInput;
+    std::vector<Coin>& prefetched = pf->prefetched;
+    const std::unique_ptr<uint8_t[]>& prefetchedFound = pf->prefetchedFound;
+    const size_t nOutputs = pf->nOutputs, maxJobs = pf->maxJobs;
+    if (pf->bip30Clash)
         return state.DoS(100, error("ConnectBlock(): tried to overwrite transaction"), REJECT_INVALID, "bad-txns-BIP30");
     phase(PH_PRECOMPUTE);
 
@@ -999,7 +1117,10 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // every return below drains and closes the session first (jobs/sinks outlive it)
     struct CompleteOnExit {
         CheckQueue& q;
-        ~CompleteOnExit() { q.Complete(); }
+        bool armed = true;
+        ~CompleteOnExit() {
+            if (armed) q.Complete();
+        }
     } completeOnExit{*scriptQueue};
 
     // The UTXO pass, in parallel for a valid block (round 4). Every input's coin is resolved
@@ -1419,6 +1540,11 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                         return std::make_pair(std::move(ser), sum);
                     });
                 }
+                // the scripts' session is closed: the next block's read-only pass may use the queue
+                if (!fJustCheck && opts.connectLookahead && p.tipApplied && ntx >= 1024 && GpuBatchesExpected(opts.useGpu)) {
+                    completeOnExit.armed = false;
+                    StartLookahead(pindex);
+                }
                 ok = BatchVerifySignatures(all, groups, pool.get(), opts.useGpu, false, !fJustCheck);
                 phase(PH_BATCH);
             }
@@ -1715,6 +1841,8 @@ bool Chainstate::ReadBlock(CBlock& block, const CBlockIndex* pindex, bool checkP
 }
 
 bool Chainstate::DisconnectTip(CValidationState& state, bool fBare) {
+    JoinLookahead();
+    lookahead.reset(); // it read the tip this disconnect changes
     CBlockIndex* pindexDelete = chainActive.Tip();
     auto pblock = std::make_shared<CBlock>();
     if (!ReadBlockFromDisk(*pblock, pindexDelete, params)) return state.Error("Failed to read block");
@@ -2072,8 +2200,13 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
         for (auto it = vpindexToConnect.rbegin(); it != vpindexToConnect.rend(); ++it) {
             CBlockIndex* pindexConnect = *it;
             const int64_t tTip = GetTimeMicros();
+            // the block after this one, for the connect lookahead
+            pindexConnectNext = pindexMostWork->nHeight > pindexConnect->nHeight
+                                    ? pindexMostWork->GetAncestor(pindexConnect->nHeight + 1)
+                                    : nullptr;
             const bool tipOk = ConnectTip(state, pindexConnect,
                                           pindexConnect == pindexMostWork ? pblock : std::shared_ptr<const CBlock>(), trace);
+            pindexConnectNext = nullptr;
             phaseMicros[PH_ABC_TIP].fetch_add(GetTimeMicros() - tTip, std::memory_order_relaxed);
             if (!tipOk) {
                 if (state.IsInvalid()) {

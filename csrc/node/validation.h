@@ -100,6 +100,9 @@ struct ChainstateOptions {
     // that pass updates the coins tip in place (undone from the undo records if a later check
     // fails) instead of a per-block view merged into the tip afterwards (-connectinplace)
     bool connectInPlace = true;
+    // with the tip updated in place and the signatures on the GPU, the next block's read-only
+    // pass runs meanwhile on the idle script threads (-connectlookahead)
+    bool connectLookahead = true;
     // -blockcachemb: blocks accepted but not yet connected stay in memory up to this many
     // serialized bytes (oldest evicted first), so the connect that follows (IBD, blocks arriving
     // out of order) skips the disk read, the deserialisation and the repeat CheckBlock; 0: off
@@ -257,6 +260,9 @@ public:
         // (prepare + finish), view flush into the coins tip, FlushStateToDisk, mempool + tip update
         PH_TIP_READ, PH_TIP_CONNECT, PH_TIP_FLUSH, PH_TIP_WRITE, PH_TIP_POST,
         PH_UNDO, // inside ConnectBlockFinish: the block's undo data serialised and written
+        // the connect lookahead: time the connecting thread waited for it after block N's
+        // verdict, and the number of blocks whose connect adopted it (a count, not micros)
+        PH_LA_WAIT, PH_LA_USED,
         PH_COUNT
     };
     int64_t ConnectPhaseMicros(ConnectPhase ph) const { return phaseMicros[ph].load(std::memory_order_relaxed); }
@@ -358,6 +364,19 @@ private:
     void CacheRecentBlock(const uint256& hash, const std::shared_ptr<const CBlock>& pblock, size_t bytes)
         EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     std::shared_ptr<const CBlock> TakeRecentBlock(const uint256& hash) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    std::shared_ptr<const CBlock> PeekRecentBlock(const uint256& hash) const EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    // Connect lookahead: while block N's signatures are on the GPU, the script threads run block
+    // N+1's read-only pass (its input coins fetched from the tip, which already holds N's
+    // in-place update; sighash midstates, sizes, sigop counts). N+1's connect adopts the result
+    // when nothing changed in between; a failed N, a disconnect or any other block drops it.
+    struct BlockPrefetch;
+    struct Lookahead;
+    std::unique_ptr<Lookahead> lookahead;
+    CBlockIndex* pindexConnectNext = nullptr; // the block ActivateBestChainStep connects after this one
+    void StartLookahead(const CBlockIndex* pindex) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    void JoinLookahead();
+    bool ScriptChecksFor(const CBlockIndex* pindex) const EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+    bool EnforceBIP30For(const CBlockIndex* pindex) const;
     std::map<uint256, std::pair<std::shared_ptr<const CBlock>, size_t>> recentBlocks GUARDED_BY(cs_main);
     std::deque<uint256> recentOrder GUARDED_BY(cs_main);
     size_t recentBytes GUARDED_BY(cs_main) = 0;

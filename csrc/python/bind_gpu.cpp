@@ -319,6 +319,21 @@ void bind_gpu(pyb::module_& m) {
     m.def("gpu_verify_set_min_shard", [](size_t ecdsa, size_t eh) {
         GpuVerifyService::Instance().SetMinShard(ecdsa, eh);
     });
+    m.def("gpu_verify_set_min_device_shard", [](size_t ecdsa, size_t eh) {
+        GpuVerifyService::Instance().SetMinDeviceShard(ecdsa, eh);
+    });
+    // the shard plan a batch of n items would get on the current lanes: (lane, lo, hi) per shard
+    m.def("gpu_verify_plan", [](size_t n, bool equihash) {
+        std::vector<std::tuple<size_t, size_t, size_t>> out;
+        for (const VerifyShard& s : GpuVerifyService::Instance().Plan(n, equihash)) out.emplace_back(s.lane, s.lo, s.hi);
+        return out;
+    }, pyb::arg("n"), pyb::arg("equihash") = false);
+    // the pure planner (no GPU): PlanShards(n, lane devices, min per device, min per lane)
+    m.def("plan_shards", [](size_t n, const std::vector<int>& laneDevices, size_t minDev, size_t minLane) {
+        std::vector<std::tuple<size_t, size_t, size_t>> out;
+        for (const VerifyShard& s : PlanShards(n, laneDevices, minDev, minLane)) out.emplace_back(s.lane, s.lo, s.hi);
+        return out;
+    });
     m.def("gpu_verify_shutdown", []() {
         pyb::gil_scoped_release nogil;
         GpuVerifyService::Instance().Shutdown();

@@ -10,6 +10,7 @@
 
 #include "consensus/merkle.h"
 #include "node/miner.h"
+#include "node/sigverify.h"
 #include "node/txdb.h"
 #include "node/validation.h"
 #include "script/sign.h"
@@ -492,6 +493,106 @@ TEST_CASE(connectblock_tests, post_bip34_coinbase_overwrite_both_paths) {
     CHECK(!res[1].coins.at(cbOut.ToString()).empty());
     CHECK(res[0].undo == res[1].undo);
     CHECK_EQ(res[0].undo.size() > 0, true);
+}
+
+// The connect lookahead: while block N's signature batch is out (here the GPU path with every
+// batch failing over to the CPU, -gpufaultinjection), block N+1's read-only pass runs on the
+// script threads against the tip N left. Four 1100-transaction blocks connected last-to-first in
+// one ActivateBestChain: the later ones adopt their lookahead, and the chain and coins are the
+// same as the node that connected them one by one without it.
+TEST_CASE(connectblock_tests, lookahead_adopted_and_same_coins) {
+    test::TestChain100Setup setup;
+    Chainstate& a = *setup.node->chainstate;
+    const CKey& key = setup.coinbaseKey;
+    const CScript spk = P2PK(key);
+    std::vector<CMutableTransaction> all;
+    const size_t W = 1100;
+    const Amount each = (setup.coinbaseTxns[0].vout[0].nValue - 100000) / (Amount)W;
+    all.push_back(Make({{setup.coinbaseTxns[0], 0}}, std::vector<CTxOut>(W, CTxOut(each, spk)), key));
+    setup.CreateAndProcessBlock({all[0]}, spk);
+    std::vector<Prev> outs;
+    {
+        const CTransaction fan(all[0]);
+        for (uint32_t i = 0; i < W; i++) outs.push_back({fan, i});
+    }
+    for (int b = 0; b < 4; b++) {
+        std::vector<CMutableTransaction> txs;
+        std::vector<Prev> next;
+        for (size_t i = 0; i < W; i++) {
+            const Amount v = outs[i].tx.vout[outs[i].n].nValue;
+            txs.push_back(Make({outs[i]}, {CTxOut(v - 500, spk)}, key));
+            next.push_back({CTransaction(txs.back()), 0});
+        }
+        setup.CreateAndProcessBlock(txs, spk);
+        all.insert(all.end(), txs.begin(), txs.end());
+        outs.swap(next);
+    }
+    std::vector<std::shared_ptr<const CBlock>> chain;
+    for (const CBlockIndex* p = a.TipNow(); p && p->pprev; p = p->pprev) {
+        auto blk = std::make_shared<CBlock>();
+        REQUIRE(ReadBlockFromDisk(*blk, p, Params(), true));
+        chain.insert(chain.begin(), blk);
+    }
+    const size_t thr = GetGpuSigThreshold();
+    SetGpuSigThreshold(1);
+    SetGpuFaultInjection(true);
+    ResetGpuSigFailures();
+    struct Undo {
+        size_t thr;
+        ~Undo() {
+            SetGpuFaultInjection(false);
+            ResetGpuSigFailures();
+            SetGpuSigThreshold(thr);
+        }
+    } undo{thr};
+    ChainstateOptions o;
+    o.memoryOnly = true;
+    char tmpl[] = "/tmp/bcp_test_lookahead_XXXXXX";
+    REQUIRE(mkdtemp(tmpl) != nullptr);
+    o.datadir = tmpl;
+    o.useGpu = true; // batches go the GPU way (and fail over to the CPU)
+    Chainstate b(Params(), o);
+    std::string err;
+    REQUIRE(b.InitBlockIndex(err));
+    auto feed = [&](const std::shared_ptr<const CBlock>& blk) {
+        bool fNew = false;
+        CValidationState st;
+        return b.ProcessNewBlock(blk, true, &fNew, &st);
+    };
+    const size_t n = chain.size();
+    for (size_t i = 0; i + 4 < n; i++) REQUIRE(feed(chain[i]));
+    std::vector<CBlockHeader> hdrs;
+    for (size_t i = n - 4; i < n; i++) hdrs.push_back(chain[i]->GetBlockHeader());
+    CValidationState hs;
+    REQUIRE(b.ProcessNewBlockHeaders(hdrs, hs));
+    const int64_t used0 = b.ConnectPhaseMicros(Chainstate::PH_LA_USED);
+    for (size_t i = n; i-- > n - 4;) REQUIRE(feed(chain[i])); // last to first
+    CHECK(b.TipNow()->GetBlockHash() == a.TipNow()->GetBlockHash());
+    // blocks 2 and 3 adopt the lookahead of the block before (after three failed GPU batches the
+    // GPU path is off, so block 4 is not looked ahead)
+    CHECK(b.ConnectPhaseMicros(Chainstate::PH_LA_USED) - used0 >= 2);
+    std::map<std::string, std::string> sa, sb;
+    {
+        std::lock_guard<CCriticalSection> l(a.cs());
+        sa = Snapshot(a, all, {});
+    }
+    {
+        std::lock_guard<CCriticalSection> l(b.cs());
+        sb = Snapshot(b, all, {});
+    }
+    CHECK(Same(sa, sb));
+    {
+        // their undo records (serialised and checksummed beside the batch) read back
+        std::lock_guard<CCriticalSection> l(b.cs());
+        int k = 0;
+        for (const CBlockIndex* p = b.Tip(); k < 4; p = p->pprev, k++) {
+            CBlockUndo u;
+            CHECK(UndoReadFromDisk(u, p->GetUndoPos(), p->pprev->GetBlockHash()));
+            CHECK_EQ(u.vtxundo.size(), W);
+        }
+    }
+    const std::string cmd = std::string("rm -rf '") + tmpl + "'";
+    if (system(cmd.c_str()) != 0) {}
 }
 
 // Blocks accepted out of order connect from the recent-block cache (no disk read, no second

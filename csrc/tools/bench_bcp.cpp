@@ -1184,9 +1184,12 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         o.useGpu = useGpu;
         o.connectPipeline = pipeline;
         o.connectInPlace = gArgs.GetBoolArg("-connectinplace", o.connectInPlace);
-        // -ibdab: alternate in-place (odd runs) and merged-view (even runs) connects, for an
-        // interleaved A/B in one process over one fixture
-        if (gArgs.GetBoolArg("-ibdab", false)) o.connectInPlace = iters % 2 == 1;
+        o.connectLookahead = gArgs.GetBoolArg("-connectlookahead", o.connectLookahead);
+        // -ibdab=inplace|lookahead: alternate that option on (odd runs) and off (even runs), for
+        // an interleaved A/B in one process over one fixture
+        const std::string ab = gArgs.GetArg("-ibdab", "");
+        if (ab == "inplace") o.connectInPlace = iters % 2 == 1;
+        if (ab == "lookahead") o.connectLookahead = iters % 2 == 1;
         o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)std::min(16, std::max(2, GetNumCores())));
         o.parallelUtxoMinTx = (size_t)gArgs.GetArg("-parallelutxo", (int64_t)o.parallelUtxoMinTx);
         Chainstate cs(Params(), o);
@@ -1229,9 +1232,11 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
                     ms(Chainstate::PH_SCRIPTS), ms(Chainstate::PH_BATCH), ms(Chainstate::PH_UNDO), ms(Chainstate::PH_TIP_FLUSH),
                     ms(Chainstate::PH_TIP_WRITE), ms(Chainstate::PH_TIP_POST),
                     (unsigned long long)cs.RecentBlockHits(), (unsigned long long)cs.RecentBlockMisses());
-            fprintf(stderr, "# ibd fast-utxo sub-phases (ms/block): setup %.2f checks %.2f undo %.2f apply %.2f\n",
+            fprintf(stderr, "# ibd fast-utxo sub-phases (ms/block): setup %.2f checks %.2f undo %.2f apply %.2f; "
+                    "lookahead wait %.2f, adopted by %lld of %zu blocks\n",
                     ms(Chainstate::PH_FU_SETUP), ms(Chainstate::PH_FU_CHECKS), ms(Chainstate::PH_FU_UNDO),
-                    ms(Chainstate::PH_FU_APPLY));
+                    ms(Chainstate::PH_FU_APPLY), ms(Chainstate::PH_LA_WAIT),
+                    (long long)(cs.ConnectPhaseMicros(Chainstate::PH_LA_USED) - ph0[Chainstate::PH_LA_USED]), f.run.size());
         }
         if (cs.HeightNow() != f.run.size() + f.setup.size()) {
             fprintf(stderr, "IBD run ended at height %d\n", cs.HeightNow());
@@ -1250,8 +1255,8 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         }
         totalMs += (t1 - t0) / 1000.0;
         iters++;
-        printf("{\"bench\": \"IbdPipelineRun\", \"gpu\": %s, \"pipeline\": %d, \"in_place\": %s, \"iter\": %d, \"ms_per_block\": %.2f}\n",
-               useGpu ? "true" : "false", pipeline, o.connectInPlace ? "true" : "false", iters, (t1 - t0) / 1000.0 / f.run.size());
+        printf("{\"bench\": \"IbdPipelineRun\", \"gpu\": %s, \"pipeline\": %d, \"in_place\": %s, \"lookahead\": %s, \"iter\": %d, \"ms_per_block\": %.2f}\n",
+               useGpu ? "true" : "false", pipeline, o.connectInPlace ? "true" : "false", o.connectLookahead ? "true" : "false", iters, (t1 - t0) / 1000.0 / f.run.size());
         fflush(stdout);
         const std::string cmd = std::string("rm -rf '") + tmpl + "'";
         if (system(cmd.c_str()) != 0) {}
