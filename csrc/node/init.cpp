@@ -107,9 +107,6 @@ std::string HelpMessage() {
         {"-logips", "Include IP addresses in debug output (default: 0)"},
         {"-shrinkdebugfile", "Shrink debug.log file on client startup (default: 1)"},
         {"-fastprune", "Use 64 KiB block files (regtest only; for pruning tests)"},
-        {"-connectpipeline=<n>", "Blocks in flight when connecting several in a row: block N+1's UTXO pass overlaps "
-                                 "block N's signature batch (default: 1, one block at a time; measured faster since the "
-                                 "signature batch takes 2 ms, profiles/connect_r5.md)"},
         {"-blockcachemb=<n>", "Keep blocks accepted out of order in memory until they connect, up to <n> MiB "
                               "(decoded in-memory size, several times the serialized size; default: 512; 0 reads them back "
                               "from disk like the reference)"},

@@ -31,7 +31,6 @@ std::unique_ptr<NodeContext> BuildNode(const std::string& chain, const std::stri
     o.coinsCacheBytes = (size_t)gArgs.GetArg("-dbcache", (int64_t)450) << 20;
     o.scriptThreads = (int)gArgs.GetArg("-par", (int64_t)0);
     o.maxTipAge = gArgs.GetArg("-maxtipage", DEFAULT_MAX_TIP_AGE);
-    o.connectPipeline = (int)gArgs.GetArg("-connectpipeline", (int64_t)o.connectPipeline);
     o.parallelUtxoMinTx = (size_t)std::max<int64_t>(0, gArgs.GetArg("-parallelutxo", (int64_t)o.parallelUtxoMinTx));
     o.connectInPlace = gArgs.GetBoolArg("-connectinplace", o.connectInPlace);
     o.connectLookahead = gArgs.GetBoolArg("-connectlookahead", o.connectLookahead);

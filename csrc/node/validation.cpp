@@ -839,8 +839,7 @@ struct Chainstate::PendingConnect {
     CBlockIndex* pindex = nullptr;
     bool genesis = false, postfork = false;
     size_t nJobs = 0;               // script jobs run for this block
-    bool sigsOk = true;             // verdict when the batch ran synchronously (or scripts failed)
-    std::future<bool> sigs;         // verdict of an asynchronous batch
+    bool sigsOk = true;             // the batch's verdict (false too when scripts failed)
     CBlockUndo blockundo;
     std::vector<std::pair<uint256, CDiskTxPos>> vPos;
     int64_t nTimeStart = 0, nTime2 = 0;
@@ -985,7 +984,7 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
     p.directTip = fJustCheck ? nullptr : directTip;
     bool ok = false;
     try {
-        ok = ConnectBlockPrepare(block, state, pindex, view, fJustCheck, false, p) && ConnectBlockFinish(p, state, fJustCheck);
+        ok = ConnectBlockPrepare(block, state, pindex, view, fJustCheck, p) && ConnectBlockFinish(p, state, fJustCheck);
     } catch (...) {
         JoinLookahead();
         lookahead.reset();
@@ -1009,11 +1008,10 @@ bool Chainstate::ConnectBlock(const CBlock& block, CValidationState& state, CBlo
 }
 
 // Phase 1 of connecting a block: every consensus check that needs the UTXO view, the script
-// runs (ECDSA deferred), and the block's signature batch started - synchronously, or (`async`)
-// on a helper thread so the caller can go on with the next block. The view is fully updated
-// (best block included) when this returns; the block is valid only once Finish agrees.
+// runs (ECDSA deferred) and the block's signature batch. The view (or, in place, the tip) is
+// fully updated when this returns; the block is valid only once Finish agrees.
 bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& state, CBlockIndex* pindex,
-                                     CCoinsViewCache& view, bool fJustCheck, bool async, PendingConnect& p) {
+                                     CCoinsViewCache& view, bool fJustCheck, PendingConnect& p) {
     JoinLookahead(); // normally closed already (ConnectBlock joins it after the previous block)
     const int64_t nTimeStart = GetTimeMicros();
     p.pindex = pindex;
@@ -1518,16 +1516,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 },
                 512);
             phase(PH_COLLECT);
-            if (async) {
-                // the batch owns the sinks (moving the outer vector keeps every check in place);
-                // the pool is shared (ParallelFor calls serialise)
-                WorkerPool* wp = pool.get();
-                const bool useGpu = opts.useGpu, erase = !fJustCheck;
-                p.sigs = std::async(std::launch::async, [wp, useGpu, erase, sinks = std::move(sinks), all = std::move(all),
-                                                         groups = std::move(groups)]() mutable {
-                    return BatchVerifySignatures(all, groups, wp, useGpu, false, erase);
-                });
-            } else {
+            {
                 // While the GPU checks the signatures the CPU is idle: the undo record is
                 // serialised and checksummed meanwhile (written once the verdict is in)
                 if (!fJustCheck && pindex->GetUndoPos().IsNull() && ntx >= 1024 && GpuBatchesExpected(opts.useGpu)) {
@@ -1551,7 +1540,6 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         }
         p.sigsOk = ok;
     }
-    // the next block of a pipeline layers its view on this one
     if (!fJustCheck) view.SetBestBlock(pindex->GetBlockHash());
     // a big block leaves ~100k heap objects in these: freed on the reaper thread
     if (ntx >= 1024) {
@@ -1569,8 +1557,7 @@ bool Chainstate::ConnectBlockFinish(PendingConnect& p, CValidationState& state, 
     if (p.genesis) return true;
     CBlockIndex* pindex = p.pindex;
     const CBlockUndo& blockundo = p.blockundo;
-    bool ok = p.sigsOk;
-    if (p.sigs.valid()) ok = p.sigs.get() && ok;
+    const bool ok = p.sigsOk;
     // Before the fork script failures do not invalidate blocks (reference validation.cpp:2121-2126:
     // control.Wait() is ignored below BCPHeight; the checks always go through the queue control,
     // :2010-2011 and :2080-2087, whatever -par says, so this holds for every thread count).
@@ -1945,114 +1932,6 @@ bool Chainstate::ConnectTip(CValidationState& state, CBlockIndex* pindexNew, con
     return true;
 }
 
-// Cross-block pipeline (SURVEY §2.3 PP; the reference connects strictly one block at a time,
-// src/validation.cpp:2698-2746): block N+1's UTXO pass and script runs (CPU) overlap block N's
-// ECDSA batch (GPU). Each block gets a view layered on the previous block's; a block is
-// committed - view flushed into the coins tip, undo written, tip advanced - only after its own
-// verdict, in order. A failed verdict discards that block's view and every later one, exactly
-// as if the blocks had been connected one by one and the failing one had been rejected.
-bool Chainstate::ConnectTipsPipelined(CValidationState& state, const std::vector<CBlockIndex*>& chain,
-                                      const std::shared_ptr<const CBlock>& pblock, ConnectTrace& trace) {
-    struct Stage {
-        CBlockIndex* pindex;
-        std::shared_ptr<const CBlock> block;
-        std::unique_ptr<CCoinsViewCache> view;
-        std::unique_ptr<PendingConnect> p;
-    };
-    std::deque<Stage> inflight;
-    const size_t depth = (size_t)std::max(2, opts.connectPipeline);
-    LogPrint(BCLog::BENCH, "ConnectTipsPipelined: %u blocks, up to %u in flight\n", (unsigned)chain.size(), (unsigned)depth);
-    // the oldest in-flight block: verdict, then commit (or discard it and everything after it)
-    auto commitFront = [&]() -> bool {
-        AssertLockHeld(cs_main); // runs inside this function's cs_main scope
-        Stage& s = inflight.front();
-        const int64_t tc0 = GetTimeMicros();
-        const bool rv = ConnectBlockFinish(*s.p, state, false);
-        phaseMicros[PH_TIP_CONNECT].fetch_add(GetTimeMicros() - tc0, std::memory_order_relaxed);
-        GetMainSignals().BlockChecked(*s.block, state);
-        if (!rv) {
-            if (state.IsInvalid()) InvalidBlockFound(s.pindex, state);
-            for (size_t k = 0; k < inflight.size(); k++) trace.blocksConnected.pop_back();
-            // later stages' batches may still run: their results are dropped with them
-            inflight.clear();
-            return error("ConnectTipsPipelined(): block %s failed (%s)", s.pindex->GetBlockHash().ToString().c_str(),
-                         FormatStateMessage(state).c_str());
-        }
-        const int64_t tf0 = GetTimeMicros();
-        s.view->Flush(); // into the coins tip: everything older is committed already
-        if (inflight.size() > 1) inflight[1].view->SetBackend(*pcoinsTip);
-        const int64_t tf1 = GetTimeMicros();
-        if (mempool) mempool->removeForBlock(s.block->vtx, s.pindex->nHeight);
-        UpdateTip(s.pindex);
-        // the block's undo records (21k+ vectors for a big block) and its emptied view are freed
-        // on the reaper thread, as ConnectBlock does for the one-at-a-time path
-        Reaper::Get().Drop(std::move(s.p->blockundo));
-        Reaper::Get().Drop(std::move(s.view));
-        inflight.pop_front();
-        const int64_t tf2 = GetTimeMicros();
-        CValidationState fs;
-        const bool flushed = FlushStateToDisk(fs, FLUSH_STATE_IF_NEEDED);
-        phaseMicros[PH_TIP_FLUSH].fetch_add(tf1 - tf0, std::memory_order_relaxed);
-        phaseMicros[PH_TIP_POST].fetch_add(tf2 - tf1, std::memory_order_relaxed);
-        phaseMicros[PH_TIP_WRITE].fetch_add(GetTimeMicros() - tf2, std::memory_order_relaxed);
-        if (!flushed) {
-            state = fs;
-            for (size_t k = 0; k < inflight.size(); k++) trace.blocksConnected.pop_back();
-            inflight.clear();
-            return false;
-        }
-        return true;
-    };
-    for (CBlockIndex* pindex : chain) {
-        Stage st;
-        st.pindex = pindex;
-        std::shared_ptr<const CBlock> cached = TakeRecentBlock(pindex->GetBlockHash());
-        if (pblock && pblock->GetHash(params.GetConsensus()) == pindex->GetBlockHash()) {
-            st.block = pblock;
-        } else if (cached) {
-            recentHits.fetch_add(1, std::memory_order_relaxed);
-            st.block = std::move(cached);
-        } else {
-            recentMisses.fetch_add(1, std::memory_order_relaxed);
-            auto b = std::make_shared<CBlock>();
-            const int64_t tr0 = GetTimeMicros();
-            const bool read = ReadBlockFromDisk(*b, pindex, params, true, pool.get());
-            phaseMicros[PH_TIP_READ].fetch_add(GetTimeMicros() - tr0, std::memory_order_relaxed);
-            if (!read) {
-                while (!inflight.empty())
-                    if (!commitFront()) return false;
-                return state.Error("Failed to read block");
-            }
-            st.block = b;
-        }
-        CCoinsView* base = inflight.empty() ? static_cast<CCoinsView*>(pcoinsTip.get()) : inflight.back().view.get();
-        st.view.reset(new CCoinsViewCache(base));
-        st.p.reset(new PendingConnect());
-        trace.blocksConnected.emplace_back(pindex, st.block);
-        const int64_t tp0 = GetTimeMicros();
-        const bool prepared = ConnectBlockPrepare(*st.block, state, pindex, *st.view, false, true, *st.p);
-        phaseMicros[PH_TIP_CONNECT].fetch_add(GetTimeMicros() - tp0, std::memory_order_relaxed);
-        if (!prepared) {
-            // the blocks before it may still be valid: settle them first (in order)
-            CValidationState failed = state;
-            state = CValidationState();
-            trace.blocksConnected.pop_back();
-            while (!inflight.empty())
-                if (!commitFront()) return false;
-            state = failed;
-            GetMainSignals().BlockChecked(*st.block, state);
-            if (state.IsInvalid()) InvalidBlockFound(pindex, state);
-            return error("ConnectTipsPipelined(): ConnectBlock %s failed (%s)", pindex->GetBlockHash().ToString().c_str(),
-                         FormatStateMessage(state).c_str());
-        }
-        inflight.push_back(std::move(st));
-        if (inflight.size() >= depth && !commitFront()) return false;
-    }
-    while (!inflight.empty())
-        if (!commitFront()) return false;
-    return true;
-}
-
 CBlockIndex* Chainstate::FindMostWorkChain() {
     while (true) {
         if (setBlockIndexCandidates.empty()) return nullptr;
@@ -2177,26 +2056,6 @@ bool Chainstate::ActivateBestChainStep(CValidationState& state, CBlockIndex* pin
             pindexIter = pindexIter->pprev;
         }
         nHeight = nTargetHeight;
-        if (opts.connectPipeline > 1 && vpindexToConnect.size() > 1) {
-            // several blocks in a row: connect them through the pipeline, then let the caller
-            // publish the new tip (one step per batch instead of one per block)
-            const std::vector<CBlockIndex*> chain(vpindexToConnect.rbegin(), vpindexToConnect.rend());
-            const int64_t tTip = GetTimeMicros();
-            const bool tipsOk = ConnectTipsPipelined(state, chain, pblock, trace);
-            phaseMicros[PH_ABC_TIP].fetch_add(GetTimeMicros() - tTip, std::memory_order_relaxed);
-            if (!tipsOk) {
-                if (state.IsInvalid()) {
-                    if (!state.CorruptionPossible()) InvalidChainFound(vpindexToConnect.front());
-                    CheckForkWarningConditionsOnNewFork(vpindexToConnect.back());
-                    state = CValidationState();
-                    fInvalidFound = true;
-                    break;
-                }
-                return false;
-            }
-            PruneBlockIndexCandidates();
-            break;
-        }
         for (auto it = vpindexToConnect.rbegin(); it != vpindexToConnect.rend(); ++it) {
             CBlockIndex* pindexConnect = *it;
             const int64_t tTip = GetTimeMicros();

@@ -90,11 +90,6 @@ struct ChainstateOptions {
     uint64_t pruneTarget = 0;       // bytes; 0 = no pruning
     uint256 assumeValid;
     int64_t maxTipAge = DEFAULT_MAX_TIP_AGE;
-    // -connectpipeline: when several blocks connect in a row (IBD, reorgs), block N+1's UTXO pass
-    // runs while block N's signature batch is on the GPU (at most this many blocks in flight;
-    // <= 1 connects one block at a time like the reference, the default: with a 2 ms batch the
-    // layered views cost more than the overlap gains, profiles/connect_r5.md)
-    int connectPipeline = 1;
     // the UTXO pass of a block with at least this many transactions runs in parallel (0: never)
     size_t parallelUtxoMinTx = 64;
     // that pass updates the coins tip in place (undone from the undo records if a later check
@@ -292,11 +287,8 @@ private:
     void FlushBlockFile(bool fFinalize = false);
     struct PendingConnect; // a block between its UTXO pass and its signature verdict
     bool ConnectBlockPrepare(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
-                             bool fJustCheck, bool async, PendingConnect& p) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
+                             bool fJustCheck, PendingConnect& p) EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ConnectBlockFinish(PendingConnect& p, CValidationState& state, bool fJustCheck)
-        EXCLUSIVE_LOCKS_REQUIRED(cs_main);
-    bool ConnectTipsPipelined(CValidationState& state, const std::vector<CBlockIndex*>& chain,
-                              const std::shared_ptr<const CBlock>& pblock, ConnectTrace& trace)
         EXCLUSIVE_LOCKS_REQUIRED(cs_main);
     bool ConnectBlock(const CBlock& block, CValidationState& state, CBlockIndex* pindex, CCoinsViewCache& view,
                       bool fJustCheck = false, CCoinsViewCache* directTip = nullptr) EXCLUSIVE_LOCKS_REQUIRED(cs_main);

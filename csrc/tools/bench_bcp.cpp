@@ -1064,13 +1064,15 @@ BENCHMARK(ConnectBlock8MB_160kSigops_GPU);
 BENCHMARK(ConnectBlock8MB_Multisig_CPU);
 BENCHMARK(ConnectBlock8MB_Multisig_GPU);
 
-// ------------------------------------------------------------------ IBD pipeline
-// IbdPipeline_{Seq,Pipe}_{CPU,GPU}: a fresh node connects -ibdblocks consecutive big blocks
-// (default 50; each ~7.3 MB: 20,000 2-in/2-out P2PKH spends of the previous block's outputs,
-// 40,000 signatures). The blocks arrive last-to-first, so nothing connects until the first one
-// lands and then the whole run connects in ActivateBestChain steps - one block at a time
-// (-connectpipeline=1, "Seq") or with block N+1's UTXO pass overlapping block N's signature
-// batch ("Pipe"). Reported: ms per block (one iteration = the whole run).
+// ------------------------------------------------------------------ IBD
+// IbdPipeline_Seq_{CPU,GPU}: a fresh node connects -ibdblocks consecutive big blocks (default
+// 50; each ~7.3 MB: 20,000 2-in/2-out P2PKH spends of the previous block's outputs, 40,000
+// signatures). The blocks arrive last-to-first, so nothing connects until the first one lands
+// and then the whole run connects in ActivateBestChain steps, one block at a time (with the GPU:
+// each block's UTXO pass in place on the tip, and the next block's read-only pass overlapping
+// its signature batch - -connectinplace, -connectlookahead). Reported: ms per block (one
+// iteration = the whole run). The round-3..5 "Pipe" variant (-connectpipeline, layered per-block
+// views) was removed in round 6: it lost to this path (profiles/connect_r6.md).
 namespace {
 struct IbdFixture {
     std::vector<std::shared_ptr<const CBlock>> setup, run; // setup: to the fork + fan-out; run: timed
@@ -1182,7 +1184,6 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
         if (!mkdtemp(tmpl)) throw std::runtime_error("bench: mkdtemp failed");
         o.datadir = tmpl;
         o.useGpu = useGpu;
-        o.connectPipeline = pipeline;
         o.connectInPlace = gArgs.GetBoolArg("-connectinplace", o.connectInPlace);
         o.connectLookahead = gArgs.GetBoolArg("-connectlookahead", o.connectLookahead);
         // -ibdab=inplace|lookahead: alternate that option on (odd runs) and off (even runs), for
@@ -1268,17 +1269,11 @@ void IbdRun(State& st, bool useGpu, int pipeline) {
 }
 } // namespace
 static void IbdPipeline_Seq_CPU(State& st) { IbdRun(st, false, 1); }
-static void IbdPipeline_Pipe_CPU(State& st) { IbdRun(st, false, 2); }
 static void IbdPipeline_Seq_GPU(State& st) {
     if (gpu::GpuAvailable()) IbdRun(st, true, 1);
 }
-static void IbdPipeline_Pipe_GPU(State& st) {
-    if (gpu::GpuAvailable()) IbdRun(st, true, 2);
-}
 BENCHMARK(IbdPipeline_Seq_CPU);
-BENCHMARK(IbdPipeline_Pipe_CPU);
 BENCHMARK(IbdPipeline_Seq_GPU);
-BENCHMARK(IbdPipeline_Pipe_GPU);
 
 int main(int argc, char* argv[]) {
     gArgs.ParseParameters(argc, argv);
@@ -1286,7 +1281,9 @@ int main(int argc, char* argv[]) {
         printf("Usage: bench_bcp [-filter=<regex>] [-time=<seconds per bench>] [-list] [-datadir=bench/data]\n"
                "                 [-par=<script threads>] [-ibdblocks=<n>] [-kvcoins=<n>] [-kvdbcache=<MiB>]\n"
                "                 [-parallelutxo=<min txs>] [-ecdsaminshard=<signatures>] [-debug=<category>]\n"
-               "                 [-shardplan] (print the GPU verify shard plans for 1, 2 and 8 devices)\n");
+               "                 [-shardplan] (print the GPU verify shard plans for 1, 2 and 8 devices)\n"
+               "                 [-connectinplace=0|1] [-connectlookahead=0|1] [-ibdab=inplace|lookahead]\n"
+               "                 (IBD: alternate one of those options run by run) [-tipcoins=<n>]\n");
         return 0;
     }
     { // default: <dir of the binary>/../bench/data, so the working directory does not matter

@@ -252,3 +252,49 @@ def test_differential_equihash_10k(native, two_lanes, n, k, total):
     diff = [i for i, (a, b) in enumerate(zip(cpu, gpu)) if a != b]
     assert not diff, diff[:5]
     assert 0.05 < sum(cpu) / len(cpu) < 0.6
+
+
+def test_plan_shards_at_block_scale(native):
+    """PlanShards at the 8 MB block's 199,680 signatures (pure, no GPU): four lanes on ONE
+    device take three shards (each >= the 65,536 per-lane floor); eight devices with two lanes
+    each take one shard per device first (>= 4,096 per device)."""
+    n = 199_680
+    plan = native.plan_shards(n, [0, 0, 0, 0], 4096, 65536)
+    assert [(lane, hi - lo) for lane, lo, hi in plan] == [(0, 66560), (1, 66560), (2, 66560)]
+    assert plan[0][1] == 0 and plan[-1][2] == n and all(a[2] == b[1] for a, b in zip(plan, plan[1:]))
+    devs = [d for d in range(8) for _ in range(2)]
+    plan8 = native.plan_shards(n, devs, 4096, 65536)
+    assert sorted({devs[lane] for lane, _, _ in plan8}) == list(range(8))
+    assert sum(hi - lo for _, lo, hi in plan8) == n and len(plan8) == 8
+
+
+@pytest.fixture
+def four_lanes(native):
+    native.gpu_verify_set_devices([0, 0, 0, 0])
+    yield
+    native.gpu_verify_set_devices([])
+
+
+@pytest.mark.gpu
+def test_four_lanes_block_scale_ecdsa_matches_cpu(native, four_lanes):
+    """The node's verify service with four lanes on device 0 at the 199,680-signature shape of an
+    8 MB block (service defaults: 65,536 per extra lane on one device): the batch splits into the
+    planned three shards, each lane that got a shard did its items, and every verdict equals the
+    CPU consensus verifier's. 4,096 distinct signatures (valid, wrong message/key, high-S,
+    garbage DER, ...) are tiled to the full size."""
+    n = 199_680
+    plan = native.gpu_verify_plan(n)
+    assert [hi - lo for _, lo, hi in plan] == [66560, 66560, 66560]
+    uniq, expect = make_items(native, 4096, seed=23)
+    cpu, _ = native.ecdsa_verify_batch(uniq, use_gpu=False)
+    assert cpu == expect
+    items = (uniq * (n // len(uniq) + 1))[:n]
+    want = (cpu * (n // len(cpu) + 1))[:n]
+    before = native.gpu_verify_stats()
+    gpu, _ = native.ecdsa_verify_batch(items, use_gpu=True)  # the node's deferred batch -> the service
+    assert gpu == want
+    st = native.gpu_verify_stats()
+    assert st["sharded_batches"] == before["sharded_batches"] + 1
+    got = [l["items"] for l in st["lanes"]]
+    assert [l["device"] for l in st["lanes"]] == [0, 0, 0, 0]
+    assert sorted(got, reverse=True)[:3] == [66560, 66560, 66560] and sum(got) == n

@@ -22,7 +22,8 @@
 #   ecdsa-cpu TAG        CPU ECDSA / ecmult micro-benches and the CPU 8 MB connect
 #   connect TAG [BLOCKS] 8 MB block connects on the GPU path, parallel vs serial UTXO pass, the IBD pipeline, a kernel profile
 #                        of the 160k-sigop GPU connect
-#   ibd TAG [BLOCKS] [SECS]  IBD runs (sequential and pipelined): per-run ms/block, median/min/max, phase split
+#   ibd TAG [BLOCKS] [SECS]  IBD runs, plus interleaved A/Bs of -connectlookahead and -connectinplace:
+#                            per-run ms/block, median/min/max per configuration, phase split
 #   relay TAG            BIP152 short-id kernel: GPU tests and the CPU vs GPU micro-bench
 #   lanes TAG            verify-service tests, then a 199k-signature and a 2000-header batch over
 #                        lanes [0], [0,0], [0,0,0,0] (sharding overhead) and the host-built-state
@@ -149,20 +150,23 @@ connect)
   timeout -k 10 300 ./bin/bench_bcp -filter='ConnectBlock8MB.*_GPU' -time=4 -parallelutxo=0 > "$O/connect_serial.log" \
     2> "$O/connect_serial.err"
   cat "$O/connect_serial.log"; grep '^#' "$O/connect_serial.err" | tail -n 12
-  timeout -k 10 600 ./bin/bench_bcp -filter='IbdPipeline_(Seq|Pipe)_GPU' -ibdblocks="${3:-50}" -time=0 > "$O/ibd.log" 2> "$O/ibd.err"
+  timeout -k 10 600 ./bin/bench_bcp -filter='IbdPipeline_Seq_GPU' -ibdblocks="${3:-50}" -time=0 > "$O/ibd.log" 2> "$O/ibd.err"
   cat "$O/ibd.log"
   (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof" -o run -- "$R/bin/bench_bcp" \
     -filter='ConnectBlock8MB_160kSigops_GPU' -time=2 > "$O/prof.log" 2>&1) ;;
 ibd)
-  # IBD of -ibdblocks big blocks, sequential and pipelined connects on the GPU path: one fixture,
-  # then as many whole runs as fit in -time seconds; per-run ms/block and the phase split around
-  # ConnectTip (stderr '# ibd' lines), summarised as median / min / max
-  for m in Seq Pipe; do
-    timeout -k 10 900 ./bin/bench_bcp -filter="IbdPipeline_${m}_GPU" -ibdblocks="${3:-50}" -time="${4:-12}" \
-      > "$O/ibd_$m.log" 2> "$O/ibd_$m.err"
+  # IBD of -ibdblocks big blocks on the GPU path: one fixture, then as many whole runs as fit in
+  # -time seconds (default config), then the same with each of the two overlap options alternated
+  # on/off run by run; per-run ms/block and the phase split around ConnectTip (stderr '# ibd'
+  # lines), summarised as median / min / max per configuration
+  timeout -k 10 900 ./bin/bench_bcp -filter="IbdPipeline_Seq_GPU" -ibdblocks="${3:-50}" -time="${4:-12}" \
+    > "$O/ibd_default.log" 2> "$O/ibd_default.err"
+  for ab in lookahead inplace; do
+    timeout -k 10 900 ./bin/bench_bcp -filter="IbdPipeline_Seq_GPU" -ibdblocks="${3:-50}" -time="${4:-12}" -ibdab=$ab \
+      > "$O/ibd_ab_$ab.log" 2> "$O/ibd_ab_$ab.err"
   done
   python3 tools/ibd_summary.py "$O"
-  grep -h '^# ibd GPU' "$O"/ibd_*.err | tail -n 4 ;;
+  grep -h '^# ibd' "$O"/ibd_default.err | tail -n 2 ;;
 relay)
   timeout -k 10 300 python -u -m pytest tests/test_shortid_gpu.py -m gpu -x -v --timeout 120 --timeout-method thread \
     > "$O/pytest.log" 2>&1
