@@ -180,7 +180,11 @@ def run(args, world):
     # several solvers in flight (default two, double-buffered): while the GPU runs batch s, the
     # host decodes batch s-1, and one solver's kernels fill the other's tails
     nsolv = max(1, args.solvers)
+    free0 = torch.cuda.mem_get_info(device)[0]
     solvers = [native.EquihashGpuSolver(200, 9, args.batch, device) for _ in range(nsolv)]
+    torch.cuda.synchronize()
+    # device memory the solvers took (ranks sharing a GPU in the rehearsal overlap here)
+    solver_gib = (free0 - torch.cuda.mem_get_info(device)[0]) / 2**30
     # Template: CEquihashInput of a mainnet-shaped header (108 B), random-ish but fixed.
     header = bytes((i * 37 + 11) & 0xFF for i in range(108))
 
@@ -252,7 +256,18 @@ def run(args, world):
     pairs_lost = sum(sum(sv.stats()["pair_dropped_all"] or [0]) for sv in solvers)
     cands_lost = sum(sv.stats()["cand_dropped"] for sv in solvers)
     total_sols, max_dt, total_bad = aggregate(nsol, dt, nbad, world, red_dev)
+    per_rank = None
     if world > 1:
+        # each rank's nonce lane (the rank id in the nonce's top word, states_for) and its
+        # solution count: the lanes must be disjoint and the counts sum to the job total
+        # row: [nonce top word, first and last low word timed, solutions]
+        mine = torch.tensor([float(rank), 0.0, float(args.steps * args.batch - 1), float(nsol)],
+                            dtype=torch.float64, device=red_dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = [[int(x) for x in t.tolist()] for t in allr]
+        if len({r[0] for r in per_rank}) != world:
+            raise SystemExit(f"bench: nonce lanes overlap across ranks: {per_rank}")
         lost = torch.tensor([rows_lost, pairs_lost, cands_lost], dtype=torch.float64, device=red_dev)
         dist.all_reduce(lost, op=dist.ReduceOp.SUM)
         rows_lost, pairs_lost, cands_lost = (int(x) for x in lost.tolist())
@@ -290,6 +305,8 @@ def run(args, world):
                 "verified": verified,
                 "verified_solutions": int(total_sols) if verified else 0,
                 "gpu_cpu_verifier_disagreements": gpu_cpu_disagree,
+                "per_rank_nonce_lane_range_solutions": per_rank,
+                "solver_device_gib_per_rank": round(solver_gib, 2),
                 "rows_dropped_all_nonces": int(rows_lost),
                 "pairs_dropped_all_nonces": int(pairs_lost),
                 "candidates_dropped_all_nonces": int(cands_lost),
