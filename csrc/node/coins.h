@@ -86,8 +86,10 @@ public:
     bool IsCoinBase() const { return fCoinBase; }
     uint32_t GetHeight() const { return nHeight; }
     const CTxOut& GetTxOut() const { return out; }
+    // the script's heap block, if it has one (scripts of up to 28 bytes live inside the Coin)
     size_t DynamicMemoryUsage() const {
-        return out.scriptPubKey.capacity() ? ((out.scriptPubKey.capacity() + 8 + 15) & ~(size_t)15) : 0;
+        const size_t a = out.scriptPubKey.allocated_memory();
+        return a ? ((a + 8 + 15) & ~(size_t)15) : 0;
     }
 
     template <typename S> void Serialize(S& s) const {

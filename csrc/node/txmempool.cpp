@@ -22,9 +22,9 @@ namespace bcp {
 static size_t TxUsage(const CTransaction& tx) {
     size_t mem = memusage::MallocUsage(sizeof(CTransaction) + 2 * sizeof(long) + sizeof(void*)) +
                  memusage::DynamicUsage(tx.vin) + memusage::DynamicUsage(tx.vout);
-    for (const CTxIn& in : tx.vin) mem += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(in.scriptSig));
+    for (const CTxIn& in : tx.vin) mem += memusage::DynamicUsage(static_cast<const CScriptBase&>(in.scriptSig));
     for (const CTxOut& out : tx.vout)
-        mem += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(out.scriptPubKey));
+        mem += memusage::DynamicUsage(static_cast<const CScriptBase&>(out.scriptPubKey));
     return mem;
 }
 

@@ -712,9 +712,9 @@ static size_t BlockMemoryUsage(const CBlock& block) {
     for (const CTransactionRef& tx : block.vtx) {
         m += memusage::MallocUsage(sizeof(CTransaction) + 16); // object + control block (make_shared)
         m += memusage::DynamicUsage(tx->vin) + memusage::DynamicUsage(tx->vout);
-        for (const CTxIn& in : tx->vin) m += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(in.scriptSig));
+        for (const CTxIn& in : tx->vin) m += memusage::DynamicUsage(static_cast<const CScriptBase&>(in.scriptSig));
         for (const CTxOut& out : tx->vout)
-            m += memusage::DynamicUsage(static_cast<const std::vector<unsigned char>&>(out.scriptPubKey));
+            m += memusage::DynamicUsage(static_cast<const CScriptBase&>(out.scriptPubKey));
     }
     return m;
 }

@@ -5,6 +5,7 @@
 // Design: a small set of free functions dispatching to member Serialize/Unserialize;
 // no READWRITE macro machinery.
 #pragma once
+#include "util/prevector.h"
 #include "crypto/hashes.h"
 #include "primitives/uint256.h"
 
@@ -168,6 +169,26 @@ template <typename S> void Unserialize(S& s, std::string& str) {
     uint64_t n = ReadCompactSize(s);
     str.resize(n);
     if (n) s.read(&str[0], n);
+}
+
+// prevector (script bytes): like a byte vector
+template <typename S, unsigned N, typename T> void Serialize(S& s, const prevector<N, T>& v) {
+    static_assert(sizeof(T) == 1, "byte prevectors only");
+    WriteCompactSize(s, v.size());
+    if (!v.empty()) s.write((const char*)v.data(), v.size());
+}
+template <typename S, unsigned N, typename T> void Unserialize(S& s, prevector<N, T>& v) {
+    static_assert(sizeof(T) == 1, "byte prevectors only");
+    v.clear();
+    const uint64_t n = ReadCompactSize(s);
+    // in chunks, so a lying length prefix cannot force a huge allocation
+    uint64_t i = 0;
+    while (i < n) {
+        const uint64_t blk = std::min<uint64_t>(n - i, 5000000);
+        v.resize((uint32_t)(i + blk));
+        s.read((char*)v.data() + i, blk);
+        i += blk;
+    }
 }
 
 // vectors: byte vectors are raw, others element-wise
@@ -409,6 +430,11 @@ inline uint256 Hash256Concat(const uint256& a, const uint256& b) {
     return Hash256(buf, 64);
 }
 inline uint160 Hash160(const std::vector<unsigned char>& v) {
+    uint160 r;
+    ::bcp::Hash160(v.data(), v.size(), r.begin());
+    return r;
+}
+template <unsigned N> inline uint160 Hash160(const prevector<N, unsigned char>& v) {
     uint160 r;
     ::bcp::Hash160(v.data(), v.size(), r.begin());
     return r;

@@ -781,7 +781,7 @@ uint256 SignatureHash(const CScript& scriptCode, const CTransaction& txTo, unsig
         }
         HashWriter ss;
         ss << txTo.nVersion << hashPrevouts << hashSequence << txTo.vin[nIn].prevout
-           << static_cast<const std::vector<unsigned char>&>(scriptCode) << amount << txTo.vin[nIn].nSequence
+           << static_cast<const CScriptBase&>(scriptCode) << amount << txTo.vin[nIn].nSequence
            << hashOutputs << txTo.nLockTime << nHashType;
         return ss.GetHash();
     }

@@ -4,6 +4,7 @@
 // IsPushOnly, IsUnspendable, IsCommitment for the BCP anti-replay OP_RETURN
 // (script.cpp:316-333)).
 #pragma once
+#include "util/prevector.h"
 #include "primitives/serialize.h"
 
 #include <cstdint>
@@ -100,12 +101,16 @@ private:
     int64_t m_value;
 };
 
-class CScript : public std::vector<unsigned char> {
+// Script bytes: inline up to 28 (every standard output script), on the heap beyond
+// (reference src/script/script.h:371 CScriptBase = prevector<28, unsigned char>)
+typedef prevector<28, unsigned char> CScriptBase;
+
+class CScript : public CScriptBase {
 public:
     CScript() {}
-    CScript(const_iterator b, const_iterator e) : std::vector<unsigned char>(b, e) {}
-    CScript(const unsigned char* b, const unsigned char* e) : std::vector<unsigned char>(b, e) {}
-    explicit CScript(const std::vector<unsigned char>& v) : std::vector<unsigned char>(v) {}
+    CScript(const_iterator b, const_iterator e) : CScriptBase(b, e) {}
+    CScript(std::vector<unsigned char>::const_iterator b, std::vector<unsigned char>::const_iterator e) : CScriptBase(b, e) {}
+    explicit CScript(const std::vector<unsigned char>& v) : CScriptBase(v.begin(), v.end()) {}
     explicit CScript(opcodetype op) { *this << op; }
 
     static opcodetype EncodeOP_N(int n) { return n == 0 ? OP_0 : (opcodetype)(OP_1 + n - 1); }
@@ -137,13 +142,13 @@ public:
     // OP_RETURN <push of exactly `commitment`> (reference script.cpp:316-333).
     bool IsCommitment(const std::vector<unsigned char>& commitment) const;
     bool IsUnspendable() const { return (size() > 0 && *begin() == OP_RETURN) || (size() > MAX_SCRIPT_SIZE); }
-    void clear() { std::vector<unsigned char>::clear(); }
+    void clear() { CScriptBase::clear(); }
     std::string ToString() const;
     // Remove all occurrences of a serialized sub-script (legacy FindAndDelete).
     int FindAndDelete(const CScript& b);
 
-    template <typename S> void Serialize(S& s) const { ::bcp::Serialize(s, (const std::vector<unsigned char>&)*this); }
-    template <typename S> void Unserialize(S& s) { ::bcp::Unserialize(s, (std::vector<unsigned char>&)*this); }
+    template <typename S> void Serialize(S& s) const { ::bcp::Serialize(s, static_cast<const CScriptBase&>(*this)); }
+    template <typename S> void Unserialize(S& s) { ::bcp::Unserialize(s, static_cast<CScriptBase&>(*this)); }
 };
 
 // Parse a script from the human-readable assembler syntax used by the reference's JSON test

@@ -3,6 +3,7 @@
 // hands out, not by element counts: glibc malloc on 64-bit rounds every request plus its
 // 8-byte chunk header up to a 16-byte multiple, with a 32-byte minimum chunk.
 #pragma once
+#include "util/prevector.h"
 #include <cstddef>
 #include <map>
 #include <memory>
@@ -32,6 +33,9 @@ struct stl_hash_node {
     size_t hash;
 };
 
+template <unsigned N, typename X> inline size_t DynamicUsage(const prevector<N, X>& v) {
+    return MallocUsage(v.allocated_memory());
+}
 template <typename X> inline size_t DynamicUsage(const std::vector<X>& v) {
     return MallocUsage(v.capacity() * sizeof(X));
 }
