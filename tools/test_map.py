@@ -15,7 +15,6 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 NOT_PORTED = {
     "create_cache.py": "framework helper (builds the 200-block cache); tests mine their own chains",
     "test_runner.py": "framework runner; pytest runs the suite (`pytest tests -m 'not gpu'`)",
-    "prevector_tests.cpp": "no prevector here: scripts are std::vector based",
     "reverselock_tests.cpp": "no reverse_lock helper here",
     "raii_event_tests.cpp": "libevent RAII wrappers; the HTTP server here does not use libevent",
     "scriptflags.cpp": "helper of script_tests (flag-name parsing), used by tests/test_script.py",
