@@ -1057,6 +1057,47 @@ static void ScriptP2SH101_Deferred(State& st) {
 }
 BENCHMARK(ScriptP2SH101_Deferred);
 
+// One P2PKH input through the interpreter with its CHECKSIG deferred (what each of IBD's 40k
+// script jobs per block does before the batch): sighash, stack, HASH160; no ECDSA
+static void ScriptP2PKH_Deferred(State& st) {
+    CKey key;
+    key.MakeNewKey(true);
+    const CPubKey pub = key.GetPubKey();
+    const CScript spk = GetScriptForDestination(pub.GetID());
+    const uint32_t hashType = SIGHASH_ALL | SIGHASH_FORKID;
+    CMutableTransaction m;
+    m.vin.resize(2);
+    m.vin[0].prevout = COutPoint(uint256S("01"), 0);
+    m.vin[1].prevout = COutPoint(uint256S("02"), 1);
+    m.vout.push_back(CTxOut(1000, spk));
+    m.vout.push_back(CTxOut(1000, spk));
+    const Amount amount = 2000;
+    {
+        const CTransaction u(m);
+        std::vector<unsigned char> sig;
+        key.Sign(SignatureHash(spk, u, 0, hashType, amount), sig);
+        sig.push_back((unsigned char)hashType);
+        m.vin[0].scriptSig = CScript() << sig << std::vector<unsigned char>(pub.begin(), pub.end());
+    }
+    const CTransaction tx(m);
+    const PrecomputedTransactionData txdata(tx);
+    const uint32_t flags = MANDATORY_SCRIPT_VERIFY_FLAGS | SCRIPT_VERIFY_DERSIG;
+    std::vector<DeferredSigCheck> sink;
+    sink.reserve(1 << 16);
+    while (st.KeepRunning()) {
+        sink.clear();
+        for (int r = 0; r < 1000; r++) {
+            DeferringSignatureChecker chk(&tx, 0, amount, &txdata, &sink);
+            ScriptError err;
+            if (!VerifyScript(tx.vin[0].scriptSig, spk, flags, chk, &err)) {
+                fprintf(stderr, "ScriptP2PKH_Deferred: %s\n", ScriptErrorString(err));
+                exit(1);
+            }
+        }
+    }
+}
+BENCHMARK(ScriptP2PKH_Deferred);
+
 BENCHMARK(ConnectBlock8MB_CPU);
 BENCHMARK(ConnectBlock8MB_GPU);
 BENCHMARK(ConnectBlock8MB_160kSigops_CPU);
