@@ -1097,6 +1097,10 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // publishes jobs into a pre-sized array; the script queue's own threads execute them as they
     // appear (sleeping while none are available), deferring every ECDSA check into a per-job sink
     // for the batch verifier. Nothing in the UTXO loop may wait on the queue's threads.
+    // coins of in-block outputs spent within the block (and copies of the view's own coins): the
+    // parallel pass's script jobs read them, so they outlive the script session (declared before
+    // completeOnExit, which closes it)
+    std::vector<Coin> made;
     std::vector<ScriptJob> jobs(maxJobs);
     std::vector<std::vector<DeferredSigCheck>> sinks(maxJobs);
     std::vector<std::vector<DeferredMultisig>> groupSinks(maxJobs); // deferred CHECKMULTISIGs per job
@@ -1188,7 +1192,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         };
         enum : uint8_t { SRC_PREFETCH = 0, SRC_VIEW = 1, SRC_BLOCK = 2 };
         std::vector<const Coin*> coinOf(maxJobs, nullptr);
-        std::vector<Coin> made(maxJobs); // coins of in-block outputs spent within the block
+        made.resize(maxJobs);
         std::vector<uint8_t> src(maxJobs, SRC_PREFETCH);
         std::vector<uint64_t> txSigOps(ntx, 0);
         std::vector<Amount> txFee(ntx, 0);
@@ -1284,9 +1288,43 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         if (!bad.load()) {
             fastDone = true;
             phaseMicros[PH_FASTUTXO].fetch_add(1, std::memory_order_relaxed);
-            // undo records (the spent coins, moved into place) and script-cache probes
-            blockundo.vtxundo.resize(ntx - 1);
+            // Script jobs first, so the scripts run under the rest of the pass: each job reads its
+            // spent coin where the checks found it (the prefetched copy, or `made` for an output of
+            // this block and for a copy of a coin the view holds, which the updates below change)
             std::vector<uint8_t> needScripts(ntx, 0);
+            pool->ParallelFor(
+                (ntx + TCHUNK - 1) / TCHUNK,
+                [&](size_t chunk) {
+                    for (size_t i = std::max<size_t>(1, chunk * TCHUNK); i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
+                        needScripts[i] = fScriptChecks && !(scMayHold && sc.Has(scKeys[i], !fJustCheck));
+                        for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++)
+                            if (src[k] == SRC_VIEW) {
+                                made[k] = *coinOf[k];
+                                coinOf[k] = &made[k];
+                            }
+                    }
+                },
+                1);
+            std::vector<size_t> jobOff(ntx + 1, 0);
+            for (size_t i = 0; i < ntx; i++) jobOff[i + 1] = jobOff[i] + (needScripts[i] ? block.vtx[i]->vin.size() : 0);
+            pool->ParallelFor(
+                ntx,
+                [&](size_t i) {
+                    if (!needScripts[i]) return;
+                    const CTransaction& tx = *block.vtx[i];
+                    for (size_t j = 0; j < tx.vin.size(); j++) {
+                        const CTxOut& out = coinOf[firstInput[i] + j]->GetTxOut();
+                        jobs[jobOff[i] + j] = ScriptJob{&tx, (unsigned)j, &out.scriptPubKey, out.nValue, txdatas[i].get()};
+                    }
+                },
+                64);
+            nProduced = jobOff[ntx];
+            if (queued && nProduced > 0) {
+                scriptQueue->Publish(nProduced);
+                nPublished = nProduced;
+            }
+            // undo records (copies of the spent coins: the scripts are reading the originals)
+            blockundo.vtxundo.resize(ntx - 1);
             std::vector<Coin> newCoins(nOutputs); // the block's outputs that stay unspent, built here
             std::vector<uint8_t> inShard(maxJobs), outShard(nOutputs); // CCoinsMap::ShardOf of each
             pool->ParallelFor(
@@ -1296,13 +1334,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                         const CTransaction& tx = *block.vtx[i];
                         CTxUndo& undo = blockundo.vtxundo[i - 1];
                         undo.vprevout.resize(tx.vin.size());
-                        for (size_t j = 0; j < tx.vin.size(); j++) {
-                            const size_t k = firstInput[i] + j;
-                            if (src[k] == SRC_PREFETCH) undo.vprevout[j] = std::move(prefetched[k]);
-                            else if (src[k] == SRC_BLOCK) undo.vprevout[j] = std::move(made[k]);
-                            else undo.vprevout[j] = *coinOf[k];
-                        }
-                        needScripts[i] = fScriptChecks && !(scMayHold && sc.Has(scKeys[i], !fJustCheck));
+                        for (size_t j = 0; j < tx.vin.size(); j++) undo.vprevout[j] = *coinOf[firstInput[i] + j];
                     }
                     for (size_t i = chunk * TCHUNK; i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
                         const CTransaction& tx = *block.vtx[i];
@@ -1317,28 +1349,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                     }
                 },
                 1);
-            // script jobs (the spent coins are read from the undo records, whose addresses are
-            // fixed from here on), then the scripts start while the view is updated
-            std::vector<size_t> jobOff(ntx + 1, 0);
-            for (size_t i = 0; i < ntx; i++) jobOff[i + 1] = jobOff[i] + (needScripts[i] ? block.vtx[i]->vin.size() : 0);
-            pool->ParallelFor(
-                ntx,
-                [&](size_t i) {
-                    if (!needScripts[i]) return;
-                    const CTransaction& tx = *block.vtx[i];
-                    const CTxUndo& undo = blockundo.vtxundo[i - 1];
-                    for (size_t j = 0; j < tx.vin.size(); j++) {
-                        const CTxOut& out = undo.vprevout[j].GetTxOut();
-                        jobs[jobOff[i] + j] = ScriptJob{&tx, (unsigned)j, &out.scriptPubKey, out.nValue, txdatas[i].get()};
-                    }
-                },
-                64);
-            nProduced = jobOff[ntx];
             sub(PH_FU_UNDO);
-            if (queued && nProduced > 0) {
-                scriptQueue->Publish(nProduced);
-                nPublished = nProduced;
-            }
             for (size_t i = 0; i < ntx; i++) {
                 nInputs += (int)block.vtx[i]->vin.size();
                 nFees += txFee[i];
