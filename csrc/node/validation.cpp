@@ -1370,6 +1370,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                         for (size_t k = 0; k < maxJobs; k++) {
                             if (inShard[k] != sh) continue;
                             const COutPoint& op = prevoutOf(k);
+                            if (src[k] == SRC_BLOCK) continue; // created and spent inside the block: no entry
                             if (tip) tip->SpendPeeked(op);
                             else if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(op);
                             else if (src[k] == SRC_VIEW && !view.SpendCoin(op)) throw std::runtime_error("view spend failed");

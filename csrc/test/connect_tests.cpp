@@ -157,6 +157,12 @@ TEST_CASE(connectblock_tests, parallel_pass_matches_serial) {
     CHECK(cb.find(strprintf("/%d/1/", h)) != std::string::npos);
     const std::string last = parallel.at(COutPoint(CTransaction(txs.back()).GetHash(), 0).ToString());
     CHECK(last.find(strprintf("/%d/0/", h)) != std::string::npos);
+    {
+        // the in-place update leaves no tip entry at all for an output created and spent inside
+        // the block (as AddCoin + SpendCoin of a FRESH entry would not)
+        std::lock_guard<CCriticalSection> l(cs.cs());
+        for (uint32_t i = 0; i < 35; i++) CHECK(cs.CoinsTip().FindInCache(COutPoint(children[2 * i].GetHash(), 0)) == nullptr);
+    }
 
     // disconnecting with the parallel pass's undo data restores every spent coin exactly
     CBlockIndex* pindex = cs.LookupBlockIndex(blk.GetHash());
