@@ -1323,32 +1323,40 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                 scriptQueue->Publish(nProduced);
                 nPublished = nProduced;
             }
-            // undo records (copies of the spent coins: the scripts are reading the originals)
-            blockundo.vtxundo.resize(ntx - 1);
-            std::vector<Coin> newCoins(nOutputs); // the block's outputs that stay unspent, built here
-            std::vector<uint8_t> inShard(maxJobs), outShard(nOutputs); // CCoinsMap::ShardOf of each
-            pool->ParallelFor(
-                (ntx + TCHUNK - 1) / TCHUNK,
-                [&](size_t chunk) {
-                    for (size_t i = std::max<size_t>(1, chunk * TCHUNK); i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
-                        const CTransaction& tx = *block.vtx[i];
-                        CTxUndo& undo = blockundo.vtxundo[i - 1];
-                        undo.vprevout.resize(tx.vin.size());
-                        for (size_t j = 0; j < tx.vin.size(); j++) undo.vprevout[j] = *coinOf[firstInput[i] + j];
-                    }
-                    for (size_t i = chunk * TCHUNK; i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
-                        const CTransaction& tx = *block.vtx[i];
-                        for (size_t j = 0; i > 0 && j < tx.vin.size(); j++)
-                            inShard[firstInput[i] + j] = (uint8_t)CCoinsMap::ShardOf(tx.vin[j].prevout);
-                        for (size_t o = 0; o < tx.vout.size(); o++)
-                            outShard[firstOutput[i] + o] = (uint8_t)CCoinsMap::ShardOf(COutPoint(tx.GetHash(), (uint32_t)o));
-                        for (size_t o = 0; o < tx.vout.size(); o++)
-                            if (!outSpent[firstOutput[i] + o].load(std::memory_order_relaxed) &&
-                                !tx.vout[o].scriptPubKey.IsUnspendable())
-                                newCoins[firstOutput[i] + o] = Coin(tx.vout[o], pindex->nHeight, i == 0);
-                    }
-                },
-                1);
+            // A check-only connect (TestBlockValidity) discards its view and writes no undo record:
+            // the verdict needs neither, so the records and the view updates are skipped (the
+            // checks above already resolved every input, spends inside the block included).
+            // Otherwise: undo records (copies of the spent coins: the scripts read the originals)
+            std::vector<Coin> newCoins; // the block's outputs that stay unspent, built here
+            std::vector<uint8_t> inShard, outShard; // CCoinsMap::ShardOf of each input / output
+            if (!fJustCheck) {
+                blockundo.vtxundo.resize(ntx - 1);
+                newCoins.resize(nOutputs);
+                inShard.resize(maxJobs);
+                outShard.resize(nOutputs);
+                pool->ParallelFor(
+                    (ntx + TCHUNK - 1) / TCHUNK,
+                    [&](size_t chunk) {
+                        for (size_t i = std::max<size_t>(1, chunk * TCHUNK); i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
+                            const CTransaction& tx = *block.vtx[i];
+                            CTxUndo& undo = blockundo.vtxundo[i - 1];
+                            undo.vprevout.resize(tx.vin.size());
+                            for (size_t j = 0; j < tx.vin.size(); j++) undo.vprevout[j] = *coinOf[firstInput[i] + j];
+                        }
+                        for (size_t i = chunk * TCHUNK; i < std::min(ntx, (chunk + 1) * TCHUNK); i++) {
+                            const CTransaction& tx = *block.vtx[i];
+                            for (size_t j = 0; i > 0 && j < tx.vin.size(); j++)
+                                inShard[firstInput[i] + j] = (uint8_t)CCoinsMap::ShardOf(tx.vin[j].prevout);
+                            for (size_t o = 0; o < tx.vout.size(); o++)
+                                outShard[firstOutput[i] + o] = (uint8_t)CCoinsMap::ShardOf(COutPoint(tx.GetHash(), (uint32_t)o));
+                            for (size_t o = 0; o < tx.vout.size(); o++)
+                                if (!outSpent[firstOutput[i] + o].load(std::memory_order_relaxed) &&
+                                    !tx.vout[o].scriptPubKey.IsUnspendable())
+                                    newCoins[firstOutput[i] + o] = Coin(tx.vout[o], pindex->nHeight, i == 0);
+                        }
+                    },
+                    1);
+            }
             sub(PH_FU_UNDO);
             for (size_t i = 0; i < ntx; i++) {
                 nInputs += (int)block.vtx[i]->vin.size();
@@ -1360,35 +1368,37 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             // The view updates (or the tip's), one coins-map shard per task (CCoinsMap): spends of
             // fetched coins and of the view's own coins, then the block's outputs that stay
             // unspent. The scripts published above run meanwhile; nothing they read is in the view.
-            if (!tip) view.Reserve(view.GetCacheSize() + maxJobs + nOutputs);
-            p.tipApplied = tip != nullptr;
             std::string applyError;
             std::mutex applyMu;
-            target.ForEachShard(
-                [&](unsigned sh) {
-                    try {
-                        for (size_t k = 0; k < maxJobs; k++) {
-                            if (inShard[k] != sh) continue;
-                            const COutPoint& op = prevoutOf(k);
-                            if (src[k] == SRC_BLOCK) continue; // created and spent inside the block: no entry
-                            if (tip) tip->SpendPeeked(op);
-                            else if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(op);
-                            else if (src[k] == SRC_VIEW && !view.SpendCoin(op)) throw std::runtime_error("view spend failed");
-                        }
-                        for (size_t i = 0; i < ntx; i++) {
-                            const CTransaction& tx = *block.vtx[i];
-                            for (size_t o = 0; o < tx.vout.size(); o++) {
-                                const size_t q = firstOutput[i] + o;
-                                if (outShard[q] == sh && !newCoins[q].IsSpent())
-                                    target.AddCoin(COutPoint(tx.GetHash(), (uint32_t)o), std::move(newCoins[q]), i == 0);
+            if (!fJustCheck) {
+                if (!tip) view.Reserve(view.GetCacheSize() + maxJobs + nOutputs);
+                p.tipApplied = tip != nullptr;
+                target.ForEachShard(
+                    [&](unsigned sh) {
+                        try {
+                            for (size_t k = 0; k < maxJobs; k++) {
+                                if (inShard[k] != sh) continue;
+                                const COutPoint& op = prevoutOf(k);
+                                if (src[k] == SRC_BLOCK) continue; // created and spent inside the block: no entry
+                                if (tip) tip->SpendPeeked(op);
+                                else if (src[k] == SRC_PREFETCH) view.SpendFetchedMoved(op);
+                                else if (src[k] == SRC_VIEW && !view.SpendCoin(op)) throw std::runtime_error("view spend failed");
                             }
+                            for (size_t i = 0; i < ntx; i++) {
+                                const CTransaction& tx = *block.vtx[i];
+                                for (size_t o = 0; o < tx.vout.size(); o++) {
+                                    const size_t q = firstOutput[i] + o;
+                                    if (outShard[q] == sh && !newCoins[q].IsSpent())
+                                        target.AddCoin(COutPoint(tx.GetHash(), (uint32_t)o), std::move(newCoins[q]), i == 0);
+                                }
+                            }
+                        } catch (const std::exception& e) {
+                            std::lock_guard<std::mutex> l(applyMu);
+                            applyError = e.what();
                         }
-                    } catch (const std::exception& e) {
-                        std::lock_guard<std::mutex> l(applyMu);
-                        applyError = e.what();
-                    }
-                },
-                pool.get());
+                    },
+                    pool.get());
+            }
             sub(PH_FU_APPLY);
             if (!applyError.empty()) return state.Error("ConnectBlock: " + applyError);
         }
