@@ -432,8 +432,7 @@ bool EvalScript(std::vector<valtype>& stack, const CScript& script, uint32_t fla
                 } break;
                 case OP_DUP: {
                     if (stack.size() < 1) return set_error(serror, SCRIPT_ERR_INVALID_STACK_OPERATION);
-                    valtype v = stacktop(stack, -1);
-                    stack.push_back(v);
+                    stack.push_back(stacktop(stack, -1)); // push_back copies an aliased element safely
                 } break;
                 case OP_NIP: {
                     if (stack.size() < 2) return set_error(serror, SCRIPT_ERR_INVALID_STACK_OPERATION);
@@ -559,8 +558,7 @@ bool EvalScript(std::vector<valtype>& stack, const CScript& script, uint32_t fla
                     else if (opcode == OP_SHA256) CSHA256().Write(vch.data(), vch.size()).Finalize(vchHash.data());
                     else if (opcode == OP_HASH160) Hash160(vch.data(), vch.size(), vchHash.data());
                     else Sha256d(vch.data(), vch.size(), vchHash.data());
-                    popstack(stack);
-                    stack.push_back(vchHash);
+                    vch.swap(vchHash); // the digest replaces the top element in place
                 } break;
 
                 case OP_CODESEPARATOR:
@@ -939,12 +937,15 @@ bool VerifyScript(const CScript& scriptSig, const CScript& scriptPubKey, uint32_
         return set_error(serror, SCRIPT_ERR_SIG_PUSHONLY);
 
     std::vector<valtype> stack, stackCopy;
+    stack.reserve(8); // P2PKH / multisig / P2SH spends stay within it: no regrowth while evaluating
     if (!EvalScript(stack, scriptSig, flags, checker, serror)) return false;
-    if (flags & SCRIPT_VERIFY_P2SH) stackCopy = stack;
+    // the copy is only read for a P2SH output (below); the reference copies for every output
+    const bool p2sh = (flags & SCRIPT_VERIFY_P2SH) && scriptPubKey.IsPayToScriptHash();
+    if (p2sh) stackCopy = stack;
     if (!EvalScript(stack, scriptPubKey, flags, checker, serror)) return false;
     if (stack.empty() || !CastToBool(stack.back())) return set_error(serror, SCRIPT_ERR_EVAL_FALSE);
 
-    if ((flags & SCRIPT_VERIFY_P2SH) && scriptPubKey.IsPayToScriptHash()) {
+    if (p2sh) {
         if (!scriptSig.IsPushOnly()) return set_error(serror, SCRIPT_ERR_SIG_PUSHONLY);
         std::swap(stack, stackCopy);
         // non-empty: HASH160 <h> EQUAL over an empty stack would have failed above
