@@ -1100,7 +1100,9 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     // coins of in-block outputs spent within the block (and copies of the view's own coins): the
     // parallel pass's script jobs read them, so they outlive the script session (declared before
     // completeOnExit, which closes it)
-    std::vector<Coin> made;
+    // (one deque per chunk of transactions: stable addresses, filled only for the rare inputs
+    // that need one, no per-input array to construct)
+    std::vector<std::deque<Coin>> made;
     std::vector<ScriptJob> jobs(maxJobs);
     std::vector<std::vector<DeferredSigCheck>> sinks(maxJobs);
     std::vector<std::vector<DeferredMultisig>> groupSinks(maxJobs); // deferred CHECKMULTISIGs per job
@@ -1192,13 +1194,13 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
         };
         enum : uint8_t { SRC_PREFETCH = 0, SRC_VIEW = 1, SRC_BLOCK = 2 };
         std::vector<const Coin*> coinOf(maxJobs, nullptr);
-        made.resize(maxJobs);
+        const size_t TCHUNK = 32; // transactions per task of the parallel pass
+        made.resize((ntx + TCHUNK - 1) / TCHUNK);
         std::vector<uint8_t> src(maxJobs, SRC_PREFETCH);
         std::vector<uint64_t> txSigOps(ntx, 0);
         std::vector<Amount> txFee(ntx, 0);
         std::atomic<bool> bad{false};
         txSigOps[0] = legacySigOps[0];
-        const size_t TCHUNK = 32;
         sub(PH_FU_SETUP);
         pool->ParallelFor(
             (ntx + TCHUNK - 1) / TCHUNK,
@@ -1221,8 +1223,8 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                             if (t >= (int)i || op.n >= ptx.vout.size() || ptx.vout[op.n].scriptPubKey.IsUnspendable()) {
                                 ok = false;
                             } else {
-                                made[k] = Coin(ptx.vout[op.n], pindex->nHeight, t == 0);
-                                c = &made[k];
+                                made[chunk].emplace_back(ptx.vout[op.n], pindex->nHeight, t == 0);
+                                c = &made[chunk].back();
                                 src[k] = SRC_BLOCK;
                                 outSpent[firstOutput[t] + op.n].store(1, std::memory_order_relaxed);
                             }
@@ -1299,8 +1301,8 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
                         needScripts[i] = fScriptChecks && !(scMayHold && sc.Has(scKeys[i], !fJustCheck));
                         for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++)
                             if (src[k] == SRC_VIEW) {
-                                made[k] = *coinOf[k];
-                                coinOf[k] = &made[k];
+                                made[chunk].push_back(*coinOf[k]);
+                                coinOf[k] = &made[chunk].back();
                             }
                     }
                 },
