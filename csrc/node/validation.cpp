@@ -123,6 +123,43 @@ struct Chainstate::BlockPrefetch {
         prefetchedFound.reset(new uint8_t[maxJobs + 1]);
     }
     size_t Chunks() const { return (ntx + CHUNK - 1) / CHUNK; }
+    // Jobs: 0 is Setup, 1.. are the chunks (ParallelFor / script-queue index)
+    size_t Jobs() const { return Chunks() + 1; }
+    void Job(size_t k, ScriptCache& sc) {
+        if (k == 0) Setup();
+        else Chunk(k - 1, sc);
+    }
+
+    // The parallel UTXO pass's per-block tables, built beside the chunks: the block-local txid
+    // index (open addressing; CheckBlock refused duplicate txids), each transaction's first
+    // output, each input's transaction, and the zeroed scratch of the in-block spend tracking.
+    size_t tcap = 0, scap = 0;
+    std::vector<int32_t> tslot;
+    std::vector<size_t> firstOutput, inputTx;
+    std::unique_ptr<std::atomic<uint8_t>[]> outSpent;  // an output spent inside the block
+    std::unique_ptr<std::atomic<uint32_t>[]> spentSet; // concurrent set of spent outpoints
+    void Setup() {
+        const CBlock& blk = *block;
+        tcap = 16;
+        while (tcap < 2 * ntx) tcap <<= 1;
+        tslot.assign(tcap, -1);
+        for (size_t i = 0; i < ntx; i++) {
+            size_t h = ReadLE64(blk.vtx[i]->GetHash().begin()) & (tcap - 1);
+            while (tslot[h] >= 0) h = (h + 1) & (tcap - 1);
+            tslot[h] = (int32_t)i;
+        }
+        firstOutput.assign(ntx + 1, 0);
+        for (size_t i = 0; i < ntx; i++) firstOutput[i + 1] = firstOutput[i] + blk.vtx[i]->vout.size();
+        outSpent.reset(new std::atomic<uint8_t>[nOutputs + 1]);
+        for (size_t o = 0; o <= nOutputs; o++) outSpent[o].store(0, std::memory_order_relaxed);
+        scap = 16;
+        while (scap < 2 * maxJobs) scap <<= 1;
+        spentSet.reset(new std::atomic<uint32_t>[scap]);
+        for (size_t q = 0; q < scap; q++) spentSet[q].store(0, std::memory_order_relaxed);
+        inputTx.resize(maxJobs);
+        for (size_t i = 1; i < ntx; i++)
+            for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++) inputTx[k] = i;
+    }
     void Chunk(size_t chunk, ScriptCache& sc) {
         const CBlock& blk = *block;
         const size_t lo = chunk * CHUNK, hi = std::min(ntx, lo + CHUNK);
@@ -962,8 +999,8 @@ void Chainstate::StartLookahead(const CBlockIndex* pindex) {
     la->pf.Init(*nb, *pcoinsTip, EnforceBIP30For(next), ScriptChecksFor(next), GetScriptCache().MayHold(),
                 GetBlockScriptFlags(next));
     Lookahead* raw = la.get();
-    scriptQueue->Begin([raw](size_t chunk) { raw->pf.Chunk(chunk, GetScriptCache()); });
-    scriptQueue->Publish(raw->pf.Chunks());
+    scriptQueue->Begin([raw](size_t k) { raw->pf.Job(k, GetScriptCache()); });
+    scriptQueue->Publish(raw->pf.Jobs());
     la->open = true;
     lookahead = std::move(la);
 }
@@ -1077,7 +1114,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     } else {
         own.reset(new BlockPrefetch());
         own->Init(block, view, fEnforceBIP30, fScriptChecks, scMayHold, flags);
-        pool->ParallelFor(own->Chunks(), [&](size_t chunk) { own->Chunk(chunk, sc); }, 1);
+        pool->ParallelFor(own->Jobs(), [&](size_t k) { own->Job(k, sc); }, 1);
         pf = own.get();
     }
     std::vector<std::unique_ptr<PrecomputedTransactionData>>& txdatas = pf->txdatas;
@@ -1149,14 +1186,8 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             phaseMicros[ph].fetch_add(t - tSub, std::memory_order_relaxed);
             tSub = t;
         };
-        size_t tcap = 16;
-        while (tcap < 2 * ntx) tcap <<= 1;
-        std::vector<int32_t> tslot(tcap, -1); // block-local txid -> index (CheckBlock refused duplicates)
-        for (size_t i = 0; i < ntx; i++) {
-            size_t h = ReadLE64(block.vtx[i]->GetHash().begin()) & (tcap - 1);
-            while (tslot[h] >= 0) h = (h + 1) & (tcap - 1);
-            tslot[h] = (int32_t)i;
-        }
+        const size_t tcap = pf->tcap, scap = pf->scap;
+        const std::vector<int32_t>& tslot = pf->tslot; // block-local txid -> index
         auto findTx = [&](const uint256& txid) -> int {
             size_t h = ReadLE64(txid.begin()) & (tcap - 1);
             while (tslot[h] >= 0) {
@@ -1165,19 +1196,12 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
             }
             return -1;
         };
-        std::vector<size_t> firstOutput(ntx + 1, 0);
-        for (size_t i = 0; i < ntx; i++) firstOutput[i + 1] = firstOutput[i] + block.vtx[i]->vout.size();
-        std::unique_ptr<std::atomic<uint8_t>[]> outSpent(new std::atomic<uint8_t>[nOutputs + 1]);
-        for (size_t o = 0; o <= nOutputs; o++) outSpent[o].store(0, std::memory_order_relaxed);
+        const std::vector<size_t>& firstOutput = pf->firstOutput;
+        std::atomic<uint8_t>* outSpent = pf->outSpent.get();
         // concurrent set of spent outpoints (input index + 1 per slot): a second spend of one
         // outpoint within the block is found by whichever insert comes second
-        size_t scap = 16;
-        while (scap < 2 * maxJobs) scap <<= 1;
-        std::unique_ptr<std::atomic<uint32_t>[]> spentSet(new std::atomic<uint32_t>[scap]);
-        for (size_t q = 0; q < scap; q++) spentSet[q].store(0, std::memory_order_relaxed);
-        std::vector<size_t> inputTx(maxJobs);
-        for (size_t i = 1; i < ntx; i++)
-            for (size_t k = firstInput[i]; k < firstInput[i + 1]; k++) inputTx[k] = i;
+        std::atomic<uint32_t>* spentSet = pf->spentSet.get();
+        const std::vector<size_t>& inputTx = pf->inputTx;
         auto prevoutOf = [&](size_t k) -> const COutPoint& {
             return block.vtx[inputTx[k]]->vin[k - firstInput[inputTx[k]]].prevout;
         };
