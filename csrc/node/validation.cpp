@@ -722,7 +722,7 @@ bool Chainstate::AcceptBlock(const std::shared_ptr<const CBlock>& pblock, CValid
     if (!IsInitialBlockDownload() && chainActive.Tip() == pindex->pprev) GetMainSignals().NewPoWValidBlock(pindex, pblock);
     const int nHeight = pindex->nHeight;
     try {
-        const unsigned nBlockSize = (unsigned)GetSerializeSize(block, PROTOCOL_VERSION);
+        const unsigned nBlockSize = (unsigned)BlockSerializeSize(block, PROTOCOL_VERSION);
         CDiskBlockPos blockPos;
         if (dbp != nullptr) blockPos = *dbp;
         if (!FindBlockPos(state, blockPos, nBlockSize + 8, nHeight, block.GetBlockTime(), dbp != nullptr))
@@ -1085,7 +1085,7 @@ bool Chainstate::ConnectBlockPrepare(const CBlock& block, CValidationState& stat
     Amount nFees = 0;
     int nInputs = 0;
     uint64_t nSigOpsCount = 0;
-    const uint64_t currentBlockSize = GetSerializeSize(block, PROTOCOL_VERSION);
+    const uint64_t currentBlockSize = BlockSerializeSize(block, PROTOCOL_VERSION); // cached tx sizes, no re-walk
     const uint64_t nMaxSigOpsCount = GetMaxBlockSigOpsCount(currentBlockSize);
     CDiskTxPos pos(pindex->GetBlockPos(), GetSizeOfCompactSize(block.vtx.size()));
     std::vector<std::pair<uint256, CDiskTxPos>>& vPos = p.vPos;
