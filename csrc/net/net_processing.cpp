@@ -611,8 +611,21 @@ void PeerLogicValidation::Impl::ProcessGetData(CNode* pfrom, std::deque<CInv>& v
             bool send = false;
             const CBlockIndex* pi = cs->LookupBlockIndex(inv.hash);
             if (pi) {
-                if (pi->nChainTx && !pi->IsValid(BLOCK_VALID_SCRIPTS) && pi->IsValid(BLOCK_VALID_TREE))
-                    ; // requested block not yet connected: fall through to the checks below
+                if (pi->nChainTx && !pi->IsValid(BLOCK_VALID_SCRIPTS) && pi->IsValid(BLOCK_VALID_TREE)) {
+                    // The block and all its parents are here but not yet validated: this node may be
+                    // between AcceptBlock and ActivateBestChain of that block (its compact-block
+                    // announcement, NewPoWValidBlock, goes out first, and a peer asks for it right
+                    // away). Connect it now so the relay check below sees it; otherwise the request
+                    // is dropped and the peer waits for the block until its download times out
+                    // (reference net_processing.cpp:1164-1180).
+                    std::shared_ptr<const CBlock> recent;
+                    {
+                        std::lock_guard<std::mutex> lr(cs_most_recent);
+                        recent = most_recent_block;
+                    }
+                    CValidationState dummy;
+                    cs->ActivateBestChain(dummy, recent);
+                }
                 if (cs->ActiveChain().Contains(pi)) {
                     send = true;
                 } else {
@@ -1109,6 +1122,18 @@ bool PeerLogicValidation::Impl::ProcessMessage(CNode* pfrom, const std::string& 
         CBlockLocator locator;
         uint256 hashStop;
         vRecv >> locator >> hashStop;
+        {
+            // a block announced by compact block may still be between its AcceptBlock and its
+            // ActivateBestChain: be on the best chain before answering (reference
+            // net_processing.cpp:1874-1894)
+            std::shared_ptr<const CBlock> recent;
+            {
+                std::lock_guard<std::mutex> lr(cs_most_recent);
+                recent = most_recent_block;
+            }
+            CValidationState dummy;
+            cs->ActivateBestChain(dummy, recent);
+        }
         std::lock_guard<CCriticalSection> l(csMain());
         const CBlockIndex* pi = cs->FindForkInGlobalIndex(locator);
         if (pi) pi = cs->ActiveChain().Next(pi);
