@@ -1,7 +1,13 @@
 // Browser wallet GUI served by bcpd (GET /gui on the RPC port, -webgui).
-// Parity: reference src/qt/ (bitcoin-qt: overview page with balances and recent transactions,
-// send coins dialog, receive coins with labels, transaction list, peers table, debug console
-// with RPC history). Qt is not available here; the same functions are a single page that
+// Parity: reference src/qt/ (bitcoin-qt: overview page with balances and recent transactions
+// (overviewpage.cpp), send coins dialog with several recipients and coin control
+// (sendcoinsdialog.cpp, coincontroldialog.cpp), receive coins with labels and payment requests
+// (receivecoinsdialog.cpp, recentrequeststablemodel.cpp), address book with label editing
+// (addressbookpage.cpp, editaddressdialog.cpp), transaction list with CSV export, wallet
+// encryption, passphrase change, lock and backup (askpassphrasedialog.cpp, walletview.cpp
+// backupWallet), transaction fee settings (sendcoinsdialog.cpp fee section), peers and banned
+// peers with ban/unban (peertablemodel.cpp, bantablemodel.cpp, rpcconsole.cpp), network traffic
+// totals (trafficgraphwidget.cpp), debug console with RPC history). Qt is not available here; the same functions are a single page that
 // talks JSON-RPC to this node over the authenticated HTTP port, so it needs no extra
 // dependency and no separate binary. The page is served only to authenticated RPC users.
 #include "rpc/httpserver.h"
@@ -34,6 +40,7 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 <div class="card"><b>Recent transactions</b><table><thead><tr><th>Date</th><th>Type</th><th>Address</th><th>Amount</th><th>Conf.</th></tr></thead><tbody id="recent"></tbody></table></div></section>
 <section id="send"><div class="card"><div>Pay to</div><input class="wide" id="sendto" placeholder="address (CashAddr or Base58)">
 <div>Amount (BCP)</div><input id="sendamt" type="number" step="0.00000001" min="0">
+<div id="morercp"></div><p><button onclick="addRcp()">Add recipient</button></p>
 <label><input type="checkbox" id="sendsub"> subtract fee from amount</label>
 <div>Comment</div><input class="wide" id="sendcomment">
 <div id="passrow" style="display:none">Wallet passphrase <input type="password" id="sendpass"></div>
@@ -43,17 +50,30 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 <div class="card"><div>BIP70 payment request (hex or base64)</div><textarea class="wide" id="preq" rows="3"></textarea>
 <p><button onclick="checkReq()">Check</button> <button class="act" onclick="payReq()">Pay request</button> <span id="preqres"></span></p>
 <div id="preqinfo"></div></div></section>
-<section id="receive"><div class="card">Label <input id="rcvlabel"> <button class="act" onclick="newAddr()">New address</button>
-<p class="mono big" id="newaddr"></p></div>
+<section id="receive"><div class="card">Label <input id="rcvlabel"> Amount <input id="rcvamt" type="number" step="0.00000001" min="0" style="width:130px">
+Message <input id="rcvmsg"> <button class="act" onclick="newAddr()">Request payment</button>
+<p class="mono" id="newaddr"></p></div>
+<div class="card"><b>Requested payments</b> <button onclick="clearReqs()">Clear</button><table><thead><tr><th>Date</th><th>Label</th><th>Message</th><th>Amount</th><th>URI</th></tr></thead><tbody id="reqlist"></tbody></table></div>
 <div class="card"><b>Receiving addresses</b><table><thead><tr><th>Address</th><th>Label</th><th>Received</th><th>Conf.</th></tr></thead><tbody id="rcvlist"></tbody></table></div></section>
 <section id="transactions"><div class="card"><button onclick="exportCsv()">Export CSV</button></div><div class="card"><table><thead><tr><th>Date</th><th>Type</th><th>Address</th><th>Amount</th><th>Conf.</th><th>Txid</th></tr></thead><tbody id="txlist"></tbody></table></div></section>
+<section id="addresses"><div class="card"><b>Receiving addresses</b> (label edits apply to the wallet's address book)<table><thead><tr><th>Address</th><th>Label</th><th></th></tr></thead><tbody id="ablist"></tbody></table></div>
+<div class="card"><b>Address groupings</b> (addresses whose coins have been spent together)<table><thead><tr><th>Address</th><th>Balance</th><th>Label</th></tr></thead><tbody id="grplist"></tbody></table></div></section>
+<section id="wallet"><div class="card"><b>Encryption</b> <span id="encstate"></span>
+<div id="encnew">New passphrase <input type="password" id="encpass1"> Repeat <input type="password" id="encpass2"> <button class="act" onclick="encryptWallet()">Encrypt wallet</button></div>
+<div id="encchg" style="display:none">Old passphrase <input type="password" id="chgold"> New <input type="password" id="chgnew1"> Repeat <input type="password" id="chgnew2"> <button class="act" onclick="changePass()">Change passphrase</button> <button onclick="lockWallet()">Lock now</button></div>
+<p id="encres"></p></div>
+<div class="card"><b>Backup</b> Destination on the node's host <input class="wide" id="bkpath" placeholder="/path/to/wallet-backup"> <button class="act" onclick="backupWallet()">Back up wallet</button> <span id="bkres"></span></div>
+<div class="card"><b>Transaction fee</b><table><tbody id="feeinfo"></tbody></table>
+Custom fee rate (BCP/kB, 0 = automatic) <input id="feerate" type="number" step="0.00000001" min="0" style="width:130px"> <button class="act" onclick="setFee()">Set</button> <span id="feeres"></span></div></section>
 <section id="signverify"><div class="card"><b>Sign message</b><div>Address</div><input class="wide" id="smaddr">
 <div>Message</div><textarea class="wide" id="smmsg" rows="3"></textarea>
 <p><button class="act" onclick="signMsg()">Sign</button></p><p class="mono" id="smsig"></p></div>
 <div class="card"><b>Verify message</b><div>Address</div><input class="wide" id="vmaddr">
 <div>Message</div><textarea class="wide" id="vmmsg" rows="3"></textarea><div>Signature</div><input class="wide" id="vmsig">
 <p><button class="act" onclick="verifyMsg()">Verify</button> <span id="vmres"></span></p></div></section>
-<section id="peers"><div class="card"><table><thead><tr><th>Address</th><th>Client</th><th>Version</th><th>Direction</th><th>Height</th><th>Sent</th><th>Recv</th><th>Ping ms</th></tr></thead><tbody id="peerlist"></tbody></table></div></section>
+<section id="peers"><div class="card"><table><tbody id="traffic"></tbody></table></div>
+<div class="card"><table><thead><tr><th>Address</th><th>Client</th><th>Version</th><th>Direction</th><th>Height</th><th>Sent</th><th>Recv</th><th>Ping ms</th><th></th></tr></thead><tbody id="peerlist"></tbody></table></div>
+<div class="card"><b>Banned peers</b> <button onclick="clearBans()">Unban all</button><table><thead><tr><th>Subnet</th><th>Banned until</th><th>Reason</th><th></th></tr></thead><tbody id="banlist"></tbody></table></div></section>
 <section id="mining"><div class="card"><table><tbody id="mininfo"></tbody></table></div>
 <div class="card"><table><tbody id="gpuinfo"></tbody></table></div>
 <div class="card">Generate <input id="gencount" type="number" value="1" min="1" style="width:70px"> block(s) to this wallet (regtest)
@@ -62,7 +82,7 @@ button.act{background:#1d3557;color:#fff;border:0;border-radius:4px;padding:7px 
 <input class="wide mono" id="conin" placeholder="method arg1 arg2 …  (e.g. getblockchaininfo, getblockhash 10; ↑/↓ history)"></div></section>
 </main>
 <script>
-const TABS=[["overview","Overview"],["send","Send"],["receive","Receive"],["transactions","Transactions"],["signverify","Sign / verify"],["peers","Peers"],["mining","Mining"],["console","Console"]];
+const TABS=[["overview","Overview"],["send","Send"],["receive","Receive"],["transactions","Transactions"],["addresses","Addresses"],["wallet","Wallet"],["signverify","Sign / verify"],["peers","Peers"],["mining","Mining"],["console","Console"]];
 let rpcId=0;
 async function rpc(method,params=[]){
   const r=await fetch("/",{method:"POST",credentials:"same-origin",headers:{"Content-Type":"application/json","X-Requested-With":"bcp-webgui"},
@@ -83,13 +103,31 @@ async function refresh(id){current=id||current;
     const bc=await rpc("getblockchaininfo");
     $("status").textContent=bc.chain+" · height "+bc.blocks+(bc.initialblockdownload?" · syncing":"");
     if(current=="overview"){
-      const [b,u,w,n,tx]=await Promise.all([rpc("getbalance"),rpc("getunconfirmedbalance"),rpc("getwalletinfo"),rpc("getnetworkinfo"),rpc("listtransactions",["*",10])]);
+      const [b,u,w,n,tx,mp,up]=await Promise.all([rpc("getbalance"),rpc("getunconfirmedbalance"),rpc("getwalletinfo"),rpc("getnetworkinfo"),rpc("listtransactions",["*",10]),rpc("getmempoolinfo"),rpc("uptime")]);
       $("bal").textContent=amt(b);$("ubal").textContent=amt(u);$("ibal").textContent=amt(w.immature_balance);
-      kv("chaininfo",Object.assign({},bc,{connections:n.connections,subversion:n.subversion}),["chain","blocks","headers","bestblockhash","difficulty","verificationprogress","connections","subversion"]);
+      kv("chaininfo",Object.assign({},bc,{connections:n.connections,subversion:n.subversion,mempool_transactions:mp.size,mempool_bytes:mp.bytes,uptime_s:up}),["chain","blocks","headers","bestblockhash","difficulty","verificationprogress","connections","subversion","mempool_transactions","mempool_bytes","uptime_s"]);
       rows("recent",tx.reverse(),TXCOLS);}
-    if(current=="receive") rows("rcvlist",await rpc("listreceivedbyaddress",[0,true]),[[a=>a.address,'mono'],[a=>a.label||a.account],[a=>amt(a.amount)],[a=>a.confirmations]]);
+    if(current=="receive"){rows("rcvlist",await rpc("listreceivedbyaddress",[0,true]),[[a=>a.address,'mono'],[a=>a.label||a.account],[a=>amt(a.amount)],[a=>a.confirmations]]);
+      rows("reqlist",reqs().slice().reverse(),[[r=>date(r.time)],[r=>r.label],[r=>r.message],[r=>r.amount?amt(r.amount):""],[r=>r.uri,'mono']]);}
+    if(current=="addresses"){
+      const ab=await rpc("listreceivedbyaddress",[0,true]);
+      $("ablist").innerHTML=ab.map((a,i)=>"<tr><td class='mono'>"+esc(a.address)+"</td><td><input id='lbl"+i+"' value='"+esc(a.label||a.account||"")+"'></td><td><button onclick=\"setLabel('"+esc(a.address)+"','lbl"+i+"')\">Save label</button></td></tr>").join("");
+      rows("grplist",(await rpc("listaddressgroupings")).flat(),[[g=>g[0],'mono'],[g=>amt(g[1])],[g=>g[2]===undefined?"":g[2]]]);}
+    if(current=="wallet"){
+      const w=await rpc("getwalletinfo"),enc=w.unlocked_until!==undefined;
+      $("encstate").textContent=enc?(w.unlocked_until>0?"encrypted, unlocked until "+date(w.unlocked_until):"encrypted, locked"):"not encrypted";
+      $("encnew").style.display=enc?"none":"block";$("encchg").style.display=enc?"block":"none";
+      const ef=await rpc("estimatesmartfee",[6]);
+      kv("feeinfo",{paytxfee:w.paytxfee,estimated_rate_6_blocks:ef.feerate<0?"not enough data":ef.feerate,estimate_target_blocks:ef.blocks},["paytxfee","estimated_rate_6_blocks","estimate_target_blocks"]);}
     if(current=="transactions") rows("txlist",(await rpc("listtransactions",["*",200])).reverse(),TXCOLS.concat([[t=>t.txid,'mono']]));
-    if(current=="peers") rows("peerlist",await rpc("getpeerinfo"),[[p=>p.addr,'mono'],[p=>p.subver],[p=>p.version],[p=>p.inbound?"in":"out"],[p=>p.synced_blocks],[p=>p.bytessent],[p=>p.bytesrecv],[p=>p.pingtime===undefined?"":Math.round(p.pingtime*1000)]]);
+    if(current=="peers"){
+      const nt=await rpc("getnettotals");
+      kv("traffic",{received_bytes:nt.totalbytesrecv,sent_bytes:nt.totalbytessent},["received_bytes","sent_bytes"]);
+      const ps=await rpc("getpeerinfo");
+      $("peerlist").innerHTML=ps.map(p=>"<tr>"+[[p.addr,'mono'],[p.subver],[p.version],[p.inbound?"in":"out"],[p.synced_blocks],[p.bytessent],[p.bytesrecv],[p.pingtime===undefined?"":Math.round(p.pingtime*1000)]].map(c=>"<td class='"+(c[1]||"")+"'>"+esc(c[0])+"</td>").join("")+
+        "<td><button onclick=\"banPeer('"+esc(p.addr)+"')\">Ban 24 h</button></td></tr>").join("");
+      $("banlist").innerHTML=(await rpc("listbanned")).map(b=>"<tr><td class='mono'>"+esc(b.address)+"</td><td>"+esc(date(b.banned_until))+"</td><td>"+esc(b.ban_reason||"")+
+        "</td><td><button onclick=\"unban('"+esc(b.address)+"')\">Unban</button></td></tr>").join("");}
     if(current=="mining"){
       kv("mininfo",await rpc("getmininginfo"),["blocks","difficulty","networkhashps","pooledtx","chain","errors"]);
       kv("gpuinfo",await rpc("getgpuinfo"),Object.keys(await rpc("getgpuinfo")));}
@@ -106,6 +144,10 @@ async function doSend(){
     if(picked.length){const to=$("sendto").value.trim(),amts={};amts[to]=Number($("sendamt").value);
       const r=await rpc("sendwithcoincontrol",[amts,picked,$("ccchange").value.trim(),$("sendsub").checked?[to]:[]]);
       $("sendres").innerHTML="<span class='ok'>sent "+esc(r.txid)+" (fee "+amt(r.fee)+")</span>";$("sendpass").value="";loadCoins();return;}
+    const extra=[...document.querySelectorAll(".rcp")].map(r=>[r.querySelector(".rto").value.trim(),Number(r.querySelector(".ramt").value)]).filter(r=>r[0]);
+    if(extra.length){const amts={};amts[to]=Number($("sendamt").value);for(const [a,v] of extra) amts[a]=(amts[a]||0)+v;
+      const txid=await rpc("sendmany",["",amts,1,$("sendcomment").value,$("sendsub").checked?Object.keys(amts):[]]);
+      $("sendres").innerHTML="<span class='ok'>sent "+esc(txid)+" to "+Object.keys(amts).length+" recipients</span>";$("sendpass").value="";return;}
     const txid=await rpc("sendtoaddress",[$("sendto").value.trim(),Number($("sendamt").value),$("sendcomment").value,"",$("sendsub").checked]);
     $("sendres").innerHTML="<span class='ok'>sent "+esc(txid)+"</span>";$("sendpass").value="";
   }catch(e){ if(e.code==-13) $("passrow").style.display="block";
@@ -128,7 +170,7 @@ async function verifyMsg(){try{const ok=await rpc("verifymessage",[$("vmaddr").v
   $("vmres").innerHTML=ok?"<span class='ok'>message verified</span>":"<span class='err'>signature does not match</span>";}
   catch(e){$("vmres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
 async function exportCsv(){const txs=await rpc("listtransactions",["*",100000]);
-  const q=v=>'"'+String(v??"").replace(/"/g,'""')+'"';
+  const q=v=>'"'+String(v==null?"":v).replace(/"/g,'""')+'"';
   const lines=[["Confirmed","Date","Type","Label","Address","Amount","ID"].map(q).join(",")].concat(txs.map(t=>
     [t.confirmations>0,new Date(t.time*1000).toISOString(),t.category,t.label||t.account||"",t.address||"",t.amount,t.txid].map(q).join(",")));
   const a=document.createElement("a");a.href=URL.createObjectURL(new Blob([lines.join("\n")],{type:"text/csv"}));
@@ -136,9 +178,33 @@ async function exportCsv(){const txs=await rpc("listtransactions",["*",100000]);
 async function loadCoins(){const u=await rpc("listunspent",[0]);
   $("cclist").innerHTML=u.map(c=>"<tr><td><input type='checkbox' class='ccpick' data-txid='"+esc(c.txid)+"' data-vout='"+c.vout+"'></td><td>"+amt(c.amount)+
     "</td><td class='mono'>"+esc(c.address||"")+"</td><td>"+c.confirmations+"</td><td class='mono'>"+esc(c.txid.slice(0,16))+"…:"+c.vout+"</td></tr>").join("");}
-async function newAddr(){try{const a=await rpc("getnewaddress",[$("rcvlabel").value]);
-  $("newaddr").textContent=a+"  "+await rpc("formatbitcoinuri",[a,null,$("rcvlabel").value]);refresh("receive");}
+function addRcp(){const d=document.createElement("div");d.className="rcp";
+  d.innerHTML="Pay to <input class='wide rto' placeholder='address'> Amount (BCP) <input class='ramt' type='number' step='0.00000001' min='0'>";$("morercp").appendChild(d);}
+// requested payments live in this browser (the reference keeps them in the wallet's destdata)
+const reqs=()=>JSON.parse(localStorage.getItem("bcpRequests")||"[]");
+function clearReqs(){localStorage.removeItem("bcpRequests");refresh("receive");}
+async function newAddr(){try{const label=$("rcvlabel").value,msg=$("rcvmsg").value,v=Number($("rcvamt").value)||null;
+  const a=await rpc("getnewaddress",[label]),uri=await rpc("formatbitcoinuri",[a,v,label,msg]);
+  $("newaddr").textContent=uri;
+  localStorage.setItem("bcpRequests",JSON.stringify(reqs().concat([{time:Math.floor(Date.now()/1000),label:label,message:msg,amount:v,uri:uri}])));refresh("receive");}
   catch(e){$("newaddr").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function setLabel(addr,id){try{await rpc("setaccount",[addr,$(id).value]);refresh("addresses");}catch(e){alert(e.message);}}
+async function encryptWallet(){const a=$("encpass1").value;$("encres").textContent="";
+  if(!a||a!=$("encpass2").value){$("encres").innerHTML="<span class='err'>the passphrases differ or are empty</span>";return;}
+  try{const r=await rpc("encryptwallet",[a]);$("encres").innerHTML="<span class='ok'>"+esc(r)+"</span>";$("encpass1").value=$("encpass2").value="";refresh("wallet");}
+  catch(e){$("encres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function changePass(){const n=$("chgnew1").value;$("encres").textContent="";
+  if(!n||n!=$("chgnew2").value){$("encres").innerHTML="<span class='err'>the new passphrases differ or are empty</span>";return;}
+  try{await rpc("walletpassphrasechange",[$("chgold").value,n]);$("encres").innerHTML="<span class='ok'>passphrase changed</span>";$("chgold").value=$("chgnew1").value=$("chgnew2").value="";}
+  catch(e){$("encres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function lockWallet(){try{await rpc("walletlock");refresh("wallet");}catch(e){$("encres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function backupWallet(){try{await rpc("backupwallet",[$("bkpath").value.trim()]);$("bkres").innerHTML="<span class='ok'>backed up</span>";}
+  catch(e){$("bkres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function setFee(){try{await rpc("settxfee",[Number($("feerate").value)]);$("feeres").innerHTML="<span class='ok'>set</span>";refresh("wallet");}
+  catch(e){$("feeres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
+async function banPeer(addr){try{await rpc("setban",[addr.replace(/:\d+$/,"").replace(/^\[|\]$/g,""),"add",86400]);refresh("peers");}catch(e){alert(e.message);}}
+async function unban(sub){try{await rpc("setban",[sub,"remove"]);refresh("peers");}catch(e){alert(e.message);}}
+async function clearBans(){try{await rpc("clearbanned");refresh("peers");}catch(e){alert(e.message);}}
 async function doGenerate(){$("genres").textContent="mining…";
   try{const h=await rpc("generate",[Number($("gencount").value)]);$("genres").innerHTML="<span class='ok'>"+h.length+" block(s)</span>";refresh("mining");}
   catch(e){$("genres").innerHTML="<span class='err'>"+esc(e.message)+"</span>";}}
