@@ -63,7 +63,11 @@ build/obj/python/%.o: csrc/python/%.cpp
 
 build/obj/kernels/%.o: csrc/kernels/%.hip
 	@mkdir -p $(dir $@)
-	$(HIPCC) $(HIPFLAGS) -MMD -MP -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(HIPFLAGS_$*) -MMD -MP -c $< -o $@
+
+# Per-kernel-file flags. The Equihash solver is scheduled for instruction-level parallelism:
+# +0.5-0.7% Sol/s in two interleaved A/Bs of 10 and 12 reps (profiles/equihash_r6.md).
+HIPFLAGS_equihash_solver := -mllvm -amdgpu-sched-strategy=max-ilp
 
 $(CORELIB): $(CORE_OBJS) $(HIP_OBJS)
 	@mkdir -p $(dir $@)
