@@ -596,7 +596,8 @@ template <class C> constexpr bool round_prunes(int stage) {
 // equal on all remaining bits.
 // Input rows whose slots carry compact parents keep the parent-bucket bits in their padding in
 // LDS (the prune check reads them); every comparison and the emit XOR mask them out (RMI).
-// pdrop[STAGE]: pairs lost to a full pair list; pdrop[K + STAGE]: stage-(STAGE-1) rows past the
+// pdrop[STAGE]: pairs lost to a full pair list or to the 14-partner cap of a row in a large key
+// group (duplicate subtrees); pdrop[K + STAGE]: stage-(STAGE-1) rows past the
 // round's capacity (offered to a bucket but never read), counted for every nonce.
 template <class C, int STAGE, bool STAMP>
 __global__ __launch_bounds__(C::NT) __attribute__((amdgpu_waves_per_eu(C::WGCU * C::NT / 256)))
@@ -819,6 +820,7 @@ void eh_round(const uint32_t* __restrict__ Rin, const uint32_t* __restrict__ CTR
                     sidx[pos] = (uint16_t)r;
                     krank[u] = pos;
                     kpairs[u] = min(e - pos - 1, 14u);
+                    if (e - pos - 1 > 14u) atomicAdd(&pdrop[STAGE], e - pos - 1 - 14u); // capped pairs (rare) count as pair-list drops
                 }
             }
         } else {

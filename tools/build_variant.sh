@@ -11,7 +11,7 @@ EXT=$(python3 -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))
 D=build/var/$NAME
 mkdir -p "$D" ab/"$NAME"
 # the Makefile's per-file flags of the solver (HIPFLAGS_equihash_solver) unless EH_FLAGS overrides them
-[ "${OBJ:-equihash_solver}" = equihash_solver ] && DEF=${EH_FLAGS-"-mllvm -amdgpu-sched-strategy=max-ilp"} || DEF=""
+[ "${OBJ:-equihash_solver}" = equihash_solver ] && DEF=${EH_FLAGS-"-mllvm -amdgpu-sched-strategy=max-ilp -mllvm -amdgpu-use-amdgpu-trackers=1 -mllvm -amdgpu-atomic-optimizer-strategy=None"} || DEF=""
 /opt/rocm/bin/hipcc -std=c++17 -O2 -fPIC --offload-arch=gfx950 -Icsrc -munsafe-fp-atomics -Wno-unused-result \
     -Wno-unused-variable -Wno-pass-failed $DEF "$@" -c "${SRC:-csrc/kernels/${OBJ:-equihash_solver}.hip}" -o "$D/${OBJ:-equihash_solver}.o"
 cp build/libbcpcore.a "$D/libbcpcore.a"

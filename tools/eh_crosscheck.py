@@ -34,6 +34,7 @@ def main():
     solver.set_debug(True)
     tot_cpu = sum(len(c) for c in cpu)
     for rep in range(args.reps):
+        solver.reset_stats()  # the *_all counters below cover this repetition's nonces
         got = []
         for b0 in range(0, args.nonces, args.batch):
             got += solver.solve(states[b0:b0 + args.batch])
@@ -43,7 +44,12 @@ def main():
                           "missing": miss, "extra": extra,
                           "per_nonce": [[len(c), len(g)] for c, g in zip(cpu, got)],
                           "dropped": solver.stats()["stage_dropped"], "top": solver.stats()["stage_top"][6:],
-                          "pair_dropped": solver.stats()["pair_dropped"]}), flush=True)
+                          "pair_dropped": solver.stats()["pair_dropped"],
+                          # every nonce of the repetition: rows past a round's capacity, pairs lost
+                          # to a full list or the per-row partner cap, candidates past MAXCAND
+                          "stage_dropped_all": solver.stats()["stage_dropped_all"],
+                          "pair_dropped_all": solver.stats()["pair_dropped_all"],
+                          "cand_dropped": solver.stats()["cand_dropped"]}), flush=True)
 
 
 if __name__ == "__main__":
