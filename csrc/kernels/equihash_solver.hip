@@ -81,7 +81,7 @@ namespace bcpk {
 // the LDS budget must allow. GENWG/NTG: LDS-sorted generation geometry; GNT x GHPT: register
 // generation (threads x hashes per thread; 0 = use the LDS-sorted kernel).
 template <int N_, int K_, int BB_, int CAP_, int NT_, int GENWG_, int NTG_, int MAXCAND_, int CAP4_ = CAP_,
-          int CAP3_ = CAP_, int WGCU_ = 1, int GNT_ = 512, int GHPT_ = 2, int CAPF_ = 0>
+          int CAP3_ = CAP_, int WGCU_ = 1, int GNT_ = 512, int GHPT_ = 2, int CAPF_ = 0, int MPX_ = 0>
 struct EhCfg {
     static constexpr int N = N_, K = K_;
     static constexpr int DB = N / (K + 1);           // digit bits
@@ -96,6 +96,7 @@ struct EhCfg {
     // duplicate subtrees pile up in a few stage-(K-1) buckets; a larger final area keeps the valid
     // rows of such a bucket from being crowded out (which rows are dropped follows the atomics).
     static constexpr int CAPF = CAPF_ > 0 ? CAPF_ : CAP3_;
+    static constexpr int MPX = MPX_;                 // extra pair-list slots per lane in every collision round
     static constexpr int cap(int round) {
         return round == K_ ? CAPF : words(round - 1) >= 5 ? CAP_ : words(round - 1) == 4 ? CAP4_ : CAP3_;
     }
@@ -152,7 +153,11 @@ struct EhCfg {
 #define BCP_EH_CAPF 6016 // 5120 overflowed by 2-140 rows in ~12 buckets per 32 nonces (recall_base.json, round 5); 6016 keeps two final-round WGs per CU
 #endif
 using Cfg200_9 = EhCfg<200, 9, 9, 4416, 1024, 512, 1024, 256, 4864, 5120, 1, BCP_EH_GEN_NT, BCP_EH_GEN_HPT, BCP_EH_CAPF>;
-using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256>;
+// (96,5): one extra pair slot per lane. ~1024 rows per bucket over 512 keys make ~1024 pairs, and
+// a list of 1280 overflowed in some bucket of most nonces: 84 + 18 + 36 + ~80 pairs per 16 nonces
+// in rounds 1-4, which pairs depending on the atomics' order, so a solution was lost now and then
+// (tools/eh_crosscheck.py --n 96 --k 5, profiles/equihash_r6.md).
+using Cfg96_5 = EhCfg<96, 5, 7, 1280, 256, 256, 256, 256, 1280, 1280, 1, 512, 2, 0, 1>;
 using Cfg48_5 = EhCfg<48, 5, 3, 512, 64, 8, 64, 256>; // 512-slot areas: 8 pairs per lane (a 256-pair list overflowed on duplicate-heavy nonces)
 
 constexpr uint32_t NIL = 0xffffffffu;
@@ -545,12 +550,13 @@ template <class C> __host__ __device__ __forceinline__ uint32_t cunpack_d(uint32
 // u32 (aliasing plist) after it.
 template <class C> constexpr int un_walk_bend(int cap) { return (cap * 2 + 3) / 4 * 4; }
 template <class C> constexpr int un_walk_list(int cap) { return un_walk_bend<C>(cap) + C::NRESTS * 4; }
-// Pairs per lane: one lane per LDS row slot, plus BCP_EH_MP_LATE extra from round
-// BCP_EH_MP_LATE_FROM on ((200,9) only): without depth-1 pruning the late rounds' pair lists
-// grow past the row count (duplicate subtrees) and overflowed in round 8.
+// Pairs per lane: one lane per LDS row slot, plus the configuration's MPX, plus BCP_EH_MP_LATE
+// extra from round BCP_EH_MP_LATE_FROM on ((200,9) only): without depth-1 pruning the late rounds'
+// pair lists grow past the row count (duplicate subtrees) and overflowed in round 8.
 template <class C> constexpr int round_mp(int stage) {
     return stage == C::K ? 1
-                         : (C::AREA_NF + C::NT - 1) / C::NT + (C::K == 9 && stage >= BCP_EH_MP_LATE_FROM ? BCP_EH_MP_LATE : 0);
+                         : (C::AREA_NF + C::NT - 1) / C::NT + C::MPX +
+                               (C::K == 9 && stage >= BCP_EH_MP_LATE_FROM ? BCP_EH_MP_LATE : 0);
 }
 template <class C> constexpr int round_un(int stage) {
     const int cap = C::cap(stage);
