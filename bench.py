@@ -71,7 +71,10 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "48")))
+    # 96 nonces per solver batch: +2.1% Sol/s over 48 in a 10-rep interleaved A/B on the final
+    # round-6 solver (88-112 all within 0.3% of it; profiles/equihash_r6.md); two solvers of 96
+    # hold ~100 GiB of the GPU's 288 GB
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("BCP_EH_BATCH", "96")))
     ap.add_argument("--verify", type=int, default=1, help="GPU-verify every solution after timing")
     ap.add_argument("--solvers", type=int, default=int(os.environ.get("BCP_EH_SOLVERS", "2")),
                     help="solvers in flight per GPU (each its own stream and buffers)")

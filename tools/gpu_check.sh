@@ -191,7 +191,7 @@ baseline)
   tail -n 20 "$O/bench_bcp.log" ;;
 multirank)
   BCP_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 > "$O/bench2.log" 2>&1
+    --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --batch 48 > "$O/bench2.log" 2>&1  # two ranks share one GPU: half the default batch each
   tail -n 1 "$O/bench2.log" ;;
 *)
   echo "unknown mode $MODE"; exit 2 ;;
