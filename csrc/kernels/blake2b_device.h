@@ -39,6 +39,14 @@ __device__ __constant__ static const uint8_t kB2Sigma[12][16] = {
 // 64-bit rotate right as two 32-bit funnel shifts (v_alignbit_b32): the generic shift/or form
 // compiles to two 64-bit shifts plus two ORs. n is a compile-time constant at every call site
 // (32 is a plain half swap).
+// a ^ b ^ c in one gfx950 three-input bit operation per 32-bit half (v_bitop3_b32, truth table
+// 0x96) instead of two xors: the digest words of every hash (h ^ v[i] ^ v[i + 8]).
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+    const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, 0x96);
+    const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), 0x96);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) {
     const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
     uint32_t rlo, rhi;
@@ -105,14 +113,14 @@ __device__ __forceinline__ void blake2b_compress_final(const uint64_t hin[8], co
         BCPK_B2G(v2, v7, v8, v13, m[kB2Sigma[r][12]], m[kB2Sigma[r][13]]);
         BCPK_B2G(v3, v4, v9, v14, m[kB2Sigma[r][14]], m[kB2Sigma[r][15]]);
     }
-    out[0] = hin[0] ^ v0 ^ v8;
-    out[1] = hin[1] ^ v1 ^ v9;
-    out[2] = hin[2] ^ v2 ^ v10;
-    out[3] = hin[3] ^ v3 ^ v11;
-    out[4] = hin[4] ^ v4 ^ v12;
-    out[5] = hin[5] ^ v5 ^ v13;
-    out[6] = hin[6] ^ v6 ^ v14;
-    out[7] = hin[7] ^ v7 ^ v15;
+    out[0] = xor3_64(hin[0], v0, v8);
+    out[1] = xor3_64(hin[1], v1, v9);
+    out[2] = xor3_64(hin[2], v2, v10);
+    out[3] = xor3_64(hin[3], v3, v11);
+    out[4] = xor3_64(hin[4], v4, v12);
+    out[5] = xor3_64(hin[5], v5, v13);
+    out[6] = xor3_64(hin[6], v6, v14);
+    out[7] = xor3_64(hin[7], v7, v15);
 }
 
 // One compression of a full, non-final 128-byte block (t0 = bytes hashed so far, this block
@@ -133,14 +141,14 @@ __device__ __forceinline__ void blake2b_compress_block(uint64_t h[8], const uint
         BCPK_B2G(v2, v7, v8, v13, m[kB2Sigma[r][12]], m[kB2Sigma[r][13]]);
         BCPK_B2G(v3, v4, v9, v14, m[kB2Sigma[r][14]], m[kB2Sigma[r][15]]);
     }
-    h[0] ^= v0 ^ v8;
-    h[1] ^= v1 ^ v9;
-    h[2] ^= v2 ^ v10;
-    h[3] ^= v3 ^ v11;
-    h[4] ^= v4 ^ v12;
-    h[5] ^= v5 ^ v13;
-    h[6] ^= v6 ^ v14;
-    h[7] ^= v7 ^ v15;
+    h[0] = xor3_64(h[0], v0, v8);
+    h[1] = xor3_64(h[1], v1, v9);
+    h[2] = xor3_64(h[2], v2, v10);
+    h[3] = xor3_64(h[3], v3, v11);
+    h[4] = xor3_64(h[4], v4, v12);
+    h[5] = xor3_64(h[5], v5, v13);
+    h[6] = xor3_64(h[6], v6, v14);
+    h[7] = xor3_64(h[7], v7, v15);
 }
 
 // The base state of a block header's Equihash input, built on the device from the raw 140 bytes
@@ -258,14 +266,14 @@ __device__ __forceinline__ void eh_hash_g_hdr_from(const uint64_t P[16], const E
         BCPK_B2G(v2, v7, v8, v13, m[kB2Sigma[r][12]], m[kB2Sigma[r][13]]);
         BCPK_B2G(v3, v4, v9, v14, m[kB2Sigma[r][14]], m[kB2Sigma[r][15]]);
     }
-    out[0] = bs.h[0] ^ v0 ^ v8;
-    out[1] = bs.h[1] ^ v1 ^ v9;
-    out[2] = bs.h[2] ^ v2 ^ v10;
-    out[3] = bs.h[3] ^ v3 ^ v11;
-    out[4] = bs.h[4] ^ v4 ^ v12;
-    out[5] = bs.h[5] ^ v5 ^ v13;
-    out[6] = bs.h[6] ^ v6 ^ v14;
-    out[7] = bs.h[7] ^ v7 ^ v15;
+    out[0] = xor3_64(bs.h[0], v0, v8);
+    out[1] = xor3_64(bs.h[1], v1, v9);
+    out[2] = xor3_64(bs.h[2], v2, v10);
+    out[3] = xor3_64(bs.h[3], v3, v11);
+    out[4] = xor3_64(bs.h[4], v4, v12);
+    out[5] = xor3_64(bs.h[5], v5, v13);
+    out[6] = xor3_64(bs.h[6], v6, v14);
+    out[7] = xor3_64(bs.h[7], v7, v15);
 }
 
 // Byte k (0-based) of the digest held in 8 little-endian words.
